@@ -1,0 +1,36 @@
+/*
+ * klt_amd.h -- libklt_amd.so extensions beyond the reference klt.h surface.
+ * Used by bench.py / tests / tools for device-resident work; a reference
+ * caller never needs them.
+ */
+#ifndef KLT_AMD_EXT_H
+#define KLT_AMD_EXT_H
+
+#include <stdint.h>
+
+#include "klt.h"
+#include "klt_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* the device context behind a tracking context (created on first use) */
+klt_hip_ctx *klt_amd_device_context(KLT_TrackingContext tc);
+/* the descriptors KLTTrackFeatures would build for this context */
+void klt_amd_pyr_desc(KLT_TrackingContext tc, int ncols, int nrows, int nlevels, int smooth,
+                      klt_hip_pyr_desc *desc);
+void klt_amd_track_desc(KLT_TrackingContext tc, klt_hip_track_desc *desc);
+/* KLT_HIP_EXACT (default) or KLT_HIP_FAST; env KLT_AMD_REDUCTION=fast sets FAST */
+void klt_amd_set_reduction(KLT_TrackingContext tc, int reduction);
+
+/* host side of the synthetic generator (include/klt_synth.h) */
+void klt_synth_frame(uint64_t seed, int t, int ncols, int nrows, unsigned char *out);
+/* the reference quicksort's permutation on {val, idx} pairs (test hook) */
+void klt_sort_pairs_full(int *val, int *idx, int n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

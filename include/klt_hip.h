@@ -1,0 +1,153 @@
+/*
+ * klt_hip.h -- the device C ABI of libklt_amd.so (HIP / CDNA4 gfx950).
+ *
+ * Plain C: pointers, sizes and POD descriptors, no HIP or torch types.  The
+ * klt.h host layer (csrc/klt_api.c) is the main caller; bench.py and the
+ * tests call it through ctypes for device-resident work.  Each entry point
+ * replaces a reference CPU routine:
+ *
+ *   klt_hip_build_pyramid  <- _KLTToFloatImage + _KLTComputeSmoothedImage +
+ *                             _KLTComputePyramid + _KLTComputeGradients per level
+ *                             (convolve.c:37-53,273-314; pyramid.c:87-131;
+ *                              trackFeatures.c:1296-1321)
+ *   klt_hip_min_eigen      <- the trackability loop of _KLTSelectGoodFeatures
+ *                             (selectGoodFeatures.c:375-424, :289-292)
+ *   klt_hip_track          <- the per-feature loop of KLTTrackFeatures with
+ *                             _trackFeature (trackFeatures.c:1343-1501, :381-486)
+ *
+ * All functions return 0 on success and a negative code on failure; the
+ * message is available from klt_hip_last_error().  Work is queued on the
+ * context's stream (its own, or one handed in with klt_hip_set_stream) and is
+ * asynchronous unless documented otherwise.
+ */
+#ifndef KLT_HIP_H
+#define KLT_HIP_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KLT_HIP_MAX_TAPS 71  /* MAX_KERNEL_WIDTH, convolve.c:16 */
+#define KLT_HIP_MAX_LEVELS 8
+#define KLT_HIP_MAX_SLOTS 4  /* pyramid slots per context */
+
+/* reduction order inside the Newton loop */
+#define KLT_HIP_EXACT 0 /* reference order: bit-identical to the CPU path */
+#define KLT_HIP_FAST 1  /* wave64 shuffle tree: not bit-identical (tolerance) */
+
+/* taps exactly as _computeKernels produces them: k[0..width-1], un-reversed */
+typedef struct {
+  int width;
+  float k[KLT_HIP_MAX_TAPS];
+} klt_hip_taps;
+
+/* how to turn a u8 frame into a pyramid slot */
+typedef struct {
+  int ncols, nrows;      /* level-0 size */
+  int nlevels;           /* tc->nPyramidLevels (1 for selection images) */
+  int subsampling;       /* tc->subsampling */
+  int smooth_input;      /* 1: smooth the u8 frame with `smooth` first */
+  klt_hip_taps smooth;   /* gauss, sigma = _KLTComputeSmoothSigma(tc) */
+  klt_hip_taps pyr;      /* gauss, sigma = subsampling * pyramid_sigma_fact */
+  klt_hip_taps grad_gauss; /* sigma = grad_sigma */
+  klt_hip_taps grad_deriv;
+} klt_hip_pyr_desc;
+
+/* _trackFeature / KLTTrackFeatures parameters */
+typedef struct {
+  int window_width, window_height;
+  int max_iterations;
+  float min_determinant, min_displacement, max_residue, step_factor;
+  int borderx, bordery;
+  int lighting_insensitive;
+  int reduction; /* KLT_HIP_EXACT or KLT_HIP_FAST */
+} klt_hip_track_desc;
+
+/* trackability-map parameters */
+typedef struct {
+  int window_width, window_height;
+  int borderx, bordery; /* already max'ed with the window half sizes */
+  int nSkippedPixels;
+} klt_hip_select_desc;
+
+/* per-kernel timing (HIP events on the context stream), milliseconds */
+typedef struct {
+  int n_pyr_l0, n_pyr_l1, n_track, n_eigen, n_generic;
+  double ms_pyr_l0, ms_pyr_l1, ms_track, ms_eigen, ms_generic;
+} klt_hip_timing;
+
+typedef struct klt_hip_ctx klt_hip_ctx;
+
+/* device < 0: the calling thread's current HIP device */
+klt_hip_ctx *klt_hip_ctx_create(int device);
+void klt_hip_ctx_destroy(klt_hip_ctx *ctx);
+const char *klt_hip_last_error(klt_hip_ctx *ctx);
+/* stream: a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL
+   restores the context's own non-blocking stream */
+int klt_hip_set_stream(klt_hip_ctx *ctx, void *stream);
+void *klt_hip_get_stream(klt_hip_ctx *ctx);
+int klt_hip_sync(klt_hip_ctx *ctx);
+int klt_hip_device_count(void);
+
+/* host u8 frame -> device staging buffer `buf` (0 or 1), via pinned memory */
+int klt_hip_upload_frame(klt_hip_ctx *ctx, int buf, const unsigned char *host, int ncols,
+                         int nrows);
+/* build pyramid slot `slot` from device u8 frame (row pitch in bytes);
+   frame == NULL -> staging buffer `buf` from klt_hip_upload_frame */
+int klt_hip_build_pyramid(klt_hip_ctx *ctx, int slot, const klt_hip_pyr_desc *desc,
+                          const unsigned char *frame, long pitch, int buf);
+/* test hook: 1 forces the generic one-pass-per-launch path even when the
+   fused kernels apply (they must agree bit for bit) */
+int klt_hip_set_path(klt_hip_ctx *ctx, int force_generic);
+/* 1 if the slot was built by the fused gfx950 kernels, 0 generic, <0 invalid */
+int klt_hip_pyramid_path(klt_hip_ctx *ctx, int slot);
+int klt_hip_level_dims(klt_hip_ctx *ctx, int slot, int level, int *ncols, int *nrows);
+/* synchronous copy of one level plane (which: 0 img, 1 gradx, 2 grady) */
+int klt_hip_download_level(klt_hip_ctx *ctx, int slot, int level, int which, float *host);
+/* device pointer of a level plane (valid until the slot is rebuilt at a new size) */
+const float *klt_hip_level_ptr(klt_hip_ctx *ctx, int slot, int level, int which);
+
+/* track n features from slot1 (previous image) to slot2 (current image).
+   on_device = 0: x/y/val are host arrays (copied in/out, synchronous);
+   on_device = 1: x/y/val are device arrays, updated in place, asynchronous. */
+int klt_hip_track(klt_hip_ctx *ctx, int slot1, int slot2, const klt_hip_track_desc *desc,
+                  float *x, float *y, int *val, int n, int on_device);
+
+/* device-resident sequential tracking (the bench hot loop): for each step k,
+   build frame t0+k (frames + (t0+k)*stride) into the slot not holding the
+   previous pyramid (*cur_slot, 0 or 1), then track the device feature arrays
+   from *cur_slot into it and flip *cur_slot.  Asynchronous. */
+int klt_hip_track_sequence(klt_hip_ctx *ctx, const klt_hip_pyr_desc *pdesc,
+                           const klt_hip_track_desc *tdesc, const unsigned char *frames, long pitch,
+                           long stride, int t0, int nsteps, float *x, float *y, int *val, int n,
+                           int *cur_slot);
+
+/* trackability map of level 0 of `slot`: nx*ny int values, row-major over the
+   border-trimmed grid; vals == NULL only reports nx, ny.  Synchronous. */
+int klt_hip_min_eigen(klt_hip_ctx *ctx, int slot, const klt_hip_select_desc *desc, int *vals,
+                      int *nx, int *ny);
+
+/* synthetic frames t0..t0+n-1 (include/klt_synth.h) into device memory */
+int klt_hip_synth_frames(klt_hip_ctx *ctx, unsigned long long seed, int t0, int n, int ncols,
+                         int nrows, unsigned char *dev, long pitch, long frame_stride);
+
+/* device memory helpers (for callers without torch) */
+void *klt_hip_malloc(klt_hip_ctx *ctx, size_t bytes);
+void klt_hip_free(klt_hip_ctx *ctx, void *p);
+int klt_hip_memcpy(klt_hip_ctx *ctx, void *dst, const void *src, size_t bytes, int kind);
+
+int klt_hip_set_timing(klt_hip_ctx *ctx, int on);
+/* synchronises, resolves the recorded events, resets the counters */
+int klt_hip_get_timing(klt_hip_ctx *ctx, klt_hip_timing *out);
+
+/* numerics self-checks used by the tests: f64 sqrt and f32 divide on device */
+int klt_hip_selftest_sqrt(klt_hip_ctx *ctx, const double *in, double *out, int n);
+int klt_hip_selftest_div(klt_hip_ctx *ctx, const float *a, const float *b, float *out, int n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KLT_HIP_H */

@@ -1,0 +1,721 @@
+/*
+ * klt_api.c -- the klt.h C API of libklt_amd.so (host C).
+ *
+ * Mirrors the reference library's public behaviour (klt.c, selectGoodFeatures.c
+ * :297-541, trackFeatures.c:1234-1529, storeFeatures.c) -- same defaults,
+ * derived parameters, warnings, error exits and in-place feature updates --
+ * while the pixel work runs on the GPU through include/klt_hip.h:
+ *
+ *   KLTTrackFeatures:  u8 frame -> klt_hip_upload_frame -> klt_hip_build_pyramid
+ *                      (fused gfx950 kernels) -> klt_hip_track (wave64 per feature)
+ *   KLTSelectGoodFeatures / KLTReplaceLostFeatures:
+ *                      -> klt_hip_build_pyramid(level 0) -> klt_hip_min_eigen
+ *                      -> exact lazy quicksort + min-distance on the host
+ *
+ * Device state lives in a private block allocated right behind the public
+ * KLT_TrackingContextRec (callers only ever see the public part, whose layout
+ * is the reference's).  In sequential mode tc->pyramid_last* point into that
+ * block: non-NULL exactly when the reference's would be.
+ *
+ * There is no CPU fallback: a missing or failing GPU is a KLTError.
+ */
+#include <math.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "klt.h"
+#include "klt_amd.h"
+#include "klt_hip.h"
+#include "klt_select.h"
+#include "klt_util.h"
+#include "pnmio.h"
+
+#define EXPORT __attribute__((visibility("default")))
+
+EXPORT int KLT_verbose = 1; /* selectGoodFeatures.c:22 */
+
+/* defaults (klt.c:20-44) */
+enum { DEF_MINDIST = 10, DEF_WINDOW = 7, DEF_MIN_EIG = 1, DEF_MAX_IT = 10, DEF_SEARCH = 15 };
+
+/* ------------------------------------------------------------------ */
+/* private context                                                     */
+/* ------------------------------------------------------------------ */
+typedef struct {
+  KLT_TrackingContextRec pub; /* must stay first */
+  klt_hip_ctx *dev;
+  int last_slot; /* slot holding the sequential-mode pyramid, -1 none */
+  int last_w, last_h;
+  int reduction; /* KLT_HIP_EXACT unless KLT_AMD_REDUCTION=fast */
+} klt_ctx_full;
+
+#define FULL(tc) ((klt_ctx_full *)(tc))
+
+enum { SLOT_A = 0, SLOT_B = 1, SLOT_SELECT = 2 };
+
+static klt_hip_ctx *device_of(KLT_TrackingContext tc)
+{
+  klt_ctx_full *f = FULL(tc);
+  if (!f->dev) {
+    if (klt_hip_device_count() <= 0)
+      KLTError("(KLT) no HIP device available: libklt_amd runs the tracker on the GPU only");
+    f->dev = klt_hip_ctx_create(-1);
+    if (!f->dev) KLTError("(KLT) could not create the HIP context");
+  }
+  return f->dev;
+}
+
+static void dev_check(KLT_TrackingContext tc, int rc, const char *what)
+{
+  if (rc != 0) KLTError("(KLT) %s failed: %s", what, klt_hip_last_error(FULL(tc)->dev));
+}
+
+/* ------------------------------------------------------------------ */
+/* Gaussian taps: convolve.c:60-114 with the global sigma cache of      */
+/* convolve.c:25-27 (process-wide, like the reference).                 */
+/* ------------------------------------------------------------------ */
+static pthread_mutex_t g_taps_lock = PTHREAD_MUTEX_INITIALIZER;
+static klt_hip_taps g_gauss, g_deriv;
+static float g_sigma_last = -10.0f;
+
+static void taps_make(float sigma, klt_hip_taps *gauss, klt_hip_taps *deriv)
+{
+  enum { MAXW = KLT_HIP_MAX_TAPS, HW = KLT_HIP_MAX_TAPS / 2 };
+  const float factor = 0.01f;
+  float g[MAXW], d[MAXW];
+  const float max_gauss = 1.0f;
+  const float max_deriv = (float)(sigma * exp(-0.5f));
+  int i, wg = MAXW, wd = MAXW, shift;
+
+  for (i = -HW; i <= HW; i++) {
+    g[i + HW] = (float)exp(-i * i / (2 * sigma * sigma));
+    d[i + HW] = -i * g[i + HW];
+  }
+  for (i = -HW; fabs(g[i + HW] / max_gauss) < factor; i++) wg -= 2;
+  for (i = -HW; fabs(d[i + HW] / max_deriv) < factor; i++) wd -= 2;
+  if (wg == MAXW || wd == MAXW)
+    KLTError("(_computeKernels) MAX_KERNEL_WIDTH %d is too small for a sigma of %f", MAXW, sigma);
+
+  memset(gauss, 0, sizeof *gauss);
+  memset(deriv, 0, sizeof *deriv);
+  gauss->width = wg;
+  deriv->width = wd;
+  shift = (MAXW - wg) / 2;
+  for (i = 0; i < wg; i++) gauss->k[i] = g[i + shift];
+  shift = (MAXW - wd) / 2;
+  for (i = 0; i < wd; i++) deriv->k[i] = d[i + shift];
+  {
+    float sum = 0.0f;
+    const int h = wd / 2;
+    for (i = 0; i < wg; i++) sum += gauss->k[i];
+    for (i = 0; i < wg; i++) gauss->k[i] /= sum;
+    sum = 0.0f;
+    for (i = -h; i <= h; i++) sum -= i * deriv->k[i + h];
+    for (i = -h; i <= h; i++) deriv->k[i + h] /= sum;
+  }
+}
+
+/* cached lookup as _KLTComputeSmoothedImage / _KLTComputeGradients do it */
+static void taps_lookup(float sigma, klt_hip_taps *gauss, klt_hip_taps *deriv)
+{
+  pthread_mutex_lock(&g_taps_lock);
+  if (fabs(sigma - g_sigma_last) > 0.05) {
+    taps_make(sigma, &g_gauss, &g_deriv);
+    g_sigma_last = sigma;
+  }
+  if (gauss) *gauss = g_gauss;
+  if (deriv) *deriv = g_deriv;
+  pthread_mutex_unlock(&g_taps_lock);
+}
+
+/* _KLTGetKernelWidths (convolve.c:122-130): recomputes unconditionally */
+static void taps_widths(float sigma, int *gw, int *dw)
+{
+  pthread_mutex_lock(&g_taps_lock);
+  taps_make(sigma, &g_gauss, &g_deriv);
+  g_sigma_last = sigma;
+  *gw = g_gauss.width;
+  *dw = g_deriv.width;
+  pthread_mutex_unlock(&g_taps_lock);
+}
+
+/* ------------------------------------------------------------------ */
+/* parameters                                                          */
+/* ------------------------------------------------------------------ */
+EXPORT float _KLTComputeSmoothSigma(KLT_TrackingContext tc)
+{
+  const int m = tc->window_width > tc->window_height ? tc->window_width : tc->window_height;
+  return tc->smooth_sigma_fact * m;
+}
+
+static float pyramid_sigma(KLT_TrackingContext tc)
+{
+  return tc->pyramid_sigma_fact * tc->subsampling; /* klt.c:350-354 */
+}
+
+/* odd window >= 3, with the caller's warning prefix */
+static void window_fix(KLT_TrackingContext tc, const char *who)
+{
+  const char *pre = who ? who : "";
+  const char *sep = who ? " " : "";
+  if (tc->window_width % 2 != 1) {
+    tc->window_width = tc->window_width + 1;
+    KLTWarning("%s%s%s.  Changing to %d.\n", pre, sep,
+               who ? "Window width must be odd" : "Tracking context's window width must be odd",
+               tc->window_width);
+  }
+  if (tc->window_height % 2 != 1) {
+    tc->window_height = tc->window_height + 1;
+    KLTWarning("%s%s%s.  Changing to %d.\n", pre, sep,
+               who ? "Window height must be odd" : "Tracking context's window height must be odd",
+               tc->window_height);
+  }
+  if (tc->window_width < 3) {
+    tc->window_width = 3;
+    KLTWarning("%s%s%s.  \nChanging to %d.\n", pre, sep,
+               who ? "Window width must be at least three"
+                   : "Tracking context's window width must be at least three",
+               tc->window_width);
+  }
+  if (tc->window_height < 3) {
+    tc->window_height = 3;
+    KLTWarning("%s%s%s.  \nChanging to %d.\n", pre, sep,
+               who ? "Window height must be at least three"
+                   : "Tracking context's window height must be at least three",
+               tc->window_height);
+  }
+}
+
+EXPORT void KLTChangeTCPyramid(KLT_TrackingContext tc, int search_range)
+{
+  float half, ss;
+  window_fix(tc, "(KLTChangeTCPyramid)");
+  half = (tc->window_width < tc->window_height ? tc->window_width : tc->window_height) / 2.0f;
+  ss = ((float)search_range) / half;
+  if (ss < 1.0) {
+    tc->nPyramidLevels = 1;
+  } else if (ss <= 3.0) {
+    tc->nPyramidLevels = 2;
+    tc->subsampling = 2;
+  } else if (ss <= 5.0) {
+    tc->nPyramidLevels = 2;
+    tc->subsampling = 4;
+  } else if (ss <= 9.0) {
+    tc->nPyramidLevels = 2;
+    tc->subsampling = 8;
+  } else {
+    /* search_range = half * (8^L - 1) / 7, rounded up (klt.c:332-341) */
+    const float v = (float)(log(7.0 * ss + 1.0) / log(8.0));
+    tc->nPyramidLevels = (int)(v + 0.99);
+    tc->subsampling = 8;
+  }
+}
+
+EXPORT void KLTUpdateTCBorder(KLT_TrackingContext tc)
+{
+  int gw, dw, smooth_hw, pyr_hw, invalid, i, ss_pow = 1, win_hw;
+  window_fix(tc, "(KLTUpdateTCBorder)");
+  win_hw = (tc->window_width > tc->window_height ? tc->window_width : tc->window_height) / 2;
+  taps_widths(_KLTComputeSmoothSigma(tc), &gw, &dw);
+  smooth_hw = gw / 2;
+  taps_widths(pyramid_sigma(tc), &gw, &dw);
+  pyr_hw = gw / 2;
+  invalid = smooth_hw;
+  for (i = 1; i < tc->nPyramidLevels; i++) {
+    const float v = ((float)invalid + pyr_hw) / tc->subsampling;
+    invalid = (int)(v + 0.99);
+  }
+  for (i = 1; i < tc->nPyramidLevels; i++) ss_pow *= tc->subsampling;
+  tc->borderx = tc->bordery = (invalid + win_hw) * ss_pow;
+}
+
+EXPORT KLT_TrackingContext KLTCreateTrackingContext(void)
+{
+  klt_ctx_full *f = (klt_ctx_full *)calloc(1, sizeof(klt_ctx_full));
+  KLT_TrackingContext tc;
+  const char *red = getenv("KLT_AMD_REDUCTION");
+  if (!f) KLTError("(KLTCreateTrackingContext) Out of memory");
+  tc = &f->pub;
+  tc->mindist = DEF_MINDIST;
+  tc->window_width = DEF_WINDOW;
+  tc->window_height = DEF_WINDOW;
+  tc->sequentialMode = FALSE;
+  tc->smoothBeforeSelecting = TRUE;
+  tc->writeInternalImages = FALSE;
+  tc->lighting_insensitive = FALSE;
+  tc->min_eigenvalue = DEF_MIN_EIG;
+  tc->min_determinant = 0.01f;
+  tc->max_iterations = DEF_MAX_IT;
+  tc->min_displacement = 0.1f;
+  tc->max_residue = 10.0f;
+  tc->grad_sigma = 1.0f;
+  tc->smooth_sigma_fact = 0.1f;
+  tc->pyramid_sigma_fact = 0.9f;
+  tc->step_factor = 1.0f;
+  tc->nSkippedPixels = 0;
+  tc->pyramid_last = tc->pyramid_last_gradx = tc->pyramid_last_grady = NULL;
+  tc->affineConsistencyCheck = -1;
+  tc->affine_window_width = tc->affine_window_height = 15;
+  tc->affine_max_iterations = 10;
+  tc->affine_max_residue = 10.0f;
+  tc->affine_min_displacement = 0.02f;
+  tc->affine_max_displacement_differ = 1.5f;
+  f->dev = NULL;
+  f->last_slot = -1;
+  f->reduction = (red && strcmp(red, "fast") == 0) ? KLT_HIP_FAST : KLT_HIP_EXACT;
+  KLTChangeTCPyramid(tc, DEF_SEARCH);
+  KLTUpdateTCBorder(tc);
+  return tc;
+}
+
+EXPORT void klt_amd_track_desc(KLT_TrackingContext tc, klt_hip_track_desc *td);
+
+static void drop_sequential(KLT_TrackingContext tc)
+{
+  FULL(tc)->last_slot = -1;
+  tc->pyramid_last = tc->pyramid_last_gradx = tc->pyramid_last_grady = NULL;
+}
+
+EXPORT void KLTFreeTrackingContext(KLT_TrackingContext tc)
+{
+  klt_ctx_full *f;
+  if (!tc) return;
+  f = FULL(tc);
+  if (f->dev) klt_hip_ctx_destroy(f->dev);
+  free(f);
+}
+
+EXPORT void KLTStopSequentialMode(KLT_TrackingContext tc)
+{
+  tc->sequentialMode = FALSE;
+  drop_sequential(tc);
+}
+
+EXPORT void KLTSetVerbosity(int verbosity) { KLT_verbose = verbosity; }
+
+EXPORT void KLTPrintTrackingContext(KLT_TrackingContext tc)
+{
+  fprintf(stderr, "\n\nTracking context:\n\n");
+  fprintf(stderr, "\tmindist = %d\n", tc->mindist);
+  fprintf(stderr, "\twindow_width = %d\n", tc->window_width);
+  fprintf(stderr, "\twindow_height = %d\n", tc->window_height);
+  fprintf(stderr, "\tsequentialMode = %s\n", tc->sequentialMode ? "TRUE" : "FALSE");
+  fprintf(stderr, "\tsmoothBeforeSelecting = %s\n", tc->smoothBeforeSelecting ? "TRUE" : "FALSE");
+  fprintf(stderr, "\twriteInternalImages = %s\n", tc->writeInternalImages ? "TRUE" : "FALSE");
+  fprintf(stderr, "\tmin_eigenvalue = %d\n", tc->min_eigenvalue);
+  fprintf(stderr, "\tmin_determinant = %f\n", tc->min_determinant);
+  fprintf(stderr, "\tmin_displacement = %f\n", tc->min_displacement);
+  fprintf(stderr, "\tmax_iterations = %d\n", tc->max_iterations);
+  fprintf(stderr, "\tmax_residue = %f\n", tc->max_residue);
+  fprintf(stderr, "\tgrad_sigma = %f\n", tc->grad_sigma);
+  fprintf(stderr, "\tsmooth_sigma_fact = %f\n", tc->smooth_sigma_fact);
+  fprintf(stderr, "\tpyramid_sigma_fact = %f\n", tc->pyramid_sigma_fact);
+  fprintf(stderr, "\tnSkippedPixels = %d\n", tc->nSkippedPixels);
+  fprintf(stderr, "\tborderx = %d\n", tc->borderx);
+  fprintf(stderr, "\tbordery = %d\n", tc->bordery);
+  fprintf(stderr, "\tnPyramidLevels = %d\n", tc->nPyramidLevels);
+  fprintf(stderr, "\tsubsampling = %d\n", tc->subsampling);
+  fprintf(stderr, "\n\tpyramid_last = %s\n", tc->pyramid_last ? "points to old image" : "NULL");
+  fprintf(stderr, "\tpyramid_last_gradx = %s\n",
+          tc->pyramid_last_gradx ? "points to old image" : "NULL");
+  fprintf(stderr, "\tpyramid_last_grady = %s\n",
+          tc->pyramid_last_grady ? "points to old image" : "NULL");
+  fprintf(stderr, "\n\n");
+}
+
+/* ------------------------------------------------------------------ */
+/* lists, histories, tables (klt.c:143-236, 453-483; storeFeatures.c)   */
+/* ------------------------------------------------------------------ */
+EXPORT KLT_FeatureList KLTCreateFeatureList(int n)
+{
+  const size_t bytes = sizeof(KLT_FeatureListRec) + (size_t)n * (sizeof(KLT_Feature) + sizeof(KLT_FeatureRec));
+  KLT_FeatureList fl = (KLT_FeatureList)malloc(bytes);
+  KLT_Feature recs;
+  int i;
+  if (!fl) KLTError("(KLTCreateFeatureList) Out of memory");
+  fl->nFeatures = n;
+  fl->feature = (KLT_Feature *)(fl + 1);
+  recs = (KLT_Feature)(fl->feature + n);
+  for (i = 0; i < n; i++) {
+    fl->feature[i] = recs + i;
+    recs[i].aff_img = recs[i].aff_img_gradx = recs[i].aff_img_grady = NULL;
+  }
+  return fl;
+}
+
+EXPORT KLT_FeatureHistory KLTCreateFeatureHistory(int n)
+{
+  const size_t bytes =
+      sizeof(KLT_FeatureHistoryRec) + (size_t)n * (sizeof(KLT_Feature) + sizeof(KLT_FeatureRec));
+  KLT_FeatureHistory fh = (KLT_FeatureHistory)malloc(bytes);
+  KLT_Feature recs;
+  int i;
+  if (!fh) KLTError("(KLTCreateFeatureHistory) Out of memory");
+  fh->nFrames = n;
+  fh->feature = (KLT_Feature *)(fh + 1);
+  recs = (KLT_Feature)(fh->feature + n);
+  for (i = 0; i < n; i++) fh->feature[i] = recs + i;
+  return fh;
+}
+
+EXPORT KLT_FeatureTable KLTCreateFeatureTable(int nFrames, int nFeatures)
+{
+  KLT_FeatureTable ft = (KLT_FeatureTable)malloc(sizeof(KLT_FeatureTableRec));
+  KLT_Feature recs;
+  KLT_Feature **rows;
+  int i, j;
+  if (!ft) KLTError("(KLTCreateFeatureTable) Out of memory");
+  ft->nFrames = nFrames;
+  ft->nFeatures = nFeatures;
+  /* row pointers followed by the pointer matrix in one block (klt.c:67-82) */
+  rows = (KLT_Feature **)malloc((size_t)nFeatures * sizeof(void *) +
+                                (size_t)nFrames * nFeatures * sizeof(KLT_Feature));
+  recs = (KLT_Feature)malloc((size_t)nFrames * nFeatures * sizeof(KLT_FeatureRec) + 1);
+  if (!rows || !recs) KLTError("(createArray2D) Out of memory");
+  for (j = 0; j < nFeatures; j++)
+    rows[j] = (KLT_Feature *)((char *)rows + (size_t)nFeatures * sizeof(void *) +
+                              (size_t)j * nFrames * sizeof(KLT_Feature));
+  for (j = 0; j < nFeatures; j++)
+    for (i = 0; i < nFrames; i++) rows[j][i] = recs + (size_t)j * nFrames + i;
+  ft->feature = rows;
+  return ft;
+}
+
+EXPORT void KLTFreeFeatureList(KLT_FeatureList fl)
+{
+  int i;
+  if (!fl) return;
+  for (i = 0; i < fl->nFeatures; i++) {
+    free(fl->feature[i]->aff_img);
+    free(fl->feature[i]->aff_img_gradx);
+    free(fl->feature[i]->aff_img_grady);
+    fl->feature[i]->aff_img = fl->feature[i]->aff_img_gradx = fl->feature[i]->aff_img_grady = NULL;
+  }
+  free(fl);
+}
+
+EXPORT void KLTFreeFeatureHistory(KLT_FeatureHistory fh) { free(fh); }
+
+EXPORT void KLTFreeFeatureTable(KLT_FeatureTable ft)
+{
+  if (!ft) return;
+  if (ft->nFeatures > 0 && ft->nFrames > 0) free(ft->feature[0][0]);
+  free(ft->feature);
+  free(ft);
+}
+
+EXPORT int KLTCountRemainingFeatures(KLT_FeatureList fl)
+{
+  int n = 0, i;
+  for (i = 0; i < fl->nFeatures; i++) n += fl->feature[i]->val >= 0;
+  return n;
+}
+
+static void copy_xyv(KLT_Feature dst, const KLT_FeatureRec *src)
+{
+  dst->x = src->x;
+  dst->y = src->y;
+  dst->val = src->val;
+}
+
+EXPORT void KLTStoreFeatureList(KLT_FeatureList fl, KLT_FeatureTable ft, int frame)
+{
+  int k;
+  if (frame < 0 || frame >= ft->nFrames)
+    KLTError("(KLTStoreFeatures) Frame number %d is not between 0 and %d", frame, ft->nFrames - 1);
+  if (fl->nFeatures != ft->nFeatures)
+    KLTError("(KLTStoreFeatures) FeatureList and FeatureTable must have the same number of features");
+  for (k = 0; k < fl->nFeatures; k++) copy_xyv(ft->feature[k][frame], fl->feature[k]);
+}
+
+EXPORT void KLTExtractFeatureList(KLT_FeatureList fl, KLT_FeatureTable ft, int frame)
+{
+  int k;
+  if (frame < 0 || frame >= ft->nFrames)
+    KLTError("(KLTExtractFeatures) Frame number %d is not between 0 and %d", frame, ft->nFrames - 1);
+  if (fl->nFeatures != ft->nFeatures)
+    KLTError("(KLTExtractFeatures) FeatureList and FeatureTable must have the same number of features");
+  for (k = 0; k < fl->nFeatures; k++) copy_xyv(fl->feature[k], ft->feature[k][frame]);
+}
+
+EXPORT void KLTStoreFeatureHistory(KLT_FeatureHistory fh, KLT_FeatureTable ft, int feat)
+{
+  int i;
+  if (feat < 0 || feat >= ft->nFeatures)
+    KLTError("(KLTStoreFeatureHistory) Feature number %d is not between 0 and %d", feat,
+             ft->nFeatures - 1);
+  if (fh->nFrames != ft->nFrames)
+    KLTError("(KLTStoreFeatureHistory) FeatureHistory and FeatureTable must have the same number of frames");
+  for (i = 0; i < fh->nFrames; i++) copy_xyv(ft->feature[feat][i], fh->feature[i]);
+}
+
+EXPORT void KLTExtractFeatureHistory(KLT_FeatureHistory fh, KLT_FeatureTable ft, int feat)
+{
+  int i;
+  if (feat < 0 || feat >= ft->nFeatures)
+    KLTError("(KLTExtractFeatureHistory) Feature number %d is not between 0 and %d", feat,
+             ft->nFeatures - 1);
+  if (fh->nFrames != ft->nFrames)
+    KLTError("(KLTExtractFeatureHistory) FeatureHistory and FeatureTable must have the same number of frames");
+  for (i = 0; i < fh->nFrames; i++) copy_xyv(fh->feature[i], ft->feature[feat][i]);
+}
+
+/* ------------------------------------------------------------------ */
+/* device glue                                                         */
+/* ------------------------------------------------------------------ */
+
+/* taps for one frame's pyramid, looked up in the reference's call order:
+   smooth (sigma_s), level >= 1 smoothing (sigma_p), then per-level
+   gradients (sigma_g) -- trackFeatures.c:1298-1307 */
+static void pyr_desc(KLT_TrackingContext tc, int ncols, int nrows, int nlevels, int smooth,
+                     klt_hip_pyr_desc *d)
+{
+  int l;
+  memset(d, 0, sizeof *d);
+  d->ncols = ncols;
+  d->nrows = nrows;
+  d->nlevels = nlevels;
+  d->subsampling = nlevels > 1 ? tc->subsampling : 1;
+  d->smooth_input = smooth;
+  if (smooth) taps_lookup(_KLTComputeSmoothSigma(tc), &d->smooth, NULL);
+  for (l = 1; l < nlevels; l++) taps_lookup(pyramid_sigma(tc), &d->pyr, NULL);
+  for (l = 0; l < nlevels; l++) taps_lookup(tc->grad_sigma, &d->grad_gauss, &d->grad_deriv);
+}
+
+static void build_from_host(KLT_TrackingContext tc, int slot, int buf, KLT_PixelType *img,
+                            const klt_hip_pyr_desc *d)
+{
+  klt_hip_ctx *dev = device_of(tc);
+  dev_check(tc, klt_hip_upload_frame(dev, buf, img, d->ncols, d->nrows), "frame upload");
+  dev_check(tc, klt_hip_build_pyramid(dev, slot, d, NULL, 0, buf), "pyramid build");
+}
+
+static void write_level_pgm(KLT_TrackingContext tc, int slot, int level, int which, const char *name)
+{
+  klt_hip_ctx *dev = FULL(tc)->dev;
+  int w, h;
+  _KLT_FloatImage img;
+  dev_check(tc, klt_hip_level_dims(dev, slot, level, &w, &h), "level dims");
+  img = _KLTCreateFloatImage(w, h);
+  dev_check(tc, klt_hip_download_level(dev, slot, level, which, img->data), "level download");
+  _KLTWriteFloatImageToPGM(img, (char *)name);
+  _KLTFreeFloatImage(img);
+}
+
+/* _KLTSelectGoodFeatures (selectGoodFeatures.c:297-453) */
+static void select_features(KLT_TrackingContext tc, KLT_PixelType *img, int ncols, int nrows,
+                            KLT_FeatureList fl, int replacing)
+{
+  klt_ctx_full *f = FULL(tc);
+  klt_hip_ctx *dev;
+  klt_hip_select_desc sd;
+  int slot, nx = 0, ny = 0, *vals;
+
+  window_fix(tc, NULL);
+  dev = device_of(tc);
+  if (replacing && tc->sequentialMode && tc->pyramid_last != NULL && f->last_slot >= 0) {
+    slot = f->last_slot; /* level 0 of the last pyramid (:342-348) */
+  } else {
+    klt_hip_pyr_desc d;
+    slot = SLOT_SELECT;
+    pyr_desc(tc, ncols, nrows, 1, tc->smoothBeforeSelecting, &d);
+    build_from_host(tc, slot, 0, img, &d);
+  }
+  if (tc->writeInternalImages) {
+    write_level_pgm(tc, slot, 0, 0, "kltimg_sgfrlf.pgm");
+    write_level_pgm(tc, slot, 0, 1, "kltimg_sgfrlf_gx.pgm");
+    write_level_pgm(tc, slot, 0, 2, "kltimg_sgfrlf_gy.pgm");
+  }
+  sd.window_width = tc->window_width;
+  sd.window_height = tc->window_height;
+  sd.borderx = tc->borderx < tc->window_width / 2 ? tc->window_width / 2 : tc->borderx;
+  sd.bordery = tc->bordery < tc->window_height / 2 ? tc->window_height / 2 : tc->bordery;
+  sd.nSkippedPixels = tc->nSkippedPixels;
+  dev_check(tc, klt_hip_min_eigen(dev, slot, &sd, NULL, &nx, &ny), "trackability map");
+  vals = (int *)malloc(sizeof(int) * ((size_t)nx * ny + 1));
+  if (!vals) KLTError("(KLTSelectGoodFeatures) Out of memory");
+  dev_check(tc, klt_hip_min_eigen(dev, slot, &sd, vals, &nx, &ny), "trackability map");
+  if (tc->mindist < 0) {
+    KLTWarning("(_KLTSelectGoodFeatures) Tracking context field tc->mindist is negative (%d); "
+               "setting to zero",
+               tc->mindist);
+    tc->mindist = 0;
+  }
+  klt_select_from_map(vals, nx, ny, sd.borderx, sd.bordery, tc->nSkippedPixels + 1, ncols, nrows, fl,
+                      tc->mindist, tc->min_eigenvalue, !replacing);
+  free(vals);
+}
+
+EXPORT void KLTSelectGoodFeatures(KLT_TrackingContext tc, KLT_PixelType *img, int ncols, int nrows,
+                                  KLT_FeatureList fl)
+{
+  if (KLT_verbose >= 1) {
+    fprintf(stderr, "(KLT) Selecting the %d best features from a %d by %d image...  ", fl->nFeatures,
+            ncols, nrows);
+    fflush(stderr);
+  }
+  select_features(tc, img, ncols, nrows, fl, 0);
+  if (KLT_verbose >= 1) {
+    fprintf(stderr, "\n\t%d features found.\n", KLTCountRemainingFeatures(fl));
+    if (tc->writeInternalImages) fprintf(stderr, "\tWrote images to 'kltimg_sgfrlf*.pgm'.\n");
+    fflush(stderr);
+  }
+}
+
+EXPORT void KLTReplaceLostFeatures(KLT_TrackingContext tc, KLT_PixelType *img, int ncols, int nrows,
+                                   KLT_FeatureList fl)
+{
+  const int lost = fl->nFeatures - KLTCountRemainingFeatures(fl);
+  if (KLT_verbose >= 1) {
+    fprintf(stderr, "(KLT) Attempting to replace %d features in a %d by %d image...  ", lost, ncols,
+            nrows);
+    fflush(stderr);
+  }
+  if (lost > 0) select_features(tc, img, ncols, nrows, fl, 1);
+  if (KLT_verbose >= 1) {
+    fprintf(stderr, "\n\t%d features replaced.\n", lost - fl->nFeatures + KLTCountRemainingFeatures(fl));
+    if (tc->writeInternalImages) fprintf(stderr, "\tWrote images to 'kltimg_sgfrlf*.pgm'.\n");
+    fflush(stderr);
+  }
+}
+
+static void drop_affine(KLT_Feature f)
+{
+  free(f->aff_img);
+  free(f->aff_img_gradx);
+  free(f->aff_img_grady);
+  f->aff_img = f->aff_img_gradx = f->aff_img_grady = NULL;
+}
+
+/* KLTTrackFeatures (trackFeatures.c:1234-1529) */
+EXPORT void KLTTrackFeatures(KLT_TrackingContext tc, KLT_PixelType *img1, KLT_PixelType *img2,
+                             int ncols, int nrows, KLT_FeatureList fl)
+{
+  klt_ctx_full *f = FULL(tc);
+  klt_hip_ctx *dev;
+  klt_hip_pyr_desc d;
+  klt_hip_track_desc td;
+  int slot1, slot2, k, n = fl->nFeatures;
+  float *x, *y;
+  int *v;
+
+  if (KLT_verbose >= 1) {
+    fprintf(stderr, "(KLT) Tracking %d features in a %d by %d image...  ", KLTCountRemainingFeatures(fl),
+            ncols, nrows);
+    fflush(stderr);
+  }
+  window_fix(tc, NULL);
+  if (tc->affineConsistencyCheck >= 0)
+    KLTError("(KLTTrackFeatures) affineConsistencyCheck=%d is not supported by libklt_amd "
+             "(only -1, the reference harness setting)",
+             tc->affineConsistencyCheck);
+  dev = device_of(tc);
+
+  if (tc->sequentialMode && tc->pyramid_last != NULL && f->last_slot >= 0) {
+    if (f->last_w != ncols || f->last_h != nrows)
+      KLTError("(KLTTrackFeatures) Size of incoming image (%d by %d) is different from size of "
+               "previous image (%d by %d)\n",
+               ncols, nrows, f->last_w, f->last_h);
+    slot1 = f->last_slot;
+  } else {
+    slot1 = SLOT_A;
+    pyr_desc(tc, ncols, nrows, tc->nPyramidLevels, 1, &d);
+    build_from_host(tc, slot1, 0, img1, &d);
+  }
+  slot2 = slot1 == SLOT_A ? SLOT_B : SLOT_A;
+  pyr_desc(tc, ncols, nrows, tc->nPyramidLevels, 1, &d);
+  build_from_host(tc, slot2, 1, img2, &d);
+
+  if (tc->writeInternalImages) {
+    char name[80];
+    int l;
+    for (l = 0; l < tc->nPyramidLevels; l++) {
+      sprintf(name, "kltimg_tf_i%d.pgm", l);
+      write_level_pgm(tc, slot1, l, 0, name);
+      sprintf(name, "kltimg_tf_i%d_gx.pgm", l);
+      write_level_pgm(tc, slot1, l, 1, name);
+      sprintf(name, "kltimg_tf_i%d_gy.pgm", l);
+      write_level_pgm(tc, slot1, l, 2, name);
+      sprintf(name, "kltimg_tf_j%d.pgm", l);
+      write_level_pgm(tc, slot2, l, 0, name);
+      sprintf(name, "kltimg_tf_j%d_gx.pgm", l);
+      write_level_pgm(tc, slot2, l, 1, name);
+      sprintf(name, "kltimg_tf_j%d_gy.pgm", l);
+      write_level_pgm(tc, slot2, l, 2, name);
+    }
+  }
+
+  klt_amd_track_desc(tc, &td);
+
+  x = (float *)malloc(sizeof(float) * (n + 1));
+  y = (float *)malloc(sizeof(float) * (n + 1));
+  v = (int *)malloc(sizeof(int) * (n + 1));
+  if (!x || !y || !v) KLTError("(KLTTrackFeatures) Out of memory");
+  for (k = 0; k < n; k++) {
+    x[k] = fl->feature[k]->x;
+    y[k] = fl->feature[k]->y;
+    v[k] = fl->feature[k]->val;
+  }
+  dev_check(tc, klt_hip_track(dev, slot1, slot2, &td, x, y, v, n, 0), "feature tracking");
+  for (k = 0; k < n; k++) {
+    KLT_Feature ft = fl->feature[k];
+    if (ft->val < 0) continue; /* untouched, like the reference (:1346) */
+    ft->x = x[k];
+    ft->y = y[k];
+    ft->val = v[k];
+    if (v[k] != KLT_TRACKED) drop_affine(ft);
+  }
+  free(x);
+  free(y);
+  free(v);
+
+  if (tc->sequentialMode) {
+    f->last_slot = slot2;
+    f->last_w = ncols;
+    f->last_h = nrows;
+    tc->pyramid_last = &f->last_slot;
+    tc->pyramid_last_gradx = &f->last_w;
+    tc->pyramid_last_grady = &f->last_h;
+  }
+
+  if (KLT_verbose >= 1) {
+    fprintf(stderr, "\n\t%d features successfully tracked.\n", KLTCountRemainingFeatures(fl));
+    if (tc->writeInternalImages) fprintf(stderr, "\tWrote images to 'kltimg_tf*.pgm'.\n");
+    fflush(stderr);
+  }
+}
+
+/* ------------------------------------------------------------------ */
+/* hooks for device-resident callers (bench.py, tests): the descriptors  */
+/* KLTTrackFeatures itself would use for this context                  */
+/* ------------------------------------------------------------------ */
+EXPORT klt_hip_ctx *klt_amd_device_context(KLT_TrackingContext tc) { return device_of(tc); }
+
+EXPORT void klt_amd_pyr_desc(KLT_TrackingContext tc, int ncols, int nrows, int nlevels, int smooth,
+                             klt_hip_pyr_desc *d)
+{
+  window_fix(tc, NULL);
+  pyr_desc(tc, ncols, nrows, nlevels, smooth, d);
+}
+
+EXPORT void klt_amd_track_desc(KLT_TrackingContext tc, klt_hip_track_desc *td)
+{
+  window_fix(tc, NULL);
+  td->window_width = tc->window_width;
+  td->window_height = tc->window_height;
+  td->max_iterations = tc->max_iterations;
+  td->min_determinant = tc->min_determinant;
+  td->min_displacement = tc->min_displacement;
+  td->max_residue = tc->max_residue;
+  td->step_factor = tc->step_factor;
+  td->borderx = tc->borderx;
+  td->bordery = tc->bordery;
+  td->lighting_insensitive = tc->lighting_insensitive;
+  td->reduction = FULL(tc)->reduction;
+}
+
+EXPORT void klt_amd_set_reduction(KLT_TrackingContext tc, int reduction)
+{
+  FULL(tc)->reduction = reduction;
+}

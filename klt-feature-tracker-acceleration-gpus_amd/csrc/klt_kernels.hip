@@ -1,0 +1,1326 @@
+// klt_kernels.hip -- CDNA4 (gfx950) kernels of the MI355X KLT tracker and the
+// klt_hip_* C ABI that launches them (include/klt_hip.h).
+//
+// Parity contract: every output is bit-identical to the reference CPU path
+// (FatimaSohailll/KLT-Feature-Tracker-Acceleration-GPUs src/V3).  That needs
+//   * no multiply-add contraction (built with -ffp-contract=off, and the pragma
+//     below): the reference is compiled for x86-64 without FMA;
+//   * every sum accumulated from +0 in the reference's order;
+//   * IEEE division/sqrt (HIP defaults; never -ffast-math);
+//   * the reference's zero borders after every 1-D pass (convolve.c:164-178,
+//     :216-237), its pyramid sampling points (pyramid.c:120-124) and its
+//     x86 float->int conversion for the trackability values.
+//
+// Memory: every pyramid plane is a tight row-major f32 array (pitch = ncols),
+// the layout the reference's _KLT_FloatImage uses (klt_util.c:31-47).
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "klt_hip.h"
+#include "klt_synth.h"
+
+#define KLT_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;
+
+// status codes (klt.h:28-33)
+constexpr int kTracked = 0, kSmallDet = -2, kMaxIter = -3, kOOB = -4, kLargeResidue = -5;
+
+// taps reversed so that out[c] = sum_{m=0}^{w-1} in[c-r+m] * rk[m], the
+// accumulation order of convolve.c:171-172 / :225-228.
+struct RTaps {
+  int w;
+  float k[KLT_HIP_MAX_TAPS];
+};
+
+RTaps reverse_taps(const klt_hip_taps &t) {
+  RTaps r;
+  r.w = t.width;
+  for (int m = 0; m < t.width; ++m) r.k[m] = t.k[t.width - 1 - m];
+  for (int m = t.width; m < KLT_HIP_MAX_TAPS; ++m) r.k[m] = 0.0f;
+  return r;
+}
+
+template <int RS, int RG, int RP>
+struct FusedTaps {
+  float s[2 * RS + 1];  // smoothing gauss
+  float g[2 * RG + 1];  // gradient gauss
+  float d[2 * RG + 1];  // gradient derivative
+  float p[2 * RP + 1];  // pyramid gauss
+};
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// ---------------------------------------------------------------------------
+// Fused level-0 kernel.  One 256-thread workgroup produces a TH x TW tile of
+//   img0 = cols_s(rows_s(float(u8)))          (_KLTComputeSmoothedImage)
+//   gx0  = cols_g(rows_d(img0)), gy0 = cols_d(rows_g(img0))  (_KLTComputeGradients)
+//   hs   = rows_p(img0) at the columns SS*X+SS/2 only (first half of the
+//          pyramid smoothing, pyramid.c:114 + :120-124), for the tile's rows.
+// Every intermediate stays in LDS; global traffic is the u8 tile (+halo) in
+// and img0/gx0/gy0/hs out.
+// ---------------------------------------------------------------------------
+template <int RS, int RG, int RP, int SS, int TW, int TH>
+struct L0Geom {
+  static constexpr int XP = (RG > RP - SS / 2 + 1) ? RG : (RP - SS / 2 + 1);  // img0 column halo
+  static constexpr int IW = TW + 2 * XP;  // img0 / t1 width
+  static constexpr int IH = TH + 2 * RG;  // img0 rows
+  static constexpr int UW = IW + 2 * RS;  // u8 width
+  static constexpr int UH = IH + 2 * RS;  // u8 / t1 rows
+  static constexpr int A = UH * UW + UH * IW;
+  static constexpr int B = 2 * IH * TW;
+  static constexpr int LDS = (A > B ? A : B) + IH * IW;
+};
+
+template <int RS, int RG, int RP, int SS, int TW, int TH>
+__global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ src, long spitch,
+                                                   int W, int H, FusedTaps<RS, RG, RP> T,
+                                                   float *__restrict__ img0, float *__restrict__ gx0,
+                                                   float *__restrict__ gy0, float *__restrict__ hs,
+                                                   int hsW, int do_hs) {
+  using G = L0Geom<RS, RG, RP, SS, TW, TH>;
+  constexpr int XP = G::XP, IW = G::IW, IH = G::IH, UW = G::UW, UH = G::UH;
+  __shared__ float lds[G::LDS];
+  float *u = lds;             // [UH][UW] float(u8)
+  float *t1 = lds + UH * UW;  // [UH][IW] rows_s
+  float *tx = lds;            // [IH][TW] rows_d(img0)   (reuses u/t1)
+  float *ty = lds + IH * TW;  // [IH][TW] rows_g(img0)
+  float *im = lds + (G::A > G::B ? G::A : G::B);  // [IH][IW] img0
+
+  const int C0 = blockIdx.x * TW, R0 = blockIdx.y * TH;
+  const int tid = threadIdx.x;
+
+  // u8 tile + halo; clamped addresses never feed a non-zero output
+  for (int i = tid; i < UH * UW; i += kBlock) {
+    const int r = i / UW, c = i - r * UW;
+    const int gy = clampi(R0 - RG - RS + r, 0, H - 1);
+    const int gx = clampi(C0 - XP - RS + c, 0, W - 1);
+    u[i] = (float)src[(long)gy * spitch + gx];
+  }
+  __syncthreads();
+
+  // rows pass of the smoothing (zero for x < RS or x >= W-RS)
+  for (int i = tid; i < UH * IW; i += kBlock) {
+    const int r = i / IW, c = i - r * IW;
+    const int gx = C0 - XP + c;
+    float acc = 0.0f;
+    if (gx >= RS && gx < W - RS) {
+      const float *p = u + r * UW + c;
+#pragma unroll
+      for (int m = 0; m < 2 * RS + 1; ++m) acc += p[m] * T.s[m];
+    }
+    t1[i] = acc;
+  }
+  __syncthreads();
+
+  // columns pass -> img0 (zero for y < RS or y >= H-RS)
+  for (int i = tid; i < IH * IW; i += kBlock) {
+    const int r = i / IW, c = i - r * IW;
+    const int gy = R0 - RG + r;
+    float acc = 0.0f;
+    if (gy >= RS && gy < H - RS) {
+      const float *p = t1 + r * IW + c;
+#pragma unroll
+      for (int m = 0; m < 2 * RS + 1; ++m) acc += p[m * IW] * T.s[m];
+    }
+    im[i] = acc;
+  }
+  __syncthreads();
+
+  // img0 tile out; rows pass of both gradients (zero for x < RG or x >= W-RG)
+  for (int i = tid; i < TH * TW; i += kBlock) {
+    const int r = i / TW, c = i - r * TW;
+    const int gy = R0 + r, gx = C0 + c;
+    if (gy < H && gx < W) img0[(long)gy * W + gx] = im[(r + RG) * IW + c + XP];
+  }
+  for (int i = tid; i < IH * TW; i += kBlock) {
+    const int r = i / TW, c = i - r * TW;
+    const int gx = C0 + c;
+    float ax = 0.0f, ay = 0.0f;
+    if (gx >= RG && gx < W - RG) {
+      const float *p = im + r * IW + c + XP - RG;
+#pragma unroll
+      for (int m = 0; m < 2 * RG + 1; ++m) {
+        ax += p[m] * T.d[m];
+        ay += p[m] * T.g[m];
+      }
+    }
+    tx[i] = ax;
+    ty[i] = ay;
+  }
+  // pyramid rows pass at the sampled columns (reads img0 only)
+  if (do_hs) {
+    constexpr int NX = TW / SS;
+    for (int i = tid; i < TH * NX; i += kBlock) {
+      const int r = i / NX, j = i - r * NX;
+      const int gy = R0 + r, X = C0 / SS + j;
+      const int c = SS * j + SS / 2;  // tile column
+      const int gx = C0 + c;
+      float acc = 0.0f;
+      if (gx >= RP && gx < W - RP) {
+        const float *p = im + (r + RG) * IW + c + XP - RP;
+#pragma unroll
+        for (int m = 0; m < 2 * RP + 1; ++m) acc += p[m] * T.p[m];
+      }
+      if (gy < H && X < hsW) hs[(long)gy * hsW + X] = acc;
+    }
+  }
+  __syncthreads();
+
+  // columns pass of both gradients (zero for y < RG or y >= H-RG)
+  for (int i = tid; i < TH * TW; i += kBlock) {
+    const int r = i / TW, c = i - r * TW;
+    const int gy = R0 + r, gx = C0 + c;
+    float ax = 0.0f, ay = 0.0f;
+    if (gy >= RG && gy < H - RG) {
+      const float *px = tx + r * TW + c;
+      const float *py = ty + r * TW + c;
+#pragma unroll
+      for (int m = 0; m < 2 * RG + 1; ++m) {
+        ax += px[m * TW] * T.g[m];
+        ay += py[m * TW] * T.d[m];
+      }
+    }
+    if (gy < H && gx < W) {
+      gx0[(long)gy * W + gx] = ax;
+      gy0[(long)gy * W + gx] = ay;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused level-1 kernel: img1 = cols_p(hs) at rows SS*Y+SS/2 (the rest of
+// pyramid.c:114-124), then its gradients.  Tile = TH x TW level-1 pixels.
+// ---------------------------------------------------------------------------
+template <int RG, int RP, int SS, int TW, int TH>
+struct L1Geom {
+  static constexpr int JW = TW + 2 * RG, JH = TH + 2 * RG;
+  static constexpr int HR = SS * (JH - 1) + 2 * RP + 1;  // hs rows staged
+  static constexpr int A = HR * JW;
+  static constexpr int B = 2 * JH * TW;
+  static constexpr int LDS = (A > B ? A : B) + JH * JW;
+};
+
+template <int RS, int RG, int RP, int SS, int TW, int TH>
+__global__ __launch_bounds__(kBlock) void k_pyr_l1(const float *__restrict__ hs, int W1, int H,
+                                                   int H1, FusedTaps<RS, RG, RP> T,
+                                                   float *__restrict__ img1, float *__restrict__ gx1,
+                                                   float *__restrict__ gy1) {
+  using G = L1Geom<RG, RP, SS, TW, TH>;
+  constexpr int JW = G::JW, JH = G::JH, HR = G::HR;
+  __shared__ float lds[G::LDS];
+  float *hl = lds;           // [HR][JW]
+  float *tx = lds;           // [JH][TW] (reuses hl)
+  float *ty = lds + JH * TW;
+  float *im = lds + (G::A > G::B ? G::A : G::B);  // [JH][JW]
+
+  const int x0 = blockIdx.x * TW, y0 = blockIdx.y * TH;
+  const int tid = threadIdx.x;
+  const int hr0 = SS * (y0 - RG) + SS / 2 - RP;
+
+  for (int i = tid; i < HR * JW; i += kBlock) {
+    const int r = i / JW, c = i - r * JW;
+    const int gy = clampi(hr0 + r, 0, H - 1);
+    const int gx = clampi(x0 - RG + c, 0, W1 - 1);
+    hl[i] = hs[(long)gy * W1 + gx];
+  }
+  __syncthreads();
+
+  for (int i = tid; i < JH * JW; i += kBlock) {
+    const int r = i / JW, c = i - r * JW;
+    const int Y = y0 - RG + r, X = x0 - RG + c;
+    const int rr = SS * Y + SS / 2;
+    float acc = 0.0f;
+    if (Y >= 0 && Y < H1 && X >= 0 && X < W1 && rr >= RP && rr < H - RP) {
+      const float *p = hl + (SS * r) * JW + c;
+#pragma unroll
+      for (int m = 0; m < 2 * RP + 1; ++m) acc += p[m * JW] * T.p[m];
+    }
+    im[i] = acc;
+  }
+  __syncthreads();
+
+  for (int i = tid; i < TH * TW; i += kBlock) {
+    const int r = i / TW, c = i - r * TW;
+    const int Y = y0 + r, X = x0 + c;
+    if (Y < H1 && X < W1) img1[(long)Y * W1 + X] = im[(r + RG) * JW + c + RG];
+  }
+  for (int i = tid; i < JH * TW; i += kBlock) {
+    const int r = i / TW, c = i - r * TW;
+    const int X = x0 + c;
+    float ax = 0.0f, ay = 0.0f;
+    if (X >= RG && X < W1 - RG) {
+      const float *p = im + r * JW + c;
+#pragma unroll
+      for (int m = 0; m < 2 * RG + 1; ++m) {
+        ax += p[m] * T.d[m];
+        ay += p[m] * T.g[m];
+      }
+    }
+    tx[i] = ax;
+    ty[i] = ay;
+  }
+  __syncthreads();
+
+  for (int i = tid; i < TH * TW; i += kBlock) {
+    const int r = i / TW, c = i - r * TW;
+    const int Y = y0 + r, X = x0 + c;
+    float ax = 0.0f, ay = 0.0f;
+    if (Y >= RG && Y < H1 - RG) {
+      const float *px = tx + r * TW + c;
+      const float *py = ty + r * TW + c;
+#pragma unroll
+      for (int m = 0; m < 2 * RG + 1; ++m) {
+        ax += px[m * TW] * T.g[m];
+        ay += py[m * TW] * T.d[m];
+      }
+    }
+    if (Y < H1 && X < W1) {
+      gx1[(long)Y * W1 + X] = ax;
+      gy1[(long)Y * W1 + X] = ay;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Generic path (any sigma / levels / subsampling): one 1-D pass per launch.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_u8_to_f32(const uint8_t *__restrict__ src, long spitch,
+                                                      int W, int H, float *__restrict__ out) {
+  const long i = (long)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= (long)W * H) return;
+  const int y = (int)(i / W), x = (int)(i - (long)y * W);
+  out[i] = (float)src[(long)y * spitch + x];
+}
+
+__global__ __launch_bounds__(kBlock) void k_rows(const float *__restrict__ in, int W, int H, RTaps t,
+                                                 float *__restrict__ out) {
+  const long i = (long)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= (long)W * H) return;
+  const int y = (int)(i / W), x = (int)(i - (long)y * W);
+  const int r = t.w / 2;
+  float acc = 0.0f;
+  if (x >= r && x < W - r) {
+    const float *p = in + (long)y * W + x - r;
+    for (int m = 0; m < t.w; ++m) acc += p[m] * t.k[m];
+  }
+  out[i] = acc;
+}
+
+__global__ __launch_bounds__(kBlock) void k_cols(const float *__restrict__ in, int W, int H, RTaps t,
+                                                 float *__restrict__ out) {
+  const long i = (long)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= (long)W * H) return;
+  const int y = (int)(i / W), x = (int)(i - (long)y * W);
+  const int r = t.w / 2;
+  float acc = 0.0f;
+  if (y >= r && y < H - r) {
+    const float *p = in + (long)(y - r) * W + x;
+    for (int m = 0; m < t.w; ++m) acc += p[(long)m * W] * t.k[m];
+  }
+  out[i] = acc;
+}
+
+__global__ __launch_bounds__(kBlock) void k_subsample(const float *__restrict__ in, int W, int ss,
+                                                      float *__restrict__ out, int W1, int H1) {
+  const long i = (long)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= (long)W1 * H1) return;
+  const int y = (int)(i / W1), x = (int)(i - (long)y * W1);
+  out[i] = in[(long)(ss * y + ss / 2) * W + (ss * x + ss / 2)];
+}
+
+// ---------------------------------------------------------------------------
+// Trackability map (selectGoodFeatures.c:396-423): one thread per grid point,
+// window sums in row-major order, _minEigenvalue with a double sqrt, then
+// the x86-64 float->int conversion the reference binary performs.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int x86_ftoi(float v) {
+  // cvttss2si: NaN / out of range -> INT_MIN
+  if (!(v > -2147483904.0f && v < 2147483648.0f)) return (int)0x80000000u;
+  return (int)v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_min_eigen(const float *__restrict__ gx,
+                                                      const float *__restrict__ gy, int W, int bx,
+                                                      int by, int step, int nx, int ny, int hw, int hh,
+                                                      int *__restrict__ out) {
+  const long i = (long)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= (long)nx * ny) return;
+  const int iy = (int)(i / nx), ix = (int)(i - (long)iy * nx);
+  const int x = bx + ix * step, y = by + iy * step;
+  float sxx = 0.0f, sxy = 0.0f, syy = 0.0f;
+  for (int v = y - hh; v <= y + hh; ++v) {
+    const float *px = gx + (long)v * W;
+    const float *py = gy + (long)v * W;
+    for (int u = x - hw; u <= x + hw; ++u) {
+      const float a = px[u], b = py[u];
+      sxx += a * a;
+      sxy += a * b;
+      syy += b * b;
+    }
+  }
+  // (float)((gxx + gyy - sqrt((gxx-gyy)^2 + 4*gxy*gxy)) / 2.0f), :289-292
+  const float disc = (sxx - syy) * (sxx - syy) + 4.0f * sxy * sxy;
+  float val = (float)(((double)(sxx + syy) - sqrt((double)disc)) / 2.0);
+  if (val > 2147483648.0f) val = 2147483648.0f;  // (float)limit, :415-420
+  out[i] = x86_ftoi(val);
+}
+
+// ---------------------------------------------------------------------------
+// Lucas-Kanade: one wave64 per feature.  Lane l owns window pixels
+// l, l+64, ... (row-major index p = (j+hh)*ww + (i+hw)); interpolation runs in
+// parallel, the window sums are then accumulated in the reference's order by
+// lanes 0..NS-1 (one sum each) from an LDS staging area.
+// ---------------------------------------------------------------------------
+struct TrkLevel {
+  const float *img, *gx, *gy;
+  int w, h;
+};
+
+struct TrkArgs {
+  TrkLevel A[KLT_HIP_MAX_LEVELS];  // previous image (img1)
+  TrkLevel B[KLT_HIP_MAX_LEVELS];  // current image (img2)
+  int nlev;
+  float ss;
+  int ww, wh, max_it;
+  float min_det, min_disp, max_res, step;
+  int borderx, bordery, ncols, nrows;
+  int li;
+};
+
+// _interpolate (trackFeatures.c:31-57); the clamp only guards addresses that
+// the window bounds test already excludes
+__device__ __forceinline__ float bilerp(const float *__restrict__ img, int w, int h, float x, float y) {
+  int xt = (int)x, yt = (int)y;
+  const float ax = x - xt, ay = y - yt;
+  xt = clampi(xt, 0, w - 2);
+  yt = clampi(yt, 0, h - 2);
+  const float *p = img + (long)yt * w + xt;
+  return (1.0f - ax) * (1.0f - ay) * p[0] + ax * (1.0f - ay) * p[1] + (1.0f - ax) * ay * p[w] +
+         ax * ay * p[w + 1];
+}
+
+__device__ __forceinline__ bool window_out(float x, float y, int hw, int hh, int nc, int nr) {
+  const float e = 1.001f;
+  if (!(isfinite(x) && isfinite(y))) return true;  // reference would fault; treat as OOB
+  return x - hw < 0.0f || nc - (x + hw) < e || y - hh < 0.0f || nr - (y + hh) < e;
+}
+
+__device__ __forceinline__ void lds_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ float bcast(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+// NS sequential sums over npx pixels; v[s][k] is lane's pixel lane+64k.
+// LDS layout red[p*NS + s] keeps lanes 0..NS-1 on distinct banks.
+template <int NS, int PPL>
+__device__ __forceinline__ void exact_sums(const float (&v)[NS][PPL], float *red, int npx, int lane,
+                                           float (&out)[NS]) {
+#pragma unroll
+  for (int k = 0; k < PPL; ++k) {
+    const int p = lane + kWave * k;
+    if (p < npx) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) red[p * NS + s] = v[s][k];
+    }
+  }
+  lds_wave_sync();
+  float acc = 0.0f;
+  if (lane < NS) {
+    const float *r = red + lane;
+    for (int q = 0; q < npx; ++q) acc += r[q * NS];
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) out[s] = bcast(acc, s);
+  lds_wave_sync();
+}
+
+// fast mode: butterfly over the wave (not the reference's order)
+template <int NS, int PPL>
+__device__ __forceinline__ void tree_sums(const float (&v)[NS][PPL], int npx, int lane, float (&out)[NS]) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < PPL; ++k)
+      if (lane + kWave * k < npx) acc += v[s][k];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
+    out[s] = acc;
+  }
+}
+
+template <int PPL, bool EXACT>
+__device__ int track_level(const TrkArgs &a, const TrkLevel &A, const TrkLevel &B, float x1, float y1,
+                           float &x2, float &y2, int lane, float *red) {
+  const int ww = a.ww, wh = a.wh, npx = ww * wh, hw = ww / 2, hh = wh / 2;
+  const int nc = A.w, nr = A.h;
+  int oi[PPL], oj[PPL];
+  bool on[PPL];
+#pragma unroll
+  for (int k = 0; k < PPL; ++k) {
+    const int p = lane + kWave * k;
+    on[k] = p < npx;
+    const int jj = p / ww;
+    oi[k] = p - jj * ww - hw;
+    oj[k] = jj - hh;
+  }
+
+  // img1 samples do not move during the iterations: interpolate once
+  float a_im[PPL], a_gx[PPL], a_gy[PPL];
+  const bool x1_out = window_out(x1, y1, hw, hh, nc, nr);
+  if (!x1_out) {
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+      const float xs = x1 + oi[k], ys = y1 + oj[k];
+      a_im[k] = on[k] ? bilerp(A.img, nc, nr, xs, ys) : 0.0f;
+      a_gx[k] = on[k] ? bilerp(A.gx, nc, nr, xs, ys) : 0.0f;
+      a_gy[k] = on[k] ? bilerp(A.gy, nc, nr, xs, ys) : 0.0f;
+    }
+  }
+
+  float dx = 0.0f, dy = 0.0f;
+  int it = 0, status = kTracked;
+  do {
+    if (x1_out || window_out(x2, y2, hw, hh, nc, nr)) {
+      status = kOOB;
+      break;
+    }
+    float b_im[PPL], gxs[PPL], gys[PPL], dif[PPL];
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+      const float xs = x2 + oi[k], ys = y2 + oj[k];
+      b_im[k] = on[k] ? bilerp(B.img, nc, nr, xs, ys) : 0.0f;
+      const float bgx = on[k] ? bilerp(B.gx, nc, nr, xs, ys) : 0.0f;
+      const float bgy = on[k] ? bilerp(B.gy, nc, nr, xs, ys) : 0.0f;
+      gxs[k] = a_gx[k] + bgx;
+      gys[k] = a_gy[k] + bgy;
+      dif[k] = a_im[k] - b_im[k];
+    }
+    if (a.li) {
+      // gain/bias normalisation (trackFeatures.c:133-220)
+      float mom[4][PPL], S[4];
+#pragma unroll
+      for (int k = 0; k < PPL; ++k) {
+        mom[0][k] = a_im[k];
+        mom[1][k] = b_im[k];
+        mom[2][k] = a_im[k] * a_im[k];
+        mom[3][k] = b_im[k] * b_im[k];
+      }
+      if (EXACT) exact_sums<4, PPL>(mom, red, npx, lane, S);
+      else tree_sums<4, PPL>(mom, npx, lane, S);
+      const float n = (float)(ww * wh);
+      const float alpha = (float)sqrt((double)((S[2] / n) / (S[3] / n)));
+      const float beta = S[0] / n - alpha * (S[1] / n);
+      const float alpha_g = (float)sqrt((double)((S[0] / n) / (S[1] / n)));
+#pragma unroll
+      for (int k = 0; k < PPL; ++k) {
+        dif[k] = a_im[k] - b_im[k] * alpha - beta;
+        const float xs = x2 + oi[k], ys = y2 + oj[k];
+        const float bgx = on[k] ? bilerp(B.gx, nc, nr, xs, ys) : 0.0f;
+        const float bgy = on[k] ? bilerp(B.gy, nc, nr, xs, ys) : 0.0f;
+        gxs[k] = a_gx[k] + bgx * alpha_g;
+        gys[k] = a_gy[k] + bgy * alpha_g;
+      }
+    }
+    float prod[5][PPL], S[5];
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+      prod[0][k] = gxs[k] * gxs[k];
+      prod[1][k] = gxs[k] * gys[k];
+      prod[2][k] = gys[k] * gys[k];
+      prod[3][k] = dif[k] * gxs[k];
+      prod[4][k] = dif[k] * gys[k];
+    }
+    if (EXACT) exact_sums<5, PPL>(prod, red, npx, lane, S);
+    else tree_sums<5, PPL>(prod, npx, lane, S);
+    const float gxx = S[0], gxy = S[1], gyy = S[2];
+    const float ex = S[3] * a.step, ey = S[4] * a.step;
+    // _solveEquation (:293-307)
+    const float det = gxx * gyy - gxy * gxy;
+    if (det < a.min_det) {
+      status = kSmallDet;
+      break;
+    }
+    dx = (gyy * ex - gxy * ey) / det;
+    dy = (gxx * ey - gxy * ex) / det;
+    status = kTracked;
+    x2 += dx;
+    y2 += dy;
+    ++it;
+  } while ((fabsf(dx) >= a.min_disp || fabsf(dy) >= a.min_disp) && it < a.max_it);
+
+  if (window_out(x2, y2, hw, hh, nc, nr)) status = kOOB;
+
+  if (status == kTracked) {
+    // residue: mean |img1 - img2| over the window at the final position (:465-474)
+    float dif[1][PPL], S[1];
+    float alpha = 1.0f, beta = 0.0f;
+    float b_im[PPL];
+#pragma unroll
+    for (int k = 0; k < PPL; ++k)
+      b_im[k] = on[k] ? bilerp(B.img, nc, nr, x2 + oi[k], y2 + oj[k]) : 0.0f;
+    if (a.li) {
+      float mom[4][PPL], M[4];
+#pragma unroll
+      for (int k = 0; k < PPL; ++k) {
+        mom[0][k] = a_im[k];
+        mom[1][k] = b_im[k];
+        mom[2][k] = a_im[k] * a_im[k];
+        mom[3][k] = b_im[k] * b_im[k];
+      }
+      if (EXACT) exact_sums<4, PPL>(mom, red, npx, lane, M);
+      else tree_sums<4, PPL>(mom, npx, lane, M);
+      const float n = (float)(ww * wh);
+      alpha = (float)sqrt((double)((M[2] / n) / (M[3] / n)));
+      beta = M[0] / n - alpha * (M[1] / n);
+    }
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+      const float d = a.li ? (a_im[k] - b_im[k] * alpha - beta) : (a_im[k] - b_im[k]);
+      dif[0][k] = fabsf(d);
+    }
+    if (EXACT) exact_sums<1, PPL>(dif, red, npx, lane, S);
+    else tree_sums<1, PPL>(dif, npx, lane, S);
+    if (S[0] / (float)(ww * wh) > a.max_res) status = kLargeResidue;
+  }
+  if (status == kSmallDet) return kSmallDet;
+  if (status == kOOB) return kOOB;
+  if (status == kLargeResidue) return kLargeResidue;
+  if (it >= a.max_it) return kMaxIter;
+  return kTracked;
+}
+
+template <int PPL, bool EXACT>
+__global__ __launch_bounds__(kBlock) void k_track(TrkArgs a, float *__restrict__ fx,
+                                                  float *__restrict__ fy, int *__restrict__ fv, int n) {
+  __shared__ float red_all[kBlock / kWave][5 * kWave * PPL];
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int f = blockIdx.x * (kBlock / kWave) + wave;
+  if (f >= n) return;  // whole wave; the kernel has no workgroup barrier
+  const int v0 = fv[f];
+  if (v0 < 0) return;  // lost features are not tracked (:1346)
+  float *red = red_all[wave];
+
+  // KLTTrackFeatures coarse-to-fine driver (:1348-1380)
+  float xl = fx[f], yl = fy[f];
+  for (int r = a.nlev - 1; r >= 0; --r) {
+    xl /= a.ss;
+    yl /= a.ss;
+  }
+  float xo = xl, yo = yl;
+  int val = kTracked;
+  for (int r = a.nlev - 1; r >= 0; --r) {
+    xl *= a.ss;
+    yl *= a.ss;
+    xo *= a.ss;
+    yo *= a.ss;
+    val = track_level<PPL, EXACT>(a, a.A[r], a.B[r], xl, yl, xo, yo, lane, red);
+    if (val == kSmallDet || val == kOOB) break;
+  }
+  if (lane == 0) {
+    // status mapping (:1383-1437) with _outOfBounds (:491-501)
+    const bool border = xo < a.borderx || xo > a.ncols - 1 - a.borderx || yo < a.bordery ||
+                        yo > a.nrows - 1 - a.bordery;
+    if (val == kOOB || border) {
+      fx[f] = -1.0f;
+      fy[f] = -1.0f;
+      fv[f] = kOOB;
+    } else if (val != kTracked) {
+      fx[f] = -1.0f;
+      fy[f] = -1.0f;
+      fv[f] = val;
+    } else {
+      fx[f] = xo;
+      fy[f] = yo;
+      fv[f] = kTracked;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// synthetic frames (include/klt_synth.h), one thread per pixel
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_synth(unsigned long long seed, int t0, int W, int H,
+                                                  uint8_t *__restrict__ out, long pitch, long fstride) {
+  const long i = (long)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= (long)W * H) return;
+  const int y = (int)(i / W), x = (int)(i - (long)y * W);
+  const int t = t0 + blockIdx.y;
+  out[(long)blockIdx.y * fstride + (long)y * pitch + x] = klt_synth_pixel(seed, t, x, y);
+}
+
+__global__ void k_selftest_sqrt(const double *in, double *out, int n) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) out[i] = sqrt(in[i]);
+}
+
+__global__ void k_selftest_div(const float *a, const float *b, float *out, int n) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) out[i] = a[i] / b[i];
+}
+
+// default configuration of the fused path: sigma 0.7 / 1.0 / 3.6, subsampling 4
+constexpr int kRS = 2, kRG = 3, kRP = 10, kSS = 4;
+constexpr int kL0TW = 64, kL0TH = 32;
+constexpr int kL1TW = 64, kL1TH = 16;
+
+}  // namespace
+
+// ===========================================================================
+// host side
+// ===========================================================================
+struct Level {
+  int w = 0, h = 0;
+  float *img = nullptr, *gx = nullptr, *gy = nullptr;
+  size_t cap = 0;  // floats per plane
+};
+
+struct Slot {
+  int nlev = 0;
+  int ss = 1;
+  int fused = -1;
+  Level lv[KLT_HIP_MAX_LEVELS];
+};
+
+enum TimerClass { T_L0 = 0, T_L1, T_TRACK, T_EIG, T_GEN, T_N };
+
+struct klt_hip_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  Slot slot[KLT_HIP_MAX_SLOTS];
+  uint8_t *d_u8[2] = {nullptr, nullptr};
+  uint8_t *h_u8[2] = {nullptr, nullptr};
+  hipEvent_t u8_done[2] = {nullptr, nullptr};
+  size_t u8_cap = 0;
+  int u8_w[2] = {0, 0}, u8_h[2] = {0, 0};
+  float *d_hs = nullptr;
+  size_t hs_cap = 0;
+  float *d_tmp[2] = {nullptr, nullptr};
+  size_t tmp_cap[2] = {0, 0};
+  float *d_fx = nullptr, *d_fy = nullptr;
+  int *d_fv = nullptr;
+  size_t f_cap = 0;
+  int *d_eig = nullptr;
+  size_t eig_cap = 0;
+  std::string err;
+  int force_generic = 0;
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_used[T_N];
+};
+
+namespace {
+
+int fail(klt_hip_ctx *c, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return -1;
+}
+
+#define HIPCHK(c, expr)                                                                \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess) return fail((c), "%s: %s", #expr, hipGetErrorString(e_));    \
+  } while (0)
+
+int use_device(klt_hip_ctx *c) {
+  HIPCHK(c, hipSetDevice(c->device));
+  return 0;
+}
+
+template <class T>
+int grow(klt_hip_ctx *c, T **p, size_t *cap, size_t n) {
+  if (*cap >= n && *p) return 0;
+  if (*p) HIPCHK(c, hipFree(*p));
+  *p = nullptr;
+  HIPCHK(c, hipMalloc((void **)p, sizeof(T) * (n ? n : 1)));
+  *cap = n;
+  return 0;
+}
+
+hipEvent_t take_event(klt_hip_ctx *c) {
+  if (!c->ev_pool.empty()) {
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+struct TimedScope {
+  klt_hip_ctx *c;
+  int cls;
+  hipEvent_t a = nullptr, b = nullptr;
+  TimedScope(klt_hip_ctx *c_, int cls_) : c(c_), cls(cls_) {
+    if (!c->timing) return;
+    a = take_event(c);
+    b = take_event(c);
+    if (a) hipEventRecord(a, c->stream);
+  }
+  ~TimedScope() {
+    if (!c->timing || !a || !b) return;
+    hipEventRecord(b, c->stream);
+    c->ev_used[cls].push_back({a, b});
+  }
+};
+
+unsigned blocks_for(long n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+int check_launch(klt_hip_ctx *c, const char *what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(c, "launch %s: %s", what, hipGetErrorString(e));
+  return 0;
+}
+
+bool fused_ok(const klt_hip_pyr_desc *d) {
+  return d->smooth_input && d->smooth.width == 2 * kRS + 1 && d->grad_gauss.width == 2 * kRG + 1 &&
+         d->grad_deriv.width == 2 * kRG + 1 &&
+         (d->nlevels == 1 || (d->nlevels == 2 && d->subsampling == kSS && d->pyr.width == 2 * kRP + 1));
+}
+
+int ensure_slot(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d) {
+  Slot &S = c->slot[s];
+  int w = d->ncols, h = d->nrows;
+  S.nlev = d->nlevels;
+  S.ss = d->nlevels > 1 ? d->subsampling : 1;
+  for (int l = 0; l < d->nlevels; ++l) {
+    Level &L = S.lv[l];
+    L.w = w;
+    L.h = h;
+    size_t n = (size_t)w * h;
+    if (L.cap < n || !L.img) {
+      if (L.img) hipFree(L.img);
+      if (L.gx) hipFree(L.gx);
+      if (L.gy) hipFree(L.gy);
+      L.img = L.gx = L.gy = nullptr;
+      size_t m = n ? n : 1;
+      HIPCHK(c, hipMalloc((void **)&L.img, m * sizeof(float)));
+      HIPCHK(c, hipMalloc((void **)&L.gx, m * sizeof(float)));
+      HIPCHK(c, hipMalloc((void **)&L.gy, m * sizeof(float)));
+      L.cap = n;
+    }
+    w /= d->subsampling > 0 ? d->subsampling : 1;
+    h /= d->subsampling > 0 ? d->subsampling : 1;
+  }
+  return 0;
+}
+
+int launch_rows(klt_hip_ctx *c, const float *in, int w, int h, const RTaps &t, float *out) {
+  long n = (long)w * h;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_rows, dim3(blocks_for(n)), dim3(kBlock), 0, c->stream, in, w, h, t, out);
+  return check_launch(c, "k_rows");
+}
+
+int launch_cols(klt_hip_ctx *c, const float *in, int w, int h, const RTaps &t, float *out) {
+  long n = (long)w * h;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_cols, dim3(blocks_for(n)), dim3(kBlock), 0, c->stream, in, w, h, t, out);
+  return check_launch(c, "k_cols");
+}
+
+int build_generic(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch) {
+  Slot &S = c->slot[s];
+  const long n0 = (long)d->ncols * d->nrows;
+  if (grow(c, &c->d_tmp[0], &c->tmp_cap[0], (size_t)n0)) return -1;
+  if (grow(c, &c->d_tmp[1], &c->tmp_cap[1], (size_t)n0)) return -1;
+  TimedScope ts(c, T_GEN);
+  const RTaps sm = reverse_taps(d->smooth), py = reverse_taps(d->pyr);
+  const RTaps gg = reverse_taps(d->grad_gauss), gd = reverse_taps(d->grad_deriv);
+  Level &L0 = S.lv[0];
+  float *t0 = c->d_tmp[0], *t1 = c->d_tmp[1];
+  if (n0 > 0) {
+    if (d->smooth_input) {
+      hipLaunchKernelGGL(k_u8_to_f32, dim3(blocks_for(n0)), dim3(kBlock), 0, c->stream, src, pitch,
+                         d->ncols, d->nrows, t1);
+      if (check_launch(c, "k_u8_to_f32")) return -1;
+      if (launch_rows(c, t1, d->ncols, d->nrows, sm, t0)) return -1;
+      if (launch_cols(c, t0, d->ncols, d->nrows, sm, L0.img)) return -1;
+    } else {
+      hipLaunchKernelGGL(k_u8_to_f32, dim3(blocks_for(n0)), dim3(kBlock), 0, c->stream, src, pitch,
+                         d->ncols, d->nrows, L0.img);
+      if (check_launch(c, "k_u8_to_f32")) return -1;
+    }
+  }
+  for (int l = 1; l < d->nlevels; ++l) {
+    Level &P = S.lv[l - 1], &L = S.lv[l];
+    if ((long)P.w * P.h == 0) continue;
+    if (launch_rows(c, P.img, P.w, P.h, py, t0)) return -1;
+    if (launch_cols(c, t0, P.w, P.h, py, t1)) return -1;
+    long n = (long)L.w * L.h;
+    if (n > 0) {
+      hipLaunchKernelGGL(k_subsample, dim3(blocks_for(n)), dim3(kBlock), 0, c->stream, t1, P.w,
+                         d->subsampling, L.img, L.w, L.h);
+      if (check_launch(c, "k_subsample")) return -1;
+    }
+  }
+  for (int l = 0; l < d->nlevels; ++l) {
+    Level &L = S.lv[l];
+    if (launch_rows(c, L.img, L.w, L.h, gd, t0)) return -1;
+    if (launch_cols(c, t0, L.w, L.h, gg, L.gx)) return -1;
+    if (launch_rows(c, L.img, L.w, L.h, gg, t0)) return -1;
+    if (launch_cols(c, t0, L.w, L.h, gd, L.gy)) return -1;
+  }
+  return 0;
+}
+
+template <int RS, int RG, int RP>
+FusedTaps<RS, RG, RP> fused_taps(const klt_hip_pyr_desc *d) {
+  FusedTaps<RS, RG, RP> T;
+  const RTaps s = reverse_taps(d->smooth), g = reverse_taps(d->grad_gauss);
+  const RTaps dd = reverse_taps(d->grad_deriv), p = reverse_taps(d->pyr);
+  for (int m = 0; m < 2 * RS + 1; ++m) T.s[m] = s.k[m];
+  for (int m = 0; m < 2 * RG + 1; ++m) {
+    T.g[m] = g.k[m];
+    T.d[m] = dd.k[m];
+  }
+  for (int m = 0; m < 2 * RP + 1; ++m) T.p[m] = d->nlevels > 1 ? p.k[m] : 0.0f;
+  return T;
+}
+
+int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch) {
+  Slot &S = c->slot[s];
+  const int W = d->ncols, H = d->nrows;
+  const auto T = fused_taps<kRS, kRG, kRP>(d);
+  const bool two = d->nlevels == 2;
+  const int W1 = two ? S.lv[1].w : 0, H1 = two ? S.lv[1].h : 0;
+  if (two && grow(c, &c->d_hs, &c->hs_cap, (size_t)(W1 > 0 ? W1 : 1) * H)) return -1;
+  if ((long)W * H == 0) return 0;
+  {
+    TimedScope ts(c, T_L0);
+    dim3 grid((W + kL0TW - 1) / kL0TW, (H + kL0TH - 1) / kL0TH);
+    hipLaunchKernelGGL((k_pyr_l0<kRS, kRG, kRP, kSS, kL0TW, kL0TH>), grid, dim3(kBlock), 0, c->stream,
+                       src, pitch, W, H, T, S.lv[0].img, S.lv[0].gx, S.lv[0].gy, c->d_hs, W1,
+                       (two && W1 > 0) ? 1 : 0);
+    if (check_launch(c, "k_pyr_l0")) return -1;
+  }
+  if (two && (long)W1 * H1 > 0) {
+    TimedScope ts(c, T_L1);
+    dim3 grid((W1 + kL1TW - 1) / kL1TW, (H1 + kL1TH - 1) / kL1TH);
+    hipLaunchKernelGGL((k_pyr_l1<kRS, kRG, kRP, kSS, kL1TW, kL1TH>), grid, dim3(kBlock), 0, c->stream,
+                       c->d_hs, W1, H, H1, T, S.lv[1].img, S.lv[1].gx, S.lv[1].gy);
+    if (check_launch(c, "k_pyr_l1")) return -1;
+  }
+  return 0;
+}
+
+template <int PPL, bool EXACT>
+void launch_track(klt_hip_ctx *c, const TrkArgs &a, float *x, float *y, int *v, int n) {
+  const int per = kBlock / kWave;
+  hipLaunchKernelGGL((k_track<PPL, EXACT>), dim3((n + per - 1) / per), dim3(kBlock), 0, c->stream, a, x,
+                     y, v, n);
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+KLT_API int klt_hip_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+KLT_API klt_hip_ctx *klt_hip_ctx_create(int device) {
+  klt_hip_ctx *c = new klt_hip_ctx();
+  if (device < 0) {
+    if (hipGetDevice(&device) != hipSuccess) device = 0;
+  }
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return nullptr;
+  }
+  c->stream = c->own;
+  for (int i = 0; i < 2; ++i) hipEventCreateWithFlags(&c->u8_done[i], hipEventDisableTiming);
+  return c;
+}
+
+KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  if (c->own) hipStreamSynchronize(c->own);
+  for (auto &S : c->slot)
+    for (auto &L : S.lv) {
+      hipFree(L.img);
+      hipFree(L.gx);
+      hipFree(L.gy);
+    }
+  for (int i = 0; i < 2; ++i) {
+    hipFree(c->d_u8[i]);
+    if (c->h_u8[i]) hipHostFree(c->h_u8[i]);
+    if (c->u8_done[i]) hipEventDestroy(c->u8_done[i]);
+    hipFree(c->d_tmp[i]);
+  }
+  hipFree(c->d_hs);
+  hipFree(c->d_fx);
+  hipFree(c->d_fy);
+  hipFree(c->d_fv);
+  hipFree(c->d_eig);
+  for (auto e : c->ev_pool) hipEventDestroy(e);
+  for (auto &v : c->ev_used)
+    for (auto &p : v) {
+      hipEventDestroy(p.first);
+      hipEventDestroy(p.second);
+    }
+  if (c->own) hipStreamDestroy(c->own);
+  delete c;
+}
+
+KLT_API const char *klt_hip_last_error(klt_hip_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+KLT_API int klt_hip_set_stream(klt_hip_ctx *c, void *stream) {
+  if (!c) return -1;
+  c->stream = stream ? (hipStream_t)stream : c->own;
+  return 0;
+}
+
+KLT_API void *klt_hip_get_stream(klt_hip_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+KLT_API int klt_hip_sync(klt_hip_ctx *c) {
+  if (use_device(c)) return -1;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+KLT_API int klt_hip_upload_frame(klt_hip_ctx *c, int buf, const unsigned char *host, int ncols,
+                                 int nrows) {
+  if (buf < 0 || buf > 1 || !host || ncols < 0 || nrows < 0) return fail(c, "upload: bad arguments");
+  if (use_device(c)) return -1;
+  const size_t n = (size_t)ncols * nrows;
+  if (n > c->u8_cap) {
+    for (int i = 0; i < 2; ++i) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      hipFree(c->d_u8[i]);
+      if (c->h_u8[i]) hipHostFree(c->h_u8[i]);
+      c->d_u8[i] = nullptr;
+      c->h_u8[i] = nullptr;
+      HIPCHK(c, hipMalloc((void **)&c->d_u8[i], n));
+      HIPCHK(c, hipHostMalloc((void **)&c->h_u8[i], n, hipHostMallocDefault));
+    }
+    c->u8_cap = n;
+  }
+  // the previous copy out of this bounce buffer must have finished
+  HIPCHK(c, hipEventSynchronize(c->u8_done[buf]));
+  memcpy(c->h_u8[buf], host, n);
+  HIPCHK(c, hipMemcpyAsync(c->d_u8[buf], c->h_u8[buf], n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipEventRecord(c->u8_done[buf], c->stream));
+  c->u8_w[buf] = ncols;
+  c->u8_h[buf] = nrows;
+  return 0;
+}
+
+KLT_API int klt_hip_build_pyramid(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d,
+                                  const unsigned char *frame, long pitch, int buf) {
+  if (!c || !d) return fail(c, "build_pyramid: null argument");
+  if (s < 0 || s >= KLT_HIP_MAX_SLOTS) return fail(c, "build_pyramid: bad slot %d", s);
+  if (d->nlevels < 1 || d->nlevels > KLT_HIP_MAX_LEVELS) return fail(c, "bad nlevels %d", d->nlevels);
+  if (d->nlevels > 1 && d->subsampling < 2) return fail(c, "bad subsampling %d", d->subsampling);
+  for (const klt_hip_taps *t : {&d->smooth, &d->pyr, &d->grad_gauss, &d->grad_deriv})
+    if (t->width < 0 || t->width > KLT_HIP_MAX_TAPS || (t->width % 2) != 1)
+      if (!(t == &d->pyr && d->nlevels == 1) && !(t == &d->smooth && !d->smooth_input))
+        return fail(c, "build_pyramid: bad tap width %d", t->width);
+  if (use_device(c)) return -1;
+  const uint8_t *src = frame;
+  if (!src) {
+    if (buf < 0 || buf > 1 || !c->d_u8[buf]) return fail(c, "build_pyramid: no uploaded frame");
+    if (c->u8_w[buf] != d->ncols || c->u8_h[buf] != d->nrows)
+      return fail(c, "build_pyramid: uploaded frame is %dx%d, desc %dx%d", c->u8_w[buf], c->u8_h[buf],
+                  d->ncols, d->nrows);
+    src = c->d_u8[buf];
+    pitch = d->ncols;
+  }
+  if (pitch < d->ncols) return fail(c, "build_pyramid: pitch %ld < ncols %d", pitch, d->ncols);
+  if (ensure_slot(c, s, d)) return -1;
+  const bool fz = fused_ok(d) && !c->force_generic;
+  c->slot[s].fused = fz ? 1 : 0;
+  return fz ? build_fused(c, s, d, src, pitch) : build_generic(c, s, d, src, pitch);
+}
+
+KLT_API int klt_hip_set_path(klt_hip_ctx *c, int force_generic) {
+  if (!c) return -1;
+  c->force_generic = force_generic != 0;
+  return 0;
+}
+
+KLT_API int klt_hip_pyramid_path(klt_hip_ctx *c, int s) {
+  if (!c || s < 0 || s >= KLT_HIP_MAX_SLOTS) return -1;
+  return c->slot[s].fused;
+}
+
+KLT_API int klt_hip_level_dims(klt_hip_ctx *c, int s, int l, int *w, int *h) {
+  if (!c || s < 0 || s >= KLT_HIP_MAX_SLOTS || l < 0 || l >= c->slot[s].nlev) return fail(c, "bad slot/level");
+  *w = c->slot[s].lv[l].w;
+  *h = c->slot[s].lv[l].h;
+  return 0;
+}
+
+KLT_API const float *klt_hip_level_ptr(klt_hip_ctx *c, int s, int l, int which) {
+  if (!c || s < 0 || s >= KLT_HIP_MAX_SLOTS || l < 0 || l >= c->slot[s].nlev) return nullptr;
+  const Level &L = c->slot[s].lv[l];
+  return which == 0 ? L.img : (which == 1 ? L.gx : L.gy);
+}
+
+KLT_API int klt_hip_download_level(klt_hip_ctx *c, int s, int l, int which, float *host) {
+  const float *p = klt_hip_level_ptr(c, s, l, which);
+  if (!p) return fail(c, "download_level: bad slot/level");
+  if (use_device(c)) return -1;
+  const Level &L = c->slot[s].lv[l];
+  HIPCHK(c, hipMemcpyAsync(host, p, sizeof(float) * L.w * L.h, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+KLT_API int klt_hip_track(klt_hip_ctx *c, int s1, int s2, const klt_hip_track_desc *d, float *x, float *y,
+                          int *val, int n, int on_device) {
+  if (!c || !d) return fail(c, "track: null argument");
+  if (s1 < 0 || s1 >= KLT_HIP_MAX_SLOTS || s2 < 0 || s2 >= KLT_HIP_MAX_SLOTS) return fail(c, "track: bad slot");
+  const Slot &A = c->slot[s1], &B = c->slot[s2];
+  if (A.nlev < 1 || A.nlev != B.nlev) return fail(c, "track: slots not built / level mismatch");
+  for (int l = 0; l < A.nlev; ++l)
+    if (A.lv[l].w != B.lv[l].w || A.lv[l].h != B.lv[l].h) return fail(c, "track: slot size mismatch");
+  const int npx = d->window_width * d->window_height;
+  if (d->window_width < 1 || d->window_height < 1 || npx > 16 * kWave)
+    return fail(c, "track: window %dx%d unsupported (max %d pixels)", d->window_width, d->window_height,
+                16 * kWave);
+  if (n <= 0) return 0;
+  if (use_device(c)) return -1;
+  TrkArgs a;
+  memset(&a, 0, sizeof a);
+  for (int l = 0; l < A.nlev; ++l) {
+    a.A[l] = {A.lv[l].img, A.lv[l].gx, A.lv[l].gy, A.lv[l].w, A.lv[l].h};
+    a.B[l] = {B.lv[l].img, B.lv[l].gx, B.lv[l].gy, B.lv[l].w, B.lv[l].h};
+  }
+  a.nlev = A.nlev;
+  a.ss = (float)A.ss;
+  a.ww = d->window_width;
+  a.wh = d->window_height;
+  a.max_it = d->max_iterations;
+  a.min_det = d->min_determinant;
+  a.min_disp = d->min_displacement;
+  a.max_res = d->max_residue;
+  a.step = d->step_factor;
+  a.borderx = d->borderx;
+  a.bordery = d->bordery;
+  a.ncols = A.lv[0].w;
+  a.nrows = A.lv[0].h;
+  a.li = d->lighting_insensitive;
+
+  float *x_d = x, *y_d = y;
+  int *v_d = val;
+  if (!on_device) {
+    if ((size_t)n > c->f_cap) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      hipFree(c->d_fx);
+      hipFree(c->d_fy);
+      hipFree(c->d_fv);
+      c->d_fx = c->d_fy = nullptr;
+      c->d_fv = nullptr;
+      c->f_cap = 0;
+      HIPCHK(c, hipMalloc((void **)&c->d_fx, sizeof(float) * n));
+      HIPCHK(c, hipMalloc((void **)&c->d_fy, sizeof(float) * n));
+      HIPCHK(c, hipMalloc((void **)&c->d_fv, sizeof(int) * n));
+      c->f_cap = (size_t)n;
+    }
+    x_d = c->d_fx;
+    y_d = c->d_fy;
+    v_d = c->d_fv;
+    HIPCHK(c, hipMemcpyAsync(x_d, x, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(y_d, y, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(v_d, val, sizeof(int) * n, hipMemcpyHostToDevice, c->stream));
+  }
+  {
+    TimedScope ts(c, T_TRACK);
+    const bool exact = d->reduction == KLT_HIP_EXACT;
+    if (npx <= kWave) {
+      if (exact) launch_track<1, true>(c, a, x_d, y_d, v_d, n);
+      else launch_track<1, false>(c, a, x_d, y_d, v_d, n);
+    } else if (npx <= 4 * kWave) {
+      if (exact) launch_track<4, true>(c, a, x_d, y_d, v_d, n);
+      else launch_track<4, false>(c, a, x_d, y_d, v_d, n);
+    } else {
+      if (exact) launch_track<16, true>(c, a, x_d, y_d, v_d, n);
+      else launch_track<16, false>(c, a, x_d, y_d, v_d, n);
+    }
+    if (check_launch(c, "k_track")) return -1;
+  }
+  if (!on_device) {
+    HIPCHK(c, hipMemcpyAsync(x, x_d, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(y, y_d, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(val, v_d, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return 0;
+}
+
+KLT_API int klt_hip_track_sequence(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
+                                   const unsigned char *frames, long pitch, long stride, int t0, int nsteps,
+                                   float *x, float *y, int *val, int n, int *cur_slot) {
+  if (!c || !pd || !td || !frames || !cur_slot) return fail(c, "track_sequence: null argument");
+  for (int k = 0; k < nsteps; ++k) {
+    const int prev = *cur_slot, next = prev == 0 ? 1 : 0;
+    if (klt_hip_build_pyramid(c, next, pd, frames + (long)(t0 + k) * stride, pitch, 0)) return -1;
+    if (klt_hip_track(c, prev, next, td, x, y, val, n, 1)) return -1;
+    *cur_slot = next;
+  }
+  return 0;
+}
+
+KLT_API int klt_hip_min_eigen(klt_hip_ctx *c, int s, const klt_hip_select_desc *d, int *vals, int *nx,
+                              int *ny) {
+  if (!c || !d) return fail(c, "min_eigen: null argument");
+  if (s < 0 || s >= KLT_HIP_MAX_SLOTS || c->slot[s].nlev < 1) return fail(c, "min_eigen: bad slot");
+  const Level &L = c->slot[s].lv[0];
+  const int hw = d->window_width / 2, hh = d->window_height / 2;
+  const int step = d->nSkippedPixels + 1;
+  if (step < 1) return fail(c, "min_eigen: bad nSkippedPixels");
+  const int bx = d->borderx, by = d->bordery;
+  if (bx < hw || by < hh) return fail(c, "min_eigen: border smaller than window half size");
+  const int cx = L.w - 2 * bx, cy = L.h - 2 * by;
+  const int gx = cx > 0 ? (cx + step - 1) / step : 0;
+  const int gy = cy > 0 ? (cy + step - 1) / step : 0;
+  *nx = gx;
+  *ny = gy;
+  if (!vals) return 0;
+  const long np = (long)gx * gy;
+  if (np == 0) return 0;
+  if (use_device(c)) return -1;
+  if (grow(c, &c->d_eig, &c->eig_cap, (size_t)np)) return -1;
+  {
+    TimedScope ts(c, T_EIG);
+    hipLaunchKernelGGL(k_min_eigen, dim3(blocks_for(np)), dim3(kBlock), 0, c->stream, L.gx, L.gy, L.w, bx,
+                       by, step, gx, gy, hw, hh, c->d_eig);
+    if (check_launch(c, "k_min_eigen")) return -1;
+  }
+  HIPCHK(c, hipMemcpyAsync(vals, c->d_eig, sizeof(int) * np, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+KLT_API int klt_hip_synth_frames(klt_hip_ctx *c, unsigned long long seed, int t0, int n, int ncols, int nrows,
+                                 unsigned char *dev, long pitch, long fstride) {
+  if (!c || !dev || n < 0 || pitch < ncols) return fail(c, "synth: bad arguments");
+  if (use_device(c)) return -1;
+  const long np = (long)ncols * nrows;
+  if (np == 0 || n == 0) return 0;
+  for (int f0 = 0; f0 < n; f0 += 65535) {
+    const int cnt = (n - f0) < 65535 ? (n - f0) : 65535;
+    hipLaunchKernelGGL(k_synth, dim3(blocks_for(np), cnt), dim3(kBlock), 0, c->stream, seed, t0 + f0, ncols,
+                       nrows, dev + (long)f0 * fstride, pitch, fstride);
+    if (check_launch(c, "k_synth")) return -1;
+  }
+  return 0;
+}
+
+KLT_API void *klt_hip_malloc(klt_hip_ctx *c, size_t bytes) {
+  void *p = nullptr;
+  if (!c || use_device(c)) return nullptr;
+  if (hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) {
+    fail(c, "hipMalloc(%zu) failed", bytes);
+    return nullptr;
+  }
+  return p;
+}
+
+KLT_API void klt_hip_free(klt_hip_ctx *c, void *p) {
+  if (!c || !p) return;
+  use_device(c);
+  hipFree(p);
+}
+
+KLT_API int klt_hip_memcpy(klt_hip_ctx *c, void *dst, const void *src, size_t bytes, int kind) {
+  if (use_device(c)) return -1;
+  HIPCHK(c, hipMemcpyAsync(dst, src, bytes, (hipMemcpyKind)kind, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+KLT_API int klt_hip_set_timing(klt_hip_ctx *c, int on) {
+  if (!c) return -1;
+  c->timing = on != 0;
+  return 0;
+}
+
+KLT_API int klt_hip_get_timing(klt_hip_ctx *c, klt_hip_timing *out) {
+  if (!c || !out) return -1;
+  if (klt_hip_sync(c)) return -1;
+  double ms[T_N] = {0, 0, 0, 0, 0};
+  int cnt[T_N] = {0, 0, 0, 0, 0};
+  for (int k = 0; k < T_N; ++k) {
+    for (auto &p : c->ev_used[k]) {
+      float t = 0.0f;
+      if (hipEventElapsedTime(&t, p.first, p.second) == hipSuccess) {
+        ms[k] += t;
+        cnt[k]++;
+      }
+      c->ev_pool.push_back(p.first);
+      c->ev_pool.push_back(p.second);
+    }
+    c->ev_used[k].clear();
+  }
+  out->n_pyr_l0 = cnt[T_L0];
+  out->ms_pyr_l0 = ms[T_L0];
+  out->n_pyr_l1 = cnt[T_L1];
+  out->ms_pyr_l1 = ms[T_L1];
+  out->n_track = cnt[T_TRACK];
+  out->ms_track = ms[T_TRACK];
+  out->n_eigen = cnt[T_EIG];
+  out->ms_eigen = ms[T_EIG];
+  out->n_generic = cnt[T_GEN];
+  out->ms_generic = ms[T_GEN];
+  return 0;
+}
+
+KLT_API int klt_hip_selftest_sqrt(klt_hip_ctx *c, const double *in, double *out, int n) {
+  if (use_device(c)) return -1;
+  double *d = nullptr;
+  HIPCHK(c, hipMalloc((void **)&d, sizeof(double) * 2 * (n ? n : 1)));
+  hipMemcpy(d, in, sizeof(double) * n, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(k_selftest_sqrt, dim3(blocks_for(n)), dim3(kBlock), 0, 0, d, d + n, n);
+  hipError_t e = hipMemcpy(out, d + n, sizeof(double) * n, hipMemcpyDeviceToHost);
+  hipFree(d);
+  if (e != hipSuccess) return fail(c, "selftest_sqrt: %s", hipGetErrorString(e));
+  return 0;
+}
+
+KLT_API int klt_hip_selftest_div(klt_hip_ctx *c, const float *a, const float *b, float *out, int n) {
+  if (use_device(c)) return -1;
+  float *d = nullptr;
+  HIPCHK(c, hipMalloc((void **)&d, sizeof(float) * 3 * (n ? n : 1)));
+  hipMemcpy(d, a, sizeof(float) * n, hipMemcpyHostToDevice);
+  hipMemcpy(d + n, b, sizeof(float) * n, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(k_selftest_div, dim3(blocks_for(n)), dim3(kBlock), 0, 0, d, d + n, d + 2 * n, n);
+  hipError_t e = hipMemcpy(out, d + 2 * n, sizeof(float) * n, hipMemcpyDeviceToHost);
+  hipFree(d);
+  if (e != hipSuccess) return fail(c, "selftest_div: %s", hipGetErrorString(e));
+  return 0;
+}

@@ -1,0 +1,294 @@
+"""ctypes view of the klt.h C ABI, shared by every library that exports it.
+
+The same struct layouts and prototypes bind three libraries:
+  * klt-feature-tracker-acceleration-gpus_amd/lib/libklt_amd.so  (the product),
+  * oracle/_ref/libklt_ref.so  (the reference compiled from /root/reference),
+  * oracle/build/libklt_oracle.so is NOT klt.h -- see OracleTracker below.
+
+Layouts follow src/V3/klt.h:41-125 (x86-64: TrackingContext 136 B with
+pyramid_last at 112, FeatureRec 64 B, FeatureList 16 B, FeatureTable 16 B).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import struct
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+PKG = ROOT / "klt-feature-tracker-acceleration-gpus_amd"
+AMD_LIB = PKG / "lib" / "libklt_amd.so"
+REF_LIB = ROOT / "oracle" / "_ref" / "libklt_ref.so"
+ORACLE_LIB = ROOT / "oracle" / "build" / "libklt_oracle.so"
+GOLDEN = ROOT / "tests" / "golden"
+
+import sys as _sys
+
+_sys.path.insert(0, str(ROOT))
+import kltamd  # noqa: E402  (the product package; its abi module loads no library)
+from kltamd.abi import *  # noqa: E402,F401,F403
+from kltamd.abi import KLT_PROTOS, U8P  # noqa: E402
+
+
+def bind_klt(path: os.PathLike | str) -> C.CDLL:
+    """Load any klt.h library privately (RTLD_LOCAL) and attach the prototypes."""
+    lib = C.CDLL(str(path), mode=C.RTLD_LOCAL)
+    return kltamd.abi.bind_klt(lib)
+
+
+def u8ptr(a: np.ndarray):
+    assert a.dtype == np.uint8 and a.flags.c_contiguous
+    return a.ctypes.data_as(U8P)
+
+
+def read_pgm(path) -> np.ndarray:
+    """Binary P5 reader (pnmio.c:46-77 header rules: '#' comments, maxval line)."""
+    data = Path(path).read_bytes()
+    toks, i = [], 0
+    while len(toks) < 4:
+        while data[i:i + 1].isspace():
+            i += 1
+        if data[i:i + 1] == b"#":
+            while data[i:i + 1] != b"\n":
+                i += 1
+            continue
+        j = i
+        while not data[j:j + 1].isspace():
+            j += 1
+        toks.append(data[i:j])
+        i = j
+    assert toks[0] == b"P5", toks
+    w, h = int(toks[1]), int(toks[2])
+    i += 1  # single whitespace after maxval
+    return np.frombuffer(data[i:i + w * h], dtype=np.uint8).reshape(h, w).copy()
+
+
+def fl_to_arrays(fl) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    n = fl.contents.nFeatures
+    x = np.empty(n, np.float32)
+    y = np.empty(n, np.float32)
+    v = np.empty(n, np.int32)
+    for k in range(n):
+        f = fl.contents.feature[k].contents
+        x[k], y[k], v[k] = f.x, f.y, f.val
+    return x, y, v
+
+
+def arrays_to_fl(fl, x, y, v) -> None:
+    for k in range(fl.contents.nFeatures):
+        f = fl.contents.feature[k].contents
+        f.x, f.y, f.val = float(x[k]), float(y[k]), int(v[k])
+
+
+def ft_bytes(x: np.ndarray, y: np.ndarray, v: np.ndarray) -> bytes:
+    """KLTWriteFeatureTable binary form (writeFeatures.c:430-441): 'KLTFT1',
+    nFrames, nFeatures, then per feature per frame {f32 x, f32 y, i32 val}."""
+    nfeat, nframes = x.shape
+    rec = np.empty((nfeat, nframes), dtype=[("x", "<f4"), ("y", "<f4"), ("v", "<i4")])
+    rec["x"], rec["y"], rec["v"] = x, y, v
+    return b"KLTFT1" + struct.pack("<ii", nframes, nfeat) + rec.tobytes()
+
+
+def parse_ft(data: bytes):
+    assert data[:6] == b"KLTFT1"
+    nframes, nfeat = struct.unpack("<ii", data[6:14])
+    rec = np.frombuffer(data[14:], dtype=[("x", "<f4"), ("y", "<f4"), ("v", "<i4")])
+    rec = rec.reshape(nfeat, nframes)
+    return rec["x"].copy(), rec["y"].copy(), rec["v"].copy()
+
+
+class KLTRunner:
+    """Drives any klt.h library like src/V3/example3.c:35-80 does."""
+
+    def __init__(self, lib: C.CDLL, verbose: int = 0):
+        self.lib = lib
+        lib.KLTSetVerbosity(verbose)
+
+    def harness(self, frames, n_features: int, n_frames: int, first: np.ndarray | None = None,
+                sequential: bool = True, replace: bool = False, tc_setup=None):
+        """frames[i] = image i of the dataset.  V3 semantics (example3.c:44-76):
+        first image = frames[1] unless `first` given; loop i=1..n_frames-1 tracks
+        (img1 -> frames[i]); the list is stored into table column i-1 and column
+        n_frames-1 is never written (returned as zeros)."""
+        lib = self.lib
+        img1 = np.ascontiguousarray(frames[1] if first is None else first).copy()
+        h, w = img1.shape
+        tc = lib.KLTCreateTrackingContext()
+        fl = lib.KLTCreateFeatureList(n_features)
+        tc.contents.sequentialMode = 1 if sequential else 0
+        tc.contents.writeInternalImages = 0
+        tc.contents.affineConsistencyCheck = -1
+        if tc_setup:
+            tc_setup(tc.contents)
+        X = np.zeros((n_features, n_frames), np.float32)
+        Y = np.zeros((n_features, n_frames), np.float32)
+        V = np.zeros((n_features, n_frames), np.int32)
+        lib.KLTSelectGoodFeatures(tc, u8ptr(img1), w, h, fl)
+        X[:, 0], Y[:, 0], V[:, 0] = fl_to_arrays(fl)
+        for i in range(1, n_frames):
+            img2 = np.ascontiguousarray(frames[i])
+            lib.KLTTrackFeatures(tc, u8ptr(img1), u8ptr(img2), w, h, fl)
+            if replace:
+                lib.KLTReplaceLostFeatures(tc, u8ptr(img2), w, h, fl)
+            X[:, i - 1], Y[:, i - 1], V[:, i - 1] = fl_to_arrays(fl)
+            img1 = img2.copy()
+        lib.KLTFreeFeatureList(fl)
+        lib.KLTFreeTrackingContext(tc)
+        return X, Y, V
+
+
+# ---------------------------------------------------------------------------
+# oracle/build/libklt_oracle.so (test infrastructure restatement)
+# ---------------------------------------------------------------------------
+class OracleParams(C.Structure):
+    _fields_ = [
+        ("mindist", C.c_int), ("window_width", C.c_int), ("window_height", C.c_int),
+        ("sequentialMode", C.c_int), ("smoothBeforeSelecting", C.c_int),
+        ("lighting_insensitive", C.c_int), ("min_eigenvalue", C.c_int),
+        ("min_determinant", C.c_float), ("min_displacement", C.c_float),
+        ("max_iterations", C.c_int), ("max_residue", C.c_float), ("grad_sigma", C.c_float),
+        ("smooth_sigma_fact", C.c_float), ("pyramid_sigma_fact", C.c_float),
+        ("step_factor", C.c_float), ("nSkippedPixels", C.c_int), ("borderx", C.c_int),
+        ("bordery", C.c_int), ("nPyramidLevels", C.c_int), ("subsampling", C.c_int),
+    ]
+
+    @classmethod
+    def from_tc(cls, tc: TrackingContextRec) -> "OracleParams":
+        p = cls()
+        for name, _ in cls._fields_:
+            setattr(p, name, getattr(tc, name))
+        return p
+
+
+_FP = C.POINTER(C.c_float)
+_IP = C.POINTER(C.c_int)
+
+
+def load_oracle() -> C.CDLL:
+    lib = C.CDLL(str(ORACLE_LIB), mode=C.RTLD_LOCAL)
+    P = C.POINTER(OracleParams)
+    sig = {
+        "orc_default_params": (None, [P]),
+        "orc_change_pyramid": (None, [P, C.c_int]),
+        "orc_update_border": (None, [P]),
+        "orc_create": (C.c_void_p, [P]),
+        "orc_destroy": (None, [C.c_void_p]),
+        "orc_set_params": (None, [C.c_void_p, P]),
+        "orc_stop_sequential": (None, [C.c_void_p]),
+        "orc_select": (None, [C.c_void_p, U8P, C.c_int, C.c_int, C.c_int, _FP, _FP, _IP]),
+        "orc_replace": (None, [C.c_void_p, U8P, C.c_int, C.c_int, C.c_int, _FP, _FP, _IP]),
+        "orc_track": (None, [C.c_void_p, U8P, U8P, C.c_int, C.c_int, C.c_int, _FP, _FP, _IP]),
+        "orc_level_dims": (None, [P, C.c_int, C.c_int, _IP, _IP]),
+        "orc_frame_pyramid": (None, [P, U8P, C.c_int, C.c_int, _FP, _FP, _FP]),
+        "orc_select_images": (None, [P, U8P, C.c_int, C.c_int, _FP, _FP, _FP]),
+        "orc_eigen_points": (C.c_int, [P, _FP, _FP, C.c_int, C.c_int, _IP]),
+        "orc_quicksort": (None, [_IP, C.c_int]),
+        "orc_kernel_widths": (None, [C.c_float, _IP, _IP]),
+        "orc_taps_for_sigma": (C.c_int, [C.c_float, _FP, _IP, _FP, _IP]),
+        "orc_reset_kernel_cache": (None, []),
+        "orc_params_size": (C.c_int, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    assert lib.orc_params_size() == C.sizeof(OracleParams)
+    return lib
+
+
+def fp(a):
+    return a.ctypes.data_as(_FP)
+
+
+def ip(a):
+    return a.ctypes.data_as(_IP)
+
+
+class OracleTracker:
+    """Same call pattern as the klt.h harness, backed by the restatement."""
+
+    def __init__(self, lib: C.CDLL, params: OracleParams | None = None):
+        self.lib = lib
+        if params is None:
+            params = OracleParams()
+            lib.orc_default_params(C.byref(params))
+        self.params = params
+        self.h = lib.orc_create(C.byref(params))
+
+    def close(self):
+        if self.h:
+            self.lib.orc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def select(self, img, n):
+        h, w = img.shape
+        x = np.zeros(n, np.float32); y = np.zeros(n, np.float32); v = np.zeros(n, np.int32)
+        self.lib.orc_select(self.h, u8ptr(np.ascontiguousarray(img)), w, h, n, fp(x), fp(y), ip(v))
+        return x, y, v
+
+    def replace(self, img, x, y, v):
+        h, w = img.shape
+        self.lib.orc_replace(self.h, u8ptr(np.ascontiguousarray(img)), w, h, len(x), fp(x), fp(y), ip(v))
+
+    def track(self, img1, img2, x, y, v):
+        h, w = img1.shape
+        self.lib.orc_track(self.h, u8ptr(np.ascontiguousarray(img1)), u8ptr(np.ascontiguousarray(img2)),
+                           w, h, len(x), fp(x), fp(y), ip(v))
+
+    def harness(self, frames, n_features, n_frames, first=None, replace=False):
+        img1 = np.ascontiguousarray(frames[1] if first is None else first)
+        self.params.sequentialMode = 1
+        self.lib.orc_set_params(self.h, C.byref(self.params))
+        X = np.zeros((n_features, n_frames), np.float32)
+        Y = np.zeros((n_features, n_frames), np.float32)
+        V = np.zeros((n_features, n_frames), np.int32)
+        x, y, v = self.select(img1, n_features)
+        X[:, 0], Y[:, 0], V[:, 0] = x, y, v
+        for i in range(1, n_frames):
+            img2 = np.ascontiguousarray(frames[i])
+            self.track(img1, img2, x, y, v)
+            if replace:
+                self.replace(img2, x, y, v)
+            X[:, i - 1], Y[:, i - 1], V[:, i - 1] = x, y, v
+            img1 = img2
+        return X, Y, V
+
+    def frame_pyramid(self, img):
+        h, w = img.shape
+        n = self.params.nPyramidLevels
+        ws = (C.c_int * n)(); hs = (C.c_int * n)()
+        self.lib.orc_level_dims(C.byref(self.params), w, h, ws, hs)
+        tot = sum(ws[i] * hs[i] for i in range(n))
+        a = np.zeros(tot, np.float32); gx = np.zeros(tot, np.float32); gy = np.zeros(tot, np.float32)
+        self.lib.orc_frame_pyramid(C.byref(self.params), u8ptr(np.ascontiguousarray(img)), w, h,
+                                   fp(a), fp(gx), fp(gy))
+        out, off = [], 0
+        for i in range(n):
+            m = ws[i] * hs[i]
+            out.append(tuple(z[off:off + m].reshape(hs[i], ws[i]) for z in (a, gx, gy)))
+            off += m
+        return out
+
+    def select_images(self, img):
+        h, w = img.shape
+        a = np.zeros((h, w), np.float32); gx = np.zeros((h, w), np.float32); gy = np.zeros((h, w), np.float32)
+        self.lib.orc_select_images(C.byref(self.params), u8ptr(np.ascontiguousarray(img)), w, h,
+                                   fp(a), fp(gx), fp(gy))
+        return a, gx, gy
+
+    def eigen_points(self, gx, gy):
+        h, w = gx.shape
+        out = np.zeros(3 * w * h + 3, np.int32)
+        n = self.lib.orc_eigen_points(C.byref(self.params), fp(np.ascontiguousarray(gx)),
+                                      fp(np.ascontiguousarray(gy)), w, h, ip(out))
+        return out[:3 * n].reshape(n, 3)
+
+
+def load_dataset(name: str = "images_provided", n: int = 10):
+    d = GOLDEN / name
+    return [read_pgm(d / f"img{i}.pgm") for i in range(n)]

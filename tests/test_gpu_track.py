@@ -1,0 +1,154 @@
+"""End-to-end klt.h API on the GPU vs the reference's golden outputs and the
+CPU oracle.  Exact mode: positions and status codes bit-identical in every
+(feature, frame) cell except the never-written last column (example3.c:71)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from conftest import synth
+from kltabi import GOLDEN, KLTRunner, OracleParams, OracleTracker, ft_bytes, parse_ft
+from test_oracle import table_eq
+
+pytestmark = pytest.mark.gpu
+
+
+def test_v1_golden(gpu, frames):
+    got = KLTRunner(gpu).harness(frames, 150, 10, first=frames[0])
+    assert table_eq(got, parse_ft((GOLDEN / "v1_features2.ft").read_bytes()))
+
+
+@pytest.mark.parametrize("n", [100, 150])
+def test_config1_golden(gpu, frames, n):
+    got = KLTRunner(gpu).harness(frames, n, 10)
+    assert table_eq(got, parse_ft((GOLDEN / f"config1_{n}x10.ft").read_bytes()))
+
+
+def test_config1_replace_golden(gpu, frames):
+    got = KLTRunner(gpu).harness(frames, 150, 10, replace=True)
+    assert table_eq(got, parse_ft((GOLDEN / "seq_config1_replace_150x10.ft").read_bytes()))
+
+
+def test_synthetic_golden(gpu, syn640, syn333):
+    got = KLTRunner(gpu).harness(syn640, 1000, 12)
+    assert table_eq(got, parse_ft((GOLDEN / "seq_syn640_1000x12.ft").read_bytes()))
+    got = KLTRunner(gpu).harness(syn333, 300, 8)
+    assert table_eq(got, parse_ft((GOLDEN / "seq_syn333x251_300x8.ft").read_bytes()))
+
+
+def test_non_sequential_mode(gpu, oracle, syn640):
+    got = KLTRunner(gpu).harness(syn640, 500, 8, sequential=False)
+    want = OracleTracker(oracle).harness(syn640, 500, 8)  # same results by construction
+    assert table_eq(got, want)
+
+
+def run_both(gpu, oracle, frames, n, nframes, setup, search=None, replace=False):
+    tc = gpu.KLTCreateTrackingContext()
+    setup(tc.contents)
+    if search is not None:
+        gpu.KLTChangeTCPyramid(tc, search)
+    gpu.KLTUpdateTCBorder(tc)
+    p = OracleParams.from_tc(tc.contents)
+    t = tc.contents
+
+    def full(tt):
+        setup(tt)
+        tt.nPyramidLevels, tt.subsampling = t.nPyramidLevels, t.subsampling
+        tt.borderx, tt.bordery = t.borderx, t.bordery
+
+    got = KLTRunner(gpu).harness(frames, n, nframes, tc_setup=full, replace=replace)
+    gpu.KLTFreeTrackingContext(tc)
+    want = OracleTracker(oracle, p).harness(frames, n, nframes, replace=replace)
+    return got, want
+
+
+CASES = {
+    "win5": (lambda t: setattr(t, "window_width", 5) or setattr(t, "window_height", 5), None),
+    "win9x7": (lambda t: setattr(t, "window_width", 9), None),
+    "win15": (lambda t: setattr(t, "window_width", 15) or setattr(t, "window_height", 15), None),
+    "ss2": (lambda t: None, 6),
+    "levels3": (lambda t: None, 120),
+    "lighting": (lambda t: setattr(t, "lighting_insensitive", 1), None),
+    "step2": (lambda t: setattr(t, "step_factor", 2.0), None),
+    "maxit3": (lambda t: setattr(t, "max_iterations", 3), None),
+    "residue3": (lambda t: setattr(t, "max_residue", 3.0), None),
+}
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_nondefault_vs_oracle(gpu, oracle, syn333, name):
+    setup, search = CASES[name]
+    got, want = run_both(gpu, oracle, syn333, 200, 8, setup, search)
+    assert table_eq(got, want), name
+
+
+def test_replace_vs_oracle(gpu, oracle, syn640):
+    got, want = run_both(gpu, oracle, syn640, 300, 12, lambda t: None, replace=True)
+    assert table_eq(got, want)
+
+
+def test_hd_vs_oracle(gpu, oracle):
+    """BASELINE config 3 shape (1920x1080, 5000 features) on a few frames."""
+    fr = synth(gpu, 1080, 1920, 1080, 4)
+    got = KLTRunner(gpu).harness(fr, 5000, 4)
+    want = OracleTracker(oracle).harness(fr, 5000, 4)
+    assert table_eq(got, want)
+    assert (got[2][:, 1] == 0).sum() > 4000
+
+
+def test_device_numerics(gpu):
+    """f64 sqrt and f32 division on gfx950 are correctly rounded (numpy == IEEE)."""
+    import kltamd
+    from kltamd.device import check
+    tc = gpu.KLTCreateTrackingContext()
+    ctx = gpu.klt_amd_device_context(tc)
+    rng = np.random.default_rng(1)
+    x = np.concatenate([rng.random(200000) * 10.0 ** rng.integers(-30, 30, 200000),
+                        np.array([0.0, 1.0, 2.0, 4.0, 1e-310, 1.7e308])])
+    out = np.empty_like(x)
+    DP = C.POINTER(C.c_double)
+    check(gpu, ctx, gpu.klt_hip_selftest_sqrt(ctx, x.ctypes.data_as(DP), out.ctypes.data_as(DP), x.size), "sqrt")
+    assert np.array_equal(out, np.sqrt(x))
+    a = (rng.standard_normal(200000) * 1e3).astype(np.float32)
+    b = (rng.standard_normal(200000) * 1e-2).astype(np.float32)
+    q = np.empty_like(a)
+    FP = C.POINTER(C.c_float)
+    check(gpu, ctx, gpu.klt_hip_selftest_div(ctx, a.ctypes.data_as(FP), b.ctypes.data_as(FP),
+                                             q.ctypes.data_as(FP), a.size), "div")
+    assert np.array_equal(q.view(np.int32), (a / b).view(np.int32))
+    gpu.KLTFreeTrackingContext(tc)
+
+
+def test_device_synth_matches_host(gpu):
+    from kltamd.device import D2H, check
+    tc = gpu.KLTCreateTrackingContext()
+    ctx = gpu.klt_amd_device_context(tc)
+    w, h, n = 333, 251, 3
+    buf = gpu.klt_hip_malloc(ctx, w * h * n)
+    check(gpu, ctx, gpu.klt_hip_synth_frames(ctx, 333, 0, n, w, h, buf, w, w * h), "synth")
+    out = np.empty((n, h, w), np.uint8)
+    check(gpu, ctx, gpu.klt_hip_memcpy(ctx, out.ctypes.data, buf, out.nbytes, D2H), "d2h")
+    gpu.klt_hip_free(ctx, buf)
+    host = synth(gpu, 333, w, h, n)
+    for t in range(n):
+        assert np.array_equal(out[t], host[t])
+    gpu.KLTFreeTrackingContext(tc)
+
+
+def test_stop_sequential_and_size_change(gpu, syn640):
+    from kltabi import u8ptr
+    lib = gpu
+    tc = lib.KLTCreateTrackingContext()
+    tc.contents.sequentialMode = 1
+    fl = lib.KLTCreateFeatureList(50)
+    a, b = syn640[0], syn640[1]
+    lib.KLTSelectGoodFeatures(tc, u8ptr(a), 640, 480, fl)
+    assert not tc.contents.pyramid_last
+    lib.KLTTrackFeatures(tc, u8ptr(a), u8ptr(b), 640, 480, fl)
+    assert tc.contents.pyramid_last and tc.contents.pyramid_last_gradx
+    lib.KLTStopSequentialMode(tc)
+    assert not tc.contents.pyramid_last and tc.contents.sequentialMode == 0
+    lib.KLTFreeFeatureList(fl)
+    lib.KLTFreeTrackingContext(tc)
