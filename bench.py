@@ -1,0 +1,310 @@
+#!/usr/bin/env python3
+"""KLT hot-path benchmark (BASELINE.json: frames/sec + pyramid Gpix/s @1080p 5000 feats).
+
+One step = one frame of sequential tracking, entirely on the device:
+  build the new frame's pyramid (fused gfx950 kernels) + track every live
+  feature from the previous frame's pyramid (wave64-per-feature LK),
+the work KLTTrackFeatures does per call in sequential mode
+(trackFeatures.c:1285-1511).  Frames are synthetic (include/klt_synth.h),
+generated straight into HBM before timing; features are selected on frame 0
+with KLTSelectGoodFeatures and stay device-resident.
+
+N GPUs: one process per GPU (torchrun), each tracks its own sequence
+(BASELINE config 5: "8 independent 1080p/5000-feat sequences", seed 1080+rank);
+no data-path collective; value = total frames / max-over-ranks time.
+
+Extra keys: pyramid_gpix_s, roofline (pyramid pass, HIP events on the launch
+stream), kernels (avg us per launch), cpu_baseline (the reference compiled
+from its own sources, oracle/_ref, timed on this host), parity (GPU vs that
+reference on the CPU sample, cell by cell).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+
+METRIC = "frames/sec + pyramid Gpix/s @1080p 5000 feats, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=489)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--features", type=int, default=5000)
+    p.add_argument("--seed", type=int, default=1080)
+    p.add_argument("--cpu-frames", type=int, default=160,
+                   help="frames of the bounded CPU-baseline sample (rank 0, N=1)")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--reduction", choices=["exact", "fast"], default="exact")
+    p.add_argument("--event-timing", choices=["timed", "replay"], default="replay",
+                   help="record per-kernel HIP events inside the timed region or in a replay")
+    return p.parse_args()
+
+
+def main() -> None:
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import kltamd
+    from kltamd.device import EXACT, FAST, PyrDesc, Timing, TrackDesc, check
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    lib = kltamd.load()
+    lib.KLTSetVerbosity(0)
+    W, H, NF = args.width, args.height, args.features
+    nframes = 1 + args.warmup + args.steps
+    seed = args.seed + rank
+
+    tc = lib.KLTCreateTrackingContext()
+    tc.contents.sequentialMode = 1
+    lib.klt_amd_set_reduction(tc, EXACT if args.reduction == "exact" else FAST)
+    ctx = lib.klt_amd_device_context(tc)
+    stream = torch.cuda.current_stream(dev)
+    check(lib, ctx, lib.klt_hip_set_stream(ctx, C.c_void_p(stream.cuda_stream)), "set_stream")
+
+    # frames straight into HBM (torch owns the memory; the library only sees pointers)
+    frames = torch.empty((nframes, H, W), dtype=torch.uint8, device=dev)
+    check(lib, ctx, lib.klt_hip_synth_frames(ctx, seed, 0, nframes, W, H, C.c_void_p(frames.data_ptr()),
+                                             W, W * H), "synth")
+    torch.cuda.synchronize()
+
+    # selection on frame 0 through the public API
+    f0 = frames[0].cpu().numpy()
+    fl = lib.KLTCreateFeatureList(NF)
+    lib.KLTSelectGoodFeatures(tc, f0.ctypes.data_as(C.POINTER(C.c_ubyte)), W, H, fl)
+    sel = np.array([[fl.contents.feature[k].contents.x, fl.contents.feature[k].contents.y]
+                    for k in range(NF)], np.float32)
+    selv = np.array([fl.contents.feature[k].contents.val for k in range(NF)], np.int32)
+    lib.KLTFreeFeatureList(fl)
+    x0 = torch.from_numpy(sel[:, 0].copy()).to(dev)
+    y0 = torch.from_numpy(sel[:, 1].copy()).to(dev)
+    v0 = torch.from_numpy(selv.copy()).to(dev)
+    x, y, v = x0.clone(), y0.clone(), v0.clone()
+
+    pd, td = PyrDesc(), TrackDesc()
+    lib.klt_amd_pyr_desc(tc, W, H, tc.contents.nPyramidLevels, 1, C.byref(pd))
+    lib.klt_amd_track_desc(tc, C.byref(td))
+    fptr = frames.data_ptr()
+    slot = C.c_int(0)
+
+    def build0(t):
+        check(lib, ctx, lib.klt_hip_build_pyramid(ctx, 0, C.byref(pd), C.c_void_p(fptr + t * W * H), W, 0),
+              "build")
+        slot.value = 0
+
+    def run(t0, n):
+        check(lib, ctx, lib.klt_hip_track_sequence(ctx, C.byref(pd), C.byref(td), C.c_void_p(fptr), W, W * H,
+                                                   t0, n, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()),
+                                                   C.c_void_p(v.data_ptr()), NF, C.byref(slot)), "track_sequence")
+
+    build0(0)
+    run(1, args.warmup)
+    fused = lib.klt_hip_pyramid_path(ctx, slot.value) == 1
+    live_before = int((v >= 0).sum().item())
+    xs, ys, vs, t_start = x.clone(), y.clone(), v.clone(), 1 + args.warmup
+
+    timed_events = args.event_timing == "timed"
+    lib.klt_hip_set_timing(ctx, 1 if timed_events else 0)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(t_start, args.steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    live_after = int((v >= 0).sum().item())
+
+    tm = Timing()
+    if not timed_events:  # replay the same frames from the same state with events on
+        x.copy_(xs); y.copy_(ys); v.copy_(vs)
+        build0(t_start - 1)
+        lib.klt_hip_set_timing(ctx, 1)
+        run(t_start, args.steps)
+    check(lib, ctx, lib.klt_hip_get_timing(ctx, C.byref(tm)), "timing")
+    lib.klt_hip_set_timing(ctx, 0)
+
+    dt_max = dt
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt_max = float(t.item())
+
+    us = lambda ms, n: (1000.0 * ms / n) if n else None  # noqa: E731
+    l0 = us(tm.ms_pyr_l0, tm.n_pyr_l0)
+    l1 = us(tm.ms_pyr_l1, tm.n_pyr_l1)
+    trk = us(tm.ms_track, tm.n_track)
+    gen = us(tm.ms_generic, tm.n_generic)
+    pass_us = (l0 or 0) + (l1 or 0) if fused else gen
+    px = W * H
+    W1, H1 = W // 4, H // 4
+    pass_bytes = px * 13 + W1 * H1 * 12  # u8 in; img/gx/gy out at L0 and L1
+    l0_bytes = px * 13 + W1 * H * 4      # k_pyr_l0: u8 in, img/gx/gy + sampled row pass out
+
+    result = {
+        "metric": METRIC,
+        "value": world * args.steps / dt_max,
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1000.0 * dt_max / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": f"synthetic: include/klt_synth.h value-noise frames, (0.7,0.3) px/frame, seed {args.seed}+rank",
+        "config": {"workload": f"{W}x{H}, {NF} features, sequential KLTTrackFeatures pass per frame, "
+                               f"{nframes} frames per GPU (BASELINE config 3; config 5 at N>1)",
+                   "resolution": f"{W}x{H}", "features": NF, "frames": nframes,
+                   "parallelism": "independent sequence per GPU" if world > 1 else "single GPU",
+                   "reduction": args.reduction, "pyramid_path": "fused" if fused else "generic"},
+        "pyramid_gpix_s": (px / (pass_us * 1e-6) / 1e9) if pass_us else None,
+        "kernels_us": {"k_pyr_l0": l0, "k_pyr_l1": l1, "k_track": trk, "generic_pass": gen},
+        "live_features": {"after_warmup": live_before, "at_end": live_after},
+    }
+    if pass_us:
+        ach = pass_bytes / (pass_us * 1e-6) / 1e9
+        result["roofline"] = {
+            "kernel": "pyramid pass (k_pyr_l0 + k_pyr_l1)", "bound": "hbm", "achieved": ach,
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "traffic": None, "algorithmic_bytes_per_launch": pass_bytes,
+            "us_per_launch": pass_us,
+            "k_pyr_l0": {"achieved": (l0_bytes / (l0 * 1e-6) / 1e9) if l0 else None,
+                         "algorithmic_bytes": l0_bytes},
+            "event_timing": "timed region" if timed_events else "replay of the timed region",
+        }
+        pmc = ROOT / "profiles" / "pmc_latest.json"
+        if pmc.exists():
+            try:
+                d = json.loads(pmc.read_text())
+                if d.get("resolution") == f"{W}x{H}":
+                    result["roofline"]["traffic"] = d.get("pass_hbm_bytes_per_launch")
+                    result["roofline"]["traffic_source"] = str(pmc.relative_to(ROOT))
+            except Exception:
+                pass
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"], result["parity"] = cpu_leg(lib, frames, W, H, NF, args, tc, ctx, dev)
+
+    lib.KLTFreeTrackingContext(tc)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_leg(lib, frames, W, H, NF, args, tc, ctx, dev):
+    """Bounded sample of the same workload on the host: the reference CPU path
+    (oracle/_ref, built from /root/reference) or, if absent, the oracle port.
+    Then the GPU runs the same frames and every cell is compared."""
+    import torch
+    from kltabi import REF_LIB, KLTRunner, OracleTracker, bind_klt, load_oracle
+
+    S = min(args.cpu_frames, frames.shape[0])
+    host = [frames[t].cpu().numpy() for t in range(S)]
+    kind = "reference" if REF_LIB.exists() else "port"
+    rl = bind_klt(REF_LIB) if kind == "reference" else None
+    sel_t = time.perf_counter()
+    if rl is not None:
+        rl.KLTSetVerbosity(0)
+        rtc = rl.KLTCreateTrackingContext()
+        rtc.contents.sequentialMode = 1
+        fl = rl.KLTCreateFeatureList(NF)
+        u8 = lambda a: a.ctypes.data_as(C.POINTER(C.c_ubyte))  # noqa: E731
+        rl.KLTSelectGoodFeatures(rtc, u8(host[0]), W, H, fl)
+        sel_s = time.perf_counter() - sel_t
+        times = []
+        for t in range(1, S):
+            a = time.perf_counter()
+            rl.KLTTrackFeatures(rtc, u8(host[t - 1]), u8(host[t]), W, H, fl)
+            times.append(time.perf_counter() - a)
+        cx = np.array([fl.contents.feature[k].contents.x for k in range(NF)], np.float32)
+        cy = np.array([fl.contents.feature[k].contents.y for k in range(NF)], np.float32)
+        cv = np.array([fl.contents.feature[k].contents.val for k in range(NF)], np.int32)
+        rl.KLTFreeFeatureList(fl)
+        rl.KLTFreeTrackingContext(rtc)
+    else:
+        ot = OracleTracker(load_oracle())
+        ot.params.sequentialMode = 1
+        ot.lib.orc_set_params(ot.h, C.byref(ot.params))
+        cx, cy, cv = ot.select(host[0], NF)
+        sel_s = time.perf_counter() - sel_t
+        times = []
+        for t in range(1, S):
+            a = time.perf_counter()
+            ot.track(host[t - 1], host[t], cx, cy, cv)
+            times.append(time.perf_counter() - a)
+    steady = times[1:] if len(times) > 1 else times  # first call builds two pyramids
+    cpu_fps = len(steady) / sum(steady)
+
+    # GPU on the same frames through the public API: cell-by-cell parity
+    gx, gy, gv = gpu_sequence(lib, host, NF)
+    mism = int((gx.view(np.int32) != cx.view(np.int32)).sum() + (gy.view(np.int32) != cy.view(np.int32)).sum()
+               + (gv != cv).sum())
+    cpu = {"value": cpu_fps, "unit": "frames/s", "cores": 1, "kind": kind,
+           "sample": f"first {S} frames of the same {W}x{H} sequence, {NF} features, sequential mode; "
+                     f"{len(steady)} steady-state KLTTrackFeatures calls timed (wall clock), "
+                     f"selection {sel_s:.2f}s not included",
+           "cpu_model": cpu_model(), "nproc": os.cpu_count()}
+    par = {"frames": S, "features": NF, "mismatched_values": mism,
+           "live_at_end": int((cv >= 0).sum()), "against": kind}
+    return cpu, par
+
+
+def gpu_sequence(lib, host, NF):
+    from kltabi import fl_to_arrays
+    W = host[0].shape[1]
+    H = host[0].shape[0]
+    tc = lib.KLTCreateTrackingContext()
+    tc.contents.sequentialMode = 1
+    fl = lib.KLTCreateFeatureList(NF)
+    u8 = lambda a: a.ctypes.data_as(C.POINTER(C.c_ubyte))  # noqa: E731
+    lib.KLTSelectGoodFeatures(tc, u8(host[0]), W, H, fl)
+    for t in range(1, len(host)):
+        lib.KLTTrackFeatures(tc, u8(host[t - 1]), u8(host[t]), W, H, fl)
+    out = fl_to_arrays(fl)
+    lib.KLTFreeFeatureList(fl)
+    lib.KLTFreeTrackingContext(tc)
+    return out
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+if __name__ == "__main__":
+    main()
