@@ -265,7 +265,7 @@ def cpu_leg(lib, frames, W, H, NF, args, tc, ctx, dev):
     steady = times[1:] if len(times) > 1 else times  # first call builds two pyramids
     cpu_fps = len(steady) / sum(steady)
 
-    # GPU on the same frames through the public API: cell-by-cell parity
+    # the timed GPU path on the same frames: value-by-value parity
     gx, gy, gv = gpu_sequence(lib, host, NF)
     mism = int((gx.view(np.int32) != cx.view(np.int32)).sum() + (gy.view(np.int32) != cy.view(np.int32)).sum()
                + (gv != cv).sum())
@@ -280,18 +280,33 @@ def cpu_leg(lib, frames, W, H, NF, args, tc, ctx, dev):
 
 
 def gpu_sequence(lib, host, NF):
-    from kltabi import fl_to_arrays
-    W = host[0].shape[1]
-    H = host[0].shape[0]
+    """The timed path (klt_hip_track_sequence, frames + features in HBM) on the
+    CPU sample's frames: select on frame 0, then track frames 1..S-1."""
+    import torch
+    from kltamd.device import PyrDesc, TrackDesc, check
+    H, W = host[0].shape
     tc = lib.KLTCreateTrackingContext()
     tc.contents.sequentialMode = 1
+    ctx = lib.klt_amd_device_context(tc)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    check(lib, ctx, lib.klt_hip_set_stream(ctx, C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "stream")
     fl = lib.KLTCreateFeatureList(NF)
-    u8 = lambda a: a.ctypes.data_as(C.POINTER(C.c_ubyte))  # noqa: E731
-    lib.KLTSelectGoodFeatures(tc, u8(host[0]), W, H, fl)
-    for t in range(1, len(host)):
-        lib.KLTTrackFeatures(tc, u8(host[t - 1]), u8(host[t]), W, H, fl)
-    out = fl_to_arrays(fl)
+    lib.KLTSelectGoodFeatures(tc, host[0].ctypes.data_as(C.POINTER(C.c_ubyte)), W, H, fl)
+    x = torch.tensor([fl.contents.feature[k].contents.x for k in range(NF)], dtype=torch.float32, device=dev)
+    y = torch.tensor([fl.contents.feature[k].contents.y for k in range(NF)], dtype=torch.float32, device=dev)
+    v = torch.tensor([fl.contents.feature[k].contents.val for k in range(NF)], dtype=torch.int32, device=dev)
     lib.KLTFreeFeatureList(fl)
+    fr = torch.from_numpy(np.stack(host)).to(dev)
+    pd, td = PyrDesc(), TrackDesc()
+    lib.klt_amd_pyr_desc(tc, W, H, tc.contents.nPyramidLevels, 1, C.byref(pd))
+    lib.klt_amd_track_desc(tc, C.byref(td))
+    check(lib, ctx, lib.klt_hip_build_pyramid(ctx, 0, C.byref(pd), C.c_void_p(fr.data_ptr()), W, 0), "build")
+    slot = C.c_int(0)
+    check(lib, ctx, lib.klt_hip_track_sequence(ctx, C.byref(pd), C.byref(td), C.c_void_p(fr.data_ptr()), W, W * H,
+                                               1, len(host) - 1, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()),
+                                               C.c_void_p(v.data_ptr()), NF, C.byref(slot)), "sequence")
+    torch.cuda.synchronize()
+    out = (x.cpu().numpy(), y.cpu().numpy(), v.cpu().numpy())
     lib.KLTFreeTrackingContext(tc)
     return out
 

@@ -65,232 +65,384 @@ struct FusedTaps {
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 // ---------------------------------------------------------------------------
-// Fused level-0 kernel.  One 256-thread workgroup produces a TH x TW tile of
-//   img0 = cols_s(rows_s(float(u8)))          (_KLTComputeSmoothedImage)
-//   gx0  = cols_g(rows_d(img0)), gy0 = cols_d(rows_g(img0))  (_KLTComputeGradients)
-//   hs   = rows_p(img0) at the columns SS*X+SS/2 only (first half of the
-//          pyramid smoothing, pyramid.c:114 + :120-124), for the tile's rows.
-// Every intermediate stays in LDS; global traffic is the u8 tile (+halo) in
-// and img0/gx0/gy0/hs out.
+// Fused pyramid kernels for the default parameters (sigma 0.7 / 1.0 / 3.6,
+// subsampling 4, two levels: smoothing 5 taps, gradients 7+7, pyramid 21).
+//
+// k_pyr_l0: one 256-thread workgroup per 64x32 tile of level 0 produces
+//   img0 = cols_s(rows_s(float(u8)))                  _KLTComputeSmoothedImage
+//   gx0  = cols_g(rows_d(img0)), gy0 = cols_d(rows_g(img0))  _KLTComputeGradients
+//   hs   = rows_p(img0) at columns 4X+2 only          first half of pyramid.c:114
+// All intermediates stay in LDS.  Every thread owns 4 adjacent columns (one
+// 16-byte LDS access per row), the column passes are register-blocked over
+// rows, and each output is still summed from +0 in the reference's tap order.
 // ---------------------------------------------------------------------------
-template <int RS, int RG, int RP, int SS, int TW, int TH>
-struct L0Geom {
-  static constexpr int XP = (RG > RP - SS / 2 + 1) ? RG : (RP - SS / 2 + 1);  // img0 column halo
-  static constexpr int IW = TW + 2 * XP;  // img0 / t1 width
-  static constexpr int IH = TH + 2 * RG;  // img0 rows
-  static constexpr int UW = IW + 2 * RS;  // u8 width
-  static constexpr int UH = IH + 2 * RS;  // u8 / t1 rows
-  static constexpr int A = UH * UW + UH * IW;
-  static constexpr int B = 2 * IH * TW;
-  static constexpr int LDS = (A > B ? A : B) + IH * IW;
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4 ld4(const float *p) { return *reinterpret_cast<const f4 *>(p); }
+__device__ __forceinline__ void st4(float *p, f4 v) { *reinterpret_cast<f4 *>(p) = v; }
+
+// acc[i] += v[i + off] * k for 4 lanes, as two packed-f32 pairs
+__device__ __forceinline__ void mac4(f4 &acc, const float *v, float k) {
+  f2 lo = {v[0], v[1]}, hi = {v[2], v[3]};
+  f2 kk = {k, k};
+  f2 alo = {acc.x, acc.y}, ahi = {acc.z, acc.w};
+  alo += lo * kk;
+  ahi += hi * kk;
+  acc = f4{alo.x, alo.y, ahi.x, ahi.y};
+}
+
+struct DefTaps {
+  float s[5];   // smoothing gauss, reversed
+  float g[7];   // gradient gauss, reversed
+  float d[7];   // gradient derivative, reversed
+  float p[21];  // pyramid gauss, reversed
 };
 
-template <int RS, int RG, int RP, int SS, int TW, int TH>
-__global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ src, long spitch,
-                                                   int W, int H, FusedTaps<RS, RG, RP> T,
-                                                   float *__restrict__ img0, float *__restrict__ gx0,
-                                                   float *__restrict__ gy0, float *__restrict__ hs,
-                                                   int hsW, int do_hs) {
-  using G = L0Geom<RS, RG, RP, SS, TW, TH>;
-  constexpr int XP = G::XP, IW = G::IW, IH = G::IH, UW = G::UW, UH = G::UH;
-  __shared__ float lds[G::LDS];
-  float *u = lds;             // [UH][UW] float(u8)
-  float *t1 = lds + UH * UW;  // [UH][IW] rows_s
-  float *tx = lds;            // [IH][TW] rows_d(img0)   (reuses u/t1)
-  float *ty = lds + IH * TW;  // [IH][TW] rows_g(img0)
-  float *im = lds + (G::A > G::B ? G::A : G::B);  // [IH][IW] img0
+namespace l0 {
+constexpr int RS = 2, RG = 3, RP = 10, SS = 4, TW = 64, TH = 32;
+constexpr int UW = 96;            // staged u8 columns: global [C0-12, C0+84)
+constexpr int UH = TH + 2 * RG + 2 * RS + 2;  // 44 rows: global R0-5 ..  (2 spare for 4-row blocks)
+constexpr int PW = 84;            // t1 / img0 columns: global [C0-8, C0+76)
+constexpr int NG = PW / 4;        // 21 four-column groups
+constexpr int IH = TH + 2 * RG;   // 38 img0 rows used (global R0-3 ..)
+constexpr int IHB = 10;           // 4-row blocks of img0 computed (40 rows)
+constexpr int LDS_U = UH * UW, LDS_T = UH * PW, LDS_I = IHB * 4 * PW, LDS_X = IH * TW;
+constexpr int LDS = LDS_U + LDS_T + LDS_I;
+static_assert(2 * LDS_X <= LDS_U + LDS_T, "tx/ty reuse the u8/t1 region");
+}  // namespace l0
+
+__global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ src, long spitch, int W,
+                                                   int H, DefTaps T, int vec_u8, float *__restrict__ img0,
+                                                   float *__restrict__ gx0, float *__restrict__ gy0,
+                                                   float *__restrict__ hs, int hsW, int do_hs, int vec_out) {
+  using namespace l0;
+  __shared__ __attribute__((aligned(16))) float lds[LDS];
+  float *u = lds;                // [UH][UW]
+  float *t1 = lds + LDS_U;       // [UH][PW]
+  float *im = t1 + LDS_T;        // [IHB*4][PW]
+  float *tx = lds;               // [IH][TW]  (after u/t1 are dead)
+  float *ty = lds + LDS_X;
 
   const int C0 = blockIdx.x * TW, R0 = blockIdx.y * TH;
   const int tid = threadIdx.x;
 
-  // u8 tile + halo; clamped addresses never feed a non-zero output
-  for (int i = tid; i < UH * UW; i += kBlock) {
-    const int r = i / UW, c = i - r * UW;
-    const int gy = clampi(R0 - RG - RS + r, 0, H - 1);
-    const int gx = clampi(C0 - XP - RS + c, 0, W - 1);
-    u[i] = (float)src[(long)gy * spitch + gx];
-  }
-  __syncthreads();
-
-  // rows pass of the smoothing (zero for x < RS or x >= W-RS)
-  for (int i = tid; i < UH * IW; i += kBlock) {
-    const int r = i / IW, c = i - r * IW;
-    const int gx = C0 - XP + c;
-    float acc = 0.0f;
-    if (gx >= RS && gx < W - RS) {
-      const float *p = u + r * UW + c;
+  // A. u8 tile + halo -> float.  All of a thread's loads are issued before
+  //    the first one is consumed.  Clamped addresses only feed outputs that
+  //    the zero-border rules discard.
+  {
+    constexpr int NQ = UW / 4, NA = UH * NQ, PER = (NA + kBlock - 1) / kBlock;
+    uint32_t w[PER];
+    if (vec_u8) {
 #pragma unroll
-      for (int m = 0; m < 2 * RS + 1; ++m) acc += p[m] * T.s[m];
-    }
-    t1[i] = acc;
-  }
-  __syncthreads();
-
-  // columns pass -> img0 (zero for y < RS or y >= H-RS)
-  for (int i = tid; i < IH * IW; i += kBlock) {
-    const int r = i / IW, c = i - r * IW;
-    const int gy = R0 - RG + r;
-    float acc = 0.0f;
-    if (gy >= RS && gy < H - RS) {
-      const float *p = t1 + r * IW + c;
+      for (int k = 0; k < PER; ++k) {
+        const int i = tid + k * kBlock;
+        if (i < NA) {
+          const int r = i / NQ, q = i - r * NQ;
+          const long rowp = (long)clampi(R0 - RG - RS + r, 0, H - 1) * spitch;
+          w[k] = *reinterpret_cast<const uint32_t *>(src + rowp + clampi(C0 - 12 + 4 * q, 0, W - 4));
+        }
+      }
+    } else {
 #pragma unroll
-      for (int m = 0; m < 2 * RS + 1; ++m) acc += p[m * IW] * T.s[m];
-    }
-    im[i] = acc;
-  }
-  __syncthreads();
-
-  // img0 tile out; rows pass of both gradients (zero for x < RG or x >= W-RG)
-  for (int i = tid; i < TH * TW; i += kBlock) {
-    const int r = i / TW, c = i - r * TW;
-    const int gy = R0 + r, gx = C0 + c;
-    if (gy < H && gx < W) img0[(long)gy * W + gx] = im[(r + RG) * IW + c + XP];
-  }
-  for (int i = tid; i < IH * TW; i += kBlock) {
-    const int r = i / TW, c = i - r * TW;
-    const int gx = C0 + c;
-    float ax = 0.0f, ay = 0.0f;
-    if (gx >= RG && gx < W - RG) {
-      const float *p = im + r * IW + c + XP - RG;
-#pragma unroll
-      for (int m = 0; m < 2 * RG + 1; ++m) {
-        ax += p[m] * T.d[m];
-        ay += p[m] * T.g[m];
+      for (int k = 0; k < PER; ++k) {
+        const int i = tid + k * kBlock;
+        if (i < NA) {
+          const int r = i / NQ, q = i - r * NQ;
+          const long rowp = (long)clampi(R0 - RG - RS + r, 0, H - 1) * spitch;
+          const int x = C0 - 12 + 4 * q;
+          w[k] = (uint32_t)src[rowp + clampi(x, 0, W - 1)] | ((uint32_t)src[rowp + clampi(x + 1, 0, W - 1)] << 8) |
+                 ((uint32_t)src[rowp + clampi(x + 2, 0, W - 1)] << 16) |
+                 ((uint32_t)src[rowp + clampi(x + 3, 0, W - 1)] << 24);
+        }
       }
     }
-    tx[i] = ax;
-    ty[i] = ay;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + k * kBlock;
+      if (i < NA) {
+        const f4 v = {(float)(w[k] & 0xFF), (float)((w[k] >> 8) & 0xFF), (float)((w[k] >> 16) & 0xFF),
+                      (float)(w[k] >> 24)};
+        st4(u + 4 * i, v);  // row-major [UH][UW]: element i*4
+      }
+    }
   }
-  // pyramid rows pass at the sampled columns (reads img0 only)
+  __syncthreads();
+
+  // B. rows pass of the smoothing: t1 col idx k <-> global C0-8+k; zero unless RS <= x < W-RS
+  for (int i = tid; i < UH * NG; i += kBlock) {
+    const int r = i / NG, g = i - r * NG;
+    const float *row = u + r * UW + 4 * g;
+    float v[12];
+    *reinterpret_cast<f4 *>(v) = ld4(row);
+    *reinterpret_cast<f4 *>(v + 4) = ld4(row + 4);
+    *reinterpret_cast<f4 *>(v + 8) = ld4(row + 8);
+    f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int m = 0; m < 5; ++m) mac4(acc, v + 2 + m, T.s[m]);
+    const int x = C0 - 8 + 4 * g;
+    acc.x = (x + 0 >= RS && x + 0 < W - RS) ? acc.x : 0.0f;
+    acc.y = (x + 1 >= RS && x + 1 < W - RS) ? acc.y : 0.0f;
+    acc.z = (x + 2 >= RS && x + 2 < W - RS) ? acc.z : 0.0f;
+    acc.w = (x + 3 >= RS && x + 3 < W - RS) ? acc.w : 0.0f;
+    st4(t1 + r * PW + 4 * g, acc);
+  }
+  __syncthreads();
+
+  // C. columns pass -> img0, 4 rows x 4 columns per thread; zero unless RS <= y < H-RS
+  for (int i = tid; i < IHB * NG; i += kBlock) {
+    const int b = i / NG, g = i - b * NG;
+    const float *col = t1 + (4 * b) * PW + 4 * g;
+    f4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = ld4(col + k * PW);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int m = 0; m < 5; ++m) mac4(acc, reinterpret_cast<const float *>(&v[rr + m]), T.s[m]);
+      const int y = R0 - RG + 4 * b + rr;
+      if (!(y >= RS && y < H - RS)) acc = f4{0.0f, 0.0f, 0.0f, 0.0f};
+      st4(im + (4 * b + rr) * PW + 4 * g, acc);
+    }
+  }
+  __syncthreads();
+
+  // D1. img0 tile -> HBM
+  for (int i = tid; i < TH * (TW / 4); i += kBlock) {
+    const int r = i / (TW / 4), g = i - r * (TW / 4);
+    const int y = R0 + r, x = C0 + 4 * g;
+    if (y >= H || x >= W) continue;
+    const f4 val = ld4(im + (r + RG) * PW + 8 + 4 * g);
+    float *dst = img0 + (long)y * W + x;
+    if (vec_out && x + 3 < W) {
+      st4(dst, val);
+    } else {
+      for (int e = 0; e < 4 && x + e < W; ++e) dst[e] = val[e];
+    }
+  }
+  // D2. rows passes of both gradients; zero unless RG <= x < W-RG
+  for (int i = tid; i < IH * (TW / 4); i += kBlock) {
+    const int r = i / (TW / 4), g = i - r * (TW / 4);
+    const float *row = im + r * PW + 4 * g + 4;  // img0 idx c0+4 <-> global C0+c0-4
+    float v[12];
+    *reinterpret_cast<f4 *>(v) = ld4(row);
+    *reinterpret_cast<f4 *>(v + 4) = ld4(row + 4);
+    *reinterpret_cast<f4 *>(v + 8) = ld4(row + 8);
+    f4 ax = {0.0f, 0.0f, 0.0f, 0.0f}, ay = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int m = 0; m < 7; ++m) {
+      mac4(ax, v + 1 + m, T.d[m]);
+      mac4(ay, v + 1 + m, T.g[m]);
+    }
+    const int x = C0 + 4 * g;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (!(x + e >= RG && x + e < W - RG)) {
+        ax[e] = 0.0f;
+        ay[e] = 0.0f;
+      }
+    }
+    st4(tx + r * TW + 4 * g, ax);
+    st4(ty + r * TW + 4 * g, ay);
+  }
+  // D3. pyramid rows pass at columns 4X+2, two per thread; zero unless RP <= c < W-RP
   if (do_hs) {
-    constexpr int NX = TW / SS;
-    for (int i = tid; i < TH * NX; i += kBlock) {
-      const int r = i / NX, j = i - r * NX;
-      const int gy = R0 + r, X = C0 / SS + j;
-      const int c = SS * j + SS / 2;  // tile column
-      const int gx = C0 + c;
-      float acc = 0.0f;
-      if (gx >= RP && gx < W - RP) {
-        const float *p = im + (r + RG) * IW + c + XP - RP;
+    for (int i = tid; i < TH * (TW / 8); i += kBlock) {
+      const int r = i / (TW / 8), pq = i - r * (TW / 8);
+      const float *row = im + (r + RG) * PW + 8 * pq;  // idx 8p <-> global C0+8p-8
+      float v[28];
 #pragma unroll
-        for (int m = 0; m < 2 * RP + 1; ++m) acc += p[m] * T.p[m];
+      for (int k = 0; k < 7; ++k) *reinterpret_cast<f4 *>(v + 4 * k) = ld4(row + 4 * k);
+      f2 acc = {0.0f, 0.0f};
+#pragma unroll
+      for (int m = 0; m < 21; ++m) {
+        f2 a = {v[m], v[m + 4]};
+        f2 kk = {T.p[m], T.p[m]};
+        acc += a * kk;
       }
-      if (gy < H && X < hsW) hs[(long)gy * hsW + X] = acc;
+      const int y = R0 + r;
+      const int X = C0 / SS + 2 * pq;
+      const int c = C0 + 8 * pq + 2;
+      if (y < H) {
+        if (X < hsW) hs[(long)y * hsW + X] = (c >= RP && c < W - RP) ? acc.x : 0.0f;
+        if (X + 1 < hsW) hs[(long)y * hsW + X + 1] = (c + 4 >= RP && c + 4 < W - RP) ? acc.y : 0.0f;
+      }
     }
   }
   __syncthreads();
 
-  // columns pass of both gradients (zero for y < RG or y >= H-RG)
-  for (int i = tid; i < TH * TW; i += kBlock) {
-    const int r = i / TW, c = i - r * TW;
-    const int gy = R0 + r, gx = C0 + c;
-    float ax = 0.0f, ay = 0.0f;
-    if (gy >= RG && gy < H - RG) {
-      const float *px = tx + r * TW + c;
-      const float *py = ty + r * TW + c;
+  // E. columns passes of both gradients, 2 rows x 4 columns per thread; zero unless RG <= y < H-RG
+  for (int i = tid; i < (TH / 2) * (TW / 4); i += kBlock) {
+    const int b = i / (TW / 4), g = i - b * (TW / 4);
+    f4 vx[8], vy[8];
 #pragma unroll
-      for (int m = 0; m < 2 * RG + 1; ++m) {
-        ax += px[m * TW] * T.g[m];
-        ay += py[m * TW] * T.d[m];
-      }
+    for (int k = 0; k < 8; ++k) {
+      vx[k] = ld4(tx + (2 * b + k) * TW + 4 * g);
+      vy[k] = ld4(ty + (2 * b + k) * TW + 4 * g);
     }
-    if (gy < H && gx < W) {
-      gx0[(long)gy * W + gx] = ax;
-      gy0[(long)gy * W + gx] = ay;
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      f4 ax = {0.0f, 0.0f, 0.0f, 0.0f}, ay = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int m = 0; m < 7; ++m) {
+        mac4(ax, reinterpret_cast<const float *>(&vx[rr + m]), T.g[m]);
+        mac4(ay, reinterpret_cast<const float *>(&vy[rr + m]), T.d[m]);
+      }
+      const int y = R0 + 2 * b + rr, x = C0 + 4 * g;
+      if (y >= H || x >= W) continue;
+      if (!(y >= RG && y < H - RG)) {
+        ax = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        ay = ax;
+      }
+      float *px = gx0 + (long)y * W + x;
+      float *py = gy0 + (long)y * W + x;
+      if (vec_out && x + 3 < W) {
+        st4(px, ax);
+        st4(py, ay);
+      } else {
+        for (int e = 0; e < 4 && x + e < W; ++e) {
+          px[e] = ax[e];
+          py[e] = ay[e];
+        }
+      }
     }
   }
 }
 
 // ---------------------------------------------------------------------------
-// Fused level-1 kernel: img1 = cols_p(hs) at rows SS*Y+SS/2 (the rest of
-// pyramid.c:114-124), then its gradients.  Tile = TH x TW level-1 pixels.
+// k_pyr_l1: img1 = cols_p(hs) sampled at rows 4Y+2 (rest of pyramid.c:114-124)
+// and its gradients.  One 128-thread workgroup per 32x8 tile of level 1.
 // ---------------------------------------------------------------------------
-template <int RG, int RP, int SS, int TW, int TH>
-struct L1Geom {
-  static constexpr int JW = TW + 2 * RG, JH = TH + 2 * RG;
-  static constexpr int HR = SS * (JH - 1) + 2 * RP + 1;  // hs rows staged
-  static constexpr int A = HR * JW;
-  static constexpr int B = 2 * JH * TW;
-  static constexpr int LDS = (A > B ? A : B) + JH * JW;
-};
+namespace l1 {
+constexpr int RG = 3, RP = 10, SS = 4, TW = 32, TH = 8, NT = 128;
+constexpr int JW = 40;              // img1 / hs columns: X in [x0-4, x0+36)
+constexpr int JH = TH + 2 * RG;     // 14 img1 rows: Y in [y0-3, y0+11)
+constexpr int HR = SS * (JH - 1) + 2 * RP + 1;  // 73 hs rows: [4y0-20, 4y0+53)
+constexpr int LDS_H = HR * JW, LDS_J = JH * JW, LDS_X = JH * TW;
+constexpr int LDS = LDS_H + LDS_J;
+static_assert(2 * LDS_X <= LDS_H, "tx/ty reuse the hs region");
+}  // namespace l1
 
-template <int RS, int RG, int RP, int SS, int TW, int TH>
-__global__ __launch_bounds__(kBlock) void k_pyr_l1(const float *__restrict__ hs, int W1, int H,
-                                                   int H1, FusedTaps<RS, RG, RP> T,
-                                                   float *__restrict__ img1, float *__restrict__ gx1,
-                                                   float *__restrict__ gy1) {
-  using G = L1Geom<RG, RP, SS, TW, TH>;
-  constexpr int JW = G::JW, JH = G::JH, HR = G::HR;
-  __shared__ float lds[G::LDS];
-  float *hl = lds;           // [HR][JW]
-  float *tx = lds;           // [JH][TW] (reuses hl)
-  float *ty = lds + JH * TW;
-  float *im = lds + (G::A > G::B ? G::A : G::B);  // [JH][JW]
+__global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs, int W1, int H, int H1,
+                                                   DefTaps T, int vec, float *__restrict__ img1,
+                                                   float *__restrict__ gx1, float *__restrict__ gy1) {
+  using namespace l1;
+  __shared__ __attribute__((aligned(16))) float lds[LDS];
+  float *hl = lds;          // [HR][JW]
+  float *im = lds + LDS_H;  // [JH][JW]
+  float *tx = lds;          // [JH][TW]
+  float *ty = lds + LDS_X;
 
   const int x0 = blockIdx.x * TW, y0 = blockIdx.y * TH;
   const int tid = threadIdx.x;
-  const int hr0 = SS * (y0 - RG) + SS / 2 - RP;
 
-  for (int i = tid; i < HR * JW; i += kBlock) {
-    const int r = i / JW, c = i - r * JW;
-    const int gy = clampi(hr0 + r, 0, H - 1);
-    const int gx = clampi(x0 - RG + c, 0, W1 - 1);
-    hl[i] = hs[(long)gy * W1 + gx];
-  }
-  __syncthreads();
-
-  for (int i = tid; i < JH * JW; i += kBlock) {
-    const int r = i / JW, c = i - r * JW;
-    const int Y = y0 - RG + r, X = x0 - RG + c;
-    const int rr = SS * Y + SS / 2;
-    float acc = 0.0f;
-    if (Y >= 0 && Y < H1 && X >= 0 && X < W1 && rr >= RP && rr < H - RP) {
-      const float *p = hl + (SS * r) * JW + c;
+  {
+    constexpr int NQ = JW / 4, NA = HR * NQ, PER = (NA + NT - 1) / NT;
+    f4 v[PER];
 #pragma unroll
-      for (int m = 0; m < 2 * RP + 1; ++m) acc += p[m * JW] * T.p[m];
-    }
-    im[i] = acc;
-  }
-  __syncthreads();
-
-  for (int i = tid; i < TH * TW; i += kBlock) {
-    const int r = i / TW, c = i - r * TW;
-    const int Y = y0 + r, X = x0 + c;
-    if (Y < H1 && X < W1) img1[(long)Y * W1 + X] = im[(r + RG) * JW + c + RG];
-  }
-  for (int i = tid; i < JH * TW; i += kBlock) {
-    const int r = i / TW, c = i - r * TW;
-    const int X = x0 + c;
-    float ax = 0.0f, ay = 0.0f;
-    if (X >= RG && X < W1 - RG) {
-      const float *p = im + r * JW + c;
-#pragma unroll
-      for (int m = 0; m < 2 * RG + 1; ++m) {
-        ax += p[m] * T.d[m];
-        ay += p[m] * T.g[m];
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + k * NT;
+      if (i < NA) {
+        const int r = i / NQ, q = i - r * NQ;
+        const long rowp = (long)clampi(SS * y0 - 20 + r, 0, H - 1) * W1;
+        const int X = x0 - 4 + 4 * q;
+        if (vec) {
+          v[k] = ld4(hs + rowp + clampi(X, 0, W1 - 4));
+        } else {
+          v[k] = f4{hs[rowp + clampi(X, 0, W1 - 1)], hs[rowp + clampi(X + 1, 0, W1 - 1)],
+                    hs[rowp + clampi(X + 2, 0, W1 - 1)], hs[rowp + clampi(X + 3, 0, W1 - 1)]};
+        }
       }
     }
-    tx[i] = ax;
-    ty[i] = ay;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + k * NT;
+      if (i < NA) st4(hl + 4 * i, v[k]);
+    }
   }
   __syncthreads();
 
-  for (int i = tid; i < TH * TW; i += kBlock) {
-    const int r = i / TW, c = i - r * TW;
-    const int Y = y0 + r, X = x0 + c;
-    float ax = 0.0f, ay = 0.0f;
-    if (Y >= RG && Y < H1 - RG) {
-      const float *px = tx + r * TW + c;
-      const float *py = ty + r * TW + c;
+  // img1 row i <-> Y = y0-3+i reads hs rows 4i..4i+20; zero unless 0<=Y<H1, 0<=X<W1, RP<=4Y+2<H-RP
+  for (int i = tid; i < JH * (JW / 4); i += NT) {
+    const int r = i / (JW / 4), g = i - r * (JW / 4);
+    const float *col = hl + (SS * r) * JW + 4 * g;
+    f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-      for (int m = 0; m < 2 * RG + 1; ++m) {
-        ax += px[m * TW] * T.g[m];
-        ay += py[m * TW] * T.d[m];
+    for (int m = 0; m < 21; ++m) {
+      const f4 v = ld4(col + m * JW);
+      mac4(acc, reinterpret_cast<const float *>(&v), T.p[m]);
+    }
+    const int Y = y0 - RG + r, X = x0 - 4 + 4 * g, rr = SS * Y + SS / 2;
+    const bool rowok = Y >= 0 && Y < H1 && rr >= RP && rr < H - RP;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (!(rowok && X + e >= 0 && X + e < W1)) acc[e] = 0.0f;
+    st4(im + r * JW + 4 * g, acc);
+  }
+  __syncthreads();
+
+  for (int i = tid; i < TH * (TW / 4); i += NT) {  // img1 tile out
+    const int r = i / (TW / 4), g = i - r * (TW / 4);
+    const int Y = y0 + r, X = x0 + 4 * g;
+    if (Y >= H1 || X >= W1) continue;
+    const f4 v = ld4(im + (r + RG) * JW + 4 + 4 * g);
+    float *dst = img1 + (long)Y * W1 + X;
+    if (vec && X + 3 < W1) st4(dst, v);
+    else
+      for (int e = 0; e < 4 && X + e < W1; ++e) dst[e] = v[e];
+  }
+  for (int i = tid; i < JH * (TW / 4); i += NT) {  // gradient rows passes
+    const int r = i / (TW / 4), g = i - r * (TW / 4);
+    const float *row = im + r * JW + 4 * g;  // idx 4g <-> X = x0+4g-4
+    float v[12];
+    *reinterpret_cast<f4 *>(v) = ld4(row);
+    *reinterpret_cast<f4 *>(v + 4) = ld4(row + 4);
+    *reinterpret_cast<f4 *>(v + 8) = ld4(row + 8);
+    f4 ax = {0.0f, 0.0f, 0.0f, 0.0f}, ay = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int m = 0; m < 7; ++m) {
+      mac4(ax, v + 1 + m, T.d[m]);
+      mac4(ay, v + 1 + m, T.g[m]);
+    }
+    const int X = x0 + 4 * g;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (!(X + e >= RG && X + e < W1 - RG)) {
+        ax[e] = 0.0f;
+        ay[e] = 0.0f;
       }
     }
-    if (Y < H1 && X < W1) {
-      gx1[(long)Y * W1 + X] = ax;
-      gy1[(long)Y * W1 + X] = ay;
+    st4(tx + r * TW + 4 * g, ax);
+    st4(ty + r * TW + 4 * g, ay);
+  }
+  __syncthreads();
+
+  for (int i = tid; i < TH * (TW / 4); i += NT) {  // gradient columns passes
+    const int r = i / (TW / 4), g = i - r * (TW / 4);
+    f4 ax = {0.0f, 0.0f, 0.0f, 0.0f}, ay = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int m = 0; m < 7; ++m) {
+      const f4 a = ld4(tx + (r + m) * TW + 4 * g), b = ld4(ty + (r + m) * TW + 4 * g);
+      mac4(ax, reinterpret_cast<const float *>(&a), T.g[m]);
+      mac4(ay, reinterpret_cast<const float *>(&b), T.d[m]);
+    }
+    const int Y = y0 + r, X = x0 + 4 * g;
+    if (Y >= H1 || X >= W1) continue;
+    if (!(Y >= RG && Y < H1 - RG)) {
+      ax = f4{0.0f, 0.0f, 0.0f, 0.0f};
+      ay = ax;
+    }
+    float *px = gx1 + (long)Y * W1 + X;
+    float *py = gy1 + (long)Y * W1 + X;
+    if (vec && X + 3 < W1) {
+      st4(px, ax);
+      st4(py, ay);
+    } else {
+      for (int e = 0; e < 4 && X + e < W1; ++e) {
+        px[e] = ax[e];
+        py[e] = ay[e];
+      }
     }
   }
 }
@@ -680,8 +832,6 @@ __global__ void k_selftest_div(const float *a, const float *b, float *out, int n
 
 // default configuration of the fused path: sigma 0.7 / 1.0 / 3.6, subsampling 4
 constexpr int kRS = 2, kRG = 3, kRP = 10, kSS = 4;
-constexpr int kL0TW = 64, kL0TH = 32;
-constexpr int kL1TW = 64, kL1TH = 16;
 
 }  // namespace
 
@@ -707,6 +857,10 @@ struct klt_hip_ctx {
   int device = 0;
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
+  hipStream_t pstream = nullptr;  // pyramid stream of the pipelined sequence
+  hipEvent_t ev_built[KLT_HIP_MAX_SLOTS] = {};
+  hipEvent_t ev_free[KLT_HIP_MAX_SLOTS] = {};
+  hipEvent_t ev_start = nullptr;
   Slot slot[KLT_HIP_MAX_SLOTS];
   uint8_t *d_u8[2] = {nullptr, nullptr};
   uint8_t *h_u8[2] = {nullptr, nullptr};
@@ -773,19 +927,21 @@ hipEvent_t take_event(klt_hip_ctx *c) {
   return e;
 }
 
+// HIP events around one launch, recorded on the stream the kernel runs on
 struct TimedScope {
   klt_hip_ctx *c;
   int cls;
+  hipStream_t st;
   hipEvent_t a = nullptr, b = nullptr;
-  TimedScope(klt_hip_ctx *c_, int cls_) : c(c_), cls(cls_) {
+  TimedScope(klt_hip_ctx *c_, int cls_, hipStream_t st_) : c(c_), cls(cls_), st(st_) {
     if (!c->timing) return;
     a = take_event(c);
     b = take_event(c);
-    if (a) hipEventRecord(a, c->stream);
+    if (a) hipEventRecord(a, st);
   }
   ~TimedScope() {
     if (!c->timing || !a || !b) return;
-    hipEventRecord(b, c->stream);
+    hipEventRecord(b, st);
     c->ev_used[cls].push_back({a, b});
   }
 };
@@ -831,39 +987,40 @@ int ensure_slot(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d) {
   return 0;
 }
 
-int launch_rows(klt_hip_ctx *c, const float *in, int w, int h, const RTaps &t, float *out) {
+int launch_rows(klt_hip_ctx *c, hipStream_t st, const float *in, int w, int h, const RTaps &t, float *out) {
   long n = (long)w * h;
   if (n == 0) return 0;
-  hipLaunchKernelGGL(k_rows, dim3(blocks_for(n)), dim3(kBlock), 0, c->stream, in, w, h, t, out);
+  hipLaunchKernelGGL(k_rows, dim3(blocks_for(n)), dim3(kBlock), 0, st, in, w, h, t, out);
   return check_launch(c, "k_rows");
 }
 
-int launch_cols(klt_hip_ctx *c, const float *in, int w, int h, const RTaps &t, float *out) {
+int launch_cols(klt_hip_ctx *c, hipStream_t st, const float *in, int w, int h, const RTaps &t, float *out) {
   long n = (long)w * h;
   if (n == 0) return 0;
-  hipLaunchKernelGGL(k_cols, dim3(blocks_for(n)), dim3(kBlock), 0, c->stream, in, w, h, t, out);
+  hipLaunchKernelGGL(k_cols, dim3(blocks_for(n)), dim3(kBlock), 0, st, in, w, h, t, out);
   return check_launch(c, "k_cols");
 }
 
-int build_generic(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch) {
+int build_generic(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
+                  hipStream_t st) {
   Slot &S = c->slot[s];
   const long n0 = (long)d->ncols * d->nrows;
   if (grow(c, &c->d_tmp[0], &c->tmp_cap[0], (size_t)n0)) return -1;
   if (grow(c, &c->d_tmp[1], &c->tmp_cap[1], (size_t)n0)) return -1;
-  TimedScope ts(c, T_GEN);
+  TimedScope ts(c, T_GEN, st);
   const RTaps sm = reverse_taps(d->smooth), py = reverse_taps(d->pyr);
   const RTaps gg = reverse_taps(d->grad_gauss), gd = reverse_taps(d->grad_deriv);
   Level &L0 = S.lv[0];
   float *t0 = c->d_tmp[0], *t1 = c->d_tmp[1];
   if (n0 > 0) {
     if (d->smooth_input) {
-      hipLaunchKernelGGL(k_u8_to_f32, dim3(blocks_for(n0)), dim3(kBlock), 0, c->stream, src, pitch,
+      hipLaunchKernelGGL(k_u8_to_f32, dim3(blocks_for(n0)), dim3(kBlock), 0, st, src, pitch,
                          d->ncols, d->nrows, t1);
       if (check_launch(c, "k_u8_to_f32")) return -1;
-      if (launch_rows(c, t1, d->ncols, d->nrows, sm, t0)) return -1;
-      if (launch_cols(c, t0, d->ncols, d->nrows, sm, L0.img)) return -1;
+      if (launch_rows(c, st, t1, d->ncols, d->nrows, sm, t0)) return -1;
+      if (launch_cols(c, st, t0, d->ncols, d->nrows, sm, L0.img)) return -1;
     } else {
-      hipLaunchKernelGGL(k_u8_to_f32, dim3(blocks_for(n0)), dim3(kBlock), 0, c->stream, src, pitch,
+      hipLaunchKernelGGL(k_u8_to_f32, dim3(blocks_for(n0)), dim3(kBlock), 0, st, src, pitch,
                          d->ncols, d->nrows, L0.img);
       if (check_launch(c, "k_u8_to_f32")) return -1;
     }
@@ -871,70 +1028,71 @@ int build_generic(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_
   for (int l = 1; l < d->nlevels; ++l) {
     Level &P = S.lv[l - 1], &L = S.lv[l];
     if ((long)P.w * P.h == 0) continue;
-    if (launch_rows(c, P.img, P.w, P.h, py, t0)) return -1;
-    if (launch_cols(c, t0, P.w, P.h, py, t1)) return -1;
+    if (launch_rows(c, st, P.img, P.w, P.h, py, t0)) return -1;
+    if (launch_cols(c, st, t0, P.w, P.h, py, t1)) return -1;
     long n = (long)L.w * L.h;
     if (n > 0) {
-      hipLaunchKernelGGL(k_subsample, dim3(blocks_for(n)), dim3(kBlock), 0, c->stream, t1, P.w,
+      hipLaunchKernelGGL(k_subsample, dim3(blocks_for(n)), dim3(kBlock), 0, st, t1, P.w,
                          d->subsampling, L.img, L.w, L.h);
       if (check_launch(c, "k_subsample")) return -1;
     }
   }
   for (int l = 0; l < d->nlevels; ++l) {
     Level &L = S.lv[l];
-    if (launch_rows(c, L.img, L.w, L.h, gd, t0)) return -1;
-    if (launch_cols(c, t0, L.w, L.h, gg, L.gx)) return -1;
-    if (launch_rows(c, L.img, L.w, L.h, gg, t0)) return -1;
-    if (launch_cols(c, t0, L.w, L.h, gd, L.gy)) return -1;
+    if (launch_rows(c, st, L.img, L.w, L.h, gd, t0)) return -1;
+    if (launch_cols(c, st, t0, L.w, L.h, gg, L.gx)) return -1;
+    if (launch_rows(c, st, L.img, L.w, L.h, gg, t0)) return -1;
+    if (launch_cols(c, st, t0, L.w, L.h, gd, L.gy)) return -1;
   }
   return 0;
 }
 
-template <int RS, int RG, int RP>
-FusedTaps<RS, RG, RP> fused_taps(const klt_hip_pyr_desc *d) {
-  FusedTaps<RS, RG, RP> T;
+DefTaps default_taps(const klt_hip_pyr_desc *d) {
+  DefTaps T;
   const RTaps s = reverse_taps(d->smooth), g = reverse_taps(d->grad_gauss);
   const RTaps dd = reverse_taps(d->grad_deriv), p = reverse_taps(d->pyr);
-  for (int m = 0; m < 2 * RS + 1; ++m) T.s[m] = s.k[m];
-  for (int m = 0; m < 2 * RG + 1; ++m) {
+  for (int m = 0; m < 5; ++m) T.s[m] = s.k[m];
+  for (int m = 0; m < 7; ++m) {
     T.g[m] = g.k[m];
     T.d[m] = dd.k[m];
   }
-  for (int m = 0; m < 2 * RP + 1; ++m) T.p[m] = d->nlevels > 1 ? p.k[m] : 0.0f;
+  for (int m = 0; m < 21; ++m) T.p[m] = d->nlevels > 1 ? p.k[m] : 0.0f;
   return T;
 }
 
-int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch) {
+int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
+                hipStream_t st) {
   Slot &S = c->slot[s];
   const int W = d->ncols, H = d->nrows;
-  const auto T = fused_taps<kRS, kRG, kRP>(d);
+  const DefTaps T = default_taps(d);
   const bool two = d->nlevels == 2;
   const int W1 = two ? S.lv[1].w : 0, H1 = two ? S.lv[1].h : 0;
   if (two && grow(c, &c->d_hs, &c->hs_cap, (size_t)(W1 > 0 ? W1 : 1) * H)) return -1;
   if ((long)W * H == 0) return 0;
+  const int vec_u8 = (W % 4 == 0 && W >= 16 && pitch % 4 == 0 && ((uintptr_t)src & 3) == 0) ? 1 : 0;
+  const int vec_out = (W % 4 == 0) ? 1 : 0;
   {
-    TimedScope ts(c, T_L0);
-    dim3 grid((W + kL0TW - 1) / kL0TW, (H + kL0TH - 1) / kL0TH);
-    hipLaunchKernelGGL((k_pyr_l0<kRS, kRG, kRP, kSS, kL0TW, kL0TH>), grid, dim3(kBlock), 0, c->stream,
-                       src, pitch, W, H, T, S.lv[0].img, S.lv[0].gx, S.lv[0].gy, c->d_hs, W1,
-                       (two && W1 > 0) ? 1 : 0);
+    TimedScope ts(c, T_L0, st);
+    dim3 grid((W + l0::TW - 1) / l0::TW, (H + l0::TH - 1) / l0::TH);
+    hipLaunchKernelGGL(k_pyr_l0, grid, dim3(kBlock), 0, st, src, pitch, W, H, T, vec_u8, S.lv[0].img,
+                       S.lv[0].gx, S.lv[0].gy, c->d_hs, W1, (two && W1 > 0) ? 1 : 0, vec_out);
     if (check_launch(c, "k_pyr_l0")) return -1;
   }
   if (two && (long)W1 * H1 > 0) {
-    TimedScope ts(c, T_L1);
-    dim3 grid((W1 + kL1TW - 1) / kL1TW, (H1 + kL1TH - 1) / kL1TH);
-    hipLaunchKernelGGL((k_pyr_l1<kRS, kRG, kRP, kSS, kL1TW, kL1TH>), grid, dim3(kBlock), 0, c->stream,
-                       c->d_hs, W1, H, H1, T, S.lv[1].img, S.lv[1].gx, S.lv[1].gy);
+    TimedScope ts(c, T_L1, st);
+    const int vec = (W1 % 4 == 0 && W1 >= 8) ? 1 : 0;
+    dim3 grid((W1 + l1::TW - 1) / l1::TW, (H1 + l1::TH - 1) / l1::TH);
+    hipLaunchKernelGGL(k_pyr_l1, grid, dim3(l1::NT), 0, st, c->d_hs, W1, H, H1, T, vec, S.lv[1].img,
+                       S.lv[1].gx, S.lv[1].gy);
     if (check_launch(c, "k_pyr_l1")) return -1;
   }
   return 0;
 }
 
 template <int PPL, bool EXACT>
-void launch_track(klt_hip_ctx *c, const TrkArgs &a, float *x, float *y, int *v, int n) {
+void launch_track(hipStream_t st, const TrkArgs &a, float *x, float *y, int *v, int n) {
   const int per = kBlock / kWave;
-  hipLaunchKernelGGL((k_track<PPL, EXACT>), dim3((n + per - 1) / per), dim3(kBlock), 0, c->stream, a, x,
-                     y, v, n);
+  hipLaunchKernelGGL((k_track<PPL, EXACT>), dim3((n + per - 1) / per), dim3(kBlock), 0, st, a, x, y, v, n);
 }
 
 }  // namespace
@@ -969,6 +1127,7 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
   if (c->own) hipStreamSynchronize(c->own);
+  if (c->pstream) hipStreamSynchronize(c->pstream);
   for (auto &S : c->slot)
     for (auto &L : S.lv) {
       hipFree(L.img);
@@ -992,6 +1151,15 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
       hipEventDestroy(p.first);
       hipEventDestroy(p.second);
     }
+  if (c->pstream) {
+    hipStreamSynchronize(c->pstream);
+    hipStreamDestroy(c->pstream);
+  }
+  for (int k = 0; k < KLT_HIP_MAX_SLOTS; ++k) {
+    if (c->ev_built[k]) hipEventDestroy(c->ev_built[k]);
+    if (c->ev_free[k]) hipEventDestroy(c->ev_free[k]);
+  }
+  if (c->ev_start) hipEventDestroy(c->ev_start);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
 }
@@ -1039,8 +1207,17 @@ KLT_API int klt_hip_upload_frame(klt_hip_ctx *c, int buf, const unsigned char *h
   return 0;
 }
 
+static int build_pyramid_on(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const unsigned char *frame,
+                            long pitch, int buf, hipStream_t st);
+
 KLT_API int klt_hip_build_pyramid(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d,
                                   const unsigned char *frame, long pitch, int buf) {
+  if (!c) return fail(c, "build_pyramid: null context");
+  return build_pyramid_on(c, s, d, frame, pitch, buf, c->stream);
+}
+
+static int build_pyramid_on(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const unsigned char *frame,
+                            long pitch, int buf, hipStream_t st) {
   if (!c || !d) return fail(c, "build_pyramid: null argument");
   if (s < 0 || s >= KLT_HIP_MAX_SLOTS) return fail(c, "build_pyramid: bad slot %d", s);
   if (d->nlevels < 1 || d->nlevels > KLT_HIP_MAX_LEVELS) return fail(c, "bad nlevels %d", d->nlevels);
@@ -1063,7 +1240,7 @@ KLT_API int klt_hip_build_pyramid(klt_hip_ctx *c, int s, const klt_hip_pyr_desc 
   if (ensure_slot(c, s, d)) return -1;
   const bool fz = fused_ok(d) && !c->force_generic;
   c->slot[s].fused = fz ? 1 : 0;
-  return fz ? build_fused(c, s, d, src, pitch) : build_generic(c, s, d, src, pitch);
+  return fz ? build_fused(c, s, d, src, pitch, st) : build_generic(c, s, d, src, pitch, st);
 }
 
 KLT_API int klt_hip_set_path(klt_hip_ctx *c, int force_generic) {
@@ -1159,17 +1336,17 @@ KLT_API int klt_hip_track(klt_hip_ctx *c, int s1, int s2, const klt_hip_track_de
     HIPCHK(c, hipMemcpyAsync(v_d, val, sizeof(int) * n, hipMemcpyHostToDevice, c->stream));
   }
   {
-    TimedScope ts(c, T_TRACK);
+    TimedScope ts(c, T_TRACK, c->stream);
     const bool exact = d->reduction == KLT_HIP_EXACT;
     if (npx <= kWave) {
-      if (exact) launch_track<1, true>(c, a, x_d, y_d, v_d, n);
-      else launch_track<1, false>(c, a, x_d, y_d, v_d, n);
+      if (exact) launch_track<1, true>(c->stream, a, x_d, y_d, v_d, n);
+      else launch_track<1, false>(c->stream, a, x_d, y_d, v_d, n);
     } else if (npx <= 4 * kWave) {
-      if (exact) launch_track<4, true>(c, a, x_d, y_d, v_d, n);
-      else launch_track<4, false>(c, a, x_d, y_d, v_d, n);
+      if (exact) launch_track<4, true>(c->stream, a, x_d, y_d, v_d, n);
+      else launch_track<4, false>(c->stream, a, x_d, y_d, v_d, n);
     } else {
-      if (exact) launch_track<16, true>(c, a, x_d, y_d, v_d, n);
-      else launch_track<16, false>(c, a, x_d, y_d, v_d, n);
+      if (exact) launch_track<16, true>(c->stream, a, x_d, y_d, v_d, n);
+      else launch_track<16, false>(c->stream, a, x_d, y_d, v_d, n);
     }
     if (check_launch(c, "k_track")) return -1;
   }
@@ -1182,14 +1359,36 @@ KLT_API int klt_hip_track(klt_hip_ctx *c, int s1, int s2, const klt_hip_track_de
   return 0;
 }
 
+// Pipelined sequence: pyramids are built on a second stream one frame ahead of
+// the tracker.  Three slots rotate: frame t's pyramid goes into the slot that
+// held frame t-3, which the tracker released after tracking t-3 -> t-2.
 KLT_API int klt_hip_track_sequence(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
                                    const unsigned char *frames, long pitch, long stride, int t0, int nsteps,
                                    float *x, float *y, int *val, int n, int *cur_slot) {
   if (!c || !pd || !td || !frames || !cur_slot) return fail(c, "track_sequence: null argument");
+  if (*cur_slot < 0 || *cur_slot > 2) return fail(c, "track_sequence: cur_slot must be 0, 1 or 2");
+  if (nsteps <= 0) return 0;
+  if (use_device(c)) return -1;
+  if (!c->pstream) {
+    HIPCHK(c, hipStreamCreateWithFlags(&c->pstream, hipStreamNonBlocking));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
+    for (int k = 0; k < 3; ++k) {
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_built[k], hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_free[k], hipEventDisableTiming));
+    }
+  }
+  // the pyramid stream starts behind everything already queued on the tracking stream
+  HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
+  HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_start, 0));
+  hipStream_t track_stream = c->stream;
   for (int k = 0; k < nsteps; ++k) {
-    const int prev = *cur_slot, next = prev == 0 ? 1 : 0;
-    if (klt_hip_build_pyramid(c, next, pd, frames + (long)(t0 + k) * stride, pitch, 0)) return -1;
+    const int prev = *cur_slot, next = (prev + 1) % 3;
+    HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_free[next], 0));
+    if (build_pyramid_on(c, next, pd, frames + (long)(t0 + k) * stride, pitch, 0, c->pstream)) return -1;
+    HIPCHK(c, hipEventRecord(c->ev_built[next], c->pstream));
+    HIPCHK(c, hipStreamWaitEvent(track_stream, c->ev_built[next], 0));
     if (klt_hip_track(c, prev, next, td, x, y, val, n, 1)) return -1;
+    HIPCHK(c, hipEventRecord(c->ev_free[prev], track_stream));
     *cur_slot = next;
   }
   return 0;
@@ -1216,7 +1415,7 @@ KLT_API int klt_hip_min_eigen(klt_hip_ctx *c, int s, const klt_hip_select_desc *
   if (use_device(c)) return -1;
   if (grow(c, &c->d_eig, &c->eig_cap, (size_t)np)) return -1;
   {
-    TimedScope ts(c, T_EIG);
+    TimedScope ts(c, T_EIG, c->stream);
     hipLaunchKernelGGL(k_min_eigen, dim3(blocks_for(np)), dim3(kBlock), 0, c->stream, L.gx, L.gy, L.w, bx,
                        by, step, gx, gy, hw, hh, c->d_eig);
     if (check_launch(c, "k_min_eigen")) return -1;

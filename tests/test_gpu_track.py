@@ -152,3 +152,69 @@ def test_stop_sequential_and_size_change(gpu, syn640):
     assert not tc.contents.pyramid_last and tc.contents.sequentialMode == 0
     lib.KLTFreeFeatureList(fl)
     lib.KLTFreeTrackingContext(tc)
+
+
+def device_sequence(gpu, frames, nfeat, setup=None, reduction=0):
+    """Select on frames[0], then klt_hip_track_sequence over frames[1:] with
+    frames and features resident on the device (the path bench.py times)."""
+    from kltabi import fl_to_arrays, u8ptr
+    from kltamd.device import D2H, H2D, PyrDesc, TrackDesc, check
+    h, w = frames[0].shape
+    tc = gpu.KLTCreateTrackingContext()
+    tc.contents.sequentialMode = 1
+    if setup:
+        setup(tc.contents)
+    gpu.klt_amd_set_reduction(tc, reduction)
+    ctx = gpu.klt_amd_device_context(tc)
+    fl = gpu.KLTCreateFeatureList(nfeat)
+    gpu.KLTSelectGoodFeatures(tc, u8ptr(np.ascontiguousarray(frames[0])), w, h, fl)
+    x, y, v = fl_to_arrays(fl)
+    gpu.KLTFreeFeatureList(fl)
+    stack = np.ascontiguousarray(np.stack(frames))
+    dfr = gpu.klt_hip_malloc(ctx, stack.nbytes)
+    dx, dy, dv = (gpu.klt_hip_malloc(ctx, 4 * nfeat) for _ in range(3))
+    check(gpu, ctx, gpu.klt_hip_memcpy(ctx, dfr, stack.ctypes.data, stack.nbytes, H2D), "h2d")
+    for d, a in ((dx, x), (dy, y), (dv, v)):
+        check(gpu, ctx, gpu.klt_hip_memcpy(ctx, d, a.ctypes.data, a.nbytes, H2D), "h2d")
+    pd, td = PyrDesc(), TrackDesc()
+    gpu.klt_amd_pyr_desc(tc, w, h, tc.contents.nPyramidLevels, 1, C.byref(pd))
+    gpu.klt_amd_track_desc(tc, C.byref(td))
+    check(gpu, ctx, gpu.klt_hip_build_pyramid(ctx, 0, C.byref(pd), dfr, w, 0), "build")
+    slot = C.c_int(0)
+    check(gpu, ctx, gpu.klt_hip_track_sequence(ctx, C.byref(pd), C.byref(td), dfr, w, w * h, 1,
+                                               len(frames) - 1, dx, dy, dv, nfeat, C.byref(slot)), "seq")
+    for d, a in ((dx, x), (dy, y), (dv, v)):
+        check(gpu, ctx, gpu.klt_hip_memcpy(ctx, a.ctypes.data, d, a.nbytes, D2H), "d2h")
+    for d in (dfr, dx, dy, dv):
+        gpu.klt_hip_free(ctx, d)
+    gpu.KLTFreeTrackingContext(tc)
+    return x, y, v
+
+
+@pytest.mark.parametrize("shape,nfeat,nframes", [((480, 640), 1000, 12), ((251, 333), 300, 9),
+                                                 ((1080, 1920), 5000, 6)])
+def test_pipelined_device_sequence_vs_oracle(gpu, oracle, shape, nfeat, nframes):
+    h, w = shape
+    frames = synth(gpu, 4242 + w, w, h, nframes)
+    x, y, v = device_sequence(gpu, frames, nfeat)
+    X, Y, V = OracleTracker(oracle).harness(frames, nfeat, nframes, first=frames[0])
+    k = nframes - 2  # column of the last tracked frame
+    assert np.array_equal(x.view(np.int32), X[:, k].view(np.int32))
+    assert np.array_equal(y.view(np.int32), Y[:, k].view(np.int32))
+    assert np.array_equal(v, V[:, k])
+
+
+def test_pipelined_generic_path_vs_oracle(gpu, oracle):
+    """Non-default parameters: the pipeline drives the generic pyramid path."""
+    frames = synth(gpu, 99, 333, 251, 7)
+
+    def setup(t):
+        t.window_width = t.window_height = 9
+
+    x, y, v = device_sequence(gpu, frames, 200, setup)
+    tc = gpu.KLTCreateTrackingContext()
+    setup(tc.contents)
+    p = OracleParams.from_tc(tc.contents)
+    gpu.KLTFreeTrackingContext(tc)
+    X, Y, V = OracleTracker(oracle, p).harness(frames, 200, 7, first=frames[0])
+    assert np.array_equal(x.view(np.int32), X[:, 5].view(np.int32)) and np.array_equal(v, V[:, 5])
