@@ -1,0 +1,123 @@
+#!/usr/bin/env python3
+"""Kernel microbenchmarks (one kernel class at a time, nothing overlapping).
+
+  python tools/microbench.py pyr   --width 3840 --height 2160 --reps 200
+  python tools/microbench.py track --width 1920 --height 1080 --features 5000 --reps 200
+
+pyr:   builds pyramids of resident frames back to back on one stream.
+track: tracks the same feature set between the same two resident pyramids,
+       restoring the feature arrays before each launch.
+Prints one JSON line with per-launch averages from HIP events, and is meant to
+run under `rocprofv3 --kernel-trace --stats` or `--pmc` as well.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mode", choices=["pyr", "track"])
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--features", type=int, default=5000)
+    ap.add_argument("--reps", type=int, default=200)
+    ap.add_argument("--frames", type=int, default=8)
+    ap.add_argument("--reduction", choices=["exact", "fast"], default="exact")
+    ap.add_argument("--generic", action="store_true")
+    a = ap.parse_args()
+
+    import kltamd
+    from kltamd.device import D2D, H2D, PyrDesc, Timing, TrackDesc, check
+
+    lib = kltamd.load()
+    lib.KLTSetVerbosity(0)
+    W, H = a.width, a.height
+    tc = lib.KLTCreateTrackingContext()
+    tc.contents.sequentialMode = 1
+    lib.klt_amd_set_reduction(tc, 0 if a.reduction == "exact" else 1)
+    ctx = lib.klt_amd_device_context(tc)
+    lib.klt_hip_set_path(ctx, 1 if a.generic else 0)
+    nf = max(a.frames, 2)
+    frames = lib.klt_hip_malloc(ctx, nf * W * H)
+    check(lib, ctx, lib.klt_hip_synth_frames(ctx, 1080, 0, nf, W, H, frames, W, W * H), "synth")
+    pd, td = PyrDesc(), TrackDesc()
+    lib.klt_amd_pyr_desc(tc, W, H, tc.contents.nPyramidLevels, 1, C.byref(pd))
+    lib.klt_amd_track_desc(tc, C.byref(td))
+    out = {"mode": a.mode, "resolution": f"{W}x{H}", "reps": a.reps}
+
+    def build(slot, t):
+        check(lib, ctx, lib.klt_hip_build_pyramid(ctx, slot, C.byref(pd), C.c_void_p(frames + (t % nf) * W * H),
+                                                  W, 0), "build")
+
+    if a.mode == "pyr":
+        for t in range(10):
+            build(t % 2, t)
+        lib.klt_hip_sync(ctx)
+        lib.klt_hip_set_timing(ctx, 1)
+        t0 = time.perf_counter()
+        for t in range(a.reps):
+            build(t % 2, t)
+        lib.klt_hip_sync(ctx)
+        wall = time.perf_counter() - t0
+        tm = Timing()
+        check(lib, ctx, lib.klt_hip_get_timing(ctx, C.byref(tm)), "timing")
+        l0 = 1e3 * tm.ms_pyr_l0 / max(tm.n_pyr_l0, 1)
+        l1 = 1e3 * tm.ms_pyr_l1 / max(tm.n_pyr_l1, 1)
+        gen = 1e3 * tm.ms_generic / max(tm.n_generic, 1)
+        px = W * H
+        byts = px * 13 + (W // 4) * (H // 4) * 12
+        pass_us = gen if a.generic else l0 + l1
+        out.update({"k_pyr_l0_us": l0, "k_pyr_l1_us": l1, "generic_us": gen, "wall_us_per_frame": 1e6 * wall / a.reps,
+                    "pass_GBps": byts / (pass_us * 1e-6) / 1e9, "frac_8TBs": byts / (pass_us * 1e-6) / 8e12,
+                    "gpix_s": px / (pass_us * 1e-6) / 1e9})
+    else:
+        h0 = np.empty((H, W), np.uint8)
+        lib.klt_synth_frame(1080, 0, W, H, h0.ctypes.data)
+        fl = lib.KLTCreateFeatureList(a.features)
+        lib.KLTSelectGoodFeatures(tc, h0.ctypes.data_as(kltamd.abi.U8P), W, H, fl)
+        n = a.features
+        xs = np.array([fl.contents.feature[k].contents.x for k in range(n)], np.float32)
+        ys = np.array([fl.contents.feature[k].contents.y for k in range(n)], np.float32)
+        vs = np.array([fl.contents.feature[k].contents.val for k in range(n)], np.int32)
+        lib.KLTFreeFeatureList(fl)
+        build(0, 0)
+        build(1, 1)
+        st = [lib.klt_hip_malloc(ctx, 4 * n) for _ in range(3)]
+        wk = [lib.klt_hip_malloc(ctx, 4 * n) for _ in range(3)]
+        for d, arr in zip(st, (xs, ys, vs)):
+            check(lib, ctx, lib.klt_hip_memcpy(ctx, d, arr.ctypes.data, arr.nbytes, H2D), "h2d")
+
+        def once():
+            for d, s in zip(wk, st):
+                check(lib, ctx, lib.klt_hip_memcpy(ctx, d, s, 4 * n, D2D), "d2d")
+            check(lib, ctx, lib.klt_hip_track(ctx, 0, 1, C.byref(td), wk[0], wk[1], wk[2], n, 1), "track")
+
+        for _ in range(5):
+            once()
+        lib.klt_hip_sync(ctx)
+        lib.klt_hip_set_timing(ctx, 1)
+        for _ in range(a.reps):
+            once()
+        tm = Timing()
+        check(lib, ctx, lib.klt_hip_get_timing(ctx, C.byref(tm)), "timing")
+        vv = np.empty(n, np.int32)
+        check(lib, ctx, lib.klt_hip_memcpy(ctx, vv.ctypes.data, wk[2], 4 * n, 2), "d2h")
+        out.update({"features": n, "k_track_us": 1e3 * tm.ms_track / max(tm.n_track, 1),
+                    "status_hist": {int(k): int(c) for k, c in zip(*np.unique(vv, return_counts=True))}})
+    print(json.dumps(out), flush=True)
+    lib.KLTFreeTrackingContext(tc)
+
+
+if __name__ == "__main__":
+    main()
