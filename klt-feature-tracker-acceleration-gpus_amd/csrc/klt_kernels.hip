@@ -582,6 +582,7 @@ struct TrkArgs {
   float min_det, min_disp, max_res, step;
   int borderx, bordery, ncols, nrows;
   int li;
+  int red_pitch;     // per-sum row pitch of the reduction staging area (floats)
 };
 
 // _interpolate (trackFeatures.c:31-57); the clamp only guards addresses that
@@ -595,6 +596,11 @@ __device__ __forceinline__ float bilerp(const float *__restrict__ img, int w, in
   return (1.0f - ax) * (1.0f - ay) * p[0] + ax * (1.0f - ay) * p[1] + (1.0f - ax) * ay * p[w] +
          ax * ay * p[w + 1];
 }
+
+// unconditional gather, then a select: bilerp clamps its corner to the plane,
+// so lanes past the window read valid memory and the loads of all planes can
+// be in flight together (a guarded call makes the compiler branch per plane)
+__device__ __forceinline__ float sel(bool on, float v) { return on ? v : 0.0f; }
 
 __device__ __forceinline__ bool window_out(float x, float y, int hw, int hh, int nc, int nr) {
   const float e = 1.001f;
@@ -612,24 +618,44 @@ __device__ __forceinline__ float bcast(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
 
-// NS sequential sums over npx pixels; v[s][k] is lane's pixel lane+64k.
-// LDS layout red[p*NS + s] keeps lanes 0..NS-1 on distinct banks.
+// NS sequential sums over npx pixels; v[s][k] is the value of pixel lane+64k.
+// Sum s lives at red[s*rp ...] (rp/4 odd: the NS readers hit distinct bank
+// slots); lane s reads it back 16 bytes at a time and adds in pixel order.
 template <int NS, int PPL>
-__device__ __forceinline__ void exact_sums(const float (&v)[NS][PPL], float *red, int npx, int lane,
+__device__ __forceinline__ void exact_sums(const float (&v)[NS][PPL], float *red, int rp, int npx, int lane,
                                            float (&out)[NS]) {
+  // the pad of the last 16-byte chunk is written as +0 and added without a
+  // guard: acc + (+0) == acc exactly, since an ordered sum from +0 is never -0
 #pragma unroll
   for (int k = 0; k < PPL; ++k) {
     const int p = lane + kWave * k;
-    if (p < npx) {
+    if (p < rp) {
 #pragma unroll
-      for (int s = 0; s < NS; ++s) red[p * NS + s] = v[s][k];
+      for (int s = 0; s < NS; ++s) red[s * rp + p] = p < npx ? v[s][k] : 0.0f;
     }
   }
   lds_wave_sync();
   float acc = 0.0f;
   if (lane < NS) {
-    const float *r = red + lane;
-    for (int q = 0; q < npx; ++q) acc += r[q * NS];
+    // all reads issued before the first add: one LDS round trip, then the
+    // ordered chain of adds (batches of 8 chunks keep the registers bounded)
+    const float *r = red + lane * rp;
+    const int nch = (npx + 3) >> 2;
+    constexpr int MAXCH = (kWave * PPL) / 4, B = 8;
+    for (int b0 = 0; b0 < MAXCH; b0 += B) {
+      if (b0 >= nch) break;
+      f4 c[B];
+#pragma unroll
+      for (int k = 0; k < B; ++k) c[k] = (b0 + k < nch) ? ld4(r + 4 * (b0 + k)) : f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int k = 0; k < B; ++k) {
+        if (b0 + k >= nch) break;
+        acc += c[k].x;
+        acc += c[k].y;
+        acc += c[k].z;
+        acc += c[k].w;
+      }
+    }
   }
 #pragma unroll
   for (int s = 0; s < NS; ++s) out[s] = bcast(acc, s);
@@ -660,8 +686,9 @@ __device__ int track_level(const TrkArgs &a, const TrkLevel &A, const TrkLevel &
   bool on[PPL];
 #pragma unroll
   for (int k = 0; k < PPL; ++k) {
-    const int p = lane + kWave * k;
-    on[k] = p < npx;
+    const int p0 = lane + kWave * k;
+    on[k] = p0 < npx;
+    const int p = on[k] ? p0 : npx - 1;  // idle lanes gather the last pixel's lines
     const int jj = p / ww;
     oi[k] = p - jj * ww - hw;
     oj[k] = jj - hh;
@@ -674,9 +701,9 @@ __device__ int track_level(const TrkArgs &a, const TrkLevel &A, const TrkLevel &
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
       const float xs = x1 + oi[k], ys = y1 + oj[k];
-      a_im[k] = on[k] ? bilerp(A.img, nc, nr, xs, ys) : 0.0f;
-      a_gx[k] = on[k] ? bilerp(A.gx, nc, nr, xs, ys) : 0.0f;
-      a_gy[k] = on[k] ? bilerp(A.gy, nc, nr, xs, ys) : 0.0f;
+      a_im[k] = sel(on[k], bilerp(A.img, nc, nr, xs, ys));
+      a_gx[k] = sel(on[k], bilerp(A.gx, nc, nr, xs, ys));
+      a_gy[k] = sel(on[k], bilerp(A.gy, nc, nr, xs, ys));
     }
   }
 
@@ -691,9 +718,9 @@ __device__ int track_level(const TrkArgs &a, const TrkLevel &A, const TrkLevel &
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
       const float xs = x2 + oi[k], ys = y2 + oj[k];
-      b_im[k] = on[k] ? bilerp(B.img, nc, nr, xs, ys) : 0.0f;
-      const float bgx = on[k] ? bilerp(B.gx, nc, nr, xs, ys) : 0.0f;
-      const float bgy = on[k] ? bilerp(B.gy, nc, nr, xs, ys) : 0.0f;
+      b_im[k] = sel(on[k], bilerp(B.img, nc, nr, xs, ys));
+      const float bgx = sel(on[k], bilerp(B.gx, nc, nr, xs, ys));
+      const float bgy = sel(on[k], bilerp(B.gy, nc, nr, xs, ys));
       gxs[k] = a_gx[k] + bgx;
       gys[k] = a_gy[k] + bgy;
       dif[k] = a_im[k] - b_im[k];
@@ -708,7 +735,7 @@ __device__ int track_level(const TrkArgs &a, const TrkLevel &A, const TrkLevel &
         mom[2][k] = a_im[k] * a_im[k];
         mom[3][k] = b_im[k] * b_im[k];
       }
-      if (EXACT) exact_sums<4, PPL>(mom, red, npx, lane, S);
+      if (EXACT) exact_sums<4, PPL>(mom, red, a.red_pitch, npx, lane, S);
       else tree_sums<4, PPL>(mom, npx, lane, S);
       const float n = (float)(ww * wh);
       const float alpha = (float)sqrt((double)((S[2] / n) / (S[3] / n)));
@@ -718,8 +745,8 @@ __device__ int track_level(const TrkArgs &a, const TrkLevel &A, const TrkLevel &
       for (int k = 0; k < PPL; ++k) {
         dif[k] = a_im[k] - b_im[k] * alpha - beta;
         const float xs = x2 + oi[k], ys = y2 + oj[k];
-        const float bgx = on[k] ? bilerp(B.gx, nc, nr, xs, ys) : 0.0f;
-        const float bgy = on[k] ? bilerp(B.gy, nc, nr, xs, ys) : 0.0f;
+        const float bgx = sel(on[k], bilerp(B.gx, nc, nr, xs, ys));
+        const float bgy = sel(on[k], bilerp(B.gy, nc, nr, xs, ys));
         gxs[k] = a_gx[k] + bgx * alpha_g;
         gys[k] = a_gy[k] + bgy * alpha_g;
       }
@@ -733,7 +760,7 @@ __device__ int track_level(const TrkArgs &a, const TrkLevel &A, const TrkLevel &
       prod[3][k] = dif[k] * gxs[k];
       prod[4][k] = dif[k] * gys[k];
     }
-    if (EXACT) exact_sums<5, PPL>(prod, red, npx, lane, S);
+    if (EXACT) exact_sums<5, PPL>(prod, red, a.red_pitch, npx, lane, S);
     else tree_sums<5, PPL>(prod, npx, lane, S);
     const float gxx = S[0], gxy = S[1], gyy = S[2];
     const float ex = S[3] * a.step, ey = S[4] * a.step;
@@ -760,7 +787,7 @@ __device__ int track_level(const TrkArgs &a, const TrkLevel &A, const TrkLevel &
     float b_im[PPL];
 #pragma unroll
     for (int k = 0; k < PPL; ++k)
-      b_im[k] = on[k] ? bilerp(B.img, nc, nr, x2 + oi[k], y2 + oj[k]) : 0.0f;
+      b_im[k] = sel(on[k], bilerp(B.img, nc, nr, x2 + oi[k], y2 + oj[k]));
     if (a.li) {
       float mom[4][PPL], M[4];
 #pragma unroll
@@ -770,7 +797,7 @@ __device__ int track_level(const TrkArgs &a, const TrkLevel &A, const TrkLevel &
         mom[2][k] = a_im[k] * a_im[k];
         mom[3][k] = b_im[k] * b_im[k];
       }
-      if (EXACT) exact_sums<4, PPL>(mom, red, npx, lane, M);
+      if (EXACT) exact_sums<4, PPL>(mom, red, a.red_pitch, npx, lane, M);
       else tree_sums<4, PPL>(mom, npx, lane, M);
       const float n = (float)(ww * wh);
       alpha = (float)sqrt((double)((M[2] / n) / (M[3] / n)));
@@ -781,7 +808,7 @@ __device__ int track_level(const TrkArgs &a, const TrkLevel &A, const TrkLevel &
       const float d = a.li ? (a_im[k] - b_im[k] * alpha - beta) : (a_im[k] - b_im[k]);
       dif[0][k] = fabsf(d);
     }
-    if (EXACT) exact_sums<1, PPL>(dif, red, npx, lane, S);
+    if (EXACT) exact_sums<1, PPL>(dif, red, a.red_pitch, npx, lane, S);
     else tree_sums<1, PPL>(dif, npx, lane, S);
     if (S[0] / (float)(ww * wh) > a.max_res) status = kLargeResidue;
   }
@@ -795,7 +822,7 @@ __device__ int track_level(const TrkArgs &a, const TrkLevel &A, const TrkLevel &
 template <int PPL, bool EXACT>
 __global__ __launch_bounds__(kBlock) void k_track(TrkArgs a, float *__restrict__ fx,
                                                   float *__restrict__ fy, int *__restrict__ fv, int n) {
-  __shared__ float red_all[kBlock / kWave][5 * kWave * PPL];
+  __shared__ __attribute__((aligned(16))) float red_all[kBlock / kWave][5 * (kWave * PPL + 4)];
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   const int f = blockIdx.x * (kBlock / kWave) + wave;
   if (f >= n) return;  // whole wave; the kernel has no workgroup barrier
@@ -1342,6 +1369,11 @@ KLT_API int klt_hip_track(klt_hip_ctx *c, int s1, int s2, const klt_hip_track_de
   a.ncols = A.lv[0].w;
   a.nrows = A.lv[0].h;
   a.li = d->lighting_insensitive;
+  {
+    int rp = (npx + 3) & ~3;  // 16-byte rows with an odd slot count: distinct banks per sum
+    if (((rp / 4) & 1) == 0) rp += 4;
+    a.red_pitch = rp;
+  }
 
   float *x_d = x, *y_d = y;
   int *v_d = val;

@@ -637,6 +637,11 @@ static void sample_windows(const orc_level *A, const orc_level *B, float x1, flo
 enum { TRACKED = 0, NOT_FOUND = -1, SMALL_DET = -2, MAX_ITERATIONS = -3, OOB = -4,
        LARGE_RESIDUE = -5 };
 
+/* diagnostics: Newton iterations per (feature, level) of the last orc_track */
+static int *g_iter_log = NULL;
+static int g_iter_feature = 0, g_iter_level = 0, g_iter_nlev = 0;
+ORC_EXPORT void orc_set_iter_log(int *buf) { g_iter_log = buf; }
+
 static int window_out(float x, float y, int hw, int hh, int nc, int nr)
 {
   const float eps1 = 1.001f;
@@ -695,6 +700,7 @@ static int track_one(float x1, float y1, float *x2, float *y2, const orc_level *
            it < P->max_iterations);
 
   if (window_out(*x2, *y2, hw, hh, nc, nr)) status = OOB;
+  if (g_iter_log) g_iter_log[g_iter_feature * g_iter_nlev + g_iter_level] = it;
 
   if (status == TRACKED) {
     float s = 0.0f;
@@ -750,6 +756,9 @@ ORC_EXPORT void orc_track(orc_tracker *t, const uint8_t *img1, const uint8_t *im
       yl *= ss;
       xo *= ss;
       yo *= ss;
+      g_iter_feature = k;
+      g_iter_level = r;
+      g_iter_nlev = P->nPyramidLevels;
       val = track_one(xl, yl, &xo, &yo, &A, &B, P);
       if (val == SMALL_DET || val == OOB) break;
     }

@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--frames", type=int, default=8)
     ap.add_argument("--reduction", choices=["exact", "fast"], default="exact")
     ap.add_argument("--generic", action="store_true")
+    ap.add_argument("--max-it", type=int, default=0, help="tracker: override max_iterations")
+    ap.add_argument("--lost", action="store_true", help="tracker: mark every feature lost (launch floor)")
+    ap.add_argument("--window", type=int, default=0, help="tracker: override window width/height")
     a = ap.parse_args()
 
     import kltamd
@@ -53,6 +56,10 @@ def main():
     check(lib, ctx, lib.klt_hip_synth_frames(ctx, 1080, 0, nf, W, H, frames, W, W * H), "synth")
     pd, td = PyrDesc(), TrackDesc()
     lib.klt_amd_pyr_desc(tc, W, H, tc.contents.nPyramidLevels, 1, C.byref(pd))
+    if a.max_it:
+        tc.contents.max_iterations = a.max_it
+    if a.window:
+        tc.contents.window_width = tc.contents.window_height = a.window
     lib.klt_amd_track_desc(tc, C.byref(td))
     out = {"mode": a.mode, "resolution": f"{W}x{H}", "reps": a.reps}
 
@@ -91,6 +98,8 @@ def main():
         ys = np.array([fl.contents.feature[k].contents.y for k in range(n)], np.float32)
         vs = np.array([fl.contents.feature[k].contents.val for k in range(n)], np.int32)
         lib.KLTFreeFeatureList(fl)
+        if a.lost:
+            vs[:] = -1
         build(0, 0)
         build(1, 1)
         st = [lib.klt_hip_malloc(ctx, 4 * n) for _ in range(3)]
