@@ -51,6 +51,9 @@ def parse():
                    help="frames of the bounded CPU-baseline sample (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--reduction", choices=["exact", "fast"], default="exact")
+    p.add_argument("--chunk", type=int, default=16,
+                   help="frames per batched pyramid/track launch (klt_hip_track_frames); 0 = the per-frame "
+                        "pipelined path (klt_hip_track_sequence)")
     p.add_argument("--event-timing", choices=["timed", "replay"], default="replay",
                    help="record per-kernel HIP events inside the timed region or in a replay")
     return p.parse_args()
@@ -112,20 +115,32 @@ def main() -> None:
     lib.klt_amd_track_desc(tc, C.byref(td))
     fptr = frames.data_ptr()
     slot = C.c_int(0)
+    # the harness's feature table (KLTStoreFeatureList after every frame), in HBM
+    tab = [torch.empty((nframes, NF), dtype=dt, device=dev) for dt in (torch.float32, torch.float32, torch.int32)]
 
     def build0(t):
+        if args.chunk > 0:
+            check(lib, ctx, lib.klt_hip_frames_begin(ctx, C.byref(pd), C.c_void_p(fptr + t * W * H), W), "begin")
+            return
         check(lib, ctx, lib.klt_hip_build_pyramid(ctx, 0, C.byref(pd), C.c_void_p(fptr + t * W * H), W, 0),
               "build")
         slot.value = 0
 
     def run(t0, n):
+        if args.chunk > 0:
+            tp = [C.c_void_p(a.data_ptr() + a.element_size() * t0 * NF) for a in tab]
+            check(lib, ctx, lib.klt_hip_track_frames(ctx, C.byref(pd), C.byref(td), C.c_void_p(fptr + t0 * W * H),
+                                                     W, W * H, n, args.chunk, C.c_void_p(x.data_ptr()),
+                                                     C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()), NF,
+                                                     tp[0], tp[1], tp[2], NF), "track_frames")
+            return
         check(lib, ctx, lib.klt_hip_track_sequence(ctx, C.byref(pd), C.byref(td), C.c_void_p(fptr), W, W * H,
                                                    t0, n, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()),
                                                    C.c_void_p(v.data_ptr()), NF, C.byref(slot)), "track_sequence")
 
     build0(0)
     run(1, args.warmup)
-    fused = lib.klt_hip_pyramid_path(ctx, slot.value) == 1
+    fused = bool(lib.klt_hip_pyramid_path(ctx, slot.value) == 1) if args.chunk == 0 else bool(lib.klt_hip_fused_path(ctx, C.byref(pd)) == 1)
     live_before = int((v >= 0).sum().item())
     xs, ys, vs, t_start = x.clone(), y.clone(), v.clone(), 1 + args.warmup
 
@@ -158,15 +173,20 @@ def main() -> None:
         dt_max = float(t.item())
 
     us = lambda ms, n: (1000.0 * ms / n) if n else None  # noqa: E731
+    # per launch (a launch covers `chunk` frames on the batched path) and per frame
     l0 = us(tm.ms_pyr_l0, tm.n_pyr_l0)
     l1 = us(tm.ms_pyr_l1, tm.n_pyr_l1)
     trk = us(tm.ms_track, tm.n_track)
     gen = us(tm.ms_generic, tm.n_generic)
-    pass_us = (l0 or 0) + (l1 or 0) if fused else gen
+    l0f = us(tm.ms_pyr_l0, tm.frames_pyr_l0)
+    l1f = us(tm.ms_pyr_l1, tm.frames_pyr_l1)
+    trkf = us(tm.ms_track, tm.frames_track)
+    fpl = (tm.frames_pyr_l0 / tm.n_pyr_l0) if tm.n_pyr_l0 else 1.0  # frames per pyramid launch
+    pass_us = (l0f or 0) + (l1f or 0) if fused else gen
     px = W * H
     W1, H1 = W // 4, H // 4
     pass_bytes = px * 13 + W1 * H1 * 12  # u8 in; img/gx/gy out at L0 and L1
-    l0_bytes = px * 13 + W1 * H * 4      # k_pyr_l0: u8 in, img/gx/gy + sampled row pass out
+    l0_bytes = px * 13 + W1 * H * 4      # k_pyr_l0: u8 in, img/gx/gy + sampled row pass out (per frame)
 
     result = {
         "metric": METRIC,
@@ -181,13 +201,16 @@ def main() -> None:
         "vs_baseline": None,
         "dtype": "f32",
         "data": f"synthetic: include/klt_synth.h value-noise frames, (0.7,0.3) px/frame, seed {args.seed}+rank",
-        "config": {"workload": f"{W}x{H}, {NF} features, sequential KLTTrackFeatures pass per frame, "
-                               f"{nframes} frames per GPU (BASELINE config 3; config 5 at N>1)",
+        "config": {"workload": f"{W}x{H}, {NF} features, sequential KLTTrackFeatures pass + KLTStoreFeatureList "
+                               f"per frame, {nframes} frames per GPU (BASELINE config 3; config 5 at N>1)",
+                   "chunk": args.chunk,
                    "resolution": f"{W}x{H}", "features": NF, "frames": nframes,
                    "parallelism": "independent sequence per GPU" if world > 1 else "single GPU",
                    "reduction": args.reduction, "pyramid_path": "fused" if fused else "generic"},
         "pyramid_gpix_s": (px / (pass_us * 1e-6) / 1e9) if pass_us else None,
-        "kernels_us": {"k_pyr_l0": l0, "k_pyr_l1": l1, "k_track": trk, "generic_pass": gen},
+        "kernels_us_per_launch": {"k_pyr_l0": l0, "k_pyr_l1": l1, "k_track": trk, "generic_pass": gen},
+        "kernels_us_per_frame": {"k_pyr_l0": l0f, "k_pyr_l1": l1f, "k_track": trkf},
+        "frames_per_launch": fpl,
         "live_features": {"after_warmup": live_before, "at_end": live_after},
     }
     if pass_us:
@@ -195,10 +218,11 @@ def main() -> None:
         result["roofline"] = {
             "kernel": "pyramid pass (k_pyr_l0 + k_pyr_l1)", "bound": "hbm", "achieved": ach,
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-            "traffic": None, "algorithmic_bytes_per_launch": pass_bytes,
-            "us_per_launch": pass_us,
-            "k_pyr_l0": {"achieved": (l0_bytes / (l0 * 1e-6) / 1e9) if l0 else None,
-                         "algorithmic_bytes": l0_bytes},
+            "traffic": None, "algorithmic_bytes_per_frame": pass_bytes,
+            "algorithmic_bytes_per_launch": pass_bytes * fpl, "frames_per_launch": fpl,
+            "us_per_frame": pass_us,
+            "k_pyr_l0": {"achieved": (l0_bytes / (l0f * 1e-6) / 1e9) if l0f else None,
+                         "algorithmic_bytes_per_frame": l0_bytes},
             "event_timing": "timed region" if timed_events else "replay of the timed region",
         }
         pmc = ROOT / "profiles" / "pmc_latest.json"
@@ -266,7 +290,7 @@ def cpu_leg(lib, frames, W, H, NF, args, tc, ctx, dev):
     cpu_fps = len(steady) / sum(steady)
 
     # the timed GPU path on the same frames: value-by-value parity
-    gx, gy, gv = gpu_sequence(lib, host, NF)
+    gx, gy, gv = gpu_sequence(lib, host, NF, args.chunk)
     mism = int((gx.view(np.int32) != cx.view(np.int32)).sum() + (gy.view(np.int32) != cy.view(np.int32)).sum()
                + (gv != cv).sum())
     cpu = {"value": cpu_fps, "unit": "frames/s", "cores": 1, "kind": kind,
@@ -279,9 +303,10 @@ def cpu_leg(lib, frames, W, H, NF, args, tc, ctx, dev):
     return cpu, par
 
 
-def gpu_sequence(lib, host, NF):
-    """The timed path (klt_hip_track_sequence, frames + features in HBM) on the
-    CPU sample's frames: select on frame 0, then track frames 1..S-1."""
+def gpu_sequence(lib, host, NF, chunk):
+    """The timed path (klt_hip_track_frames -- or klt_hip_track_sequence for
+    chunk 0 -- frames + features in HBM) on the CPU sample's frames: select on
+    frame 0, then track frames 1..S-1."""
     import torch
     from kltamd.device import PyrDesc, TrackDesc, check
     H, W = host[0].shape
@@ -300,11 +325,19 @@ def gpu_sequence(lib, host, NF):
     pd, td = PyrDesc(), TrackDesc()
     lib.klt_amd_pyr_desc(tc, W, H, tc.contents.nPyramidLevels, 1, C.byref(pd))
     lib.klt_amd_track_desc(tc, C.byref(td))
-    check(lib, ctx, lib.klt_hip_build_pyramid(ctx, 0, C.byref(pd), C.c_void_p(fr.data_ptr()), W, 0), "build")
-    slot = C.c_int(0)
-    check(lib, ctx, lib.klt_hip_track_sequence(ctx, C.byref(pd), C.byref(td), C.c_void_p(fr.data_ptr()), W, W * H,
-                                               1, len(host) - 1, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()),
-                                               C.c_void_p(v.data_ptr()), NF, C.byref(slot)), "sequence")
+    if chunk > 0:
+        check(lib, ctx, lib.klt_hip_frames_begin(ctx, C.byref(pd), C.c_void_p(fr.data_ptr()), W), "begin")
+        check(lib, ctx, lib.klt_hip_track_frames(ctx, C.byref(pd), C.byref(td), C.c_void_p(fr.data_ptr() + W * H), W,
+                                                 W * H, len(host) - 1, chunk, C.c_void_p(x.data_ptr()),
+                                                 C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()), NF, None,
+                                                 None, None, 0), "frames")
+    else:
+        check(lib, ctx, lib.klt_hip_build_pyramid(ctx, 0, C.byref(pd), C.c_void_p(fr.data_ptr()), W, 0), "build")
+        slot = C.c_int(0)
+        check(lib, ctx, lib.klt_hip_track_sequence(ctx, C.byref(pd), C.byref(td), C.c_void_p(fr.data_ptr()), W,
+                                                   W * H, 1, len(host) - 1, C.c_void_p(x.data_ptr()),
+                                                   C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()), NF,
+                                                   C.byref(slot)), "sequence")
     torch.cuda.synchronize()
     out = (x.cpu().numpy(), y.cpu().numpy(), v.cpu().numpy())
     lib.KLTFreeTrackingContext(tc)

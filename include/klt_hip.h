@@ -76,6 +76,7 @@ typedef struct {
 typedef struct {
   int n_pyr_l0, n_pyr_l1, n_track, n_eigen, n_generic;
   double ms_pyr_l0, ms_pyr_l1, ms_track, ms_eigen, ms_generic;
+  long frames_pyr_l0, frames_pyr_l1, frames_track; /* frames covered by the timed launches */
 } klt_hip_timing;
 
 typedef struct klt_hip_ctx klt_hip_ctx;
@@ -101,6 +102,8 @@ int klt_hip_build_pyramid(klt_hip_ctx *ctx, int slot, const klt_hip_pyr_desc *de
 /* test hook: 1 forces the generic one-pass-per-launch path even when the
    fused kernels apply (they must agree bit for bit) */
 int klt_hip_set_path(klt_hip_ctx *ctx, int force_generic);
+/* 1 if pyramids for `desc` would be built by the fused gfx950 kernels, else 0 */
+int klt_hip_fused_path(klt_hip_ctx *ctx, const klt_hip_pyr_desc *desc);
 /* 1 if the slot was built by the fused gfx950 kernels, 0 generic, <0 invalid */
 int klt_hip_pyramid_path(klt_hip_ctx *ctx, int slot);
 int klt_hip_level_dims(klt_hip_ctx *ctx, int slot, int level, int *ncols, int *nrows);
@@ -123,6 +126,25 @@ int klt_hip_track_sequence(klt_hip_ctx *ctx, const klt_hip_pyr_desc *pdesc,
                            const klt_hip_track_desc *tdesc, const unsigned char *frames, long pitch,
                            long stride, int t0, int nsteps, float *x, float *y, int *val, int n,
                            int *cur_slot);
+
+/* batched device-resident sequence -- the KLTTrackFeatures +
+   KLTStoreFeatureList loop of the reference harness (example3.c:54-74) with
+   no feature replacement, `chunk` frames per pair of pyramid launches and per
+   tracking launch, pyramids built one chunk ahead on a second stream.
+   klt_hip_frames_begin builds the pyramid the first tracked frame starts from;
+   klt_hip_track_frames then tracks the device arrays x/y/val (n features)
+   through frames[0..nframes-1] (frame f at frames + f*stride, row pitch
+   `pitch`), and leaves the last frame's pyramid as the start of the next call.
+   tab_* (device, optional: all three or NULL) receive the list after each
+   frame in row f (row stride tab_stride >= n).  Three banks of `chunk`
+   pyramids are allocated on first use (and regrown, after draining the
+   streams, when chunk or the frame size grows).  Asynchronous. */
+int klt_hip_frames_begin(klt_hip_ctx *ctx, const klt_hip_pyr_desc *pdesc, const unsigned char *frame,
+                         long pitch);
+int klt_hip_track_frames(klt_hip_ctx *ctx, const klt_hip_pyr_desc *pdesc, const klt_hip_track_desc *tdesc,
+                         const unsigned char *frames, long pitch, long stride, int nframes, int chunk,
+                         float *x, float *y, int *val, int n, float *tab_x, float *tab_y, int *tab_val,
+                         long tab_stride);
 
 /* trackability map of level 0 of `slot`: nx*ny int values, row-major over the
    border-trimmed grid; vals == NULL only reports nx, ny.  Synchronous. */

@@ -327,9 +327,16 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
 __global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ src, int spitch, int W, int H,
                                                    DefTaps T, int vec_u8, float *__restrict__ img0,
                                                    float *__restrict__ gx0, float *__restrict__ gy0,
-                                                   float *__restrict__ hs, int hsW, int do_hs, int vec_out) {
+                                                   float *__restrict__ hs, int hsW, int do_hs, int vec_out,
+                                                   long fs_src, long fs0, long fs_hs) {
   __shared__ __attribute__((aligned(16))) float lds[l0::LDS];
   const int C0 = blockIdx.x * l0::TW, R0 = blockIdx.y * l0::TH;
+  // blockIdx.z: frame of a batch (frame strides in elements; 0 for one frame)
+  src += blockIdx.z * fs_src;
+  img0 += blockIdx.z * fs0;
+  gx0 += blockIdx.z * fs0;
+  gy0 += blockIdx.z * fs0;
+  hs += blockIdx.z * fs_hs;
   // interior: unclamped aligned loads, no zero-border rule applies, all stores in bounds
   const bool interior = vec_u8 && vec_out && (hsW * l0::SS == W) && (hsW % 2 == 0) && C0 >= 12 && C0 + 84 <= W &&
                         R0 >= 5 && R0 + 39 <= H;
@@ -357,8 +364,13 @@ static_assert(2 * LDS_X <= LDS_H, "tx/ty reuse the hs region");
 
 __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs, int W1, int H, int H1,
                                                    DefTaps T, int vec, float *__restrict__ img1,
-                                                   float *__restrict__ gx1, float *__restrict__ gy1) {
+                                                   float *__restrict__ gx1, float *__restrict__ gy1,
+                                                   long fs_hs, long fs1) {
   using namespace l1;
+  hs += blockIdx.z * fs_hs;
+  img1 += blockIdx.z * fs1;
+  gx1 += blockIdx.z * fs1;
+  gy1 += blockIdx.z * fs1;
   __shared__ __attribute__((aligned(16))) float lds[LDS];
   float *hl = lds;          // [HR][JW]
   float *im = lds + LDS_H;  // [JH][JW]
@@ -819,19 +831,13 @@ __device__ int track_level(const TrkArgs &a, const TrkLevel &A, const TrkLevel &
   return kTracked;
 }
 
-template <int PPL, bool EXACT>
-__global__ __launch_bounds__(kBlock) void k_track(TrkArgs a, float *__restrict__ fx,
-                                                  float *__restrict__ fy, int *__restrict__ fv, int n) {
-  __shared__ __attribute__((aligned(16))) float red_all[kBlock / kWave][5 * (kWave * PPL + 4)];
-  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  const int f = blockIdx.x * (kBlock / kWave) + wave;
-  if (f >= n) return;  // whole wave; the kernel has no workgroup barrier
-  const int v0 = fv[f];
-  if (v0 < 0) return;  // lost features are not tracked (:1346)
-  float *red = red_all[wave];
-
-  // KLTTrackFeatures coarse-to-fine driver (:1348-1380)
-  float xl = fx[f], yl = fy[f];
+// KLTTrackFeatures coarse-to-fine driver for one feature (:1348-1380) and its
+// status mapping (:1383-1437) with _outOfBounds (:491-501).  LA(r) / LB(r)
+// give level r of the previous / current pyramid.
+template <int PPL, bool EXACT, class LevA, class LevB>
+__device__ __forceinline__ void track_feature(const TrkArgs &a, LevA LA, LevB LB, float &fx, float &fy, int &fv,
+                                              int lane, float *red) {
+  float xl = fx, yl = fy;
   for (int r = a.nlev - 1; r >= 0; --r) {
     xl /= a.ss;
     yl /= a.ss;
@@ -843,26 +849,90 @@ __global__ __launch_bounds__(kBlock) void k_track(TrkArgs a, float *__restrict__
     yl *= a.ss;
     xo *= a.ss;
     yo *= a.ss;
-    val = track_level<PPL, EXACT>(a, a.A[r], a.B[r], xl, yl, xo, yo, lane, red);
+    val = track_level<PPL, EXACT>(a, LA(r), LB(r), xl, yl, xo, yo, lane, red);
     if (val == kSmallDet || val == kOOB) break;
   }
+  const bool border = xo < a.borderx || xo > a.ncols - 1 - a.borderx || yo < a.bordery ||
+                      yo > a.nrows - 1 - a.bordery;
+  if (val == kOOB || border) {
+    fx = -1.0f;
+    fy = -1.0f;
+    fv = kOOB;
+  } else if (val != kTracked) {
+    fx = -1.0f;
+    fy = -1.0f;
+    fv = val;
+  } else {
+    fx = xo;
+    fy = yo;
+    fv = kTracked;
+  }
+}
+
+template <int PPL, bool EXACT>
+__global__ __launch_bounds__(kBlock) void k_track(TrkArgs a, float *__restrict__ fx,
+                                                  float *__restrict__ fy, int *__restrict__ fv, int n) {
+  __shared__ __attribute__((aligned(16))) float red_all[kBlock / kWave][5 * (kWave * PPL + 4)];
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int f = blockIdx.x * (kBlock / kWave) + wave;
+  if (f >= n) return;  // whole wave; the kernel has no workgroup barrier
+  int v = fv[f];
+  if (v < 0) return;  // lost features are not tracked (:1346)
+  float x = fx[f], y = fy[f];
+  track_feature<PPL, EXACT>(
+      a, [&](int r) { return a.A[r]; }, [&](int r) { return a.B[r]; }, x, y, v, lane, red_all[wave]);
   if (lane == 0) {
-    // status mapping (:1383-1437) with _outOfBounds (:491-501)
-    const bool border = xo < a.borderx || xo > a.ncols - 1 - a.borderx || yo < a.bordery ||
-                        yo > a.nrows - 1 - a.bordery;
-    if (val == kOOB || border) {
-      fx[f] = -1.0f;
-      fy[f] = -1.0f;
-      fv[f] = kOOB;
-    } else if (val != kTracked) {
-      fx[f] = -1.0f;
-      fy[f] = -1.0f;
-      fv[f] = val;
-    } else {
-      fx[f] = xo;
-      fy[f] = yo;
-      fv[f] = kTracked;
+    fx[f] = x;
+    fy[f] = y;
+    fv[f] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_track_frames: one wave carries its feature through a batch of frames
+// (the KLTTrackFeatures + KLTStoreFeatureList loop of example3.c:54-74 with
+// no replacement).  Frame j tracks pyramid j-1 -> j of the bank (j = 0: from
+// a.A, the pyramid before the batch); every feature is independent, so the
+// per-frame launch and its dependency bubble disappear.  Row j of the
+// optional feature table receives the list after frame j.
+// ---------------------------------------------------------------------------
+struct TrkFramesArgs {
+  long lfs[KLT_HIP_MAX_LEVELS];  // bank frame stride per level (floats)
+  int nframes;
+  float *tx, *ty;
+  int *tv;
+  long tstride;  // table row stride (elements); tx == nullptr: no table
+};
+
+__device__ __forceinline__ TrkLevel at_frame(const TrkLevel &L, long off) {
+  return TrkLevel{L.img + off, L.gx + off, L.gy + off, L.w, L.h};
+}
+
+template <int PPL, bool EXACT>
+__global__ __launch_bounds__(kBlock) void k_track_frames(TrkArgs a, TrkFramesArgs b, float *__restrict__ fx,
+                                                         float *__restrict__ fy, int *__restrict__ fv, int n) {
+  __shared__ __attribute__((aligned(16))) float red_all[kBlock / kWave][5 * (kWave * PPL + 4)];
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int f = blockIdx.x * (kBlock / kWave) + wave;
+  if (f >= n) return;
+  float x = fx[f], y = fy[f];
+  int v = fv[f];
+  for (int j = 0; j < b.nframes; ++j) {
+    if (v >= 0) {
+      track_feature<PPL, EXACT>(
+          a, [&](int r) { return j == 0 ? a.A[r] : at_frame(a.B[r], (long)(j - 1) * b.lfs[r]); },
+          [&](int r) { return at_frame(a.B[r], (long)j * b.lfs[r]); }, x, y, v, lane, red_all[wave]);
     }
+    if (b.tx && lane == 0) {
+      b.tx[j * b.tstride + f] = x;
+      b.ty[j * b.tstride + f] = y;
+      b.tv[j * b.tstride + f] = v;
+    }
+  }
+  if (lane == 0) {
+    fx[f] = x;
+    fy[f] = y;
+    fv[f] = v;
   }
 }
 
@@ -911,6 +981,22 @@ struct Slot {
 
 enum TimerClass { T_L0 = 0, T_L1, T_TRACK, T_EIG, T_GEN, T_N };
 
+// a batch of same-size pyramids: plane l of frame f at lv[l].img + f * w*h
+struct Bank {
+  int frames = 0;  // capacity in frames
+  int nlev = 0;
+  int ss = 1;
+  Level lv[KLT_HIP_MAX_LEVELS];
+  float *hs = nullptr;  // per-frame row pass of the sigma-3.6 smoothing (fused path)
+  size_t hs_cap = 0;
+};
+
+// where the pyramid preceding the next batch lives
+struct PrevRef {
+  int bank = -1;  // -1: slot kSeedSlot
+  int frame = 0;
+};
+
 struct klt_hip_ctx {
   int device = 0;
   hipStream_t own = nullptr;
@@ -919,7 +1005,7 @@ struct klt_hip_ctx {
   hipEvent_t ev_built[KLT_HIP_MAX_SLOTS] = {};
   hipEvent_t ev_free[KLT_HIP_MAX_SLOTS] = {};
   hipEvent_t ev_start = nullptr;
-  Slot slot[KLT_HIP_MAX_SLOTS];
+  Slot slot[KLT_HIP_MAX_SLOTS + 2];  // + the batch seed and scratch slots
   uint8_t *d_u8[2] = {nullptr, nullptr};
   uint8_t *h_u8[2] = {nullptr, nullptr};
   hipEvent_t u8_done[2] = {nullptr, nullptr};
@@ -936,7 +1022,13 @@ struct klt_hip_ctx {
   size_t eig_cap = 0;
   std::string err;
   int force_generic = 0;
+  Bank bank[3];
+  int bank_next = 0;
+  PrevRef prev;
+  bool frames_ready = false;
+  hipEvent_t ev_bbuilt[3] = {}, ev_bfree[3] = {};
   bool timing = false;
+  long frames_timed[T_N] = {};
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_used[T_N];
 };
@@ -991,8 +1083,9 @@ struct TimedScope {
   int cls;
   hipStream_t st;
   hipEvent_t a = nullptr, b = nullptr;
-  TimedScope(klt_hip_ctx *c_, int cls_, hipStream_t st_) : c(c_), cls(cls_), st(st_) {
+  TimedScope(klt_hip_ctx *c_, int cls_, hipStream_t st_, int frames = 1) : c(c_), cls(cls_), st(st_) {
     if (!c->timing) return;
+    c->frames_timed[cls] += frames;
     a = take_event(c);
     b = take_event(c);
     if (a) hipEventRecord(a, st);
@@ -1133,7 +1226,7 @@ int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t 
     TimedScope ts(c, T_L0, st);
     dim3 grid((W + l0::TW - 1) / l0::TW, (H + l0::TH - 1) / l0::TH);
     hipLaunchKernelGGL(k_pyr_l0, grid, dim3(kBlock), 0, st, src, (int)pitch, W, H, T, vec_u8, S.lv[0].img,
-                       S.lv[0].gx, S.lv[0].gy, c->d_hs, W1, (two && W1 > 0) ? 1 : 0, vec_out);
+                       S.lv[0].gx, S.lv[0].gy, c->d_hs, W1, (two && W1 > 0) ? 1 : 0, vec_out, 0L, 0L, 0L);
     if (check_launch(c, "k_pyr_l0")) return -1;
   }
   if (two && (long)W1 * H1 > 0) {
@@ -1141,7 +1234,7 @@ int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t 
     const int vec = (W1 % 4 == 0 && W1 >= 8) ? 1 : 0;
     dim3 grid((W1 + l1::TW - 1) / l1::TW, (H1 + l1::TH - 1) / l1::TH);
     hipLaunchKernelGGL(k_pyr_l1, grid, dim3(l1::NT), 0, st, c->d_hs, W1, H, H1, T, vec, S.lv[1].img,
-                       S.lv[1].gx, S.lv[1].gy);
+                       S.lv[1].gx, S.lv[1].gy, 0L, 0L);
     if (check_launch(c, "k_pyr_l1")) return -1;
   }
   return 0;
@@ -1151,6 +1244,130 @@ template <int PPL, bool EXACT>
 void launch_track(hipStream_t st, const TrkArgs &a, float *x, float *y, int *v, int n) {
   const int per = kBlock / kWave;
   hipLaunchKernelGGL((k_track<PPL, EXACT>), dim3((n + per - 1) / per), dim3(kBlock), 0, st, a, x, y, v, n);
+}
+
+template <int PPL, bool EXACT>
+void launch_track_frames(hipStream_t st, const TrkArgs &a, const TrkFramesArgs &b, float *x, float *y, int *v,
+                         int n) {
+  const int per = kBlock / kWave;
+  hipLaunchKernelGGL((k_track_frames<PPL, EXACT>), dim3((n + per - 1) / per), dim3(kBlock), 0, st, a, b, x, y,
+                     v, n);
+}
+
+int check_window(klt_hip_ctx *c, const klt_hip_track_desc *d) {
+  const int npx = d->window_width * d->window_height;
+  if (d->window_width < 1 || d->window_height < 1 || npx > 16 * kWave)
+    return fail(c, "track: window %dx%d unsupported (max %d pixels)", d->window_width, d->window_height,
+                16 * kWave);
+  return 0;
+}
+
+void fill_trk_args(const klt_hip_track_desc *d, int nlev, int ss, int ncols, int nrows, TrkArgs &a) {
+  memset(&a, 0, sizeof a);
+  const int npx = d->window_width * d->window_height;
+  a.nlev = nlev;
+  a.ss = (float)ss;
+  a.ww = d->window_width;
+  a.wh = d->window_height;
+  a.max_it = d->max_iterations;
+  a.min_det = d->min_determinant;
+  a.min_disp = d->min_displacement;
+  a.max_res = d->max_residue;
+  a.step = d->step_factor;
+  a.borderx = d->borderx;
+  a.bordery = d->bordery;
+  a.ncols = ncols;
+  a.nrows = nrows;
+  a.li = d->lighting_insensitive;
+  int rp = (npx + 3) & ~3;  // 16-byte rows with an odd slot count: distinct banks per sum
+  if (((rp / 4) & 1) == 0) rp += 4;
+  a.red_pitch = rp;
+}
+
+int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc *d, const TrkArgs &a,
+                        const TrkFramesArgs &b, float *x, float *y, int *v, int n) {
+  TimedScope ts(c, T_TRACK, st, b.nframes);
+  const int npx = d->window_width * d->window_height;
+  const bool exact = d->reduction == KLT_HIP_EXACT;
+  if (npx <= kWave) {
+    if (exact) launch_track_frames<1, true>(st, a, b, x, y, v, n);
+    else launch_track_frames<1, false>(st, a, b, x, y, v, n);
+  } else if (npx <= 4 * kWave) {
+    if (exact) launch_track_frames<4, true>(st, a, b, x, y, v, n);
+    else launch_track_frames<4, false>(st, a, b, x, y, v, n);
+  } else {
+    if (exact) launch_track_frames<16, true>(st, a, b, x, y, v, n);
+    else launch_track_frames<16, false>(st, a, b, x, y, v, n);
+  }
+  return check_launch(c, "k_track_frames");
+}
+
+// allocate bank k for `frames` pyramids shaped like desc d
+int ensure_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, int frames) {
+  int w = d->ncols, h = d->nrows;
+  K.nlev = d->nlevels;
+  K.ss = d->nlevels > 1 ? d->subsampling : 1;
+  for (int l = 0; l < d->nlevels; ++l) {
+    Level &L = K.lv[l];
+    L.w = w;
+    L.h = h;
+    const size_t need = (size_t)(w > 0 ? w : 1) * (h > 0 ? h : 1) * frames;
+    if (L.cap < need || !L.img) {
+      hipFree(L.img);
+      hipFree(L.gx);
+      hipFree(L.gy);
+      L.img = L.gx = L.gy = nullptr;
+      L.cap = 0;
+      HIPCHK(c, hipMalloc((void **)&L.img, need * sizeof(float)));
+      HIPCHK(c, hipMalloc((void **)&L.gx, need * sizeof(float)));
+      HIPCHK(c, hipMalloc((void **)&L.gy, need * sizeof(float)));
+      L.cap = need;
+    }
+    w /= K.ss;
+    h /= K.ss;
+  }
+  if (d->nlevels == 2) {
+    const size_t need = (size_t)(K.lv[1].w > 0 ? K.lv[1].w : 1) * d->nrows * frames;
+    if (K.hs_cap < need || !K.hs) {
+      hipFree(K.hs);
+      K.hs = nullptr;
+      K.hs_cap = 0;
+      HIPCHK(c, hipMalloc((void **)&K.hs, need * sizeof(float)));
+      K.hs_cap = need;
+    }
+  }
+  K.frames = frames;
+  return 0;
+}
+
+// fused pyramids of F frames (src + f*stride) into bank K, two launches
+int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
+                     long stride, int F, hipStream_t st) {
+  const int W = d->ncols, H = d->nrows;
+  const DefTaps T = default_taps(d);
+  const bool two = d->nlevels == 2;
+  const int W1 = two ? K.lv[1].w : 0, H1 = two ? K.lv[1].h : 0;
+  if ((long)W * H == 0 || F <= 0) return 0;
+  const int vec_u8 =
+      (W % 4 == 0 && W >= 16 && pitch % 4 == 0 && stride % 4 == 0 && ((uintptr_t)src & 3) == 0) ? 1 : 0;
+  const int vec_out = (W % 4 == 0) ? 1 : 0;
+  const long fs0 = (long)W * H, fsh = (long)W1 * H, fs1 = (long)W1 * H1;
+  {
+    TimedScope ts(c, T_L0, st, F);
+    dim3 grid((W + l0::TW - 1) / l0::TW, (H + l0::TH - 1) / l0::TH, F);
+    hipLaunchKernelGGL(k_pyr_l0, grid, dim3(kBlock), 0, st, src, (int)pitch, W, H, T, vec_u8, K.lv[0].img,
+                       K.lv[0].gx, K.lv[0].gy, K.hs, W1, (two && W1 > 0) ? 1 : 0, vec_out, stride, fs0, fsh);
+    if (check_launch(c, "k_pyr_l0")) return -1;
+  }
+  if (two && (long)W1 * H1 > 0) {
+    TimedScope ts(c, T_L1, st, F);
+    const int vec = (W1 % 4 == 0 && W1 >= 8) ? 1 : 0;
+    dim3 grid((W1 + l1::TW - 1) / l1::TW, (H1 + l1::TH - 1) / l1::TH, F);
+    hipLaunchKernelGGL(k_pyr_l1, grid, dim3(l1::NT), 0, st, K.hs, W1, H, H1, T, vec, K.lv[1].img, K.lv[1].gx,
+                       K.lv[1].gy, fsh, fs1);
+    if (check_launch(c, "k_pyr_l1")) return -1;
+  }
+  return 0;
 }
 
 }  // namespace
@@ -1197,6 +1414,18 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
     if (c->h_u8[i]) hipHostFree(c->h_u8[i]);
     if (c->u8_done[i]) hipEventDestroy(c->u8_done[i]);
     hipFree(c->d_tmp[i]);
+  }
+  for (auto &K : c->bank) {
+    for (auto &L : K.lv) {
+      hipFree(L.img);
+      hipFree(L.gx);
+      hipFree(L.gy);
+    }
+    hipFree(K.hs);
+  }
+  for (int k = 0; k < 3; ++k) {
+    if (c->ev_bbuilt[k]) hipEventDestroy(c->ev_bbuilt[k]);
+    if (c->ev_bfree[k]) hipEventDestroy(c->ev_bfree[k]);
   }
   hipFree(c->d_hs);
   hipFree(c->d_fx);
@@ -1271,13 +1500,14 @@ static int build_pyramid_on(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, co
 KLT_API int klt_hip_build_pyramid(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d,
                                   const unsigned char *frame, long pitch, int buf) {
   if (!c) return fail(c, "build_pyramid: null context");
+  if (s < 0 || s >= KLT_HIP_MAX_SLOTS) return fail(c, "build_pyramid: bad slot %d", s);
   return build_pyramid_on(c, s, d, frame, pitch, buf, c->stream);
 }
 
 static int build_pyramid_on(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const unsigned char *frame,
                             long pitch, int buf, hipStream_t st) {
   if (!c || !d) return fail(c, "build_pyramid: null argument");
-  if (s < 0 || s >= KLT_HIP_MAX_SLOTS) return fail(c, "build_pyramid: bad slot %d", s);
+  if (s < 0 || s >= KLT_HIP_MAX_SLOTS + 2) return fail(c, "build_pyramid: bad slot %d", s);
   if (d->nlevels < 1 || d->nlevels > KLT_HIP_MAX_LEVELS) return fail(c, "bad nlevels %d", d->nlevels);
   if (d->nlevels > 1 && d->subsampling < 2) return fail(c, "bad subsampling %d", d->subsampling);
   for (const klt_hip_taps *t : {&d->smooth, &d->pyr, &d->grad_gauss, &d->grad_deriv})
@@ -1305,6 +1535,11 @@ KLT_API int klt_hip_set_path(klt_hip_ctx *c, int force_generic) {
   if (!c) return -1;
   c->force_generic = force_generic != 0;
   return 0;
+}
+
+KLT_API int klt_hip_fused_path(klt_hip_ctx *c, const klt_hip_pyr_desc *d) {
+  if (!c || !d) return fail(c, "fused_path: null argument");
+  return fused_ok(d) && !c->force_generic ? 1 : 0;
 }
 
 KLT_API int klt_hip_pyramid_path(klt_hip_ctx *c, int s) {
@@ -1343,36 +1578,15 @@ KLT_API int klt_hip_track(klt_hip_ctx *c, int s1, int s2, const klt_hip_track_de
   if (A.nlev < 1 || A.nlev != B.nlev) return fail(c, "track: slots not built / level mismatch");
   for (int l = 0; l < A.nlev; ++l)
     if (A.lv[l].w != B.lv[l].w || A.lv[l].h != B.lv[l].h) return fail(c, "track: slot size mismatch");
+  if (check_window(c, d)) return -1;
   const int npx = d->window_width * d->window_height;
-  if (d->window_width < 1 || d->window_height < 1 || npx > 16 * kWave)
-    return fail(c, "track: window %dx%d unsupported (max %d pixels)", d->window_width, d->window_height,
-                16 * kWave);
   if (n <= 0) return 0;
   if (use_device(c)) return -1;
   TrkArgs a;
-  memset(&a, 0, sizeof a);
+  fill_trk_args(d, A.nlev, A.ss, A.lv[0].w, A.lv[0].h, a);
   for (int l = 0; l < A.nlev; ++l) {
     a.A[l] = {A.lv[l].img, A.lv[l].gx, A.lv[l].gy, A.lv[l].w, A.lv[l].h};
     a.B[l] = {B.lv[l].img, B.lv[l].gx, B.lv[l].gy, B.lv[l].w, B.lv[l].h};
-  }
-  a.nlev = A.nlev;
-  a.ss = (float)A.ss;
-  a.ww = d->window_width;
-  a.wh = d->window_height;
-  a.max_it = d->max_iterations;
-  a.min_det = d->min_determinant;
-  a.min_disp = d->min_displacement;
-  a.max_res = d->max_residue;
-  a.step = d->step_factor;
-  a.borderx = d->borderx;
-  a.bordery = d->bordery;
-  a.ncols = A.lv[0].w;
-  a.nrows = A.lv[0].h;
-  a.li = d->lighting_insensitive;
-  {
-    int rp = (npx + 3) & ~3;  // 16-byte rows with an odd slot count: distinct banks per sum
-    if (((rp / 4) & 1) == 0) rp += 4;
-    a.red_pitch = rp;
   }
 
   float *x_d = x, *y_d = y;
@@ -1453,6 +1667,171 @@ KLT_API int klt_hip_track_sequence(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, c
     if (klt_hip_track(c, prev, next, td, x, y, val, n, 1)) return -1;
     HIPCHK(c, hipEventRecord(c->ev_free[prev], track_stream));
     *cur_slot = next;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// batched frames: pyramids of `chunk` frames per pair of launches into one of
+// three banks on the pyramid stream, one k_track_frames launch per chunk on
+// the tracking stream.  Bank k is rebuilt only after the chunk that used its
+// last frame as the previous pyramid has been tracked (ev_bfree[k]).
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int kSeedSlot = KLT_HIP_MAX_SLOTS, kScratchSlot = KLT_HIP_MAX_SLOTS + 1;
+
+TrkLevel prev_level(klt_hip_ctx *c, int l) {
+  if (c->prev.bank < 0) {
+    const Level &L = c->slot[kSeedSlot].lv[l];
+    return TrkLevel{L.img, L.gx, L.gy, L.w, L.h};
+  }
+  const Level &L = c->bank[c->prev.bank].lv[l];
+  const long off = (long)c->prev.frame * L.w * L.h;
+  return TrkLevel{L.img + off, L.gx + off, L.gy + off, L.w, L.h};
+}
+
+bool bank_fits(const Bank &K, const klt_hip_pyr_desc *d, int F) {
+  if (K.nlev != d->nlevels) return false;
+  int w = d->ncols, h = d->nrows;
+  for (int l = 0; l < d->nlevels; ++l) {
+    const Level &L = K.lv[l];
+    if (L.w != w || L.h != h || !L.img || L.cap < (size_t)(w > 0 ? w : 1) * (h > 0 ? h : 1) * F) return false;
+    w /= K.ss;
+    h /= K.ss;
+  }
+  if (d->nlevels == 2 && K.hs_cap < (size_t)(K.lv[1].w > 0 ? K.lv[1].w : 1) * d->nrows * F) return false;
+  return true;
+}
+
+int copy_level_planes(klt_hip_ctx *c, const Level &from, float *img, float *gx, float *gy, hipStream_t st) {
+  const size_t b = sizeof(float) * (size_t)from.w * from.h;
+  if (!b) return 0;
+  HIPCHK(c, hipMemcpyAsync(img, from.img, b, hipMemcpyDeviceToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(gx, from.gx, b, hipMemcpyDeviceToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(gy, from.gy, b, hipMemcpyDeviceToDevice, st));
+  return 0;
+}
+}  // namespace
+
+KLT_API int klt_hip_frames_begin(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const unsigned char *frame,
+                                 long pitch) {
+  if (!c || !pd || !frame) return fail(c, "frames_begin: null argument");
+  if (use_device(c)) return -1;
+  if (build_pyramid_on(c, kSeedSlot, pd, frame, pitch, 0, c->stream)) return -1;
+  c->prev = PrevRef{-1, 0};
+  c->frames_ready = true;
+  return 0;
+}
+
+KLT_API int klt_hip_track_frames(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
+                                 const unsigned char *frames, long pitch, long stride, int nframes, int chunk,
+                                 float *x, float *y, int *val, int n, float *tab_x, float *tab_y, int *tab_val,
+                                 long tab_stride) {
+  if (!c || !pd || !td) return fail(c, "track_frames: null argument");
+  if (!c->frames_ready) return fail(c, "track_frames: no previous pyramid (call klt_hip_frames_begin)");
+  if (nframes < 0 || chunk < 1 || n < 0) return fail(c, "track_frames: bad nframes/chunk/n");
+  if (nframes > 0 && !frames) return fail(c, "track_frames: null frames");
+  if (n > 0 && (!x || !y || !val)) return fail(c, "track_frames: null feature arrays");
+  const int ntab = (tab_x != nullptr) + (tab_y != nullptr) + (tab_val != nullptr);
+  if (ntab != 0 && ntab != 3) return fail(c, "track_frames: give all three table arrays or none");
+  if (ntab && tab_stride < n) return fail(c, "track_frames: table stride %ld < n %d", tab_stride, n);
+  if (pitch < pd->ncols) return fail(c, "track_frames: pitch %ld < ncols %d", pitch, pd->ncols);
+  if (check_window(c, td)) return -1;
+  {
+    const TrkLevel p0 = prev_level(c, 0);
+    int nl = c->prev.bank < 0 ? c->slot[kSeedSlot].nlev : c->bank[c->prev.bank].nlev;
+    if (p0.w != pd->ncols || p0.h != pd->nrows || nl != pd->nlevels)
+      return fail(c, "track_frames: frames are %dx%d/%d levels, previous pyramid %dx%d/%d", pd->ncols,
+                  pd->nrows, pd->nlevels, p0.w, p0.h, nl);
+  }
+  if (nframes == 0) return 0;
+  if (use_device(c)) return -1;
+  if (!c->pstream) {
+    HIPCHK(c, hipStreamCreateWithFlags(&c->pstream, hipStreamNonBlocking));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
+    for (int k = 0; k < 3; ++k) {
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_built[k], hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_free[k], hipEventDisableTiming));
+    }
+  }
+  if (!c->ev_bbuilt[0])
+    for (int k = 0; k < 3; ++k) {
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_bbuilt[k], hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_bfree[k], hipEventDisableTiming));
+    }
+  const int F = chunk < nframes ? chunk : nframes;
+  // banks hold `chunk` frames whatever this call's length, so a short first
+  // call does not force a reallocation (and a drain) in the next one
+  if (!(bank_fits(c->bank[0], pd, chunk) && bank_fits(c->bank[1], pd, chunk) &&
+        bank_fits(c->bank[2], pd, chunk))) {
+    // (re)allocation: drain both streams; a previous pyramid living in a bank
+    // moves to the seed slot first
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->pstream));
+    if (c->prev.bank >= 0) {
+      if (ensure_slot(c, kSeedSlot, pd)) return -1;
+      for (int l = 0; l < pd->nlevels; ++l) {
+        const TrkLevel p = prev_level(c, l);
+        Level from;
+        from.w = p.w;
+        from.h = p.h;
+        from.img = const_cast<float *>(p.img);
+        from.gx = const_cast<float *>(p.gx);
+        from.gy = const_cast<float *>(p.gy);
+        const Level &to = c->slot[kSeedSlot].lv[l];
+        if (copy_level_planes(c, from, to.img, to.gx, to.gy, c->stream)) return -1;
+      }
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      c->prev = PrevRef{-1, 0};
+    }
+    for (auto &K : c->bank)
+      if (ensure_bank(c, K, pd, chunk)) return -1;
+  }
+  // the pyramid stream starts behind everything already queued on the tracking stream
+  HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
+  HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_start, 0));
+  const bool fz = fused_ok(pd) && !c->force_generic;
+  TrkArgs a;
+  fill_trk_args(td, pd->nlevels, pd->nlevels > 1 ? pd->subsampling : 1, pd->ncols, pd->nrows, a);
+  for (int j0 = 0; j0 < nframes; j0 += F) {
+    const int Fc = F < nframes - j0 ? F : nframes - j0;
+    const int bi = c->bank_next;
+    c->bank_next = (bi + 1) % 3;
+    Bank &K = c->bank[bi];
+    const unsigned char *src = frames + (long)j0 * stride;
+    HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_bfree[bi], 0));
+    if (fz) {
+      if (build_fused_bank(c, K, pd, src, pitch, stride, Fc, c->pstream)) return -1;
+    } else {
+      for (int f = 0; f < Fc; ++f) {
+        if (build_pyramid_on(c, kScratchSlot, pd, src + (long)f * stride, pitch, 0, c->pstream)) return -1;
+        for (int l = 0; l < pd->nlevels; ++l) {
+          const Level &L = c->slot[kScratchSlot].lv[l];
+          const long off = (long)f * L.w * L.h;
+          if (copy_level_planes(c, L, K.lv[l].img + off, K.lv[l].gx + off, K.lv[l].gy + off, c->pstream))
+            return -1;
+        }
+      }
+    }
+    HIPCHK(c, hipEventRecord(c->ev_bbuilt[bi], c->pstream));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_bbuilt[bi], 0));
+    TrkFramesArgs b;
+    memset(&b, 0, sizeof b);
+    for (int l = 0; l < pd->nlevels; ++l) {
+      a.A[l] = prev_level(c, l);
+      a.B[l] = TrkLevel{K.lv[l].img, K.lv[l].gx, K.lv[l].gy, K.lv[l].w, K.lv[l].h};
+      b.lfs[l] = (long)K.lv[l].w * K.lv[l].h;
+    }
+    b.nframes = Fc;
+    if (ntab) {
+      b.tx = tab_x + (long)j0 * tab_stride;
+      b.ty = tab_y + (long)j0 * tab_stride;
+      b.tv = tab_val + (long)j0 * tab_stride;
+      b.tstride = tab_stride;
+    }
+    if (n > 0 && track_frames_launch(c, c->stream, td, a, b, x, y, val, n)) return -1;
+    if (c->prev.bank >= 0) HIPCHK(c, hipEventRecord(c->ev_bfree[c->prev.bank], c->stream));
+    c->prev = PrevRef{bi, Fc - 1};
   }
   return 0;
 }
@@ -1559,6 +1938,10 @@ KLT_API int klt_hip_get_timing(klt_hip_ctx *c, klt_hip_timing *out) {
   out->ms_eigen = ms[T_EIG];
   out->n_generic = cnt[T_GEN];
   out->ms_generic = ms[T_GEN];
+  out->frames_pyr_l0 = c->frames_timed[T_L0];
+  out->frames_pyr_l1 = c->frames_timed[T_L1];
+  out->frames_track = c->frames_timed[T_TRACK];
+  for (auto &f : c->frames_timed) f = 0;
   return 0;
 }
 

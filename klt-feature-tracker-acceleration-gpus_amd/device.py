@@ -39,7 +39,8 @@ class Timing(C.Structure):
     _fields_ = [("n_pyr_l0", C.c_int), ("n_pyr_l1", C.c_int), ("n_track", C.c_int),
                 ("n_eigen", C.c_int), ("n_generic", C.c_int), ("ms_pyr_l0", C.c_double),
                 ("ms_pyr_l1", C.c_double), ("ms_track", C.c_double), ("ms_eigen", C.c_double),
-                ("ms_generic", C.c_double)]
+                ("ms_generic", C.c_double), ("frames_pyr_l0", C.c_long), ("frames_pyr_l1", C.c_long),
+                ("frames_track", C.c_long)]
 
 
 V = C.c_void_p
@@ -58,6 +59,7 @@ DEVICE_PROTOS = {
     "klt_hip_upload_frame": (C.c_int, [V, C.c_int, V, C.c_int, C.c_int]),
     "klt_hip_build_pyramid": (C.c_int, [V, C.c_int, C.POINTER(PyrDesc), V, C.c_long, C.c_int]),
     "klt_hip_pyramid_path": (C.c_int, [V, C.c_int]),
+    "klt_hip_fused_path": (C.c_int, [V, C.POINTER(PyrDesc)]),
     "klt_hip_set_path": (C.c_int, [V, C.c_int]),
     "klt_hip_level_dims": (C.c_int, [V, C.c_int, C.c_int, IP, IP]),
     "klt_hip_download_level": (C.c_int, [V, C.c_int, C.c_int, C.c_int, V]),
@@ -65,6 +67,9 @@ DEVICE_PROTOS = {
     "klt_hip_track": (C.c_int, [V, C.c_int, C.c_int, C.POINTER(TrackDesc), V, V, V, C.c_int, C.c_int]),
     "klt_hip_track_sequence": (C.c_int, [V, C.POINTER(PyrDesc), C.POINTER(TrackDesc), V, C.c_long,
                                          C.c_long, C.c_int, C.c_int, V, V, V, C.c_int, IP]),
+    "klt_hip_frames_begin": (C.c_int, [V, C.POINTER(PyrDesc), V, C.c_long]),
+    "klt_hip_track_frames": (C.c_int, [V, C.POINTER(PyrDesc), C.POINTER(TrackDesc), V, C.c_long, C.c_long,
+                                       C.c_int, C.c_int, V, V, V, C.c_int, V, V, V, C.c_long]),
     "klt_hip_min_eigen": (C.c_int, [V, C.c_int, C.POINTER(SelectDesc), V, IP, IP]),
     "klt_hip_synth_frames": (C.c_int, [V, C.c_ulonglong, C.c_int, C.c_int, C.c_int, C.c_int, V,
                                        C.c_long, C.c_long]),

@@ -218,3 +218,109 @@ def test_pipelined_generic_path_vs_oracle(gpu, oracle):
     gpu.KLTFreeTrackingContext(tc)
     X, Y, V = OracleTracker(oracle, p).harness(frames, 200, 7, first=frames[0])
     assert np.array_equal(x.view(np.int32), X[:, 5].view(np.int32)) and np.array_equal(v, V[:, 5])
+
+
+def batch_sequence(gpu, frames, nfeat, chunks, setup=None, calls=None):
+    """Select on frames[0], then klt_hip_frames_begin + klt_hip_track_frames over
+    frames[1:] (split into `calls` pieces, one chunk size per call), returning
+    the device feature table: row j = the list after frame j+1."""
+    from kltabi import fl_to_arrays, u8ptr
+    from kltamd.device import D2H, H2D, PyrDesc, TrackDesc, check
+    h, w = frames[0].shape
+    tc = gpu.KLTCreateTrackingContext()
+    tc.contents.sequentialMode = 1
+    if setup:
+        setup(tc.contents)
+    ctx = gpu.klt_amd_device_context(tc)
+    fl = gpu.KLTCreateFeatureList(nfeat)
+    gpu.KLTSelectGoodFeatures(tc, u8ptr(np.ascontiguousarray(frames[0])), w, h, fl)
+    x, y, v = fl_to_arrays(fl)
+    gpu.KLTFreeFeatureList(fl)
+    stack = np.ascontiguousarray(np.stack(frames))
+    T = len(frames) - 1
+    dfr = gpu.klt_hip_malloc(ctx, stack.nbytes)
+    dx, dy, dv = (gpu.klt_hip_malloc(ctx, 4 * nfeat) for _ in range(3))
+    tx, ty, tv = (gpu.klt_hip_malloc(ctx, 4 * nfeat * T) for _ in range(3))
+    check(gpu, ctx, gpu.klt_hip_memcpy(ctx, dfr, stack.ctypes.data, stack.nbytes, H2D), "h2d")
+    for d, a in ((dx, x), (dy, y), (dv, v)):
+        check(gpu, ctx, gpu.klt_hip_memcpy(ctx, d, a.ctypes.data, a.nbytes, H2D), "h2d")
+    pd, td = PyrDesc(), TrackDesc()
+    gpu.klt_amd_pyr_desc(tc, w, h, tc.contents.nPyramidLevels, 1, C.byref(pd))
+    gpu.klt_amd_track_desc(tc, C.byref(td))
+    check(gpu, ctx, gpu.klt_hip_frames_begin(ctx, C.byref(pd), dfr, w), "begin")
+    calls = calls or [T]
+    assert sum(calls) == T and len(chunks) == len(calls)
+    j0 = 0
+    for nf, ch in zip(calls, chunks):
+        off = 4 * nfeat * j0
+        check(gpu, ctx, gpu.klt_hip_track_frames(ctx, C.byref(pd), C.byref(td), dfr + (1 + j0) * w * h, w, w * h,
+                                                 nf, ch, dx, dy, dv, nfeat, tx + off, ty + off, tv + off,
+                                                 nfeat), "frames")
+        j0 += nf
+    X = np.empty((T, nfeat), np.float32)
+    Y = np.empty((T, nfeat), np.float32)
+    V = np.empty((T, nfeat), np.int32)
+    for d, a in ((tx, X), (ty, Y), (tv, V)):
+        check(gpu, ctx, gpu.klt_hip_memcpy(ctx, a.ctypes.data, d, a.nbytes, D2H), "d2h")
+    for d, a in ((dx, x), (dy, y), (dv, v)):
+        check(gpu, ctx, gpu.klt_hip_memcpy(ctx, a.ctypes.data, d, a.nbytes, D2H), "d2h")
+    for d in (dfr, dx, dy, dv, tx, ty, tv):
+        gpu.klt_hip_free(ctx, d)
+    gpu.KLTFreeTrackingContext(tc)
+    assert np.array_equal(X[-1], x) and np.array_equal(V[-1], v)  # final list == last table row
+    return X, Y, V
+
+
+def assert_table_equal(X, Y, V, OX, OY, OV):
+    T = X.shape[0]
+    for j in range(T):
+        assert np.array_equal(V[j], OV[:, j]), f"val differs at frame {j + 1}"
+        assert np.array_equal(X[j].view(np.int32), OX[:, j].view(np.int32)), f"x differs at frame {j + 1}"
+        assert np.array_equal(Y[j].view(np.int32), OY[:, j].view(np.int32)), f"y differs at frame {j + 1}"
+
+
+@pytest.mark.parametrize("chunks,calls", [([1], None), ([4], None), ([5], None), ([64], None),
+                                          ([2, 7], [3, 8])])
+def test_batched_frames_vs_oracle(gpu, oracle, chunks, calls):
+    frames = synth(gpu, 5150, 640, 480, 12)
+    X, Y, V = batch_sequence(gpu, frames, 1000, chunks, calls=calls)
+    OX, OY, OV = OracleTracker(oracle).harness(frames, 1000, 12, first=frames[0])
+    assert_table_equal(X, Y, V, OX, OY, OV)
+
+
+def test_batched_frames_odd_size_and_1080p(gpu, oracle):
+    frames = synth(gpu, 333, 333, 251, 9)
+    X, Y, V = batch_sequence(gpu, frames, 300, [3])
+    assert_table_equal(X, Y, V, *OracleTracker(oracle).harness(frames, 300, 9, first=frames[0]))
+    frames = synth(gpu, 1080, 1920, 1080, 6)
+    X, Y, V = batch_sequence(gpu, frames, 5000, [16])
+    assert_table_equal(X, Y, V, *OracleTracker(oracle).harness(frames, 5000, 6, first=frames[0]))
+
+
+def test_batched_frames_generic_path(gpu, oracle):
+    """Non-default window: pyramids come from the generic kernels, copied into the bank."""
+    frames = synth(gpu, 98, 333, 251, 8)
+
+    def setup(t):
+        t.window_width = t.window_height = 9
+
+    X, Y, V = batch_sequence(gpu, frames, 200, [3], setup)
+    tc = gpu.KLTCreateTrackingContext()
+    setup(tc.contents)
+    p = OracleParams.from_tc(tc.contents)
+    gpu.KLTFreeTrackingContext(tc)
+    assert_table_equal(X, Y, V, *OracleTracker(oracle, p).harness(frames, 200, 8, first=frames[0]))
+
+
+def test_batched_frames_errors(gpu):
+    from kltamd.device import PyrDesc, TrackDesc
+    tc = gpu.KLTCreateTrackingContext()
+    ctx = gpu.klt_amd_device_context(tc)
+    pd, td = PyrDesc(), TrackDesc()
+    gpu.klt_amd_pyr_desc(tc, 64, 48, tc.contents.nPyramidLevels, 1, C.byref(pd))
+    gpu.klt_amd_track_desc(tc, C.byref(td))
+    # no klt_hip_frames_begin yet
+    assert gpu.klt_hip_track_frames(ctx, C.byref(pd), C.byref(td), None, 64, 64 * 48, 0, 1, None, None, None,
+                                    0, None, None, None, 0) < 0
+    assert b"frames_begin" in gpu.klt_hip_last_error(ctx)
+    gpu.KLTFreeTrackingContext(tc)

@@ -27,7 +27,8 @@ sys.path.insert(0, str(ROOT))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["pyr", "track"])
+    ap.add_argument("mode", choices=["pyr", "track", "frames"])
+    ap.add_argument("--chunk", type=int, default=16, help="frames: frames per batch")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--features", type=int, default=5000)
@@ -88,6 +89,57 @@ def main():
         out.update({"k_pyr_l0_us": l0, "k_pyr_l1_us": l1, "generic_us": gen, "wall_us_per_frame": 1e6 * wall / a.reps,
                     "pass_GBps": byts / (pass_us * 1e-6) / 1e9, "frac_8TBs": byts / (pass_us * 1e-6) / 8e12,
                     "gpix_s": px / (pass_us * 1e-6) / 1e9})
+    elif a.mode == "frames":
+        # batched sequence: select on frame 0, track frames 1..nf-1 in chunks
+        h0 = np.empty((H, W), np.uint8)
+        lib.klt_synth_frame(1080, 0, W, H, h0.ctypes.data)
+        fl = lib.KLTCreateFeatureList(a.features)
+        lib.KLTSelectGoodFeatures(tc, h0.ctypes.data_as(kltamd.abi.U8P), W, H, fl)
+        n = a.features
+        xs = np.array([fl.contents.feature[k].contents.x for k in range(n)], np.float32)
+        ys = np.array([fl.contents.feature[k].contents.y for k in range(n)], np.float32)
+        vs = np.array([fl.contents.feature[k].contents.val for k in range(n)], np.int32)
+        lib.KLTFreeFeatureList(fl)
+        d = [lib.klt_hip_malloc(ctx, 4 * n) for _ in range(3)]
+        d0 = [lib.klt_hip_malloc(ctx, 4 * n) for _ in range(3)]
+        for dd, arr in zip(d0, (xs, ys, vs)):
+            check(lib, ctx, lib.klt_hip_memcpy(ctx, dd, arr.ctypes.data, arr.nbytes, H2D), "h2d")
+        for dd, ss in zip(d, d0):
+            check(lib, ctx, lib.klt_hip_memcpy(ctx, dd, ss, 4 * n, D2D), "d2d")
+        check(lib, ctx, lib.klt_hip_frames_begin(ctx, C.byref(pd), C.c_void_p(frames), W), "begin")
+        T = nf - 1
+        warm = min(T, 2 * a.chunk)
+        check(lib, ctx, lib.klt_hip_track_frames(ctx, C.byref(pd), C.byref(td), C.c_void_p(frames + W * H), W,
+                                                 W * H, warm, a.chunk, d[0], d[1], d[2], n, None, None, None,
+                                                 0), "warm")
+        def rep():
+            # restart from the seed frame and the selected features
+            for dd, ss in zip(d, d0):
+                check(lib, ctx, lib.klt_hip_memcpy(ctx, dd, ss, 4 * n, D2D), "d2d")
+            check(lib, ctx, lib.klt_hip_frames_begin(ctx, C.byref(pd), C.c_void_p(frames), W), "begin")
+            check(lib, ctx, lib.klt_hip_track_frames(ctx, C.byref(pd), C.byref(td), C.c_void_p(frames + W * H),
+                                                     W, W * H, T, a.chunk, d[0], d[1], d[2], n, None, None,
+                                                     None, 0), "frames")
+
+        lib.klt_hip_sync(ctx)
+        t0 = time.perf_counter()
+        for r in range(a.reps):
+            rep()
+        lib.klt_hip_sync(ctx)
+        wall = time.perf_counter() - t0
+        done = a.reps * T
+        lib.klt_hip_set_timing(ctx, 1)  # one more pass with per-launch events
+        rep()
+        tm = Timing()
+        check(lib, ctx, lib.klt_hip_get_timing(ctx, C.byref(tm)), "timing")
+        vv = np.empty(n, np.int32)
+        check(lib, ctx, lib.klt_hip_memcpy(ctx, vv.ctypes.data, d[2], 4 * n, 2), "d2h")
+        out.update({"features": n, "chunk": a.chunk, "frames": done, "fps_wall": done / wall,
+                    "us_per_frame_wall": 1e6 * wall / done,
+                    "l0_us_per_frame": 1e3 * tm.ms_pyr_l0 / max(tm.frames_pyr_l0, 1),
+                    "l1_us_per_frame": 1e3 * tm.ms_pyr_l1 / max(tm.frames_pyr_l1, 1),
+                    "track_us_per_frame": 1e3 * tm.ms_track / max(tm.frames_track, 1),
+                    "status_hist": {int(k): int(c) for k, c in zip(*np.unique(vv, return_counts=True))}})
     else:
         h0 = np.empty((H, W), np.uint8)
         lib.klt_synth_frame(1080, 0, W, H, h0.ctypes.data)
