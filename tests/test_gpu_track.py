@@ -324,3 +324,29 @@ def test_batched_frames_errors(gpu):
                                     0, None, None, None, 0) < 0
     assert b"frames_begin" in gpu.klt_hip_last_error(ctx)
     gpu.KLTFreeTrackingContext(tc)
+
+
+def test_reference_harness_relinked(gpu):
+    """The reference's own example3.c, compiled unchanged and linked against
+    libklt_amd.so (oracle/ref.mk -> oracle/_ref/example3_amd), reproduces the
+    reference's config-1 output byte for byte."""
+    import os
+    import subprocess
+    import tempfile
+    from pathlib import Path
+    exe = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "example3_amd"
+    if not exe.exists():
+        pytest.skip("oracle/_ref/example3_amd not built (needs /root/reference at build time)")
+    for n in (100, 150):
+        with tempfile.TemporaryDirectory() as d:
+            run = Path(d) / "a" / "b"
+            (run / "feat").mkdir(parents=True)
+            (Path(d) / "data").mkdir()
+            os.symlink(GOLDEN / "images_provided", Path(d) / "data" / "images_provided")
+            subprocess.run([str(exe), "images_provided", str(n), "10"], cwd=run, check=True, capture_output=True,
+                           timeout=120)
+            got = (run / "feat" / "features2.ft").read_bytes()
+            txt = (run / "feat" / "features2.txt").read_bytes()
+        want = (GOLDEN / f"config1_{n}x10.ft").read_bytes()
+        assert table_eq(parse_ft(got), parse_ft(want)), f"{n} features: .ft differs from the reference"
+        assert txt.splitlines()[:2] == (GOLDEN / f"config1_{n}x10.txt").read_bytes().splitlines()[:2]

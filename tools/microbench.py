@@ -27,8 +27,9 @@ sys.path.insert(0, str(ROOT))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["pyr", "track", "frames"])
+    ap.add_argument("mode", choices=["pyr", "track", "frames", "api"])
     ap.add_argument("--chunk", type=int, default=16, help="frames: frames per batch")
+    ap.add_argument("--pyr-only", action="store_true", help="frames: build the batched pyramids, track nothing")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--features", type=int, default=5000)
@@ -89,6 +90,27 @@ def main():
         out.update({"k_pyr_l0_us": l0, "k_pyr_l1_us": l1, "generic_us": gen, "wall_us_per_frame": 1e6 * wall / a.reps,
                     "pass_GBps": byts / (pass_us * 1e-6) / 1e9, "frac_8TBs": byts / (pass_us * 1e-6) / 8e12,
                     "gpix_s": px / (pass_us * 1e-6) / 1e9})
+    elif a.mode == "api":
+        # the public klt.h path: host u8 frames, KLTTrackFeatures per frame (PCIe inclusive)
+        nh = max(a.frames, 3)
+        host = []
+        for t in range(nh):
+            h = np.empty((H, W), np.uint8)
+            lib.klt_synth_frame(1080, t, W, H, h.ctypes.data)
+            host.append(h)
+        u8 = lambda z: z.ctypes.data_as(kltamd.abi.U8P)  # noqa: E731
+        fl = lib.KLTCreateFeatureList(a.features)
+        lib.KLTSelectGoodFeatures(tc, u8(host[0]), W, H, fl)
+        lib.KLTTrackFeatures(tc, u8(host[0]), u8(host[1]), W, H, fl)  # first call builds both pyramids
+        times = []
+        for t in range(2, nh):
+            t0 = time.perf_counter()
+            lib.KLTTrackFeatures(tc, u8(host[t - 1]), u8(host[t]), W, H, fl)
+            times.append(time.perf_counter() - t0)
+        live = sum(1 for k in range(a.features) if fl.contents.feature[k].contents.val >= 0)
+        lib.KLTFreeFeatureList(fl)
+        out.update({"features": a.features, "calls": len(times), "fps": len(times) / sum(times),
+                    "us_per_call_median": 1e6 * float(np.median(times)), "live_at_end": live})
     elif a.mode == "frames":
         # batched sequence: select on frame 0, track frames 1..nf-1 in chunks
         h0 = np.empty((H, W), np.uint8)
@@ -112,6 +134,9 @@ def main():
         check(lib, ctx, lib.klt_hip_track_frames(ctx, C.byref(pd), C.byref(td), C.c_void_p(frames + W * H), W,
                                                  W * H, warm, a.chunk, d[0], d[1], d[2], n, None, None, None,
                                                  0), "warm")
+        if a.pyr_only:
+            n = 0
+
         def rep():
             # restart from the seed frame and the selected features
             for dd, ss in zip(d, d0):
