@@ -102,6 +102,15 @@ int klt_hip_build_pyramid(klt_hip_ctx *ctx, int slot, const klt_hip_pyr_desc *de
 /* test hook: 1 forces the generic one-pass-per-launch path even when the
    fused kernels apply (they must agree bit for bit) */
 int klt_hip_set_path(klt_hip_ctx *ctx, int force_generic);
+/* tuning hook: features per wavefront for windows of <= 64 pixels (1, 2 or
+   4; 0 restores the default).  Results do not depend on it. */
+int klt_hip_set_track_group(klt_hip_ctx *ctx, int features_per_wave);
+/* tuning hook: 1 tracks features in input order; 0 (default) in row-band
+   order with each XCD given one band (L2 locality).  Results do not depend on it. */
+int klt_hip_set_track_order(klt_hip_ctx *ctx, int input_order);
+/* tuning hook: 0 disables the lane-patch gather of one-feature waves (default
+   1: on where (ww+1)*(wh+1) <= 64).  Results do not depend on it. */
+int klt_hip_set_track_patch(klt_hip_ctx *ctx, int on);
 /* 1 if pyramids for `desc` would be built by the fused gfx950 kernels, else 0 */
 int klt_hip_fused_path(klt_hip_ctx *ctx, const klt_hip_pyr_desc *desc);
 /* 1 if the slot was built by the fused gfx950 kernels, 0 generic, <0 invalid */

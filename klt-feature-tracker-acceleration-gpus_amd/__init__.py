@@ -12,6 +12,7 @@ There is no Python or CPU fallback: load() raises if the library is missing.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from pathlib import Path
 
 from . import abi, device  # noqa: F401
@@ -26,10 +27,14 @@ def load() -> C.CDLL:
     """Load libklt_amd.so once and attach every prototype."""
     global _lib
     if _lib is None:
-        if not LIB_PATH.exists():
-            raise ImportError(f"{LIB_PATH} is missing: build it with `make -C {PKG_DIR / 'csrc'}` "
+        path = LIB_PATH
+        alt = os.environ.get("KLT_AMD_LIB")  # tools only: e.g. the instrumented build lib/prof/
+        if alt:
+            path = Path(alt)
+        if not path.exists():
+            raise ImportError(f"{path} is missing: build it with `make -C {PKG_DIR / 'csrc'}` "
                               "(or __graft_entry__.build()); there is no CPU fallback")
-        lib = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
+        lib = C.CDLL(str(path), mode=C.RTLD_GLOBAL)
         abi.bind_klt(lib)
         device.bind_device(lib)
         _lib = lib

@@ -34,6 +34,12 @@
 namespace {
 
 constexpr int kWave = 64;
+#ifndef KLT_SUM_BATCH
+#define KLT_SUM_BATCH 4  // 16-byte LDS reads in flight per ordered-sum batch
+#endif
+#ifndef KLT_TRACK_WAVES
+#define KLT_TRACK_WAVES 1  // amdgpu_waves_per_eu floor for the tracker (1: compiler's choice)
+#endif
 constexpr int kBlock = 256;
 
 // status codes (klt.h:28-33)
@@ -599,17 +605,38 @@ struct TrkArgs {
 
 // _interpolate (trackFeatures.c:31-57); the clamp only guards addresses that
 // the window bounds test already excludes
-__device__ __forceinline__ float bilerp(const float *__restrict__ img, int w, int h, float x, float y) {
+// The corner offset and the four weights depend only on the position, so the
+// three planes of a pyramid level share them; the offset stays 32-bit so the
+// loads use a scalar plane base plus one vector offset.
+struct Bil {
+  unsigned off;  // corner index yt*w + xt
+  float w0, w1, w2, w3;
+};
+
+__device__ __forceinline__ Bil bil_at(int w, int h, float x, float y) {
   int xt = (int)x, yt = (int)y;
   const float ax = x - xt, ay = y - yt;
   xt = clampi(xt, 0, w - 2);
   yt = clampi(yt, 0, h - 2);
-  const float *p = img + (long)yt * w + xt;
-  return (1.0f - ax) * (1.0f - ay) * p[0] + ax * (1.0f - ay) * p[1] + (1.0f - ax) * ay * p[w] +
-         ax * ay * p[w + 1];
+  Bil b;
+  b.off = (unsigned)(yt * w + xt);
+  b.w0 = (1.0f - ax) * (1.0f - ay);
+  b.w1 = ax * (1.0f - ay);
+  b.w2 = (1.0f - ax) * ay;
+  b.w3 = ax * ay;
+  return b;
 }
 
-// unconditional gather, then a select: bilerp clamps its corner to the plane,
+// (1-ax)(1-ay)p00 + ax(1-ay)p01 + (1-ax)ay p10 + ax ay p11, left to right
+__device__ __forceinline__ float bil_sample(const float *__restrict__ P, const Bil &b, unsigned w) {
+  // 32-bit byte offsets (planes are < 4 GiB): scalar base + vector offset addressing
+  const char *base = reinterpret_cast<const char *>(P);
+  const float *p0 = reinterpret_cast<const float *>(base + (unsigned)(b.off * 4u));
+  const float *p1 = reinterpret_cast<const float *>(base + (unsigned)((b.off + w) * 4u));
+  return b.w0 * p0[0] + b.w1 * p0[1] + b.w2 * p1[0] + b.w3 * p1[1];
+}
+
+// unconditional gather, then a select: bil_at clamps its corner to the plane,
 // so lanes past the window read valid memory and the loads of all planes can
 // be in flight together (a guarded call makes the compiler branch per plane)
 __device__ __forceinline__ float sel(bool on, float v) { return on ? v : 0.0f; }
@@ -630,115 +657,336 @@ __device__ __forceinline__ float bcast(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
 
-// NS sequential sums over npx pixels; v[s][k] is the value of pixel lane+64k.
-// Sum s lives at red[s*rp ...] (rp/4 odd: the NS readers hit distinct bank
-// slots); lane s reads it back 16 bytes at a time and adds in pixel order.
-template <int NS, int PPL>
-__device__ __forceinline__ void exact_sums(const float (&v)[NS][PPL], float *red, int rp, int npx, int lane,
-                                           float (&out)[NS]) {
-  // the pad of the last 16-byte chunk is written as +0 and added without a
-  // guard: acc + (+0) == acc exactly, since an ordered sum from +0 is never -0
+// ---------------------------------------------------------------------------
+// batched frames: each feature is carried through a batch of frames
+// (the KLTTrackFeatures + KLTStoreFeatureList loop of example3.c:54-74 with
+// no replacement).  Frame j tracks pyramid j-1 -> j of the bank (j = 0: from
+// a.A, the pyramid before the batch); every feature is independent, so the
+// per-frame launch and its dependency bubble disappear.  Row j of the
+// optional feature table receives the list after frame j.
+// ---------------------------------------------------------------------------
+struct TrkFramesArgs {
+  long lfs[KLT_HIP_MAX_LEVELS];  // bank frame stride per level (floats)
+  int nframes;
+  const int *perm;  // processing order (slot -> feature), nullptr: identity
+  int xcd_per;      // > 0: blockIdx -> XCD-major order, this many blocks per XCD
+#ifdef KLT_TRACK_PROF
+  unsigned long long *prof;  // per wave: kProfN phase cycle counts (instrumented build only)
+#endif
+  float *tx, *ty;
+  int *tv;
+  long tstride;  // table row stride (elements); tx == nullptr: no table
+};
+
+__device__ __forceinline__ TrkLevel at_frame(const TrkLevel &L, long off) {
+  return TrkLevel{L.img + off, L.gx + off, L.gy + off, L.w, L.h};
+}
+
+// ---------------------------------------------------------------------------
+// Grouped tracker: G features per wave, 64/G lanes each (PPL pixels per lane).
+// The per-pixel work is the same per feature as one feature per wave, but the
+// wave-wide parts -- the 49-add ordered-sum chain, the 2x2 solve, the window
+// tests, loop control -- are shared by G features.  Features of a wave iterate
+// in lock step; a converged feature's lanes are masked until the wave's last
+// feature finishes the level.  Results are bit-identical: each feature's sums
+// are still formed by one lane in pixel order.
+// ---------------------------------------------------------------------------
+// Instrumented build (make prof): per-wave shader-clock cycles per phase
+#ifdef KLT_TRACK_PROF
+constexpr int kProfN = 10;  // 0 gather+interp, 1 sums, 2 solve, 3 residue, 4 frame, 5 iterations, 6 passes, 7 wall ticks, 8/9 wall start/end
+struct Prof {
+  unsigned long long c[kProfN] = {};
+};
+#define PROF_DECL Prof &prof,
+#define PROF_ARG prof,
+#define PROF_T(t) const unsigned long long t = clock64()
+#define PROF_ADD(k, t0) prof.c[k] += clock64() - (t0)
+#define PROF_INC(k) prof.c[k] += 1
+#else
+#define PROF_DECL
+#define PROF_ARG
+#define PROF_T(t)
+#define PROF_ADD(k, t0)
+#define PROF_INC(k)
+#endif
+
+// Lane <-> window pixel map.  Default: pixel p = l + LG*k (l = lane in the
+// feature's lane group).  PATCH (G = PPL = 1, (ww+1)*(wh+1) <= 64): lanes
+// form a (ww+1)-wide patch, lane = j*(ww+1) + i holds pixel (i, j) of the
+// window for i < ww, j < wh; the extra column/row are the bilinear corners'
+// far side, so one 4-byte load per lane fetches every corner of every pixel.
+template <int G, int PPL, bool PATCH>
+struct GroupWin {
+  int oi[PPL], oj[PPL];
+  int p[PPL];  // pixel index in the reference's row-major order
+  bool on[PPL];
+  int pw;      // PATCH: patch row length ww+1
+  int ci, cj;  // PATCH: this lane's patch cell
+};
+
+template <int G, int PPL, bool PATCH>
+__device__ __forceinline__ GroupWin<G, PPL, PATCH> group_window(int ww, int wh, int lane) {
+  constexpr int LG = kWave / G;
+  const int l = lane % LG, npx = ww * wh, hw = ww / 2, hh = wh / 2;
+  GroupWin<G, PPL, PATCH> w;
+  w.pw = ww + 1;
+  if (PATCH) {
+    const int j = lane / (ww + 1), i = lane - j * (ww + 1);
+    w.ci = i;
+    w.cj = j;
+    w.on[0] = i < ww && j < wh;
+    w.p[0] = j * ww + i;
+    w.oi[0] = i - hw;
+    w.oj[0] = j - hh;
+    return w;
+  }
 #pragma unroll
   for (int k = 0; k < PPL; ++k) {
-    const int p = lane + kWave * k;
-    if (p < rp) {
+    const int p0 = l + LG * k;
+    w.on[k] = p0 < npx;
+    const int p = w.on[k] ? p0 : npx - 1;  // idle slots gather the last pixel's lines
+    const int jj = p / ww;
+    w.p[k] = p0;
+    w.oi[k] = p - jj * ww - hw;
+    w.oj[k] = jj - hh;
+  }
+  return w;
+}
+
+// NS ordered sums per feature.  Pixel p of sum s goes to red[(g*NS+s)*rp + p];
+// entries [npx, rp) of every row are zeroed once per kernel (zero_red) and
+// never written, so whole 16-byte chunks add exactly (acc + +0 == acc, an
+// ordered sum from +0 is never -0).  Lane g*NS+s then adds row g*NS+s in
+// pixel order: the reference's sequential float sum.
+template <int G, int NS, int PPL, bool PATCH>
+__device__ __forceinline__ void exact_sums_g(const GroupWin<G, PPL, PATCH> &w, const float (&v)[NS][PPL],
+                                             float *red, int rp, int npx, int lane, float (&out)[NS]) {
+  constexpr int LG = kWave / G;
+  const int g = lane / LG;
 #pragma unroll
-      for (int s = 0; s < NS; ++s) red[s * rp + p] = p < npx ? v[s][k] : 0.0f;
+  for (int k = 0; k < PPL; ++k) {
+    if (w.on[k]) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) red[(g * NS + s) * rp + w.p[k]] = v[s][k];
     }
   }
   lds_wave_sync();
   float acc = 0.0f;
-  if (lane < NS) {
-    // all reads issued before the first add: one LDS round trip, then the
-    // ordered chain of adds (batches of 8 chunks keep the registers bounded)
+  if (lane < G * NS) {
+    // B chunks per batch, read whole before the ordered adds; reads past the
+    // row's last chunk land in the next row or the buffer's tail pad, unused
     const float *r = red + lane * rp;
     const int nch = (npx + 3) >> 2;
-    constexpr int MAXCH = (kWave * PPL) / 4, B = 8;
-    for (int b0 = 0; b0 < MAXCH; b0 += B) {
-      if (b0 >= nch) break;
+    constexpr int B = KLT_SUM_BATCH;
+    for (int b0 = 0; b0 < nch; b0 += B) {
       f4 c[B];
 #pragma unroll
-      for (int k = 0; k < B; ++k) c[k] = (b0 + k < nch) ? ld4(r + 4 * (b0 + k)) : f4{0.0f, 0.0f, 0.0f, 0.0f};
+      for (int k = 0; k < B; ++k) c[k] = ld4(r + 4 * (b0 + k));
 #pragma unroll
       for (int k = 0; k < B; ++k) {
-        if (b0 + k >= nch) break;
-        acc += c[k].x;
-        acc += c[k].y;
-        acc += c[k].z;
-        acc += c[k].w;
+        if (b0 + k < nch) {
+          acc += c[k].x;
+          acc += c[k].y;
+          acc += c[k].z;
+          acc += c[k].w;
+        }
       }
     }
   }
+  if (G == 1) {
 #pragma unroll
-  for (int s = 0; s < NS; ++s) out[s] = bcast(acc, s);
+    for (int s = 0; s < NS; ++s) out[s] = bcast(acc, s);
+  } else {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) out[s] = __shfl(acc, g * NS + s);
+  }
   lds_wave_sync();
 }
 
-// fast mode: butterfly over the wave (not the reference's order)
-template <int NS, int PPL>
-__device__ __forceinline__ void tree_sums(const float (&v)[NS][PPL], int npx, int lane, float (&out)[NS]) {
+template <int G, int NS, int PPL, bool PATCH>
+__device__ __forceinline__ void tree_sums_g(const GroupWin<G, PPL, PATCH> &w, const float (&v)[NS][PPL],
+                                            float (&out)[NS]) {
+  constexpr int LG = kWave / G;
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     float acc = 0.0f;
 #pragma unroll
     for (int k = 0; k < PPL; ++k)
-      if (lane + kWave * k < npx) acc += v[s][k];
+      if (w.on[k]) acc += v[s][k];
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
+    for (int off = LG / 2; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
     out[s] = acc;
   }
 }
 
-template <int PPL, bool EXACT>
-__device__ int track_level(const TrkArgs &a, const TrkLevel &A, const TrkLevel &B, float x1, float y1,
-                           float &x2, float &y2, int lane, float *red) {
-  const int ww = a.ww, wh = a.wh, npx = ww * wh, hw = ww / 2, hh = wh / 2;
-  const int nc = A.w, nr = A.h;
-  int oi[PPL], oj[PPL];
-  bool on[PPL];
+template <int G, int NS, int PPL, bool PATCH, bool EXACT>
+__device__ __forceinline__ void sums_g(const GroupWin<G, PPL, PATCH> &w, const float (&v)[NS][PPL], float *red,
+                                       int rp, int npx, int lane, float (&out)[NS]) {
+  if (EXACT) exact_sums_g<G, NS, PPL, PATCH>(w, v, red, rp, npx, lane, out);
+  else tree_sums_g<G, NS, PPL, PATCH>(w, v, out);
+}
+
+// Bilinear samples of a level's planes for this lane's pixel(s).  PATCH: one
+// 4-byte load per lane and three lane shuffles per plane, used when every
+// pixel's integer corner is where the patch puts it (x + i can round across an
+// integer, moving one corner by one); otherwise the per-pixel gather.  Both
+// produce the same values.  All loads of a pass are issued before any result
+// is formed, so a pass costs one memory round trip.
+struct PatchPos {
+  bool ok;
+  unsigned off;  // byte offset of this lane's patch cell
+  float w0, w1, w2, w3;
+};
+
+template <int G, int PPL, bool PATCH>
+__device__ __forceinline__ PatchPos patch_pos(const GroupWin<G, PPL, PATCH> &w, int nc, int nr, float x, float y) {
+  PatchPos q;
+  const float xs = x + w.oi[0], ys = y + w.oj[0];
+  const int xt = (int)xs, yt = (int)ys;
+  const int X0 = __builtin_amdgcn_readlane(xt, 0), Y0 = __builtin_amdgcn_readlane(yt, 0);
+  q.ok = __builtin_amdgcn_ballot_w64(w.on[0] && !(xt == X0 + w.ci && yt == Y0 + w.cj)) == 0;
+  const float ax = xs - xt, ay = ys - yt;
+  q.w0 = (1.0f - ax) * (1.0f - ay);
+  q.w1 = ax * (1.0f - ay);
+  q.w2 = (1.0f - ax) * ay;
+  q.w3 = ax * ay;
+  const int cx = clampi(X0 + w.ci, 0, nc - 1), cy = clampi(Y0 + w.cj, 0, nr - 1);
+  q.off = (unsigned)(cy * nc + cx) * 4u;
+  return q;
+}
+
+__device__ __forceinline__ float patch_load(const float *P, const PatchPos &q) {
+  return *reinterpret_cast<const float *>(reinterpret_cast<const char *>(P) + q.off);
+}
+
+template <int G, int PPL, bool PATCH>
+__device__ __forceinline__ float patch_value(const GroupWin<G, PPL, PATCH> &w, const PatchPos &q, float v,
+                                             int lane) {
+  const int pw = w.pw;
+  const float v01 = __shfl(v, lane + 1), v10 = __shfl(v, lane + pw), v11 = __shfl(v, lane + pw + 1);
+  return sel(w.on[0], q.w0 * v + q.w1 * v01 + q.w2 * v10 + q.w3 * v11);
+}
+
+template <int G, int PPL, bool PATCH>
+__device__ __forceinline__ void gather_direct(const TrkLevel &L, const GroupWin<G, PPL, PATCH> &w, float x,
+                                              float y, bool grads, float (&im)[PPL], float (&gx)[PPL],
+                                              float (&gy)[PPL]) {
 #pragma unroll
   for (int k = 0; k < PPL; ++k) {
-    const int p0 = lane + kWave * k;
-    on[k] = p0 < npx;
-    const int p = on[k] ? p0 : npx - 1;  // idle lanes gather the last pixel's lines
-    const int jj = p / ww;
-    oi[k] = p - jj * ww - hw;
-    oj[k] = jj - hh;
+    const Bil q = bil_at(L.w, L.h, x + w.oi[k], y + w.oj[k]);
+    im[k] = sel(w.on[k], bil_sample(L.img, q, L.w));
+    if (grads) {
+      gx[k] = sel(w.on[k], bil_sample(L.gx, q, L.w));
+      gy[k] = sel(w.on[k], bil_sample(L.gy, q, L.w));
+    } else {
+      gx[k] = gy[k] = 0.0f;
+    }
   }
+}
 
-  // img1 samples do not move during the iterations: interpolate once
-  float a_im[PPL], a_gx[PPL], a_gy[PPL];
+// one pass: img2 planes at (x2, y2) (grads = false: img only) and, on a
+// level's first pass, the img1 planes at (x1, y1)
+template <int G, int PPL, bool PATCH>
+__device__ __forceinline__ void gather_pass(const TrkLevel &A, const TrkLevel &B, const GroupWin<G, PPL, PATCH> &w,
+                                            float x1, float y1, float x2, float y2, bool first, bool grads,
+                                            int lane, float (&a_im)[PPL], float (&a_gx)[PPL], float (&a_gy)[PPL],
+                                            float (&b_im)[PPL], float (&b_gx)[PPL], float (&b_gy)[PPL]) {
+  if constexpr (PATCH) {
+    const PatchPos qb = patch_pos(w, B.w, B.h, x2, y2);
+    const PatchPos qa = first ? patch_pos(w, A.w, A.h, x1, y1) : qb;
+    if (qb.ok && qa.ok) {
+      float vb0 = patch_load(B.img, qb), vb1 = 0.0f, vb2 = 0.0f, va0 = 0.0f, va1 = 0.0f, va2 = 0.0f;
+      if (grads) {
+        vb1 = patch_load(B.gx, qb);
+        vb2 = patch_load(B.gy, qb);
+      }
+      if (first) {
+        va0 = patch_load(A.img, qa);
+        va1 = patch_load(A.gx, qa);
+        va2 = patch_load(A.gy, qa);
+      }
+      b_im[0] = patch_value(w, qb, vb0, lane);
+      b_gx[0] = grads ? patch_value(w, qb, vb1, lane) : 0.0f;
+      b_gy[0] = grads ? patch_value(w, qb, vb2, lane) : 0.0f;
+      if (first) {
+        a_im[0] = patch_value(w, qa, va0, lane);
+        a_gx[0] = patch_value(w, qa, va1, lane);
+        a_gy[0] = patch_value(w, qa, va2, lane);
+      }
+      return;
+    }
+  }
+  gather_direct(B, w, x2, y2, grads, b_im, b_gx, b_gy);
+  if (first) gather_direct(A, w, x1, y1, true, a_im, a_gx, a_gy);
+}
+
+__device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+
+// One feature per wave (G == 1): per-feature state is wave-uniform; pinning it
+// to scalar registers keeps the vector register file for the window pixels.
+template <int G>
+__device__ __forceinline__ float uni(float v) {
+  if (G == 1) return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+  return v;
+}
+template <int G>
+__device__ __forceinline__ int uni(int v) {
+  if (G == 1) return __builtin_amdgcn_readfirstlane(v);
+  return v;
+}
+
+// _trackFeature (trackFeatures.c:381-486) for the G features of a wave at one
+// level.  Per-lane state is uniform within a feature's lane group; `live`
+// says whether the group's feature is tracked at this level.
+//
+// Latency layout: every global round trip gathers img2 at the current
+// position x2.  The img1 samples are gathered with the first of them, and the
+// residue uses the gather at the final position -- the one the next
+// iteration would have made -- so a level with k Newton steps costs k+1 round
+// trips instead of k+2.  The order of tests is the reference's: window test
+// at the top of each iteration and once after the loop (same x2, same test),
+// SMALL_DET ends the loop before x2 moves, residue only for TRACKED.
+template <int G, int PPL, bool PATCH, bool EXACT, bool LI>
+__device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, PATCH> &w, const TrkLevel &A,
+                             const TrkLevel &B, float x1, float y1, float &x2, float &y2, bool live, int lane,
+                             float *red) {
+  const int ww = a.ww, wh = a.wh, npx = ww * wh, hw = ww / 2, hh = wh / 2;
+  const int nc = A.w, nr = A.h;
+  const float n = (float)(ww * wh);
+
   const bool x1_out = window_out(x1, y1, hw, hh, nc, nr);
-  if (!x1_out) {
-#pragma unroll
-    for (int k = 0; k < PPL; ++k) {
-      const float xs = x1 + oi[k], ys = y1 + oj[k];
-      a_im[k] = sel(on[k], bilerp(A.img, nc, nr, xs, ys));
-      a_gx[k] = sel(on[k], bilerp(A.gx, nc, nr, xs, ys));
-      a_gy[k] = sel(on[k], bilerp(A.gy, nc, nr, xs, ys));
-    }
-  }
-
-  float dx = 0.0f, dy = 0.0f;
+  float a_im[PPL], a_gx[PPL], a_gy[PPL];
+  bool act = live;       // still iterating
+  bool fin = false;      // iterations over (converged or max_it): residue next
   int it = 0, status = kTracked;
-  do {
-    if (x1_out || window_out(x2, y2, hw, hh, nc, nr)) {
+  bool first = true;
+  while (true) {
+    // window test: top of an iteration, or the post-loop test for a finished one
+    if (act && ((first && x1_out) || window_out(x2, y2, hw, hh, nc, nr))) {
       status = kOOB;
-      break;
+      act = false;
     }
-    float b_im[PPL], gxs[PPL], gys[PPL], dif[PPL];
+    if (!wave_any(act)) break;
+    PROF_INC(6);
+    PROF_T(t_g0);
+    float b_im[PPL], b_gx[PPL], b_gy[PPL];
+    const bool grads = wave_any(act && !fin);  // a residue-only pass needs img2 alone
+    if (act) {  // img1 is sampled once per level, with the level's first img2 gather
+      gather_pass<G, PPL, PATCH>(A, B, w, x1, y1, x2, y2, first, grads, lane, a_im, a_gx, a_gy, b_im, b_gx,
+                                 b_gy);
+    } else {
 #pragma unroll
-    for (int k = 0; k < PPL; ++k) {
-      const float xs = x2 + oi[k], ys = y2 + oj[k];
-      b_im[k] = sel(on[k], bilerp(B.img, nc, nr, xs, ys));
-      const float bgx = sel(on[k], bilerp(B.gx, nc, nr, xs, ys));
-      const float bgy = sel(on[k], bilerp(B.gy, nc, nr, xs, ys));
-      gxs[k] = a_gx[k] + bgx;
-      gys[k] = a_gy[k] + bgy;
-      dif[k] = a_im[k] - b_im[k];
+      for (int k = 0; k < PPL; ++k) b_im[k] = b_gx[k] = b_gy[k] = 0.0f;
+      if (first) {
+#pragma unroll
+        for (int k = 0; k < PPL; ++k) a_im[k] = a_gx[k] = a_gy[k] = 0.0f;
+      }
     }
-    if (a.li) {
-      // gain/bias normalisation (trackFeatures.c:133-220)
+    first = false;
+
+    // gain/bias of the window pair (trackFeatures.c:133-220); also needed by the residue
+    float alpha = 1.0f, beta = 0.0f, alpha_g = 1.0f;
+    if (LI) {
       float mom[4][PPL], S[4];
 #pragma unroll
       for (int k = 0; k < PPL; ++k) {
@@ -747,82 +995,85 @@ __device__ int track_level(const TrkArgs &a, const TrkLevel &A, const TrkLevel &
         mom[2][k] = a_im[k] * a_im[k];
         mom[3][k] = b_im[k] * b_im[k];
       }
-      if (EXACT) exact_sums<4, PPL>(mom, red, a.red_pitch, npx, lane, S);
-      else tree_sums<4, PPL>(mom, npx, lane, S);
-      const float n = (float)(ww * wh);
-      const float alpha = (float)sqrt((double)((S[2] / n) / (S[3] / n)));
-      const float beta = S[0] / n - alpha * (S[1] / n);
-      const float alpha_g = (float)sqrt((double)((S[0] / n) / (S[1] / n)));
+      sums_g<G, 4, PPL, PATCH, EXACT>(w, mom, red, a.red_pitch, npx, lane, S);
+      alpha = (float)sqrt((double)((S[2] / n) / (S[3] / n)));
+      beta = S[0] / n - alpha * (S[1] / n);
+      alpha_g = (float)sqrt((double)((S[0] / n) / (S[1] / n)));
+    }
+
+    if (wave_any(act && fin)) {
+      // residue: mean |img1 - img2| over the window at the final position (:465-474)
+      PROF_T(t_r0);
+      float dif[1][PPL], S[1];
+      const bool res = act && fin;
 #pragma unroll
       for (int k = 0; k < PPL; ++k) {
-        dif[k] = a_im[k] - b_im[k] * alpha - beta;
-        const float xs = x2 + oi[k], ys = y2 + oj[k];
-        const float bgx = sel(on[k], bilerp(B.gx, nc, nr, xs, ys));
-        const float bgy = sel(on[k], bilerp(B.gy, nc, nr, xs, ys));
-        gxs[k] = a_gx[k] + bgx * alpha_g;
-        gys[k] = a_gy[k] + bgy * alpha_g;
+        const float d = LI ? (a_im[k] - b_im[k] * alpha - beta) : (a_im[k] - b_im[k]);
+        dif[0][k] = res ? fabsf(d) : 0.0f;
       }
+      sums_g<G, 1, PPL, PATCH, EXACT>(w, dif, red, a.red_pitch, npx, lane, S);
+      if (res) {
+        if (S[0] / n > a.max_res) status = kLargeResidue;
+        act = false;
+      }
+      PROF_ADD(3, t_r0);
     }
+    if (!wave_any(act)) break;
+
     float prod[5][PPL], S[5];
+    const bool step = act;  // groups in their residue pass are done by now
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
-      prod[0][k] = gxs[k] * gxs[k];
-      prod[1][k] = gxs[k] * gys[k];
-      prod[2][k] = gys[k] * gys[k];
-      prod[3][k] = dif[k] * gxs[k];
-      prod[4][k] = dif[k] * gys[k];
-    }
-    if (EXACT) exact_sums<5, PPL>(prod, red, a.red_pitch, npx, lane, S);
-    else tree_sums<5, PPL>(prod, npx, lane, S);
-    const float gxx = S[0], gxy = S[1], gyy = S[2];
-    const float ex = S[3] * a.step, ey = S[4] * a.step;
-    // _solveEquation (:293-307)
-    const float det = gxx * gyy - gxy * gxy;
-    if (det < a.min_det) {
-      status = kSmallDet;
-      break;
-    }
-    dx = (gyy * ex - gxy * ey) / det;
-    dy = (gxx * ey - gxy * ex) / det;
-    status = kTracked;
-    x2 += dx;
-    y2 += dy;
-    ++it;
-  } while ((fabsf(dx) >= a.min_disp || fabsf(dy) >= a.min_disp) && it < a.max_it);
-
-  if (window_out(x2, y2, hw, hh, nc, nr)) status = kOOB;
-
-  if (status == kTracked) {
-    // residue: mean |img1 - img2| over the window at the final position (:465-474)
-    float dif[1][PPL], S[1];
-    float alpha = 1.0f, beta = 0.0f;
-    float b_im[PPL];
-#pragma unroll
-    for (int k = 0; k < PPL; ++k)
-      b_im[k] = sel(on[k], bilerp(B.img, nc, nr, x2 + oi[k], y2 + oj[k]));
-    if (a.li) {
-      float mom[4][PPL], M[4];
-#pragma unroll
-      for (int k = 0; k < PPL; ++k) {
-        mom[0][k] = a_im[k];
-        mom[1][k] = b_im[k];
-        mom[2][k] = a_im[k] * a_im[k];
-        mom[3][k] = b_im[k] * b_im[k];
+      float gxs, gys, dif;
+      if (LI) {
+        dif = a_im[k] - b_im[k] * alpha - beta;
+        gxs = a_gx[k] + b_gx[k] * alpha_g;
+        gys = a_gy[k] + b_gy[k] * alpha_g;
+      } else {
+        dif = a_im[k] - b_im[k];
+        gxs = a_gx[k] + b_gx[k];
+        gys = a_gy[k] + b_gy[k];
       }
-      if (EXACT) exact_sums<4, PPL>(mom, red, a.red_pitch, npx, lane, M);
-      else tree_sums<4, PPL>(mom, npx, lane, M);
-      const float n = (float)(ww * wh);
-      alpha = (float)sqrt((double)((M[2] / n) / (M[3] / n)));
-      beta = M[0] / n - alpha * (M[1] / n);
+      if (!step) gxs = gys = dif = 0.0f;
+      prod[0][k] = gxs * gxs;
+      prod[1][k] = gxs * gys;
+      prod[2][k] = gys * gys;
+      prod[3][k] = dif * gxs;
+      prod[4][k] = dif * gys;
     }
+#ifdef KLT_TRACK_PROF
+    {  // force the gathered values before the clock read
+      float z = 0.0f;
 #pragma unroll
-    for (int k = 0; k < PPL; ++k) {
-      const float d = a.li ? (a_im[k] - b_im[k] * alpha - beta) : (a_im[k] - b_im[k]);
-      dif[0][k] = fabsf(d);
+      for (int k = 0; k < PPL; ++k) z += prod[4][k];
+      asm volatile("" ::"v"(z));
     }
-    if (EXACT) exact_sums<1, PPL>(dif, red, a.red_pitch, npx, lane, S);
-    else tree_sums<1, PPL>(dif, npx, lane, S);
-    if (S[0] / (float)(ww * wh) > a.max_res) status = kLargeResidue;
+#endif
+    PROF_ADD(0, t_g0);
+    PROF_T(t_s0);
+    sums_g<G, 5, PPL, PATCH, EXACT>(w, prod, red, a.red_pitch, npx, lane, S);
+    PROF_ADD(1, t_s0);
+    PROF_T(t_v0);
+    if (step) {
+      const float gxx = S[0], gxy = S[1], gyy = S[2];
+      const float ex = S[3] * a.step, ey = S[4] * a.step;
+      // _solveEquation (:293-307)
+      const float det = gxx * gyy - gxy * gxy;
+      if (det < a.min_det) {
+        status = kSmallDet;  // x2 has not moved: the post-loop window test repeats this iteration's
+        act = false;
+      } else {
+        const float dx = uni<G>((gyy * ex - gxy * ey) / det);
+        const float dy = uni<G>((gxx * ey - gxy * ex) / det);
+        status = kTracked;
+        x2 = uni<G>(x2 + dx);
+        y2 = uni<G>(y2 + dy);
+        ++it;
+        if (!((fabsf(dx) >= a.min_disp || fabsf(dy) >= a.min_disp) && it < a.max_it)) fin = true;
+      }
+      PROF_INC(5);
+    }
+    PROF_ADD(2, t_v0);
   }
   if (status == kSmallDet) return kSmallDet;
   if (status == kOOB) return kOOB;
@@ -831,27 +1082,36 @@ __device__ int track_level(const TrkArgs &a, const TrkLevel &A, const TrkLevel &
   return kTracked;
 }
 
-// KLTTrackFeatures coarse-to-fine driver for one feature (:1348-1380) and its
-// status mapping (:1383-1437) with _outOfBounds (:491-501).  LA(r) / LB(r)
-// give level r of the previous / current pyramid.
-template <int PPL, bool EXACT, class LevA, class LevB>
-__device__ __forceinline__ void track_feature(const TrkArgs &a, LevA LA, LevB LB, float &fx, float &fy, int &fv,
-                                              int lane, float *red) {
+// one frame of KLTTrackFeatures for the feature of this lane's group (:1348-1437)
+template <int G, int PPL, bool PATCH, bool EXACT, bool LI, class LevA, class LevB>
+__device__ __forceinline__ void track_feature_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, PATCH> &w,
+                                                LevA LA,
+                                                LevB LB,
+                                                float &fx, float &fy, int &fv, bool live, int lane,
+                                                float *red) {
   float xl = fx, yl = fy;
   for (int r = a.nlev - 1; r >= 0; --r) {
-    xl /= a.ss;
-    yl /= a.ss;
+    xl = uni<G>(xl / a.ss);
+    yl = uni<G>(yl / a.ss);
   }
   float xo = xl, yo = yl;
   int val = kTracked;
+  bool go = live;
   for (int r = a.nlev - 1; r >= 0; --r) {
-    xl *= a.ss;
-    yl *= a.ss;
-    xo *= a.ss;
-    yo *= a.ss;
-    val = track_level<PPL, EXACT>(a, LA(r), LB(r), xl, yl, xo, yo, lane, red);
-    if (val == kSmallDet || val == kOOB) break;
+    if (!wave_any(go)) break;
+    if (go) {  // a feature that stopped keeps the coordinates of its last level (border test below)
+      xl = uni<G>(xl * a.ss);
+      yl = uni<G>(yl * a.ss);
+      xo = uni<G>(xo * a.ss);
+      yo = uni<G>(yo * a.ss);
+    }
+    const int v = track_level_g<G, PPL, PATCH, EXACT, LI>(PROF_ARG a, w, LA(r), LB(r), xl, yl, xo, yo, go, lane, red);
+    if (go) {
+      val = v;
+      if (v == kSmallDet || v == kOOB) go = false;
+    }
   }
+  if (!live) return;
   const bool border = xo < a.borderx || xo > a.ncols - 1 - a.borderx || yo < a.bordery ||
                       yo > a.nrows - 1 - a.bordery;
   if (val == kOOB || border) {
@@ -869,71 +1129,100 @@ __device__ __forceinline__ void track_feature(const TrkArgs &a, LevA LA, LevB LB
   }
 }
 
-template <int PPL, bool EXACT>
-__global__ __launch_bounds__(kBlock) void k_track(TrkArgs a, float *__restrict__ fx,
-                                                  float *__restrict__ fy, int *__restrict__ fv, int n) {
-  __shared__ __attribute__((aligned(16))) float red_all[kBlock / kWave][5 * (kWave * PPL + 4)];
+template <int G, int PPL, bool PATCH, bool EXACT, bool LI>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KLT_TRACK_WAVES))) void k_track_frames_g(TrkArgs a, TrkFramesArgs b, float *__restrict__ fx,
+                                                           float *__restrict__ fy, int *__restrict__ fv, int n) {
+  constexpr int LG = kWave / G;
+  __shared__ __attribute__((aligned(16))) float red_all[kBlock / kWave][5 * G * (LG * PPL + 4) + 16];
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  const int f = blockIdx.x * (kBlock / kWave) + wave;
-  if (f >= n) return;  // whole wave; the kernel has no workgroup barrier
-  int v = fv[f];
-  if (v < 0) return;  // lost features are not tracked (:1346)
-  float x = fx[f], y = fy[f];
-  track_feature<PPL, EXACT>(
-      a, [&](int r) { return a.A[r]; }, [&](int r) { return a.B[r]; }, x, y, v, lane, red_all[wave]);
-  if (lane == 0) {
-    fx[f] = x;
-    fy[f] = y;
-    fv[f] = v;
+  // consecutive workgroups land on the 8 XCDs round-robin: give each XCD a
+  // contiguous run of the (band-sorted) order so its L2 sees one image band
+  const int blk = b.xcd_per > 0 ? (int)(blockIdx.x % 8) * b.xcd_per + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  const int s0 = (blk * (kBlock / kWave) + wave) * G;
+  if (s0 >= n) return;  // whole wave; the kernel has no workgroup barrier
+  const int g = lane / LG, slot = s0 + g;
+  const bool exists = slot < n;
+  const int f = exists ? (b.perm ? b.perm[slot] : slot) : 0;
+  float x = 0.0f, y = 0.0f;
+  int v = -1;
+  if (exists) {
+    x = uni<G>(fx[f]);
+    y = uni<G>(fy[f]);
+    v = uni<G>(fv[f]);
   }
-}
-
-// ---------------------------------------------------------------------------
-// k_track_frames: one wave carries its feature through a batch of frames
-// (the KLTTrackFeatures + KLTStoreFeatureList loop of example3.c:54-74 with
-// no replacement).  Frame j tracks pyramid j-1 -> j of the bank (j = 0: from
-// a.A, the pyramid before the batch); every feature is independent, so the
-// per-frame launch and its dependency bubble disappear.  Row j of the
-// optional feature table receives the list after frame j.
-// ---------------------------------------------------------------------------
-struct TrkFramesArgs {
-  long lfs[KLT_HIP_MAX_LEVELS];  // bank frame stride per level (floats)
-  int nframes;
-  float *tx, *ty;
-  int *tv;
-  long tstride;  // table row stride (elements); tx == nullptr: no table
-};
-
-__device__ __forceinline__ TrkLevel at_frame(const TrkLevel &L, long off) {
-  return TrkLevel{L.img + off, L.gx + off, L.gy + off, L.w, L.h};
-}
-
-template <int PPL, bool EXACT>
-__global__ __launch_bounds__(kBlock) void k_track_frames(TrkArgs a, TrkFramesArgs b, float *__restrict__ fx,
-                                                         float *__restrict__ fy, int *__restrict__ fv, int n) {
-  __shared__ __attribute__((aligned(16))) float red_all[kBlock / kWave][5 * (kWave * PPL + 4)];
-  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  const int f = blockIdx.x * (kBlock / kWave) + wave;
-  if (f >= n) return;
-  float x = fx[f], y = fy[f];
-  int v = fv[f];
+  const GroupWin<G, PPL, PATCH> w = group_window<G, PPL, PATCH>(a.ww, a.wh, lane);
+  {  // row pads of the ordered-sum staging stay +0 for the whole kernel
+    float *red = red_all[wave];
+    constexpr int RED = 5 * G * (LG * PPL + 4) + 16;
+    for (int i = lane; i < RED; i += kWave) red[i] = 0.0f;
+    lds_wave_sync();
+  }
+  const bool head = exists && (lane % LG) == 0;
+#ifdef KLT_TRACK_PROF
+  Prof prof;
+  const unsigned long long wall0 = wall_clock64();
+#endif
   for (int j = 0; j < b.nframes; ++j) {
-    if (v >= 0) {
-      track_feature<PPL, EXACT>(
-          a, [&](int r) { return j == 0 ? a.A[r] : at_frame(a.B[r], (long)(j - 1) * b.lfs[r]); },
-          [&](int r) { return at_frame(a.B[r], (long)j * b.lfs[r]); }, x, y, v, lane, red_all[wave]);
+    const bool live = exists && v >= 0;  // lost features are not tracked (:1346)
+    PROF_T(t_f0);
+    if (wave_any(live)) {
+      track_feature_g<G, PPL, PATCH, EXACT, LI>(
+          PROF_ARG a, w, [&](int r) { return j == 0 ? a.A[r] : at_frame(a.B[r], (long)(j - 1) * b.lfs[r]); },
+          [&](int r) { return at_frame(a.B[r], (long)j * b.lfs[r]); }, x, y, v, live, lane, red_all[wave]);
     }
-    if (b.tx && lane == 0) {
+    PROF_ADD(4, t_f0);
+    if (b.tx && head) {
       b.tx[j * b.tstride + f] = x;
       b.ty[j * b.tstride + f] = y;
       b.tv[j * b.tstride + f] = v;
     }
   }
-  if (lane == 0) {
+  if (head) {
     fx[f] = x;
     fy[f] = y;
     fv[f] = v;
   }
+#ifdef KLT_TRACK_PROF
+  prof.c[8] = wall0;
+  prof.c[9] = wall_clock64();
+  prof.c[7] = prof.c[9] - wall0;  // constant-rate ticks over the wave's life
+  if (b.prof && lane == 0)
+    for (int k = 0; k < kProfN; ++k) b.prof[(long)(blk * (kBlock / kWave) + wave) * kProfN + k] = prof.c[k];
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// k_band_order: processing order for the tracker -- live features bucketed by
+// image row band (counting sort, one workgroup), lost features last.  Only
+// the order of work changes; every feature's result is independent of it.
+// ---------------------------------------------------------------------------
+constexpr int kBands = 128, kSortThreads = 1024;
+
+__global__ __launch_bounds__(kSortThreads) void k_band_order(const float *__restrict__ fy,
+                                                             const int *__restrict__ fv, int n, int nrows,
+                                                             int *__restrict__ perm) {
+  __shared__ int cnt[kBands + 1];
+  const int t = threadIdx.x;
+  for (int i = t; i <= kBands; i += kSortThreads) cnt[i] = 0;
+  __syncthreads();
+  const float scale = (float)kBands / (float)(nrows > 0 ? nrows : 1);
+  auto band_of = [&](int i) {
+    if (fv[i] < 0) return kBands;
+    const float b = fy[i] * scale;
+    return b >= 0.0f ? (b < (float)kBands ? (int)b : kBands - 1) : 0;  // NaN -> band 0
+  };
+  for (int i = t; i < n; i += kSortThreads) atomicAdd(&cnt[band_of(i)], 1);
+  __syncthreads();
+  if (t == 0) {
+    int run = 0;
+    for (int i = 0; i <= kBands; ++i) {
+      const int c = cnt[i];
+      cnt[i] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < n; i += kSortThreads) perm[atomicAdd(&cnt[band_of(i)], 1)] = i;
 }
 
 // ---------------------------------------------------------------------------
@@ -1022,6 +1311,14 @@ struct klt_hip_ctx {
   size_t eig_cap = 0;
   std::string err;
   int force_generic = 0;
+  int track_group = 0;  // features per wave for small windows (0: default)
+  int track_order = 0;  // 0: band-sorted, XCD-major processing order; 1: input order
+  int track_patch = 1;  // one-feature waves gather through a lane patch when the window fits
+  int *d_perm = nullptr;
+  size_t perm_cap = 0;
+#ifdef KLT_TRACK_PROF
+  unsigned long long *prof = nullptr;
+#endif
   Bank bank[3];
   int bank_next = 0;
   PrevRef prev;
@@ -1240,20 +1537,6 @@ int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t 
   return 0;
 }
 
-template <int PPL, bool EXACT>
-void launch_track(hipStream_t st, const TrkArgs &a, float *x, float *y, int *v, int n) {
-  const int per = kBlock / kWave;
-  hipLaunchKernelGGL((k_track<PPL, EXACT>), dim3((n + per - 1) / per), dim3(kBlock), 0, st, a, x, y, v, n);
-}
-
-template <int PPL, bool EXACT>
-void launch_track_frames(hipStream_t st, const TrkArgs &a, const TrkFramesArgs &b, float *x, float *y, int *v,
-                         int n) {
-  const int per = kBlock / kWave;
-  hipLaunchKernelGGL((k_track_frames<PPL, EXACT>), dim3((n + per - 1) / per), dim3(kBlock), 0, st, a, b, x, y,
-                     v, n);
-}
-
 int check_window(klt_hip_ctx *c, const klt_hip_track_desc *d) {
   const int npx = d->window_width * d->window_height;
   if (d->window_width < 1 || d->window_height < 1 || npx > 16 * kWave)
@@ -1284,20 +1567,62 @@ void fill_trk_args(const klt_hip_track_desc *d, int nlev, int ss, int ncols, int
   a.red_pitch = rp;
 }
 
+template <int G, int PPL, bool PATCH, bool EXACT, bool LI>
+void launch_track_frames_g(hipStream_t st, const TrkArgs &a, const TrkFramesArgs &b, float *x, float *y, int *v,
+                           int n) {
+  const int per = (kBlock / kWave) * G;  // features per workgroup
+  const int nb = (n + per - 1) / per;
+  const int grid = b.xcd_per > 0 ? 8 * b.xcd_per : nb;
+  hipLaunchKernelGGL((k_track_frames_g<G, PPL, PATCH, EXACT, LI>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
+}
+
+// fewer features than this: input order (the sort launch would not pay)
+constexpr int kOrderMin = 2048;
+
+// features per wave for a window of npx pixels: 1 for large windows and the
+// lighting-insensitive variant, else the tuning choice (default 1)
+int track_group(const klt_hip_ctx *c, int npx, bool li) {
+  if (npx > kWave || li) return 1;
+  return c->track_group > 0 ? c->track_group : 1;
+}
+
+template <bool EXACT, bool LI>
+void launch_track_sel(int G, bool patch, int npx, hipStream_t st, const TrkArgs &a, const TrkFramesArgs &b,
+                      float *x, float *y, int *v, int n) {
+  if (G == 4) launch_track_frames_g<4, 4, false, EXACT, false>(st, a, b, x, y, v, n);
+  else if (G == 2) launch_track_frames_g<2, 2, false, EXACT, false>(st, a, b, x, y, v, n);
+  else if (patch) launch_track_frames_g<1, 1, true, EXACT, LI>(st, a, b, x, y, v, n);
+  else if (npx <= kWave) launch_track_frames_g<1, 1, false, EXACT, LI>(st, a, b, x, y, v, n);
+  else if (npx <= 4 * kWave) launch_track_frames_g<1, 4, false, EXACT, LI>(st, a, b, x, y, v, n);
+  else launch_track_frames_g<1, 16, false, EXACT, LI>(st, a, b, x, y, v, n);
+}
+
 int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc *d, const TrkArgs &a,
                         const TrkFramesArgs &b, float *x, float *y, int *v, int n) {
   TimedScope ts(c, T_TRACK, st, b.nframes);
   const int npx = d->window_width * d->window_height;
-  const bool exact = d->reduction == KLT_HIP_EXACT;
-  if (npx <= kWave) {
-    if (exact) launch_track_frames<1, true>(st, a, b, x, y, v, n);
-    else launch_track_frames<1, false>(st, a, b, x, y, v, n);
-  } else if (npx <= 4 * kWave) {
-    if (exact) launch_track_frames<4, true>(st, a, b, x, y, v, n);
-    else launch_track_frames<4, false>(st, a, b, x, y, v, n);
+  const bool exact = d->reduction == KLT_HIP_EXACT, li = d->lighting_insensitive != 0;
+  const int G = track_group(c, npx, li);
+  const bool patch = G == 1 && c->track_patch && (d->window_width + 1) * (d->window_height + 1) <= kWave;
+  TrkFramesArgs bb = b;
+  if (c->track_order == 0 && n >= kOrderMin) {
+    if (grow(c, &c->d_perm, &c->perm_cap, (size_t)n)) return -1;
+    hipLaunchKernelGGL(k_band_order, dim3(1), dim3(kSortThreads), 0, st, y, v, n, a.nrows, c->d_perm);
+    if (check_launch(c, "k_band_order")) return -1;
+    const int per = (kBlock / kWave) * G, nb = (n + per - 1) / per;
+    bb.perm = c->d_perm;
+    bb.xcd_per = (nb + 7) / 8;
+  }
+#ifdef KLT_TRACK_PROF
+  bb.prof = c->prof;
+#endif
+  const TrkFramesArgs &b2 = bb;
+  if (exact) {
+    if (li) launch_track_sel<true, true>(G, patch, npx, st, a, b2, x, y, v, n);
+    else launch_track_sel<true, false>(G, patch, npx, st, a, b2, x, y, v, n);
   } else {
-    if (exact) launch_track_frames<16, true>(st, a, b, x, y, v, n);
-    else launch_track_frames<16, false>(st, a, b, x, y, v, n);
+    if (li) launch_track_sel<false, true>(G, patch, npx, st, a, b2, x, y, v, n);
+    else launch_track_sel<false, false>(G, patch, npx, st, a, b2, x, y, v, n);
   }
   return check_launch(c, "k_track_frames");
 }
@@ -1427,6 +1752,7 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
     if (c->ev_bbuilt[k]) hipEventDestroy(c->ev_bbuilt[k]);
     if (c->ev_bfree[k]) hipEventDestroy(c->ev_bfree[k]);
   }
+  hipFree(c->d_perm);
   hipFree(c->d_hs);
   hipFree(c->d_fx);
   hipFree(c->d_fy);
@@ -1537,6 +1863,34 @@ KLT_API int klt_hip_set_path(klt_hip_ctx *c, int force_generic) {
   return 0;
 }
 
+KLT_API int klt_hip_set_track_group(klt_hip_ctx *c, int features_per_wave) {
+  if (!c) return fail(c, "set_track_group: null context");
+  if (features_per_wave != 0 && features_per_wave != 1 && features_per_wave != 2 && features_per_wave != 4)
+    return fail(c, "set_track_group: %d not in {0, 1, 2, 4}", features_per_wave);
+  c->track_group = features_per_wave;
+  return 0;
+}
+
+#ifdef KLT_TRACK_PROF
+// instrumented build only: device buffer of kProfN u64 per wave slot
+KLT_API int klt_hip_set_prof(klt_hip_ctx *c, void *dev) {
+  c->prof = (unsigned long long *)dev;
+  return 0;
+}
+#endif
+
+KLT_API int klt_hip_set_track_patch(klt_hip_ctx *c, int on) {
+  if (!c) return fail(c, "set_track_patch: null context");
+  c->track_patch = on ? 1 : 0;
+  return 0;
+}
+
+KLT_API int klt_hip_set_track_order(klt_hip_ctx *c, int input_order) {
+  if (!c) return fail(c, "set_track_order: null context");
+  c->track_order = input_order ? 1 : 0;
+  return 0;
+}
+
 KLT_API int klt_hip_fused_path(klt_hip_ctx *c, const klt_hip_pyr_desc *d) {
   if (!c || !d) return fail(c, "fused_path: null argument");
   return fused_ok(d) && !c->force_generic ? 1 : 0;
@@ -1613,19 +1967,11 @@ KLT_API int klt_hip_track(klt_hip_ctx *c, int s1, int s2, const klt_hip_track_de
     HIPCHK(c, hipMemcpyAsync(v_d, val, sizeof(int) * n, hipMemcpyHostToDevice, c->stream));
   }
   {
-    TimedScope ts(c, T_TRACK, c->stream);
-    const bool exact = d->reduction == KLT_HIP_EXACT;
-    if (npx <= kWave) {
-      if (exact) launch_track<1, true>(c->stream, a, x_d, y_d, v_d, n);
-      else launch_track<1, false>(c->stream, a, x_d, y_d, v_d, n);
-    } else if (npx <= 4 * kWave) {
-      if (exact) launch_track<4, true>(c->stream, a, x_d, y_d, v_d, n);
-      else launch_track<4, false>(c->stream, a, x_d, y_d, v_d, n);
-    } else {
-      if (exact) launch_track<16, true>(c->stream, a, x_d, y_d, v_d, n);
-      else launch_track<16, false>(c->stream, a, x_d, y_d, v_d, n);
-    }
-    if (check_launch(c, "k_track")) return -1;
+    // one frame through the batched kernels: frame 0 tracks a.A -> a.B, no table
+    TrkFramesArgs b;
+    memset(&b, 0, sizeof b);
+    b.nframes = 1;
+    if (track_frames_launch(c, c->stream, d, a, b, x_d, y_d, v_d, n)) return -1;
   }
   if (!on_device) {
     HIPCHK(c, hipMemcpyAsync(x, x_d, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));

@@ -350,3 +350,71 @@ def test_reference_harness_relinked(gpu):
         want = (GOLDEN / f"config1_{n}x10.ft").read_bytes()
         assert table_eq(parse_ft(got), parse_ft(want)), f"{n} features: .ft differs from the reference"
         assert txt.splitlines()[:2] == (GOLDEN / f"config1_{n}x10.txt").read_bytes().splitlines()[:2]
+
+
+def _edge_positions():
+    """Window centres where x+i / y+j round across an integer for some window
+    pixel (just below a power of two), plus ordinary ones: exercises both the
+    lane-patch gather and its per-pixel fallback."""
+    f32 = np.float32
+    xs, ys = [], []
+    for base in (64.0, 128.0, 256.0, 512.0):
+        for d in (-3, -2, -1, 1, 2):
+            xs.append(np.nextafter(f32(base), f32(0)) if d == -1 else f32(base) + f32(d) * f32(1e-5))
+            ys.append(f32(200.25) + f32(d))
+    for d in range(8):
+        xs.append(f32(300.5) + f32(d) * f32(0.37))
+        ys.append(np.nextafter(f32(256.0), f32(0)) if d % 2 else f32(128.0) - f32(3e-6))
+    return np.array(xs, np.float32), np.array(ys, np.float32)
+
+
+@pytest.mark.parametrize("patch", [1, 0])
+def test_patch_gather_edge_positions(gpu, oracle, patch):
+    from kltabi import arrays_to_fl, fl_to_arrays, u8ptr
+    frames = synth(gpu, 777, 640, 480, 2)
+    x0, y0 = _edge_positions()
+    n = len(x0)
+    tc = gpu.KLTCreateTrackingContext()
+    ctx = gpu.klt_amd_device_context(tc)
+    assert gpu.klt_hip_set_track_patch(ctx, patch) == 0
+    fl = gpu.KLTCreateFeatureList(n)
+    arrays_to_fl(fl, x0, y0, np.zeros(n, np.int32))
+    gpu.KLTTrackFeatures(tc, u8ptr(frames[0]), u8ptr(frames[1]), 640, 480, fl)
+    gx, gy, gv = fl_to_arrays(fl)
+    gpu.KLTFreeFeatureList(fl)
+    gpu.KLTFreeTrackingContext(tc)
+    ox, oy, ov = x0.copy(), y0.copy(), np.zeros(n, np.int32)
+    ot = OracleTracker(oracle)
+    ot.params.sequentialMode = 0
+    oracle.orc_set_params(ot.h, C.byref(ot.params))
+    ot.track(frames[0], frames[1], ox, oy, ov)
+    assert np.array_equal(gv, ov)
+    assert np.array_equal(gx.view(np.int32), ox.view(np.int32))
+    assert np.array_equal(gy.view(np.int32), oy.view(np.int32))
+
+
+@pytest.mark.parametrize("opts", [dict(group=1, patch=0), dict(group=2, patch=1), dict(group=4, patch=1),
+                                  dict(order=1, patch=1)])
+def test_tracker_tuning_hooks_do_not_change_results(gpu, oracle, opts):
+    """Features per wave, lane patch and processing order only reorganise work."""
+    frames = synth(gpu, 5151, 640, 480, 8)
+    X, Y, V = batch_sequence_opts(gpu, frames, 3000, 4, opts)
+    assert_table_equal(X, Y, V, *OracleTracker(oracle).harness(frames, 3000, 8, first=frames[0]))
+
+
+def batch_sequence_opts(gpu, frames, nfeat, chunk, opts):
+    """batch_sequence with the tuning hooks applied to its device context."""
+    orig = gpu.klt_amd_device_context
+
+    def hooked(tc):
+        ctx = orig(tc)
+        assert gpu.klt_hip_set_track_group(ctx, opts.get("group", 0)) == 0
+        assert gpu.klt_hip_set_track_patch(ctx, opts.get("patch", 1)) == 0
+        assert gpu.klt_hip_set_track_order(ctx, opts.get("order", 0)) == 0
+        return ctx
+
+    gpu.klt_amd_device_context = hooked
+    try:
+        return batch_sequence(gpu, frames, nfeat, [chunk])
+    finally:
+        gpu.klt_amd_device_context = orig

@@ -28,6 +28,11 @@ sys.path.insert(0, str(ROOT))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("mode", choices=["pyr", "track", "frames", "api"])
+    ap.add_argument("--prof", action="store_true",
+                    help="per-wave phase cycles (needs KLT_AMD_LIB=.../lib/prof/libklt_amd.so)")
+    ap.add_argument("--no-patch", action="store_true", help="tracker: per-pixel gathers only")
+    ap.add_argument("--input-order", action="store_true", help="tracker: no band ordering")
+    ap.add_argument("--group", type=int, default=0, help="tracker: features per wave (0 default, 1, 2, 4)")
     ap.add_argument("--chunk", type=int, default=16, help="frames: frames per batch")
     ap.add_argument("--pyr-only", action="store_true", help="frames: build the batched pyramids, track nothing")
     ap.add_argument("--width", type=int, default=1920)
@@ -53,6 +58,9 @@ def main():
     lib.klt_amd_set_reduction(tc, 0 if a.reduction == "exact" else 1)
     ctx = lib.klt_amd_device_context(tc)
     lib.klt_hip_set_path(ctx, 1 if a.generic else 0)
+    check(lib, ctx, lib.klt_hip_set_track_group(ctx, a.group), "group")
+    check(lib, ctx, lib.klt_hip_set_track_order(ctx, 1 if a.input_order else 0), "order")
+    check(lib, ctx, lib.klt_hip_set_track_patch(ctx, 0 if a.no_patch else 1), "patch")
     nf = max(a.frames, 2)
     frames = lib.klt_hip_malloc(ctx, nf * W * H)
     check(lib, ctx, lib.klt_hip_synth_frames(ctx, 1080, 0, nf, W, H, frames, W, W * H), "synth")
@@ -154,7 +162,36 @@ def main():
         wall = time.perf_counter() - t0
         done = a.reps * T
         lib.klt_hip_set_timing(ctx, 1)  # one more pass with per-launch events
+        pbuf = None
+        if a.prof:
+            nslot = (n + 64) * 10
+            pbuf = lib.klt_hip_malloc(ctx, 8 * nslot)
+            lib.klt_hip_set_prof.restype = C.c_int
+            lib.klt_hip_set_prof.argtypes = [C.c_void_p, C.c_void_p]
+            check(lib, ctx, lib.klt_hip_memcpy(ctx, pbuf, np.zeros(nslot, np.uint64).ctypes.data, 8 * nslot, H2D),
+                  "zero")
+            lib.klt_hip_set_prof(ctx, pbuf)
         rep()
+        if a.prof:
+            lib.klt_hip_sync(ctx)
+            pr = np.empty(nslot, np.uint64)
+            check(lib, ctx, lib.klt_hip_memcpy(ctx, pr.ctypes.data, pbuf, 8 * nslot, 2), "prof")
+            pr = pr.reshape(-1, 10).astype(np.float64)
+            pr = pr[pr[:, 4] > 0]  # waves that ran frames
+            names = ["gather_interp", "sums", "solve", "residue", "frame", "iterations", "passes", "wall_ticks"]
+            # accumulated over the timed rep's launches (last launch overwrites per slot): per wave per frame
+            fr = a.chunk
+            out["prof_cycles_per_wave_frame"] = {nm: float(pr[:, k].mean() / fr) for k, nm in enumerate(names)}
+            out["prof_cycles_per_wave_frame"].pop("wall_ticks")
+            out["prof_waves"] = int(pr.shape[0])
+            rate = C.c_int(0)
+            # wall_clock64 runs at hipDeviceAttributeWallClockRate kHz (100 MHz on MI300-class parts)
+            out["prof_clock64_ghz"] = float(pr[:, 4].sum() / (pr[:, 7].sum() / 100e6) / 1e9)
+            out["prof_wave_life_us"] = float(pr[:, 7].mean() / 100.0)
+            st = (pr[:, 8] - pr[:, 8].min()) / 100.0
+            en = (pr[:, 9] - pr[:, 8].min()) / 100.0
+            out["prof_start_us_pct"] = [float(np.percentile(st, q)) for q in (0, 25, 50, 75, 90, 100)]
+            out["prof_end_us_pct"] = [float(np.percentile(en, q)) for q in (0, 25, 50, 75, 90, 100)]
         tm = Timing()
         check(lib, ctx, lib.klt_hip_get_timing(ctx, C.byref(tm)), "timing")
         vv = np.empty(n, np.int32)
