@@ -51,9 +51,11 @@ def parse():
                    help="frames of the bounded CPU-baseline sample (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--reduction", choices=["exact", "fast"], default="exact")
-    p.add_argument("--chunk", type=int, default=16,
+    p.add_argument("--chunk", type=int, default=32,
                    help="frames per batched pyramid/track launch (klt_hip_track_frames); 0 = the per-frame "
                         "pipelined path (klt_hip_track_sequence)")
+    p.add_argument("--overlap", action="store_true",
+                   help="build chunk c+1's pyramids on a second stream while chunk c is tracked")
     p.add_argument("--event-timing", choices=["timed", "replay"], default="replay",
                    help="record per-kernel HIP events inside the timed region or in a replay")
     return p.parse_args()
@@ -88,6 +90,7 @@ def main() -> None:
     tc.contents.sequentialMode = 1
     lib.klt_amd_set_reduction(tc, EXACT if args.reduction == "exact" else FAST)
     ctx = lib.klt_amd_device_context(tc)
+    check(lib, ctx, lib.klt_hip_set_frames_overlap(ctx, 1 if args.overlap else 0), "overlap")
     stream = torch.cuda.current_stream(dev)
     check(lib, ctx, lib.klt_hip_set_stream(ctx, C.c_void_p(stream.cuda_stream)), "set_stream")
 
@@ -203,7 +206,7 @@ def main() -> None:
         "data": f"synthetic: include/klt_synth.h value-noise frames, (0.7,0.3) px/frame, seed {args.seed}+rank",
         "config": {"workload": f"{W}x{H}, {NF} features, sequential KLTTrackFeatures pass + KLTStoreFeatureList "
                                f"per frame, {nframes} frames per GPU (BASELINE config 3; config 5 at N>1)",
-                   "chunk": args.chunk,
+                   "chunk": args.chunk, "overlap": bool(args.overlap),
                    "resolution": f"{W}x{H}", "features": NF, "frames": nframes,
                    "parallelism": "independent sequence per GPU" if world > 1 else "single GPU",
                    "reduction": args.reduction, "pyramid_path": "fused" if fused else "generic"},

@@ -111,6 +111,9 @@ int klt_hip_set_track_order(klt_hip_ctx *ctx, int input_order);
 /* tuning hook: 0 disables the lane-patch gather of one-feature waves (default
    1: on where (ww+1)*(wh+1) <= 64).  Results do not depend on it. */
 int klt_hip_set_track_patch(klt_hip_ctx *ctx, int on);
+/* klt_hip_track_frames scheduling: 1 builds chunk c+1's pyramids on a second
+   stream while chunk c is tracked; 0 (default) runs both on the context stream. */
+int klt_hip_set_frames_overlap(klt_hip_ctx *ctx, int overlap);
 /* 1 if pyramids for `desc` would be built by the fused gfx950 kernels, else 0 */
 int klt_hip_fused_path(klt_hip_ctx *ctx, const klt_hip_pyr_desc *desc);
 /* 1 if the slot was built by the fused gfx950 kernels, 0 generic, <0 invalid */
@@ -127,10 +130,11 @@ const float *klt_hip_level_ptr(klt_hip_ctx *ctx, int slot, int level, int which)
 int klt_hip_track(klt_hip_ctx *ctx, int slot1, int slot2, const klt_hip_track_desc *desc,
                   float *x, float *y, int *val, int n, int on_device);
 
-/* device-resident sequential tracking (the bench hot loop): for each step k,
-   build frame t0+k (frames + (t0+k)*stride) into the slot not holding the
-   previous pyramid (*cur_slot, 0 or 1), then track the device feature arrays
-   from *cur_slot into it and flip *cur_slot.  Asynchronous. */
+/* device-resident sequential tracking, one frame per step: for step k, build
+   frame t0+k (frames + (t0+k)*stride) on a second stream into the next of
+   three slots (one frame ahead of the tracker), then track the device feature
+   arrays from *cur_slot (0..2, the previous frame's pyramid) into it and
+   advance *cur_slot.  Asynchronous.  klt_hip_track_frames is the batched form. */
 int klt_hip_track_sequence(klt_hip_ctx *ctx, const klt_hip_pyr_desc *pdesc,
                            const klt_hip_track_desc *tdesc, const unsigned char *frames, long pitch,
                            long stride, int t0, int nsteps, float *x, float *y, int *val, int n,
@@ -139,7 +143,8 @@ int klt_hip_track_sequence(klt_hip_ctx *ctx, const klt_hip_pyr_desc *pdesc,
 /* batched device-resident sequence -- the KLTTrackFeatures +
    KLTStoreFeatureList loop of the reference harness (example3.c:54-74) with
    no feature replacement, `chunk` frames per pair of pyramid launches and per
-   tracking launch, pyramids built one chunk ahead on a second stream.
+   tracking launch (pyramids of a chunk, then its tracking; see
+   klt_hip_set_frames_overlap).
    klt_hip_frames_begin builds the pyramid the first tracked frame starts from;
    klt_hip_track_frames then tracks the device arrays x/y/val (n features)
    through frames[0..nframes-1] (frame f at frames + f*stride, row pitch

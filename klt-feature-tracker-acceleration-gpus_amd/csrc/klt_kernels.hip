@@ -715,7 +715,7 @@ struct Prof {
 // form a (ww+1)-wide patch, lane = j*(ww+1) + i holds pixel (i, j) of the
 // window for i < ww, j < wh; the extra column/row are the bilinear corners'
 // far side, so one 4-byte load per lane fetches every corner of every pixel.
-template <int G, int PPL, bool PATCH>
+template <int G, int PPL, bool PATCH, int WIN>
 struct GroupWin {
   int oi[PPL], oj[PPL];
   int p[PPL];  // pixel index in the reference's row-major order
@@ -724,11 +724,12 @@ struct GroupWin {
   int ci, cj;  // PATCH: this lane's patch cell
 };
 
-template <int G, int PPL, bool PATCH>
-__device__ __forceinline__ GroupWin<G, PPL, PATCH> group_window(int ww, int wh, int lane) {
+template <int G, int PPL, bool PATCH, int WIN>
+__device__ __forceinline__ GroupWin<G, PPL, PATCH, WIN> group_window(int ww_rt, int wh_rt, int lane) {
+  const int ww = WIN ? WIN : ww_rt, wh = WIN ? WIN : wh_rt;
   constexpr int LG = kWave / G;
   const int l = lane % LG, npx = ww * wh, hw = ww / 2, hh = wh / 2;
-  GroupWin<G, PPL, PATCH> w;
+  GroupWin<G, PPL, PATCH, WIN> w;
   w.pw = ww + 1;
   if (PATCH) {
     const int j = lane / (ww + 1), i = lane - j * (ww + 1);
@@ -758,8 +759,8 @@ __device__ __forceinline__ GroupWin<G, PPL, PATCH> group_window(int ww, int wh, 
 // never written, so whole 16-byte chunks add exactly (acc + +0 == acc, an
 // ordered sum from +0 is never -0).  Lane g*NS+s then adds row g*NS+s in
 // pixel order: the reference's sequential float sum.
-template <int G, int NS, int PPL, bool PATCH>
-__device__ __forceinline__ void exact_sums_g(const GroupWin<G, PPL, PATCH> &w, const float (&v)[NS][PPL],
+template <int G, int NS, int PPL, bool PATCH, int WIN>
+__device__ __forceinline__ void exact_sums_g(const GroupWin<G, PPL, PATCH, WIN> &w, const float (&v)[NS][PPL],
                                              float *red, int rp, int npx, int lane, float (&out)[NS]) {
   constexpr int LG = kWave / G;
   const int g = lane / LG;
@@ -772,7 +773,26 @@ __device__ __forceinline__ void exact_sums_g(const GroupWin<G, PPL, PATCH> &w, c
   }
   lds_wave_sync();
   float acc = 0.0f;
-  if (lane < G * NS) {
+  if (WIN > 0 && lane < G * NS) {
+    // compile-time window: fully unrolled, exactly one add per pixel
+    constexpr int NPX = WIN * WIN, NCH = (NPX + 3) / 4, B = KLT_SUM_BATCH;
+    const float *r = red + lane * rp;
+#pragma unroll
+    for (int b0 = 0; b0 < NCH; b0 += B) {
+      f4 c[B];
+#pragma unroll
+      for (int k = 0; k < B; ++k)
+        if (b0 + k < NCH) c[k] = ld4(r + 4 * (b0 + k));
+#pragma unroll
+      for (int k = 0; k < B; ++k) {
+        const int q = 4 * (b0 + k);
+        if (q + 0 < NPX) acc += c[k].x;
+        if (q + 1 < NPX) acc += c[k].y;
+        if (q + 2 < NPX) acc += c[k].z;
+        if (q + 3 < NPX) acc += c[k].w;
+      }
+    }
+  } else if (lane < G * NS) {
     // B chunks per batch, read whole before the ordered adds; reads past the
     // row's last chunk land in the next row or the buffer's tail pad, unused
     const float *r = red + lane * rp;
@@ -803,8 +823,8 @@ __device__ __forceinline__ void exact_sums_g(const GroupWin<G, PPL, PATCH> &w, c
   lds_wave_sync();
 }
 
-template <int G, int NS, int PPL, bool PATCH>
-__device__ __forceinline__ void tree_sums_g(const GroupWin<G, PPL, PATCH> &w, const float (&v)[NS][PPL],
+template <int G, int NS, int PPL, bool PATCH, int WIN>
+__device__ __forceinline__ void tree_sums_g(const GroupWin<G, PPL, PATCH, WIN> &w, const float (&v)[NS][PPL],
                                             float (&out)[NS]) {
   constexpr int LG = kWave / G;
 #pragma unroll
@@ -819,11 +839,11 @@ __device__ __forceinline__ void tree_sums_g(const GroupWin<G, PPL, PATCH> &w, co
   }
 }
 
-template <int G, int NS, int PPL, bool PATCH, bool EXACT>
-__device__ __forceinline__ void sums_g(const GroupWin<G, PPL, PATCH> &w, const float (&v)[NS][PPL], float *red,
+template <int G, int NS, int PPL, bool PATCH, int WIN, bool EXACT>
+__device__ __forceinline__ void sums_g(const GroupWin<G, PPL, PATCH, WIN> &w, const float (&v)[NS][PPL], float *red,
                                        int rp, int npx, int lane, float (&out)[NS]) {
-  if (EXACT) exact_sums_g<G, NS, PPL, PATCH>(w, v, red, rp, npx, lane, out);
-  else tree_sums_g<G, NS, PPL, PATCH>(w, v, out);
+  if (EXACT) exact_sums_g<G, NS, PPL, PATCH, WIN>(w, v, red, rp, npx, lane, out);
+  else tree_sums_g<G, NS, PPL, PATCH, WIN>(w, v, out);
 }
 
 // Bilinear samples of a level's planes for this lane's pixel(s).  PATCH: one
@@ -838,8 +858,8 @@ struct PatchPos {
   float w0, w1, w2, w3;
 };
 
-template <int G, int PPL, bool PATCH>
-__device__ __forceinline__ PatchPos patch_pos(const GroupWin<G, PPL, PATCH> &w, int nc, int nr, float x, float y) {
+template <int G, int PPL, bool PATCH, int WIN>
+__device__ __forceinline__ PatchPos patch_pos(const GroupWin<G, PPL, PATCH, WIN> &w, int nc, int nr, float x, float y) {
   PatchPos q;
   const float xs = x + w.oi[0], ys = y + w.oj[0];
   const int xt = (int)xs, yt = (int)ys;
@@ -859,35 +879,69 @@ __device__ __forceinline__ float patch_load(const float *P, const PatchPos &q) {
   return *reinterpret_cast<const float *>(reinterpret_cast<const char *>(P) + q.off);
 }
 
-template <int G, int PPL, bool PATCH>
-__device__ __forceinline__ float patch_value(const GroupWin<G, PPL, PATCH> &w, const PatchPos &q, float v,
+template <int G, int PPL, bool PATCH, int WIN>
+__device__ __forceinline__ float patch_value(const GroupWin<G, PPL, PATCH, WIN> &w, const PatchPos &q, float v,
                                              int lane) {
   const int pw = w.pw;
   const float v01 = __shfl(v, lane + 1), v10 = __shfl(v, lane + pw), v11 = __shfl(v, lane + pw + 1);
   return sel(w.on[0], q.w0 * v + q.w1 * v01 + q.w2 * v10 + q.w3 * v11);
 }
 
-template <int G, int PPL, bool PATCH>
-__device__ __forceinline__ void gather_direct(const TrkLevel &L, const GroupWin<G, PPL, PATCH> &w, float x,
-                                              float y, bool grads, float (&im)[PPL], float (&gx)[PPL],
-                                              float (&gy)[PPL]) {
+// per-pixel gather, split into corner loads and interpolation so that the
+// loads of every plane of both images go out before the first one is used
+struct Corners {
+  float2 r0, r1;  // (p00, p01), (p10, p11)
+};
+
+__device__ __forceinline__ Corners corner_load(const float *__restrict__ P, const Bil &b, unsigned w) {
+  const char *base = reinterpret_cast<const char *>(P);
+  Corners c;
+  c.r0 = *reinterpret_cast<const float2 *>(base + (unsigned)(b.off * 4u));
+  c.r1 = *reinterpret_cast<const float2 *>(base + (unsigned)((b.off + w) * 4u));
+  return c;
+}
+
+__device__ __forceinline__ float corner_interp(const Bil &b, const Corners &c) {
+  return b.w0 * c.r0.x + b.w1 * c.r0.y + b.w2 * c.r1.x + b.w3 * c.r1.y;
+}
+
+template <int G, int PPL, bool PATCH, int WIN>
+__device__ __forceinline__ void gather_direct2(const TrkLevel &A, const TrkLevel &B,
+                                               const GroupWin<G, PPL, PATCH, WIN> &w, float x1, float y1, float x2,
+                                               float y2, bool first, bool grads, float (&a_im)[PPL],
+                                               float (&a_gx)[PPL], float (&a_gy)[PPL], float (&b_im)[PPL],
+                                               float (&b_gx)[PPL], float (&b_gy)[PPL]) {
 #pragma unroll
   for (int k = 0; k < PPL; ++k) {
-    const Bil q = bil_at(L.w, L.h, x + w.oi[k], y + w.oj[k]);
-    im[k] = sel(w.on[k], bil_sample(L.img, q, L.w));
+    const Bil qb = bil_at(B.w, B.h, x2 + w.oi[k], y2 + w.oj[k]);
+    const Corners bi = corner_load(B.img, qb, B.w);
+    Corners bx{}, by{}, ai{}, ax{}, ay{};
+    Bil qa = qb;
     if (grads) {
-      gx[k] = sel(w.on[k], bil_sample(L.gx, q, L.w));
-      gy[k] = sel(w.on[k], bil_sample(L.gy, q, L.w));
-    } else {
-      gx[k] = gy[k] = 0.0f;
+      bx = corner_load(B.gx, qb, B.w);
+      by = corner_load(B.gy, qb, B.w);
+    }
+    if (first) {
+      qa = bil_at(A.w, A.h, x1 + w.oi[k], y1 + w.oj[k]);
+      ai = corner_load(A.img, qa, A.w);
+      ax = corner_load(A.gx, qa, A.w);
+      ay = corner_load(A.gy, qa, A.w);
+    }
+    b_im[k] = sel(w.on[k], corner_interp(qb, bi));
+    b_gx[k] = grads ? sel(w.on[k], corner_interp(qb, bx)) : 0.0f;
+    b_gy[k] = grads ? sel(w.on[k], corner_interp(qb, by)) : 0.0f;
+    if (first) {
+      a_im[k] = sel(w.on[k], corner_interp(qa, ai));
+      a_gx[k] = sel(w.on[k], corner_interp(qa, ax));
+      a_gy[k] = sel(w.on[k], corner_interp(qa, ay));
     }
   }
 }
 
 // one pass: img2 planes at (x2, y2) (grads = false: img only) and, on a
 // level's first pass, the img1 planes at (x1, y1)
-template <int G, int PPL, bool PATCH>
-__device__ __forceinline__ void gather_pass(const TrkLevel &A, const TrkLevel &B, const GroupWin<G, PPL, PATCH> &w,
+template <int G, int PPL, bool PATCH, int WIN>
+__device__ __forceinline__ void gather_pass(const TrkLevel &A, const TrkLevel &B, const GroupWin<G, PPL, PATCH, WIN> &w,
                                             float x1, float y1, float x2, float y2, bool first, bool grads,
                                             int lane, float (&a_im)[PPL], float (&a_gx)[PPL], float (&a_gy)[PPL],
                                             float (&b_im)[PPL], float (&b_gx)[PPL], float (&b_gy)[PPL]) {
@@ -916,8 +970,7 @@ __device__ __forceinline__ void gather_pass(const TrkLevel &A, const TrkLevel &B
       return;
     }
   }
-  gather_direct(B, w, x2, y2, grads, b_im, b_gx, b_gy);
-  if (first) gather_direct(A, w, x1, y1, true, a_im, a_gx, a_gy);
+  gather_direct2(A, B, w, x1, y1, x2, y2, first, grads, a_im, a_gx, a_gy, b_im, b_gx, b_gy);
 }
 
 __device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
@@ -946,11 +999,11 @@ __device__ __forceinline__ int uni(int v) {
 // trips instead of k+2.  The order of tests is the reference's: window test
 // at the top of each iteration and once after the loop (same x2, same test),
 // SMALL_DET ends the loop before x2 moves, residue only for TRACKED.
-template <int G, int PPL, bool PATCH, bool EXACT, bool LI>
-__device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, PATCH> &w, const TrkLevel &A,
+template <int G, int PPL, bool PATCH, int WIN, bool EXACT, bool LI>
+__device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, PATCH, WIN> &w, const TrkLevel &A,
                              const TrkLevel &B, float x1, float y1, float &x2, float &y2, bool live, int lane,
                              float *red) {
-  const int ww = a.ww, wh = a.wh, npx = ww * wh, hw = ww / 2, hh = wh / 2;
+  const int ww = WIN ? WIN : a.ww, wh = WIN ? WIN : a.wh, npx = ww * wh, hw = ww / 2, hh = wh / 2;
   const int nc = A.w, nr = A.h;
   const float n = (float)(ww * wh);
 
@@ -972,7 +1025,7 @@ __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, 
     float b_im[PPL], b_gx[PPL], b_gy[PPL];
     const bool grads = wave_any(act && !fin);  // a residue-only pass needs img2 alone
     if (act) {  // img1 is sampled once per level, with the level's first img2 gather
-      gather_pass<G, PPL, PATCH>(A, B, w, x1, y1, x2, y2, first, grads, lane, a_im, a_gx, a_gy, b_im, b_gx,
+      gather_pass<G, PPL, PATCH, WIN>(A, B, w, x1, y1, x2, y2, first, grads, lane, a_im, a_gx, a_gy, b_im, b_gx,
                                  b_gy);
     } else {
 #pragma unroll
@@ -995,7 +1048,7 @@ __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, 
         mom[2][k] = a_im[k] * a_im[k];
         mom[3][k] = b_im[k] * b_im[k];
       }
-      sums_g<G, 4, PPL, PATCH, EXACT>(w, mom, red, a.red_pitch, npx, lane, S);
+      sums_g<G, 4, PPL, PATCH, WIN, EXACT>(w, mom, red, a.red_pitch, npx, lane, S);
       alpha = (float)sqrt((double)((S[2] / n) / (S[3] / n)));
       beta = S[0] / n - alpha * (S[1] / n);
       alpha_g = (float)sqrt((double)((S[0] / n) / (S[1] / n)));
@@ -1011,7 +1064,7 @@ __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, 
         const float d = LI ? (a_im[k] - b_im[k] * alpha - beta) : (a_im[k] - b_im[k]);
         dif[0][k] = res ? fabsf(d) : 0.0f;
       }
-      sums_g<G, 1, PPL, PATCH, EXACT>(w, dif, red, a.red_pitch, npx, lane, S);
+      sums_g<G, 1, PPL, PATCH, WIN, EXACT>(w, dif, red, a.red_pitch, npx, lane, S);
       if (res) {
         if (S[0] / n > a.max_res) status = kLargeResidue;
         act = false;
@@ -1051,7 +1104,7 @@ __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, 
 #endif
     PROF_ADD(0, t_g0);
     PROF_T(t_s0);
-    sums_g<G, 5, PPL, PATCH, EXACT>(w, prod, red, a.red_pitch, npx, lane, S);
+    sums_g<G, 5, PPL, PATCH, WIN, EXACT>(w, prod, red, a.red_pitch, npx, lane, S);
     PROF_ADD(1, t_s0);
     PROF_T(t_v0);
     if (step) {
@@ -1083,8 +1136,8 @@ __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, 
 }
 
 // one frame of KLTTrackFeatures for the feature of this lane's group (:1348-1437)
-template <int G, int PPL, bool PATCH, bool EXACT, bool LI, class LevA, class LevB>
-__device__ __forceinline__ void track_feature_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, PATCH> &w,
+template <int G, int PPL, bool PATCH, int WIN, bool EXACT, bool LI, class LevA, class LevB>
+__device__ __forceinline__ void track_feature_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, PATCH, WIN> &w,
                                                 LevA LA,
                                                 LevB LB,
                                                 float &fx, float &fy, int &fv, bool live, int lane,
@@ -1105,7 +1158,7 @@ __device__ __forceinline__ void track_feature_g(PROF_DECL const TrkArgs &a, cons
       xo = uni<G>(xo * a.ss);
       yo = uni<G>(yo * a.ss);
     }
-    const int v = track_level_g<G, PPL, PATCH, EXACT, LI>(PROF_ARG a, w, LA(r), LB(r), xl, yl, xo, yo, go, lane, red);
+    const int v = track_level_g<G, PPL, PATCH, WIN, EXACT, LI>(PROF_ARG a, w, LA(r), LB(r), xl, yl, xo, yo, go, lane, red);
     if (go) {
       val = v;
       if (v == kSmallDet || v == kOOB) go = false;
@@ -1129,7 +1182,7 @@ __device__ __forceinline__ void track_feature_g(PROF_DECL const TrkArgs &a, cons
   }
 }
 
-template <int G, int PPL, bool PATCH, bool EXACT, bool LI>
+template <int G, int PPL, bool PATCH, int WIN, bool EXACT, bool LI>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KLT_TRACK_WAVES))) void k_track_frames_g(TrkArgs a, TrkFramesArgs b, float *__restrict__ fx,
                                                            float *__restrict__ fy, int *__restrict__ fv, int n) {
   constexpr int LG = kWave / G;
@@ -1150,7 +1203,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KLT_TRAC
     y = uni<G>(fy[f]);
     v = uni<G>(fv[f]);
   }
-  const GroupWin<G, PPL, PATCH> w = group_window<G, PPL, PATCH>(a.ww, a.wh, lane);
+  const GroupWin<G, PPL, PATCH, WIN> w = group_window<G, PPL, PATCH, WIN>(a.ww, a.wh, lane);
   {  // row pads of the ordered-sum staging stay +0 for the whole kernel
     float *red = red_all[wave];
     constexpr int RED = 5 * G * (LG * PPL + 4) + 16;
@@ -1166,7 +1219,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KLT_TRAC
     const bool live = exists && v >= 0;  // lost features are not tracked (:1346)
     PROF_T(t_f0);
     if (wave_any(live)) {
-      track_feature_g<G, PPL, PATCH, EXACT, LI>(
+      track_feature_g<G, PPL, PATCH, WIN, EXACT, LI>(
           PROF_ARG a, w, [&](int r) { return j == 0 ? a.A[r] : at_frame(a.B[r], (long)(j - 1) * b.lfs[r]); },
           [&](int r) { return at_frame(a.B[r], (long)j * b.lfs[r]); }, x, y, v, live, lane, red_all[wave]);
     }
@@ -1314,6 +1367,8 @@ struct klt_hip_ctx {
   int track_group = 0;  // features per wave for small windows (0: default)
   int track_order = 0;  // 0: band-sorted, XCD-major processing order; 1: input order
   int track_patch = 1;  // one-feature waves gather through a lane patch when the window fits
+  int serial_frames = 1;  // klt_hip_track_frames: 1 builds and tracks on one stream (default: the
+                          // tracker and the pyramid kernels compete for the same CUs; overlap buys ~3 %)
   int *d_perm = nullptr;
   size_t perm_cap = 0;
 #ifdef KLT_TRACK_PROF
@@ -1567,13 +1622,13 @@ void fill_trk_args(const klt_hip_track_desc *d, int nlev, int ss, int ncols, int
   a.red_pitch = rp;
 }
 
-template <int G, int PPL, bool PATCH, bool EXACT, bool LI>
+template <int G, int PPL, bool PATCH, int WIN, bool EXACT, bool LI>
 void launch_track_frames_g(hipStream_t st, const TrkArgs &a, const TrkFramesArgs &b, float *x, float *y, int *v,
                            int n) {
   const int per = (kBlock / kWave) * G;  // features per workgroup
   const int nb = (n + per - 1) / per;
   const int grid = b.xcd_per > 0 ? 8 * b.xcd_per : nb;
-  hipLaunchKernelGGL((k_track_frames_g<G, PPL, PATCH, EXACT, LI>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
+  hipLaunchKernelGGL((k_track_frames_g<G, PPL, PATCH, WIN, EXACT, LI>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
 }
 
 // fewer features than this: input order (the sort launch would not pay)
@@ -1587,14 +1642,16 @@ int track_group(const klt_hip_ctx *c, int npx, bool li) {
 }
 
 template <bool EXACT, bool LI>
-void launch_track_sel(int G, bool patch, int npx, hipStream_t st, const TrkArgs &a, const TrkFramesArgs &b,
-                      float *x, float *y, int *v, int n) {
-  if (G == 4) launch_track_frames_g<4, 4, false, EXACT, false>(st, a, b, x, y, v, n);
-  else if (G == 2) launch_track_frames_g<2, 2, false, EXACT, false>(st, a, b, x, y, v, n);
-  else if (patch) launch_track_frames_g<1, 1, true, EXACT, LI>(st, a, b, x, y, v, n);
-  else if (npx <= kWave) launch_track_frames_g<1, 1, false, EXACT, LI>(st, a, b, x, y, v, n);
-  else if (npx <= 4 * kWave) launch_track_frames_g<1, 4, false, EXACT, LI>(st, a, b, x, y, v, n);
-  else launch_track_frames_g<1, 16, false, EXACT, LI>(st, a, b, x, y, v, n);
+void launch_track_sel(int G, bool patch, bool win7, int npx, hipStream_t st, const TrkArgs &a,
+                      const TrkFramesArgs &b, float *x, float *y, int *v, int n) {
+  if (G == 4) launch_track_frames_g<4, 4, false, 0, EXACT, false>(st, a, b, x, y, v, n);
+  else if (G == 2) launch_track_frames_g<2, 2, false, 0, EXACT, false>(st, a, b, x, y, v, n);
+  else if (patch && win7) launch_track_frames_g<1, 1, true, 7, EXACT, LI>(st, a, b, x, y, v, n);
+  else if (patch) launch_track_frames_g<1, 1, true, 0, EXACT, LI>(st, a, b, x, y, v, n);
+  else if (win7) launch_track_frames_g<1, 1, false, 7, EXACT, LI>(st, a, b, x, y, v, n);
+  else if (npx <= kWave) launch_track_frames_g<1, 1, false, 0, EXACT, LI>(st, a, b, x, y, v, n);
+  else if (npx <= 4 * kWave) launch_track_frames_g<1, 4, false, 0, EXACT, LI>(st, a, b, x, y, v, n);
+  else launch_track_frames_g<1, 16, false, 0, EXACT, LI>(st, a, b, x, y, v, n);
 }
 
 int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc *d, const TrkArgs &a,
@@ -1604,6 +1661,8 @@ int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc
   const bool exact = d->reduction == KLT_HIP_EXACT, li = d->lighting_insensitive != 0;
   const int G = track_group(c, npx, li);
   const bool patch = G == 1 && c->track_patch && (d->window_width + 1) * (d->window_height + 1) <= kWave;
+  // the default 7x7 window gets compile-time window geometry (unrolled ordered sums)
+  const bool win7 = G == 1 && d->window_width == 7 && d->window_height == 7;
   TrkFramesArgs bb = b;
   if (c->track_order == 0 && n >= kOrderMin) {
     if (grow(c, &c->d_perm, &c->perm_cap, (size_t)n)) return -1;
@@ -1618,11 +1677,11 @@ int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc
 #endif
   const TrkFramesArgs &b2 = bb;
   if (exact) {
-    if (li) launch_track_sel<true, true>(G, patch, npx, st, a, b2, x, y, v, n);
-    else launch_track_sel<true, false>(G, patch, npx, st, a, b2, x, y, v, n);
+    if (li) launch_track_sel<true, true>(G, patch, win7, npx, st, a, b2, x, y, v, n);
+    else launch_track_sel<true, false>(G, patch, win7, npx, st, a, b2, x, y, v, n);
   } else {
-    if (li) launch_track_sel<false, true>(G, patch, npx, st, a, b2, x, y, v, n);
-    else launch_track_sel<false, false>(G, patch, npx, st, a, b2, x, y, v, n);
+    if (li) launch_track_sel<false, true>(G, patch, win7, npx, st, a, b2, x, y, v, n);
+    else launch_track_sel<false, false>(G, patch, win7, npx, st, a, b2, x, y, v, n);
   }
   return check_launch(c, "k_track_frames");
 }
@@ -1878,6 +1937,12 @@ KLT_API int klt_hip_set_prof(klt_hip_ctx *c, void *dev) {
   return 0;
 }
 #endif
+
+KLT_API int klt_hip_set_frames_overlap(klt_hip_ctx *c, int overlap) {
+  if (!c) return fail(c, "set_frames_overlap: null context");
+  c->serial_frames = overlap ? 0 : 1;
+  return 0;
+}
 
 KLT_API int klt_hip_set_track_patch(klt_hip_ctx *c, int on) {
   if (!c) return fail(c, "set_track_patch: null context");
@@ -2145,21 +2210,24 @@ KLT_API int klt_hip_track_frames(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, con
     c->bank_next = (bi + 1) % 3;
     Bank &K = c->bank[bi];
     const unsigned char *src = frames + (long)j0 * stride;
-    HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_bfree[bi], 0));
+    // overlapped: the pyramid stream builds chunk c+1 while chunk c is tracked;
+    // serial: both on the tracking stream (no two kernels share the CUs)
+    hipStream_t ps = c->serial_frames ? c->stream : c->pstream;
+    HIPCHK(c, hipStreamWaitEvent(ps, c->ev_bfree[bi], 0));
     if (fz) {
-      if (build_fused_bank(c, K, pd, src, pitch, stride, Fc, c->pstream)) return -1;
+      if (build_fused_bank(c, K, pd, src, pitch, stride, Fc, ps)) return -1;
     } else {
       for (int f = 0; f < Fc; ++f) {
-        if (build_pyramid_on(c, kScratchSlot, pd, src + (long)f * stride, pitch, 0, c->pstream)) return -1;
+        if (build_pyramid_on(c, kScratchSlot, pd, src + (long)f * stride, pitch, 0, ps)) return -1;
         for (int l = 0; l < pd->nlevels; ++l) {
           const Level &L = c->slot[kScratchSlot].lv[l];
           const long off = (long)f * L.w * L.h;
-          if (copy_level_planes(c, L, K.lv[l].img + off, K.lv[l].gx + off, K.lv[l].gy + off, c->pstream))
+          if (copy_level_planes(c, L, K.lv[l].img + off, K.lv[l].gx + off, K.lv[l].gy + off, ps))
             return -1;
         }
       }
     }
-    HIPCHK(c, hipEventRecord(c->ev_bbuilt[bi], c->pstream));
+    HIPCHK(c, hipEventRecord(c->ev_bbuilt[bi], ps));
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_bbuilt[bi], 0));
     TrkFramesArgs b;
     memset(&b, 0, sizeof b);

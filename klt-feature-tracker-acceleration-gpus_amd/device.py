@@ -63,6 +63,7 @@ DEVICE_PROTOS = {
     "klt_hip_set_track_group": (C.c_int, [V, C.c_int]),
     "klt_hip_set_track_order": (C.c_int, [V, C.c_int]),
     "klt_hip_set_track_patch": (C.c_int, [V, C.c_int]),
+    "klt_hip_set_frames_overlap": (C.c_int, [V, C.c_int]),
     "klt_hip_set_path": (C.c_int, [V, C.c_int]),
     "klt_hip_level_dims": (C.c_int, [V, C.c_int, C.c_int, IP, IP]),
     "klt_hip_download_level": (C.c_int, [V, C.c_int, C.c_int, C.c_int, V]),

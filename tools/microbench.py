@@ -30,6 +30,7 @@ def main():
     ap.add_argument("mode", choices=["pyr", "track", "frames", "api"])
     ap.add_argument("--prof", action="store_true",
                     help="per-wave phase cycles (needs KLT_AMD_LIB=.../lib/prof/libklt_amd.so)")
+    ap.add_argument("--serial", action="store_true", help="frames: pyramids and tracking on one stream")
     ap.add_argument("--no-patch", action="store_true", help="tracker: per-pixel gathers only")
     ap.add_argument("--input-order", action="store_true", help="tracker: no band ordering")
     ap.add_argument("--group", type=int, default=0, help="tracker: features per wave (0 default, 1, 2, 4)")
@@ -61,6 +62,7 @@ def main():
     check(lib, ctx, lib.klt_hip_set_track_group(ctx, a.group), "group")
     check(lib, ctx, lib.klt_hip_set_track_order(ctx, 1 if a.input_order else 0), "order")
     check(lib, ctx, lib.klt_hip_set_track_patch(ctx, 0 if a.no_patch else 1), "patch")
+    check(lib, ctx, lib.klt_hip_set_frames_overlap(ctx, 0 if a.serial else 1), "overlap")
     nf = max(a.frames, 2)
     frames = lib.klt_hip_malloc(ctx, nf * W * H)
     check(lib, ctx, lib.klt_hip_synth_frames(ctx, 1080, 0, nf, W, H, frames, W, W * H), "synth")
