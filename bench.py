@@ -41,12 +41,17 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=489)
-    p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--width", type=int, default=1920)
-    p.add_argument("--height", type=int, default=1080)
-    p.add_argument("--features", type=int, default=5000)
-    p.add_argument("--seed", type=int, default=1080)
+    p.add_argument("--mode", choices=["sequences", "sharded"], default="sequences",
+                   help="sequences: one independent sequence per GPU (configs 3/5, weak scaling); "
+                        "sharded: one 4K sequence, features sharded by row band over the GPUs (config 4, "
+                        "strong scaling)")
+    p.add_argument("--steps", type=int, default=None, help="timed frames (default 489; sharded 490)")
+    p.add_argument("--warmup", type=int, default=None, help="untimed frames (default 10; sharded 64)")
+    p.add_argument("--width", type=int, default=None, help="default 1920 (sharded 3840)")
+    p.add_argument("--height", type=int, default=None, help="default 1080 (sharded 2160)")
+    p.add_argument("--features", type=int, default=None, help="default 5000 (sharded 20000)")
+    p.add_argument("--seed", type=int, default=None, help="default 1080 (sharded 2160)")
+    p.add_argument("--margin", type=int, default=128, help="sharded: level-0 rows built beyond a band")
     p.add_argument("--cpu-frames", type=int, default=160,
                    help="frames of the bounded CPU-baseline sample (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
@@ -58,7 +63,13 @@ def parse():
                    help="build chunk c+1's pyramids on a second stream while chunk c is tracked")
     p.add_argument("--event-timing", choices=["timed", "replay"], default="replay",
                    help="record per-kernel HIP events inside the timed region or in a replay")
-    return p.parse_args()
+    a = p.parse_args()
+    sharded = a.mode == "sharded"
+    for k, dflt, shd in (("steps", 489, 490), ("warmup", 10, 64), ("width", 1920, 3840), ("height", 1080, 2160),
+                         ("features", 5000, 20000), ("seed", 1080, 2160)):
+        if getattr(a, k) is None:
+            setattr(a, k, shd if sharded else dflt)
+    return a
 
 
 def main() -> None:
@@ -67,7 +78,7 @@ def main() -> None:
     import torch.distributed as dist
 
     import kltamd
-    from kltamd.device import EXACT, FAST, PyrDesc, Timing, TrackDesc, check
+    from kltamd.device import EXACT, FAST, PyrDesc, Timing, TrackDesc, check, use_torch_stream
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -75,10 +86,18 @@ def main() -> None:
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # rehearsal only (KLT_BENCH_SHARE_GPU=1): every rank on GPU 0, gloo instead of RCCL
+    share = os.environ.get("KLT_BENCH_SHARE_GPU") == "1"
+    gpu_index = 0 if share else local
+    torch.cuda.set_device(gpu_index)
+    dev = torch.device("cuda", gpu_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+    if args.mode == "sharded":
+        return run_sharded(args, world, rank, dev)
 
     lib = kltamd.load()
     lib.KLTSetVerbosity(0)
@@ -91,8 +110,7 @@ def main() -> None:
     lib.klt_amd_set_reduction(tc, EXACT if args.reduction == "exact" else FAST)
     ctx = lib.klt_amd_device_context(tc)
     check(lib, ctx, lib.klt_hip_set_frames_overlap(ctx, 1 if args.overlap else 0), "overlap")
-    stream = torch.cuda.current_stream(dev)
-    check(lib, ctx, lib.klt_hip_set_stream(ctx, C.c_void_p(stream.cuda_stream)), "set_stream")
+    use_torch_stream(lib, ctx, dev)  # library kernels and torch ops ordered on one stream
 
     # frames straight into HBM (torch owns the memory; the library only sees pointers)
     frames = torch.empty((nframes, H, W), dtype=torch.uint8, device=dev)
@@ -248,6 +266,94 @@ def main() -> None:
         dist.destroy_process_group()
 
 
+def run_sharded(args, world, rank, dev) -> None:
+    """BASELINE config 4: one sequence (default 4K, 20k features); every rank
+    builds pyramids for its row band (+margin) and tracks the features it owns;
+    one all-reduce of the owners' (x, y, val) per chunk (kltamd.shard)."""
+    import torch
+    import torch.distributed as dist
+
+    import kltamd
+    from kltamd.device import EXACT, FAST, PyrDesc, TrackDesc, check, use_torch_stream
+    from kltamd.shard import ShardedSequence
+
+    lib = kltamd.load()
+    lib.KLTSetVerbosity(0)
+    W, H, NF = args.width, args.height, args.features
+    nframes = 1 + args.warmup + args.steps
+    tc = lib.KLTCreateTrackingContext()
+    tc.contents.sequentialMode = 1
+    lib.klt_amd_set_reduction(tc, EXACT if args.reduction == "exact" else FAST)
+    ctx = lib.klt_amd_device_context(tc)
+    use_torch_stream(lib, ctx, dev)  # library kernels and torch ops ordered on one stream
+    frames = torch.empty((nframes, H, W), dtype=torch.uint8, device=dev)  # the same sequence on every rank
+    check(lib, ctx, lib.klt_hip_synth_frames(ctx, args.seed, 0, nframes, W, H, C.c_void_p(frames.data_ptr()),
+                                             W, W * H), "synth")
+    torch.cuda.synchronize()
+    f0 = frames[0].cpu().numpy()
+    fl = lib.KLTCreateFeatureList(NF)
+    lib.KLTSelectGoodFeatures(tc, f0.ctypes.data_as(C.POINTER(C.c_ubyte)), W, H, fl)
+    sel = np.array([[fl.contents.feature[k].contents.x, fl.contents.feature[k].contents.y,
+                     fl.contents.feature[k].contents.val] for k in range(NF)], np.float64)
+    lib.KLTFreeFeatureList(fl)
+    x = torch.from_numpy(sel[:, 0].astype(np.float32)).to(dev)
+    y = torch.from_numpy(sel[:, 1].astype(np.float32)).to(dev)
+    v = torch.from_numpy(sel[:, 2].astype(np.int32)).to(dev)
+    pd, td = PyrDesc(), TrackDesc()
+    lib.klt_amd_pyr_desc(tc, W, H, tc.contents.nPyramidLevels, 1, C.byref(pd))
+    lib.klt_amd_track_desc(tc, C.byref(td))
+
+    def all_reduce(t):
+        if world > 1:
+            dist.all_reduce(t)
+
+    seq = ShardedSequence(lib, ctx, pd, td, frames, x, y, v, rank, world, all_reduce, chunk=args.chunk or 32,
+                          margin=args.margin)
+    seq.begin(0)
+    seq.run(1, args.warmup)
+    live_before = int((v >= 0).sum().item())
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    seq.run(1 + args.warmup, args.steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    digest = int((x.view(torch.int32).to(torch.int64).sum() * 3 + y.view(torch.int32).to(torch.int64).sum() * 5
+                  + v.to(torch.int64).sum() * 7).item())
+    result = {
+        "metric": METRIC,
+        "value": args.steps / dt,
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1000.0 * dt / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": f"synthetic: include/klt_synth.h value-noise frames, (0.7,0.3) px/frame, seed {args.seed}",
+        "config": {"workload": f"{W}x{H}, {NF} features, one sequence, features sharded by row band over "
+                               f"{world} GPU(s) (BASELINE config 4)",
+                   "resolution": f"{W}x{H}", "features": NF, "frames": nframes, "chunk": args.chunk or 32,
+                   "margin_rows": args.margin, "parallelism": f"row-band feature sharding x{world}"},
+        "live_features": {"after_warmup": live_before, "at_end": int((v >= 0).sum().item())},
+        "chunks_redone_full_frame": seq.redone,
+        "state_digest": digest,
+    }
+    lib.KLTFreeTrackingContext(tc)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def cpu_leg(lib, frames, W, H, NF, args, tc, ctx, dev):
     """Bounded sample of the same workload on the host: the reference CPU path
     (oracle/_ref, built from /root/reference) or, if absent, the oracle port.
@@ -311,13 +417,13 @@ def gpu_sequence(lib, host, NF, chunk):
     chunk 0 -- frames + features in HBM) on the CPU sample's frames: select on
     frame 0, then track frames 1..S-1."""
     import torch
-    from kltamd.device import PyrDesc, TrackDesc, check
+    from kltamd.device import PyrDesc, TrackDesc, check, use_torch_stream
     H, W = host[0].shape
     tc = lib.KLTCreateTrackingContext()
     tc.contents.sequentialMode = 1
     ctx = lib.klt_amd_device_context(tc)
     dev = torch.device("cuda", torch.cuda.current_device())
-    check(lib, ctx, lib.klt_hip_set_stream(ctx, C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "stream")
+    use_torch_stream(lib, ctx, dev)
     fl = lib.KLTCreateFeatureList(NF)
     lib.KLTSelectGoodFeatures(tc, host[0].ctypes.data_as(C.POINTER(C.c_ubyte)), W, H, fl)
     x = torch.tensor([fl.contents.feature[k].contents.x for k in range(NF)], dtype=torch.float32, device=dev)

@@ -68,7 +68,7 @@ struct FusedTaps {
   float p[2 * RP + 1];  // pyramid gauss
 };
 
-__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+__host__ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 // ---------------------------------------------------------------------------
 // Fused pyramid kernels for the default parameters (sigma 0.7 / 1.0 / 3.6,
@@ -334,9 +334,9 @@ __global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ s
                                                    DefTaps T, int vec_u8, float *__restrict__ img0,
                                                    float *__restrict__ gx0, float *__restrict__ gy0,
                                                    float *__restrict__ hs, int hsW, int do_hs, int vec_out,
-                                                   long fs_src, long fs0, long fs_hs) {
+                                                   long fs_src, long fs0, long fs_hs, int ty0) {
   __shared__ __attribute__((aligned(16))) float lds[l0::LDS];
-  const int C0 = blockIdx.x * l0::TW, R0 = blockIdx.y * l0::TH;
+  const int C0 = blockIdx.x * l0::TW, R0 = (blockIdx.y + ty0) * l0::TH;
   // blockIdx.z: frame of a batch (frame strides in elements; 0 for one frame)
   src += blockIdx.z * fs_src;
   img0 += blockIdx.z * fs0;
@@ -371,7 +371,7 @@ static_assert(2 * LDS_X <= LDS_H, "tx/ty reuse the hs region");
 __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs, int W1, int H, int H1,
                                                    DefTaps T, int vec, float *__restrict__ img1,
                                                    float *__restrict__ gx1, float *__restrict__ gy1,
-                                                   long fs_hs, long fs1) {
+                                                   long fs_hs, long fs1, int ty0) {
   using namespace l1;
   hs += blockIdx.z * fs_hs;
   img1 += blockIdx.z * fs1;
@@ -383,7 +383,7 @@ __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs,
   float *tx = lds;          // [JH][TW]
   float *ty = lds + LDS_X;
 
-  const int x0 = blockIdx.x * TW, y0 = blockIdx.y * TH;
+  const int x0 = blockIdx.x * TW, y0 = (blockIdx.y + ty0) * TH;
   const int tid = threadIdx.x;
 
   {
@@ -589,6 +589,7 @@ __global__ __launch_bounds__(kBlock) void k_min_eigen(const float *__restrict__ 
 struct TrkLevel {
   const float *img, *gx, *gy;
   int w, h;
+  int vlo = 0, vhi = 1 << 30;  // rows that hold valid data (a band-built pyramid: fewer)
 };
 
 struct TrkArgs {
@@ -601,6 +602,7 @@ struct TrkArgs {
   int borderx, bordery, ncols, nrows;
   int li;
   int red_pitch;     // per-sum row pitch of the reduction staging area (floats)
+  int *escape;       // band mode: set when a window needs rows outside [vlo, vhi)
 };
 
 // _interpolate (trackFeatures.c:31-57); the clamp only guards addresses that
@@ -669,6 +671,7 @@ struct TrkFramesArgs {
   long lfs[KLT_HIP_MAX_LEVELS];  // bank frame stride per level (floats)
   int nframes;
   const int *perm;  // processing order (slot -> feature), nullptr: identity
+  const int *n_dev;  // non-null: number of slots to process (device value, <= n)
   int xcd_per;      // > 0: blockIdx -> XCD-major order, this many blocks per XCD
 #ifdef KLT_TRACK_PROF
   unsigned long long *prof;  // per wave: kProfN phase cycle counts (instrumented build only)
@@ -679,7 +682,7 @@ struct TrkFramesArgs {
 };
 
 __device__ __forceinline__ TrkLevel at_frame(const TrkLevel &L, long off) {
-  return TrkLevel{L.img + off, L.gx + off, L.gy + off, L.w, L.h};
+  return TrkLevel{L.img + off, L.gx + off, L.gy + off, L.w, L.h, L.vlo, L.vhi};
 }
 
 // ---------------------------------------------------------------------------
@@ -1019,6 +1022,16 @@ __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, 
       status = kOOB;
       act = false;
     }
+    if (a.escape && act) {
+      // band-built pyramids: every row the bilinear window touches must exist
+      const bool bad = (int)(y2 - hh) < B.vlo || (int)(y2 + hh) + 1 >= B.vhi ||
+                       (first && ((int)(y1 - hh) < A.vlo || (int)(y1 + hh) + 1 >= A.vhi));
+      if (bad) {
+        *a.escape = 1;  // the caller redoes the chunk from full-frame pyramids
+        status = kOOB;
+        act = false;
+      }
+    }
     if (!wave_any(act)) break;
     PROF_INC(6);
     PROF_T(t_g0);
@@ -1191,6 +1204,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KLT_TRAC
   // consecutive workgroups land on the 8 XCDs round-robin: give each XCD a
   // contiguous run of the (band-sorted) order so its L2 sees one image band
   const int blk = b.xcd_per > 0 ? (int)(blockIdx.x % 8) * b.xcd_per + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  if (b.n_dev) n = *b.n_dev;
   const int s0 = (blk * (kBlock / kWave) + wave) * G;
   if (s0 >= n) return;  // whole wave; the kernel has no workgroup barrier
   const int g = lane / LG, slot = s0 + g;
@@ -1253,13 +1267,17 @@ constexpr int kBands = 128, kSortThreads = 1024;
 
 __global__ __launch_bounds__(kSortThreads) void k_band_order(const float *__restrict__ fy,
                                                              const int *__restrict__ fv, int n, int nrows,
-                                                             int *__restrict__ perm) {
-  __shared__ int cnt[kBands + 1];
+                                                             int *__restrict__ perm, float own_lo, float own_hi,
+                                                             int *__restrict__ count) {
+  // count != nullptr: keep only live features with own_lo <= y < own_hi (a
+  // rank's band in sharded mode), *count = how many; else every feature
+  __shared__ int cnt[kBands + 2];
   const int t = threadIdx.x;
-  for (int i = t; i <= kBands; i += kSortThreads) cnt[i] = 0;
+  for (int i = t; i <= kBands + 1; i += kSortThreads) cnt[i] = 0;
   __syncthreads();
   const float scale = (float)kBands / (float)(nrows > 0 ? nrows : 1);
   auto band_of = [&](int i) {
+    if (count && !(fv[i] >= 0 && fy[i] >= own_lo && fy[i] < own_hi)) return kBands + 1;
     if (fv[i] < 0) return kBands;
     const float b = fy[i] * scale;
     return b >= 0.0f ? (b < (float)kBands ? (int)b : kBands - 1) : 0;  // NaN -> band 0
@@ -1268,14 +1286,18 @@ __global__ __launch_bounds__(kSortThreads) void k_band_order(const float *__rest
   __syncthreads();
   if (t == 0) {
     int run = 0;
-    for (int i = 0; i <= kBands; ++i) {
+    for (int i = 0; i <= kBands + 1; ++i) {
       const int c = cnt[i];
       cnt[i] = run;
       run += c;
     }
   }
   __syncthreads();
-  for (int i = t; i < n; i += kSortThreads) perm[atomicAdd(&cnt[band_of(i)], 1)] = i;
+  if (count && t == 0) *count = cnt[kBands + 1];  // start of the excluded bucket = kept features
+  for (int i = t; i < n; i += kSortThreads) {
+    const int bnd = band_of(i);
+    if (bnd <= kBands) perm[atomicAdd(&cnt[bnd], 1)] = i;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1331,6 +1353,7 @@ struct Bank {
   Level lv[KLT_HIP_MAX_LEVELS];
   float *hs = nullptr;  // per-frame row pass of the sigma-3.6 smoothing (fused path)
   size_t hs_cap = 0;
+  int vlo[KLT_HIP_MAX_LEVELS] = {}, vhi[KLT_HIP_MAX_LEVELS] = {};  // rows built (band mode: a subset)
 };
 
 // where the pyramid preceding the next batch lives
@@ -1371,6 +1394,7 @@ struct klt_hip_ctx {
                           // tracker and the pyramid kernels compete for the same CUs; overlap buys ~3 %)
   int *d_perm = nullptr;
   size_t perm_cap = 0;
+  int *d_count = nullptr;  // band mode: features owned in this chunk
 #ifdef KLT_TRACK_PROF
   unsigned long long *prof = nullptr;
 #endif
@@ -1578,7 +1602,7 @@ int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t 
     TimedScope ts(c, T_L0, st);
     dim3 grid((W + l0::TW - 1) / l0::TW, (H + l0::TH - 1) / l0::TH);
     hipLaunchKernelGGL(k_pyr_l0, grid, dim3(kBlock), 0, st, src, (int)pitch, W, H, T, vec_u8, S.lv[0].img,
-                       S.lv[0].gx, S.lv[0].gy, c->d_hs, W1, (two && W1 > 0) ? 1 : 0, vec_out, 0L, 0L, 0L);
+                       S.lv[0].gx, S.lv[0].gy, c->d_hs, W1, (two && W1 > 0) ? 1 : 0, vec_out, 0L, 0L, 0L, 0);
     if (check_launch(c, "k_pyr_l0")) return -1;
   }
   if (two && (long)W1 * H1 > 0) {
@@ -1586,7 +1610,7 @@ int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t 
     const int vec = (W1 % 4 == 0 && W1 >= 8) ? 1 : 0;
     dim3 grid((W1 + l1::TW - 1) / l1::TW, (H1 + l1::TH - 1) / l1::TH);
     hipLaunchKernelGGL(k_pyr_l1, grid, dim3(l1::NT), 0, st, c->d_hs, W1, H, H1, T, vec, S.lv[1].img,
-                       S.lv[1].gx, S.lv[1].gy, 0L, 0L);
+                       S.lv[1].gx, S.lv[1].gy, 0L, 0L, 0);
     if (check_launch(c, "k_pyr_l1")) return -1;
   }
   return 0;
@@ -1654,8 +1678,9 @@ void launch_track_sel(int G, bool patch, bool win7, int npx, hipStream_t st, con
   else launch_track_frames_g<1, 16, false, 0, EXACT, LI>(st, a, b, x, y, v, n);
 }
 
+// own != nullptr (band mode): only live features with own[0] <= y < own[1]
 int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc *d, const TrkArgs &a,
-                        const TrkFramesArgs &b, float *x, float *y, int *v, int n) {
+                        const TrkFramesArgs &b, float *x, float *y, int *v, int n, const float *own = nullptr) {
   TimedScope ts(c, T_TRACK, st, b.nframes);
   const int npx = d->window_width * d->window_height;
   const bool exact = d->reduction == KLT_HIP_EXACT, li = d->lighting_insensitive != 0;
@@ -1664,10 +1689,13 @@ int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc
   // the default 7x7 window gets compile-time window geometry (unrolled ordered sums)
   const bool win7 = G == 1 && d->window_width == 7 && d->window_height == 7;
   TrkFramesArgs bb = b;
-  if (c->track_order == 0 && n >= kOrderMin) {
+  if (own || (c->track_order == 0 && n >= kOrderMin)) {
     if (grow(c, &c->d_perm, &c->perm_cap, (size_t)n)) return -1;
-    hipLaunchKernelGGL(k_band_order, dim3(1), dim3(kSortThreads), 0, st, y, v, n, a.nrows, c->d_perm);
+    if (own && !c->d_count) HIPCHK(c, hipMalloc((void **)&c->d_count, sizeof(int)));
+    hipLaunchKernelGGL(k_band_order, dim3(1), dim3(kSortThreads), 0, st, y, v, n, a.nrows, c->d_perm,
+                       own ? own[0] : 0.0f, own ? own[1] : 0.0f, own ? c->d_count : (int *)nullptr);
     if (check_launch(c, "k_band_order")) return -1;
+    if (own) bb.n_dev = c->d_count;
     const int per = (kBlock / kWave) * G, nb = (n + per - 1) / per;
     bb.perm = c->d_perm;
     bb.xcd_per = (nb + 7) / 8;
@@ -1724,9 +1752,12 @@ int ensure_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, int frames) 
   return 0;
 }
 
-// fused pyramids of F frames (src + f*stride) into bank K, two launches
+// fused pyramids of F frames (src + f*stride) into bank K, two launches.
+// Level-0 rows [row_lo, row_hi) are built (whole 32-row tiles, global
+// coordinates, so every built value is the full-frame value) and the level-1
+// tiles whose sigma-3.6 inputs lie inside them; K.vlo/vhi record what is valid.
 int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
-                     long stride, int F, hipStream_t st) {
+                     long stride, int F, hipStream_t st, int row_lo = 0, int row_hi = 1 << 30) {
   const int W = d->ncols, H = d->nrows;
   const DefTaps T = default_taps(d);
   const bool two = d->nlevels == 2;
@@ -1736,24 +1767,37 @@ int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const u
       (W % 4 == 0 && W >= 16 && pitch % 4 == 0 && stride % 4 == 0 && ((uintptr_t)src & 3) == 0) ? 1 : 0;
   const int vec_out = (W % 4 == 0) ? 1 : 0;
   const long fs0 = (long)W * H, fsh = (long)W1 * H, fs1 = (long)W1 * H1;
-  {
+  const int nty = (H + l0::TH - 1) / l0::TH;
+  const int ty0 = clampi(row_lo, 0, H) / l0::TH;
+  const int ty1 = row_hi >= H ? nty : clampi((row_hi + l0::TH - 1) / l0::TH, ty0, nty);
+  const int r0 = ty0 * l0::TH, r1 = ty1 >= nty ? H : ty1 * l0::TH;
+  K.vlo[0] = r0;
+  K.vhi[0] = r1 >= H ? (1 << 30) : r1;
+  if (ty1 > ty0) {
     TimedScope ts(c, T_L0, st, F);
-    dim3 grid((W + l0::TW - 1) / l0::TW, (H + l0::TH - 1) / l0::TH, F);
+    dim3 grid((W + l0::TW - 1) / l0::TW, ty1 - ty0, F);
     hipLaunchKernelGGL(k_pyr_l0, grid, dim3(kBlock), 0, st, src, (int)pitch, W, H, T, vec_u8, K.lv[0].img,
-                       K.lv[0].gx, K.lv[0].gy, K.hs, W1, (two && W1 > 0) ? 1 : 0, vec_out, stride, fs0, fsh);
+                       K.lv[0].gx, K.lv[0].gy, K.hs, W1, (two && W1 > 0) ? 1 : 0, vec_out, stride, fs0, fsh, ty0);
     if (check_launch(c, "k_pyr_l0")) return -1;
   }
   if (two && (long)W1 * H1 > 0) {
-    TimedScope ts(c, T_L1, st, F);
-    const int vec = (W1 % 4 == 0 && W1 >= 8) ? 1 : 0;
-    dim3 grid((W1 + l1::TW - 1) / l1::TW, (H1 + l1::TH - 1) / l1::TH, F);
-    hipLaunchKernelGGL(k_pyr_l1, grid, dim3(l1::NT), 0, st, K.hs, W1, H, H1, T, vec, K.lv[1].img, K.lv[1].gx,
-                       K.lv[1].gy, fsh, fs1);
-    if (check_launch(c, "k_pyr_l1")) return -1;
+    // an L1 tile at rows [y0, y0+8) reads hs rows [4*y0-20, 4*y0+52] (clamped to the image)
+    const int nt1 = (H1 + l1::TH - 1) / l1::TH;
+    const int t1lo = r0 == 0 ? 0 : (r0 + 20 + 4 * l1::TH - 1) / (4 * l1::TH);
+    const int t1hi = r1 >= H ? nt1 : (r1 >= 53 ? clampi((r1 - 53) / (4 * l1::TH) + 1, 0, nt1) : 0);
+    K.vlo[1] = t1lo * l1::TH;
+    K.vhi[1] = t1hi >= nt1 ? (1 << 30) : t1hi * l1::TH;
+    if (t1hi > t1lo) {
+      TimedScope ts(c, T_L1, st, F);
+      const int vec = (W1 % 4 == 0 && W1 >= 8) ? 1 : 0;
+      dim3 grid((W1 + l1::TW - 1) / l1::TW, t1hi - t1lo, F);
+      hipLaunchKernelGGL(k_pyr_l1, grid, dim3(l1::NT), 0, st, K.hs, W1, H, H1, T, vec, K.lv[1].img, K.lv[1].gx,
+                         K.lv[1].gy, fsh, fs1, t1lo);
+      if (check_launch(c, "k_pyr_l1")) return -1;
+    }
   }
   return 0;
 }
-
 }  // namespace
 
 // ===========================================================================
@@ -1812,6 +1856,7 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
     if (c->ev_bfree[k]) hipEventDestroy(c->ev_bfree[k]);
   }
   hipFree(c->d_perm);
+  hipFree(c->d_count);
   hipFree(c->d_hs);
   hipFree(c->d_fx);
   hipFree(c->d_fy);
@@ -2096,9 +2141,10 @@ TrkLevel prev_level(klt_hip_ctx *c, int l) {
     const Level &L = c->slot[kSeedSlot].lv[l];
     return TrkLevel{L.img, L.gx, L.gy, L.w, L.h};
   }
-  const Level &L = c->bank[c->prev.bank].lv[l];
+  const Bank &K = c->bank[c->prev.bank];
+  const Level &L = K.lv[l];
   const long off = (long)c->prev.frame * L.w * L.h;
-  return TrkLevel{L.img + off, L.gx + off, L.gy + off, L.w, L.h};
+  return TrkLevel{L.img + off, L.gx + off, L.gy + off, L.w, L.h, K.vlo[l], K.vhi[l]};
 }
 
 bool bank_fits(const Bank &K, const klt_hip_pyr_desc *d, int F) {
@@ -2134,10 +2180,17 @@ KLT_API int klt_hip_frames_begin(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, con
   return 0;
 }
 
-KLT_API int klt_hip_track_frames(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
-                                 const unsigned char *frames, long pitch, long stride, int nframes, int chunk,
-                                 float *x, float *y, int *val, int n, float *tab_x, float *tab_y, int *tab_val,
-                                 long tab_stride) {
+namespace {
+struct BandSpec {
+  float own[2];        // features owned: own[0] <= y < own[1] (level-0 rows) at the chunk start
+  int row_lo, row_hi;  // level-0 rows to build
+  int *escape;         // device flag
+};
+
+int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
+                      const unsigned char *frames, long pitch, long stride, int nframes, int chunk, float *x,
+                      float *y, int *val, int n, float *tab_x, float *tab_y, int *tab_val, long tab_stride,
+                      const BandSpec *band) {
   if (!c || !pd || !td) return fail(c, "track_frames: null argument");
   if (!c->frames_ready) return fail(c, "track_frames: no previous pyramid (call klt_hip_frames_begin)");
   if (nframes < 0 || chunk < 1 || n < 0) return fail(c, "track_frames: bad nframes/chunk/n");
@@ -2202,8 +2255,10 @@ KLT_API int klt_hip_track_frames(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, con
   HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
   HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_start, 0));
   const bool fz = fused_ok(pd) && !c->force_generic;
+  if (band && !fz) return fail(c, "track_frames_band: needs the fused (default-parameter) pyramid path");
   TrkArgs a;
   fill_trk_args(td, pd->nlevels, pd->nlevels > 1 ? pd->subsampling : 1, pd->ncols, pd->nrows, a);
+  if (band) a.escape = band->escape;
   for (int j0 = 0; j0 < nframes; j0 += F) {
     const int Fc = F < nframes - j0 ? F : nframes - j0;
     const int bi = c->bank_next;
@@ -2215,7 +2270,9 @@ KLT_API int klt_hip_track_frames(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, con
     hipStream_t ps = c->serial_frames ? c->stream : c->pstream;
     HIPCHK(c, hipStreamWaitEvent(ps, c->ev_bfree[bi], 0));
     if (fz) {
-      if (build_fused_bank(c, K, pd, src, pitch, stride, Fc, ps)) return -1;
+      if (band ? build_fused_bank(c, K, pd, src, pitch, stride, Fc, ps, band->row_lo, band->row_hi)
+               : build_fused_bank(c, K, pd, src, pitch, stride, Fc, ps))
+        return -1;
     } else {
       for (int f = 0; f < Fc; ++f) {
         if (build_pyramid_on(c, kScratchSlot, pd, src + (long)f * stride, pitch, 0, ps)) return -1;
@@ -2233,7 +2290,8 @@ KLT_API int klt_hip_track_frames(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, con
     memset(&b, 0, sizeof b);
     for (int l = 0; l < pd->nlevels; ++l) {
       a.A[l] = prev_level(c, l);
-      a.B[l] = TrkLevel{K.lv[l].img, K.lv[l].gx, K.lv[l].gy, K.lv[l].w, K.lv[l].h};
+      a.B[l] = TrkLevel{K.lv[l].img, K.lv[l].gx, K.lv[l].gy, K.lv[l].w, K.lv[l].h, fz ? K.vlo[l] : 0,
+                        fz ? K.vhi[l] : (1 << 30)};
       b.lfs[l] = (long)K.lv[l].w * K.lv[l].h;
     }
     b.nframes = Fc;
@@ -2243,11 +2301,31 @@ KLT_API int klt_hip_track_frames(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, con
       b.tv = tab_val + (long)j0 * tab_stride;
       b.tstride = tab_stride;
     }
-    if (n > 0 && track_frames_launch(c, c->stream, td, a, b, x, y, val, n)) return -1;
+    if (n > 0 && track_frames_launch(c, c->stream, td, a, b, x, y, val, n, band ? band->own : nullptr))
+      return -1;
     if (c->prev.bank >= 0) HIPCHK(c, hipEventRecord(c->ev_bfree[c->prev.bank], c->stream));
     c->prev = PrevRef{bi, Fc - 1};
   }
   return 0;
+}
+}  // namespace
+
+KLT_API int klt_hip_track_frames(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
+                                 const unsigned char *frames, long pitch, long stride, int nframes, int chunk,
+                                 float *x, float *y, int *val, int n, float *tab_x, float *tab_y, int *tab_val,
+                                 long tab_stride) {
+  return track_frames_impl(c, pd, td, frames, pitch, stride, nframes, chunk, x, y, val, n, tab_x, tab_y, tab_val,
+                           tab_stride, nullptr);
+}
+
+KLT_API int klt_hip_track_frames_band(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
+                                      const unsigned char *frames, long pitch, long stride, int nframes,
+                                      float *x, float *y, int *val, int n, float own_lo, float own_hi,
+                                      int row_lo, int row_hi, int *escape) {
+  if (!escape) return fail(c, "track_frames_band: null escape flag");
+  BandSpec bs{{own_lo, own_hi}, row_lo, row_hi, escape};
+  return track_frames_impl(c, pd, td, frames, pitch, stride, nframes, nframes > 0 ? nframes : 1, x, y, val, n,
+                           nullptr, nullptr, nullptr, 0, &bs);
 }
 
 KLT_API int klt_hip_min_eigen(klt_hip_ctx *c, int s, const klt_hip_select_desc *d, int *vals, int *nx,

@@ -5,6 +5,7 @@ feature arrays kept in HBM); the klt.h API (abi.py) is the drop-in surface.
 """
 from __future__ import annotations
 
+import ctypes
 import ctypes as C
 
 MAX_TAPS = 71
@@ -74,6 +75,8 @@ DEVICE_PROTOS = {
     "klt_hip_frames_begin": (C.c_int, [V, C.POINTER(PyrDesc), V, C.c_long]),
     "klt_hip_track_frames": (C.c_int, [V, C.POINTER(PyrDesc), C.POINTER(TrackDesc), V, C.c_long, C.c_long,
                                        C.c_int, C.c_int, V, V, V, C.c_int, V, V, V, C.c_long]),
+    "klt_hip_track_frames_band": (C.c_int, [V, C.POINTER(PyrDesc), C.POINTER(TrackDesc), V, C.c_long, C.c_long,
+                                            C.c_int, V, V, V, C.c_int, C.c_float, C.c_float, C.c_int, C.c_int, V]),
     "klt_hip_min_eigen": (C.c_int, [V, C.c_int, C.POINTER(SelectDesc), V, IP, IP]),
     "klt_hip_synth_frames": (C.c_int, [V, C.c_ulonglong, C.c_int, C.c_int, C.c_int, C.c_int, V,
                                        C.c_long, C.c_long]),
@@ -113,3 +116,17 @@ def check(lib: C.CDLL, ctx, rc: int, what: str) -> None:
     if rc != 0:
         msg = lib.klt_hip_last_error(ctx)
         raise DeviceError(f"{what}: {msg.decode() if msg else 'error'}")
+
+
+def use_torch_stream(lib, ctx, device=None):
+    """Run the library and torch on one stream.  torch's default stream is the
+    null stream (handle 0), which klt_hip_set_stream reads as "the context's
+    own non-blocking stream" -- unordered with torch.  So make a dedicated
+    torch stream current and hand that to the library.  Returns the stream."""
+    import torch
+    s = torch.cuda.current_stream(device)
+    if s.cuda_stream == 0:
+        s = torch.cuda.Stream(device)
+        torch.cuda.set_stream(s)
+    check(lib, ctx, lib.klt_hip_set_stream(ctx, ctypes.c_void_p(s.cuda_stream)), "set_stream")
+    return s

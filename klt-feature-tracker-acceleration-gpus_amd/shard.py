@@ -1,0 +1,118 @@
+"""Feature-sharded tracking across ranks (BASELINE config 4).
+
+Row-band decomposition: rank r of N owns the features whose y lies in its band
+[r*H/N, (r+1)*H/N) at the start of a chunk, builds pyramids only for its band
+plus a margin (klt_hip_track_frames_band), and tracks its features through the
+chunk.  After every chunk the ranks exchange results with one all-reduce of
+the 32-bit patterns of (x, y, val): every feature has exactly one contributor
+(its owner; rank 0 for lost features, which nobody tracks), so the sum is the
+owner's value bit for bit.  A feature whose window would leave a rank's built
+rows raises the chunk's escape flag; all ranks then redo that chunk from
+full-frame pyramids, so the result never depends on the margin.
+
+The data path has one collective per chunk (3*n int32, 240 KB at 20k
+features) -- the position exchange the path really has -- and no other.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import torch
+
+# level-0 rows built beyond the band: L1 tiles need ~52 rows of sigma-3.6
+# input on each side, the L1 window 4*(hh+1) more, plus a chunk of motion
+DEFAULT_MARGIN = 128
+
+
+@dataclass(frozen=True)
+class Band:
+    own_lo: float  # features with own_lo <= y < own_hi belong to the rank
+    own_hi: float
+    row_lo: int  # level-0 rows the rank builds
+    row_hi: int
+
+
+def band_of(nrows: int, world: int, rank: int, margin: int = DEFAULT_MARGIN) -> Band:
+    lo = rank * nrows // world
+    hi = (rank + 1) * nrows // world
+    own_lo = float("-inf") if rank == 0 else float(lo)
+    own_hi = float("inf") if rank == world - 1 else float(hi)
+    return Band(own_lo, own_hi, max(0, lo - margin), min(nrows, hi + margin))
+
+
+def owned_mask(y0: torch.Tensor, v0: torch.Tensor, band: Band) -> torch.Tensor:
+    """The features klt_hip_track_frames_band tracks for this band (same tests as k_band_order)."""
+    return (v0 >= 0) & (y0 >= band.own_lo) & (y0 < band.own_hi)
+
+
+def merge_chunk(x, y, v, y0, v0, band: Band, rank: int, all_reduce) -> None:
+    """In place, after one chunk: every rank ends with the owners' (x, y, val).
+    y0/v0 are the chunk-start state (ownership); lost features, which nobody
+    tracks, are contributed by rank 0."""
+    owned = owned_mask(y0, v0, band)
+    keep = owned | (v0 < 0) if rank == 0 else owned
+    bits = torch.stack([x.view(torch.int32), y.view(torch.int32), v.view(torch.int32)])
+    bits = torch.where(keep.unsqueeze(0), bits, torch.zeros_like(bits))
+    all_reduce(bits)
+    x.view(torch.int32).copy_(bits[0])
+    y.view(torch.int32).copy_(bits[1])
+    v.copy_(bits[2])
+
+
+class ShardedSequence:
+    """Drives klt_hip_track_frames_band chunk by chunk for one rank.
+
+    lib/ctx: the loaded library and a device context; pd/td: descriptors;
+    frames: device u8 frames (uint8 tensor [T, H, W]); x/y/v: device feature
+    arrays (identical on every rank at the start), on the stream the context
+    uses.  all_reduce(tensor) sums a device tensor over the ranks in place
+    (torch.distributed.all_reduce in production).
+    """
+
+    def __init__(self, lib, ctx, pd, td, frames: torch.Tensor, x, y, v, rank: int, world: int, all_reduce,
+                 chunk: int = 32, margin: int = DEFAULT_MARGIN):
+        from .device import check
+        self.lib, self.ctx, self.pd, self.td = lib, ctx, pd, td
+        self.frames, self.x, self.y, self.v = frames, x, y, v
+        self.rank, self.world, self.all_reduce, self.chunk = rank, world, all_reduce, chunk
+        T, H, W = frames.shape
+        self.H, self.W = H, W
+        self.band = band_of(H, world, rank, margin)
+        self.escape = torch.zeros(1, dtype=torch.int32, device=frames.device)
+        self.redone = 0
+        self._check = check
+
+    def _ptr(self, t: int) -> C.c_void_p:
+        return C.c_void_p(self.frames.data_ptr() + t * self.H * self.W)
+
+    def begin(self, t: int) -> None:
+        self._check(self.lib, self.ctx, self.lib.klt_hip_frames_begin(self.ctx, C.byref(self.pd), self._ptr(t),
+                                                                      self.W), "frames_begin")
+
+    def _band_call(self, t0: int, n: int, row_lo: int, row_hi: int) -> None:
+        b = self.band
+        self._check(self.lib, self.ctx, self.lib.klt_hip_track_frames_band(
+            self.ctx, C.byref(self.pd), C.byref(self.td), self._ptr(t0), self.W, self.H * self.W, n,
+            C.c_void_p(self.x.data_ptr()), C.c_void_p(self.y.data_ptr()), C.c_void_p(self.v.data_ptr()),
+            self.x.numel(), b.own_lo, b.own_hi, row_lo, row_hi, C.c_void_p(self.escape.data_ptr())),
+            "track_frames_band")
+
+    def run(self, t0: int, nframes: int) -> None:
+        """Track frames t0 .. t0+nframes-1 (the pyramid of t0-1 must be current:
+        begin(t0-1) first, or a previous run ending at t0-1)."""
+        for c0 in range(t0, t0 + nframes, self.chunk):
+            n = min(self.chunk, t0 + nframes - c0)
+            xs, ys, vs = self.x.clone(), self.y.clone(), self.v.clone()
+            self.escape.zero_()
+            self._band_call(c0, n, self.band.row_lo, self.band.row_hi)
+            flag = self.escape.clone()
+            self.all_reduce(flag)  # any rank escaped?
+            if int(flag.item()) != 0:
+                # redo the chunk from full-frame pyramids (exact whatever the motion)
+                self.redone += 1
+                self.x.copy_(xs), self.y.copy_(ys), self.v.copy_(vs)
+                self.begin(c0 - 1)
+                self.escape.zero_()
+                self._band_call(c0, n, 0, self.H)
+            merge_chunk(self.x, self.y, self.v, ys, vs, self.band, self.rank, self.all_reduce)

@@ -1,0 +1,203 @@
+"""Feature-sharded mode (BASELINE config 4): the exchange logic on CPU with a
+real world-size-2 gloo process group, band bookkeeping, and (GPU) bit-exact
+equality of the sharded sequence with the single-GPU one."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import synth
+
+import kltamd  # noqa: F401  (package import path)
+from kltamd.shard import Band, band_of, merge_chunk, owned_mask
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("H,world", [(480, 2), (2160, 8), (251, 3), (7, 4)])
+def test_bands_partition_rows_and_features(H, world):
+    bands = [band_of(H, world, r, margin=16) for r in range(world)]
+    assert bands[0].own_lo == float("-inf") and bands[-1].own_hi == float("inf")
+    for a, b in zip(bands, bands[1:]):
+        assert a.own_hi == b.own_lo
+    for b in bands:
+        assert 0 <= b.row_lo <= b.row_hi <= H
+    rng = np.random.default_rng(world)
+    y = torch.from_numpy(np.concatenate([rng.uniform(-5, H + 5, 500), [0.0, H - 1e-3, float(H)]]).astype(np.float32))
+    v = torch.from_numpy(rng.integers(-5, 1, y.numel()).astype(np.int32))
+    owners = sum(owned_mask(y, v, b).int() for b in bands)
+    assert torch.equal(owners, (v >= 0).int())  # every live feature has exactly one owner
+
+
+def _merge_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = 64
+        g = torch.Generator().manual_seed(7)
+        y0 = torch.rand(n, generator=g) * 100
+        v0 = torch.where(torch.rand(n, generator=g) < 0.2, torch.full((n,), -1), torch.zeros(n, dtype=torch.int64))
+        v0 = v0.to(torch.int32)
+        x0 = torch.rand(n, generator=g) * 100
+        band = band_of(100, world, rank, margin=0)
+        # each rank "tracks" its own features: a rank-specific result; others stale
+        owned = owned_mask(y0, v0, band)
+        x, y, v = x0.clone(), y0.clone(), v0.clone()
+        x[owned] = x0[owned] + 1000 * (rank + 1)
+        y[owned] = -1.0
+        v[owned] = -3 - rank
+        merge_chunk(x, y, v, y0.clone(), v0.clone(), band, rank, lambda t: dist.all_reduce(t))
+        q.put((rank, x.numpy(), y.numpy(), v.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_merge_chunk_gloo_world2():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_merge_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort(key=lambda t: t[0])
+    # both ranks hold identical arrays ...
+    for a, b in zip(res[0][1:], res[1][1:]):
+        assert np.array_equal(a.view(np.int32), b.view(np.int32))
+    # ... equal to the owners' values
+    n = 64
+    g = torch.Generator().manual_seed(7)
+    y0 = torch.rand(n, generator=g) * 100
+    v0 = torch.where(torch.rand(n, generator=g) < 0.2, torch.full((n,), -1), torch.zeros(n, dtype=torch.int64))
+    v0 = v0.to(torch.int32)
+    x0 = torch.rand(n, generator=g) * 100
+    x, y, v = x0.clone(), y0.clone(), v0.clone()
+    for r in range(world):
+        own = owned_mask(y0, v0, band_of(100, world, r, margin=0))
+        x[own] = x0[own] + 1000 * (r + 1)
+        y[own] = -1.0
+        v[own] = -3 - r
+    assert np.array_equal(res[0][1].view(np.int32), x.numpy().view(np.int32))
+    assert np.array_equal(res[0][2].view(np.int32), y.numpy().view(np.int32))
+    assert np.array_equal(res[0][3], v.numpy())
+
+
+# ---------------------------------------------------------------------------
+# GPU: ranks simulated one after another in one process (one context each)
+# ---------------------------------------------------------------------------
+def _select(gpu, frame, nfeat):
+    from kltabi import fl_to_arrays, u8ptr
+    h, w = frame.shape
+    tc = gpu.KLTCreateTrackingContext()
+    fl = gpu.KLTCreateFeatureList(nfeat)
+    gpu.KLTSelectGoodFeatures(tc, u8ptr(np.ascontiguousarray(frame)), w, h, fl)
+    x, y, v = fl_to_arrays(fl)
+    gpu.KLTFreeFeatureList(fl)
+    gpu.KLTFreeTrackingContext(tc)
+    return x, y, v
+
+
+class _Rank:
+    def __init__(self, gpu, dfr, H, W, world, rank, margin):
+        from kltamd.device import PyrDesc, TrackDesc
+        self.gpu, self.dfr, self.H, self.W = gpu, dfr, H, W
+        self.tc = gpu.KLTCreateTrackingContext()
+        self.tc.contents.sequentialMode = 1
+        self.ctx = gpu.klt_amd_device_context(self.tc)
+        from kltamd.device import use_torch_stream
+        use_torch_stream(gpu, self.ctx)
+        self.pd, self.td = PyrDesc(), TrackDesc()
+        gpu.klt_amd_pyr_desc(self.tc, W, H, self.tc.contents.nPyramidLevels, 1, C.byref(self.pd))
+        gpu.klt_amd_track_desc(self.tc, C.byref(self.td))
+        self.band = band_of(H, world, rank, margin)
+        self.rank = rank
+
+    def ptr(self, t):
+        return C.c_void_p(self.dfr.data_ptr() + t * self.H * self.W)
+
+    def begin(self, t):
+        assert self.gpu.klt_hip_frames_begin(self.ctx, C.byref(self.pd), self.ptr(t), self.W) == 0
+
+    def chunk(self, t0, n, x, y, v, esc, full=False):
+        b = self.band
+        rc = self.gpu.klt_hip_track_frames_band(
+            self.ctx, C.byref(self.pd), C.byref(self.td), self.ptr(t0), self.W, self.H * self.W, n,
+            C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()), x.numel(),
+            b.own_lo, b.own_hi, 0 if full else b.row_lo, self.H if full else b.row_hi, C.c_void_p(esc.data_ptr()))
+        assert rc == 0, self.gpu.klt_hip_last_error(self.ctx)
+
+
+def sharded_sequence(gpu, frames, nfeat, world, chunk, margin):
+    """Frames[0] selects; frames[1:] are tracked by `world` simulated ranks."""
+    H, W = frames[0].shape
+    dev = torch.device("cuda", 0)
+    dfr = torch.from_numpy(np.ascontiguousarray(np.stack(frames))).to(dev)
+    x0, y0, v0 = (torch.from_numpy(a).to(dev) for a in _select(gpu, frames[0], nfeat))
+    ranks = [_Rank(gpu, dfr, H, W, world, r, margin) for r in range(world)]
+    for rk in ranks:
+        rk.begin(0)
+    x, y, v = x0.clone(), y0.clone(), v0.clone()
+    redone = 0
+    T = len(frames) - 1
+    for c0 in range(1, 1 + T, chunk):
+        n = min(chunk, 1 + T - c0)
+        state = (x.clone(), y.clone(), v.clone())
+        outs, esc_any = [], 0
+        for rk in ranks:
+            xr, yr, vr = (s.clone() for s in state)
+            esc = torch.zeros(1, dtype=torch.int32, device=dev)
+            rk.chunk(c0, n, xr, yr, vr, esc)
+            esc_any += int(esc.item())
+            outs.append((xr, yr, vr))
+        if esc_any:
+            redone += 1
+            outs = []
+            for rk in ranks:
+                xr, yr, vr = (s.clone() for s in state)
+                esc = torch.zeros(1, dtype=torch.int32, device=dev)
+                rk.begin(c0 - 1)
+                rk.chunk(c0, n, xr, yr, vr, esc, full=True)
+                assert int(esc.item()) == 0
+                outs.append((xr, yr, vr))
+        # the all-reduce, done by hand: sum of the ranks' kept bit patterns
+        acc = None
+        for rk, (xr, yr, vr) in zip(ranks, outs):
+            parts = []
+
+            def fake_reduce(t, parts=parts):
+                parts.append(t.clone())
+            merge_chunk(xr, yr, vr, state[1], state[2], rk.band, rk.rank, fake_reduce)
+            acc = parts[0] if acc is None else acc + parts[0]
+        x.view(torch.int32).copy_(acc[0]), y.view(torch.int32).copy_(acc[1]), v.copy_(acc[2])
+    for rk in ranks:
+        gpu.KLTFreeTrackingContext(rk.tc)
+    return x.cpu().numpy(), y.cpu().numpy(), v.cpu().numpy(), redone
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,chunk,margin", [(2, 4, 128), (3, 5, 128), (4, 3, 40), (2, 4, 0)])
+def test_sharded_equals_single_gpu(gpu, oracle, world, chunk, margin):
+    from kltabi import OracleTracker
+    frames = synth(gpu, 2160 + world, 640, 480, 11)
+    x, y, v, redone = sharded_sequence(gpu, frames, 1500, world, chunk, margin)
+    X, Y, V = OracleTracker(oracle).harness(frames, 1500, 11, first=frames[0])
+    k = 11 - 2
+    assert np.array_equal(v, V[:, k])
+    assert np.array_equal(x.view(np.int32), X[:, k].view(np.int32))
+    assert np.array_equal(y.view(np.int32), Y[:, k].view(np.int32))
+    if margin == 0:
+        assert redone > 0  # no margin: features near band edges must escape and be redone
