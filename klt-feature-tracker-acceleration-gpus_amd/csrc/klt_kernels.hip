@@ -105,16 +105,23 @@ struct DefTaps {
   float p[21];  // pyramid gauss, reversed
 };
 
+#ifndef KLT_L0_TH
+#define KLT_L0_TH 32
+#endif
 namespace l0 {
-constexpr int RS = 2, RG = 3, RP = 10, SS = 4, TW = 64, TH = 32;
+constexpr int RS = 2, RG = 3, RP = 10, SS = 4, TW = 64, TH = KLT_L0_TH;
 constexpr int UQ = 24;            // staged u8 dwords per row: global [C0-12, C0+84)
 constexpr int UH = TH + 2 * RG + 2 * RS + 2;  // 44 rows: global R0-5 ..  (2 spare for 4-row blocks)
 constexpr int NG = 21;            // 4-column groups of t1 / img0: global [C0-8, C0+76)
 constexpr int IH = TH + 2 * RG;   // 38 img0 rows used (global R0-3 ..)
-constexpr int IHB = 10;           // 4-row blocks of img0 computed (40 rows)
+constexpr int IHB = (IH + 3) / 4;  // 4-row blocks of img0 computed
 // LDS pitches (floats) chosen with tools/lds_banks.py so that the 16-lane
 // groups of each ds_read_b128 hit (nearly) distinct bank slots
-constexpr int PU = 148, PT = 84, PI = 128, PX = TW;
+#ifndef KLT_L0_PU
+#define KLT_L0_PU 100  // u / img0 pitches: a few bank conflicts for a 4th block per CU
+#define KLT_L0_PI 92
+#endif
+constexpr int PU = KLT_L0_PU, PT = 84, PI = KLT_L0_PI, PX = TW;
 constexpr int REG_A = UH * PU;            // u8 (float) during A-B, then img0 during C-D
 constexpr int REG_B = 2 * IH * PX;        // t1 during B-C, then tx|ty during D-E
 constexpr int LDS = REG_A + REG_B;
@@ -345,7 +352,7 @@ __global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ s
   hs += blockIdx.z * fs_hs;
   // interior: unclamped aligned loads, no zero-border rule applies, all stores in bounds
   const bool interior = vec_u8 && vec_out && (hsW * l0::SS == W) && (hsW % 2 == 0) && C0 >= 12 && C0 + 84 <= W &&
-                        R0 >= 5 && R0 + 39 <= H;
+                        R0 >= 5 && R0 + l0::TH + 7 <= H;
   if (interior)
     pyr_l0_tile<true>(lds, src, spitch, W, H, T, vec_u8, img0, gx0, gy0, hs, hsW, do_hs, vec_out, C0, R0,
                       threadIdx.x);
@@ -358,11 +365,15 @@ __global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ s
 // k_pyr_l1: img1 = cols_p(hs) sampled at rows 4Y+2 (rest of pyramid.c:114-124)
 // and its gradients.  One 128-thread workgroup per 32x8 tile of level 1.
 // ---------------------------------------------------------------------------
+#ifndef KLT_L1_TH
+#define KLT_L1_TH 32
+#define KLT_L1_NT 256
+#endif
 namespace l1 {
-constexpr int RG = 3, RP = 10, SS = 4, TW = 32, TH = 8, NT = 128;
+constexpr int RG = 3, RP = 10, SS = 4, TW = 32, TH = KLT_L1_TH, NT = KLT_L1_NT;
 constexpr int JW = 40;              // img1 / hs columns: X in [x0-4, x0+36)
-constexpr int JH = TH + 2 * RG;     // 14 img1 rows: Y in [y0-3, y0+11)
-constexpr int HR = SS * (JH - 1) + 2 * RP + 1;  // 73 hs rows: [4y0-20, 4y0+53)
+constexpr int JH = TH + 2 * RG;     // img1 rows: Y in [y0-3, y0+TH+3)
+constexpr int HR = SS * (JH - 1) + 2 * RP + 1;  // hs rows: [4y0-20, 4y0-20+HR)
 constexpr int LDS_H = HR * JW, LDS_J = JH * JW, LDS_X = JH * TW;
 constexpr int LDS = LDS_H + LDS_J;
 static_assert(2 * LDS_X <= LDS_H, "tx/ty reuse the hs region");
@@ -1781,10 +1792,11 @@ int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const u
     if (check_launch(c, "k_pyr_l0")) return -1;
   }
   if (two && (long)W1 * H1 > 0) {
-    // an L1 tile at rows [y0, y0+8) reads hs rows [4*y0-20, 4*y0+52] (clamped to the image)
+    // an L1 tile at rows [y0, y0+TH) reads hs rows [4*y0-20, 4*y0-20+HR) (clamped to the image)
     const int nt1 = (H1 + l1::TH - 1) / l1::TH;
+    const int last = l1::HR - 20;  // 4*y0 + last is the last hs row read
     const int t1lo = r0 == 0 ? 0 : (r0 + 20 + 4 * l1::TH - 1) / (4 * l1::TH);
-    const int t1hi = r1 >= H ? nt1 : (r1 >= 53 ? clampi((r1 - 53) / (4 * l1::TH) + 1, 0, nt1) : 0);
+    const int t1hi = r1 >= H ? nt1 : (r1 > last ? clampi((r1 - last - 1) / (4 * l1::TH) + 1, 0, nt1) : 0);
     K.vlo[1] = t1lo * l1::TH;
     K.vhi[1] = t1hi >= nt1 ? (1 << 30) : t1hi * l1::TH;
     if (t1hi > t1lo) {
@@ -2252,8 +2264,10 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
       if (ensure_bank(c, K, pd, chunk)) return -1;
   }
   // the pyramid stream starts behind everything already queued on the tracking stream
-  HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
-  HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_start, 0));
+  if (!c->serial_frames) {
+    HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_start, 0));
+  }
   const bool fz = fused_ok(pd) && !c->force_generic;
   if (band && !fz) return fail(c, "track_frames_band: needs the fused (default-parameter) pyramid path");
   TrkArgs a;
@@ -2267,8 +2281,10 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     const unsigned char *src = frames + (long)j0 * stride;
     // overlapped: the pyramid stream builds chunk c+1 while chunk c is tracked;
     // serial: both on the tracking stream (no two kernels share the CUs)
-    hipStream_t ps = c->serial_frames ? c->stream : c->pstream;
-    HIPCHK(c, hipStreamWaitEvent(ps, c->ev_bfree[bi], 0));
+    const bool serial = c->serial_frames != 0;
+    hipStream_t ps = serial ? c->stream : c->pstream;
+    // one stream: stream order is the dependency (an event wait would add a queue barrier)
+    if (!serial) HIPCHK(c, hipStreamWaitEvent(ps, c->ev_bfree[bi], 0));
     if (fz) {
       if (band ? build_fused_bank(c, K, pd, src, pitch, stride, Fc, ps, band->row_lo, band->row_hi)
                : build_fused_bank(c, K, pd, src, pitch, stride, Fc, ps))
@@ -2284,8 +2300,10 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
         }
       }
     }
-    HIPCHK(c, hipEventRecord(c->ev_bbuilt[bi], ps));
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_bbuilt[bi], 0));
+    if (!serial) {
+      HIPCHK(c, hipEventRecord(c->ev_bbuilt[bi], ps));
+      HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_bbuilt[bi], 0));
+    }
     TrkFramesArgs b;
     memset(&b, 0, sizeof b);
     for (int l = 0; l < pd->nlevels; ++l) {
@@ -2303,7 +2321,7 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     }
     if (n > 0 && track_frames_launch(c, c->stream, td, a, b, x, y, val, n, band ? band->own : nullptr))
       return -1;
-    if (c->prev.bank >= 0) HIPCHK(c, hipEventRecord(c->ev_bfree[c->prev.bank], c->stream));
+    if (!serial && c->prev.bank >= 0) HIPCHK(c, hipEventRecord(c->ev_bfree[c->prev.bank], c->stream));
     c->prev = PrevRef{bi, Fc - 1};
   }
   return 0;
