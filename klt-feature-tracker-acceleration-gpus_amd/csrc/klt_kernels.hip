@@ -1016,7 +1016,7 @@ __device__ __forceinline__ int uni(int v) {
 template <int G, int PPL, bool PATCH, int WIN, bool EXACT, bool LI>
 __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, PATCH, WIN> &w, const TrkLevel &A,
                              const TrkLevel &B, float x1, float y1, float &x2, float &y2, bool live, int lane,
-                             float *red) {
+                             float *red, bool residue) {
   const int ww = WIN ? WIN : a.ww, wh = WIN ? WIN : a.wh, npx = ww * wh, hw = ww / 2, hh = wh / 2;
   const int nc = A.w, nr = A.h;
   const float n = (float)(ww * wh);
@@ -1043,6 +1043,11 @@ __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, 
         act = false;
       }
     }
+    // Above the finest level the residue cannot change the result: its status
+    // (LARGE_RESIDUE / MAX_ITERATIONS) is replaced by the next level's, only
+    // SMALL_DET and OOB stop the level loop (trackFeatures.c:1378), and the
+    // window test just above is the post-loop test.  No final gather there.
+    if (act && fin && !residue) act = false;
     if (!wave_any(act)) break;
     PROF_INC(6);
     PROF_T(t_g0);
@@ -1182,7 +1187,8 @@ __device__ __forceinline__ void track_feature_g(PROF_DECL const TrkArgs &a, cons
       xo = uni<G>(xo * a.ss);
       yo = uni<G>(yo * a.ss);
     }
-    const int v = track_level_g<G, PPL, PATCH, WIN, EXACT, LI>(PROF_ARG a, w, LA(r), LB(r), xl, yl, xo, yo, go, lane, red);
+    const int v = track_level_g<G, PPL, PATCH, WIN, EXACT, LI>(PROF_ARG a, w, LA(r), LB(r), xl, yl, xo, yo, go,
+                                                               lane, red, r == 0);
     if (go) {
       val = v;
       if (v == kSmallDet || v == kOOB) go = false;
