@@ -251,7 +251,9 @@ def main() -> None:
             try:
                 d = json.loads(pmc.read_text())
                 if d.get("resolution") == f"{W}x{H}":
-                    result["roofline"]["traffic"] = d.get("pass_hbm_bytes_per_launch")
+                    # per launch, like `achieved` (a launch covers frames_per_launch frames)
+                    result["roofline"]["traffic"] = d["pass_hbm_bytes_per_frame"] * fpl
+                    result["roofline"]["traffic_per_frame"] = d["pass_hbm_bytes_per_frame"]
                     result["roofline"]["traffic_source"] = str(pmc.relative_to(ROOT))
             except Exception:
                 pass

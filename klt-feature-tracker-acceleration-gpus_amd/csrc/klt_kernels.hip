@@ -128,6 +128,19 @@ constexpr int LDS = REG_A + REG_B;
 static_assert(IHB * 4 * PI <= REG_A && UH * PT <= REG_B, "LDS aliasing");
 }  // namespace l0
 
+// XCD-aware tile order: consecutive workgroups are dealt to the 8 XCDs in
+// turn, so workgroup w takes tile (w % 8) * per + w / 8 (grid.x = 8 * per) and
+// each XCD's L2 sees one contiguous band of rows -- the halo rows a tile
+// shares with its neighbours above and below are then mostly L2 hits.
+__device__ __forceinline__ bool xcd_tile(int tiles_x, int tiles_y, int &bx, int &by) {
+  const int per = (int)gridDim.x / 8;
+  const int t = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+  if (t >= tiles_x * tiles_y) return false;
+  by = t / tiles_x;
+  bx = t - by * tiles_x;
+  return true;
+}
+
 // Edge tiles clamp their loads and apply the zero-border rules per element;
 // interior tiles (~90 % at 1080p, 94 % at 4K) need neither.
 template <bool INT>
@@ -341,9 +354,12 @@ __global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ s
                                                    DefTaps T, int vec_u8, float *__restrict__ img0,
                                                    float *__restrict__ gx0, float *__restrict__ gy0,
                                                    float *__restrict__ hs, int hsW, int do_hs, int vec_out,
-                                                   long fs_src, long fs0, long fs_hs, int ty0) {
+                                                   long fs_src, long fs0, long fs_hs, int ty0, int tiles_x,
+                                                   int tiles_y) {
   __shared__ __attribute__((aligned(16))) float lds[l0::LDS];
-  const int C0 = blockIdx.x * l0::TW, R0 = (blockIdx.y + ty0) * l0::TH;
+  int bx, by;
+  if (!xcd_tile(tiles_x, tiles_y, bx, by)) return;  // whole workgroup: no barrier is skipped
+  const int C0 = bx * l0::TW, R0 = (by + ty0) * l0::TH;
   // blockIdx.z: frame of a batch (frame strides in elements; 0 for one frame)
   src += blockIdx.z * fs_src;
   img0 += blockIdx.z * fs0;
@@ -382,7 +398,7 @@ static_assert(2 * LDS_X <= LDS_H, "tx/ty reuse the hs region");
 __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs, int W1, int H, int H1,
                                                    DefTaps T, int vec, float *__restrict__ img1,
                                                    float *__restrict__ gx1, float *__restrict__ gy1,
-                                                   long fs_hs, long fs1, int ty0) {
+                                                   long fs_hs, long fs1, int ty0, int tiles_x, int tiles_y) {
   using namespace l1;
   hs += blockIdx.z * fs_hs;
   img1 += blockIdx.z * fs1;
@@ -394,7 +410,9 @@ __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs,
   float *tx = lds;          // [JH][TW]
   float *ty = lds + LDS_X;
 
-  const int x0 = blockIdx.x * TW, y0 = (blockIdx.y + ty0) * TH;
+  int bx, by;
+  if (!xcd_tile(tiles_x, tiles_y, bx, by)) return;
+  const int x0 = bx * TW, y0 = (by + ty0) * TH;
   const int tid = threadIdx.x;
 
   {
@@ -1492,6 +1510,9 @@ struct TimedScope {
 
 unsigned blocks_for(long n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
+// grid.x for xcd_tile: a multiple of 8 covering `tiles`
+unsigned xcd_grid(int tiles) { return (unsigned)(8 * ((tiles + 7) / 8)); }
+
 int check_launch(klt_hip_ctx *c, const char *what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(c, "launch %s: %s", what, hipGetErrorString(e));
@@ -1617,17 +1638,20 @@ int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t 
   const int vec_out = (W % 4 == 0) ? 1 : 0;
   {
     TimedScope ts(c, T_L0, st);
-    dim3 grid((W + l0::TW - 1) / l0::TW, (H + l0::TH - 1) / l0::TH);
+    const int tx = (W + l0::TW - 1) / l0::TW, ty = (H + l0::TH - 1) / l0::TH;
+    dim3 grid(xcd_grid(tx * ty));
     hipLaunchKernelGGL(k_pyr_l0, grid, dim3(kBlock), 0, st, src, (int)pitch, W, H, T, vec_u8, S.lv[0].img,
-                       S.lv[0].gx, S.lv[0].gy, c->d_hs, W1, (two && W1 > 0) ? 1 : 0, vec_out, 0L, 0L, 0L, 0);
+                       S.lv[0].gx, S.lv[0].gy, c->d_hs, W1, (two && W1 > 0) ? 1 : 0, vec_out, 0L, 0L, 0L, 0, tx,
+                       ty);
     if (check_launch(c, "k_pyr_l0")) return -1;
   }
   if (two && (long)W1 * H1 > 0) {
     TimedScope ts(c, T_L1, st);
     const int vec = (W1 % 4 == 0 && W1 >= 8) ? 1 : 0;
-    dim3 grid((W1 + l1::TW - 1) / l1::TW, (H1 + l1::TH - 1) / l1::TH);
+    const int tx = (W1 + l1::TW - 1) / l1::TW, ty = (H1 + l1::TH - 1) / l1::TH;
+    dim3 grid(xcd_grid(tx * ty));
     hipLaunchKernelGGL(k_pyr_l1, grid, dim3(l1::NT), 0, st, c->d_hs, W1, H, H1, T, vec, S.lv[1].img,
-                       S.lv[1].gx, S.lv[1].gy, 0L, 0L, 0);
+                       S.lv[1].gx, S.lv[1].gy, 0L, 0L, 0, tx, ty);
     if (check_launch(c, "k_pyr_l1")) return -1;
   }
   return 0;
@@ -1792,9 +1816,11 @@ int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const u
   K.vhi[0] = r1 >= H ? (1 << 30) : r1;
   if (ty1 > ty0) {
     TimedScope ts(c, T_L0, st, F);
-    dim3 grid((W + l0::TW - 1) / l0::TW, ty1 - ty0, F);
+    const int tx = (W + l0::TW - 1) / l0::TW;
+    dim3 grid(xcd_grid(tx * (ty1 - ty0)), 1, F);
     hipLaunchKernelGGL(k_pyr_l0, grid, dim3(kBlock), 0, st, src, (int)pitch, W, H, T, vec_u8, K.lv[0].img,
-                       K.lv[0].gx, K.lv[0].gy, K.hs, W1, (two && W1 > 0) ? 1 : 0, vec_out, stride, fs0, fsh, ty0);
+                       K.lv[0].gx, K.lv[0].gy, K.hs, W1, (two && W1 > 0) ? 1 : 0, vec_out, stride, fs0, fsh, ty0,
+                       tx, ty1 - ty0);
     if (check_launch(c, "k_pyr_l0")) return -1;
   }
   if (two && (long)W1 * H1 > 0) {
@@ -1808,9 +1834,10 @@ int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const u
     if (t1hi > t1lo) {
       TimedScope ts(c, T_L1, st, F);
       const int vec = (W1 % 4 == 0 && W1 >= 8) ? 1 : 0;
-      dim3 grid((W1 + l1::TW - 1) / l1::TW, t1hi - t1lo, F);
+      const int tx = (W1 + l1::TW - 1) / l1::TW;
+      dim3 grid(xcd_grid(tx * (t1hi - t1lo)), 1, F);
       hipLaunchKernelGGL(k_pyr_l1, grid, dim3(l1::NT), 0, st, K.hs, W1, H, H1, T, vec, K.lv[1].img, K.lv[1].gx,
-                         K.lv[1].gy, fsh, fs1, t1lo);
+                         K.lv[1].gy, fsh, fs1, t1lo, tx, t1hi - t1lo);
       if (check_launch(c, "k_pyr_l1")) return -1;
     }
   }

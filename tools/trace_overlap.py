@@ -48,3 +48,11 @@ print(f"span {span/1e3:.1f} us, busy(any) {total(allu)/1e3:.1f}, track {total(tr
       f"overlap {inter/1e3:.1f}")
 for s, e, k in ks[:40]:
     print(f"{k:6s} {(s-t0)/1e3:9.1f} {(e-t0)/1e3:9.1f} {(e-s)/1e3:8.1f}")
+
+# gaps between consecutive kernels (any kind)
+allk = sorted([(s, e, k) for s, e, k in ks])
+gaps = [allk[i + 1][0] - allk[i][1] for i in range(len(allk) - 1)]
+import statistics
+if gaps:
+    print("gap us: median", statistics.median(gaps) / 1e3, "mean", statistics.mean(gaps) / 1e3,
+          "max", max(gaps) / 1e3)
