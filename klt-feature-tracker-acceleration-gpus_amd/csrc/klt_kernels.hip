@@ -886,8 +886,17 @@ __device__ __forceinline__ void sums_g(const GroupWin<G, PPL, PATCH, WIN> &w, co
 // is formed, so a pass costs one memory round trip.
 struct PatchPos {
   bool ok;
+  int X0, Y0;    // patch origin (wave-uniform)
   unsigned off;  // byte offset of this lane's patch cell
   float w0, w1, w2, w3;
+};
+
+// img2 patch values of the last pass of a level: a Newton step that stays in
+// the same pixel cell (same patch origin) needs new weights, not new loads
+struct PatchCache {
+  bool valid = false, grads = false;
+  int X0 = 0, Y0 = 0;
+  float v0 = 0.0f, v1 = 0.0f, v2 = 0.0f;
 };
 
 template <int G, int PPL, bool PATCH, int WIN>
@@ -897,6 +906,8 @@ __device__ __forceinline__ PatchPos patch_pos(const GroupWin<G, PPL, PATCH, WIN>
   const int xt = (int)xs, yt = (int)ys;
   const int X0 = __builtin_amdgcn_readlane(xt, 0), Y0 = __builtin_amdgcn_readlane(yt, 0);
   q.ok = __builtin_amdgcn_ballot_w64(w.on[0] && !(xt == X0 + w.ci && yt == Y0 + w.cj)) == 0;
+  q.X0 = X0;
+  q.Y0 = Y0;
   const float ax = xs - xt, ay = ys - yt;
   q.w0 = (1.0f - ax) * (1.0f - ay);
   q.w1 = ax * (1.0f - ay);
@@ -976,15 +987,30 @@ template <int G, int PPL, bool PATCH, int WIN>
 __device__ __forceinline__ void gather_pass(const TrkLevel &A, const TrkLevel &B, const GroupWin<G, PPL, PATCH, WIN> &w,
                                             float x1, float y1, float x2, float y2, bool first, bool grads,
                                             int lane, float (&a_im)[PPL], float (&a_gx)[PPL], float (&a_gy)[PPL],
-                                            float (&b_im)[PPL], float (&b_gx)[PPL], float (&b_gy)[PPL]) {
+                                            float (&b_im)[PPL], float (&b_gx)[PPL], float (&b_gy)[PPL],
+                                            PatchCache &pc) {
   if constexpr (PATCH) {
     const PatchPos qb = patch_pos(w, B.w, B.h, x2, y2);
     const PatchPos qa = first ? patch_pos(w, A.w, A.h, x1, y1) : qb;
     if (qb.ok && qa.ok) {
-      float vb0 = patch_load(B.img, qb), vb1 = 0.0f, vb2 = 0.0f, va0 = 0.0f, va1 = 0.0f, va2 = 0.0f;
-      if (grads) {
-        vb1 = patch_load(B.gx, qb);
-        vb2 = patch_load(B.gy, qb);
+      float vb0, vb1 = 0.0f, vb2 = 0.0f, va0 = 0.0f, va1 = 0.0f, va2 = 0.0f;
+      if (pc.valid && pc.X0 == qb.X0 && pc.Y0 == qb.Y0 && (pc.grads || !grads)) {
+        vb0 = pc.v0;  // same cell as the last pass: its corners, this pass's weights
+        vb1 = pc.v1;
+        vb2 = pc.v2;
+      } else {
+        vb0 = patch_load(B.img, qb);
+        if (grads) {
+          vb1 = patch_load(B.gx, qb);
+          vb2 = patch_load(B.gy, qb);
+        }
+        pc.valid = true;
+        pc.grads = grads;
+        pc.X0 = qb.X0;
+        pc.Y0 = qb.Y0;
+        pc.v0 = vb0;
+        pc.v1 = vb1;
+        pc.v2 = vb2;
       }
       if (first) {
         va0 = patch_load(A.img, qa);
@@ -1002,6 +1028,7 @@ __device__ __forceinline__ void gather_pass(const TrkLevel &A, const TrkLevel &B
       return;
     }
   }
+  pc.valid = false;
   gather_direct2(A, B, w, x1, y1, x2, y2, first, grads, a_im, a_gx, a_gy, b_im, b_gx, b_gy);
 }
 
@@ -1041,6 +1068,7 @@ __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, 
 
   const bool x1_out = window_out(x1, y1, hw, hh, nc, nr);
   float a_im[PPL], a_gx[PPL], a_gy[PPL];
+  PatchCache pcache;     // img2 patch of the last pass (PATCH)
   bool act = live;       // still iterating
   bool fin = false;      // iterations over (converged or max_it): residue next
   int it = 0, status = kTracked;
@@ -1073,7 +1101,7 @@ __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, 
     const bool grads = wave_any(act && !fin);  // a residue-only pass needs img2 alone
     if (act) {  // img1 is sampled once per level, with the level's first img2 gather
       gather_pass<G, PPL, PATCH, WIN>(A, B, w, x1, y1, x2, y2, first, grads, lane, a_im, a_gx, a_gy, b_im, b_gx,
-                                 b_gy);
+                                      b_gy, pcache);
     } else {
 #pragma unroll
       for (int k = 0; k < PPL; ++k) b_im[k] = b_gx[k] = b_gy[k] = 0.0f;
