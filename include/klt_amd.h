@@ -24,6 +24,19 @@ void klt_amd_track_desc(KLT_TrackingContext tc, klt_hip_track_desc *desc);
 /* KLT_HIP_EXACT (default) or KLT_HIP_FAST; env KLT_AMD_REDUCTION=fast sets FAST */
 void klt_amd_set_reduction(KLT_TrackingContext tc, int reduction);
 
+/* The reference harness loop (example3.c:54-74 without REPLACE) in one call:
+     for (i = 1; i < nframes; i++) {
+       KLTTrackFeatures(tc, frames[i-1], frames[i], ncols, nrows, fl);
+       if (ft) KLTStoreFeatureList(fl, ft, ft_col + i - 1);
+     }
+   with bit-identical results (sequential mode included), run on the batched
+   device path: frames uploaded asynchronously in chunks, pyramids built and
+   features tracked 32 frames per launch.  Where one pyramid description
+   cannot serve every frame (a kernel-cache corner case) or internal images are
+   requested, it runs exactly that loop instead. */
+void KLTTrackSequence(KLT_TrackingContext tc, KLT_PixelType **frames, int nframes, int ncols, int nrows,
+                      KLT_FeatureList fl, KLT_FeatureTable ft, int ft_col);
+
 /* host side of the synthetic generator (include/klt_synth.h) */
 void klt_synth_frame(uint64_t seed, int t, int ncols, int nrows, unsigned char *out);
 /* the reference quicksort's permutation on {val, idx} pairs (test hook) */

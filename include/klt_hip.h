@@ -159,6 +159,18 @@ int klt_hip_track_frames(klt_hip_ctx *ctx, const klt_hip_pyr_desc *pdesc, const 
                          const unsigned char *frames, long pitch, long stride, int nframes, int chunk,
                          float *x, float *y, int *val, int n, float *tab_x, float *tab_y, int *tab_val,
                          long tab_stride);
+/* start the next klt_hip_track_frames* call from pyramid slot `slot` (built by
+   klt_hip_build_pyramid) instead of klt_hip_frames_begin's seed */
+int klt_hip_frames_begin_slot(klt_hip_ctx *ctx, int slot);
+/* klt_hip_track_frames for frames in HOST memory (frames[f]: ncols*nrows u8,
+   tight rows): chunks are uploaded on a copy stream into a two-chunk device
+   ring, overlapping the upload of chunk c+1 with the work on chunk c.
+   x/y/val and tab_* are device arrays.  Asynchronous: the host frames must
+   stay valid until the context stream is synchronized (klt_hip_sync). */
+int klt_hip_track_frames_host(klt_hip_ctx *ctx, const klt_hip_pyr_desc *pdesc,
+                              const klt_hip_track_desc *tdesc, const unsigned char *const *frames,
+                              int nframes, int chunk, float *x, float *y, int *val, int n, float *tab_x,
+                              float *tab_y, int *tab_val, long tab_stride);
 
 /* one chunk of the feature-sharded sequence (BASELINE config 4), for one rank
    of a row-band decomposition: like klt_hip_track_frames over nframes frames

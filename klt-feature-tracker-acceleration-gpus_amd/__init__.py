@@ -35,7 +35,7 @@ def load() -> C.CDLL:
             raise ImportError(f"{path} is missing: build it with `make -C {PKG_DIR / 'csrc'}` "
                               "(or __graft_entry__.build()); there is no CPU fallback")
         lib = C.CDLL(str(path), mode=C.RTLD_GLOBAL)
-        abi.bind_klt(lib)
+        abi.bind_klt(lib, extensions=True)
         device.bind_device(lib)
         _lib = lib
     return _lib

@@ -109,11 +109,16 @@ KLT_PROTOS = {
 }
 
 
+# libklt_amd.so extensions of the klt.h surface (include/klt_amd.h)
+AMD_KLT_PROTOS = {
+    "KLTTrackSequence": (None, [TC, C.POINTER(U8P), C.c_int, C.c_int, C.c_int, FL, FT, C.c_int]),
+}
 
 
-def bind_klt(lib: C.CDLL) -> C.CDLL:
-    """Attach the klt.h prototypes to an already loaded library."""
-    for name, (res, args) in KLT_PROTOS.items():
+def bind_klt(lib: C.CDLL, extensions: bool = False) -> C.CDLL:
+    """Attach the klt.h prototypes (and, for libklt_amd.so, its extensions)."""
+    protos = dict(KLT_PROTOS, **AMD_KLT_PROTOS) if extensions else KLT_PROTOS
+    for name, (res, args) in protos.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

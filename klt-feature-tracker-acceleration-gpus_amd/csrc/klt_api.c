@@ -76,8 +76,11 @@ static void dev_check(KLT_TrackingContext tc, int rc, const char *what)
 /* convolve.c:25-27 (process-wide, like the reference).                 */
 /* ------------------------------------------------------------------ */
 static pthread_mutex_t g_taps_lock = PTHREAD_MUTEX_INITIALIZER;
-static klt_hip_taps g_gauss, g_deriv;
-static float g_sigma_last = -10.0f;
+typedef struct {
+  klt_hip_taps gauss, deriv;
+  float sigma_last;
+} taps_state;
+static taps_state g_taps = {.sigma_last = -10.0f};
 
 static void taps_make(float sigma, klt_hip_taps *gauss, klt_hip_taps *deriv)
 {
@@ -116,27 +119,26 @@ static void taps_make(float sigma, klt_hip_taps *gauss, klt_hip_taps *deriv)
   }
 }
 
-/* cached lookup as _KLTComputeSmoothedImage / _KLTComputeGradients do it */
-static void taps_lookup(float sigma, klt_hip_taps *gauss, klt_hip_taps *deriv)
+/* cached lookup as _KLTComputeSmoothedImage / _KLTComputeGradients do it,
+   on a given cache state (the global one, or a copy for a dry run) */
+static void taps_lookup_in(taps_state *st, float sigma, klt_hip_taps *gauss, klt_hip_taps *deriv)
 {
-  pthread_mutex_lock(&g_taps_lock);
-  if (fabs(sigma - g_sigma_last) > 0.05) {
-    taps_make(sigma, &g_gauss, &g_deriv);
-    g_sigma_last = sigma;
+  if (fabs(sigma - st->sigma_last) > 0.05) {
+    taps_make(sigma, &st->gauss, &st->deriv);
+    st->sigma_last = sigma;
   }
-  if (gauss) *gauss = g_gauss;
-  if (deriv) *deriv = g_deriv;
-  pthread_mutex_unlock(&g_taps_lock);
+  if (gauss) *gauss = st->gauss;
+  if (deriv) *deriv = st->deriv;
 }
 
 /* _KLTGetKernelWidths (convolve.c:122-130): recomputes unconditionally */
 static void taps_widths(float sigma, int *gw, int *dw)
 {
   pthread_mutex_lock(&g_taps_lock);
-  taps_make(sigma, &g_gauss, &g_deriv);
-  g_sigma_last = sigma;
-  *gw = g_gauss.width;
-  *dw = g_deriv.width;
+  taps_make(sigma, &g_taps.gauss, &g_taps.deriv);
+  g_taps.sigma_last = sigma;
+  *gw = g_taps.gauss.width;
+  *dw = g_taps.deriv.width;
   pthread_mutex_unlock(&g_taps_lock);
 }
 
@@ -468,8 +470,8 @@ EXPORT void KLTExtractFeatureHistory(KLT_FeatureHistory fh, KLT_FeatureTable ft,
 /* taps for one frame's pyramid, looked up in the reference's call order:
    smooth (sigma_s), level >= 1 smoothing (sigma_p), then per-level
    gradients (sigma_g) -- trackFeatures.c:1298-1307 */
-static void pyr_desc(KLT_TrackingContext tc, int ncols, int nrows, int nlevels, int smooth,
-                     klt_hip_pyr_desc *d)
+static void pyr_desc_in(taps_state *st, KLT_TrackingContext tc, int ncols, int nrows, int nlevels, int smooth,
+                        klt_hip_pyr_desc *d)
 {
   int l;
   memset(d, 0, sizeof *d);
@@ -478,9 +480,17 @@ static void pyr_desc(KLT_TrackingContext tc, int ncols, int nrows, int nlevels, 
   d->nlevels = nlevels;
   d->subsampling = nlevels > 1 ? tc->subsampling : 1;
   d->smooth_input = smooth;
-  if (smooth) taps_lookup(_KLTComputeSmoothSigma(tc), &d->smooth, NULL);
-  for (l = 1; l < nlevels; l++) taps_lookup(pyramid_sigma(tc), &d->pyr, NULL);
-  for (l = 0; l < nlevels; l++) taps_lookup(tc->grad_sigma, &d->grad_gauss, &d->grad_deriv);
+  if (smooth) taps_lookup_in(st, _KLTComputeSmoothSigma(tc), &d->smooth, NULL);
+  for (l = 1; l < nlevels; l++) taps_lookup_in(st, pyramid_sigma(tc), &d->pyr, NULL);
+  for (l = 0; l < nlevels; l++) taps_lookup_in(st, tc->grad_sigma, &d->grad_gauss, &d->grad_deriv);
+}
+
+static void pyr_desc(KLT_TrackingContext tc, int ncols, int nrows, int nlevels, int smooth,
+                     klt_hip_pyr_desc *d)
+{
+  pthread_mutex_lock(&g_taps_lock);
+  pyr_desc_in(&g_taps, tc, ncols, nrows, nlevels, smooth, d);
+  pthread_mutex_unlock(&g_taps_lock);
 }
 
 static void build_from_host(KLT_TrackingContext tc, int slot, int buf, KLT_PixelType *img,
@@ -682,6 +692,176 @@ EXPORT void KLTTrackFeatures(KLT_TrackingContext tc, KLT_PixelType *img1, KLT_Pi
   if (KLT_verbose >= 1) {
     fprintf(stderr, "\n\t%d features successfully tracked.\n", KLTCountRemainingFeatures(fl));
     if (tc->writeInternalImages) fprintf(stderr, "\tWrote images to 'kltimg_tf*.pgm'.\n");
+    fflush(stderr);
+  }
+}
+
+/* ------------------------------------------------------------------ */
+/* KLTTrackSequence: the example3.c loop (KLTTrackFeatures on consecutive */
+/* frames + KLTStoreFeatureList, no replacement) in one call, on the     */
+/* batched device path with asynchronous uploads.  Bit-identical to the  */
+/* loop; falls back to the loop itself where it could not be.            */
+/* ------------------------------------------------------------------ */
+static int taps_state_eq(const taps_state *a, const taps_state *b)
+{
+  return a->sigma_last == b->sigma_last && !memcmp(&a->gauss, &b->gauss, sizeof a->gauss) &&
+         !memcmp(&a->deriv, &b->deriv, sizeof a->deriv);
+}
+
+/* KLTStoreFeatureList (storeFeatures.c:15-35) for one column: x, y, val only */
+static void store_column(KLT_FeatureTable ft, int col, int n, const float *x, const float *y, const int *v)
+{
+  int k;
+  for (k = 0; k < n; k++) {
+    ft->feature[k][col]->x = x[k];
+    ft->feature[k][col]->y = y[k];
+    ft->feature[k][col]->val = v[k];
+  }
+}
+
+EXPORT void KLTTrackSequence(KLT_TrackingContext tc, KLT_PixelType **frames, int nframes, int ncols, int nrows,
+                             KLT_FeatureList fl, KLT_FeatureTable ft, int ft_col)
+{
+  klt_ctx_full *f = FULL(tc);
+  klt_hip_ctx *dev;
+  klt_hip_pyr_desc d1, d2, e1, e2;
+  klt_hip_track_desc td;
+  taps_state st, after1;
+  int k, i, seq_start, steady, n = fl->nFeatures, T = nframes - 1;
+  float *hx, *hy, *tx = NULL, *ty = NULL;
+  int *hv, *tv = NULL;
+  void *dx, *dy, *dv, *dtx = NULL, *dty = NULL, *dtv = NULL;
+
+  if (nframes < 2) return;
+  window_fix(tc, NULL);
+  if (tc->affineConsistencyCheck >= 0)
+    KLTError("(KLTTrackSequence) affineConsistencyCheck=%d is not supported by libklt_amd",
+             tc->affineConsistencyCheck);
+  if (ft && (ft_col < 0 || ft_col + T > ft->nFrames))
+    KLTError("(KLTStoreFeatures) Frame number %d is not between 0 and %d", ft_col < 0 ? ft_col : ft_col + T - 1,
+             ft->nFrames - 1);
+  if (ft && ft->nFeatures != n)
+    KLTError("(KLTStoreFeatures) FeatureList and FeatureTable must have the same number of features");
+  dev = device_of(tc);
+  seq_start = tc->sequentialMode && tc->pyramid_last != NULL && f->last_slot >= 0;
+  if (seq_start && (f->last_w != ncols || f->last_h != nrows))
+    KLTError("(KLTTrackSequence) Size of incoming image (%d by %d) is different from size of "
+             "previous image (%d by %d)\n",
+             ncols, nrows, f->last_w, f->last_h);
+
+  /* dry run of the kernel-cache lookups of the first two KLTTrackFeatures
+     calls: one pyramid description serves every frame only if call 2 sees
+     the same taps as call 1 (then every later call does too) */
+  pthread_mutex_lock(&g_taps_lock);
+  st = g_taps;
+  pthread_mutex_unlock(&g_taps_lock);
+  if (!seq_start) pyr_desc_in(&st, tc, ncols, nrows, tc->nPyramidLevels, 1, &d1);
+  pyr_desc_in(&st, tc, ncols, nrows, tc->nPyramidLevels, 1, &d2);
+  after1 = st;
+  if (!tc->sequentialMode) pyr_desc_in(&st, tc, ncols, nrows, tc->nPyramidLevels, 1, &e1);
+  pyr_desc_in(&st, tc, ncols, nrows, tc->nPyramidLevels, 1, &e2);
+  steady = taps_state_eq(&st, &after1) && !memcmp(&e2, &d2, sizeof d2) &&
+           (tc->sequentialMode || !memcmp(&e1, &d2, sizeof d2)) && !tc->writeInternalImages;
+  if (!steady) {
+    for (i = 1; i < nframes; i++) {
+      KLTTrackFeatures(tc, frames[i - 1], frames[i], ncols, nrows, fl);
+      if (ft) KLTStoreFeatureList(fl, ft, ft_col + i - 1);
+    }
+    return;
+  }
+  if (KLT_verbose >= 1) {
+    fprintf(stderr, "(KLT) Tracking %d features through %d %d by %d frames...  ", KLTCountRemainingFeatures(fl),
+            T, ncols, nrows);
+    fflush(stderr);
+  }
+
+  if (seq_start) {
+    dev_check(tc, klt_hip_frames_begin_slot(dev, f->last_slot), "sequence start");
+  } else {
+    build_from_host(tc, SLOT_A, 0, frames[0], &d1);
+    dev_check(tc, klt_hip_frames_begin_slot(dev, SLOT_A), "sequence start");
+  }
+  klt_amd_track_desc(tc, &td);
+
+  hx = (float *)malloc(sizeof(float) * (n + 1));
+  hy = (float *)malloc(sizeof(float) * (n + 1));
+  hv = (int *)malloc(sizeof(int) * (n + 1));
+  if (!hx || !hy || !hv) KLTError("(KLTTrackSequence) Out of memory");
+  for (k = 0; k < n; k++) {
+    hx[k] = fl->feature[k]->x;
+    hy[k] = fl->feature[k]->y;
+    hv[k] = fl->feature[k]->val;
+  }
+  dx = klt_hip_malloc(dev, sizeof(float) * (n + 1));
+  dy = klt_hip_malloc(dev, sizeof(float) * (n + 1));
+  dv = klt_hip_malloc(dev, sizeof(int) * (n + 1));
+  if (!dx || !dy || !dv) KLTError("(KLTTrackSequence) device allocation failed");
+  dev_check(tc, klt_hip_memcpy(dev, dx, hx, sizeof(float) * n, 1), "upload");
+  dev_check(tc, klt_hip_memcpy(dev, dy, hy, sizeof(float) * n, 1), "upload");
+  dev_check(tc, klt_hip_memcpy(dev, dv, hv, sizeof(int) * n, 1), "upload");
+  if (ft) {
+    const size_t cells = (size_t)T * (n > 0 ? n : 1);
+    dtx = klt_hip_malloc(dev, sizeof(float) * cells);
+    dty = klt_hip_malloc(dev, sizeof(float) * cells);
+    dtv = klt_hip_malloc(dev, sizeof(int) * cells);
+    tx = (float *)malloc(sizeof(float) * cells);
+    ty = (float *)malloc(sizeof(float) * cells);
+    tv = (int *)malloc(sizeof(int) * cells);
+    if (!dtx || !dty || !dtv || !tx || !ty || !tv) KLTError("(KLTTrackSequence) Out of memory");
+  }
+  dev_check(tc, klt_hip_track_frames_host(dev, &d2, &td, (const unsigned char *const *)(frames + 1), T, 32,
+                                          (float *)dx, (float *)dy, (int *)dv, n, (float *)dtx, (float *)dty,
+                                          (int *)dtv, n),
+            "sequence tracking");
+  dev_check(tc, klt_hip_sync(dev), "sequence tracking");
+  dev_check(tc, klt_hip_memcpy(dev, hx, dx, sizeof(float) * n, 2), "download");
+  dev_check(tc, klt_hip_memcpy(dev, hy, dy, sizeof(float) * n, 2), "download");
+  dev_check(tc, klt_hip_memcpy(dev, hv, dv, sizeof(int) * n, 2), "download");
+  if (ft) {
+    const size_t cells = (size_t)T * n;
+    dev_check(tc, klt_hip_memcpy(dev, tx, dtx, sizeof(float) * cells, 2), "download");
+    dev_check(tc, klt_hip_memcpy(dev, ty, dty, sizeof(float) * cells, 2), "download");
+    dev_check(tc, klt_hip_memcpy(dev, tv, dtv, sizeof(int) * cells, 2), "download");
+    for (i = 0; i < T; i++) store_column(ft, ft_col + i, n, tx + (size_t)i * n, ty + (size_t)i * n,
+                                         tv + (size_t)i * n);
+  }
+  for (k = 0; k < n; k++) {
+    KLT_Feature ftr = fl->feature[k];
+    if (ftr->val < 0) continue; /* untouched, like the reference (:1346) */
+    ftr->x = hx[k];
+    ftr->y = hy[k];
+    ftr->val = hv[k];
+    if (hv[k] != KLT_TRACKED) drop_affine(ftr);
+  }
+  klt_hip_free(dev, dx);
+  klt_hip_free(dev, dy);
+  klt_hip_free(dev, dv);
+  klt_hip_free(dev, dtx);
+  klt_hip_free(dev, dty);
+  klt_hip_free(dev, dtv);
+  free(hx);
+  free(hy);
+  free(hv);
+  free(tx);
+  free(ty);
+  free(tv);
+
+  /* the kernel cache ends where the per-frame loop would leave it */
+  pthread_mutex_lock(&g_taps_lock);
+  g_taps = st;
+  pthread_mutex_unlock(&g_taps_lock);
+  if (tc->sequentialMode) { /* the last frame's pyramid carries over, as after the loop */
+    const int slot = f->last_slot == SLOT_A ? SLOT_B : SLOT_A;
+    build_from_host(tc, slot, 1, frames[nframes - 1], &d2);
+    f->last_slot = slot;
+    f->last_w = ncols;
+    f->last_h = nrows;
+    tc->pyramid_last = &f->last_slot;
+    tc->pyramid_last_gradx = &f->last_w;
+    tc->pyramid_last_grady = &f->last_h;
+  }
+  if (KLT_verbose >= 1) {
+    fprintf(stderr, "\n\t%d features successfully tracked.\n", KLTCountRemainingFeatures(fl));
     fflush(stderr);
   }
 }

@@ -1421,8 +1421,9 @@ struct Bank {
 
 // where the pyramid preceding the next batch lives
 struct PrevRef {
-  int bank = -1;  // -1: slot kSeedSlot
+  int bank = -1;  // -1: pyramid slot `slot`
   int frame = 0;
+  int slot = KLT_HIP_MAX_SLOTS;  // the batch seed slot unless klt_hip_frames_begin_slot
 };
 
 struct klt_hip_ctx {
@@ -1458,6 +1459,10 @@ struct klt_hip_ctx {
   int *d_perm = nullptr;
   size_t perm_cap = 0;
   int *d_count = nullptr;  // band mode: features owned in this chunk
+  unsigned char *d_ring = nullptr;  // klt_hip_track_frames_host: 2 chunks of uploaded frames
+  size_t ring_cap = 0;
+  hipStream_t cstream = nullptr;
+  hipEvent_t ev_ring_ready[2] = {}, ev_ring_free[2] = {};
 #ifdef KLT_TRACK_PROF
   unsigned long long *prof = nullptr;
 #endif
@@ -1930,6 +1935,15 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
   }
   hipFree(c->d_perm);
   hipFree(c->d_count);
+  if (c->cstream) {
+    hipStreamSynchronize(c->cstream);
+    hipStreamDestroy(c->cstream);
+  }
+  for (int k = 0; k < 2; ++k) {
+    if (c->ev_ring_ready[k]) hipEventDestroy(c->ev_ring_ready[k]);
+    if (c->ev_ring_free[k]) hipEventDestroy(c->ev_ring_free[k]);
+  }
+  hipFree(c->d_ring);
   hipFree(c->d_hs);
   hipFree(c->d_fx);
   hipFree(c->d_fy);
@@ -2211,7 +2225,7 @@ constexpr int kSeedSlot = KLT_HIP_MAX_SLOTS, kScratchSlot = KLT_HIP_MAX_SLOTS + 
 
 TrkLevel prev_level(klt_hip_ctx *c, int l) {
   if (c->prev.bank < 0) {
-    const Level &L = c->slot[kSeedSlot].lv[l];
+    const Level &L = c->slot[c->prev.slot].lv[l];
     return TrkLevel{L.img, L.gx, L.gy, L.w, L.h};
   }
   const Bank &K = c->bank[c->prev.bank];
@@ -2248,7 +2262,16 @@ KLT_API int klt_hip_frames_begin(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, con
   if (!c || !pd || !frame) return fail(c, "frames_begin: null argument");
   if (use_device(c)) return -1;
   if (build_pyramid_on(c, kSeedSlot, pd, frame, pitch, 0, c->stream)) return -1;
-  c->prev = PrevRef{-1, 0};
+  c->prev = PrevRef{-1, 0, kSeedSlot};
+  c->frames_ready = true;
+  return 0;
+}
+
+KLT_API int klt_hip_frames_begin_slot(klt_hip_ctx *c, int slot) {
+  if (!c) return fail(c, "frames_begin_slot: null context");
+  if (slot < 0 || slot >= KLT_HIP_MAX_SLOTS || c->slot[slot].nlev < 1)
+    return fail(c, "frames_begin_slot: slot %d is not built", slot);
+  c->prev = PrevRef{-1, 0, slot};
   c->frames_ready = true;
   return 0;
 }
@@ -2276,7 +2299,7 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
   if (check_window(c, td)) return -1;
   {
     const TrkLevel p0 = prev_level(c, 0);
-    int nl = c->prev.bank < 0 ? c->slot[kSeedSlot].nlev : c->bank[c->prev.bank].nlev;
+    int nl = c->prev.bank < 0 ? c->slot[c->prev.slot].nlev : c->bank[c->prev.bank].nlev;
     if (p0.w != pd->ncols || p0.h != pd->nrows || nl != pd->nlevels)
       return fail(c, "track_frames: frames are %dx%d/%d levels, previous pyramid %dx%d/%d", pd->ncols,
                   pd->nrows, pd->nlevels, p0.w, p0.h, nl);
@@ -2319,7 +2342,7 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
         if (copy_level_planes(c, from, to.img, to.gx, to.gy, c->stream)) return -1;
       }
       HIPCHK(c, hipStreamSynchronize(c->stream));
-      c->prev = PrevRef{-1, 0};
+      c->prev = PrevRef{-1, 0, kSeedSlot};
     }
     for (auto &K : c->bank)
       if (ensure_bank(c, K, pd, chunk)) return -1;
@@ -2395,6 +2418,56 @@ KLT_API int klt_hip_track_frames(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, con
                                  long tab_stride) {
   return track_frames_impl(c, pd, td, frames, pitch, stride, nframes, chunk, x, y, val, n, tab_x, tab_y, tab_val,
                            tab_stride, nullptr);
+}
+
+// Host frames: uploaded chunk by chunk into a two-slot device ring on a copy
+// stream (pageable sources, staged by the runtime), so the upload of chunk
+// c+1 overlaps the pyramids and tracking of chunk c.
+KLT_API int klt_hip_track_frames_host(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
+                                      const unsigned char *const *frames, int nframes, int chunk, float *x,
+                                      float *y, int *val, int n, float *tab_x, float *tab_y, int *tab_val,
+                                      long tab_stride) {
+  if (!c || !pd || !td || (nframes > 0 && !frames)) return fail(c, "track_frames_host: null argument");
+  if (chunk < 1 || nframes < 0) return fail(c, "track_frames_host: bad nframes/chunk");
+  if (nframes == 0) return 0;
+  if (use_device(c)) return -1;
+  const long fb = (long)pd->ncols * pd->nrows;
+  const int F = chunk < nframes ? chunk : nframes;
+  if (grow(c, &c->d_ring, &c->ring_cap, (size_t)(2 * F * fb))) return -1;
+  if (!c->cstream) {
+    HIPCHK(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    for (int k = 0; k < 2; ++k) {
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_ring_ready[k], hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_ring_free[k], hipEventDisableTiming));
+    }
+  }
+  // the ring may still be read by earlier work on the context stream
+  HIPCHK(c, hipEventRecord(c->ev_ring_free[0], c->stream));
+  HIPCHK(c, hipEventRecord(c->ev_ring_free[1], c->stream));
+  auto upload = [&](int j0, int k) -> int {
+    const int nf = F < nframes - j0 ? F : nframes - j0;
+    HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_ring_free[k], 0));
+    for (int f = 0; f < nf; ++f) {
+      if (!frames[j0 + f]) return fail(c, "track_frames_host: frame %d is NULL", j0 + f);
+      HIPCHK(c, hipMemcpyAsync(c->d_ring + (size_t)(k * F + f) * fb, frames[j0 + f], (size_t)fb,
+                               hipMemcpyHostToDevice, c->cstream));
+    }
+    HIPCHK(c, hipEventRecord(c->ev_ring_ready[k], c->cstream));
+    return 0;
+  };
+  if (upload(0, 0)) return -1;
+  for (int j0 = 0, k = 0; j0 < nframes; j0 += F, k ^= 1) {
+    const int nf = F < nframes - j0 ? F : nframes - j0;
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_ring_ready[k], 0));
+    const long off = (long)j0 * tab_stride;
+    if (track_frames_impl(c, pd, td, c->d_ring + (size_t)k * F * fb, pd->ncols, fb, nf, F, x, y, val, n,
+                          tab_x ? tab_x + off : nullptr, tab_y ? tab_y + off : nullptr,
+                          tab_val ? tab_val + off : nullptr, tab_stride, nullptr))
+      return -1;
+    HIPCHK(c, hipEventRecord(c->ev_ring_free[k], c->stream));
+    if (j0 + F < nframes && upload(j0 + F, k ^ 1)) return -1;  // overlaps the chunk just queued
+  }
+  return 0;
 }
 
 KLT_API int klt_hip_track_frames_band(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,

@@ -418,3 +418,68 @@ def batch_sequence_opts(gpu, frames, nfeat, chunk, opts):
         return batch_sequence(gpu, frames, nfeat, [chunk])
     finally:
         gpu.klt_amd_device_context = orig
+
+
+def _seq_via_api(gpu, frames, nfeat, sequential=True, first_call=False):
+    """KLTTrackSequence over frames (selection on frames[0]); optionally one
+    KLTTrackFeatures call first so that sequential mode starts from a kept pyramid."""
+    from kltabi import fl_to_arrays, u8ptr
+    h, w = frames[0].shape
+    tc = gpu.KLTCreateTrackingContext()
+    tc.contents.sequentialMode = 1 if sequential else 0
+    fl = gpu.KLTCreateFeatureList(nfeat)
+    gpu.KLTSelectGoodFeatures(tc, u8ptr(np.ascontiguousarray(frames[0])), w, h, fl)
+    seq = frames
+    if first_call:
+        gpu.KLTTrackFeatures(tc, u8ptr(frames[0]), u8ptr(frames[1]), w, h, fl)
+        seq = frames[1:]
+    T = len(seq) - 1
+    ft = gpu.KLTCreateFeatureTable(T, nfeat)
+    keep = [np.ascontiguousarray(f) for f in seq]
+    arr = (C.POINTER(C.c_ubyte) * len(keep))(*[u8ptr(f) for f in keep])
+    gpu.KLTTrackSequence(tc, arr, len(keep), w, h, fl, ft, 0)
+    X = np.array([[ft.contents.feature[j][i].contents.x for i in range(T)] for j in range(nfeat)], np.float32)
+    Y = np.array([[ft.contents.feature[j][i].contents.y for i in range(T)] for j in range(nfeat)], np.float32)
+    V = np.array([[ft.contents.feature[j][i].contents.val for i in range(T)] for j in range(nfeat)], np.int32)
+    x, y, v = fl_to_arrays(fl)
+    gpu.KLTFreeFeatureTable(ft)
+    gpu.KLTFreeFeatureList(fl)
+    gpu.KLTFreeTrackingContext(tc)
+    return X, Y, V, (x, y, v)
+
+
+@pytest.mark.parametrize("sequential,first_call", [(True, False), (False, False), (True, True)])
+def test_track_sequence_api_vs_loop(gpu, oracle, sequential, first_call):
+    """KLTTrackSequence == the per-frame KLTTrackFeatures + KLTStoreFeatureList loop (oracle)."""
+    frames = synth(gpu, 6060, 640, 480, 40)  # > one 32-frame chunk
+    X, Y, V, last = _seq_via_api(gpu, frames, 800, sequential, first_call)
+    OX, OY, OV = OracleTracker(oracle).harness(frames, 800, 40, first=frames[0])
+    off = 1 if first_call else 0
+    T = X.shape[1]
+    assert np.array_equal(V, OV[:, off:off + T])
+    assert np.array_equal(X.view(np.int32), OX[:, off:off + T].view(np.int32))
+    assert np.array_equal(Y.view(np.int32), OY[:, off:off + T].view(np.int32))
+    assert np.array_equal(last[2], OV[:, off + T - 1])
+
+
+def test_track_sequence_then_track_features(gpu, oracle):
+    """Sequential mode: a KLTTrackFeatures call after KLTTrackSequence continues
+    from the sequence's last pyramid, exactly like after the per-frame loop."""
+    from kltabi import fl_to_arrays, u8ptr
+    frames = synth(gpu, 6161, 333, 251, 9)
+    h, w = frames[0].shape
+    tc = gpu.KLTCreateTrackingContext()
+    tc.contents.sequentialMode = 1
+    fl = gpu.KLTCreateFeatureList(300)
+    gpu.KLTSelectGoodFeatures(tc, u8ptr(frames[0]), w, h, fl)
+    keep = [np.ascontiguousarray(f) for f in frames[:6]]
+    arr = (C.POINTER(C.c_ubyte) * 6)(*[u8ptr(f) for f in keep])
+    gpu.KLTTrackSequence(tc, arr, 6, w, h, fl, None, 0)
+    for t in range(6, 9):  # img1 is ignored in sequential mode: pass garbage
+        junk = np.zeros_like(frames[0])
+        gpu.KLTTrackFeatures(tc, u8ptr(junk), u8ptr(frames[t]), w, h, fl)
+    x, y, v = fl_to_arrays(fl)
+    gpu.KLTFreeFeatureList(fl)
+    gpu.KLTFreeTrackingContext(tc)
+    OX, OY, OV = OracleTracker(oracle).harness(frames, 300, 9, first=frames[0])
+    assert np.array_equal(v, OV[:, 7]) and np.array_equal(x.view(np.int32), OX[:, 7].view(np.int32))

@@ -27,10 +27,10 @@ sys.path.insert(0, str(ROOT))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["pyr", "track", "frames", "api"])
+    ap.add_argument("mode", choices=["pyr", "track", "frames", "api", "apiseq"])
     ap.add_argument("--prof", action="store_true",
                     help="per-wave phase cycles (needs KLT_AMD_LIB=.../lib/prof/libklt_amd.so)")
-    ap.add_argument("--serial", action="store_true", help="frames: pyramids and tracking on one stream")
+    ap.add_argument("--overlap", action="store_true", help="frames: pyramids of chunk c+1 on a second stream")
     ap.add_argument("--no-patch", action="store_true", help="tracker: per-pixel gathers only")
     ap.add_argument("--input-order", action="store_true", help="tracker: no band ordering")
     ap.add_argument("--group", type=int, default=0, help="tracker: features per wave (0 default, 1, 2, 4)")
@@ -62,7 +62,7 @@ def main():
     check(lib, ctx, lib.klt_hip_set_track_group(ctx, a.group), "group")
     check(lib, ctx, lib.klt_hip_set_track_order(ctx, 1 if a.input_order else 0), "order")
     check(lib, ctx, lib.klt_hip_set_track_patch(ctx, 0 if a.no_patch else 1), "patch")
-    check(lib, ctx, lib.klt_hip_set_frames_overlap(ctx, 0 if a.serial else 1), "overlap")
+    check(lib, ctx, lib.klt_hip_set_frames_overlap(ctx, 1 if a.overlap else 0), "overlap")
     nf = max(a.frames, 2)
     frames = lib.klt_hip_malloc(ctx, nf * W * H)
     check(lib, ctx, lib.klt_hip_synth_frames(ctx, 1080, 0, nf, W, H, frames, W, W * H), "synth")
@@ -121,6 +121,32 @@ def main():
         lib.KLTFreeFeatureList(fl)
         out.update({"features": a.features, "calls": len(times), "fps": len(times) / sum(times),
                     "us_per_call_median": 1e6 * float(np.median(times)), "live_at_end": live})
+    elif a.mode == "apiseq":
+        # KLTTrackSequence: host u8 frames, uploads overlapped with the batched device path
+        nh = max(a.frames, 3)
+        host = []
+        for t in range(nh):
+            h = np.empty((H, W), np.uint8)
+            lib.klt_synth_frame(1080, t, W, H, h.ctypes.data)
+            host.append(h)
+        u8 = lambda z: z.ctypes.data_as(kltamd.abi.U8P)  # noqa: E731
+        arr = (kltamd.abi.U8P * nh)(*[u8(z) for z in host])
+        fl = lib.KLTCreateFeatureList(a.features)
+        lib.KLTSelectGoodFeatures(tc, u8(host[0]), W, H, fl)
+        ft = lib.KLTCreateFeatureTable(nh - 1, a.features)
+        lib.KLTTrackSequence(tc, arr, min(nh, 40), W, H, fl, ft, 0)  # warm-up (allocations)
+        lib.KLTFreeFeatureList(fl)
+        fl = lib.KLTCreateFeatureList(a.features)
+        lib.KLTSelectGoodFeatures(tc, u8(host[0]), W, H, fl)
+        t0 = time.perf_counter()
+        lib.KLTTrackSequence(tc, arr, nh, W, H, fl, ft, 0)
+        dt = time.perf_counter() - t0
+        live = sum(1 for k in range(a.features) if fl.contents.feature[k].contents.val >= 0)
+        lib.KLTFreeFeatureTable(ft)
+        lib.KLTFreeFeatureList(fl)
+        out.update({"features": a.features, "frames_tracked": nh - 1, "fps": (nh - 1) / dt,
+                    "us_per_frame": 1e6 * dt / (nh - 1), "live_at_end": live,
+                    "note": "host frames, PCIe upload and feature-table download included"})
     elif a.mode == "frames":
         # batched sequence: select on frame 0, track frames 1..nf-1 in chunks
         h0 = np.empty((H, W), np.uint8)
