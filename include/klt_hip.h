@@ -111,6 +111,14 @@ int klt_hip_set_track_order(klt_hip_ctx *ctx, int input_order);
 /* tuning hook: 0 disables the lane-patch gather of one-feature waves (default
    1: on where (ww+1)*(wh+1) <= 64).  Results do not depend on it. */
 int klt_hip_set_track_patch(klt_hip_ctx *ctx, int on);
+/* tuning hook: the level-0 kernel of the fused pyramid.  mode 0 (default):
+   64x32 tiles, one workgroup each (k_pyr_l0); 1: rolling 64-column strips that
+   keep the rows shared by consecutive steps in LDS (k_pyr_l0s, needs width % 8
+   == 0 and 4-byte aligned rows; strip_steps 16-row steps per strip, <= 0 keeps
+   the current value, default 8); 2: persistent tiles fed by an LDS-DMA loading
+   wave (k_pyr_l0p, 4-byte aligned rows).  Shapes a mode cannot take use tiles.
+   Results do not depend on it (tests/test_gpu_pyramid.py). */
+int klt_hip_set_pyr_l0(klt_hip_ctx *ctx, int mode, int strip_steps);
 /* klt_hip_track_frames scheduling: 1 builds chunk c+1's pyramids on a second
    stream while chunk c is tracked; 0 (default) runs both on the context stream. */
 int klt_hip_set_frames_overlap(klt_hip_ctx *ctx, int overlap);

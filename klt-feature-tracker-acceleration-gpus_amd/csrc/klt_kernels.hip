@@ -70,6 +70,20 @@ struct FusedTaps {
 
 __host__ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+// hs (the level-0 rows pass of the pyramid smoothing, W1 = W/4 columns, H rows)
+// is stored in column slabs 16 wide: slab X/16 holds rows 0..H-1 of its 16
+// columns contiguously.  A 64-column level-0 tile owns exactly one slab, so
+// its 32 rows are one contiguous 2 KB run of whole cache lines; row-major, the
+// rows of two neighbouring tiles would share every 128-byte line (64 B each),
+// and partial-line writes cost more than all the other level-0 output.
+constexpr int kHsSlab = 16;
+__host__ __device__ __forceinline__ long hs_at(int y, int X, int H) {
+  return ((long)(X / kHsSlab) * H + y) * kHsSlab + (X % kHsSlab);
+}
+__host__ __device__ __forceinline__ long hs_size(int W1, int H) {
+  return (long)((W1 + kHsSlab - 1) / kHsSlab) * kHsSlab * H;
+}
+
 // ---------------------------------------------------------------------------
 // Fused pyramid kernels for the default parameters (sigma 0.7 / 1.0 / 3.6,
 // subsampling 4, two levels: smoothing 5 taps, gradients 7+7, pyramid 21).
@@ -121,11 +135,17 @@ constexpr int IHB = (IH + 3) / 4;  // 4-row blocks of img0 computed
 #define KLT_L0_PU 100  // u / img0 pitches: a few bank conflicts for a 4th block per CU
 #define KLT_L0_PI 92
 #endif
+#ifndef KLT_L0_U8
+#define KLT_L0_U8 1  // 1: stage the input tile as bytes (converted in the row pass)
+#endif
+constexpr bool U8 = KLT_L0_U8 != 0;
 constexpr int PU = KLT_L0_PU, PT = 84, PI = KLT_L0_PI, PX = TW;
-constexpr int REG_A = UH * PU;            // u8 (float) during A-B, then img0 during C-D
+constexpr int PUB = 24;                   // U8: staged row pitch in dwords (96 bytes)
+constexpr int U_WORDS = U8 ? UH * PUB : UH * PU;
+constexpr int REG_A = U_WORDS > IH * PI ? U_WORDS : IH * PI;  // u during A-B, then img0 during C-D
 constexpr int REG_B = 2 * IH * PX;        // t1 during B-C, then tx|ty during D-E
 constexpr int LDS = REG_A + REG_B;
-static_assert(IHB * 4 * PI <= REG_A && UH * PT <= REG_B, "LDS aliasing");
+static_assert(IH * PI <= REG_A && UH * PT <= REG_B, "LDS aliasing");
 }  // namespace l0
 
 // XCD-aware tile order: consecutive workgroups are dealt to the 8 XCDs in
@@ -143,13 +163,67 @@ __device__ __forceinline__ bool xcd_tile(int tiles_x, int tiles_y, int &bx, int 
 
 // Edge tiles clamp their loads and apply the zero-border rules per element;
 // interior tiles (~90 % at 1080p, 94 % at 4K) need neither.
-template <bool INT>
+#ifndef KLT_L0T_XST  // timing experiments only: bit 1 img0, 2 hs, 4 gx/gy stores
+#define KLT_L0T_XST 7
+#endif
+// Taps read from the kernarg segment through a pointer laundered where the
+// compiler must not hoist them: a loop kernel would otherwise keep all 40
+// (80 SGPRs as broadcast pairs) live and spill them to VGPR lanes.
+typedef const DefTaps __attribute__((address_space(4))) *TapsK;
+typedef const __attribute__((address_space(4))) DefTaps DefTapsK;
+__device__ __forceinline__ TapsK fresh_taps(TapsK p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+__device__ __forceinline__ const DefTaps &phase_taps(const DefTaps &T) { return T; }
+__device__ __forceinline__ DefTapsK &phase_taps(DefTapsK &T) { return *fresh_taps(&T); }
+
+#ifdef KLT_TRACK_PROF
+// level-0 kernel phase profile (prof build): k_pyr_l0s: [0] prologue, [1..2]
+// intervals (wave 0, incl. barrier), [5] workgroups, [8 + 4*wave + interval]
+// a wave's own work.  k_pyr_l0 (non-staged): [16 + phase] cycles of wave 0 from
+// the previous barrier to the end of the phase's barrier (A..E), [21] tiles,
+// [24 + phase] its own work before the barrier.
+__device__ unsigned long long g_l0s_prof[64];
+#define L0T_MARK(ph)                                                                          \
+  {                                                                                           \
+    const long long t_ = clock64();                                                           \
+    const int b_ = STAGED ? 32 : 0;                                                           \
+    if (tid == 0 && (blockIdx.x & 63) == 0)                                                   \
+      atomicAdd(&g_l0s_prof[b_ + 24 + (ph)], (unsigned long long)(t_ - tprev));               \
+    if (STAGED && (tid == 64 || tid == 128 || tid == 192 || tid == 256) && (blockIdx.x & 63) == 0) \
+      atomicAdd(&g_l0s_prof[(tid >> 6) * 4 + (ph)], (unsigned long long)(t_ - tprev));        \
+    __syncthreads();                                                                          \
+    const long long u_ = clock64();                                                           \
+    if (tid == 0 && (blockIdx.x & 63) == 0)                                                   \
+      atomicAdd(&g_l0s_prof[b_ + 16 + (ph)], (unsigned long long)(u_ - tprev));               \
+    tprev = u_;                                                                               \
+  }
+#else
+#define L0T_MARK(ph) __syncthreads()
+#endif
+
+struct NoHook {
+  __device__ void operator()() const {}
+};
+
+// STAGED: the u8 tile is already in LDS at `us` ([UH][UQ] dwords, k_pyr_l0p's
+// loading wave put it there), phase A is skipped and `hook` runs on every
+// thread right after the B barrier (when `us` may be refilled); threads with
+// tid >= kBlock (the loading wave) only take part in the barriers.
+template <bool INT, bool STAGED = false, class Hook = NoHook, class Taps = DefTaps>
 __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8_t *__restrict__ src, int spitch,
-                                            int W, int H, const DefTaps &T, int vec_u8,
+                                            int W, int H, const Taps &Tin, int vec_u8,
                                             float *__restrict__ img0, float *__restrict__ gx0,
                                             float *__restrict__ gy0, float *__restrict__ hs, int hsW,
-                                            int do_hs, int vec_out, int C0, int R0, int tid) {
+                                            int do_hs, int vec_out, int C0, int R0, int tid,
+                                            const uint32_t *__restrict__ us = nullptr, Hook hook = Hook()) {
   using namespace l0;
+  const bool comp = !STAGED || tid < kBlock;
+#ifdef KLT_TRACK_PROF
+  long long tprev = clock64();
+#endif
   float *u = lds;            // [UH][PU]
   float *im = lds;           // [IHB*4][PI]   (after u is dead)
   float *t1 = lds + REG_A;   // [UH][PT]
@@ -157,7 +231,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
   float *ty = tx + IH * PX;
 
   // A. u8 tile + halo -> float; every load issued before the first is used
-  {
+  if (!STAGED) {
     constexpr int NA = UH * UQ, PER = (NA + kBlock - 1) / kBlock;
     uint32_t w[PER];
 #pragma unroll
@@ -185,25 +259,42 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
       const int i = tid + k * kBlock;
       if (i < NA) {
         const int r = i / UQ, q = i - r * UQ;
-        const f4 v = {(float)(w[k] & 0xFF), (float)((w[k] >> 8) & 0xFF), (float)((w[k] >> 16) & 0xFF),
-                      (float)(w[k] >> 24)};
-        st4(u + r * PU + 4 * q, v);
+        if (U8) {
+          reinterpret_cast<uint32_t *>(u)[r * PUB + q] = w[k];
+        } else {
+          const f4 v = {(float)(w[k] & 0xFF), (float)((w[k] >> 8) & 0xFF), (float)((w[k] >> 16) & 0xFF),
+                        (float)(w[k] >> 24)};
+          st4(u + r * PU + 4 * q, v);
+        }
       }
     }
+    L0T_MARK(0);
   }
-  __syncthreads();
 
+  const auto &T0 = phase_taps(Tin);
   // B. rows pass of the smoothing: t1 idx k <-> global C0-8+k; zero unless RS <= x < W-RS
-  for (int i = tid; i < UH * NG; i += kBlock) {
+  for (int i = tid; comp && i < UH * NG; i += kBlock) {
     const int r = i / NG, g = i - r * NG;
-    const float *row = u + r * PU + 4 * g;
     float v[12];
-    *reinterpret_cast<f4 *>(v) = ld4(row);
-    *reinterpret_cast<f4 *>(v + 4) = ld4(row + 4);
-    *reinterpret_cast<f4 *>(v + 8) = ld4(row + 8);
+    if (U8 || STAGED) {
+      const uint32_t *row = STAGED ? us + r * UQ + g : reinterpret_cast<const uint32_t *>(u) + r * PUB + g;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const uint32_t d = row[k];
+        v[4 * k + 0] = (float)(d & 0xFF);
+        v[4 * k + 1] = (float)((d >> 8) & 0xFF);
+        v[4 * k + 2] = (float)((d >> 16) & 0xFF);
+        v[4 * k + 3] = (float)(d >> 24);
+      }
+    } else {
+      const float *row = u + r * PU + 4 * g;
+      *reinterpret_cast<f4 *>(v) = ld4(row);
+      *reinterpret_cast<f4 *>(v + 4) = ld4(row + 4);
+      *reinterpret_cast<f4 *>(v + 8) = ld4(row + 8);
+    }
     f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int m = 0; m < 5; ++m) mac4(acc, v + 2 + m, T.s[m]);
+    for (int m = 0; m < 5; ++m) mac4(acc, v + 2 + m, T0.s[m]);
     if (!INT) {
       const int x = C0 - 8 + 4 * g;
 #pragma unroll
@@ -212,10 +303,12 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     }
     st4(t1 + r * PT + 4 * g, acc);
   }
-  __syncthreads();
+  L0T_MARK(1);
+  hook();
 
+  const auto &T1 = phase_taps(Tin);
   // C. columns pass -> img0, 4 rows x 4 columns per thread; zero unless RS <= y < H-RS
-  for (int i = tid; i < IHB * NG; i += kBlock) {
+  for (int i = tid; comp && i < IHB * NG; i += kBlock) {
     const int b = i / NG, g = i - b * NG;
     const float *col = t1 + (4 * b) * PT + 4 * g;
     f4 v[8];
@@ -225,18 +318,18 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     for (int rr = 0; rr < 4; ++rr) {
       f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-      for (int m = 0; m < 5; ++m) mac4(acc, reinterpret_cast<const float *>(&v[rr + m]), T.s[m]);
+      for (int m = 0; m < 5; ++m) mac4(acc, reinterpret_cast<const float *>(&v[rr + m]), T1.s[m]);
       if (!INT) {
         const int y = R0 - RG + 4 * b + rr;
         if (!(y >= RS && y < H - RS)) acc = f4{0.0f, 0.0f, 0.0f, 0.0f};
       }
-      st4(im + (4 * b + rr) * PI + 4 * g, acc);
+      if (IH % 4 == 0 || 4 * b + rr < IH) st4(im + (4 * b + rr) * PI + 4 * g, acc);  // rows >= IH unused
     }
   }
-  __syncthreads();
+  L0T_MARK(2);
 
   // D1. img0 tile -> HBM
-  for (int i = tid; i < TH * (TW / 4); i += kBlock) {
+  for (int i = tid; comp && (KLT_L0T_XST & 1) && i < TH * (TW / 4); i += kBlock) {
     const int r = i / (TW / 4), g = i - r * (TW / 4);
     const int y = R0 + r, x = C0 + 4 * g;
     const f4 val = ld4(im + (r + RG) * PI + 8 + 4 * g);
@@ -250,8 +343,9 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
         for (int e = 0; e < 4 && x + e < W; ++e) dst[e] = val[e];
     }
   }
+  const auto &T2 = phase_taps(Tin);
   // D2. rows passes of both gradients; zero unless RG <= x < W-RG
-  for (int i = tid; i < IH * (TW / 4); i += kBlock) {
+  for (int i = tid; comp && i < IH * (TW / 4); i += kBlock) {
     const int r = i / (TW / 4), g = i - r * (TW / 4);
     const float *row = im + r * PI + 4 * g + 4;  // img0 idx c0+4 <-> global C0+c0-4
     float v[12];
@@ -261,8 +355,8 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     f4 ax = {0.0f, 0.0f, 0.0f, 0.0f}, ay = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int m = 0; m < 7; ++m) {
-      mac4(ax, v + 1 + m, T.d[m]);
-      mac4(ay, v + 1 + m, T.g[m]);
+      mac4(ax, v + 1 + m, T2.d[m]);
+      mac4(ay, v + 1 + m, T2.g[m]);
     }
     if (!INT) {
       const int x = C0 + 4 * g;
@@ -277,9 +371,11 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     st4(tx + r * PX + 4 * g, ax);
     st4(ty + r * PX + 4 * g, ay);
   }
+  const auto &T3 = phase_taps(Tin);
   // D3. pyramid rows pass at columns 4X+2, two per thread; zero unless RP <= c < W-RP
-  if (do_hs) {
+  if (do_hs && comp) {
     for (int i = tid; i < TH * (TW / 8); i += kBlock) {
+      if (!(KLT_L0T_XST & 2)) break;
       const int r = i / (TW / 8), pq = i - r * (TW / 8);
       const float *row = im + (r + RG) * PI + 8 * pq;  // idx 8p <-> global C0+8p-8
       float v[28];
@@ -289,26 +385,27 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
 #pragma unroll
       for (int m = 0; m < 21; ++m) {
         f2 a = {v[m], v[m + 4]};
-        f2 kk = {T.p[m], T.p[m]};
+        f2 kk = {T3.p[m], T3.p[m]};
         acc += a * kk;
       }
       const int y = R0 + r;
       const int X = C0 / SS + 2 * pq;
       if (INT) {
-        *reinterpret_cast<f2 *>(hs + (unsigned)(y * hsW + X)) = acc;
+        *reinterpret_cast<f2 *>(hs + hs_at(y, X, H)) = acc;
       } else {
         const int c = C0 + 8 * pq + 2;
         if (y < H) {
-          if (X < hsW) hs[(unsigned)(y * hsW + X)] = (c >= RP && c < W - RP) ? acc.x : 0.0f;
-          if (X + 1 < hsW) hs[(unsigned)(y * hsW + X + 1)] = (c + 4 >= RP && c + 4 < W - RP) ? acc.y : 0.0f;
+          if (X < hsW) hs[hs_at(y, X, H)] = (c >= RP && c < W - RP) ? acc.x : 0.0f;
+          if (X + 1 < hsW) hs[hs_at(y, X + 1, H)] = (c + 4 >= RP && c + 4 < W - RP) ? acc.y : 0.0f;
         }
       }
     }
   }
-  __syncthreads();
+  L0T_MARK(3);
 
+  const auto &T4 = phase_taps(Tin);
   // E. columns passes of both gradients, 2 rows x 4 columns per thread; zero unless RG <= y < H-RG
-  for (int i = tid; i < (TH / 2) * (TW / 4); i += kBlock) {
+  for (int i = tid; comp && i < (TH / 2) * (TW / 4); i += kBlock) {
     const int b = i / (TW / 4), g = i - b * (TW / 4);
     f4 vx[8], vy[8];
 #pragma unroll
@@ -321,11 +418,12 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
       f4 ax = {0.0f, 0.0f, 0.0f, 0.0f}, ay = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
       for (int m = 0; m < 7; ++m) {
-        mac4(ax, reinterpret_cast<const float *>(&vx[rr + m]), T.g[m]);
-        mac4(ay, reinterpret_cast<const float *>(&vy[rr + m]), T.d[m]);
+        mac4(ax, reinterpret_cast<const float *>(&vx[rr + m]), T4.g[m]);
+        mac4(ay, reinterpret_cast<const float *>(&vy[rr + m]), T4.d[m]);
       }
       const int y = R0 + 2 * b + rr, x = C0 + 4 * g;
-      if (INT) {
+      if (!(KLT_L0T_XST & 4)) {
+      } else if (INT) {
         st4(gx0 + (unsigned)(y * W + x), ax);
         st4(gy0 + (unsigned)(y * W + x), ay);
       } else {
@@ -348,6 +446,12 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
       }
     }
   }
+#ifdef KLT_TRACK_PROF
+  if (tid == 0 && (blockIdx.x & 63) == 0) {
+    atomicAdd(&g_l0s_prof[(STAGED ? 32 : 0) + 28], (unsigned long long)(clock64() - tprev));
+    atomicAdd(&g_l0s_prof[(STAGED ? 32 : 0) + 21], 1ull);
+  }
+#endif
 }
 
 __global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ src, int spitch, int W, int H,
@@ -375,6 +479,552 @@ __global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ s
   else
     pyr_l0_tile<false>(lds, src, spitch, W, H, T, vec_u8, img0, gx0, gy0, hs, hsW, do_hs, vec_out, C0, R0,
                        threadIdx.x);
+}
+
+// ---------------------------------------------------------------------------
+// k_pyr_l0p: k_pyr_l0 as a persistent kernel.  Each workgroup walks a run of
+// tiles (XCD-aware: XCD x takes the x-th eighth of the tiles of all frames in
+// order) with 4 computing waves and one loading wave.  The loading wave
+// fetches the next tile's u8 rows straight into LDS (global_load_lds_dword)
+// while the current tile is computed; the computing waves issue no loads, so
+// their stores drain in the background instead of being waited for -- on gfx9
+// loads and stores share one in-order counter, and a workgroup's waves also
+// wait for their stores before they end.  Needs dword-aligned u8 rows
+// (vec_u8) and vec_out; results are the tile kernel's.
+// ---------------------------------------------------------------------------
+constexpr int L0P_NT = kBlock + 64;
+constexpr int L0P_NDMA = (l0::UH * l0::UQ + 63) / 64;  // DMA instructions per tile
+static_assert(l0::U8, "k_pyr_l0p stages bytes");
+
+#ifndef KLT_L0P_WPE
+#define KLT_L0P_WPE 5
+#endif
+__global__ __launch_bounds__(L0P_NT) __attribute__((amdgpu_waves_per_eu(KLT_L0P_WPE))) void k_pyr_l0p(DefTaps T, const uint8_t *__restrict__ src, int spitch, int W,
+                                                   int H, float *__restrict__ img0, float *__restrict__ gx0,
+                                                   float *__restrict__ gy0, float *__restrict__ hs, int hsW,
+                                                   int do_hs, long fs_src, long fs0, long fs_hs, int ty0,
+                                                   int tiles_x, int tiles_y, int nframes) {
+  using namespace l0;
+  __shared__ __attribute__((aligned(16))) float lds[LDS];
+  __shared__ __attribute__((aligned(16))) uint32_t us[L0P_NDMA * 64];
+  (void)T;  // read through the kernarg segment (TapsK)
+  const TapsK tp = (TapsK)__builtin_amdgcn_kernarg_segment_ptr();
+  const int tid = threadIdx.x, lane = tid & 63;
+  const bool loader = tid >= kBlock;
+  const int per_frame = tiles_x * tiles_y, total = per_frame * nframes;
+  const int per = (int)gridDim.x / 8, chunk = (total + 7) / 8;
+  const int xcd = (int)(blockIdx.x % 8);
+  const int t_end = min(total, (xcd + 1) * chunk);
+  const unsigned us0 = (unsigned)(uintptr_t)us;
+  struct Tile {
+    int z, C0, R0;
+  };
+  auto tile = [&](int t) {
+    const int z = t / per_frame, rem = t - z * per_frame, by = rem / tiles_x, bx = rem - by * tiles_x;
+    return Tile{z, bx * TW, (by + ty0) * TH};
+  };
+  // u8 rows [R0-5, R0+39), dwords at columns C0-12+4q, clamped as k_pyr_l0's edge tiles clamp them
+  auto dma = [&](int t) {
+    const Tile q = tile(t);
+    int ln = lane;
+    asm volatile("" : "+v"(ln));  // per-lane offsets are recomputed, not kept live across the loop
+    const uint8_t *f = src + q.z * fs_src;
+#pragma unroll
+    for (int k = 0; k < L0P_NDMA; ++k) {
+      const int i = min(ln + 64 * k, UH * UQ - 1);
+      const int r = i / UQ, c = i - r * UQ;
+      const int x = clampi(q.C0 - 12 + 4 * c, 0, W - 4), y = clampi(q.R0 - RG - RS + r, 0, H - 1);
+      const uint8_t *p = f + (unsigned)(y * spitch + x);
+      asm volatile("global_load_lds_dword %0, off" ::"v"(p), "{m0}"(us0 + 256u * k) : "memory");
+    }
+  };
+  int t = xcd * chunk + (int)(blockIdx.x / 8);
+  if (loader && t < t_end) {
+    dma(t);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  while (t < t_end) {
+    const Tile q = tile(t);
+    int tl = tid;
+    asm volatile("" : "+v"(tl));  // likewise the phases' per-thread indexing
+    const int nxt = t + per;
+    // the loading wave refills `us` once phase B has consumed it
+    auto hook = [&]() {
+      if (loader && nxt < t_end) dma(nxt);
+    };
+    const bool interior = (hsW * SS == W) && (hsW % 2 == 0) && q.C0 >= 12 && q.C0 + 84 <= W && q.R0 >= 5 &&
+                          q.R0 + TH + 7 <= H;
+    DefTapsK &Tk = *fresh_taps(tp);
+    const uint8_t *fsrc = src + q.z * fs_src;
+    float *fi = img0 + q.z * fs0, *fx = gx0 + q.z * fs0, *fy = gy0 + q.z * fs0, *fh = hs + q.z * fs_hs;
+    if (interior)
+      pyr_l0_tile<true, true>(lds, fsrc, spitch, W, H, Tk, 1, fi, fx, fy, fh, hsW, do_hs, 1, q.C0, q.R0, tl, us,
+                              hook);
+    else
+      pyr_l0_tile<false, true>(lds, fsrc, spitch, W, H, Tk, 1, fi, fx, fy, fh, hsW, do_hs, 1, q.C0, q.R0, tl, us,
+                               hook);
+#ifdef KLT_TRACK_PROF
+    const long long tw0 = clock64();
+#endif
+    if (loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef KLT_TRACK_PROF
+    if (tid == kBlock && (blockIdx.x & 63) == 0) atomicAdd(&g_l0s_prof[62], (unsigned long long)(clock64() - tw0));
+#endif
+    __syncthreads();
+#ifdef KLT_TRACK_PROF
+    if (tid == 0 && (blockIdx.x & 63) == 0) atomicAdd(&g_l0s_prof[63], (unsigned long long)(clock64() - tw0));
+#endif
+    t = nxt;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_pyr_l0s: k_pyr_l0's outputs, computed by rolling down vertical strips.
+// One workgroup owns a 64-column strip of rows [S0, S1) and walks it in steps
+// of TH rows.  The rows that consecutive steps share in the separable column
+// passes (4 rows of the smoothing rows pass, 6 rows of each gradient rows
+// pass) stay in LDS instead of being recomputed as tile halos, so a step
+// computes TH new rows of every pass.  A step with base R0:
+//   u8    rows [R0+5, R0+5+TH)  -> t1 (smoothing rows pass), LDS rows 4..TH+3
+//   img0  rows [R0+3, R0+3+TH)  <- t1 LDS rows 0..TH+3   (LDS + HBM), hs (HBM)
+//   tx/ty rows [R0+3, R0+3+TH)  <- img0                    LDS rows 6..TH+5
+//   gx/gy rows [R0, R0+TH)      <- tx/ty LDS rows 0..TH+5 (HBM)
+// then t1 rows TH..TH+3 and tx/ty rows TH..TH+5 move to the top for the next
+// step.  A warm-up step at R0 = S0-TH computes only what those carried rows
+// and img0/hs rows [S0, S0+3) need.
+// Waves 0-3 compute and only store to HBM; wave 4 only loads: it fetches the
+// u8 rows of step s+2 while step s runs and puts step s+1's into LDS.  On
+// gfx9 loads and stores share one in-order counter, so a computing wave that
+// also loaded would wait for its own stores to drain before using a load.
+// Every output is the tile kernel's sum term for term; the +0 start is left
+// out only where every term is >= +0 (u8 or img0 times a positive gauss tap),
+// where it cannot change a bit.
+// Needs W % 8 == 0, 4-byte aligned u8 rows (dword loads), hsW == W/4.
+// ---------------------------------------------------------------------------
+#ifndef KLT_L0S_TH
+#define KLT_L0S_TH 16
+#endif
+#ifndef KLT_L0S_PI
+#define KLT_L0S_PI 92
+#define KLT_L0S_PT 84
+#define KLT_L0S_PX 64
+#endif
+#ifndef KLT_L0S_ERB
+#define KLT_L0S_ERB 2
+#endif
+namespace l0s {
+constexpr int RS = 2, RG = 3, RP = 10, SS = 4, TW = 64, TH = KLT_L0S_TH;
+constexpr int NT = 256;       // computing threads (waves 0-3)
+constexpr int NTB = NT + 64;  // + the loading wave
+constexpr int NG = 21;        // t1 / img0 column groups: LDS idx k <-> global column C0-8+k, k < 84
+constexpr int UQ = 23;        // u8 dwords per row: global columns [C0-12, C0+80)
+constexpr int PUB = 23, PI = KLT_L0S_PI, PT = KLT_L0S_PT, PX = KLT_L0S_PX;
+constexpr int T1R = TH + 4, TXR = TH + 6;
+#ifndef KLT_L0S_LEAD
+#define KLT_L0S_LEAD 2
+#endif
+constexpr int LEAD = KLT_L0S_LEAD;  // u8 rows are fetched LEAD steps ahead into a ring of LEAD slots
+constexpr int USLOT = ((TH * UQ + 63) / 64) * 64;  // dwords per ring slot (whole 64-lane DMA rows)
+constexpr int OFF_IM = LEAD * USLOT, OFF_T1 = OFF_IM + TH * PI;  // t1: 2 buffers (step parity)
+constexpr int OFF_TX = OFF_T1 + 2 * T1R * PT;                     // tx, ty: 2 buffers each (step parity)
+constexpr int SZ_TX = TXR * PX;
+constexpr int LDS = OFF_TX + 4 * SZ_TX;
+constexpr int NLD = (TH * UQ + 63) / 64;  // u8 dwords per loading lane and step
+constexpr int RB = NT / NG;               // rows per pass of the 21-group mapping (12)
+constexpr int RBC = TH / 8;               // img0 rows per smoothing columns-pass item (8 x 21 items)
+constexpr int ERB = KLT_L0S_ERB, NRB = TH / ERB;  // gradient rows per columns-pass item, row blocks
+static_assert(TH % 16 == 0 && 8 * TH <= NT && 32 * NRB <= NT && PI >= 84 && PT >= 84 && PX >= 64, "l0s shape");
+}  // namespace l0s
+
+// The taps are read from the kernarg segment (T is k_pyr_l0s's first
+// argument, at offset 0) through a pointer re-laundered per pass: the
+// compiler cannot then hoist all 40 taps (80 SGPRs as broadcast pairs) out of
+// the step loop and spill them to VGPR lanes; each pass loads its own.
+
+__device__ __forceinline__ f4 mul4(const float *v, float k) {
+  f2 lo = {v[0], v[1]}, hi = {v[2], v[3]};
+  f2 kk = {k, k};
+  lo = lo * kk;
+  hi = hi * kk;
+  return f4{lo.x, lo.y, hi.x, hi.y};
+}
+
+// Loading wave: the u8 rows [y0, y0+TH) of the strip go straight to LDS
+// ring slot `slot` by LDS-DMA (global_load_lds_dword: lane l of instruction k
+// lands at dword 64k+l, i.e. row (64k+l)/UQ, dword (64k+l)%UQ of the slot),
+// clamped into the frame (clamped values only feed outputs that a zero-border
+// rule replaces).  Always exactly NLD instructions, so that counted waits
+// (vmcnt) identify a step's rows.  Written in asm: the compiler neither sees
+// nor waits for these loads; the loading wave waits for them itself.
+__device__ __forceinline__ void l0s_dma(const uint8_t *__restrict__ src, int spitch, int W, int H, int C0, int y0,
+                                        unsigned slot_lds, int lane) {
+  using namespace l0s;
+#pragma unroll
+  for (int k = 0; k < NLD; ++k) {
+    const int i = min(lane + 64 * k, TH * UQ - 1);
+    const int r = i / UQ, q = i - r * UQ;
+    const int x = clampi(C0 - 12 + 4 * q, 0, W - 4), y = clampi(y0 + r, 0, H - 1);
+    const uint8_t *p = src + (unsigned)(y * spitch + x);
+    asm volatile("global_load_lds_dword %0, off" ::"v"(p), "{m0}"(slot_lds + 256u * k) : "memory");
+  }
+}
+template <int N>
+__device__ __forceinline__ void l0s_dma_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// One step in four passes separated by barriers; each pass is instantiated for
+// interior steps (INT: no clamp, no zero-border rule, every store in range)
+// and for the rest, and chosen per pass so that the loop body (and the
+// loading wave's registers) exists once.
+struct L0sStep {
+  const uint32_t *u;  // this step's u8 rows [TH][PUB]
+  float *t1, *im, *tx, *ty;  // this step's t1 [T1R][PT], img0 [TH][PI], tx/ty [TXR][PX]
+  TapsK tp;
+  int W, H;
+  float *img0, *gx0, *gy0, *hs;
+  int hsW, do_hs, C0, R0, ylo, yhi;
+  bool warm;
+  int tid;
+};
+
+#ifndef KLT_L0S_XST  // timing experiments only: bit 1 img0, 2 hs, 4 gx/gy stores
+#define KLT_L0S_XST 7
+#endif
+// B. smoothing rows pass of the new u8 rows -> t1 rows 4..TH+3; zero unless RS <= x < W-RS.
+//    Warm-up: only the last 10 (they feed img0 rows [S0-3, S0+3)).
+template <bool INT>
+__device__ __forceinline__ void l0s_pass_b(const L0sStep &P) {
+  using namespace l0s;
+  const uint32_t *u = P.u;
+  float *t1 = P.t1;
+  const TapsK T = fresh_taps(P.tp);
+  const int g21 = P.tid % NG, r21 = P.tid / NG;
+  const int rmin = P.warm ? TH - 10 : 0;
+#pragma unroll
+  for (int k = 0; k < (TH + RB - 1) / RB; ++k) {
+    const int r = r21 + RB * k;
+    if (r21 < RB && r < TH && r >= rmin) {
+      const uint32_t *row = u + r * PUB + g21;
+      const uint32_t d0 = row[0], d1 = row[1], d2 = row[2];
+      float v[12];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = (float)((d0 >> (8 * e)) & 0xFF);
+        v[4 + e] = (float)((d1 >> (8 * e)) & 0xFF);
+        v[8 + e] = (float)((d2 >> (8 * e)) & 0xFF);
+      }
+      f4 acc = mul4(v + 2, T->s[0]);  // terms >= +0: 0 + t == t
+#pragma unroll
+      for (int m = 1; m < 5; ++m) mac4(acc, v + 2 + m, T->s[m]);
+      if (!INT) {
+        const int x = P.C0 - 8 + 4 * g21;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (!(x + e >= RS && x + e < P.W - RS)) acc[e] = 0.0f;
+      }
+      st4(t1 + (4 + r) * PT + 4 * g21, acc);
+    }
+  }
+}
+
+// C. smoothing columns pass -> img0 rows 0..TH-1 (LDS, and HBM for the strip's own rows);
+//    zero unless RS <= y < H-RS.  Warm-up: rows TH-6.. only.
+template <bool INT>
+__device__ __forceinline__ void l0s_pass_c(const L0sStep &P) {
+  using namespace l0s;
+  const int g21 = P.tid % NG, r21 = P.tid / NG;
+  if (r21 >= 8) return;
+  float *im = P.im;
+  const float *col = P.t1 + (r21 * RBC) * PT + 4 * g21;
+  const TapsK T = fresh_taps(P.tp);
+  f4 v[RBC + 4];
+#pragma unroll
+  for (int k = 0; k < RBC + 4; ++k) v[k] = ld4(col + k * PT);
+  const int rmin = P.warm ? TH - 6 : 0;
+#pragma unroll
+  for (int rr = 0; rr < RBC; ++rr) {
+    const int i = r21 * RBC + rr;
+    if (i < rmin) continue;
+    f4 acc = mul4(reinterpret_cast<const float *>(&v[rr]), T->s[0]);
+#pragma unroll
+    for (int m = 1; m < 5; ++m) mac4(acc, reinterpret_cast<const float *>(&v[rr + m]), T->s[m]);
+    const int y = P.R0 + 3 + i, x = P.C0 - 8 + 4 * g21;
+    if (!INT && !(y >= RS && y < P.H - RS)) acc = f4{0.0f, 0.0f, 0.0f, 0.0f};
+    st4(im + i * PI + 4 * g21, acc);
+    if ((KLT_L0S_XST & 1) && g21 >= 2 && g21 < 18) {
+      if (INT)
+        st4(P.img0 + (unsigned)(y * P.W + x), acc);
+      else if (y >= P.ylo && y < P.yhi && x < P.W)
+        st4(P.img0 + (unsigned)(y * P.W + x), acc);
+    }
+  }
+}
+
+// D2. gradient rows passes -> tx/ty rows 6..TH+5; zero unless RG <= x < W-RG
+template <bool INT>
+__device__ __forceinline__ void l0s_pass_d2(const L0sStep &P) {
+  using namespace l0s;
+  const float *im = P.im;
+  float *tx = P.tx, *ty = P.ty;
+  const TapsK T = fresh_taps(P.tp);
+  const int g = P.tid & 15, rl = P.tid >> 4;
+  const int rmin = P.warm ? TH - 6 : 0;
+#pragma unroll
+  for (int k = 0; k < TH / 16; ++k) {
+    const int i = rl + 16 * k;
+    if (i < rmin) continue;
+    const float *row = im + i * PI + 4 * g + 4;  // idx 4g+4 <-> global C0+4g-4
+    float v[12];
+    *reinterpret_cast<f4 *>(v) = ld4(row);
+    *reinterpret_cast<f4 *>(v + 4) = ld4(row + 4);
+    *reinterpret_cast<f4 *>(v + 8) = ld4(row + 8);
+    f4 ax = {0.0f, 0.0f, 0.0f, 0.0f}, ay = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int m = 0; m < 7; ++m) {
+      mac4(ax, v + 1 + m, T->d[m]);
+      mac4(ay, v + 1 + m, T->g[m]);
+    }
+    if (!INT) {
+      const int x = P.C0 + 4 * g;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (!(x + e >= RG && x + e < P.W - RG)) {
+          ax[e] = 0.0f;
+          ay[e] = 0.0f;
+        }
+      }
+    }
+    st4(tx + (6 + i) * PX + 4 * g, ax);
+    st4(ty + (6 + i) * PX + 4 * g, ay);
+  }
+}
+
+// D3. pyramid rows pass at columns 4X+2 (two per item) -> hs; zero unless RP <= c < W-RP.
+//     Item i < 8*TH; warm-up: rows of [S0, S0+3) only.
+template <bool INT>
+__device__ __forceinline__ void l0s_pass_d3(const L0sStep &P, int i) {
+  using namespace l0s;
+  const int pq = i & 7, r = i >> 3;
+  if (P.warm && r < TH - 3) return;
+  const TapsK T = fresh_taps(P.tp);
+  const float *row = P.im + r * PI + 8 * pq;  // idx 8pq <-> global C0+8pq-8
+  float v[28];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) *reinterpret_cast<f4 *>(v + 4 * k) = ld4(row + 4 * k);
+  f2 acc = f2{v[0], v[4]} * f2{T->p[0], T->p[0]};  // terms >= +0
+#pragma unroll
+  for (int m = 1; m < 21; ++m) {
+    f2 a = {v[m], v[m + 4]};
+    f2 kk = {T->p[m], T->p[m]};
+    acc += a * kk;
+  }
+  const int y = P.R0 + 3 + r, X = P.C0 / SS + 2 * pq;
+  if (!(KLT_L0S_XST & 2)) {
+  } else if (INT) {
+    *reinterpret_cast<f2 *>(P.hs + hs_at(y, X, P.H)) = acc;
+  } else if (y >= P.ylo && y < P.yhi) {
+    const int c = P.C0 + 8 * pq + 2;
+    if (X < P.hsW) P.hs[hs_at(y, X, P.H)] = (c >= RP && c < P.W - RP) ? acc.x : 0.0f;
+    if (X + 1 < P.hsW) P.hs[hs_at(y, X + 1, P.H)] = (c + 4 >= RP && c + 4 < P.W - RP) ? acc.y : 0.0f;
+  }
+}
+
+// E. gradient columns passes -> gx (tx, gauss) / gy (ty, derivative); zero unless RG <= y < H-RG
+template <bool INT>
+__device__ __forceinline__ void l0s_pass_e(const L0sStep &P) {
+  using namespace l0s;
+  const int tid = P.tid;
+  const int g = tid & 15, rb = (tid >> 4) % NRB;
+  const int grad = __builtin_amdgcn_readfirstlane((tid >> 4) / NRB);  // wave-uniform
+  const float *sp = (grad ? P.ty : P.tx) + (rb * ERB) * PX + 4 * g;
+  const TapsK T = fresh_taps(P.tp);
+  const __attribute__((address_space(4))) float *tap = grad ? T->d : T->g;
+  float *dst = grad ? P.gy0 : P.gx0;
+  f4 v[ERB + 6];
+#pragma unroll
+  for (int k = 0; k < ERB + 6; ++k) v[k] = ld4(sp + k * PX);
+#pragma unroll
+  for (int j = 0; j < ERB; ++j) {
+    f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int m = 0; m < 7; ++m) mac4(acc, reinterpret_cast<const float *>(&v[j + m]), tap[m]);
+    const int y = P.R0 + rb * ERB + j, x = P.C0 + 4 * g;
+    if (!(KLT_L0S_XST & 4)) {
+    } else if (INT) {
+      st4(dst + (unsigned)(y * P.W + x), acc);
+    } else if (y >= P.ylo && y < P.yhi && x < P.W) {
+      if (!(y >= RG && y < P.H - RG)) acc = f4{0.0f, 0.0f, 0.0f, 0.0f};
+      st4(dst + (unsigned)(y * P.W + x), acc);
+    }
+  }
+}
+
+#ifndef KLT_L0S_WPE
+#define KLT_L0S_WPE 1
+#endif
+// Steps k = 0 (warm-up), 1..n; step k has base R0 = S0 + (k-1)*TH.  Passes of
+// consecutive steps are software-pipelined so that a step costs two barriers:
+//   prologue: B(0) | C(0)
+//   iteration j = 0..n:  I1 = D(j) + B(j+1)  |  I2 = E(j) + C(j+1)
+// (B writes t1 and C reads it; D writes tx/ty and E reads them: t1 and tx/ty
+// are double-buffered by step parity, img0 is single: C(j+1) runs after D(j).)
+__global__ __launch_bounds__(l0s::NTB) __attribute__((amdgpu_waves_per_eu(KLT_L0S_WPE))) void k_pyr_l0s(
+    DefTaps T, const uint8_t *__restrict__ src, int spitch, int W, int H, float *__restrict__ img0,
+    float *__restrict__ gx0, float *__restrict__ gy0, float *__restrict__ hs, int hsW, int do_hs, long fs_src,
+    long fs0, long fs_hs, int row_lo, int row_hi, int strip_h, int nstrips, int tiles_x) {
+  using namespace l0s;
+  __shared__ __attribute__((aligned(16))) float lds[LDS];
+  (void)T;  // read through the kernarg segment (TapsK)
+  const TapsK tp = (TapsK)__builtin_amdgcn_kernarg_segment_ptr();
+  int bx, by;
+  if (!xcd_tile(tiles_x, nstrips, bx, by)) return;  // whole workgroup
+  src += blockIdx.z * fs_src;
+  img0 += blockIdx.z * fs0;
+  gx0 += blockIdx.z * fs0;
+  gy0 += blockIdx.z * fs0;
+  hs += blockIdx.z * fs_hs;
+  const int C0 = bx * TW, S0 = row_lo + by * strip_h, S1 = min(S0 + strip_h, row_hi);
+  const int n = (S1 - S0 + TH - 1) / TH;       // real steps
+  const bool hint = C0 >= 12 && C0 + 80 <= W;  // no column clamp or zero-border rule in the strip
+  const int tid = threadIdx.x;
+  const bool comp = tid < NT, loader = !comp;
+  const int lane = tid & 63;
+  const unsigned lds0 = (unsigned)(uintptr_t)lds;
+#ifdef KLT_TRACK_PROF
+  long long tph = clock64(), pw[4] = {0, 0, 0, 0}, pt[4] = {0, 0, 0, 0}, pro = 0;
+#define L0S_SYNC(k)                      \
+  {                                      \
+    const long long t_ = clock64();      \
+    pw[k] += t_ - tph;                   \
+    __syncthreads();                     \
+    const long long u_ = clock64();      \
+    pt[k] += u_ - tph;                   \
+    tph = u_;                            \
+  }
+#else
+#define L0S_SYNC(k) __syncthreads()
+#endif
+  // step k's pass arguments and buffers
+  auto step = [&](int k) {
+    const int R0 = S0 + (k - 1) * TH;
+    const int par = k & 1;
+    return L0sStep{reinterpret_cast<const uint32_t *>(lds) + (k % LEAD) * USLOT, lds + OFF_T1 + par * T1R * PT,
+                   lds + OFF_IM, lds + OFF_TX + 2 * par * SZ_TX, lds + OFF_TX + (2 * par + 1) * SZ_TX, tp, W, H,
+                   img0, gx0, gy0, hs, hsW, do_hs, C0, R0, S0, S1, k == 0, tid};
+  };
+  // rows-interior step (HBM stores and the row zero-border rules need no checks)
+  auto rows_int = [&](int k) {
+    const int R0 = S0 + (k - 1) * TH;
+    return hint && k > 0 && R0 >= RG && R0 + TH + 5 <= H && R0 + TH + 3 <= S1;
+  };
+  auto dma = [&](int k) {  // u8 rows of step k -> ring slot k % LEAD
+    l0s_dma(src, spitch, W, H, C0, S0 + (k - 1) * TH + 5, lds0 + 4u * (unsigned)((k % LEAD) * USLOT), lane);
+  };
+  auto carry_t1 = [&](int k) {  // t1 rows TH..TH+3 of step k-1 -> rows 0..3 of step k
+    if (tid < 4 * NG) {
+      const float *a = lds + OFF_T1 + ((k - 1) & 1) * T1R * PT;
+      float *b = lds + OFF_T1 + (k & 1) * T1R * PT;
+      const int g21 = tid % NG, r21 = tid / NG;
+      st4(b + r21 * PT + 4 * g21, ld4(a + (TH + r21) * PT + 4 * g21));
+    }
+  };
+  auto carry_txy = [&](int k) {  // tx/ty rows TH..TH+5 of step k-1 -> rows 0..5 of step k
+    if (tid >= NT - 2 * 6 * 16 && tid < NT) {
+      const int i = tid - (NT - 2 * 6 * 16), which = i / 96, j = i - which * 96, r = j >> 4, g = j & 15;
+      const float *a = lds + OFF_TX + (2 * ((k - 1) & 1) + which) * SZ_TX;
+      float *b = lds + OFF_TX + (2 * (k & 1) + which) * SZ_TX;
+      st4(b + r * PX + 4 * g, ld4(a + (TH + r) * PX + 4 * g));
+    }
+  };
+
+  // prologue: B(0) | C(0)
+  if (loader) {
+#pragma unroll
+    for (int k = 0; k < LEAD; ++k) dma(k);
+    l0s_dma_wait<NLD * (LEAD - 1)>();  // step 0's rows landed
+  }
+  __syncthreads();
+#ifdef KLT_TRACK_PROF
+  pro = clock64() - tph;
+  tph = clock64();
+#endif
+  if (comp) {
+    const L0sStep P = step(0);
+    l0s_pass_b<false>(P);
+  }
+  __syncthreads();
+  if (comp) {
+    const L0sStep P = step(0);
+    l0s_pass_c<false>(P);
+  } else if (n >= 1) {
+    dma(LEAD);
+    l0s_dma_wait<NLD * (LEAD - 1)>();  // step 1's rows landed
+  }
+  __syncthreads();
+
+  for (int j = 0; j <= n; ++j) {
+    // I1: D(j) + B(j+1)
+    if (comp) {
+      const L0sStep P = step(j);
+      const bool in = rows_int(j);
+      carry_txy(j);
+      if (hint)
+        l0s_pass_d2<true>(P);
+      else
+        l0s_pass_d2<false>(P);
+      if (do_hs && tid >= NT - 8 * TH) {
+        if (in)
+          l0s_pass_d3<true>(P, tid - (NT - 8 * TH));
+        else
+          l0s_pass_d3<false>(P, tid - (NT - 8 * TH));
+      }
+      if (j < n) {
+        const L0sStep Q = step(j + 1);
+        carry_t1(j + 1);
+        if (hint)
+          l0s_pass_b<true>(Q);
+        else
+          l0s_pass_b<false>(Q);
+      }
+    }
+    L0S_SYNC(0);
+    // I2: E(j) + C(j+1); the loading wave fetches step j+1+LEAD and waits for step j+2
+    if (comp) {
+      if (j >= 1 && tid < 32 * NRB) {
+        const L0sStep P = step(j);
+        if (rows_int(j))
+          l0s_pass_e<true>(P);
+        else
+          l0s_pass_e<false>(P);
+      }
+      if (j < n) {
+        const L0sStep Q = step(j + 1);
+        if (rows_int(j + 1))
+          l0s_pass_c<true>(Q);
+        else
+          l0s_pass_c<false>(Q);
+      }
+    } else if (j + 2 <= n) {
+      dma(j + 1 + LEAD);
+      l0s_dma_wait<NLD * (LEAD - 1)>();
+    }
+    L0S_SYNC(1);
+  }
+  if (loader) l0s_dma_wait<0>();  // nothing may land in LDS after the workgroup ends
+#ifdef KLT_TRACK_PROF
+  if ((tid & 63) == 0) {
+    const int wv = tid >> 6;
+    for (int q = 0; q < 4; ++q) atomicAdd(&g_l0s_prof[8 + 4 * wv + q], (unsigned long long)pw[q]);
+    if (wv == 0) {
+      for (int q = 0; q < 4; ++q) atomicAdd(&g_l0s_prof[1 + q], (unsigned long long)pt[q]);
+      atomicAdd(&g_l0s_prof[0], (unsigned long long)pro);
+      atomicAdd(&g_l0s_prof[5], 1ull);
+    }
+  }
+#endif
+#undef L0S_SYNC
 }
 
 // ---------------------------------------------------------------------------
@@ -423,13 +1073,13 @@ __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs,
       const int i = tid + k * NT;
       if (i < NA) {
         const int r = i / NQ, q = i - r * NQ;
-        const long rowp = (long)clampi(SS * y0 - 20 + r, 0, H - 1) * W1;
+        const int row = clampi(SS * y0 - 20 + r, 0, H - 1);
         const int X = x0 - 4 + 4 * q;
-        if (vec) {
-          v[k] = ld4(hs + rowp + clampi(X, 0, W1 - 4));
+        if (vec) {  // a 4-aligned group never straddles a slab
+          v[k] = ld4(hs + hs_at(row, clampi(X, 0, W1 - 4), H));
         } else {
-          v[k] = f4{hs[rowp + clampi(X, 0, W1 - 1)], hs[rowp + clampi(X + 1, 0, W1 - 1)],
-                    hs[rowp + clampi(X + 2, 0, W1 - 1)], hs[rowp + clampi(X + 3, 0, W1 - 1)]};
+          v[k] = f4{hs[hs_at(row, clampi(X, 0, W1 - 1), H)], hs[hs_at(row, clampi(X + 1, 0, W1 - 1), H)],
+                    hs[hs_at(row, clampi(X + 2, 0, W1 - 1), H)], hs[hs_at(row, clampi(X + 3, 0, W1 - 1), H)]};
         }
       }
     }
@@ -1454,6 +2104,9 @@ struct klt_hip_ctx {
   int track_group = 0;  // features per wave for small windows (0: default)
   int track_order = 0;  // 0: band-sorted, XCD-major processing order; 1: input order
   int track_patch = 1;  // one-feature waves gather through a lane patch when the window fits
+  int l0_mode = 0;       // level 0: 0 k_pyr_l0 tiles (default), 1 k_pyr_l0s strips, 2 k_pyr_l0p persistent tiles
+  int l0p_blocks = 0;    // k_pyr_l0p resident workgroups (CUs x occupancy), filled on first use
+  int l0_strip_steps = 8;  // k_pyr_l0s steps per strip (strip height / TH)
   int serial_frames = 1;  // klt_hip_track_frames: 1 builds and tracks on one stream (default: the
                           // tracker and the pyramid kernels compete for the same CUs; overlap buys ~3 %)
   int *d_perm = nullptr;
@@ -1658,6 +2311,48 @@ DefTaps default_taps(const klt_hip_pyr_desc *d) {
   return T;
 }
 
+// Level 0 of the fused pyramid for F frames, rows [r0, r1) (global coordinates;
+// every built value is the full-frame value).  k_pyr_l0s when the shape allows
+// (the default), else k_pyr_l0, whose 32-row tiles may widen [r0, r1): the
+// rows actually built are returned in r0/r1.
+int launch_l0(klt_hip_ctx *c, hipStream_t st, const uint8_t *src, long pitch, long stride, int W, int H,
+              const DefTaps &T, int vec_u8, int vec_out, float *img, float *gx, float *gy, float *hs, int W1,
+              int do_hs, long fs0, long fsh, int F, int &r0, int &r1) {
+  if (r1 <= r0 || F <= 0) return 0;
+  const int tx = (W + l0s::TW - 1) / l0s::TW;
+  if (c->l0_mode == 1 && vec_u8 && W % 8 == 0 && (!do_hs || W1 * l0s::SS == W)) {
+    const int n = r1 - r0, want = l0s::TH * (c->l0_strip_steps > 0 ? c->l0_strip_steps : 1);
+    const int nstrips = (n + want - 1) / want;
+    const int strip_h = (n + nstrips - 1) / nstrips;
+    dim3 grid(xcd_grid(tx * nstrips), 1, F);
+    hipLaunchKernelGGL(k_pyr_l0s, grid, dim3(l0s::NTB), 0, st, T, src, (int)pitch, W, H, img, gx, gy, hs, W1,
+                       do_hs, stride, fs0, fsh, r0, r1, strip_h, nstrips, tx);
+    return check_launch(c, "k_pyr_l0s");
+  }
+  const int nty = (H + l0::TH - 1) / l0::TH;
+  const int ty0 = r0 / l0::TH, ty1 = r1 >= H ? nty : clampi((r1 + l0::TH - 1) / l0::TH, ty0, nty);
+  r0 = ty0 * l0::TH;
+  r1 = ty1 >= nty ? H : ty1 * l0::TH;
+  if (c->l0_mode == 2 && vec_u8 && vec_out) {
+    if (c->l0p_blocks == 0) {
+      int ncu = 0, per = 0;
+      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_pyr_l0p, L0P_NT, 0) != hipSuccess || ncu * per <= 0)
+        return fail(c, "k_pyr_l0p: cannot size the grid");
+      c->l0p_blocks = ncu * per;
+    }
+    const int tiles = tx * (ty1 - ty0) * F;
+    dim3 grid(xcd_grid(tiles < c->l0p_blocks ? tiles : c->l0p_blocks));
+    hipLaunchKernelGGL(k_pyr_l0p, grid, dim3(L0P_NT), 0, st, T, src, (int)pitch, W, H, img, gx, gy, hs, W1, do_hs,
+                       stride, fs0, fsh, ty0, tx, ty1 - ty0, F);
+    return check_launch(c, "k_pyr_l0p");
+  }
+  dim3 grid(xcd_grid(tx * (ty1 - ty0)), 1, F);
+  hipLaunchKernelGGL(k_pyr_l0, grid, dim3(kBlock), 0, st, src, (int)pitch, W, H, T, vec_u8, img, gx, gy, hs, W1,
+                     do_hs, vec_out, stride, fs0, fsh, ty0, tx, ty1 - ty0);
+  return check_launch(c, "k_pyr_l0");
+}
+
 int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
                 hipStream_t st) {
   Slot &S = c->slot[s];
@@ -1665,18 +2360,16 @@ int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t 
   const DefTaps T = default_taps(d);
   const bool two = d->nlevels == 2;
   const int W1 = two ? S.lv[1].w : 0, H1 = two ? S.lv[1].h : 0;
-  if (two && grow(c, &c->d_hs, &c->hs_cap, (size_t)(W1 > 0 ? W1 : 1) * H)) return -1;
+  if (two && grow(c, &c->d_hs, &c->hs_cap, (size_t)hs_size(W1 > 0 ? W1 : 1, H))) return -1;
   if ((long)W * H == 0) return 0;
   const int vec_u8 = (W % 4 == 0 && W >= 16 && pitch % 4 == 0 && ((uintptr_t)src & 3) == 0) ? 1 : 0;
   const int vec_out = (W % 4 == 0) ? 1 : 0;
   {
     TimedScope ts(c, T_L0, st);
-    const int tx = (W + l0::TW - 1) / l0::TW, ty = (H + l0::TH - 1) / l0::TH;
-    dim3 grid(xcd_grid(tx * ty));
-    hipLaunchKernelGGL(k_pyr_l0, grid, dim3(kBlock), 0, st, src, (int)pitch, W, H, T, vec_u8, S.lv[0].img,
-                       S.lv[0].gx, S.lv[0].gy, c->d_hs, W1, (two && W1 > 0) ? 1 : 0, vec_out, 0L, 0L, 0L, 0, tx,
-                       ty);
-    if (check_launch(c, "k_pyr_l0")) return -1;
+    int r0 = 0, r1 = H;
+    if (launch_l0(c, st, src, pitch, 0L, W, H, T, vec_u8, vec_out, S.lv[0].img, S.lv[0].gx, S.lv[0].gy, c->d_hs,
+                  W1, (two && W1 > 0) ? 1 : 0, 0L, 0L, 1, r0, r1))
+      return -1;
   }
   if (two && (long)W1 * H1 > 0) {
     TimedScope ts(c, T_L1, st);
@@ -1813,7 +2506,7 @@ int ensure_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, int frames) 
     h /= K.ss;
   }
   if (d->nlevels == 2) {
-    const size_t need = (size_t)(K.lv[1].w > 0 ? K.lv[1].w : 1) * d->nrows * frames;
+    const size_t need = (size_t)hs_size(K.lv[1].w > 0 ? K.lv[1].w : 1, d->nrows) * frames;
     if (K.hs_cap < need || !K.hs) {
       hipFree(K.hs);
       K.hs = nullptr;
@@ -1840,22 +2533,16 @@ int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const u
   const int vec_u8 =
       (W % 4 == 0 && W >= 16 && pitch % 4 == 0 && stride % 4 == 0 && ((uintptr_t)src & 3) == 0) ? 1 : 0;
   const int vec_out = (W % 4 == 0) ? 1 : 0;
-  const long fs0 = (long)W * H, fsh = (long)W1 * H, fs1 = (long)W1 * H1;
-  const int nty = (H + l0::TH - 1) / l0::TH;
-  const int ty0 = clampi(row_lo, 0, H) / l0::TH;
-  const int ty1 = row_hi >= H ? nty : clampi((row_hi + l0::TH - 1) / l0::TH, ty0, nty);
-  const int r0 = ty0 * l0::TH, r1 = ty1 >= nty ? H : ty1 * l0::TH;
+  const long fs0 = (long)W * H, fsh = hs_size(W1, H), fs1 = (long)W1 * H1;
+  int r0 = clampi(row_lo, 0, H), r1 = row_hi >= H ? H : clampi(row_hi, r0, H);
+  {
+    TimedScope ts(c, T_L0, st, F);
+    if (launch_l0(c, st, src, pitch, stride, W, H, T, vec_u8, vec_out, K.lv[0].img, K.lv[0].gx, K.lv[0].gy, K.hs,
+                  W1, (two && W1 > 0) ? 1 : 0, fs0, fsh, F, r0, r1))
+      return -1;
+  }
   K.vlo[0] = r0;
   K.vhi[0] = r1 >= H ? (1 << 30) : r1;
-  if (ty1 > ty0) {
-    TimedScope ts(c, T_L0, st, F);
-    const int tx = (W + l0::TW - 1) / l0::TW;
-    dim3 grid(xcd_grid(tx * (ty1 - ty0)), 1, F);
-    hipLaunchKernelGGL(k_pyr_l0, grid, dim3(kBlock), 0, st, src, (int)pitch, W, H, T, vec_u8, K.lv[0].img,
-                       K.lv[0].gx, K.lv[0].gy, K.hs, W1, (two && W1 > 0) ? 1 : 0, vec_out, stride, fs0, fsh, ty0,
-                       tx, ty1 - ty0);
-    if (check_launch(c, "k_pyr_l0")) return -1;
-  }
   if (two && (long)W1 * H1 > 0) {
     // an L1 tile at rows [y0, y0+TH) reads hs rows [4*y0-20, 4*y0-20+HR) (clamped to the image)
     const int nt1 = (H1 + l1::TH - 1) / l1::TH;
@@ -2068,6 +2755,16 @@ KLT_API int klt_hip_set_prof(klt_hip_ctx *c, void *dev) {
   c->prof = (unsigned long long *)dev;
   return 0;
 }
+
+// level-0 phase profile (64 counters, see g_l0s_prof); reset != 0 clears it
+KLT_API int klt_hip_l0s_prof(unsigned long long *out, int reset) {
+  if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_l0s_prof), sizeof(g_l0s_prof)) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long zero[64] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_l0s_prof), zero, sizeof(zero)) != hipSuccess) return -1;
+  }
+  return 0;
+}
 #endif
 
 KLT_API int klt_hip_set_frames_overlap(klt_hip_ctx *c, int overlap) {
@@ -2079,6 +2776,14 @@ KLT_API int klt_hip_set_frames_overlap(klt_hip_ctx *c, int overlap) {
 KLT_API int klt_hip_set_track_patch(klt_hip_ctx *c, int on) {
   if (!c) return fail(c, "set_track_patch: null context");
   c->track_patch = on ? 1 : 0;
+  return 0;
+}
+
+KLT_API int klt_hip_set_pyr_l0(klt_hip_ctx *c, int mode, int strip_steps) {
+  if (!c) return fail(c, "set_pyr_l0: null context");
+  if (mode < 0 || mode > 2) return fail(c, "set_pyr_l0: mode %d (0 tiles, 1 strips, 2 persistent tiles)", mode);
+  c->l0_mode = mode;
+  if (strip_steps > 0) c->l0_strip_steps = strip_steps;
   return 0;
 }
 
