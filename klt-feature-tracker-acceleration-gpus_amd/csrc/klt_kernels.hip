@@ -101,6 +101,15 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f4 ld4(const float *p) { return *reinterpret_cast<const f4 *>(p); }
 __device__ __forceinline__ void st4(float *p, f4 v) { *reinterpret_cast<f4 *>(p) = v; }
+#ifndef KLT_L0_OUTST
+#define KLT_L0_OUTST 1  // level-0 HBM stores: 0 plain, 1 nontemporal (measured 1-2 % faster)
+#endif
+__device__ __forceinline__ void st4_out(float *p, f4 v) {
+  if (KLT_L0_OUTST == 1)
+    __builtin_nontemporal_store(v, reinterpret_cast<f4 *>(p));
+  else
+    st4(p, v);
+}
 
 // acc[i] += v[i + off] * k for 4 lanes, as two packed-f32 pairs
 __device__ __forceinline__ void mac4(f4 &acc, const float *v, float k) {
@@ -110,6 +119,17 @@ __device__ __forceinline__ void mac4(f4 &acc, const float *v, float k) {
   alo += lo * kk;
   ahi += hi * kk;
   acc = f4{alo.x, alo.y, ahi.x, ahi.y};
+}
+
+// v[i] * k for 4 lanes: the first term of a sum whose terms are all >= +0
+// (u8 or smoothed values times a positive gauss tap), where 0 + t == t bit
+// for bit and the reference's +0 start can be left out
+__device__ __forceinline__ f4 mul4(const float *v, float k) {
+  f2 lo = {v[0], v[1]}, hi = {v[2], v[3]};
+  f2 kk = {k, k};
+  lo = lo * kk;
+  hi = hi * kk;
+  return f4{lo.x, lo.y, hi.x, hi.y};
 }
 
 struct DefTaps {
@@ -139,7 +159,11 @@ constexpr int IHB = (IH + 3) / 4;  // 4-row blocks of img0 computed
 #define KLT_L0_U8 1  // 1: stage the input tile as bytes (converted in the row pass)
 #endif
 constexpr bool U8 = KLT_L0_U8 != 0;
-constexpr int PU = KLT_L0_PU, PT = 84, PI = KLT_L0_PI, PX = TW;
+#ifndef KLT_L0_B8
+#define KLT_L0_B8 1  // smoothing rows pass: 8 outputs per item from 4 staged dwords (bytes only)
+#endif
+constexpr bool B8 = KLT_L0_B8 != 0;
+constexpr int PU = KLT_L0_PU, PT = B8 ? 88 : 84, PI = KLT_L0_PI, PX = TW;
 constexpr int PUB = 24;                   // U8: staged row pitch in dwords (96 bytes)
 constexpr int U_WORDS = U8 ? UH * PUB : UH * PU;
 constexpr int REG_A = U_WORDS > IH * PI ? U_WORDS : IH * PI;  // u during A-B, then img0 during C-D
@@ -230,7 +254,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
   float *tx = lds + REG_A;   // [IH][PX]      (after t1 is dead)
   float *ty = tx + IH * PX;
 
-  // A. u8 tile + halo -> float; every load issued before the first is used
+  // A. u8 tile + halo -> LDS; every load issued before the first is used
   if (!STAGED) {
     constexpr int NA = UH * UQ, PER = (NA + kBlock - 1) / kBlock;
     uint32_t w[PER];
@@ -273,8 +297,49 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
 
   const auto &T0 = phase_taps(Tin);
   // B. rows pass of the smoothing: t1 idx k <-> global C0-8+k; zero unless RS <= x < W-RS
-  for (int i = tid; comp && i < UH * NG; i += kBlock) {
-    const int r = i / NG, g = i - r * NG;
+  // 12 rows of the 21 column groups per pass: thread (g, r0) takes rows r0, r0+12, ... (no division per item)
+  const int g21 = tid % NG, r21 = tid / NG;
+  if (B8 && (U8 || STAGED)) {
+    // 23 rows of 11 eight-column groups per pass (t1 idx 0..87): bytes [8j, 8j+16) of a staged row
+    const int j = tid % 11, r0 = tid / 11;
+#pragma unroll
+    for (int k = 0; k < (UH + 22) / 23; ++k) {
+      const int r = r0 + 23 * k;
+      if (!comp || r0 >= 23 || r >= UH) break;
+      const uint32_t *row = STAGED ? us + r * UQ + 2 * j : reinterpret_cast<const uint32_t *>(u) + r * PUB + 2 * j;
+      const uint2 d01 = *reinterpret_cast<const uint2 *>(row), d23 = *reinterpret_cast<const uint2 *>(row + 2);
+      const uint32_t d[4] = {d01.x, d01.y, d23.x, d23.y};
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[4 * q + 0] = (float)(d[q] & 0xFF);
+        v[4 * q + 1] = (float)((d[q] >> 8) & 0xFF);
+        v[4 * q + 2] = (float)((d[q] >> 16) & 0xFF);
+        v[4 * q + 3] = (float)(d[q] >> 24);
+      }
+      f4 a0 = mul4(v + 2, T0.s[0]), a1 = mul4(v + 6, T0.s[0]);
+#pragma unroll
+      for (int m = 1; m < 5; ++m) {
+        mac4(a0, v + 2 + m, T0.s[m]);
+        mac4(a1, v + 6 + m, T0.s[m]);
+      }
+      if (!INT) {
+        const int x = C0 - 8 + 8 * j;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (!(x + e >= RS && x + e < W - RS)) a0[e] = 0.0f;
+          if (!(x + 4 + e >= RS && x + 4 + e < W - RS)) a1[e] = 0.0f;
+        }
+      }
+      st4(t1 + r * PT + 8 * j, a0);
+      st4(t1 + r * PT + 8 * j + 4, a1);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < (UH + 11) / 12; ++k) {
+    if (B8 && (U8 || STAGED)) break;
+    const int r = r21 + 12 * k, g = g21;
+    if (!comp || r21 >= 12 || r >= UH) break;
     float v[12];
     if (U8 || STAGED) {
       const uint32_t *row = STAGED ? us + r * UQ + g : reinterpret_cast<const uint32_t *>(u) + r * PUB + g;
@@ -292,9 +357,9 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
       *reinterpret_cast<f4 *>(v + 4) = ld4(row + 4);
       *reinterpret_cast<f4 *>(v + 8) = ld4(row + 8);
     }
-    f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    f4 acc = mul4(v + 2, T0.s[0]);
 #pragma unroll
-    for (int m = 0; m < 5; ++m) mac4(acc, v + 2 + m, T0.s[m]);
+    for (int m = 1; m < 5; ++m) mac4(acc, v + 2 + m, T0.s[m]);
     if (!INT) {
       const int x = C0 - 8 + 4 * g;
 #pragma unroll
@@ -308,17 +373,17 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
 
   const auto &T1 = phase_taps(Tin);
   // C. columns pass -> img0, 4 rows x 4 columns per thread; zero unless RS <= y < H-RS
-  for (int i = tid; comp && i < IHB * NG; i += kBlock) {
-    const int b = i / NG, g = i - b * NG;
+  if (comp && r21 < IHB) {  // IHB x 21 items, one per thread
+    const int b = r21, g = g21;
     const float *col = t1 + (4 * b) * PT + 4 * g;
     f4 v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = ld4(col + k * PT);
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
-      f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+      f4 acc = mul4(reinterpret_cast<const float *>(&v[rr]), T1.s[0]);
 #pragma unroll
-      for (int m = 0; m < 5; ++m) mac4(acc, reinterpret_cast<const float *>(&v[rr + m]), T1.s[m]);
+      for (int m = 1; m < 5; ++m) mac4(acc, reinterpret_cast<const float *>(&v[rr + m]), T1.s[m]);
       if (!INT) {
         const int y = R0 - RG + 4 * b + rr;
         if (!(y >= RS && y < H - RS)) acc = f4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -329,12 +394,15 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
   L0T_MARK(2);
 
   // D1. img0 tile -> HBM
-  for (int i = tid; comp && (KLT_L0T_XST & 1) && i < TH * (TW / 4); i += kBlock) {
-    const int r = i / (TW / 4), g = i - r * (TW / 4);
+  const int g16 = tid & 15, r16 = tid >> 4;
+#pragma unroll
+  for (int k = 0; k < TH / 16; ++k) {
+    const int r = r16 + 16 * k, g = g16;
+    if (!comp || !(KLT_L0T_XST & 1)) break;
     const int y = R0 + r, x = C0 + 4 * g;
     const f4 val = ld4(im + (r + RG) * PI + 8 + 4 * g);
     if (INT) {
-      st4(img0 + (unsigned)(y * W + x), val);
+      st4_out(img0 + (unsigned)(y * W + x), val);
     } else {
       if (y >= H || x >= W) continue;
       float *dst = img0 + (unsigned)(y * W + x);
@@ -345,8 +413,10 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
   }
   const auto &T2 = phase_taps(Tin);
   // D2. rows passes of both gradients; zero unless RG <= x < W-RG
-  for (int i = tid; comp && i < IH * (TW / 4); i += kBlock) {
-    const int r = i / (TW / 4), g = i - r * (TW / 4);
+#pragma unroll
+  for (int k = 0; k < (IH + 15) / 16; ++k) {
+    const int r = r16 + 16 * k, g = g16;
+    if (!comp || r >= IH) break;
     const float *row = im + r * PI + 4 * g + 4;  // img0 idx c0+4 <-> global C0+c0-4
     float v[12];
     *reinterpret_cast<f4 *>(v) = ld4(row);
@@ -381,9 +451,9 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
       float v[28];
 #pragma unroll
       for (int k = 0; k < 7; ++k) *reinterpret_cast<f4 *>(v + 4 * k) = ld4(row + 4 * k);
-      f2 acc = {0.0f, 0.0f};
+      f2 acc = f2{v[0], v[4]} * f2{T3.p[0], T3.p[0]};  // terms >= +0
 #pragma unroll
-      for (int m = 0; m < 21; ++m) {
+      for (int m = 1; m < 21; ++m) {
         f2 a = {v[m], v[m + 4]};
         f2 kk = {T3.p[m], T3.p[m]};
         acc += a * kk;
@@ -424,8 +494,8 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
       const int y = R0 + 2 * b + rr, x = C0 + 4 * g;
       if (!(KLT_L0T_XST & 4)) {
       } else if (INT) {
-        st4(gx0 + (unsigned)(y * W + x), ax);
-        st4(gy0 + (unsigned)(y * W + x), ay);
+        st4_out(gx0 + (unsigned)(y * W + x), ax);
+        st4_out(gy0 + (unsigned)(y * W + x), ay);
       } else {
         if (y >= H || x >= W) continue;
         if (!(y >= RG && y < H - RG)) {
@@ -642,13 +712,6 @@ static_assert(TH % 16 == 0 && 8 * TH <= NT && 32 * NRB <= NT && PI >= 84 && PT >
 // compiler cannot then hoist all 40 taps (80 SGPRs as broadcast pairs) out of
 // the step loop and spill them to VGPR lanes; each pass loads its own.
 
-__device__ __forceinline__ f4 mul4(const float *v, float k) {
-  f2 lo = {v[0], v[1]}, hi = {v[2], v[3]};
-  f2 kk = {k, k};
-  lo = lo * kk;
-  hi = hi * kk;
-  return f4{lo.x, lo.y, hi.x, hi.y};
-}
 
 // Loading wave: the u8 rows [y0, y0+TH) of the strip go straight to LDS
 // ring slot `slot` by LDS-DMA (global_load_lds_dword: lane l of instruction k
