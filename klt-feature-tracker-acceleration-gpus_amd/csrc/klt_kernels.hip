@@ -111,6 +111,13 @@ __device__ __forceinline__ void st4_out(float *p, f4 v) {
     st4(p, v);
 }
 
+__device__ __forceinline__ void st2_out(float *p, f2 v) {
+  if (KLT_L0_OUTST == 1)
+    __builtin_nontemporal_store(v, reinterpret_cast<f2 *>(p));
+  else
+    *reinterpret_cast<f2 *>(p) = v;
+}
+
 // acc[i] += v[i + off] * k for 4 lanes, as two packed-f32 pairs
 __device__ __forceinline__ void mac4(f4 &acc, const float *v, float k) {
   f2 lo = {v[0], v[1]}, hi = {v[2], v[3]};
@@ -163,6 +170,20 @@ constexpr bool U8 = KLT_L0_U8 != 0;
 #define KLT_L0_B8 1  // smoothing rows pass: 8 outputs per item from 4 staged dwords (bytes only)
 #endif
 constexpr bool B8 = KLT_L0_B8 != 0;
+#ifndef KLT_L0_E2
+#define KLT_L0_E2 1  // gradient column pass: 1: 4 rows x 2 columns per item, 0: 2 rows x 4 columns
+#endif
+constexpr bool E2 = KLT_L0_E2 != 0;
+static_assert(!E2 || TH % 4 == 0, "E2 blocks 4 rows");
+#ifndef KLT_L0_H4
+#define KLT_L0_H4 1  // pyramid rows pass: 1: 4 outputs per item (upper threads), 0: 2 per item (all threads)
+#endif
+constexpr bool H4 = KLT_L0_H4 != 0;
+#ifndef KLT_L0_HSLAST
+#define KLT_L0_HSLAST 0  // pyramid rows pass after the gradient column pass (1) or before it (0); equal within noise
+#endif
+constexpr bool HSLAST = KLT_L0_HSLAST != 0;
+static_assert(!H4 || (TH * TW / 16 <= kBlock && TW % 16 == 0), "H4 items");
 constexpr int PU = KLT_L0_PU, PT = B8 ? 88 : 84, PI = KLT_L0_PI, PX = TW;
 constexpr int PUB = 24;                   // U8: staged row pitch in dwords (96 bytes)
 constexpr int U_WORDS = U8 ? UH * PUB : UH * PU;
@@ -441,41 +462,123 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     st4(tx + r * PX + 4 * g, ax);
     st4(ty + r * PX + 4 * g, ay);
   }
-  const auto &T3 = phase_taps(Tin);
-  // D3. pyramid rows pass at columns 4X+2, two per thread; zero unless RP <= c < W-RP
-  if (do_hs && comp) {
-    for (int i = tid; i < TH * (TW / 8); i += kBlock) {
-      if (!(KLT_L0T_XST & 2)) break;
-      const int r = i / (TW / 8), pq = i - r * (TW / 8);
-      const float *row = im + (r + RG) * PI + 8 * pq;  // idx 8p <-> global C0+8p-8
-      float v[28];
-#pragma unroll
-      for (int k = 0; k < 7; ++k) *reinterpret_cast<f4 *>(v + 4 * k) = ld4(row + 4 * k);
-      f2 acc = f2{v[0], v[4]} * f2{T3.p[0], T3.p[0]};  // terms >= +0
-#pragma unroll
+  // D3 as a callable: before the D barrier (HSLAST 0) or after E (HSLAST 1),
+  // where the small hs stores are the last a workgroup issues and the
+  // gx/gy stores drain behind the hs pass instead of at the end of the tile
+  const auto d3 = [&]() {
+    const auto &T3 = phase_taps(Tin);
+    // D3. pyramid rows pass at columns 4X+2, two per thread; zero unless RP <= c < W-RP
+    // H4: four outputs per item (36 values read for 4 outputs instead of 28 for
+    // 2), TH*TW/16 items on the upper half of the threads, which take one
+    // gradient row group fewer in D2 than the lower half
+    if (H4 && do_hs && comp && tid >= kBlock - TH * (TW / 16) && (KLT_L0T_XST & 2)) {
+      const int i = tid - (kBlock - TH * (TW / 16));
+      const int r = i / (TW / 16), q = i - r * (TW / 16);
+      const float *row = im + (r + RG) * PI + 16 * q;  // idx 16q <-> global C0+16q-8
+      float v[36];
+  #pragma unroll
+      for (int k = 0; k < 9; ++k) *reinterpret_cast<f4 *>(v + 4 * k) = ld4(row + 4 * k);
+      f2 a01 = f2{v[0], v[4]} * f2{T3.p[0], T3.p[0]};  // terms >= +0
+      f2 a23 = f2{v[8], v[12]} * f2{T3.p[0], T3.p[0]};
+  #pragma unroll
       for (int m = 1; m < 21; ++m) {
-        f2 a = {v[m], v[m + 4]};
-        f2 kk = {T3.p[m], T3.p[m]};
-        acc += a * kk;
+        const f2 kk = {T3.p[m], T3.p[m]};
+        a01 += f2{v[m], v[m + 4]} * kk;
+        a23 += f2{v[m + 8], v[m + 12]} * kk;
       }
       const int y = R0 + r;
-      const int X = C0 / SS + 2 * pq;
+      const int X = C0 / SS + 4 * q;
       if (INT) {
-        *reinterpret_cast<f2 *>(hs + hs_at(y, X, H)) = acc;
+        *reinterpret_cast<f4 *>(hs + hs_at(y, X, H)) = f4{a01.x, a01.y, a23.x, a23.y};
+      } else if (y < H) {
+        const float o[4] = {a01.x, a01.y, a23.x, a23.y};
+  #pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = C0 + 16 * q + 4 * e + 2;
+          if (X + e < hsW) hs[hs_at(y, X + e, H)] = (c >= RP && c < W - RP) ? o[e] : 0.0f;
+        }
+      }
+    }
+    if (!H4 && do_hs && comp) {
+      for (int i = tid; i < TH * (TW / 8); i += kBlock) {
+        if (!(KLT_L0T_XST & 2)) break;
+        const int r = i / (TW / 8), pq = i - r * (TW / 8);
+        const float *row = im + (r + RG) * PI + 8 * pq;  // idx 8p <-> global C0+8p-8
+        float v[28];
+  #pragma unroll
+        for (int k = 0; k < 7; ++k) *reinterpret_cast<f4 *>(v + 4 * k) = ld4(row + 4 * k);
+        f2 acc = f2{v[0], v[4]} * f2{T3.p[0], T3.p[0]};  // terms >= +0
+  #pragma unroll
+        for (int m = 1; m < 21; ++m) {
+          f2 a = {v[m], v[m + 4]};
+          f2 kk = {T3.p[m], T3.p[m]};
+          acc += a * kk;
+        }
+        const int y = R0 + r;
+        const int X = C0 / SS + 2 * pq;
+        if (INT) {
+          *reinterpret_cast<f2 *>(hs + hs_at(y, X, H)) = acc;
+        } else {
+          const int c = C0 + 8 * pq + 2;
+          if (y < H) {
+            if (X < hsW) hs[hs_at(y, X, H)] = (c >= RP && c < W - RP) ? acc.x : 0.0f;
+            if (X + 1 < hsW) hs[hs_at(y, X + 1, H)] = (c + 4 >= RP && c + 4 < W - RP) ? acc.y : 0.0f;
+          }
+        }
+      }
+    }
+  };
+  if (!HSLAST) d3();
+  L0T_MARK(3);
+
+  const auto &T4 = phase_taps(Tin);
+  // E. columns passes of both gradients; zero unless RG <= y < H-RG
+  // E2: 4 rows x 2 columns per thread from 8-byte LDS reads (10 rows read for
+  // 4 outputs: 160 B per item instead of 256 B for 2 rows x 4 columns)
+  for (int i = tid; E2 && comp && i < (TH / 4) * (TW / 2); i += kBlock) {
+    const int b = i / (TW / 2), g = i - b * (TW / 2);
+    f2 vx[10], vy[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      vx[k] = *reinterpret_cast<const f2 *>(tx + (4 * b + k) * PX + 2 * g);
+      vy[k] = *reinterpret_cast<const f2 *>(ty + (4 * b + k) * PX + 2 * g);
+    }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      f2 ax = {0.0f, 0.0f}, ay = {0.0f, 0.0f};
+#pragma unroll
+      for (int m = 0; m < 7; ++m) {
+        ax += vx[rr + m] * f2{T4.g[m], T4.g[m]};
+        ay += vy[rr + m] * f2{T4.d[m], T4.d[m]};
+      }
+      const int y = R0 + 4 * b + rr, x = C0 + 2 * g;
+      if (!(KLT_L0T_XST & 4)) {
+      } else if (INT) {
+        st2_out(gx0 + (unsigned)(y * W + x), ax);
+        st2_out(gy0 + (unsigned)(y * W + x), ay);
       } else {
-        const int c = C0 + 8 * pq + 2;
-        if (y < H) {
-          if (X < hsW) hs[hs_at(y, X, H)] = (c >= RP && c < W - RP) ? acc.x : 0.0f;
-          if (X + 1 < hsW) hs[hs_at(y, X + 1, H)] = (c + 4 >= RP && c + 4 < W - RP) ? acc.y : 0.0f;
+        if (y >= H || x >= W) continue;
+        if (!(y >= RG && y < H - RG)) {
+          ax = f2{0.0f, 0.0f};
+          ay = ax;
+        }
+        float *px = gx0 + (unsigned)(y * W + x);
+        float *py = gy0 + (unsigned)(y * W + x);
+        if (vec_out && x + 1 < W) {
+          *reinterpret_cast<f2 *>(px) = ax;
+          *reinterpret_cast<f2 *>(py) = ay;
+        } else {
+          px[0] = ax.x;
+          py[0] = ay.x;
+          if (x + 1 < W) {
+            px[1] = ax.y;
+            py[1] = ay.y;
+          }
         }
       }
     }
   }
-  L0T_MARK(3);
-
-  const auto &T4 = phase_taps(Tin);
-  // E. columns passes of both gradients, 2 rows x 4 columns per thread; zero unless RG <= y < H-RG
-  for (int i = tid; comp && i < (TH / 2) * (TW / 4); i += kBlock) {
+  for (int i = tid; !E2 && comp && i < (TH / 2) * (TW / 4); i += kBlock) {
     const int b = i / (TW / 4), g = i - b * (TW / 4);
     f4 vx[8], vy[8];
 #pragma unroll
@@ -516,6 +619,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
       }
     }
   }
+  if (HSLAST) d3();
 #ifdef KLT_TRACK_PROF
   if (tid == 0 && (blockIdx.x & 63) == 0) {
     atomicAdd(&g_l0s_prof[(STAGED ? 32 : 0) + 28], (unsigned long long)(clock64() - tprev));
