@@ -558,25 +558,25 @@ static void sample_windows(const orc_level *A, const orc_level *B, float x1, flo
                            float x2, float y2, int ww, int wh, int li, float *diff,
                            float *sgx, float *sgy)
 {
-  const int hw = ww / 2, hh = wh / 2, W = A->w;
+  const int hw = ww / 2, hh = wh / 2, WA = A->w, WB = B->w;
   int i, j, q;
   if (!li) {
     q = 0;
     for (j = -hh; j <= hh; j++)
       for (i = -hw; i <= hw; i++, q++) {
-        float a = bilerp(x1 + i, y1 + j, A->img, W);
-        float b = bilerp(x2 + i, y2 + j, B->img, W);
+        float a = bilerp(x1 + i, y1 + j, A->img, WA);
+        float b = bilerp(x2 + i, y2 + j, B->img, WB);
         diff[q] = a - b;
       }
     if (sgx) {
       q = 0;
       for (j = -hh; j <= hh; j++)
         for (i = -hw; i <= hw; i++, q++) {
-          float a = bilerp(x1 + i, y1 + j, A->gx, W);
-          float b = bilerp(x2 + i, y2 + j, B->gx, W);
+          float a = bilerp(x1 + i, y1 + j, A->gx, WA);
+          float b = bilerp(x2 + i, y2 + j, B->gx, WB);
           sgx[q] = a + b;
-          a = bilerp(x1 + i, y1 + j, A->gy, W);
-          b = bilerp(x2 + i, y2 + j, B->gy, W);
+          a = bilerp(x1 + i, y1 + j, A->gy, WA);
+          b = bilerp(x2 + i, y2 + j, B->gy, WB);
           sgy[q] = a + b;
         }
     }
@@ -587,8 +587,8 @@ static void sample_windows(const orc_level *A, const orc_level *B, float x1, flo
     float s1 = 0, s2 = 0, q1 = 0, q2 = 0, m1, m2, alpha, beta;
     for (j = -hh; j <= hh; j++)
       for (i = -hw; i <= hw; i++) {
-        float a = bilerp(x1 + i, y1 + j, A->img, W);
-        float b = bilerp(x2 + i, y2 + j, B->img, W);
+        float a = bilerp(x1 + i, y1 + j, A->img, WA);
+        float b = bilerp(x2 + i, y2 + j, B->img, WB);
         s1 += a;
         s2 += b;
         q1 += a * a;
@@ -603,8 +603,8 @@ static void sample_windows(const orc_level *A, const orc_level *B, float x1, flo
     q = 0;
     for (j = -hh; j <= hh; j++)
       for (i = -hw; i <= hw; i++, q++) {
-        float a = bilerp(x1 + i, y1 + j, A->img, W);
-        float b = bilerp(x2 + i, y2 + j, B->img, W);
+        float a = bilerp(x1 + i, y1 + j, A->img, WA);
+        float b = bilerp(x2 + i, y2 + j, B->img, WB);
         diff[q] = a - b * alpha - beta;
       }
   }
@@ -613,8 +613,8 @@ static void sample_windows(const orc_level *A, const orc_level *B, float x1, flo
     float s1 = 0, s2 = 0, m1, m2, alpha;
     for (j = -hh; j <= hh; j++)
       for (i = -hw; i <= hw; i++) {
-        float a = bilerp(x1 + i, y1 + j, A->img, W);
-        float b = bilerp(x2 + i, y2 + j, B->img, W);
+        float a = bilerp(x1 + i, y1 + j, A->img, WA);
+        float b = bilerp(x2 + i, y2 + j, B->img, WB);
         s1 += a;
         s2 += b;
       }
@@ -624,11 +624,11 @@ static void sample_windows(const orc_level *A, const orc_level *B, float x1, flo
     q = 0;
     for (j = -hh; j <= hh; j++)
       for (i = -hw; i <= hw; i++, q++) {
-        float a = bilerp(x1 + i, y1 + j, A->gx, W);
-        float b = bilerp(x2 + i, y2 + j, B->gx, W);
+        float a = bilerp(x1 + i, y1 + j, A->gx, WA);
+        float b = bilerp(x2 + i, y2 + j, B->gx, WB);
         sgx[q] = a + b * alpha;
-        a = bilerp(x1 + i, y1 + j, A->gy, W);
-        b = bilerp(x2 + i, y2 + j, B->gy, W);
+        a = bilerp(x1 + i, y1 + j, A->gy, WA);
+        b = bilerp(x2 + i, y2 + j, B->gy, WB);
         sgy[q] = a + b * alpha;
       }
   }
@@ -716,9 +716,298 @@ static int track_one(float x1, float y1, float *x2, float *y2, const orc_level *
   return TRACKED;
 }
 
-/* KLTTrackFeatures (trackFeatures.c:1234-1529), affine check disabled */
-ORC_EXPORT void orc_track(orc_tracker *t, const uint8_t *img1, const uint8_t *img2,
-                          int W, int H, int nfeat, float *fx, float *fy, int *fval)
+/* ------------------------------------------------------------------ */
+/* affine consistency check (trackFeatures.c:503-1225, :1438-1497)     */
+/* ------------------------------------------------------------------ */
+typedef struct {
+  int mode;                      /* tc->affineConsistencyCheck: 0, 1, 2 */
+  int ww, wh;                    /* affine_window_width / _height */
+  int max_iterations;            /* affine_max_iterations */
+  float max_residue;             /* affine_max_residue */
+  float min_displacement;        /* affine_min_displacement (corner motion) */
+  float max_displacement_differ; /* affine_max_displacement_differ */
+} orc_affine;
+
+/* _am_gauss_jordan_elimination (:546-605) for one right-hand side: full
+ * pivoting, matrix rows 6 floats apart.  Returns SMALL_DET on a singular or
+ * repeated pivot, leaving the partial elimination in place exactly as the
+ * reference does (its caller still reads the right-hand side).  The final
+ * column unscrambling of the matrix is omitted: only the solution is read. */
+static int gj_one_rhs(float *M, int n, float *rhs)
+{
+  int used[6] = {0, 0, 0, 0, 0, 0};
+  int prow = 0, pcol = 0, step, r, c, l;
+  for (step = 0; step < n; step++) {
+    float best = 0.0f, inv;
+    for (r = 0; r < n; r++) {
+      if (used[r] == 1) continue;
+      for (c = 0; c < n; c++) {
+        if (used[c] == 0) {
+          if (fabs(M[r * 6 + c]) >= best) {
+            best = (float)fabs(M[r * 6 + c]);
+            prow = r;
+            pcol = c;
+          }
+        } else if (used[c] > 1) {
+          return SMALL_DET;
+        }
+      }
+    }
+    used[pcol]++;
+    if (prow != pcol) {
+      for (l = 0; l < n; l++) {
+        float t = M[prow * 6 + l];
+        M[prow * 6 + l] = M[pcol * 6 + l];
+        M[pcol * 6 + l] = t;
+      }
+      {
+        float t = rhs[prow];
+        rhs[prow] = rhs[pcol];
+        rhs[pcol] = t;
+      }
+    }
+    if (M[pcol * 6 + pcol] == 0.0f) return SMALL_DET;
+    inv = 1.0f / M[pcol * 6 + pcol];
+    M[pcol * 6 + pcol] = 1.0f;
+    for (l = 0; l < n; l++) M[pcol * 6 + l] *= inv;
+    rhs[pcol] *= inv;
+    for (r = 0; r < n; r++) {
+      float f;
+      if (r == pcol) continue;
+      f = M[r * 6 + pcol];
+      M[r * 6 + pcol] = 0.0f;
+      for (l = 0; l < n; l++) M[r * 6 + l] -= M[pcol * 6 + l] * f;
+      rhs[r] -= rhs[pcol] * f;
+    }
+  }
+  return TRACKED;
+}
+
+/* window samples of the affine branch: img1 (the stored window) at x1+i,
+ * img2 and its gradients at x2 + A*(i, j) -- _am_computeIntensityDifferenceAffine
+ * (:700-722) and _am_getGradientWinAffine (:610-630); pixel q = row-major */
+static void affine_samples(const orc_level *Wn, const orc_level *B, float x1, float y1, float x2,
+                           float y2, const float *A, int ww, int wh, float *diff, float *gx,
+                           float *gy)
+{
+  const int hw = ww / 2, hh = wh / 2;
+  int i, j, q = 0;
+  for (j = -hh; j <= hh; j++)
+    for (i = -hw; i <= hw; i++, q++) {
+      const float mi = A[0] * i + A[2] * j, mj = A[1] * i + A[3] * j;
+      const float g1 = bilerp(x1 + i, y1 + j, Wn->img, Wn->w);
+      diff[q] = g1 - bilerp(x2 + mi, y2 + mj, B->img, B->w);
+      if (gx) {
+        gx[q] = bilerp(x2 + mi, y2 + mj, B->gx, B->w);
+        gy[q] = bilerp(x2 + mi, y2 + mj, B->gy, B->w);
+      }
+    }
+}
+
+/* the four corners of the mapped window, (:1019-1026): ul, ll, ur, lr */
+static void affine_corners(const float *A, int hw, int hh, float x2, float y2, float *cx, float *cy)
+{
+  const int si[4] = {-hw, -hw, hw, hw}, sj[4] = {hh, -hh, hh, -hh};
+  int k;
+  for (k = 0; k < 4; k++) {
+    cx[k] = A[0] * si[k] + A[2] * sj[k] + x2;
+    cy[k] = A[1] * si[k] + A[3] * sj[k] + y2;
+  }
+}
+
+/* _am_trackFeatureAffine (:952-1225).  A = {Axx, Ayx, Axy, Ayy}, updated in
+ * place.  Returns TRACKED, SMALL_DET, OOB or LARGE_RESIDUE (no
+ * MAX_ITERATIONS: the reference returns the last solve's status). */
+static int affine_track(float x1, float y1, float *x2, float *y2, const orc_level *Wn,
+                        const orc_level *B, const orc_params *P, const orc_affine *Q, float *A)
+{
+  const int ww = Q->ww, wh = Q->wh, hw = ww / 2, hh = wh / 2, npx = ww * wh;
+  const float eps1 = 1.001f, th = P->min_displacement, th_aff = Q->min_displacement;
+  const float x2_0 = *x2, y2_0 = *y2;
+  float *diff = (float *)malloc(sizeof(float) * 3 * npx), *gx = diff + npx, *gy = gx + npx;
+  /* dx, dy: the reference leaves them uninitialised and adds them to x2 even
+   * when the first solve fails (SMALL_DET); 0 here (parity unpinned there) */
+  float dx = 0.0f, dy = 0.0f;
+  int it = 0, status = TRACKED, conv = 0, q, k;
+
+  do {
+    if (Q->mode == 0) {
+      /* translation branch (:1010-1052) */
+      float gxx = 0, gxy = 0, gyy = 0, ex = 0, ey = 0, det;
+      if (window_out(x1, y1, hw, hh, Wn->w, Wn->h) || window_out(*x2, *y2, hw, hh, B->w, B->h)) {
+        status = OOB;
+        break;
+      }
+      sample_windows(Wn, B, x1, y1, *x2, *y2, ww, wh, P->lighting_insensitive, diff, gx, gy);
+      for (q = 0; q < npx; q++) {
+        gxx += gx[q] * gx[q];
+        gxy += gx[q] * gy[q];
+        gyy += gy[q] * gy[q];
+      }
+      for (q = 0; q < npx; q++) {
+        ex += diff[q] * gx[q];
+        ey += diff[q] * gy[q];
+      }
+      ex *= P->step_factor;
+      ey *= P->step_factor;
+      det = gxx * gyy - gxy * gxy;
+      if (det < P->min_determinant) {
+        status = SMALL_DET;
+      } else {
+        dx = (gyy * ex - gxy * ey) / det;
+        dy = (gxx * ey - gxy * ex) / det;
+        status = TRACKED;
+      }
+      conv = fabs(dx) < th && fabs(dy) < th;
+      *x2 += dx;
+      *y2 += dy;
+    } else {
+      /* affine branch (:1054-1160) */
+      float cx[4], cy[4], cx1[4], cy1[4], T[36], e[6];
+      int bad = x1 - hw < 0.0f || Wn->w - (x1 + hw) < eps1 || y1 - hh < 0.0f ||
+                Wn->h - (y1 + hh) < eps1;
+      affine_corners(A, hw, hh, *x2, *y2, cx, cy);
+      for (k = 0; k < 4; k++)
+        bad = bad || cx[k] < 0.0f || B->w - cx[k] < eps1 || cy[k] < 0.0f || B->h - cy[k] < eps1;
+      if (bad) {
+        status = OOB;
+        break;
+      }
+      affine_samples(Wn, B, x1, y1, *x2, *y2, A, ww, wh, diff, gx, gy);
+      memset(T, 0, sizeof(T));
+      memset(e, 0, sizeof(e));
+      q = 0;
+      if (Q->mode == 1) {
+        /* _am_compute4by1ErrorVector (:900-940), _am_compute4by4GradientMatrix (:846-895) */
+        int i, j;
+        for (j = -hh; j <= hh; j++)
+          for (i = -hw; i <= hw; i++, q++) {
+            const float fx = (float)i, fy = (float)j, g = gx[q], h = gy[q];
+            const float dgx = diff[q] * g, dgy = diff[q] * h;
+            const float u = fx * g + fy * h, v = fx * h - fy * g;
+            e[0] += dgx * i + dgy * j;
+            e[1] += dgy * i - dgx * j;
+            e[2] += dgx;
+            e[3] += dgy;
+            T[0] += u * u;
+            T[1] += u * v;
+            T[2] += u * g;
+            T[3] += u * h;
+            T[7] += v * v;
+            T[8] += v * g;
+            T[9] += v * h;
+            T[14] += g * g;
+            T[15] += g * h;
+            T[21] += h * h;
+          }
+      } else {
+        /* _am_compute6by1ErrorVector (:806-841), _am_compute6by6GradientMatrix (:730-801) */
+        int i, j;
+        for (j = -hh; j <= hh; j++)
+          for (i = -hw; i <= hw; i++, q++) {
+            const float fx = (float)i, fy = (float)j, g = gx[q], h = gy[q];
+            const float gg = g * g, gh = g * h, hh2 = h * h;
+            const float xx = fx * fx, xy = fx * fy, yy = fy * fy;
+            const float dgx = diff[q] * g, dgy = diff[q] * h;
+            e[0] += dgx * i;
+            e[1] += dgy * i;
+            e[2] += dgx * j;
+            e[3] += dgy * j;
+            e[4] += dgx;
+            e[5] += dgy;
+            T[0] += xx * gg;
+            T[1] += xx * gh;
+            T[2] += xy * gg;
+            T[3] += xy * gh;
+            T[4] += fx * gg;
+            T[5] += fx * gh;
+            T[7] += xx * hh2;
+            T[8] += xy * gh;
+            T[9] += xy * hh2;
+            T[10] += fx * gh;
+            T[11] += fx * hh2;
+            T[14] += yy * gg;
+            T[15] += yy * gh;
+            T[16] += fy * gg;
+            T[17] += fy * gh;
+            T[21] += yy * hh2;
+            T[22] += fy * gh;
+            T[23] += fy * hh2;
+            T[28] += gg;
+            T[29] += gh;
+            T[35] += hh2;
+          }
+      }
+      {
+        const int n = Q->mode == 1 ? 4 : 6;
+        int r, c;
+        for (r = 0; r < n; r++) e[r] = (float)(e[r] * 0.5);
+        for (r = 1; r < n; r++)
+          for (c = 0; c < r; c++) T[r * 6 + c] = T[c * 6 + r];
+        status = gj_one_rhs(T, n, e);
+        if (n == 4) {
+          A[0] += e[0];
+          A[1] += e[1];
+          A[3] = A[0];
+          A[2] = -A[1];
+          dx = e[2];
+          dy = e[3];
+        } else {
+          A[0] += e[0];
+          A[1] += e[1];
+          A[2] += e[2];
+          A[3] += e[3];
+          dx = e[4];
+          dy = e[5];
+        }
+      }
+      *x2 += dx;
+      *y2 += dy;
+      affine_corners(A, hw, hh, *x2, *y2, cx1, cy1);
+      conv = fabs(dx) < th && fabs(dy) < th;
+      for (k = 0; k < 4; k++) {
+        cx[k] -= cx1[k];
+        cy[k] -= cy1[k];
+        conv = conv && fabs(cx[k]) < th_aff && fabs(cy[k]) < th_aff;
+      }
+    }
+    if (status == SMALL_DET) break;
+    it++;
+  } while (!conv && it < Q->max_iterations);
+
+  if (window_out(*x2, *y2, hw, hh, B->w, B->h)) status = OOB;
+  if ((*x2 - x2_0) > Q->max_displacement_differ || (*y2 - y2_0) > Q->max_displacement_differ)
+    status = OOB;
+  if (status == TRACKED) {
+    float s = 0.0f;
+    if (Q->mode == 0)
+      sample_windows(Wn, B, x1, y1, *x2, *y2, ww, wh, 0, diff, NULL, NULL);
+    else
+      affine_samples(Wn, B, x1, y1, *x2, *y2, A, ww, wh, diff, NULL, NULL);
+    for (q = 0; q < npx; q++) s += (float)fabs(diff[q]);
+    if (s / (ww * wh) > Q->max_residue) status = LARGE_RESIDUE;
+  }
+  free(diff);
+  return status;
+}
+
+/* _am_getSubFloatImage (:665-695): the (2h+1)x(2w+1) integer-pixel window of
+ * a level-0 plane around ((int)x, (int)y), rows top to bottom */
+static void save_window(const float *plane, int W, float x, float y, int sw, int sh, float *out)
+{
+  const int x0 = (int)x, y0 = (int)y, hw = sw / 2, hh = sh / 2;
+  int i, j;
+  for (j = -hh; j <= hh; j++)
+    for (i = -hw; i <= hw; i++) *out++ = plane[(size_t)(j + y0) * W + (i + x0)];
+}
+
+/* KLTTrackFeatures (trackFeatures.c:1234-1529).  Q == NULL or Q->mode < 0:
+ * no affine consistency check.  Otherwise per feature k: aff[6k..6k+5] =
+ * aff_x, aff_y, Axx, Ayx, Axy, Ayy; has[k] = a stored window exists; win +
+ * k*3*S = its img, gradx, grady ((ww+2) x (wh+2) each, S floats). */
+static void track_impl(orc_tracker *t, const uint8_t *img1, const uint8_t *img2, int W, int H,
+                       int nfeat, float *fx, float *fy, int *fval, const orc_affine *Q, float *aff,
+                       float *win, int *has)
 {
   orc_params *P = &t->P;
   orc_pyr *p1, *p2;
@@ -776,7 +1065,36 @@ ORC_EXPORT void orc_track(orc_tracker *t, const uint8_t *img1, const uint8_t *im
       fx[k] = xo;
       fy[k] = yo;
       fval[k] = TRACKED;
+      if (Q && Q->mode >= 0) {
+        /* (:1438-1497): the first successful track stores the feature's window
+         * of image 1 (level 0, around the pre-track position); later ones
+         * re-track that window into image 2 from the new position */
+        const int sw = Q->ww + 2, sh = Q->wh + 2, S = sw * sh;
+        float *w = win + (size_t)k * 3 * S, *a = aff + 6 * k;
+        if (!has[k]) {
+          save_window(p1->img[0], W, xl, yl, sw, sh, w);
+          save_window(p1->gx[0], W, xl, yl, sw, sh, w + S);
+          save_window(p1->gy[0], W, xl, yl, sw, sh, w + 2 * S);
+          a[0] = xl - (int)xl + sw / 2;
+          a[1] = yl - (int)yl + sh / 2;
+          has[k] = 1;
+        } else {
+          orc_level Wn = {w, w + S, w + 2 * S, sw, sh};
+          orc_level B = {p2->img[0], p2->gx[0], p2->gy[0], p2->w[0], p2->h[0]};
+          float x2 = xo, y2 = yo;
+          const int v = affine_track(a[0], a[1], &x2, &y2, &Wn, &B, P, Q, a + 2);
+          fval[k] = v;
+          if (v != TRACKED) {
+            fx[k] = -1.0f;
+            fy[k] = -1.0f;
+            a[0] = -1.0f;
+            a[1] = -1.0f;
+            has[k] = 0;
+          }
+        }
+      }
     }
+    if (Q && Q->mode >= 0 && fval[k] != TRACKED) has[k] = 0; /* windows freed (:1385-1436) */
   }
 
   /* sequential swap (:1503-1511); pyramid1 is always released (:1517-1519) */
@@ -785,6 +1103,29 @@ ORC_EXPORT void orc_track(orc_tracker *t, const uint8_t *img1, const uint8_t *im
   else
     pyr_free(p2);
   pyr_free(p1);
+}
+
+ORC_EXPORT void orc_track(orc_tracker *t, const uint8_t *img1, const uint8_t *img2,
+                          int W, int H, int nfeat, float *fx, float *fy, int *fval)
+{
+  track_impl(t, img1, img2, W, H, nfeat, fx, fy, fval, NULL, NULL, NULL, NULL);
+}
+
+/* orc_track with the affine consistency check: q = {mode, ww, wh, max_it} and
+ * f = {max_residue, min_displacement, max_displacement_differ} (klt.h:71-83) */
+ORC_EXPORT void orc_track_affine(orc_tracker *t, const uint8_t *img1, const uint8_t *img2, int W,
+                                 int H, int nfeat, float *fx, float *fy, int *fval, const int *q,
+                                 const float *f, float *aff, float *win, int *has)
+{
+  orc_affine Q;
+  Q.mode = q[0];
+  Q.ww = q[1];
+  Q.wh = q[2];
+  Q.max_iterations = q[3];
+  Q.max_residue = f[0];
+  Q.min_displacement = f[1];
+  Q.max_displacement_differ = f[2];
+  track_impl(t, img1, img2, W, H, nfeat, fx, fy, fval, &Q, aff, win, has);
 }
 
 /* ------------------------------------------------------------------ */

@@ -12,6 +12,10 @@ Outputs
   select_*.fl                 KLTSelectGoodFeatures + KLTWriteFeatureList (binary)
   seq_*.ft                    example3-style sequences on synthetic frames
   stages.json                 sha256 of every pyramid plane the reference builds
+  affine_*.npz                the affine consistency check (affineConsistencyCheck
+                              0/1/2): per-frame x/y/val and the features' affine
+                              state (aff_x, aff_y, A, stored-window crc32);
+                              warp_frames.npz holds the warped input sequence
   manifest.json               sha256 of every fixture file
 """
 from __future__ import annotations
@@ -30,8 +34,8 @@ import numpy as np
 
 HERE = Path(__file__).resolve().parent
 sys.path.insert(0, str(HERE.parent))
-from kltabi import (GOLDEN, REF_LIB, ROOT, KLTRunner, bind_klt, ft_bytes, load_dataset,  # noqa: E402
-                    u8ptr)
+from kltabi import (GOLDEN, REF_LIB, ROOT, KLTRunner, affine_setup, bind_klt, ft_bytes,  # noqa: E402
+                    load_dataset, run_affine, u8ptr)
 
 REF_BIN = ROOT / "oracle" / "_ref" / "example3_ref"
 
@@ -132,6 +136,52 @@ def write_select(lib, img: np.ndarray, n: int, path: Path) -> None:
     lib.KLTFreeTrackingContext(tc)
 
 
+def warp_frames(seed: int = 2004, w: int = 224, h: int = 176, n: int = 8) -> list[np.ndarray]:
+    """A sequence with rotation and zoom (the motion the affine check models):
+    frame t samples a larger synthetic frame bilinearly (float64) at
+    R(0.6 deg * t) (u, v) / (1 + 0.012 t) + (0.5 t, 0.2 t) around the centre."""
+    base = synth_frames(seed, w + 96, h + 96, 1)[0].astype(np.float64)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
+    u, v = xx - (w - 1) / 2.0, yy - (h - 1) / 2.0
+    out = []
+    for t in range(n):
+        th, s = np.deg2rad(0.6 * t), 1.0 + 0.012 * t
+        sx = (np.cos(th) * u - np.sin(th) * v) / s + (w + 95) / 2.0 + 0.5 * t
+        sy = (np.sin(th) * u + np.cos(th) * v) / s + (h + 95) / 2.0 + 0.2 * t
+        x0, y0 = np.floor(sx).astype(int), np.floor(sy).astype(int)
+        ax, ay = sx - x0, sy - y0
+        val = ((1 - ax) * (1 - ay) * base[y0, x0] + ax * (1 - ay) * base[y0, x0 + 1] +
+               (1 - ax) * ay * base[y0 + 1, x0] + ax * ay * base[y0 + 1, x0 + 1])
+        out.append(np.clip(np.floor(val + 0.5), 0, 255).astype(np.uint8))
+    return out
+
+
+# (fixture name, dataset, features, frames, replace, affine_setup kwargs)
+AFFINE_CASES = [
+    ("affine_m0_100x10", "images_provided", 100, 10, False, dict(mode=0)),
+    ("affine_m1_100x10", "images_provided", 100, 10, False, dict(mode=1)),
+    ("affine_m2_100x10", "images_provided", 100, 10, False, dict(mode=2)),
+    ("affine_m2_replace_150x10", "images_provided", 150, 10, True, dict(mode=2)),
+    ("affine_m2_w11_100x10", "images_provided", 100, 10, False, dict(mode=2, window=11, mdd=3.0, max_res=20.0)),
+    ("affine_m0_li_warp_200x8", "warp", 200, 8, False, dict(mode=0, li=1)),
+    ("affine_m1_warp_200x8", "warp", 200, 8, False, dict(mode=1)),
+    ("affine_m2_warp_200x8", "warp", 200, 8, False, dict(mode=2, max_it=20)),
+]
+
+
+def affine_inputs(name: str):
+    if name == "warp":
+        return list(np.load(GOLDEN / "warp_frames.npz")["frames"])
+    return load_dataset()
+
+
+def write_affine(ref) -> None:
+    np.savez_compressed(GOLDEN / "warp_frames.npz", frames=np.stack(warp_frames()))
+    for name, data, n, nf, replace, kw in AFFINE_CASES:
+        X, Y, V, A, H, K = run_affine(ref, affine_inputs(data), n, nf, affine_setup(**kw), replace=replace)
+        np.savez_compressed(GOLDEN / f"{name}.npz", X=X, Y=Y, V=V, AFF=A, HAS=H, CRC=K)
+
+
 def main() -> None:
     if not REF_LIB.exists() or not REF_BIN.exists():
         sys.exit("oracle/_ref is not built: run `make -C oracle ref` (needs /root/reference)")
@@ -162,7 +212,10 @@ def main() -> None:
     X, Y, V = runner.harness(frames, 150, 10, replace=True)
     (GOLDEN / "seq_config1_replace_150x10.ft").write_bytes(ft_bytes(X, Y, V))
 
-    # 4. per-stage planes
+    # 4. the affine consistency check
+    write_affine(ref)
+
+    # 5. per-stage planes
     st = RefStages()
     stages = {}
     for name, img in (("img0", frames[0]), ("syn640_t0", syn[0]), ("syn333x251_t0", odd[0])):

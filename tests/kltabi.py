@@ -99,6 +99,60 @@ def parse_ft(data: bytes):
     return rec["x"].copy(), rec["y"].copy(), rec["v"].copy()
 
 
+AFF_RESET = (-1.0, -1.0, 1.0, 0.0, 0.0, 1.0)  # selectGoodFeatures.c:185-190
+
+
+def fl_affine(fl):
+    """Per-feature affine state of a klt.h list: (aff[n, 6] = aff_x, aff_y, Axx,
+    Ayx, Axy, Ayy; has[n] = a stored window exists; crc[n] = crc32 of the
+    stored img|gradx|grady window bytes, 0 without a window)."""
+    import zlib
+    n = fl.contents.nFeatures
+    aff = np.zeros((n, 6), np.float32)
+    has = np.zeros(n, np.int32)
+    crc = np.zeros(n, np.uint32)
+    for k in range(n):
+        f = fl.contents.feature[k].contents
+        aff[k] = (f.aff_x, f.aff_y, f.aff_Axx, f.aff_Ayx, f.aff_Axy, f.aff_Ayy)
+        if f.aff_img:
+            has[k] = 1
+            b = b""
+            for im in (f.aff_img, f.aff_img_gradx, f.aff_img_grady):
+                r = im.contents
+                b += np.ctypeslib.as_array(r.data, shape=(r.ncols * r.nrows,)).tobytes()
+            crc[k] = zlib.crc32(b)
+    return aff, has, crc
+
+
+def affine_setup(mode: int, window: int = 15, max_it: int = 10, max_res: float = 10.0,
+                 min_disp: float = 0.02, mdd: float = 1.5, li: int = 0):
+    """tc_setup callback enabling the affine consistency check (klt.h:71-83)."""
+    def setup(tc):
+        tc.affineConsistencyCheck = mode
+        tc.affine_window_width = tc.affine_window_height = window
+        tc.affine_max_iterations = max_it
+        tc.affine_max_residue = max_res
+        tc.affine_min_displacement = min_disp
+        tc.affine_max_displacement_differ = mdd
+        tc.lighting_insensitive = li
+    return setup
+
+
+def run_affine(lib, frames, n_features, n_frames, setup, replace=False, first=None):
+    """KLTRunner.harness with the affine state captured after every track call:
+    returns X, Y, V ([n, frames], example3 column convention) and AFF [frames-1, n, 6],
+    HAS, CRC [frames-1, n] (row i-1: after tracking frame i)."""
+    A, H, K = [], [], []
+
+    def grab(i, fl):
+        a, h, c = fl_affine(fl)
+        A.append(a); H.append(h); K.append(c)
+
+    X, Y, V = KLTRunner(lib).harness(frames, n_features, n_frames, first=first, replace=replace,
+                                     tc_setup=setup, on_frame=grab)
+    return X, Y, V, np.stack(A), np.stack(H), np.stack(K)
+
+
 class KLTRunner:
     """Drives any klt.h library like src/V3/example3.c:35-80 does."""
 
@@ -107,7 +161,7 @@ class KLTRunner:
         lib.KLTSetVerbosity(verbose)
 
     def harness(self, frames, n_features: int, n_frames: int, first: np.ndarray | None = None,
-                sequential: bool = True, replace: bool = False, tc_setup=None):
+                sequential: bool = True, replace: bool = False, tc_setup=None, on_frame=None):
         """frames[i] = image i of the dataset.  V3 semantics (example3.c:44-76):
         first image = frames[1] unless `first` given; loop i=1..n_frames-1 tracks
         (img1 -> frames[i]); the list is stored into table column i-1 and column
@@ -133,6 +187,8 @@ class KLTRunner:
             if replace:
                 lib.KLTReplaceLostFeatures(tc, u8ptr(img2), w, h, fl)
             X[:, i - 1], Y[:, i - 1], V[:, i - 1] = fl_to_arrays(fl)
+            if on_frame:
+                on_frame(i, fl)
             img1 = img2.copy()
         lib.KLTFreeFeatureList(fl)
         lib.KLTFreeTrackingContext(tc)
@@ -180,6 +236,8 @@ def load_oracle() -> C.CDLL:
         "orc_select": (None, [C.c_void_p, U8P, C.c_int, C.c_int, C.c_int, _FP, _FP, _IP]),
         "orc_replace": (None, [C.c_void_p, U8P, C.c_int, C.c_int, C.c_int, _FP, _FP, _IP]),
         "orc_track": (None, [C.c_void_p, U8P, U8P, C.c_int, C.c_int, C.c_int, _FP, _FP, _IP]),
+        "orc_track_affine": (None, [C.c_void_p, U8P, U8P, C.c_int, C.c_int, C.c_int, _FP, _FP, _IP,
+                                    _IP, _FP, _FP, _FP, _IP]),
         "orc_level_dims": (None, [P, C.c_int, C.c_int, _IP, _IP]),
         "orc_frame_pyramid": (None, [P, U8P, C.c_int, C.c_int, _FP, _FP, _FP]),
         "orc_select_images": (None, [P, U8P, C.c_int, C.c_int, _FP, _FP, _FP]),
@@ -257,6 +315,46 @@ class OracleTracker:
             X[:, i - 1], Y[:, i - 1], V[:, i - 1] = x, y, v
             img1 = img2
         return X, Y, V
+
+    def harness_affine(self, frames, n_features, n_frames, tc, replace=False, first=None):
+        """harness() with the affine consistency check; `tc` holds the
+        affine_* fields (a TrackingContextRec after affine_setup).  Same
+        returns as kltabi.run_affine."""
+        import zlib
+        q = np.array([tc.affineConsistencyCheck, tc.affine_window_width, tc.affine_window_height,
+                      tc.affine_max_iterations], np.int32)
+        f = np.array([tc.affine_max_residue, tc.affine_min_displacement,
+                      tc.affine_max_displacement_differ], np.float32)
+        S = (tc.affine_window_width + 2) * (tc.affine_window_height + 2)
+        img1 = np.ascontiguousarray(frames[1] if first is None else first)
+        h, w = img1.shape
+        self.params.sequentialMode = 1
+        self.lib.orc_set_params(self.h, C.byref(self.params))
+        X = np.zeros((n_features, n_frames), np.float32)
+        Y = np.zeros((n_features, n_frames), np.float32)
+        V = np.zeros((n_features, n_frames), np.int32)
+        aff = np.tile(np.array(AFF_RESET, np.float32), (n_features, 1))
+        has = np.zeros(n_features, np.int32)
+        win = np.zeros(n_features * 3 * S, np.float32)
+        x, y, v = self.select(img1, n_features)
+        X[:, 0], Y[:, 0], V[:, 0] = x, y, v
+        A, H, K = [], [], []
+        for i in range(1, n_frames):
+            img2 = np.ascontiguousarray(frames[i])
+            self.lib.orc_track_affine(self.h, u8ptr(img1), u8ptr(img2), w, h, n_features, fp(x), fp(y),
+                                      ip(v), ip(q), fp(f), fp(aff), fp(win), ip(has))
+            if replace:
+                lost = v < 0
+                self.replace(img2, x, y, v)
+                aff[lost] = AFF_RESET
+                has[lost] = 0
+            X[:, i - 1], Y[:, i - 1], V[:, i - 1] = x, y, v
+            A.append(aff.copy())
+            H.append(has.copy())
+            K.append(np.array([zlib.crc32(win[k * 3 * S:(k + 1) * 3 * S].tobytes()) if has[k] else 0
+                               for k in range(n_features)], np.uint32))
+            img1 = img2
+        return X, Y, V, np.stack(A), np.stack(H), np.stack(K)
 
     def frame_pyramid(self, img):
         h, w = img.shape
