@@ -14,6 +14,9 @@
  *                             (selectGoodFeatures.c:375-424, :289-292)
  *   klt_hip_track          <- the per-feature loop of KLTTrackFeatures with
  *                             _trackFeature (trackFeatures.c:1343-1501, :381-486)
+ *   klt_hip_track_affine   <- the same loop with the affine consistency check
+ *                             (_am_trackFeatureAffine and the record stage,
+ *                              trackFeatures.c:952-1225, :1438-1497)
  *
  * All functions return 0 on success and a negative code on failure; the
  * message is available from klt_hip_last_error().  Work is queued on the
@@ -65,6 +68,19 @@ typedef struct {
   int reduction; /* KLT_HIP_EXACT or KLT_HIP_FAST */
 } klt_hip_track_desc;
 
+/* affine consistency check parameters (klt.h:71-83; trackFeatures.c:1472-1489) */
+typedef struct {
+  int mode;                          /* tc->affineConsistencyCheck: 0, 1 or 2 */
+  int window_width, window_height;   /* tc->affine_window_*, odd */
+  int max_iterations;                /* tc->affine_max_iterations */
+  float min_determinant;             /* tc->min_determinant */
+  float min_displacement;            /* tc->min_displacement */
+  float affine_min_displacement;     /* tc->affine_min_displacement */
+  float max_residue;                 /* tc->affine_max_residue */
+  float max_displacement_differ;     /* tc->affine_max_displacement_differ */
+  float step_factor;                 /* tc->step_factor */
+  int lighting_insensitive;          /* tc->lighting_insensitive (mode 0) */
+} klt_hip_affine_desc;
 /* trackability-map parameters */
 typedef struct {
   int window_width, window_height;
@@ -138,6 +154,28 @@ const float *klt_hip_level_ptr(klt_hip_ctx *ctx, int slot, int level, int which)
 int klt_hip_track(klt_hip_ctx *ctx, int slot1, int slot2, const klt_hip_track_desc *desc,
                   float *x, float *y, int *val, int n, int on_device);
 
+/* The affine consistency check keeps each feature's stored window (img,
+   gradx, grady of (ww+2) x (wh+2) floats: _KLTCreateFloatImage of
+   trackFeatures.c:1449-1451) in a device store indexed by feature slot.
+   klt_hip_affine_reserve sizes it for n features of window ww x wh and
+   returns 1 when it was (re)allocated -- every stored window is then gone --,
+   0 when it was kept.  klt_hip_affine_put / _get copy m windows between the
+   store entries idx[0..m-1] and host memory win ([m][3][(ww+2)*(wh+2)],
+   img | gradx | grady).  Synchronous. */
+int klt_hip_affine_reserve(klt_hip_ctx *ctx, int n, int window_width, int window_height);
+int klt_hip_affine_put(klt_hip_ctx *ctx, const int *idx, int m, const float *win);
+int klt_hip_affine_get(klt_hip_ctx *ctx, const int *idx, int m, float *win);
+/* klt_hip_track (host arrays, synchronous) followed by the affine consistency
+   check of KLTTrackFeatures for every feature the translation tracker left
+   TRACKED (trackFeatures.c:1438-1497).  Per feature k:
+     aff[6k..6k+5]  aff_x, aff_y, Axx, Ayx, Axy, Ayy (in/out);
+     state[k] in:   1 the store holds k's window, 0 it holds none;
+              out:  0 none (lost, or never stored), 1 held, 2 stored by this call.
+   A feature the affine stage rejects gets x = y = -1, aff_x = aff_y = -1 and
+   its status in val, as in the reference. */
+int klt_hip_track_affine(klt_hip_ctx *ctx, int slot1, int slot2, const klt_hip_track_desc *tdesc,
+                         const klt_hip_affine_desc *adesc, float *x, float *y, int *val, float *aff,
+                         int *state, int n);
 /* device-resident sequential tracking, one frame per step: for step k, build
    frame t0+k (frames + (t0+k)*stride) on a second stream into the next of
    three slots (one frame ahead of the tracker), then track the device feature

@@ -48,6 +48,11 @@ typedef struct {
   int last_slot; /* slot holding the sequential-mode pyramid, -1 none */
   int last_w, last_h;
   int reduction; /* KLT_HIP_EXACT unless KLT_AMD_REDUCTION=fast */
+  /* affine consistency check: the feature list whose stored windows the
+     device store holds, and per slot the aff_img whose data it holds */
+  KLT_FeatureList aff_list;
+  int aff_n;
+  _KLT_FloatImage *aff_owner;
 } klt_ctx_full;
 
 #define FULL(tc) ((klt_ctx_full *)(tc))
@@ -285,6 +290,7 @@ EXPORT void KLTFreeTrackingContext(KLT_TrackingContext tc)
   if (!tc) return;
   f = FULL(tc);
   if (f->dev) klt_hip_ctx_destroy(f->dev);
+  free(f->aff_owner);
   free(f);
 }
 
@@ -598,6 +604,125 @@ static void drop_affine(KLT_Feature f)
   f->aff_img = f->aff_img_gradx = f->aff_img_grady = NULL;
 }
 
+static _KLT_FloatImage new_window(int sw, int sh, const float *data)
+{
+  _KLT_FloatImage w = _KLTCreateFloatImage(sw, sh);
+  memcpy(w->data, data, sizeof(float) * sw * sh);
+  return w;
+}
+
+/* KLTTrackFeatures' per-feature loop with the affine consistency check
+ * (trackFeatures.c:1343-1497) on the device: klt_hip_track_affine.  The
+ * stored windows live in the device store; the features' aff_img images are
+ * host mirrors of them (the reference's own representation), written when a
+ * window is stored and uploaded again only when a slot holds a window the
+ * store does not (a different list, a reallocated store, or a window the
+ * caller placed there). */
+static void track_affine(KLT_TrackingContext tc, KLT_FeatureList fl, int slot1, int slot2,
+                         const klt_hip_track_desc *td, float *x, float *y, int *v)
+{
+  klt_ctx_full *f = FULL(tc);
+  klt_hip_ctx *dev = f->dev;
+  klt_hip_affine_desc ad;
+  const int n = fl->nFeatures, sw = tc->affine_window_width + 2, sh = tc->affine_window_height + 2;
+  const int S = sw * sh;
+  float *aff = (float *)malloc(sizeof(float) * 6 * (n + 1));
+  int *state = (int *)malloc(sizeof(int) * (n + 1)), *idx = (int *)malloc(sizeof(int) * (n + 1));
+  float *win = NULL;
+  int k, m = 0, fresh;
+
+  if (!aff || !state || !idx) KLTError("(KLTTrackFeatures) Out of memory");
+  fresh = klt_hip_affine_reserve(dev, n, tc->affine_window_width, tc->affine_window_height);
+  if (fresh < 0) dev_check(tc, fresh, "affine window store");
+  if (fresh || f->aff_list != fl || f->aff_n != n) {
+    free(f->aff_owner);
+    f->aff_owner = (_KLT_FloatImage *)calloc(n + 1, sizeof(_KLT_FloatImage));
+    if (!f->aff_owner) KLTError("(KLTTrackFeatures) Out of memory");
+    f->aff_list = fl;
+    f->aff_n = n;
+  }
+  for (k = 0; k < n; k++) {
+    KLT_Feature ft = fl->feature[k];
+    aff[6 * k + 0] = ft->aff_x;
+    aff[6 * k + 1] = ft->aff_y;
+    aff[6 * k + 2] = ft->aff_Axx;
+    aff[6 * k + 3] = ft->aff_Ayx;
+    aff[6 * k + 4] = ft->aff_Axy;
+    aff[6 * k + 5] = ft->aff_Ayy;
+    state[k] = ft->val >= 0 && ft->aff_img != NULL;
+    if (state[k] && f->aff_owner[k] != ft->aff_img) idx[m++] = k;
+  }
+  if (m > 0) { /* windows the store does not hold yet */
+    win = (float *)malloc(sizeof(float) * 3 * S * m);
+    if (!win) KLTError("(KLTTrackFeatures) Out of memory");
+    for (k = 0; k < m; k++) {
+      KLT_Feature ft = fl->feature[idx[k]];
+      _KLT_FloatImage im[3] = {ft->aff_img, ft->aff_img_gradx, ft->aff_img_grady};
+      int p;
+      for (p = 0; p < 3; p++) {
+        if (!im[p] || im[p]->ncols != sw || im[p]->nrows != sh)
+          KLTError("(KLTTrackFeatures) feature %d: stored affine window is not %d by %d", idx[k], sw, sh);
+        memcpy(win + (size_t)(3 * k + p) * S, im[p]->data, sizeof(float) * S);
+      }
+      f->aff_owner[idx[k]] = ft->aff_img;
+    }
+    dev_check(tc, klt_hip_affine_put(dev, idx, m, win), "affine window upload");
+    free(win);
+    win = NULL;
+  }
+
+  ad.mode = tc->affineConsistencyCheck;
+  ad.window_width = tc->affine_window_width;
+  ad.window_height = tc->affine_window_height;
+  ad.max_iterations = tc->affine_max_iterations;
+  ad.min_determinant = tc->min_determinant;
+  ad.min_displacement = tc->min_displacement;
+  ad.affine_min_displacement = tc->affine_min_displacement;
+  ad.max_residue = tc->affine_max_residue;
+  ad.max_displacement_differ = tc->affine_max_displacement_differ;
+  ad.step_factor = tc->step_factor;
+  ad.lighting_insensitive = tc->lighting_insensitive;
+  dev_check(tc, klt_hip_track_affine(dev, slot1, slot2, td, &ad, x, y, v, aff, state, n), "feature tracking");
+
+  m = 0;
+  for (k = 0; k < n; k++) {
+    KLT_Feature ft = fl->feature[k];
+    if (ft->val < 0) continue; /* untouched, like the reference (:1346) */
+    ft->x = x[k];
+    ft->y = y[k];
+    ft->val = v[k];
+    ft->aff_x = aff[6 * k + 0];
+    ft->aff_y = aff[6 * k + 1];
+    ft->aff_Axx = aff[6 * k + 2];
+    ft->aff_Ayx = aff[6 * k + 3];
+    ft->aff_Axy = aff[6 * k + 4];
+    ft->aff_Ayy = aff[6 * k + 5];
+    if (state[k] == 0) {
+      drop_affine(ft); /* lost (:1385-1436, :1482-1492) */
+      f->aff_owner[k] = NULL;
+    } else if (state[k] == 2) {
+      idx[m++] = k;
+    }
+  }
+  if (m > 0) { /* windows stored by this call: mirror them into aff_img (:1447-1454) */
+    win = (float *)malloc(sizeof(float) * 3 * S * m);
+    if (!win) KLTError("(KLTTrackFeatures) Out of memory");
+    dev_check(tc, klt_hip_affine_get(dev, idx, m, win), "affine window download");
+    for (k = 0; k < m; k++) {
+      KLT_Feature ft = fl->feature[idx[k]];
+      drop_affine(ft);
+      ft->aff_img = new_window(sw, sh, win + (size_t)(3 * k) * S);
+      ft->aff_img_gradx = new_window(sw, sh, win + (size_t)(3 * k + 1) * S);
+      ft->aff_img_grady = new_window(sw, sh, win + (size_t)(3 * k + 2) * S);
+      f->aff_owner[idx[k]] = ft->aff_img;
+    }
+    free(win);
+  }
+  free(aff);
+  free(state);
+  free(idx);
+}
+
 /* KLTTrackFeatures (trackFeatures.c:1234-1529) */
 EXPORT void KLTTrackFeatures(KLT_TrackingContext tc, KLT_PixelType *img1, KLT_PixelType *img2,
                              int ncols, int nrows, KLT_FeatureList fl)
@@ -616,10 +741,14 @@ EXPORT void KLTTrackFeatures(KLT_TrackingContext tc, KLT_PixelType *img1, KLT_Pi
     fflush(stderr);
   }
   window_fix(tc, NULL);
-  if (tc->affineConsistencyCheck >= 0)
-    KLTError("(KLTTrackFeatures) affineConsistencyCheck=%d is not supported by libklt_amd "
-             "(only -1, the reference harness setting)",
-             tc->affineConsistencyCheck);
+  if (tc->affineConsistencyCheck > 2)
+    KLTError("(KLTTrackFeatures) affineConsistencyCheck=%d: expected -1, 0, 1 or 2", tc->affineConsistencyCheck);
+  if (tc->affineConsistencyCheck >= 0 &&
+      (tc->affine_window_width % 2 != 1 || tc->affine_window_height % 2 != 1 || tc->affine_window_width < 3 ||
+       tc->affine_window_height < 3))
+    KLTError("(KLTTrackFeatures) affine window %d by %d: must be odd and at least 3 (an even one overruns "
+             "the reference's stored window, trackFeatures.c:680-689)",
+             tc->affine_window_width, tc->affine_window_height);
   dev = device_of(tc);
 
   if (tc->sequentialMode && tc->pyramid_last != NULL && f->last_slot >= 0) {
@@ -667,14 +796,18 @@ EXPORT void KLTTrackFeatures(KLT_TrackingContext tc, KLT_PixelType *img1, KLT_Pi
     y[k] = fl->feature[k]->y;
     v[k] = fl->feature[k]->val;
   }
-  dev_check(tc, klt_hip_track(dev, slot1, slot2, &td, x, y, v, n, 0), "feature tracking");
-  for (k = 0; k < n; k++) {
-    KLT_Feature ft = fl->feature[k];
-    if (ft->val < 0) continue; /* untouched, like the reference (:1346) */
-    ft->x = x[k];
-    ft->y = y[k];
-    ft->val = v[k];
-    if (v[k] != KLT_TRACKED) drop_affine(ft);
+  if (tc->affineConsistencyCheck >= 0) {
+    track_affine(tc, fl, slot1, slot2, &td, x, y, v);
+  } else {
+    dev_check(tc, klt_hip_track(dev, slot1, slot2, &td, x, y, v, n, 0), "feature tracking");
+    for (k = 0; k < n; k++) {
+      KLT_Feature ft = fl->feature[k];
+      if (ft->val < 0) continue; /* untouched, like the reference (:1346) */
+      ft->x = x[k];
+      ft->y = y[k];
+      ft->val = v[k];
+      if (v[k] != KLT_TRACKED) drop_affine(ft);
+    }
   }
   free(x);
   free(y);
@@ -734,9 +867,6 @@ EXPORT void KLTTrackSequence(KLT_TrackingContext tc, KLT_PixelType **frames, int
 
   if (nframes < 2) return;
   window_fix(tc, NULL);
-  if (tc->affineConsistencyCheck >= 0)
-    KLTError("(KLTTrackSequence) affineConsistencyCheck=%d is not supported by libklt_amd",
-             tc->affineConsistencyCheck);
   if (ft && (ft_col < 0 || ft_col + T > ft->nFrames))
     KLTError("(KLTStoreFeatures) Frame number %d is not between 0 and %d", ft_col < 0 ? ft_col : ft_col + T - 1,
              ft->nFrames - 1);
@@ -761,7 +891,8 @@ EXPORT void KLTTrackSequence(KLT_TrackingContext tc, KLT_PixelType **frames, int
   if (!tc->sequentialMode) pyr_desc_in(&st, tc, ncols, nrows, tc->nPyramidLevels, 1, &e1);
   pyr_desc_in(&st, tc, ncols, nrows, tc->nPyramidLevels, 1, &e2);
   steady = taps_state_eq(&st, &after1) && !memcmp(&e2, &d2, sizeof d2) &&
-           (tc->sequentialMode || !memcmp(&e1, &d2, sizeof d2)) && !tc->writeInternalImages;
+           (tc->sequentialMode || !memcmp(&e1, &d2, sizeof d2)) && !tc->writeInternalImages &&
+           tc->affineConsistencyCheck < 0; /* the affine stage runs per KLTTrackFeatures call */
   if (!steady) {
     for (i = 1; i < nframes; i++) {
       KLTTrackFeatures(tc, frames[i - 1], frames[i], ncols, nrows, fl);

@@ -23,6 +23,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -2192,6 +2193,440 @@ __global__ __launch_bounds__(kBlock) void k_synth(unsigned long long seed, int t
   out[(long)blockIdx.y * fstride + (long)y * pitch + x] = klt_synth_pixel(seed, t, x, y);
 }
 
+// ---------------------------------------------------------------------------
+// Affine consistency check (trackFeatures.c:503-1225 and the record stage
+// :1438-1497).  One wave per feature, after the translation tracker of the
+// same frame.  A feature whose first successful track this is stores its
+// (ww+2)x(wh+2) window of image 1 (img, gradx, grady at level 0) in the
+// device store; a feature holding a window is re-tracked from it into image 2
+// by _am_trackFeatureAffine (mode 0 translation, 1 similarity, 2 affine).
+// Lanes sample the window pixels; every sum is formed by one lane in pixel
+// order (the reference's sequential float sums, staged through LDS in chunks
+// of 256 pixels), and the Gauss-Jordan solve runs on lane 0 over an LDS copy
+// of the system -- bit-identical to the CPU path.
+// ---------------------------------------------------------------------------
+namespace aff {
+constexpr int CH = 256;   // pixels per ordered-sum chunk (4 per lane)
+constexpr int NS = 27;    // mode 2: 21 entries of the 6x6 matrix + 6 error terms
+constexpr int LDS = NS * CH + 48;
+}  // namespace aff
+
+struct AffArgs {
+  const float *ai, *agx, *agy;  // image 1, level 0
+  const float *bi, *bgx, *bgy;  // image 2, level 0
+  int aw, ah, bw, bh;
+  const float *xp, *yp;  // positions before this frame's translation track
+  const float *x, *y;    // after it
+  int *v;                // status (in/out)
+  float *xo, *yo;        // feature positions written back (lost: -1)
+  float *aff;            // 6 per feature: aff_x, aff_y, Axx, Ayx, Axy, Ayy
+  int *state;            // in: 1 window stored, 0 none; out: 0, 1, 2 = stored by this call
+  float *store;          // 3*S floats per feature
+  int n, mode, ww, wh, max_it, li;
+  float min_det, th, th_aff, max_res, mdd, step;
+};
+
+__device__ __forceinline__ float aff_bil(const float *P, int w, int h, float x, float y) {
+  const Bil b = bil_at(w, h, x, y);
+  return bil_sample(P, b, (unsigned)w);
+}
+
+// NSUM ordered sums over the window's pixels (row-major, from +0): term(i, j,
+// v) fills v[0..NSUM) for window offset (i, j).  Every lane gets the sums.
+template <int NSUM, class Term>
+__device__ __forceinline__ void aff_sums(float *t, int npx, int ww, int hw, int hh, int lane, Term term,
+                                         float (&out)[NSUM]) {
+  float acc = 0.0f;
+  for (int c0 = 0; c0 < npx; c0 += aff::CH) {
+#pragma unroll
+    for (int k = 0; k < aff::CH / kWave; ++k) {
+      const int q = lane + kWave * k, p = c0 + q;
+      float v[NSUM];
+      if (p < npx) {
+        const int j = p / ww, i = p - j * ww;
+        term(i - hw, j - hh, v);
+      } else {
+#pragma unroll
+        for (int s = 0; s < NSUM; ++s) v[s] = 0.0f;  // whole-chunk pads: acc + +0 == acc
+      }
+#pragma unroll
+      for (int s = 0; s < NSUM; ++s) t[s * aff::CH + q] = v[s];
+    }
+    lds_wave_sync();
+    const int cnt = min(aff::CH, npx - c0), n4 = (cnt + 3) & ~3;
+    if (lane < NSUM) {
+      const float *r = t + lane * aff::CH;
+      for (int q = 0; q < n4; q += 4) {
+        const f4 c = ld4(r + q);
+        acc += c.x;
+        acc += c.y;
+        acc += c.z;
+        acc += c.w;
+      }
+    }
+    lds_wave_sync();
+  }
+#pragma unroll
+  for (int s = 0; s < NSUM; ++s) out[s] = bcast(acc, s);
+}
+
+// _am_gauss_jordan_elimination (trackFeatures.c:546-605) for one right-hand
+// side, full pivoting, rows 6 floats apart; lane 0 only.  A singular or
+// repeated pivot returns SMALL_DET with the partial elimination left in place,
+// as the reference's caller still reads the right-hand side.
+__device__ int aff_gauss_jordan(float *M, int n, float *rhs) {
+  int used[6] = {0, 0, 0, 0, 0, 0};
+  int prow = 0, pcol = 0;
+  for (int step = 0; step < n; ++step) {
+    float best = 0.0f;
+    for (int r = 0; r < n; ++r) {
+      if (used[r] == 1) continue;
+      for (int c = 0; c < n; ++c) {
+        if (used[c] == 0) {
+          if (fabsf(M[r * 6 + c]) >= best) {
+            best = fabsf(M[r * 6 + c]);
+            prow = r;
+            pcol = c;
+          }
+        } else if (used[c] > 1) {
+          return kSmallDet;
+        }
+      }
+    }
+    ++used[pcol];
+    if (prow != pcol) {
+      for (int l = 0; l < n; ++l) {
+        const float t = M[prow * 6 + l];
+        M[prow * 6 + l] = M[pcol * 6 + l];
+        M[pcol * 6 + l] = t;
+      }
+      const float t = rhs[prow];
+      rhs[prow] = rhs[pcol];
+      rhs[pcol] = t;
+    }
+    if (M[pcol * 6 + pcol] == 0.0f) return kSmallDet;
+    const float inv = 1.0f / M[pcol * 6 + pcol];
+    M[pcol * 6 + pcol] = 1.0f;
+    for (int l = 0; l < n; ++l) M[pcol * 6 + l] *= inv;
+    rhs[pcol] *= inv;
+    for (int r = 0; r < n; ++r) {
+      if (r == pcol) continue;
+      const float f = M[r * 6 + pcol];
+      M[r * 6 + pcol] = 0.0f;
+      for (int l = 0; l < n; ++l) M[r * 6 + l] -= M[pcol * 6 + l] * f;
+      rhs[r] -= rhs[pcol] * f;
+    }
+  }
+  return kTracked;
+}
+
+// corners of the mapped window (:1019-1026): ul, ll, ur, lr
+__device__ __forceinline__ void aff_corners(const float (&A)[4], int hw, int hh, float x2, float y2, float (&cx)[4],
+                                            float (&cy)[4]) {
+  const int si[4] = {-hw, -hw, hw, hw}, sj[4] = {hh, -hh, hh, -hh};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    cx[k] = A[0] * (float)si[k] + A[2] * (float)sj[k] + x2;
+    cy[k] = A[1] * (float)si[k] + A[3] * (float)sj[k] + y2;
+  }
+}
+
+__global__ __launch_bounds__(kWave) void k_affine(AffArgs a) {
+  __shared__ __attribute__((aligned(16))) float lds[aff::LDS];
+  const int k = blockIdx.x, lane = threadIdx.x;
+  if (k >= a.n) return;
+  float *T = lds + aff::NS * aff::CH, *rhs = T + 36;
+  int *res = reinterpret_cast<int *>(rhs + 6);
+  const int sw = a.ww + 2, sh = a.wh + 2, S = sw * sh;
+  float *win = a.store + (size_t)k * 3 * S;
+  const int v_in = a.v[k], st = a.state[k];
+  if (v_in != kTracked) {  // lost this frame (windows dropped) or not tracked at all
+    if (lane == 0) a.state[k] = 0;
+    return;
+  }
+  float *af = a.aff + 6 * k;
+  if (st == 0) {
+    // first successful track: _am_getSubFloatImage (:665-695) of image 1 around
+    // the pre-track position; the clamp only guards what the reference asserts
+    const float xp = a.xp[k], yp = a.yp[k];
+    const int x0 = (int)xp, y0 = (int)yp, hw = sw / 2, hh = sh / 2;
+    for (int q = lane; q < S; q += kWave) {
+      const int j = q / sw, i = q - j * sw;
+      const long src = (long)clampi(j - hh + y0, 0, a.ah - 1) * a.aw + clampi(i - hw + x0, 0, a.aw - 1);
+      win[q] = a.ai[src];
+      win[S + q] = a.agx[src];
+      win[2 * S + q] = a.agy[src];
+    }
+    if (lane == 0) {
+      af[0] = xp - (float)x0 + (float)(sw / 2);
+      af[1] = yp - (float)y0 + (float)(sh / 2);
+      a.state[k] = 2;
+    }
+    return;
+  }
+
+  // _am_trackFeatureAffine (:952-1225)
+  const float *wi = win, *wgx = win + S, *wgy = win + 2 * S;
+  const int ww = a.ww, wh = a.wh, hw = ww / 2, hh = wh / 2, npx = ww * wh;
+  const float n = (float)npx, e1 = 1.001f;
+  const float x1 = af[0], y1 = af[1];
+  float A[4] = {af[2], af[3], af[4], af[5]};
+  float x2 = a.x[k], y2 = a.y[k];
+  const float x2_0 = x2, y2_0 = y2;
+  float dx = 0.0f, dy = 0.0f;  // uninitialised in the reference before the first solve
+  int it = 0, status = kTracked;
+  bool conv = false;
+  do {
+    if (a.mode == 0) {
+      // translation branch (:1010-1052), _computeIntensityDifference /
+      // _computeGradientSum and their lighting-insensitive forms
+      if (window_out(x1, y1, hw, hh, sw, sh) || window_out(x2, y2, hw, hh, a.bw, a.bh)) {
+        status = kOOB;
+        break;
+      }
+      float alpha = 1.0f, beta = 0.0f, alpha_g = 1.0f;
+      if (a.li) {
+        float M[4];
+        aff_sums<4>(lds, npx, ww, hw, hh, lane,
+                    [&](int i, int j, float *v) {
+                      const float g1 = aff_bil(wi, sw, sh, x1 + i, y1 + j);
+                      const float g2 = aff_bil(a.bi, a.bw, a.bh, x2 + i, y2 + j);
+                      v[0] = g1;
+                      v[1] = g2;
+                      v[2] = g1 * g1;
+                      v[3] = g2 * g2;
+                    },
+                    M);
+        alpha = (float)sqrt((double)((M[2] / n) / (M[3] / n)));
+        beta = M[0] / n - alpha * (M[1] / n);
+        alpha_g = (float)sqrt((double)((M[0] / n) / (M[1] / n)));
+      }
+      float G[5];
+      aff_sums<5>(lds, npx, ww, hw, hh, lane,
+                  [&](int i, int j, float *v) {
+                    const float g1 = aff_bil(wi, sw, sh, x1 + i, y1 + j);
+                    const float g2 = aff_bil(a.bi, a.bw, a.bh, x2 + i, y2 + j);
+                    const float ax = aff_bil(wgx, sw, sh, x1 + i, y1 + j);
+                    const float bx = aff_bil(a.bgx, a.bw, a.bh, x2 + i, y2 + j);
+                    const float ay = aff_bil(wgy, sw, sh, x1 + i, y1 + j);
+                    const float by = aff_bil(a.bgy, a.bw, a.bh, x2 + i, y2 + j);
+                    float d, gx, gy;
+                    if (a.li) {
+                      d = g1 - g2 * alpha - beta;
+                      gx = ax + bx * alpha_g;
+                      gy = ay + by * alpha_g;
+                    } else {
+                      d = g1 - g2;
+                      gx = ax + bx;
+                      gy = ay + by;
+                    }
+                    v[0] = gx * gx;
+                    v[1] = gx * gy;
+                    v[2] = gy * gy;
+                    v[3] = d * gx;
+                    v[4] = d * gy;
+                  },
+                  G);
+      const float ex = G[3] * a.step, ey = G[4] * a.step;
+      const float det = G[0] * G[2] - G[1] * G[1];
+      if (det < a.min_det) {
+        status = kSmallDet;
+      } else {
+        dx = (G[2] * ex - G[1] * ey) / det;
+        dy = (G[0] * ey - G[1] * ex) / det;
+        status = kTracked;
+      }
+      conv = fabsf(dx) < a.th && fabsf(dy) < a.th;
+      x2 += dx;
+      y2 += dy;
+    } else {
+      // affine branch (:1054-1160)
+      float cx[4], cy[4];
+      aff_corners(A, hw, hh, x2, y2, cx, cy);
+      bool bad = !(isfinite(x1) && isfinite(y1)) || x1 - hw < 0.0f || sw - (x1 + hw) < e1 || y1 - hh < 0.0f ||
+                 sh - (y1 + hh) < e1;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        bad = bad || !(isfinite(cx[c]) && isfinite(cy[c])) || cx[c] < 0.0f || a.bw - cx[c] < e1 || cy[c] < 0.0f ||
+              a.bh - cy[c] < e1;
+      if (bad) {
+        status = kOOB;
+        break;
+      }
+      // _am_computeIntensityDifferenceAffine (:700-722) + _am_getGradientWinAffine (:610-630)
+      auto sample = [&](int i, int j, float &d, float &g, float &h) {
+        const float mi = A[0] * (float)i + A[2] * (float)j, mj = A[1] * (float)i + A[3] * (float)j;
+        const float g1 = aff_bil(wi, sw, sh, x1 + i, y1 + j);
+        d = g1 - aff_bil(a.bi, a.bw, a.bh, x2 + mi, y2 + mj);
+        g = aff_bil(a.bgx, a.bw, a.bh, x2 + mi, y2 + mj);
+        h = aff_bil(a.bgy, a.bw, a.bh, x2 + mi, y2 + mj);
+      };
+      const int nn = a.mode == 1 ? 4 : 6;
+      float sol[6];
+      if (a.mode == 1) {
+        // _am_compute4by1ErrorVector (:900-940), _am_compute4by4GradientMatrix (:846-895)
+        float R[14];
+        aff_sums<14>(lds, npx, ww, hw, hh, lane,
+                     [&](int i, int j, float *v) {
+                       float d, g, h;
+                       sample(i, j, d, g, h);
+                       const float fx = (float)i, fy = (float)j;
+                       const float dgx = d * g, dgy = d * h;
+                       const float u = fx * g + fy * h, w = fx * h - fy * g;
+                       v[0] = dgx * fx + dgy * fy;
+                       v[1] = dgy * fx - dgx * fy;
+                       v[2] = dgx;
+                       v[3] = dgy;
+                       v[4] = u * u;
+                       v[5] = u * w;
+                       v[6] = u * g;
+                       v[7] = u * h;
+                       v[8] = w * w;
+                       v[9] = w * g;
+                       v[10] = w * h;
+                       v[11] = g * g;
+                       v[12] = g * h;
+                       v[13] = h * h;
+                     },
+                     R);
+        if (lane == 0) {
+          const int up[10] = {0, 1, 2, 3, 7, 8, 9, 14, 15, 21};
+          for (int q = 0; q < 10; ++q) T[up[q]] = R[4 + q];
+          for (int q = 0; q < 4; ++q) rhs[q] = (float)((double)R[q] * 0.5);
+        }
+      } else {
+        // _am_compute6by1ErrorVector (:806-841), _am_compute6by6GradientMatrix (:730-801)
+        float R[27];
+        aff_sums<27>(lds, npx, ww, hw, hh, lane,
+                     [&](int i, int j, float *v) {
+                       float d, g, h;
+                       sample(i, j, d, g, h);
+                       const float fx = (float)i, fy = (float)j;
+                       const float gg = g * g, gh = g * h, hh2 = h * h;
+                       const float xx = fx * fx, xy = fx * fy, yy = fy * fy;
+                       const float dgx = d * g, dgy = d * h;
+                       v[0] = dgx * fx;
+                       v[1] = dgy * fx;
+                       v[2] = dgx * fy;
+                       v[3] = dgy * fy;
+                       v[4] = dgx;
+                       v[5] = dgy;
+                       v[6] = xx * gg;    // T00
+                       v[7] = xx * gh;    // T01
+                       v[8] = xy * gg;    // T02
+                       v[9] = xy * gh;    // T03
+                       v[10] = fx * gg;   // T04
+                       v[11] = fx * gh;   // T05
+                       v[12] = xx * hh2;  // T11
+                       v[13] = xy * gh;   // T12
+                       v[14] = xy * hh2;  // T13
+                       v[15] = fx * gh;   // T14
+                       v[16] = fx * hh2;  // T15
+                       v[17] = yy * gg;   // T22
+                       v[18] = yy * gh;   // T23
+                       v[19] = fy * gg;   // T24
+                       v[20] = fy * gh;   // T25
+                       v[21] = yy * hh2;  // T33
+                       v[22] = fy * gh;   // T34
+                       v[23] = fy * hh2;  // T35
+                       v[24] = gg;        // T44
+                       v[25] = gh;        // T45
+                       v[26] = hh2;       // T55
+                     },
+                     R);
+        if (lane == 0) {
+          const int up[21] = {0, 1, 2, 3, 4, 5, 7, 8, 9, 10, 11, 14, 15, 16, 17, 21, 22, 23, 28, 29, 35};
+          for (int q = 0; q < 21; ++q) T[up[q]] = R[6 + q];
+          for (int q = 0; q < 6; ++q) rhs[q] = (float)((double)R[q] * 0.5);
+        }
+      }
+      if (lane == 0) {
+        for (int r = 1; r < nn; ++r)
+          for (int c = 0; c < r; ++c) T[r * 6 + c] = T[c * 6 + r];
+        res[0] = aff_gauss_jordan(T, nn, rhs);
+      }
+      lds_wave_sync();
+      status = res[0];
+#pragma unroll
+      for (int q = 0; q < 6; ++q) sol[q] = q < nn ? rhs[q] : 0.0f;
+      lds_wave_sync();
+      if (nn == 4) {
+        A[0] += sol[0];
+        A[1] += sol[1];
+        A[3] = A[0];
+        A[2] = -A[1];
+        dx = sol[2];
+        dy = sol[3];
+      } else {
+        A[0] += sol[0];
+        A[1] += sol[1];
+        A[2] += sol[2];
+        A[3] += sol[3];
+        dx = sol[4];
+        dy = sol[5];
+      }
+      x2 += dx;
+      y2 += dy;
+      float nx[4], ny[4];
+      aff_corners(A, hw, hh, x2, y2, nx, ny);
+      conv = fabsf(dx) < a.th && fabsf(dy) < a.th;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) conv = conv && fabsf(cx[c] - nx[c]) < a.th_aff && fabsf(cy[c] - ny[c]) < a.th_aff;
+    }
+    if (status == kSmallDet) break;
+    ++it;
+  } while (!conv && it < a.max_it);
+
+  if (window_out(x2, y2, hw, hh, a.bw, a.bh)) status = kOOB;
+  if ((x2 - x2_0) > a.mdd || (y2 - y2_0) > a.mdd) status = kOOB;
+  if (status == kTracked) {
+    // residue (:1199-1211): plain difference in mode 0, mapped otherwise
+    float R[1];
+    aff_sums<1>(lds, npx, ww, hw, hh, lane,
+                [&](int i, int j, float *v) {
+                  float d;
+                  if (a.mode == 0) {
+                    d = aff_bil(wi, sw, sh, x1 + i, y1 + j) - aff_bil(a.bi, a.bw, a.bh, x2 + i, y2 + j);
+                  } else {
+                    const float mi = A[0] * (float)i + A[2] * (float)j, mj = A[1] * (float)i + A[3] * (float)j;
+                    d = aff_bil(wi, sw, sh, x1 + i, y1 + j) - aff_bil(a.bi, a.bw, a.bh, x2 + mi, y2 + mj);
+                  }
+                  v[0] = fabsf(d);
+                },
+                R);
+    if (R[0] / n > a.max_res) status = kLargeResidue;
+  }
+  if (lane == 0) {
+    af[2] = A[0];
+    af[3] = A[1];
+    af[4] = A[2];
+    af[5] = A[3];
+    a.v[k] = status;
+    if (status != kTracked) {
+      a.xo[k] = -1.0f;
+      a.yo[k] = -1.0f;
+      af[0] = -1.0f;
+      af[1] = -1.0f;
+      a.state[k] = 0;
+    } else {
+      a.state[k] = 1;
+    }
+  }
+}
+
+// stored windows between the store and a packed staging buffer:
+// dir 0: staging[m] -> store[idx[m]], dir 1: store[idx[m]] -> staging[m]
+__global__ __launch_bounds__(kBlock) void k_affine_move(int dir, const int *__restrict__ idx, int m, int s3,
+                                                        float *__restrict__ staging, float *__restrict__ store) {
+  const long total = (long)m * s3;
+  for (long e = blockIdx.x * (long)kBlock + threadIdx.x; e < total; e += (long)gridDim.x * kBlock) {
+    const int j = (int)(e / s3), q = (int)(e - (long)j * s3);
+    float *st = store + (long)idx[j] * s3 + q;
+    if (dir == 0) *st = staging[e];
+    else staging[e] = *st;
+  }
+}
+
 __global__ void k_selftest_sqrt(const double *in, double *out, int n) {
   const int i = blockIdx.x * kBlock + threadIdx.x;
   if (i < n) out[i] = sqrt(in[i]);
@@ -2266,6 +2701,14 @@ struct klt_hip_ctx {
   size_t f_cap = 0;
   int *d_eig = nullptr;
   size_t eig_cap = 0;
+  // affine consistency check: stored windows (3*aff_S floats per feature) and per-call arrays
+  float *d_aff_store = nullptr;
+  size_t aff_store_cap = 0;
+  int aff_S = 0;
+  float *d_aff = nullptr, *d_xp = nullptr, *d_yp = nullptr, *d_astage = nullptr;
+  size_t aff_cap = 0, xp_cap = 0, yp_cap = 0, astage_cap = 0;
+  int *d_astate = nullptr, *d_aidx = nullptr;
+  size_t astate_cap = 0, aidx_cap = 0;
   std::string err;
   int force_generic = 0;
   int track_group = 0;  // features per wave for small windows (0: default)
@@ -2803,6 +3246,9 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
   hipFree(c->d_fy);
   hipFree(c->d_fv);
   hipFree(c->d_eig);
+  for (void *p : {(void *)c->d_aff_store, (void *)c->d_aff, (void *)c->d_xp, (void *)c->d_yp, (void *)c->d_astage,
+                  (void *)c->d_astate, (void *)c->d_aidx})
+    hipFree(p);
   for (auto e : c->ev_pool) hipEventDestroy(e);
   for (auto &v : c->ev_used)
     for (auto &p : v) {
@@ -3048,6 +3494,146 @@ KLT_API int klt_hip_track(klt_hip_ctx *c, int s1, int s2, const klt_hip_track_de
     HIPCHK(c, hipMemcpyAsync(val, v_d, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// affine consistency check (include/klt_hip.h)
+// ---------------------------------------------------------------------------
+KLT_API int klt_hip_affine_reserve(klt_hip_ctx *c, int n, int ww, int wh) {
+  if (!c) return fail(c, "affine_reserve: null context");
+  if (n < 0 || ww < 1 || wh < 1) return fail(c, "affine_reserve: bad size");
+  if (use_device(c)) return -1;
+  const int S = (ww + 2) * (wh + 2);
+  const size_t need = (size_t)(n ? n : 1) * 3 * S;
+  if (c->d_aff_store && c->aff_S == S && c->aff_store_cap >= need) return 0;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  hipFree(c->d_aff_store);
+  c->d_aff_store = nullptr;
+  c->aff_store_cap = 0;
+  HIPCHK(c, hipMalloc((void **)&c->d_aff_store, sizeof(float) * need));
+  c->aff_store_cap = need;
+  c->aff_S = S;
+  return 1;
+}
+
+static int affine_move(klt_hip_ctx *c, int dir, const int *idx, int m, float *win) {
+  if (!c || (m > 0 && (!idx || !win))) return fail(c, "affine windows: null argument");
+  if (m <= 0) return 0;
+  if (!c->d_aff_store) return fail(c, "affine windows: no store (klt_hip_affine_reserve)");
+  const int s3 = 3 * c->aff_S;
+  const size_t cap_feat = c->aff_store_cap / s3;
+  for (int j = 0; j < m; ++j)
+    if (idx[j] < 0 || (size_t)idx[j] >= cap_feat) return fail(c, "affine windows: index %d out of range", idx[j]);
+  if (use_device(c)) return -1;
+  if (grow(c, &c->d_astage, &c->astage_cap, (size_t)m * s3) || grow(c, &c->d_aidx, &c->aidx_cap, (size_t)m))
+    return -1;
+  HIPCHK(c, hipMemcpyAsync(c->d_aidx, idx, sizeof(int) * m, hipMemcpyHostToDevice, c->stream));
+  if (dir == 0)
+    HIPCHK(c, hipMemcpyAsync(c->d_astage, win, sizeof(float) * m * s3, hipMemcpyHostToDevice, c->stream));
+  const long total = (long)m * s3;
+  const int blocks = (int)std::min<long>((total + kBlock - 1) / kBlock, 4096);
+  hipLaunchKernelGGL(k_affine_move, dim3(blocks), dim3(kBlock), 0, c->stream, dir, c->d_aidx, m, s3, c->d_astage,
+                     c->d_aff_store);
+  HIPCHK(c, hipGetLastError());
+  if (dir == 1)
+    HIPCHK(c, hipMemcpyAsync(win, c->d_astage, sizeof(float) * m * s3, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+KLT_API int klt_hip_affine_put(klt_hip_ctx *c, const int *idx, int m, const float *win) {
+  return affine_move(c, 0, idx, m, const_cast<float *>(win));
+}
+
+KLT_API int klt_hip_affine_get(klt_hip_ctx *c, const int *idx, int m, float *win) {
+  return affine_move(c, 1, idx, m, win);
+}
+
+KLT_API int klt_hip_track_affine(klt_hip_ctx *c, int s1, int s2, const klt_hip_track_desc *d,
+                                 const klt_hip_affine_desc *ad, float *x, float *y, int *val, float *aff,
+                                 int *state, int n) {
+  if (!c || !d || !ad || (n > 0 && (!x || !y || !val || !aff || !state)))
+    return fail(c, "track_affine: null argument");
+  if (ad->mode < 0 || ad->mode > 2) return fail(c, "track_affine: mode %d (0, 1 or 2)", ad->mode);
+  if (ad->window_width < 3 || ad->window_height < 3 || ad->window_width % 2 == 0 || ad->window_height % 2 == 0)
+    return fail(c, "track_affine: affine window %dx%d must be odd and >= 3", ad->window_width,
+                ad->window_height);
+  if (n <= 0) return 0;
+  if (s1 < 0 || s1 >= KLT_HIP_MAX_SLOTS || s2 < 0 || s2 >= KLT_HIP_MAX_SLOTS)
+    return fail(c, "track_affine: bad slot");
+  const int S = (ad->window_width + 2) * (ad->window_height + 2);
+  if (!c->d_aff_store || c->aff_S != S || c->aff_store_cap < (size_t)n * 3 * S)
+    return fail(c, "track_affine: window store not reserved for %d features (klt_hip_affine_reserve)", n);
+  if (use_device(c)) return -1;
+  if (grow(c, &c->d_aff, &c->aff_cap, (size_t)n * 6) || grow(c, &c->d_astate, &c->astate_cap, (size_t)n) ||
+      grow(c, &c->d_xp, &c->xp_cap, (size_t)n) || grow(c, &c->d_yp, &c->yp_cap, (size_t)n))
+    return -1;
+  // positions before the translation track: the window is stored around them
+  HIPCHK(c, hipMemcpyAsync(c->d_xp, x, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_yp, y, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_aff, aff, sizeof(float) * n * 6, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_astate, state, sizeof(int) * n, hipMemcpyHostToDevice, c->stream));
+  if ((size_t)n > c->f_cap) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(c->d_fx);
+    hipFree(c->d_fy);
+    hipFree(c->d_fv);
+    c->d_fx = c->d_fy = nullptr;
+    c->d_fv = nullptr;
+    c->f_cap = 0;
+    HIPCHK(c, hipMalloc((void **)&c->d_fx, sizeof(float) * n));
+    HIPCHK(c, hipMalloc((void **)&c->d_fy, sizeof(float) * n));
+    HIPCHK(c, hipMalloc((void **)&c->d_fv, sizeof(int) * n));
+    c->f_cap = (size_t)n;
+  }
+  HIPCHK(c, hipMemcpyAsync(c->d_fx, x, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_fy, y, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_fv, val, sizeof(int) * n, hipMemcpyHostToDevice, c->stream));
+  if (klt_hip_track(c, s1, s2, d, c->d_fx, c->d_fy, c->d_fv, n, 1)) return -1;
+  const Slot &A = c->slot[s1], &B = c->slot[s2];
+  AffArgs a;
+  memset(&a, 0, sizeof a);
+  a.ai = A.lv[0].img;
+  a.agx = A.lv[0].gx;
+  a.agy = A.lv[0].gy;
+  a.aw = A.lv[0].w;
+  a.ah = A.lv[0].h;
+  a.bi = B.lv[0].img;
+  a.bgx = B.lv[0].gx;
+  a.bgy = B.lv[0].gy;
+  a.bw = B.lv[0].w;
+  a.bh = B.lv[0].h;
+  a.xp = c->d_xp;
+  a.yp = c->d_yp;
+  a.x = c->d_fx;
+  a.y = c->d_fy;
+  a.v = c->d_fv;
+  a.xo = c->d_fx;
+  a.yo = c->d_fy;
+  a.aff = c->d_aff;
+  a.state = c->d_astate;
+  a.store = c->d_aff_store;
+  a.n = n;
+  a.mode = ad->mode;
+  a.ww = ad->window_width;
+  a.wh = ad->window_height;
+  a.max_it = ad->max_iterations;
+  a.li = ad->lighting_insensitive;
+  a.min_det = ad->min_determinant;
+  a.th = ad->min_displacement;
+  a.th_aff = ad->affine_min_displacement;
+  a.max_res = ad->max_residue;
+  a.mdd = ad->max_displacement_differ;
+  a.step = ad->step_factor;
+  hipLaunchKernelGGL(k_affine, dim3(n), dim3(kWave), 0, c->stream, a);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(x, c->d_fx, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(y, c->d_fy, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(val, c->d_fv, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(aff, c->d_aff, sizeof(float) * n * 6, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(state, c->d_astate, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return 0;
 }
 

@@ -131,6 +131,10 @@ static void mark_found(KLT_Feature f, int x, int y, int val)
   f->x = (KLT_locType)x;
   f->y = (KLT_locType)y;
   f->val = val;
+  /* the reference only NULLs them (a leak); the windows are this library's own mallocs */
+  free(f->aff_img);
+  free(f->aff_img_gradx);
+  free(f->aff_img_grady);
   f->aff_img = NULL;
   f->aff_img_gradx = NULL;
   f->aff_img_grady = NULL;

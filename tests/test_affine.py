@@ -114,3 +114,68 @@ def test_gpu_affine_not_sequential(gpu, oracle, frames):
     want = golden("affine_m1_100x10")
     assert np.array_equal(V[:, :-1], want[2][:, :-1])
     assert np.array_equal(np.stack(A).view(np.uint32), want[3].view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_gpu_track_sequence_affine(gpu, oracle):
+    """KLTTrackSequence with the affine check runs it in every call, like the
+    KLTTrackFeatures + KLTStoreFeatureList loop (oracle), affine state included."""
+    import ctypes as C
+    from kltabi import fl_affine, fl_to_arrays, u8ptr
+    frames = list(np.load(GOLDEN / "warp_frames.npz")["frames"])
+    setup = affine_setup(mode=2)
+    h, w = frames[0].shape
+    tc = gpu.KLTCreateTrackingContext()
+    tc.contents.sequentialMode = 1
+    setup(tc.contents)
+    fl = gpu.KLTCreateFeatureList(200)
+    gpu.KLTSelectGoodFeatures(tc, u8ptr(frames[0]), w, h, fl)
+    keep = [np.ascontiguousarray(f) for f in frames]
+    arr = (C.POINTER(C.c_ubyte) * len(keep))(*[u8ptr(f) for f in keep])
+    gpu.KLTTrackSequence(tc, arr, len(keep), w, h, fl, None, 0)
+    x, y, v = fl_to_arrays(fl)
+    aff, has, crc = fl_affine(fl)
+    gpu.KLTFreeFeatureList(fl)
+    gpu.KLTFreeTrackingContext(tc)
+    t = TrackingContextRec()
+    setup(t)
+    X, Y, V, A, H, K = OracleTracker(oracle).harness_affine(frames, 200, len(frames), t, first=frames[0])
+    assert np.array_equal(v, V[:, -2]) and np.array_equal(x.view(np.int32), X[:, -2].view(np.int32))
+    assert np.array_equal(aff.view(np.int32), A[-1].view(np.int32))
+    assert np.array_equal(has, H[-1]) and np.array_equal(crc, K[-1])
+
+
+@pytest.mark.gpu
+def test_gpu_affine_window_upload(gpu, frames):
+    """A stored window the device does not hold (here: the list's windows
+    handed to a fresh tracking context mid-sequence) is uploaded from aff_img;
+    the run continues exactly as the uninterrupted one."""
+    from kltabi import fl_affine, fl_to_arrays, u8ptr
+    setup = affine_setup(mode=2)
+    h, w = frames[0].shape
+
+    def run(switch_at):
+        tc = gpu.KLTCreateTrackingContext()
+        tc.contents.sequentialMode = 1
+        setup(tc.contents)
+        fl = gpu.KLTCreateFeatureList(100)
+        gpu.KLTSelectGoodFeatures(tc, u8ptr(frames[1]), w, h, fl)
+        img1 = frames[1]
+        for i in range(1, 10):
+            if i == switch_at:  # new context: no sequential pyramid, an empty window store
+                gpu.KLTFreeTrackingContext(tc)
+                tc = gpu.KLTCreateTrackingContext()
+                tc.contents.sequentialMode = 1
+                setup(tc.contents)
+            gpu.KLTTrackFeatures(tc, u8ptr(np.ascontiguousarray(img1)), u8ptr(np.ascontiguousarray(frames[i])),
+                                 w, h, fl)
+            img1 = frames[i]
+        out = fl_to_arrays(fl) + fl_affine(fl)
+        gpu.KLTFreeFeatureList(fl)
+        gpu.KLTFreeTrackingContext(tc)
+        return out
+
+    a, b = run(None), run(5)
+    for p, q in zip(a, b):
+        assert np.array_equal(np.asarray(p).view(np.uint8), np.asarray(q).view(np.uint8))
+    assert a[4].sum() > 20  # windows were held throughout
