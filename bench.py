@@ -56,17 +56,18 @@ def parse():
                    help="frames of the bounded CPU-baseline sample (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--reduction", choices=["exact", "fast"], default="exact")
-    p.add_argument("--chunk", type=int, default=32,
-                   help="frames per batched pyramid/track launch (klt_hip_track_frames); 0 = the per-frame "
-                        "pipelined path (klt_hip_track_sequence)")
-    p.add_argument("--overlap", action="store_true",
-                   help="build chunk c+1's pyramids on a second stream while chunk c is tracked")
+    p.add_argument("--chunk", type=int, default=None,
+                   help="frames per batched pyramid/track launch (klt_hip_track_frames; default 64, sharded 32); "
+                        "0 = the per-frame pipelined path (klt_hip_track_sequence)")
+    p.add_argument("--serial", action="store_true",
+                   help="build and track on one stream; default: chunk c+1's pyramids are built on a second "
+                        "stream while chunk c is tracked (they fill the CUs the tracker's last waves leave idle)")
     p.add_argument("--event-timing", choices=["timed", "replay"], default="replay",
                    help="record per-kernel HIP events inside the timed region or in a replay")
     a = p.parse_args()
     sharded = a.mode == "sharded"
     for k, dflt, shd in (("steps", 489, 490), ("warmup", 10, 64), ("width", 1920, 3840), ("height", 1080, 2160),
-                         ("features", 5000, 20000), ("seed", 1080, 2160)):
+                         ("features", 5000, 20000), ("seed", 1080, 2160), ("chunk", 64, 32)):
         if getattr(a, k) is None:
             setattr(a, k, shd if sharded else dflt)
     return a
@@ -109,7 +110,7 @@ def main() -> None:
     tc.contents.sequentialMode = 1
     lib.klt_amd_set_reduction(tc, EXACT if args.reduction == "exact" else FAST)
     ctx = lib.klt_amd_device_context(tc)
-    check(lib, ctx, lib.klt_hip_set_frames_overlap(ctx, 1 if args.overlap else 0), "overlap")
+    check(lib, ctx, lib.klt_hip_set_frames_overlap(ctx, 0 if args.serial else 1), "overlap")
     use_torch_stream(lib, ctx, dev)  # library kernels and torch ops ordered on one stream
 
     # frames straight into HBM (torch owns the memory; the library only sees pointers)
@@ -179,8 +180,12 @@ def main() -> None:
     live_after = int((v >= 0).sum().item())
 
     tm = Timing()
-    if not timed_events:  # replay the same frames from the same state with events on
+    if not timed_events:
+        # replay the same frames from the same state with events on, on one
+        # stream: each kernel's duration is then its own (the roofline), not
+        # time shared with a kernel overlapping it on the other stream
         x.copy_(xs); y.copy_(ys); v.copy_(vs)
+        check(lib, ctx, lib.klt_hip_set_frames_overlap(ctx, 0), "overlap")
         build0(t_start - 1)
         lib.klt_hip_set_timing(ctx, 1)
         run(t_start, args.steps)
@@ -224,7 +229,9 @@ def main() -> None:
         "data": f"synthetic: include/klt_synth.h value-noise frames, (0.7,0.3) px/frame, seed {args.seed}+rank",
         "config": {"workload": f"{W}x{H}, {NF} features, sequential KLTTrackFeatures pass + KLTStoreFeatureList "
                                f"per frame, {nframes} frames per GPU (BASELINE config 3; config 5 at N>1)",
-                   "chunk": args.chunk, "overlap": bool(args.overlap),
+                   "chunk": args.chunk,
+                   "schedule": "one stream" if args.serial else
+                               "pyramids of chunk c+1 on a second stream while chunk c is tracked",
                    "resolution": f"{W}x{H}", "features": NF, "frames": nframes,
                    "parallelism": "independent sequence per GPU" if world > 1 else "single GPU",
                    "reduction": args.reduction, "pyramid_path": "fused" if fused else "generic"},
@@ -244,7 +251,8 @@ def main() -> None:
             "us_per_frame": pass_us,
             "k_pyr_l0": {"achieved": (l0_bytes / (l0f * 1e-6) / 1e9) if l0f else None,
                          "algorithmic_bytes_per_frame": l0_bytes},
-            "event_timing": "timed region" if timed_events else "replay of the timed region",
+            "event_timing": "timed region" if timed_events else
+                            "replay of the timed region on one stream (each kernel's own duration)",
         }
         pmc = ROOT / "profiles" / "pmc_latest.json"
         if pmc.exists():
@@ -309,7 +317,7 @@ def run_sharded(args, world, rank, dev) -> None:
         if world > 1:
             dist.all_reduce(t)
 
-    seq = ShardedSequence(lib, ctx, pd, td, frames, x, y, v, rank, world, all_reduce, chunk=args.chunk or 32,
+    seq = ShardedSequence(lib, ctx, pd, td, frames, x, y, v, rank, world, all_reduce, chunk=args.chunk,
                           margin=args.margin)
     seq.begin(0)
     seq.run(1, args.warmup)
@@ -343,7 +351,7 @@ def run_sharded(args, world, rank, dev) -> None:
         "data": f"synthetic: include/klt_synth.h value-noise frames, (0.7,0.3) px/frame, seed {args.seed}",
         "config": {"workload": f"{W}x{H}, {NF} features, one sequence, features sharded by row band over "
                                f"{world} GPU(s) (BASELINE config 4)",
-                   "resolution": f"{W}x{H}", "features": NF, "frames": nframes, "chunk": args.chunk or 32,
+                   "resolution": f"{W}x{H}", "features": NF, "frames": nframes, "chunk": args.chunk,
                    "margin_rows": args.margin, "parallelism": f"row-band feature sharding x{world}"},
         "live_features": {"after_warmup": live_before, "at_end": int((v >= 0).sum().item())},
         "chunks_redone_full_frame": seq.redone,
@@ -401,7 +409,7 @@ def cpu_leg(lib, frames, W, H, NF, args, tc, ctx, dev):
     cpu_fps = len(steady) / sum(steady)
 
     # the timed GPU path on the same frames: value-by-value parity
-    gx, gy, gv = gpu_sequence(lib, host, NF, args.chunk)
+    gx, gy, gv = gpu_sequence(lib, host, NF, args.chunk, not args.serial)
     mism = int((gx.view(np.int32) != cx.view(np.int32)).sum() + (gy.view(np.int32) != cy.view(np.int32)).sum()
                + (gv != cv).sum())
     cpu = {"value": cpu_fps, "unit": "frames/s", "cores": 1, "kind": kind,
@@ -414,7 +422,7 @@ def cpu_leg(lib, frames, W, H, NF, args, tc, ctx, dev):
     return cpu, par
 
 
-def gpu_sequence(lib, host, NF, chunk):
+def gpu_sequence(lib, host, NF, chunk, overlap):
     """The timed path (klt_hip_track_frames -- or klt_hip_track_sequence for
     chunk 0 -- frames + features in HBM) on the CPU sample's frames: select on
     frame 0, then track frames 1..S-1."""
@@ -426,6 +434,7 @@ def gpu_sequence(lib, host, NF, chunk):
     ctx = lib.klt_amd_device_context(tc)
     dev = torch.device("cuda", torch.cuda.current_device())
     use_torch_stream(lib, ctx, dev)
+    check(lib, ctx, lib.klt_hip_set_frames_overlap(ctx, 1 if overlap else 0), "overlap")  # the timed schedule
     fl = lib.KLTCreateFeatureList(NF)
     lib.KLTSelectGoodFeatures(tc, host[0].ctypes.data_as(C.POINTER(C.c_ubyte)), W, H, fl)
     x = torch.tensor([fl.contents.feature[k].contents.x for k in range(NF)], dtype=torch.float32, device=dev)

@@ -15,3 +15,4 @@ timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit $?
 cat $OUT/bench.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu > $OUT/prof_bench.json 2> $OUT/prof.err || exit $?
 find $OUT/prof -name "*kernel_stats.csv" -exec cut -c1-60,200- {} \; | cut -c1-200
+python3 tools/kstats_isolated.py $(find $OUT/prof -name "*kernel_trace.csv") 5 > $OUT/kernel_stats_isolated.txt && cat $OUT/kernel_stats_isolated.txt
