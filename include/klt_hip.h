@@ -132,7 +132,9 @@ int klt_hip_set_track_patch(klt_hip_ctx *ctx, int on);
    keep the rows shared by consecutive steps in LDS (k_pyr_l0s, needs width % 8
    == 0 and 4-byte aligned rows; strip_steps 16-row steps per strip, <= 0 keeps
    the current value, default 8); 2: persistent tiles fed by an LDS-DMA loading
-   wave (k_pyr_l0p, 4-byte aligned rows).  Shapes a mode cannot take use tiles.
+   wave (k_pyr_l0p, 4-byte aligned rows); 3: persistent tiles whose gx/gy
+   stores are deferred into the next tile's phases (k_pyr_l0q).  Shapes a mode
+   cannot take use tiles.
    Results do not depend on it (tests/test_gpu_pyramid.py). */
 int klt_hip_set_pyr_l0(klt_hip_ctx *ctx, int mode, int strip_steps);
 /* klt_hip_track_frames scheduling: 1 builds chunk c+1's pyramids on a second

@@ -254,17 +254,69 @@ struct NoHook {
   __device__ void operator()() const {}
 };
 
+// Deferred gradient stores (k_pyr_l0q): an interior tile's gx/gy outputs stay
+// in registers and are stored during the NEXT tile's phases A-D, so that
+// every phase of a workgroup issues some HBM writes instead of one burst at
+// the end of E.  NoDefer stores them in E, as the one-tile kernel does.
+struct NoDefer {
+  static constexpr bool on = false;
+  __device__ void flush(int) {}
+  __device__ void flush_all() {}
+  __device__ void put(int, f2, f2, float *, float *, int) {}
+};
+
+struct Defer {
+  static constexpr bool on = true;
+  f2 vx[4], vy[4];
+  // row 0 of this thread's 4x2 block and the row stride.  Before the first
+  // put they point at a private dummy slot with stride 0: the flushes are
+  // unconditional (a branch around them would make the compiler's wait
+  // counting assume the worst and wait for them with the next loads).  After
+  // an edge tile (stored directly) the next tile re-stores the last interior
+  // block's values to the same place, which only this workgroup writes.
+  float *px, *py;
+  int W = 0;
+  __device__ explicit Defer(float *dummy) : px(dummy), py(dummy) {}
+  // phase k of the next tile stores row k of the block (both planes)
+  __device__ void flush(int k) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (r == k) {
+        st2_out(px + (unsigned)(r * W), vx[r]);
+        st2_out(py + (unsigned)(r * W), vy[r]);
+      }
+  }
+  __device__ void flush_all() {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) flush(k);
+  }
+  __device__ void put(int rr, f2 ax, f2 ay, float *gx, float *gy, int w) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (r == rr) {
+        vx[r] = ax;
+        vy[r] = ay;
+      }
+    if (rr == 0) {
+      px = gx;
+      py = gy;
+      W = w;
+    }
+  }
+};
+
 // STAGED: the u8 tile is already in LDS at `us` ([UH][UQ] dwords, k_pyr_l0p's
 // loading wave put it there), phase A is skipped and `hook` runs on every
 // thread right after the B barrier (when `us` may be refilled); threads with
 // tid >= kBlock (the loading wave) only take part in the barriers.
-template <bool INT, bool STAGED = false, class Hook = NoHook, class Taps = DefTaps>
+template <bool INT, bool STAGED = false, class Hook = NoHook, class Taps = DefTaps, class Def = NoDefer>
 __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8_t *__restrict__ src, int spitch,
                                             int W, int H, const Taps &Tin, int vec_u8,
                                             float *__restrict__ img0, float *__restrict__ gx0,
                                             float *__restrict__ gy0, float *__restrict__ hs, int hsW,
                                             int do_hs, int vec_out, int C0, int R0, int tid,
-                                            const uint32_t *__restrict__ us = nullptr, Hook hook = Hook()) {
+                                            const uint32_t *__restrict__ us = nullptr, Hook hook = Hook(),
+                                            Def *def = nullptr) {
   using namespace l0;
   const bool comp = !STAGED || tid < kBlock;
 #ifdef KLT_TRACK_PROF
@@ -282,8 +334,12 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     uint32_t w[PER];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      const int i = tid + k * kBlock;
-      if (i < NA) {
+      // unconditional: items past NA reload the last dword and land in LDS
+      // past the staged rows (unused), so no load sits under a branch -- the
+      // compiler's wait counting then stays exact, and a later reuse of these
+      // registers does not make it wait for every store in flight
+      const int i = min(tid + k * kBlock, NA - 1);
+      {
         const int r = i / UQ, q = i - r * UQ;
         const int x = C0 - 12 + 4 * q;
         if (INT) {
@@ -300,10 +356,12 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
         }
       }
     }
+    if (Def::on) def->flush(0);  // after this tile's loads: their wait does not cover these stores
+    static_assert(!U8 || PER * kBlock <= REG_A, "phase A spill-over stays inside region A");
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int i = tid + k * kBlock;
-      if (i < NA) {
+      if (U8 || i < NA) {
         const int r = i / UQ, q = i - r * UQ;
         if (U8) {
           reinterpret_cast<uint32_t *>(u)[r * PUB + q] = w[k];
@@ -392,6 +450,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
   }
   L0T_MARK(1);
   hook();
+  if (Def::on) def->flush(1);
 
   const auto &T1 = phase_taps(Tin);
   // C. columns pass -> img0, 4 rows x 4 columns per thread; zero unless RS <= y < H-RS
@@ -414,6 +473,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     }
   }
   L0T_MARK(2);
+  if (Def::on) def->flush(2);
 
   // D1. img0 tile -> HBM
   const int g16 = tid & 15, r16 = tid >> 4;
@@ -531,6 +591,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
   };
   if (!HSLAST) d3();
   L0T_MARK(3);
+  if (Def::on) def->flush(3);
 
   const auto &T4 = phase_taps(Tin);
   // E. columns passes of both gradients; zero unless RG <= y < H-RG
@@ -554,6 +615,8 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
       }
       const int y = R0 + 4 * b + rr, x = C0 + 2 * g;
       if (!(KLT_L0T_XST & 4)) {
+      } else if (INT && Def::on) {
+        def->put(rr, ax, ay, gx0 + (unsigned)(y * W + x), gy0 + (unsigned)(y * W + x), W);
       } else if (INT) {
         st2_out(gx0 + (unsigned)(y * W + x), ax);
         st2_out(gy0 + (unsigned)(y * W + x), ay);
@@ -654,6 +717,51 @@ __global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ s
   else
     pyr_l0_tile<false>(lds, src, spitch, W, H, T, vec_u8, img0, gx0, gy0, hs, hsW, do_hs, vec_out, C0, R0,
                        threadIdx.x);
+}
+
+// ---------------------------------------------------------------------------
+// k_pyr_l0q: k_pyr_l0 as a persistent kernel with deferred gradient stores.
+// Each workgroup walks a run of tiles (XCD x takes the x-th eighth of the
+// tiles of all frames, in order, so its L2 sees one band); an interior tile's
+// gx/gy block stays in registers (Defer) and is stored one row per phase
+// during the next tile.  The HBM writes of a workgroup are then spread over
+// its whole life instead of arriving in one burst at the end of a tile, when
+// the tile kernel's waves would stall on a full write path.  Results are the
+// tile kernel's (same tile function).
+// ---------------------------------------------------------------------------
+static_assert((l0::TH / 4) * (l0::TW / 2) == kBlock, "Defer holds exactly one E2 item per thread");
+__global__ __launch_bounds__(kBlock) void k_pyr_l0q(DefTaps T, const uint8_t *__restrict__ src, int spitch, int W,
+                                                    int H, float *__restrict__ img0, float *__restrict__ gx0,
+                                                    float *__restrict__ gy0, float *__restrict__ hs, int hsW,
+                                                    int do_hs, long fs_src, long fs0, long fs_hs, int ty0,
+                                                    int tiles_x, int tiles_y, int nframes, float *dummy) {
+  using namespace l0;
+  __shared__ __attribute__((aligned(16))) float lds[LDS];
+  (void)T;  // read through the kernarg segment (TapsK)
+  const TapsK tp = (TapsK)__builtin_amdgcn_kernarg_segment_ptr();
+  const int per_frame = tiles_x * tiles_y, total = per_frame * nframes;
+  const int per = (int)gridDim.x / 8, chunk = (total + 7) / 8;
+  const int xcd = (int)(blockIdx.x % 8);
+  const int t_end = min(total, (xcd + 1) * chunk);
+  Defer def(dummy + 2 * (threadIdx.x & 63));
+  for (int t = xcd * chunk + (int)(blockIdx.x / 8); t < t_end; t += per) {
+    const int z = t / per_frame, rem = t - z * per_frame, by = rem / tiles_x, bx = rem - by * tiles_x;
+    const int C0 = bx * TW, R0 = (by + ty0) * TH;
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));  // per-thread indexing recomputed per tile, not kept live
+    const bool interior = (hsW * SS == W) && (hsW % 2 == 0) && C0 >= 12 && C0 + 84 <= W && R0 >= 5 &&
+                          R0 + TH + 7 <= H;
+    DefTapsK &Tk = *fresh_taps(tp);
+    const uint8_t *fsrc = src + z * fs_src;
+    float *fi = img0 + z * fs0, *fx = gx0 + z * fs0, *fy = gy0 + z * fs0, *fh = hs + z * fs_hs;
+    if (interior)
+      pyr_l0_tile<true, false, NoHook, DefTapsK, Defer>(lds, fsrc, spitch, W, H, Tk, 1, fi, fx, fy, fh, hsW, do_hs,
+                                                         1, C0, R0, tid, nullptr, NoHook(), &def);
+    else
+      pyr_l0_tile<false, false, NoHook, DefTapsK, Defer>(lds, fsrc, spitch, W, H, Tk, 1, fi, fx, fy, fh, hsW,
+                                                          do_hs, 1, C0, R0, tid, nullptr, NoHook(), &def);
+  }
+  def.flush_all();
 }
 
 // ---------------------------------------------------------------------------
@@ -2716,6 +2824,8 @@ struct klt_hip_ctx {
   int track_patch = 1;  // one-feature waves gather through a lane patch when the window fits
   int l0_mode = 0;       // level 0: 0 k_pyr_l0 tiles (default), 1 k_pyr_l0s strips, 2 k_pyr_l0p persistent tiles
   int l0p_blocks = 0;    // k_pyr_l0p resident workgroups (CUs x occupancy), filled on first use
+  int l0q_blocks = 0;    // k_pyr_l0q likewise
+  float *d_l0q_dummy = nullptr;  // k_pyr_l0q: target of the deferred stores before a workgroup's first tile
   int l0_strip_steps = 8;  // k_pyr_l0s steps per strip (strip height / TH)
   int serial_frames = 1;  // klt_hip_track_frames: 1 builds and tracks on one stream (default: the
                           // tracker and the pyramid kernels compete for the same CUs; overlap buys ~3 %)
@@ -2943,6 +3053,21 @@ int launch_l0(klt_hip_ctx *c, hipStream_t st, const uint8_t *src, long pitch, lo
   const int ty0 = r0 / l0::TH, ty1 = r1 >= H ? nty : clampi((r1 + l0::TH - 1) / l0::TH, ty0, nty);
   r0 = ty0 * l0::TH;
   r1 = ty1 >= nty ? H : ty1 * l0::TH;
+  if (c->l0_mode == 3 && vec_u8 && vec_out) {
+    if (c->l0q_blocks == 0) {
+      int ncu = 0, per = 0;
+      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess ||
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_pyr_l0q, kBlock, 0) != hipSuccess || ncu * per <= 0)
+        return fail(c, "k_pyr_l0q: cannot size the grid");
+      c->l0q_blocks = ncu * per;
+      HIPCHK(c, hipMalloc((void **)&c->d_l0q_dummy, 128 * sizeof(float)));
+    }
+    const int tiles = tx * (ty1 - ty0) * F;
+    dim3 grid(xcd_grid(tiles < c->l0q_blocks ? tiles : c->l0q_blocks));
+    hipLaunchKernelGGL(k_pyr_l0q, grid, dim3(kBlock), 0, st, T, src, (int)pitch, W, H, img, gx, gy, hs, W1, do_hs,
+                       stride, fs0, fsh, ty0, tx, ty1 - ty0, F, c->d_l0q_dummy);
+    return check_launch(c, "k_pyr_l0q");
+  }
   if (c->l0_mode == 2 && vec_u8 && vec_out) {
     if (c->l0p_blocks == 0) {
       int ncu = 0, per = 0;
@@ -3246,6 +3371,7 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
   hipFree(c->d_fy);
   hipFree(c->d_fv);
   hipFree(c->d_eig);
+  hipFree(c->d_l0q_dummy);
   for (void *p : {(void *)c->d_aff_store, (void *)c->d_aff, (void *)c->d_xp, (void *)c->d_yp, (void *)c->d_astage,
                   (void *)c->d_astate, (void *)c->d_aidx})
     hipFree(p);
@@ -3394,7 +3520,8 @@ KLT_API int klt_hip_set_track_patch(klt_hip_ctx *c, int on) {
 
 KLT_API int klt_hip_set_pyr_l0(klt_hip_ctx *c, int mode, int strip_steps) {
   if (!c) return fail(c, "set_pyr_l0: null context");
-  if (mode < 0 || mode > 2) return fail(c, "set_pyr_l0: mode %d (0 tiles, 1 strips, 2 persistent tiles)", mode);
+  if (mode < 0 || mode > 3)
+    return fail(c, "set_pyr_l0: mode %d (0 tiles, 1 strips, 2 persistent tiles, 3 deferred stores)", mode);
   c->l0_mode = mode;
   if (strip_steps > 0) c->l0_strip_steps = strip_steps;
   return 0;

@@ -394,11 +394,12 @@ def test_patch_gather_edge_positions(gpu, oracle, patch):
 
 
 @pytest.mark.parametrize("opts", [dict(group=1, patch=0), dict(group=2, patch=1), dict(group=4, patch=1),
-                                  dict(order=1, patch=1)])
+                                  dict(order=1, patch=1), dict(l0=2), dict(l0=3), dict(l0=3, chunk=7)])
 def test_tracker_tuning_hooks_do_not_change_results(gpu, oracle, opts):
-    """Features per wave, lane patch and processing order only reorganise work."""
+    """Features per wave, lane patch, processing order and the level-0 kernel
+    (batched over a chunk's frames) only reorganise work."""
     frames = synth(gpu, 5151, 640, 480, 8)
-    X, Y, V = batch_sequence_opts(gpu, frames, 3000, 4, opts)
+    X, Y, V = batch_sequence_opts(gpu, frames, 3000, opts.get("chunk", 4), opts)
     assert_table_equal(X, Y, V, *OracleTracker(oracle).harness(frames, 3000, 8, first=frames[0]))
 
 
@@ -411,6 +412,7 @@ def batch_sequence_opts(gpu, frames, nfeat, chunk, opts):
         assert gpu.klt_hip_set_track_group(ctx, opts.get("group", 0)) == 0
         assert gpu.klt_hip_set_track_patch(ctx, opts.get("patch", 1)) == 0
         assert gpu.klt_hip_set_track_order(ctx, opts.get("order", 0)) == 0
+        assert gpu.klt_hip_set_pyr_l0(ctx, opts.get("l0", 0), 0) == 0
         return ctx
 
     gpu.klt_amd_device_context = hooked

@@ -49,7 +49,7 @@ def main():
     ap.add_argument("--l0prof", action="store_true",
                     help="k_pyr_l0s pass cycles per workgroup (needs KLT_AMD_LIB=.../lib/prof/libklt_amd.so)")
     ap.add_argument("--l0-tiles", action="store_true", help="pyramid level 0 by 64x32 tiles (k_pyr_l0)")
-    ap.add_argument("--l0-mode", type=int, default=-1, help="level-0 kernel: 0 tiles, 1 strips, 2 persistent")
+    ap.add_argument("--l0-mode", type=int, default=-1, help="level-0 kernel: 0 tiles, 1 strips, 2 persistent, 3 deferred stores")
     ap.add_argument("--strip-steps", type=int, default=0, help="k_pyr_l0s steps per strip (0: default)")
     a = ap.parse_args()
 
