@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--cpu-frames", type=int, default=160,
                    help="frames of the bounded CPU-baseline sample (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-4k", action="store_true", help="skip the 4K pyramid-pass roofline line (rank 0, N=1)")
     p.add_argument("--reduction", choices=["exact", "fast"], default="exact")
     p.add_argument("--chunk", type=int, default=None,
                    help="frames per batched pyramid/track launch (klt_hip_track_frames; default 64, sharded 32); "
@@ -270,6 +271,9 @@ def main() -> None:
         result["cpu_baseline"], result["parity"] = cpu_leg(lib, frames, W, H, NF, args, tc, ctx, dev)
 
     lib.KLTFreeTrackingContext(tc)
+    del frames, tab
+    if rank == 0 and world == 1 and not args.no_4k:
+        result["roofline_4k"] = pass_4k(lib, dev)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
@@ -362,6 +366,53 @@ def run_sharded(args, world, rank, dev) -> None:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pass_4k(lib, dev, chunk=64, reps=2):
+    """The north-star figure (BASELINE.json): the convolve+pyramid pass at
+    3840x2160 against the HBM roofline.  Batched pyramid builds of resident
+    synthetic 4K frames (klt_hip_track_frames with no features: its pyramid
+    launches only), `reps` chunks timed with HIP events on the launch stream
+    after one warm-up chunk.  Algorithmic bytes as for the 1080p line:
+    13.75 B/px (u8 in, img/gx/gy out at both levels)."""
+    import torch
+    from kltamd.device import PyrDesc, TrackDesc, Timing, check, use_torch_stream
+    W, H = 3840, 2160
+    tc = lib.KLTCreateTrackingContext()
+    ctx = lib.klt_amd_device_context(tc)
+    use_torch_stream(lib, ctx, dev)
+    n = 1 + chunk * (1 + reps)
+    fr = torch.empty((n, H, W), dtype=torch.uint8, device=dev)
+    check(lib, ctx, lib.klt_hip_synth_frames(ctx, 2160, 0, n, W, H, C.c_void_p(fr.data_ptr()), W, W * H), "synth")
+    pd, td = PyrDesc(), TrackDesc()
+    lib.klt_amd_pyr_desc(tc, W, H, tc.contents.nPyramidLevels, 1, C.byref(pd))
+    lib.klt_amd_track_desc(tc, C.byref(td))
+    base = fr.data_ptr()
+
+    def run(t0, m):
+        check(lib, ctx, lib.klt_hip_track_frames(ctx, C.byref(pd), C.byref(td), C.c_void_p(base + t0 * W * H), W,
+                                                 W * H, m, chunk, None, None, None, 0, None, None, None, 0), "4k")
+
+    check(lib, ctx, lib.klt_hip_frames_begin(ctx, C.byref(pd), C.c_void_p(base), W), "4k begin")
+    run(1, chunk)
+    torch.cuda.synchronize()
+    lib.klt_hip_set_timing(ctx, 1)
+    run(1 + chunk, chunk * reps)
+    tm = Timing()
+    check(lib, ctx, lib.klt_hip_get_timing(ctx, C.byref(tm)), "4k timing")
+    lib.KLTFreeTrackingContext(tc)
+    del fr
+    torch.cuda.empty_cache()
+    l0 = 1000.0 * tm.ms_pyr_l0 / tm.frames_pyr_l0
+    l1 = 1000.0 * tm.ms_pyr_l1 / tm.frames_pyr_l1
+    by = W * H * 13 + (W // 4) * (H // 4) * 12
+    ach = by / ((l0 + l1) * 1e-6) / 1e9
+    return {"workload": f"{W}x{H} pyramid pass, batched {chunk} frames per launch, pyramids only",
+            "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "algorithmic_bytes_per_frame": by, "us_per_frame": l0 + l1,
+            "kernels_us_per_frame": {"k_pyr_l0": l0, "k_pyr_l1": l1}, "frames_timed": int(tm.frames_pyr_l0),
+            "pyramid_gpix_s": W * H / ((l0 + l1) * 1e-6) / 1e9,
+            "event_timing": "HIP events on the launch stream, one stream"}
 
 
 def cpu_leg(lib, frames, W, H, NF, args, tc, ctx, dev):

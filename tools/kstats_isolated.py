@@ -16,6 +16,8 @@ def main(path: str, min_us: float = 0.0) -> None:
     rows = []
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
+        if int(r["Grid_Size_Z"]) > 1:  # batched pyramid launches: one row per frame size (grid.x)
+            name = f"{name} [grid.x {r['Grid_Size_X']}]"
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name, int(r["Grid_Size_Z"])))
     rows.sort()
     iso, ovl = defaultdict(list), defaultdict(list)
@@ -27,7 +29,7 @@ def main(path: str, min_us: float = 0.0) -> None:
                 break
         (ovl if overlap else iso)[n].append(((e - s) / 1e3, z))
     # grid.z of the batched pyramid kernels is the frame count of the launch
-    print(f"{'kernel':44s} {'isolated':>22s} {'us/frame':>9s} {'overlapped':>22s} {'us/frame':>9s}")
+    print(f"{'kernel':60s} {'isolated':>22s} {'us/frame':>9s} {'overlapped':>22s} {'us/frame':>9s}")
     for n in sorted(set(iso) | set(ovl)):
         a, b = iso.get(n, []), ovl.get(n, [])
         if max(d for d, _ in a + b) < min_us:
@@ -39,7 +41,7 @@ def main(path: str, min_us: float = 0.0) -> None:
                 continue
             tot, fr = sum(d for d, _ in v), sum(z for _, z in v)
             cols += [f"{len(v):5d} x {tot / len(v):10.2f} us", f"{tot / fr:9.2f}" if fr > len(v) else ""]
-        print(f"{n[:44]:44s} {cols[0]:>22s} {cols[1]:>9s} {cols[2]:>22s} {cols[3]:>9s}")
+        print(f"{n[:60]:60s} {cols[0]:>22s} {cols[1]:>9s} {cols[2]:>22s} {cols[3]:>9s}")
 
 
 if __name__ == "__main__":
