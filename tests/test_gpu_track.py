@@ -403,6 +403,16 @@ def test_tracker_tuning_hooks_do_not_change_results(gpu, oracle, opts):
     assert_table_equal(X, Y, V, *OracleTracker(oracle).harness(frames, 3000, 8, first=frames[0]))
 
 
+@pytest.mark.parametrize("opts", [dict(overlap=1), dict(overlap=0)])
+def test_overlapped_schedule_1080p(gpu, oracle, opts):
+    """The bench's overlapped schedule -- pyramids of chunk c+1 built on their
+    own stream while chunk c is tracked -- over several chunks (chunk 3, 10
+    frames, 5000 features): bit-identical to the oracle, as one stream is."""
+    frames = synth(gpu, 1080, 1920, 1080, 11)
+    X, Y, V = batch_sequence_opts(gpu, frames, 5000, 3, opts)
+    assert_table_equal(X, Y, V, *OracleTracker(oracle).harness(frames, 5000, 11, first=frames[0]))
+
+
 def batch_sequence_opts(gpu, frames, nfeat, chunk, opts):
     """batch_sequence with the tuning hooks applied to its device context."""
     orig = gpu.klt_amd_device_context
@@ -413,6 +423,7 @@ def batch_sequence_opts(gpu, frames, nfeat, chunk, opts):
         assert gpu.klt_hip_set_track_patch(ctx, opts.get("patch", 1)) == 0
         assert gpu.klt_hip_set_track_order(ctx, opts.get("order", 0)) == 0
         assert gpu.klt_hip_set_pyr_l0(ctx, opts.get("l0", 0), 0) == 0
+        assert gpu.klt_hip_set_frames_overlap(ctx, opts.get("overlap", 0)) == 0
         return ctx
 
     gpu.klt_amd_device_context = hooked
