@@ -729,6 +729,9 @@ __global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ s
 // the tile kernel's waves would stall on a full write path.  Results are the
 // tile kernel's (same tile function).
 // ---------------------------------------------------------------------------
+// (Defer holds exactly one E2 item per thread: 32-row tiles)
+#define KLT_HAVE_L0Q (KLT_L0_TH == 32)
+#if KLT_HAVE_L0Q
 static_assert((l0::TH / 4) * (l0::TW / 2) == kBlock, "Defer holds exactly one E2 item per thread");
 __global__ __launch_bounds__(kBlock) void k_pyr_l0q(DefTaps T, const uint8_t *__restrict__ src, int spitch, int W,
                                                     int H, float *__restrict__ img0, float *__restrict__ gx0,
@@ -763,6 +766,7 @@ __global__ __launch_bounds__(kBlock) void k_pyr_l0q(DefTaps T, const uint8_t *__
   }
   def.flush_all();
 }
+#endif
 
 // ---------------------------------------------------------------------------
 // k_pyr_l0p: k_pyr_l0 as a persistent kernel.  Each workgroup walks a run of
@@ -3053,7 +3057,8 @@ int launch_l0(klt_hip_ctx *c, hipStream_t st, const uint8_t *src, long pitch, lo
   const int ty0 = r0 / l0::TH, ty1 = r1 >= H ? nty : clampi((r1 + l0::TH - 1) / l0::TH, ty0, nty);
   r0 = ty0 * l0::TH;
   r1 = ty1 >= nty ? H : ty1 * l0::TH;
-  if (c->l0_mode == 3 && vec_u8 && vec_out) {
+  if (KLT_HAVE_L0Q && c->l0_mode == 3 && vec_u8 && vec_out) {
+#if KLT_HAVE_L0Q
     if (c->l0q_blocks == 0) {
       int ncu = 0, per = 0;
       if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess ||
@@ -3067,6 +3072,7 @@ int launch_l0(klt_hip_ctx *c, hipStream_t st, const uint8_t *src, long pitch, lo
     hipLaunchKernelGGL(k_pyr_l0q, grid, dim3(kBlock), 0, st, T, src, (int)pitch, W, H, img, gx, gy, hs, W1, do_hs,
                        stride, fs0, fsh, ty0, tx, ty1 - ty0, F, c->d_l0q_dummy);
     return check_launch(c, "k_pyr_l0q");
+#endif
   }
   if (c->l0_mode == 2 && vec_u8 && vec_out) {
     if (c->l0p_blocks == 0) {
