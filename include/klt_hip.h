@@ -124,6 +124,13 @@ int klt_hip_set_track_group(klt_hip_ctx *ctx, int features_per_wave);
 /* tuning hook: 1 tracks features in input order; 0 (default) in row-band
    order with each XCD given one band (L2 locality).  Results do not depend on it. */
 int klt_hip_set_track_order(klt_hip_ctx *ctx, int input_order);
+/* tuning hook: 1 (default) folds the finest level's residue pass of frame j
+   into the first pass of frame j+1 within a batched launch (one-feature
+   waves, exact sums, default gain): its gather goes out with that pass's and
+   its sum is a sixth ordered chain; frame j+1's work is dropped when the
+   verdict loses frame j's feature.  0: a residue pass of its own.  Results do
+   not depend on it. */
+int klt_hip_set_track_merge(klt_hip_ctx *ctx, int on);
 /* tuning hook: 0 disables the lane-patch gather of one-feature waves (default
    1: on where (ww+1)*(wh+1) <= 64).  Results do not depend on it. */
 int klt_hip_set_track_patch(klt_hip_ctx *ctx, int on);

@@ -1561,6 +1561,7 @@ struct TrkArgs {
   int borderx, bordery, ncols, nrows;
   int li;
   int red_pitch;     // per-sum row pitch of the reduction staging area (floats)
+  int merge_res;     // 1: defer the finest level's residue into the next frame's first pass (ResCarry)
   int *escape;       // band mode: set when a window needs rows outside [vlo, vhi)
 };
 
@@ -1913,16 +1914,59 @@ __device__ __forceinline__ void gather_direct2(const TrkLevel &A, const TrkLevel
 
 // one pass: img2 planes at (x2, y2) (grads = false: img only) and, on a
 // level's first pass, the img1 planes at (x1, y1)
+// Deferred residue (one-feature waves): the finest level's last pass of frame
+// j -- a gather of img2 at the final position and a 49-add |img1 - img2| sum,
+// a memory round trip of its own -- is folded into the first pass of frame
+// j+1: its gather goes out with that pass's gathers and its sum runs as a
+// sixth lane of that pass's ordered-sum chain.  Frame j+1 starts from frame
+// j's position before the residue is known; when the residue (or the
+// iteration cap) then loses frame j's feature, frame j+1's work is dropped and
+// the feature is recorded lost at frame j, exactly as the reference would.
+template <int PPL>
+struct ResCarry {
+  bool pending = false;
+  float x2 = 0.0f, y2 = 0.0f;  // frame j's final position at the finest level
+  int it = 0;                  // its finest-level Newton iterations
+  float aim[PPL];              // its finest-level img1 samples
+};
+
+// residue job's img2 samples: rows of plane R at (rx, ry) + the window offsets
+template <int G, int PPL, bool PATCH, int WIN>
+__device__ __forceinline__ void residue_direct(const TrkLevel &R, const GroupWin<G, PPL, PATCH, WIN> &w, float rx,
+                                               float ry, float (&r_b)[PPL]) {
+#pragma unroll
+  for (int k = 0; k < PPL; ++k) {
+    const Bil q = bil_at(R.w, R.h, rx + w.oi[k], ry + w.oj[k]);
+    r_b[k] = sel(w.on[k], corner_interp(q, corner_load(R.img, q, R.w)));
+  }
+}
+
+template <int G, int PPL, bool PATCH, int WIN>
+__device__ __forceinline__ void residue_sample(const TrkLevel &R, const GroupWin<G, PPL, PATCH, WIN> &w, float rx,
+                                               float ry, int lane, float (&r_b)[PPL]) {
+  if constexpr (PATCH) {
+    const PatchPos q = patch_pos(w, R.w, R.h, rx, ry);
+    if (q.ok) {
+      r_b[0] = patch_value(w, q, patch_load(R.img, q), lane);
+      return;
+    }
+  }
+  residue_direct(R, w, rx, ry, r_b);
+}
+
 template <int G, int PPL, bool PATCH, int WIN>
 __device__ __forceinline__ void gather_pass(const TrkLevel &A, const TrkLevel &B, const GroupWin<G, PPL, PATCH, WIN> &w,
                                             float x1, float y1, float x2, float y2, bool first, bool grads,
                                             int lane, float (&a_im)[PPL], float (&a_gx)[PPL], float (&a_gy)[PPL],
                                             float (&b_im)[PPL], float (&b_gx)[PPL], float (&b_gy)[PPL],
-                                            PatchCache &pc) {
+                                            PatchCache &pc, bool rjob = false, const TrkLevel *R = nullptr,
+                                            float rx = 0.0f, float ry = 0.0f, float *r_b = nullptr) {
   if constexpr (PATCH) {
     const PatchPos qb = patch_pos(w, B.w, B.h, x2, y2);
     const PatchPos qa = first ? patch_pos(w, A.w, A.h, x1, y1) : qb;
-    if (qb.ok && qa.ok) {
+    const PatchPos qr = rjob ? patch_pos(w, R->w, R->h, rx, ry) : qb;
+    if (qb.ok && qa.ok && qr.ok) {
+      const float vr = rjob ? patch_load(R->img, qr) : 0.0f;  // in flight with the pass's own loads
       float vb0, vb1 = 0.0f, vb2 = 0.0f, va0 = 0.0f, va1 = 0.0f, va2 = 0.0f;
       if (pc.valid && pc.X0 == qb.X0 && pc.Y0 == qb.Y0 && (pc.grads || !grads)) {
         vb0 = pc.v0;  // same cell as the last pass: its corners, this pass's weights
@@ -1955,11 +1999,18 @@ __device__ __forceinline__ void gather_pass(const TrkLevel &A, const TrkLevel &B
         a_gx[0] = patch_value(w, qa, va1, lane);
         a_gy[0] = patch_value(w, qa, va2, lane);
       }
+      if (rjob) r_b[0] = patch_value(w, qr, vr, lane);
       return;
     }
   }
   pc.valid = false;
   gather_direct2(A, B, w, x1, y1, x2, y2, first, grads, a_im, a_gx, a_gy, b_im, b_gx, b_gy);
+  if (rjob) {
+    float t[PPL];
+    residue_direct(*R, w, rx, ry, t);
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) r_b[k] = t[k];
+  }
 }
 
 __device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
@@ -1991,7 +2042,12 @@ __device__ __forceinline__ int uni(int v) {
 template <int G, int PPL, bool PATCH, int WIN, bool EXACT, bool LI>
 __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, PATCH, WIN> &w, const TrkLevel &A,
                              const TrkLevel &B, float x1, float y1, float &x2, float &y2, bool live, int lane,
-                             float *red, bool residue) {
+                             float *red, bool residue, ResCarry<PPL> &rc, bool job, bool defer, const TrkLevel &R,
+                             int &rstat) {
+  // job: rc holds the previous frame's deferred residue (img2 plane R), done
+  // in this level's first pass, verdict in rstat (the level stops when it
+  // loses that frame's feature); defer: this (finest) level's own residue is
+  // left in rc instead of taking a pass of its own
   const int ww = WIN ? WIN : a.ww, wh = WIN ? WIN : a.wh, npx = ww * wh, hw = ww / 2, hh = wh / 2;
   const int nc = A.w, nr = A.h;
   const float n = (float)(ww * wh);
@@ -2002,7 +2058,7 @@ __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, 
   bool act = live;       // still iterating
   bool fin = false;      // iterations over (converged or max_it): residue next
   int it = 0, status = kTracked;
-  bool first = true;
+  bool first = true, deferred = false;
   while (true) {
     // window test: top of an iteration, or the post-loop test for a finished one
     if (act && ((first && x1_out) || window_out(x2, y2, hw, hh, nc, nr))) {
@@ -2024,15 +2080,26 @@ __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, 
     // SMALL_DET and OOB stop the level loop (trackFeatures.c:1378), and the
     // window test just above is the post-loop test.  No final gather there.
     if (act && fin && !residue) act = false;
-    if (!wave_any(act)) break;
+    if (act && fin && defer) {  // the post-loop window test just passed: hand the residue on
+      deferred = true;
+      rc.pending = true;
+      rc.x2 = x2;
+      rc.y2 = y2;
+      rc.it = it;
+#pragma unroll
+      for (int k = 0; k < PPL; ++k) rc.aim[k] = a_im[k];
+      act = false;
+    }
+    if (!wave_any(act) && !job) break;
     PROF_INC(6);
     PROF_T(t_g0);
-    float b_im[PPL], b_gx[PPL], b_gy[PPL];
+    float b_im[PPL], b_gx[PPL], b_gy[PPL], r_b[PPL];
     const bool grads = wave_any(act && !fin);  // a residue-only pass needs img2 alone
     if (act) {  // img1 is sampled once per level, with the level's first img2 gather
       gather_pass<G, PPL, PATCH, WIN>(A, B, w, x1, y1, x2, y2, first, grads, lane, a_im, a_gx, a_gy, b_im, b_gx,
-                                      b_gy, pcache);
+                                      b_gy, pcache, job, &R, rc.x2, rc.y2, r_b);
     } else {
+      if (job) residue_sample(R, w, rc.x2, rc.y2, lane, r_b);
 #pragma unroll
       for (int k = 0; k < PPL; ++k) b_im[k] = b_gx[k] = b_gy[k] = 0.0f;
       if (first) {
@@ -2076,9 +2143,28 @@ __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, 
       }
       PROF_ADD(3, t_r0);
     }
-    if (!wave_any(act)) break;
+    float rdif[1][PPL];
+    if (job) {
+#pragma unroll
+      for (int k = 0; k < PPL; ++k) rdif[0][k] = fabsf(rc.aim[k] - r_b[k]);
+    }
+    // the previous frame's verdict (trackFeatures.c:465-484 for it)
+    auto verdict = [&](float sres) {
+      rstat = sres / n > a.max_res ? kLargeResidue : (rc.it >= a.max_it ? kMaxIter : kTracked);
+      rc.pending = false;
+      job = false;
+      if (rstat != kTracked) act = false;  // that frame's feature is lost: this frame does not happen
+    };
+    if (!wave_any(act)) {
+      if (job) {
+        float S1[1];
+        sums_g<G, 1, PPL, PATCH, WIN, EXACT>(w, rdif, red, a.red_pitch, npx, lane, S1);
+        verdict(S1[0]);
+      }
+      break;
+    }
 
-    float prod[5][PPL], S[5];
+    float prod[6][PPL], S[6];
     const bool step = act;  // groups in their residue pass are done by now
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
@@ -2109,10 +2195,21 @@ __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, 
 #endif
     PROF_ADD(0, t_g0);
     PROF_T(t_s0);
-    sums_g<G, 5, PPL, PATCH, WIN, EXACT>(w, prod, red, a.red_pitch, npx, lane, S);
+    bool stepped = step;
+    if (job) {  // the deferred residue rides along as a sixth chain
+#pragma unroll
+      for (int k = 0; k < PPL; ++k) prod[5][k] = rdif[0][k];
+      sums_g<G, 6, PPL, PATCH, WIN, EXACT>(w, prod, red, a.red_pitch, npx, lane, S);
+      verdict(S[5]);
+      stepped = step && act;
+    } else {
+      float (&p5)[5][PPL] = *reinterpret_cast<float (*)[5][PPL]>(&prod);
+      float (&s5)[5] = *reinterpret_cast<float (*)[5]>(&S);
+      sums_g<G, 5, PPL, PATCH, WIN, EXACT>(w, p5, red, a.red_pitch, npx, lane, s5);
+    }
     PROF_ADD(1, t_s0);
     PROF_T(t_v0);
-    if (step) {
+    if (stepped) {
       const float gxx = S[0], gxy = S[1], gyy = S[2];
       const float ex = S[3] * a.step, ey = S[4] * a.step;
       // _solveEquation (:293-307)
@@ -2133,6 +2230,7 @@ __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, 
     }
     PROF_ADD(2, t_v0);
   }
+  if (deferred) return kTracked;  // LARGE_RESIDUE / MAX_ITERATIONS come with the verdict
   if (status == kSmallDet) return kSmallDet;
   if (status == kOOB) return kOOB;
   if (status == kLargeResidue) return kLargeResidue;
@@ -2146,7 +2244,12 @@ __device__ __forceinline__ void track_feature_g(PROF_DECL const TrkArgs &a, cons
                                                 LevA LA,
                                                 LevB LB,
                                                 float &fx, float &fy, int &fv, bool live, int lane,
-                                                float *red) {
+                                                float *red, ResCarry<PPL> &rc, bool job, bool defer,
+                                                const TrkLevel &R, int &rstat) {
+  // job: the previous frame's residue is pending (rc) and resolves in the
+  // coarsest level's first pass; if it loses that frame's feature this frame
+  // is not tracked and fx/fy/fv stay as they are (the caller records the
+  // loss).  defer: this frame's own finest-level residue may be handed on.
   float xl = fx, yl = fy;
   for (int r = a.nlev - 1; r >= 0; --r) {
     xl = uni<G>(xl / a.ss);
@@ -2163,8 +2266,11 @@ __device__ __forceinline__ void track_feature_g(PROF_DECL const TrkArgs &a, cons
       xo = uni<G>(xo * a.ss);
       yo = uni<G>(yo * a.ss);
     }
+    const bool lj = job && r == a.nlev - 1;
     const int v = track_level_g<G, PPL, PATCH, WIN, EXACT, LI>(PROF_ARG a, w, LA(r), LB(r), xl, yl, xo, yo, go,
-                                                               lane, red, r == 0);
+                                                               lane, red, r == 0, rc, lj, defer && r == 0, R,
+                                                               rstat);
+    if (lj && rstat != kTracked) return;
     if (go) {
       val = v;
       if (v == kSmallDet || v == kOOB) go = false;
@@ -2174,6 +2280,7 @@ __device__ __forceinline__ void track_feature_g(PROF_DECL const TrkArgs &a, cons
   const bool border = xo < a.borderx || xo > a.ncols - 1 - a.borderx || yo < a.bordery ||
                       yo > a.nrows - 1 - a.bordery;
   if (val == kOOB || border) {
+    rc.pending = false;  // outside the border: OOB whatever the residue (trackFeatures.c:1398)
     fx = -1.0f;
     fy = -1.0f;
     fv = kOOB;
@@ -2192,7 +2299,7 @@ template <int G, int PPL, bool PATCH, int WIN, bool EXACT, bool LI>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KLT_TRACK_WAVES))) void k_track_frames_g(TrkArgs a, TrkFramesArgs b, float *__restrict__ fx,
                                                            float *__restrict__ fy, int *__restrict__ fv, int n) {
   constexpr int LG = kWave / G;
-  __shared__ __attribute__((aligned(16))) float red_all[kBlock / kWave][5 * G * (LG * PPL + 4) + 16];
+  __shared__ __attribute__((aligned(16))) float red_all[kBlock / kWave][6 * G * (LG * PPL + 4) + 16];
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   // consecutive workgroups land on the 8 XCDs round-robin: give each XCD a
   // contiguous run of the (band-sorted) order so its L2 sees one image band
@@ -2213,7 +2320,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KLT_TRAC
   const GroupWin<G, PPL, PATCH, WIN> w = group_window<G, PPL, PATCH, WIN>(a.ww, a.wh, lane);
   {  // row pads of the ordered-sum staging stay +0 for the whole kernel
     float *red = red_all[wave];
-    constexpr int RED = 5 * G * (LG * PPL + 4) + 16;
+    constexpr int RED = 6 * G * (LG * PPL + 4) + 16;
     for (int i = lane; i < RED; i += kWave) red[i] = 0.0f;
     lds_wave_sync();
   }
@@ -2222,16 +2329,35 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KLT_TRAC
   Prof prof;
   const unsigned long long wall0 = wall_clock64();
 #endif
+  // deferred residues (ResCarry): one-feature waves, exact sums, default gain
+  const bool merge = G == 1 && EXACT && !LI && a.merge_res && a.nlev >= 2 && !a.escape;
+  ResCarry<PPL> rc;
   for (int j = 0; j < b.nframes; ++j) {
-    const bool live = exists && v >= 0;  // lost features are not tracked (:1346)
+    const bool job = rc.pending;  // frame j-1 is tentatively tracked at (x, y)
+    const bool live = exists && (v >= 0 || job);  // lost features are not tracked (:1346)
+    const float xp = x, yp = y;
+    int rstat = kTracked;
     PROF_T(t_f0);
     if (wave_any(live)) {
+      auto LA = [&](int r) { return j == 0 ? a.A[r] : at_frame(a.B[r], (long)(j - 1) * b.lfs[r]); };
       track_feature_g<G, PPL, PATCH, WIN, EXACT, LI>(
-          PROF_ARG a, w, [&](int r) { return j == 0 ? a.A[r] : at_frame(a.B[r], (long)(j - 1) * b.lfs[r]); },
-          [&](int r) { return at_frame(a.B[r], (long)j * b.lfs[r]); }, x, y, v, live, lane, red_all[wave]);
+          PROF_ARG a, w, LA, [&](int r) { return at_frame(a.B[r], (long)j * b.lfs[r]); }, x, y, v, live, lane,
+          red_all[wave], rc, job, merge && j + 1 < b.nframes, LA(0), rstat);
     }
     PROF_ADD(4, t_f0);
-    if (b.tx && head) {
+    if (job) {  // frame j-1's verdict came with frame j's first pass
+      if (rstat != kTracked) {
+        x = -1.0f;
+        y = -1.0f;
+        v = rstat;
+      }
+      if (b.tx && head) {
+        b.tx[(j - 1) * b.tstride + f] = rstat != kTracked ? -1.0f : xp;
+        b.ty[(j - 1) * b.tstride + f] = rstat != kTracked ? -1.0f : yp;
+        b.tv[(j - 1) * b.tstride + f] = rstat;
+      }
+    }
+    if (b.tx && head && !rc.pending) {
       b.tx[j * b.tstride + f] = x;
       b.ty[j * b.tstride + f] = y;
       b.tv[j * b.tstride + f] = v;
@@ -2829,6 +2955,7 @@ struct klt_hip_ctx {
   int l0_mode = 0;       // level 0: 0 k_pyr_l0 tiles (default), 1 k_pyr_l0s strips, 2 k_pyr_l0p persistent tiles
   int l0p_blocks = 0;    // k_pyr_l0p resident workgroups (CUs x occupancy), filled on first use
   int l0q_blocks = 0;    // k_pyr_l0q likewise
+  int track_merge = 1;   // defer finest-level residues into the next frame's first pass (ResCarry)
   float *d_l0q_dummy = nullptr;  // k_pyr_l0q: target of the deferred stores before a workgroup's first tile
   int l0_strip_steps = 8;  // k_pyr_l0s steps per strip (strip height / TH)
   int serial_frames = 1;  // klt_hip_track_frames: 1 builds and tracks on one stream (default: the
@@ -3212,12 +3339,14 @@ int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc
   bb.prof = c->prof;
 #endif
   const TrkFramesArgs &b2 = bb;
+  TrkArgs aa = a;
+  aa.merge_res = c->track_merge;
   if (exact) {
-    if (li) launch_track_sel<true, true>(G, patch, win7, npx, st, a, b2, x, y, v, n);
-    else launch_track_sel<true, false>(G, patch, win7, npx, st, a, b2, x, y, v, n);
+    if (li) launch_track_sel<true, true>(G, patch, win7, npx, st, aa, b2, x, y, v, n);
+    else launch_track_sel<true, false>(G, patch, win7, npx, st, aa, b2, x, y, v, n);
   } else {
-    if (li) launch_track_sel<false, true>(G, patch, win7, npx, st, a, b2, x, y, v, n);
-    else launch_track_sel<false, false>(G, patch, win7, npx, st, a, b2, x, y, v, n);
+    if (li) launch_track_sel<false, true>(G, patch, win7, npx, st, aa, b2, x, y, v, n);
+    else launch_track_sel<false, false>(G, patch, win7, npx, st, aa, b2, x, y, v, n);
   }
   return check_launch(c, "k_track_frames");
 }
@@ -3530,6 +3659,12 @@ KLT_API int klt_hip_set_pyr_l0(klt_hip_ctx *c, int mode, int strip_steps) {
     return fail(c, "set_pyr_l0: mode %d (0 tiles, 1 strips, 2 persistent tiles, 3 deferred stores)", mode);
   c->l0_mode = mode;
   if (strip_steps > 0) c->l0_strip_steps = strip_steps;
+  return 0;
+}
+
+KLT_API int klt_hip_set_track_merge(klt_hip_ctx *c, int on) {
+  if (!c) return fail(c, "set_track_merge: null context");
+  c->track_merge = on ? 1 : 0;
   return 0;
 }
 

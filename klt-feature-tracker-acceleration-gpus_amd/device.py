@@ -63,6 +63,7 @@ DEVICE_PROTOS = {
     "klt_hip_fused_path": (C.c_int, [V, C.POINTER(PyrDesc)]),
     "klt_hip_set_track_group": (C.c_int, [V, C.c_int]),
     "klt_hip_set_track_order": (C.c_int, [V, C.c_int]),
+    "klt_hip_set_track_merge": (C.c_int, [V, C.c_int]),
     "klt_hip_set_track_patch": (C.c_int, [V, C.c_int]),
     "klt_hip_set_pyr_l0": (C.c_int, [V, C.c_int, C.c_int]),
     "klt_hip_set_frames_overlap": (C.c_int, [V, C.c_int]),

@@ -394,7 +394,8 @@ def test_patch_gather_edge_positions(gpu, oracle, patch):
 
 
 @pytest.mark.parametrize("opts", [dict(group=1, patch=0), dict(group=2, patch=1), dict(group=4, patch=1),
-                                  dict(order=1, patch=1), dict(l0=2), dict(l0=3), dict(l0=3, chunk=7)])
+                                  dict(order=1, patch=1), dict(l0=2), dict(l0=3), dict(l0=3, chunk=7),
+                                  dict(merge=0), dict(merge=0, patch=0)])
 def test_tracker_tuning_hooks_do_not_change_results(gpu, oracle, opts):
     """Features per wave, lane patch, processing order and the level-0 kernel
     (batched over a chunk's frames) only reorganise work."""
@@ -403,7 +404,7 @@ def test_tracker_tuning_hooks_do_not_change_results(gpu, oracle, opts):
     assert_table_equal(X, Y, V, *OracleTracker(oracle).harness(frames, 3000, 8, first=frames[0]))
 
 
-@pytest.mark.parametrize("opts", [dict(overlap=1), dict(overlap=0)])
+@pytest.mark.parametrize("opts", [dict(overlap=1), dict(overlap=0), dict(overlap=1, merge=0)])
 def test_overlapped_schedule_1080p(gpu, oracle, opts):
     """The bench's overlapped schedule -- pyramids of chunk c+1 built on their
     own stream while chunk c is tracked -- over several chunks (chunk 3, 10
@@ -424,6 +425,7 @@ def batch_sequence_opts(gpu, frames, nfeat, chunk, opts):
         assert gpu.klt_hip_set_track_order(ctx, opts.get("order", 0)) == 0
         assert gpu.klt_hip_set_pyr_l0(ctx, opts.get("l0", 0), 0) == 0
         assert gpu.klt_hip_set_frames_overlap(ctx, opts.get("overlap", 0)) == 0
+        assert gpu.klt_hip_set_track_merge(ctx, opts.get("merge", 1)) == 0
         return ctx
 
     gpu.klt_amd_device_context = hooked

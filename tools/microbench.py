@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--overlap", action="store_true", help="frames: pyramids of chunk c+1 on a second stream")
     ap.add_argument("--no-patch", action="store_true", help="tracker: per-pixel gathers only")
     ap.add_argument("--input-order", action="store_true", help="tracker: no band ordering")
+    ap.add_argument("--no-merge", action="store_true", help="tracker: residue passes of their own")
     ap.add_argument("--group", type=int, default=0, help="tracker: features per wave (0 default, 1, 2, 4)")
     ap.add_argument("--chunk", type=int, default=16, help="frames: frames per batch")
     ap.add_argument("--pyr-only", action="store_true", help="frames: build the batched pyramids, track nothing")
@@ -66,6 +67,7 @@ def main():
     lib.klt_hip_set_path(ctx, 1 if a.generic else 0)
     check(lib, ctx, lib.klt_hip_set_track_group(ctx, a.group), "group")
     check(lib, ctx, lib.klt_hip_set_track_order(ctx, 1 if a.input_order else 0), "order")
+    check(lib, ctx, lib.klt_hip_set_track_merge(ctx, 0 if a.no_merge else 1), "merge")
     check(lib, ctx, lib.klt_hip_set_track_patch(ctx, 0 if a.no_patch else 1), "patch")
     check(lib, ctx, lib.klt_hip_set_frames_overlap(ctx, 1 if a.overlap else 0), "overlap")
     if a.l0_mode >= 0 or a.l0_tiles:
