@@ -3446,6 +3446,7 @@ KLT_API int klt_hip_device_count(void) {
 
 KLT_API klt_hip_ctx *klt_hip_ctx_create(int device) {
   klt_hip_ctx *c = new klt_hip_ctx();
+  if (const char *m = getenv("KLT_AMD_TRACK_MERGE")) c->track_merge = atoi(m) != 0;  // A/B switch for tools
   if (device < 0) {
     if (hipGetDevice(&device) != hipSuccess) device = 0;
   }

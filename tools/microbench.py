@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--no-patch", action="store_true", help="tracker: per-pixel gathers only")
     ap.add_argument("--input-order", action="store_true", help="tracker: no band ordering")
     ap.add_argument("--no-merge", action="store_true", help="tracker: residue passes of their own")
+    ap.add_argument("--table", action="store_true", help="frames: write the feature table (as bench.py does)")
     ap.add_argument("--group", type=int, default=0, help="tracker: features per wave (0 default, 1, 2, 4)")
     ap.add_argument("--chunk", type=int, default=16, help="frames: frames per batch")
     ap.add_argument("--pyr-only", action="store_true", help="frames: build the batched pyramids, track nothing")
@@ -182,14 +183,16 @@ def main():
         if a.pyr_only:
             n = 0
 
+        tab = [lib.klt_hip_malloc(ctx, 4 * max(n, 1) * T) for _ in range(3)] if a.table else [None] * 3
+
         def rep():
             # restart from the seed frame and the selected features
             for dd, ss in zip(d, d0):
                 check(lib, ctx, lib.klt_hip_memcpy(ctx, dd, ss, 4 * n, D2D), "d2d")
             check(lib, ctx, lib.klt_hip_frames_begin(ctx, C.byref(pd), C.c_void_p(frames), W), "begin")
             check(lib, ctx, lib.klt_hip_track_frames(ctx, C.byref(pd), C.byref(td), C.c_void_p(frames + W * H),
-                                                     W, W * H, T, a.chunk, d[0], d[1], d[2], n, None, None,
-                                                     None, 0), "frames")
+                                                     W, W * H, T, a.chunk, d[0], d[1], d[2], n, tab[0], tab[1],
+                                                     tab[2], n if a.table else 0), "frames")
 
         lib.klt_hip_sync(ctx)
         t0 = time.perf_counter()
