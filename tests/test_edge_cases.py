@@ -127,3 +127,22 @@ def test_gpu_all_lost_list_is_untouched(gpu):
     gpu.KLTFreeFeatureList(fl)
     gpu.KLTFreeTrackingContext(tc)
     assert np.array_equal(gx, x) and np.array_equal(gy, y) and np.array_equal(gv, v)
+
+
+@pytest.mark.gpu
+def test_gpu_8k_frame_pyramid_and_tracking(gpu, oracle):
+    """The largest size class: a 7680x4320 pair (33 Mpx, 132 MB per f32
+    plane) -- the fused pyramid bit-identical to the oracle, and 2000
+    features tracked over it bit-identically."""
+    from gpu_helpers import Dev
+    from test_gpu_pyramid import assert_planes_equal, oracle_for
+    h, w = 4320, 7680
+    frames = synth(gpu, 4320, w, h, 3)
+    dev = Dev(gpu)
+    dev.build(frames[0])
+    assert dev.path(0) == 1
+    assert_planes_equal(dev.levels(0, 2), oracle_for(oracle, dev.tc).frame_pyramid(frames[0]), "8k")
+    got = KLTRunner(gpu).harness(frames, 2000, 3)
+    want = OracleTracker(oracle).harness(frames, 2000, 3)
+    assert table_eq(got, want)
+    assert (got[2][:, 1] == 0).sum() > 1500
