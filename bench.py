@@ -14,7 +14,8 @@ N GPUs: one process per GPU (torchrun), each tracks its own sequence
 no data-path collective; value = total frames / max-over-ranks time.
 
 Extra keys: pyramid_gpix_s, roofline (pyramid pass, HIP events on the launch
-stream), kernels (avg us per launch), cpu_baseline (the reference compiled
+stream; measured_peak: this box's copy/fill GB/s beside the 8 TB/s spec),
+roofline_4k (the same pass at 3840x2160), kernels (avg us per launch), cpu_baseline (the reference compiled
 from its own sources, oracle/_ref, timed on this host), parity (GPU vs that
 reference on the CPU sample, cell by cell).
 """
@@ -274,6 +275,13 @@ def main() -> None:
     del frames, tab
     if rank == 0 and world == 1 and not args.no_4k:
         result["roofline_4k"] = pass_4k(lib, dev)
+    if rank == 0 and world == 1:
+        # the fraction also against a measured copy peak
+        mp = measured_peaks(dev)
+        for key in ("roofline", "roofline_4k"):
+            if key in result:
+                result[key]["measured_peak"] = dict(mp, frac_vs_copy=result[key]["achieved"] / mp["copy_gbs"],
+                                                    frac_vs_fill=result[key]["achieved"] / mp["fill_gbs"])
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
@@ -413,6 +421,34 @@ def pass_4k(lib, dev, chunk=64, reps=2):
             "kernels_us_per_frame": {"k_pyr_l0": l0, "k_pyr_l1": l1}, "frames_timed": int(tm.frames_pyr_l0),
             "pyramid_gpix_s": W * H / ((l0 + l1) * 1e-6) / 1e9,
             "event_timing": "HIP events on the launch stream, one stream"}
+
+
+def measured_peaks(dev, nbytes=2 << 30, reps=5):
+    """Measured HBM peaks on this box, for context next to the 8 TB/s spec:
+    a device-to-device copy of 2 GiB (read + write bytes) and a 2 GiB fill
+    (write bytes; the pyramid pass writes 13 of its 13.75 B/px), torch's own
+    kernels, HIP events on the current stream, best of `reps`."""
+    import torch
+    a = torch.ones(nbytes // 4, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+
+    def best(fn, moved):
+        fn()
+        out = 0.0
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            out = max(out, moved / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+        return out
+
+    copy = best(lambda: b.copy_(a), 2.0 * nbytes)
+    fill = best(lambda: b.fill_(2.0), 1.0 * nbytes)
+    del a, b
+    torch.cuda.empty_cache()
+    return {"copy_gbs": copy, "fill_gbs": fill, "source": "torch copy_/fill_ of 2 GiB, HIP events, best of 5"}
 
 
 def cpu_leg(lib, frames, W, H, NF, args, tc, ctx, dev):

@@ -6,7 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
-template <bool RD, bool WR>
+template <bool RD, bool WR, bool TILED = false>
 __global__ __launch_bounds__(256) void k_tile(const unsigned char *src, float *out, int W, int H, int tiles_x,
                                               int tiles_y) {
   const int per = gridDim.x / 8;
@@ -32,7 +32,7 @@ __global__ __launch_bounds__(256) void k_tile(const unsigned char *src, float *o
     const int g = tid & 15, rl = tid >> 4;
     const float4 v = make_float4(acc, g, 1.f, 2.f);
     for (int r = rl; r < 32; r += 16) {
-      const long o = (long)(R0 + r) * W + C0 + 4 * g;
+      const long o = TILED ? (long)t * 2048 + r * 64 + 4 * g : (long)(R0 + r) * W + C0 + 4 * g;
 #pragma unroll
       for (int s = 0; s < 3; ++s) *reinterpret_cast<float4 *>(out + s * plane + o) = v;
     }
@@ -42,17 +42,17 @@ __global__ __launch_bounds__(256) void k_tile(const unsigned char *src, float *o
   }
 }
 
-template <bool RD, bool WR>
+template <bool RD, bool WR, bool TILED = false>
 void run(const unsigned char *s, float *d, int W, int H, int F, const char *name) {
   const int tx = W / 64, ty = H / 32, n = tx * ty;
   dim3 grid(8 * ((n + 7) / 8), 1, F);
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((k_tile<RD, WR>), grid, dim3(256), 0, 0, s, d, W, H, tx, ty);
+  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((k_tile<RD, WR, TILED>), grid, dim3(256), 0, 0, s, d, W, H, tx, ty);
   hipEventRecord(a);
   const int reps = 10;
-  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((k_tile<RD, WR>), grid, dim3(256), 0, 0, s, d, W, H, tx, ty);
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((k_tile<RD, WR, TILED>), grid, dim3(256), 0, 0, s, d, W, H, tx, ty);
   hipEventRecord(b);
   hipEventSynchronize(b);
   float ms;
@@ -73,6 +73,8 @@ int main() {
   run<true, true>(s, d, W, H, F, "read+write");
   run<false, true>(s, d, W, H, F, "write only");
   run<true, false>(s, d, W, H, F, "read only");
+  run<true, true, true>(s, d, W, H, F, "rw tiled");
+  run<false, true, true>(s, d, W, H, F, "w tiled");
   hipFree(s);
   hipFree(d);
   return 0;
