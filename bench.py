@@ -15,7 +15,9 @@ no data-path collective; value = total frames / max-over-ranks time.
 
 Extra keys: pyramid_gpix_s, roofline (pyramid pass, HIP events on the launch
 stream; measured_peak: this box's copy/fill GB/s beside the 8 TB/s spec),
-roofline_4k (the same pass at 3840x2160), kernels (avg us per launch), cpu_baseline (the reference compiled
+roofline_4k (the same pass at 3840x2160), kernels (avg us per launch), tracker
+(Newton iterations counted on the device in a separate replay,
+feature-iterations/s over the tracker's own event time), cpu_baseline (the reference compiled
 from its own sources, oracle/_ref, timed on this host), parity (GPU vs that
 reference on the CPU sample, cell by cell).
 """
@@ -193,6 +195,20 @@ def main() -> None:
         run(t_start, args.steps)
     check(lib, ctx, lib.klt_hip_get_timing(ctx, C.byref(tm)), "timing")
     lib.klt_hip_set_timing(ctx, 0)
+    tracker = None
+    if args.chunk > 0:
+        # tracker work counters (Newton iterations, gather passes) in a replay
+        # of their own, so that neither timed run carries the counting atomics
+        x.copy_(xs); y.copy_(ys); v.copy_(vs)
+        build0(t_start - 1)
+        check(lib, ctx, lib.klt_hip_set_track_count(ctx, 1), "track_count")
+        run(t_start, args.steps)
+        solves, passes = C.c_ulonglong(0), C.c_ulonglong(0)
+        check(lib, ctx, lib.klt_hip_get_track_count(ctx, C.byref(solves), C.byref(passes), 0), "track_count")
+        lib.klt_hip_set_track_count(ctx, 0)
+        # feature-frames: features live when frame j starts (table row j-1 holds the list after j-1)
+        ff = int((tab[2][t_start - 1:t_start - 1 + args.steps] >= 0).sum().item())
+        tracker = tracker_line(solves.value, passes.value, ff, tm)
 
     dt_max = dt
     if world > 1:
@@ -243,6 +259,8 @@ def main() -> None:
         "frames_per_launch": fpl,
         "live_features": {"after_warmup": live_before, "at_end": live_after},
     }
+    if tracker:
+        result["tracker"] = tracker
     if pass_us:
         ach = pass_bytes / (pass_us * 1e-6) / 1e9
         result["roofline"] = {
@@ -421,6 +439,24 @@ def pass_4k(lib, dev, chunk=64, reps=2):
             "kernels_us_per_frame": {"k_pyr_l0": l0, "k_pyr_l1": l1}, "frames_timed": int(tm.frames_pyr_l0),
             "pyramid_gpix_s": W * H / ((l0 + l1) * 1e-6) / 1e9,
             "event_timing": "HIP events on the launch stream, one stream"}
+
+
+def tracker_line(solves, passes, feature_frames, tm):
+    """the LK tracker is gather/latency and VALU bound, not an HBM
+    roofline kernel; report its work rate as feature-iterations per second.
+    An iteration is one 2x2 system formed (a body of the reference's Newton
+    loop, trackFeatures.c:418-455, both levels summed); counted on the device
+    (klt_hip_set_track_count) over the same frames the kernel events time."""
+    s = tm.ms_track * 1e-3
+    return {
+        "kernel": "k_track_frames_g", "bound": "VALU / gather latency (no HBM roofline, SURVEY 8d)",
+        "newton_iterations": solves, "gather_passes": passes, "feature_frames": feature_frames,
+        "iterations_per_feature_frame": solves / feature_frames if feature_frames else None,
+        "passes_per_feature_frame": passes / feature_frames if feature_frames else None,
+        "feature_iterations_per_s": solves / s if s > 0 else None,
+        "feature_frames_per_s": feature_frames / s if s > 0 else None,
+        "ns_per_iteration": s * 1e9 / solves if solves else None,
+    }
 
 
 def measured_peaks(dev, nbytes=2 << 30, reps=5):

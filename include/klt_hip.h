@@ -131,6 +131,17 @@ int klt_hip_set_track_order(klt_hip_ctx *ctx, int input_order);
    verdict loses frame j's feature.  0: a residue pass of its own.  Results do
    not depend on it. */
 int klt_hip_set_track_merge(klt_hip_ctx *ctx, int on);
+/* measurement hook: on != 0 zeroes (allocating on first use) two device
+   counters that every later tracker launch of this context adds to -- the 2x2
+   systems formed, i.e. the reference's Newton loop bodies
+   (trackFeatures.c:418-455, the SMALL_DET one included), and the gather round
+   trips -- one pair of atomics per feature per launch; 0 frees them.  Results
+   do not depend on it.  klt_hip_get_track_count synchronizes the device, reads
+   both counters and zeroes them when reset != 0; it fails while counting is
+   off. */
+int klt_hip_set_track_count(klt_hip_ctx *ctx, int on);
+int klt_hip_get_track_count(klt_hip_ctx *ctx, unsigned long long *solves, unsigned long long *passes,
+                            int reset);
 /* tuning hook: 0 disables the lane-patch gather of one-feature waves (default
    1: on where (ww+1)*(wh+1) <= 64).  Results do not depend on it. */
 int klt_hip_set_track_patch(klt_hip_ctx *ctx, int on);

@@ -140,6 +140,12 @@ __device__ __forceinline__ f4 mul4(const float *v, float k) {
   return f4{lo.x, lo.y, hi.x, hi.y};
 }
 
+// Centre of the 7-tap derivative: -0 * g / sum == +0 exactly (convolve.c:92,
+// fused_ok checks it).  A product with it is +-0, and an ordered sum started
+// from +0 is never -0 (x + (-x) rounds to +0), so acc + v * d[kDC] == acc bit
+// for bit and the derivative passes leave that term out: 6 of 7 multiply-adds.
+constexpr int kDC = 3;
+
 struct DefTaps {
   float s[5];   // smoothing gauss, reversed
   float g[7];   // gradient gauss, reversed
@@ -504,11 +510,13 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     *reinterpret_cast<f4 *>(v) = ld4(row);
     *reinterpret_cast<f4 *>(v + 4) = ld4(row + 4);
     *reinterpret_cast<f4 *>(v + 8) = ld4(row + 8);
-    f4 ax = {0.0f, 0.0f, 0.0f, 0.0f}, ay = {0.0f, 0.0f, 0.0f, 0.0f};
+    // ay: img0 >= +0 and gauss taps > 0, so every term is >= +0 and the +0
+    // start can be left out (mul4); ax has signed taps and keeps it
+    f4 ax = {0.0f, 0.0f, 0.0f, 0.0f}, ay = mul4(v + 1, T2.g[0]);
 #pragma unroll
     for (int m = 0; m < 7; ++m) {
-      mac4(ax, v + 1 + m, T2.d[m]);
-      mac4(ay, v + 1 + m, T2.g[m]);
+      if (m != kDC) mac4(ax, v + 1 + m, T2.d[m]);  // zero centre tap: exact to skip (see kDC)
+      if (m > 0) mac4(ay, v + 1 + m, T2.g[m]);
     }
     if (!INT) {
       const int x = C0 + 4 * g;
@@ -611,7 +619,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
 #pragma unroll
       for (int m = 0; m < 7; ++m) {
         ax += vx[rr + m] * f2{T4.g[m], T4.g[m]};
-        ay += vy[rr + m] * f2{T4.d[m], T4.d[m]};
+        if (m != kDC) ay += vy[rr + m] * f2{T4.d[m], T4.d[m]};
       }
       const int y = R0 + 4 * b + rr, x = C0 + 2 * g;
       if (!(KLT_L0T_XST & 4)) {
@@ -656,7 +664,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
 #pragma unroll
       for (int m = 0; m < 7; ++m) {
         mac4(ax, reinterpret_cast<const float *>(&vx[rr + m]), T4.g[m]);
-        mac4(ay, reinterpret_cast<const float *>(&vy[rr + m]), T4.d[m]);
+        if (m != kDC) mac4(ay, reinterpret_cast<const float *>(&vy[rr + m]), T4.d[m]);
       }
       const int y = R0 + 2 * b + rr, x = C0 + 4 * g;
       if (!(KLT_L0T_XST & 4)) {
@@ -1407,11 +1415,11 @@ __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs,
     *reinterpret_cast<f4 *>(v) = ld4(row);
     *reinterpret_cast<f4 *>(v + 4) = ld4(row + 4);
     *reinterpret_cast<f4 *>(v + 8) = ld4(row + 8);
-    f4 ax = {0.0f, 0.0f, 0.0f, 0.0f}, ay = {0.0f, 0.0f, 0.0f, 0.0f};
+    f4 ax = {0.0f, 0.0f, 0.0f, 0.0f}, ay = mul4(v + 1, T.g[0]);  // level-1 img >= +0: as k_pyr_l0's D2
 #pragma unroll
     for (int m = 0; m < 7; ++m) {
-      mac4(ax, v + 1 + m, T.d[m]);
-      mac4(ay, v + 1 + m, T.g[m]);
+      if (m != kDC) mac4(ax, v + 1 + m, T.d[m]);
+      if (m > 0) mac4(ay, v + 1 + m, T.g[m]);
     }
     const int X = x0 + 4 * g;
 #pragma unroll
@@ -1433,7 +1441,7 @@ __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs,
     for (int m = 0; m < 7; ++m) {
       const f4 a = ld4(tx + (r + m) * TW + 4 * g), b = ld4(ty + (r + m) * TW + 4 * g);
       mac4(ax, reinterpret_cast<const float *>(&a), T.g[m]);
-      mac4(ay, reinterpret_cast<const float *>(&b), T.d[m]);
+      if (m != kDC) mac4(ay, reinterpret_cast<const float *>(&b), T.d[m]);
     }
     const int Y = y0 + r, X = x0 + 4 * g;
     if (Y >= H1 || X >= W1) continue;
@@ -1639,6 +1647,7 @@ struct TrkFramesArgs {
   float *tx, *ty;
   int *tv;
   long tstride;  // table row stride (elements); tx == nullptr: no table
+  unsigned long long *count;  // non-null: [kCountSlots] 2x2 systems formed, [kCountSlots] gather round trips
 };
 
 __device__ __forceinline__ TrkLevel at_frame(const TrkLevel &L, long off) {
@@ -2028,6 +2037,14 @@ __device__ __forceinline__ int uni(int v) {
   return v;
 }
 
+// Work counters of a feature (klt_hip_track_counts): 2x2 systems formed --
+// the reference's Newton loop bodies (trackFeatures.c:418-455), the one that
+// ends in SMALL_DET included -- and gather round trips (passes).
+struct TrkCount {
+  unsigned solves = 0, passes = 0;
+};
+constexpr int kCountSlots = 64;  // counter pairs (the host sums them): the last waves' atomics do not queue on one address
+
 // _trackFeature (trackFeatures.c:381-486) for the G features of a wave at one
 // level.  Per-lane state is uniform within a feature's lane group; `live`
 // says whether the group's feature is tracked at this level.
@@ -2043,7 +2060,7 @@ template <int G, int PPL, bool PATCH, int WIN, bool EXACT, bool LI>
 __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, PATCH, WIN> &w, const TrkLevel &A,
                              const TrkLevel &B, float x1, float y1, float &x2, float &y2, bool live, int lane,
                              float *red, bool residue, ResCarry<PPL> &rc, bool job, bool defer, const TrkLevel &R,
-                             int &rstat) {
+                             int &rstat, TrkCount &cnt) {
   // job: rc holds the previous frame's deferred residue (img2 plane R), done
   // in this level's first pass, verdict in rstat (the level stops when it
   // loses that frame's feature); defer: this (finest) level's own residue is
@@ -2092,6 +2109,7 @@ __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, 
     }
     if (!wave_any(act) && !job) break;
     PROF_INC(6);
+    if (act || job) ++cnt.passes;
     PROF_T(t_g0);
     float b_im[PPL], b_gx[PPL], b_gy[PPL], r_b[PPL];
     const bool grads = wave_any(act && !fin);  // a residue-only pass needs img2 alone
@@ -2227,6 +2245,7 @@ __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, 
         if (!((fabsf(dx) >= a.min_disp || fabsf(dy) >= a.min_disp) && it < a.max_it)) fin = true;
       }
       PROF_INC(5);
+      ++cnt.solves;
     }
     PROF_ADD(2, t_v0);
   }
@@ -2245,7 +2264,7 @@ __device__ __forceinline__ void track_feature_g(PROF_DECL const TrkArgs &a, cons
                                                 LevB LB,
                                                 float &fx, float &fy, int &fv, bool live, int lane,
                                                 float *red, ResCarry<PPL> &rc, bool job, bool defer,
-                                                const TrkLevel &R, int &rstat) {
+                                                const TrkLevel &R, int &rstat, TrkCount &cnt) {
   // job: the previous frame's residue is pending (rc) and resolves in the
   // coarsest level's first pass; if it loses that frame's feature this frame
   // is not tracked and fx/fy/fv stay as they are (the caller records the
@@ -2269,7 +2288,7 @@ __device__ __forceinline__ void track_feature_g(PROF_DECL const TrkArgs &a, cons
     const bool lj = job && r == a.nlev - 1;
     const int v = track_level_g<G, PPL, PATCH, WIN, EXACT, LI>(PROF_ARG a, w, LA(r), LB(r), xl, yl, xo, yo, go,
                                                                lane, red, r == 0, rc, lj, defer && r == 0, R,
-                                                               rstat);
+                                                               rstat, cnt);
     if (lj && rstat != kTracked) return;
     if (go) {
       val = v;
@@ -2332,6 +2351,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KLT_TRAC
   // deferred residues (ResCarry): one-feature waves, exact sums, default gain
   const bool merge = G == 1 && EXACT && !LI && a.merge_res && a.nlev >= 2 && !a.escape;
   ResCarry<PPL> rc;
+  TrkCount cnt;
   for (int j = 0; j < b.nframes; ++j) {
     const bool job = rc.pending;  // frame j-1 is tentatively tracked at (x, y)
     const bool live = exists && (v >= 0 || job);  // lost features are not tracked (:1346)
@@ -2342,7 +2362,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KLT_TRAC
       auto LA = [&](int r) { return j == 0 ? a.A[r] : at_frame(a.B[r], (long)(j - 1) * b.lfs[r]); };
       track_feature_g<G, PPL, PATCH, WIN, EXACT, LI>(
           PROF_ARG a, w, LA, [&](int r) { return at_frame(a.B[r], (long)j * b.lfs[r]); }, x, y, v, live, lane,
-          red_all[wave], rc, job, merge && j + 1 < b.nframes, LA(0), rstat);
+          red_all[wave], rc, job, merge && j + 1 < b.nframes, LA(0), rstat, cnt);
     }
     PROF_ADD(4, t_f0);
     if (job) {  // frame j-1's verdict came with frame j's first pass
@@ -2367,6 +2387,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KLT_TRAC
     fx[f] = x;
     fy[f] = y;
     fv[f] = v;
+    if (b.count) {  // one pair of atomics per feature per launch, spread over kCountSlots addresses
+      const int k = (blk * (kBlock / kWave) + wave) & (kCountSlots - 1);
+      atomicAdd(&b.count[k], (unsigned long long)cnt.solves);
+      atomicAdd(&b.count[kCountSlots + k], (unsigned long long)cnt.passes);
+    }
   }
 #ifdef KLT_TRACK_PROF
   prof.c[8] = wall0;
@@ -2963,6 +2988,7 @@ struct klt_hip_ctx {
   int *d_perm = nullptr;
   size_t perm_cap = 0;
   int *d_count = nullptr;  // band mode: features owned in this chunk
+  unsigned long long *d_trk_count = nullptr;  // klt_hip_set_track_count: {solves, passes}, null when off
   unsigned char *d_ring = nullptr;  // klt_hip_track_frames_host: 2 chunks of uploaded frames
   size_t ring_cap = 0;
   hipStream_t cstream = nullptr;
@@ -3058,7 +3084,7 @@ int check_launch(klt_hip_ctx *c, const char *what) {
 
 bool fused_ok(const klt_hip_pyr_desc *d) {
   return d->smooth_input && d->smooth.width == 2 * kRS + 1 && d->grad_gauss.width == 2 * kRG + 1 &&
-         d->grad_deriv.width == 2 * kRG + 1 &&
+         d->grad_deriv.width == 2 * kRG + 1 && d->grad_deriv.k[kRG] == 0.0f && kDC == kRG &&
          (d->nlevels == 1 || (d->nlevels == 2 && d->subsampling == kSS && d->pyr.width == 2 * kRP + 1));
 }
 
@@ -3338,6 +3364,7 @@ int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc
 #ifdef KLT_TRACK_PROF
   bb.prof = c->prof;
 #endif
+  bb.count = c->d_trk_count;
   const TrkFramesArgs &b2 = bb;
   TrkArgs aa = a;
   aa.merge_res = c->track_merge;
@@ -3493,6 +3520,7 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
   }
   hipFree(c->d_perm);
   hipFree(c->d_count);
+  hipFree(c->d_trk_count);
   if (c->cstream) {
     hipStreamSynchronize(c->cstream);
     hipStreamDestroy(c->cstream);
@@ -3666,6 +3694,38 @@ KLT_API int klt_hip_set_pyr_l0(klt_hip_ctx *c, int mode, int strip_steps) {
 KLT_API int klt_hip_set_track_merge(klt_hip_ctx *c, int on) {
   if (!c) return fail(c, "set_track_merge: null context");
   c->track_merge = on ? 1 : 0;
+  return 0;
+}
+
+KLT_API int klt_hip_set_track_count(klt_hip_ctx *c, int on) {
+  if (!c) return fail(c, "set_track_count: null context");
+  if (use_device(c)) return -1;
+  HIPCHK(c, hipDeviceSynchronize());  // no tracker launch still holds the old pointer
+  if (!on) {
+    hipFree(c->d_trk_count);
+    c->d_trk_count = nullptr;
+    return 0;
+  }
+  const size_t bytes = 2 * kCountSlots * sizeof(unsigned long long);
+  if (!c->d_trk_count) HIPCHK(c, hipMalloc((void **)&c->d_trk_count, bytes));
+  HIPCHK(c, hipMemset(c->d_trk_count, 0, bytes));
+  return 0;
+}
+
+KLT_API int klt_hip_get_track_count(klt_hip_ctx *c, unsigned long long *solves, unsigned long long *passes,
+                                    int reset) {
+  if (!c || !solves || !passes) return fail(c, "get_track_count: null argument");
+  if (!c->d_trk_count) return fail(c, "get_track_count: counting is off (klt_hip_set_track_count)");
+  if (use_device(c)) return -1;
+  unsigned long long h[2 * kCountSlots];
+  HIPCHK(c, hipDeviceSynchronize());  // every stream the tracker may have run on
+  HIPCHK(c, hipMemcpy(h, c->d_trk_count, sizeof h, hipMemcpyDeviceToHost));
+  *solves = *passes = 0;
+  for (int k = 0; k < kCountSlots; ++k) {
+    *solves += h[k];
+    *passes += h[kCountSlots + k];
+  }
+  if (reset) HIPCHK(c, hipMemset(c->d_trk_count, 0, sizeof h));
   return 0;
 }
 

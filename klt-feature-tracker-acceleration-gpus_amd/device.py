@@ -65,6 +65,8 @@ DEVICE_PROTOS = {
     "klt_hip_set_track_order": (C.c_int, [V, C.c_int]),
     "klt_hip_set_track_merge": (C.c_int, [V, C.c_int]),
     "klt_hip_set_track_patch": (C.c_int, [V, C.c_int]),
+    "klt_hip_set_track_count": (C.c_int, [V, C.c_int]),
+    "klt_hip_get_track_count": (C.c_int, [V, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong), C.c_int]),
     "klt_hip_set_pyr_l0": (C.c_int, [V, C.c_int, C.c_int]),
     "klt_hip_set_frames_overlap": (C.c_int, [V, C.c_int]),
     "klt_hip_set_path": (C.c_int, [V, C.c_int]),

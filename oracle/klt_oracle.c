@@ -641,6 +641,16 @@ enum { TRACKED = 0, NOT_FOUND = -1, SMALL_DET = -2, MAX_ITERATIONS = -3, OOB = -
 static int *g_iter_log = NULL;
 static int g_iter_feature = 0, g_iter_level = 0, g_iter_nlev = 0;
 ORC_EXPORT void orc_set_iter_log(int *buf) { g_iter_log = buf; }
+/* diagnostics: 2x2 systems formed (Newton loop bodies that reach
+   _solveEquation, trackFeatures.c:450, the SMALL_DET one included) since the
+   last reset; pins the device counter of klt_hip_set_track_count */
+static unsigned long long g_solves = 0;
+ORC_EXPORT unsigned long long orc_solve_count(int reset)
+{
+  const unsigned long long n = g_solves;
+  if (reset) g_solves = 0;
+  return n;
+}
 
 static int window_out(float x, float y, int hw, int hh, int nc, int nr)
 {
@@ -685,6 +695,7 @@ static int track_one(float x1, float y1, float *x2, float *y2, const orc_level *
     /* _solveEquation (:293-307) */
     {
       float det = gxx * gyy - gxy * gxy;
+      g_solves++;
       if (det < P->min_determinant) {
         status = SMALL_DET;
         break;

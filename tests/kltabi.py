@@ -247,6 +247,7 @@ def load_oracle() -> C.CDLL:
         "orc_taps_for_sigma": (C.c_int, [C.c_float, _FP, _IP, _FP, _IP]),
         "orc_reset_kernel_cache": (None, []),
         "orc_params_size": (C.c_int, []),
+        "orc_solve_count": (C.c_ulonglong, [C.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -220,10 +220,11 @@ def test_pipelined_generic_path_vs_oracle(gpu, oracle):
     assert np.array_equal(x.view(np.int32), X[:, 5].view(np.int32)) and np.array_equal(v, V[:, 5])
 
 
-def batch_sequence(gpu, frames, nfeat, chunks, setup=None, calls=None):
+def batch_sequence(gpu, frames, nfeat, chunks, setup=None, calls=None, counts=None):
     """Select on frames[0], then klt_hip_frames_begin + klt_hip_track_frames over
     frames[1:] (split into `calls` pieces, one chunk size per call), returning
-    the device feature table: row j = the list after frame j+1."""
+    the device feature table: row j = the list after frame j+1.  counts (a
+    list): the tracker's work counters (klt_hip_set_track_count) are appended."""
     from kltabi import fl_to_arrays, u8ptr
     from kltamd.device import D2H, H2D, PyrDesc, TrackDesc, check
     h, w = frames[0].shape
@@ -248,6 +249,8 @@ def batch_sequence(gpu, frames, nfeat, chunks, setup=None, calls=None):
     gpu.klt_amd_pyr_desc(tc, w, h, tc.contents.nPyramidLevels, 1, C.byref(pd))
     gpu.klt_amd_track_desc(tc, C.byref(td))
     check(gpu, ctx, gpu.klt_hip_frames_begin(ctx, C.byref(pd), dfr, w), "begin")
+    if counts is not None:
+        check(gpu, ctx, gpu.klt_hip_set_track_count(ctx, 1), "count on")
     calls = calls or [T]
     assert sum(calls) == T and len(chunks) == len(calls)
     j0 = 0
@@ -257,6 +260,11 @@ def batch_sequence(gpu, frames, nfeat, chunks, setup=None, calls=None):
                                                  nf, ch, dx, dy, dv, nfeat, tx + off, ty + off, tv + off,
                                                  nfeat), "frames")
         j0 += nf
+    if counts is not None:
+        solves, passes = C.c_ulonglong(0), C.c_ulonglong(0)
+        check(gpu, ctx, gpu.klt_hip_get_track_count(ctx, C.byref(solves), C.byref(passes), 1), "count")
+        counts += [solves.value, passes.value]
+        check(gpu, ctx, gpu.klt_hip_set_track_count(ctx, 0), "count off")
     X = np.empty((T, nfeat), np.float32)
     Y = np.empty((T, nfeat), np.float32)
     V = np.empty((T, nfeat), np.int32)
@@ -286,6 +294,24 @@ def test_batched_frames_vs_oracle(gpu, oracle, chunks, calls):
     X, Y, V = batch_sequence(gpu, frames, 1000, chunks, calls=calls)
     OX, OY, OV = OracleTracker(oracle).harness(frames, 1000, 12, first=frames[0])
     assert_table_equal(X, Y, V, OX, OY, OV)
+
+
+@pytest.mark.parametrize("merge", [1, 0])
+def test_track_counts_vs_oracle(gpu, oracle, merge, monkeypatch):
+    """klt_hip_set_track_count: the device's count of 2x2 systems formed equals
+    the oracle's Newton loop bodies (both levels, SMALL_DET included) over the
+    same sequence, with the deferred residue on and off; the gather passes are
+    at least one per system."""
+    monkeypatch.setenv("KLT_AMD_TRACK_MERGE", str(merge))  # read when the device context is created
+    frames = synth(gpu, 5150, 640, 480, 12)
+    counts = []
+    X, Y, V = batch_sequence(gpu, frames, 1000, [5], counts=counts)
+    oracle.orc_solve_count(1)
+    OX, OY, OV = OracleTracker(oracle).harness(frames, 1000, 12, first=frames[0])
+    assert_table_equal(X, Y, V, OX, OY, OV)
+    solves, passes = counts
+    assert solves == oracle.orc_solve_count(1) and solves > 0
+    assert passes >= solves
 
 
 def test_batched_frames_odd_size_and_1080p(gpu, oracle):

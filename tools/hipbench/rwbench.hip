@@ -6,11 +6,11 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
-template <bool RD, bool WR, bool TILED = false>
+template <bool RD, bool WR, bool TILED = false, bool XCD = true>
 __global__ __launch_bounds__(256) void k_tile(const unsigned char *src, float *out, int W, int H, int tiles_x,
                                               int tiles_y) {
   const int per = gridDim.x / 8;
-  const int t = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  const int t = XCD ? (blockIdx.x % 8) * per + blockIdx.x / 8 : blockIdx.x;
   if (t >= tiles_x * tiles_y) return;
   const int by = t / tiles_x, bx = t - by * tiles_x;
   const int C0 = bx * 64, R0 = by * 32, tid = threadIdx.x;
@@ -42,17 +42,17 @@ __global__ __launch_bounds__(256) void k_tile(const unsigned char *src, float *o
   }
 }
 
-template <bool RD, bool WR, bool TILED = false>
+template <bool RD, bool WR, bool TILED = false, bool XCD = true>
 void run(const unsigned char *s, float *d, int W, int H, int F, const char *name) {
   const int tx = W / 64, ty = H / 32, n = tx * ty;
   dim3 grid(8 * ((n + 7) / 8), 1, F);
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((k_tile<RD, WR, TILED>), grid, dim3(256), 0, 0, s, d, W, H, tx, ty);
+  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((k_tile<RD, WR, TILED, XCD>), grid, dim3(256), 0, 0, s, d, W, H, tx, ty);
   hipEventRecord(a);
   const int reps = 10;
-  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((k_tile<RD, WR, TILED>), grid, dim3(256), 0, 0, s, d, W, H, tx, ty);
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((k_tile<RD, WR, TILED, XCD>), grid, dim3(256), 0, 0, s, d, W, H, tx, ty);
   hipEventRecord(b);
   hipEventSynchronize(b);
   float ms;
@@ -75,6 +75,8 @@ int main() {
   run<true, false>(s, d, W, H, F, "read only");
   run<true, true, true>(s, d, W, H, F, "rw tiled");
   run<false, true, true>(s, d, W, H, F, "w tiled");
+  run<true, true, false, false>(s, d, W, H, F, "rw linear");
+  run<false, true, false, false>(s, d, W, H, F, "w linear");
   hipFree(s);
   hipFree(d);
   return 0;
