@@ -156,6 +156,12 @@ struct DefTaps {
 #ifndef KLT_L0_TH
 #define KLT_L0_TH 32
 #endif
+#ifndef KLT_L0_PRIO  // experiment: wave priority while a tile's u8 loads issue (0: off)
+#define KLT_L0_PRIO 0
+#endif
+#ifndef KLT_L0_PRIO_B  // 1: keep that priority through the smoothing rows pass
+#define KLT_L0_PRIO_B 0
+#endif
 namespace l0 {
 constexpr int RS = 2, RG = 3, RP = 10, SS = 4, TW = 64, TH = KLT_L0_TH;
 constexpr int UQ = 24;            // staged u8 dwords per row: global [C0-12, C0+84)
@@ -338,6 +344,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
   if (!STAGED) {
     constexpr int NA = UH * UQ, PER = (NA + kBlock - 1) / kBlock;
     uint32_t w[PER];
+    if (KLT_L0_PRIO) __builtin_amdgcn_s_setprio(KLT_L0_PRIO);  // experiment: loads issue ahead of other waves' work
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       // unconditional: items past NA reload the last dword and land in LDS
@@ -363,6 +370,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
       }
     }
     if (Def::on) def->flush(0);  // after this tile's loads: their wait does not cover these stores
+    if (KLT_L0_PRIO && !KLT_L0_PRIO_B) __builtin_amdgcn_s_setprio(0);
     static_assert(!U8 || PER * kBlock <= REG_A, "phase A spill-over stays inside region A");
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
@@ -455,6 +463,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     st4(t1 + r * PT + 4 * g, acc);
   }
   L0T_MARK(1);
+  if (KLT_L0_PRIO && KLT_L0_PRIO_B) __builtin_amdgcn_s_setprio(0);
   hook();
   if (Def::on) def->flush(1);
 
