@@ -156,6 +156,9 @@ struct DefTaps {
 #ifndef KLT_L0_TH
 #define KLT_L0_TH 32
 #endif
+#ifndef KLT_L0_X4  // interior tiles stage their u8 rows with 16-byte loads (0: dword loads)
+#define KLT_L0_X4 1
+#endif
 #ifndef KLT_L0_PRIO  // experiment: wave priority while a tile's u8 loads issue (0: off)
 #define KLT_L0_PRIO 0
 #endif
@@ -199,6 +202,9 @@ constexpr bool HSLAST = KLT_L0_HSLAST != 0;
 static_assert(!H4 || (TH * TW / 16 <= kBlock && TW % 16 == 0), "H4 items");
 constexpr int PU = KLT_L0_PU, PT = B8 ? 88 : 84, PI = KLT_L0_PI, PX = TW;
 constexpr int PUB = 24;                   // U8: staged row pitch in dwords (96 bytes)
+// interior tiles: one 16-byte chunk per thread covers the staged rows (k_pyr_l0 phase A)
+constexpr bool X4 = KLT_L0_X4 && U8 && UQ % 4 == 0 && (TH + 2 * RG + 2 * RS) * (UQ / 4) <= kBlock &&
+                    TH + 2 * RG + 2 * RS <= UH;
 constexpr int U_WORDS = U8 ? UH * PUB : UH * PU;
 constexpr int REG_A = U_WORDS > IH * PI ? U_WORDS : IH * PI;  // u during A-B, then img0 during C-D
 constexpr int REG_B = 2 * IH * PX;        // t1 during B-C, then tx|ty during D-E
@@ -341,7 +347,24 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
   float *ty = tx + IH * PX;
 
   // A. u8 tile + halo -> LDS; every load issued before the first is used
-  if (!STAGED) {
+  if constexpr (!STAGED && INT && X4 && !Def::on) {
+    // interior tile: one 16-byte load per thread, 6 per staged row at
+    // C0-12+16q (dword-aligned: vec_u8 guarantees a 4-byte pitch and base),
+    // rows R0-5 .. R0+36 -- the 42 rows any stored output reads.  Rows 42-43
+    // of the staging area keep stale bytes: they feed only img0 rows 38-39,
+    // which are computed for the 4-row blocks and never used.  Threads past
+    // the 252 chunks repeat the last one (same bytes, same LDS slot), so the
+    // loads stay branch-free.  rwbench: 16-byte loads move the tile's bytes
+    // in under half the time of dword loads.
+    constexpr int NQ = UQ / 4, NR = TH + 2 * RG + 2 * RS, NA = NR * NQ;
+    if (KLT_L0_PRIO) __builtin_amdgcn_s_setprio(KLT_L0_PRIO);
+    const int i = min(tid, NA - 1);
+    const int r = i / NQ, q = i - r * NQ;
+    const uint4 c = *reinterpret_cast<const uint4 *>(src + (unsigned)((R0 - RG - RS + r) * spitch + C0 - 12 + 16 * q));
+    if (KLT_L0_PRIO && !KLT_L0_PRIO_B) __builtin_amdgcn_s_setprio(0);
+    *reinterpret_cast<uint4 *>(reinterpret_cast<uint32_t *>(u) + r * PUB + 4 * q) = c;
+    L0T_MARK(0);
+  } else if (!STAGED) {
     constexpr int NA = UH * UQ, PER = (NA + kBlock - 1) / kBlock;
     uint32_t w[PER];
     if (KLT_L0_PRIO) __builtin_amdgcn_s_setprio(KLT_L0_PRIO);  // experiment: loads issue ahead of other waves' work

@@ -6,7 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
-template <bool RD, bool WR, bool TILED = false, bool XCD = true>
+template <bool RD, bool WR, bool TILED = false, bool XCD = true, bool V4 = false>
 __global__ __launch_bounds__(256) void k_tile(const unsigned char *src, float *out, int W, int H, int tiles_x,
                                               int tiles_y) {
   const int per = gridDim.x / 8;
@@ -19,7 +19,16 @@ __global__ __launch_bounds__(256) void k_tile(const unsigned char *src, float *o
   out += blockIdx.z * plane * 4;
   __shared__ unsigned u[44 * 24];
   unsigned acc = 0;
-  if (RD) {
+  if (RD && V4) {
+    // 16-byte loads at dword-aligned offsets: 42 rows x 6 per tile, one per thread
+    if (tid < 42 * 6) {
+      const int r = tid / 6, q = tid - r * 6;
+      const int x = min(max(C0 - 12 + 16 * q, 0), W - 16), y = min(max(R0 - 5 + r, 0), H - 1);
+      *reinterpret_cast<uint4 *>(&u[r * 24 + 4 * q]) = *reinterpret_cast<const uint4 *>(src + (long)y * W + x);
+    }
+    __syncthreads();
+    acc = u[tid] ^ u[tid + 512];
+  } else if (RD) {
     for (int i = tid; i < 44 * 24; i += 256) {
       const int r = i / 24, q = i - r * 24;
       const int x = min(max(C0 - 12 + 4 * q, 0), W - 4), y = min(max(R0 - 5 + r, 0), H - 1);
@@ -42,17 +51,17 @@ __global__ __launch_bounds__(256) void k_tile(const unsigned char *src, float *o
   }
 }
 
-template <bool RD, bool WR, bool TILED = false, bool XCD = true>
+template <bool RD, bool WR, bool TILED = false, bool XCD = true, bool V4 = false>
 void run(const unsigned char *s, float *d, int W, int H, int F, const char *name) {
   const int tx = W / 64, ty = H / 32, n = tx * ty;
   dim3 grid(8 * ((n + 7) / 8), 1, F);
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((k_tile<RD, WR, TILED, XCD>), grid, dim3(256), 0, 0, s, d, W, H, tx, ty);
+  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((k_tile<RD, WR, TILED, XCD, V4>), grid, dim3(256), 0, 0, s, d, W, H, tx, ty);
   hipEventRecord(a);
   const int reps = 10;
-  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((k_tile<RD, WR, TILED, XCD>), grid, dim3(256), 0, 0, s, d, W, H, tx, ty);
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((k_tile<RD, WR, TILED, XCD, V4>), grid, dim3(256), 0, 0, s, d, W, H, tx, ty);
   hipEventRecord(b);
   hipEventSynchronize(b);
   float ms;
@@ -77,6 +86,9 @@ int main() {
   run<false, true, true>(s, d, W, H, F, "w tiled");
   run<true, true, false, false>(s, d, W, H, F, "rw linear");
   run<false, true, false, false>(s, d, W, H, F, "w linear");
+  run<true, true, false, true, true>(s, d, W, H, F, "rw x4 loads");
+  run<true, false, false, true, true>(s, d, W, H, F, "r x4 loads");
+  run<true, true>(s, d, W, H, F, "read+write");
   hipFree(s);
   hipFree(d);
   return 0;
