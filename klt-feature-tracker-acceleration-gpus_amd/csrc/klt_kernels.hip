@@ -2991,8 +2991,13 @@ struct klt_hip_ctx {
   size_t hs_cap = 0;
   float *d_tmp[2] = {nullptr, nullptr};
   size_t tmp_cap[2] = {0, 0};
-  float *d_fx = nullptr, *d_fy = nullptr;
+  // host-array tracking (klt.h calls): x | y | val in one device block and one
+  // pinned host block, so a call moves its feature list in one copy each way
+  float *d_fx = nullptr, *d_fy = nullptr;  // views into d_feat
   int *d_fv = nullptr;
+  float *d_feat = nullptr, *h_feat = nullptr;
+  size_t upload_piece = 512 << 10;  // klt_hip_upload_frame: bytes per host-copy/DMA piece (0: whole frame)
+  int feat_zero_copy = 1;   // klt_hip_track on host lists: kernels use h_feat in place (0: copies)
   size_t f_cap = 0;
   int *d_eig = nullptr;
   size_t eig_cap = 0;
@@ -3506,6 +3511,9 @@ KLT_API int klt_hip_device_count(void) {
 KLT_API klt_hip_ctx *klt_hip_ctx_create(int device) {
   klt_hip_ctx *c = new klt_hip_ctx();
   if (const char *m = getenv("KLT_AMD_TRACK_MERGE")) c->track_merge = atoi(m) != 0;  // A/B switch for tools
+  if (const char *m = getenv("KLT_AMD_UPLOAD_PIECE_KB")) c->upload_piece = (size_t)atol(m) * 1024;  // A/B switch
+  if (const char *m = getenv("KLT_AMD_FEAT_ZERO_COPY")) c->feat_zero_copy = atoi(m) != 0;          // A/B switch
+  if (const char *m = getenv("KLT_AMD_TRACK_ORDER")) c->track_order = atoi(m) != 0;                // A/B switch
   if (device < 0) {
     if (hipGetDevice(&device) != hipSuccess) device = 0;
   }
@@ -3563,9 +3571,8 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
   }
   hipFree(c->d_ring);
   hipFree(c->d_hs);
-  hipFree(c->d_fx);
-  hipFree(c->d_fy);
-  hipFree(c->d_fv);
+  hipFree(c->d_feat);
+  if (c->h_feat) hipHostFree(c->h_feat);
   hipFree(c->d_eig);
   hipFree(c->d_l0q_dummy);
   for (void *p : {(void *)c->d_aff_store, (void *)c->d_aff, (void *)c->d_xp, (void *)c->d_yp, (void *)c->d_astage,
@@ -3625,8 +3632,13 @@ KLT_API int klt_hip_upload_frame(klt_hip_ctx *c, int buf, const unsigned char *h
   }
   // the previous copy out of this bounce buffer must have finished
   HIPCHK(c, hipEventSynchronize(c->u8_done[buf]));
-  memcpy(c->h_u8[buf], host, n);
-  HIPCHK(c, hipMemcpyAsync(c->d_u8[buf], c->h_u8[buf], n, hipMemcpyHostToDevice, c->stream));
+  // in pieces: the DMA of piece k runs while the host copies piece k+1
+  const size_t piece = c->upload_piece > 0 ? c->upload_piece : n;
+  for (size_t o = 0; o < n; o += piece) {
+    const size_t m = n - o < piece ? n - o : piece;
+    memcpy(c->h_u8[buf] + o, host + o, m);
+    HIPCHK(c, hipMemcpyAsync(c->d_u8[buf] + o, c->h_u8[buf] + o, m, hipMemcpyHostToDevice, c->stream));
+  }
   HIPCHK(c, hipEventRecord(c->u8_done[buf], c->stream));
   c->u8_w[buf] = ncols;
   c->u8_h[buf] = nrows;
@@ -3800,6 +3812,52 @@ KLT_API int klt_hip_download_level(klt_hip_ctx *c, int s, int l, int which, floa
   return 0;
 }
 
+// A host feature list packed into the context's pinned block h_feat
+// (x | y | val).  The kernels of the per-call path read and write it in place
+// (pinned host memory is mapped into the device's address space): no copy
+// engine, no copy-to-kernel handoff.  The previous call is complete (every
+// host-list call ends with a stream synchronize).
+int feat_pack(klt_hip_ctx *c, const float *x, const float *y, const int *val, int n) {
+  if (n <= 0) return 0;
+  if ((size_t)n > c->f_cap) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(c->d_feat);
+    if (c->h_feat) hipHostFree(c->h_feat);
+    c->d_feat = c->h_feat = nullptr;
+    c->d_fx = c->d_fy = nullptr;
+    c->d_fv = nullptr;
+    c->f_cap = 0;
+    HIPCHK(c, hipMalloc((void **)&c->d_feat, 3 * sizeof(float) * n));
+    HIPCHK(c, hipHostMalloc((void **)&c->h_feat, 3 * sizeof(float) * n, hipHostMallocDefault));
+    c->f_cap = (size_t)n;
+  }
+  c->d_fx = c->d_feat;
+  c->d_fy = c->d_feat + n;
+  c->d_fv = reinterpret_cast<int *>(c->d_feat + 2 * (size_t)n);
+  memcpy(c->h_feat, x, sizeof(float) * n);
+  memcpy(c->h_feat + n, y, sizeof(float) * n);
+  memcpy(c->h_feat + 2 * (size_t)n, val, sizeof(int) * n);
+  return 0;
+}
+
+// ... or copied into the device block (d_fx | d_fy | d_fv) in one H2D copy
+int feat_stage_in(klt_hip_ctx *c, const float *x, const float *y, const int *val, int n) {
+  if (n <= 0) return 0;
+  if (feat_pack(c, x, y, val, n)) return -1;
+  HIPCHK(c, hipMemcpyAsync(c->d_feat, c->h_feat, 3 * sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+  return 0;
+}
+
+// the pinned block back into the host list once the stream is done with it
+int feat_unpack(klt_hip_ctx *c, float *x, float *y, int *val, int n) {
+  if (n <= 0) return 0;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  memcpy(x, c->h_feat, sizeof(float) * n);
+  memcpy(y, c->h_feat + n, sizeof(float) * n);
+  memcpy(val, c->h_feat + 2 * (size_t)n, sizeof(int) * n);
+  return 0;
+}
+
 KLT_API int klt_hip_track(klt_hip_ctx *c, int s1, int s2, const klt_hip_track_desc *d, float *x, float *y,
                           int *val, int n, int on_device) {
   if (!c || !d) return fail(c, "track: null argument");
@@ -3822,25 +3880,17 @@ KLT_API int klt_hip_track(klt_hip_ctx *c, int s1, int s2, const klt_hip_track_de
   float *x_d = x, *y_d = y;
   int *v_d = val;
   if (!on_device) {
-    if ((size_t)n > c->f_cap) {
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      hipFree(c->d_fx);
-      hipFree(c->d_fy);
-      hipFree(c->d_fv);
-      c->d_fx = c->d_fy = nullptr;
-      c->d_fv = nullptr;
-      c->f_cap = 0;
-      HIPCHK(c, hipMalloc((void **)&c->d_fx, sizeof(float) * n));
-      HIPCHK(c, hipMalloc((void **)&c->d_fy, sizeof(float) * n));
-      HIPCHK(c, hipMalloc((void **)&c->d_fv, sizeof(int) * n));
-      c->f_cap = (size_t)n;
+    if (c->feat_zero_copy) {
+      if (feat_pack(c, x, y, val, n)) return -1;
+      x_d = c->h_feat;
+      y_d = c->h_feat + n;
+      v_d = reinterpret_cast<int *>(c->h_feat + 2 * (size_t)n);
+    } else {
+      if (feat_stage_in(c, x, y, val, n)) return -1;
+      x_d = c->d_fx;
+      y_d = c->d_fy;
+      v_d = c->d_fv;
     }
-    x_d = c->d_fx;
-    y_d = c->d_fy;
-    v_d = c->d_fv;
-    HIPCHK(c, hipMemcpyAsync(x_d, x, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(y_d, y, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(v_d, val, sizeof(int) * n, hipMemcpyHostToDevice, c->stream));
   }
   {
     // one frame through the batched kernels: frame 0 tracks a.A -> a.B, no table
@@ -3850,10 +3900,9 @@ KLT_API int klt_hip_track(klt_hip_ctx *c, int s1, int s2, const klt_hip_track_de
     if (track_frames_launch(c, c->stream, d, a, b, x_d, y_d, v_d, n)) return -1;
   }
   if (!on_device) {
-    HIPCHK(c, hipMemcpyAsync(x, x_d, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(y, y_d, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(val, v_d, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (!c->feat_zero_copy)
+      HIPCHK(c, hipMemcpyAsync(c->h_feat, c->d_feat, 3 * sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+    return feat_unpack(c, x, y, val, n);
   }
   return 0;
 }
@@ -3935,22 +3984,7 @@ KLT_API int klt_hip_track_affine(klt_hip_ctx *c, int s1, int s2, const klt_hip_t
   HIPCHK(c, hipMemcpyAsync(c->d_yp, y, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->d_aff, aff, sizeof(float) * n * 6, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->d_astate, state, sizeof(int) * n, hipMemcpyHostToDevice, c->stream));
-  if ((size_t)n > c->f_cap) {
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    hipFree(c->d_fx);
-    hipFree(c->d_fy);
-    hipFree(c->d_fv);
-    c->d_fx = c->d_fy = nullptr;
-    c->d_fv = nullptr;
-    c->f_cap = 0;
-    HIPCHK(c, hipMalloc((void **)&c->d_fx, sizeof(float) * n));
-    HIPCHK(c, hipMalloc((void **)&c->d_fy, sizeof(float) * n));
-    HIPCHK(c, hipMalloc((void **)&c->d_fv, sizeof(int) * n));
-    c->f_cap = (size_t)n;
-  }
-  HIPCHK(c, hipMemcpyAsync(c->d_fx, x, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->d_fy, y, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->d_fv, val, sizeof(int) * n, hipMemcpyHostToDevice, c->stream));
+  if (feat_stage_in(c, x, y, val, n)) return -1;
   if (klt_hip_track(c, s1, s2, d, c->d_fx, c->d_fy, c->d_fv, n, 1)) return -1;
   const Slot &A = c->slot[s1], &B = c->slot[s2];
   AffArgs a;
