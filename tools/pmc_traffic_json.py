@@ -5,10 +5,10 @@ frame of the pyramid pass (k_pyr_l0 + k_pyr_l1), from the batched launches.
 FETCH_SIZE / WRITE_SIZE are in KiB (WRITE_SIZE checked against k_synth's known
 output).  gfx950 FETCH_SIZE counts half of the bytes of 16-byte-per-lane reads
 (MI355X_MICROARCH.md, HBM): k_pyr_l1 reads hs that way, so its FETCH is
-doubled.  k_pyr_l0 reads the u8 frame 4 bytes per lane (a width the guide
-leaves uncalibrated); its raw FETCH comes out at 0.56x the frame's own bytes,
-below the least it can read, so the same half-count holds and it is doubled
-too (raw values kept in the JSON).
+doubled.  k_pyr_l0's interior tiles read the u8 frame 16 bytes per lane
+(since v14; before, 4 bytes per lane, where its raw FETCH came out at 0.56x
+the frame's own bytes, below the least it can read); it is doubled too (raw
+values kept in the JSON).
 usage: python tools/pmc_traffic_json.py gpurun_out/<tag> WIDTH HEIGHT [out.json]
 """
 import csv
