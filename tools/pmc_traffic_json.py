@@ -47,8 +47,8 @@ res = {
     "pass_algorithmic_bytes_per_frame": px * 13 + W1 * H1 * 12,
     "raw_fetch_kib_per_frame": {"k_pyr_l0": avg[("l0", "FETCH_SIZE")] / 1024,
                                 "k_pyr_l1": avg[("l1", "FETCH_SIZE")] / 1024},
-    "note": "FETCH doubled for both kernels (gfx950 half-count; for k_pyr_l0's 4-B/lane reads inferred from "
-            "raw FETCH < the frame's own bytes); includes the sigma-3.6 row-pass round trip (hs written by "
+    "note": "FETCH doubled for both kernels (gfx950 half-count; k_pyr_l0's interior tiles read 16 B/lane "
+            "since v14, the guide's calibrated case, its edge tiles 4 B/lane); includes the sigma-3.6 row-pass round trip (hs written by "
             "k_pyr_l0, read by k_pyr_l1) that the pass-level algorithmic figure excludes; FETCH counts "
             "Infinity-Cache hits too",
 }
