@@ -24,7 +24,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "klt_hip.h"
@@ -2973,6 +2977,68 @@ struct PrevRef {
   int slot = KLT_HIP_MAX_SLOTS;  // the batch seed slot unless klt_hip_frames_begin_slot
 };
 
+// Host copies of caller frames into pinned staging (klt_hip_track_frames_host):
+// a few worker threads and the calling thread split a group of frames into
+// 512 KB pieces.  Every worker takes part in every generation, and copy()
+// returns only when all of them have finished it, so no worker can still be
+// reading the job list when the caller refills it for the next group.
+struct CopyPool {
+  struct Job {
+    unsigned char *dst;
+    const unsigned char *src;
+    size_t n;
+  };
+  std::vector<std::thread> th;
+  std::mutex m;
+  std::condition_variable cv;
+  std::vector<Job> jobs;
+  std::atomic<size_t> next{0};
+  std::atomic<int> finished{0};
+  unsigned gen = 0;
+  bool stop = false;
+
+  explicit CopyPool(int workers) {
+    for (int i = 0; i < workers; ++i) th.emplace_back([this] { worker(); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> l(m);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto &t : th) t.join();
+  }
+  void run() {
+    for (size_t i; (i = next.fetch_add(1)) < jobs.size();) memcpy(jobs[i].dst, jobs[i].src, jobs[i].n);
+  }
+  void worker() {
+    unsigned seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> l(m);
+        cv.wait(l, [&] { return stop || gen != seen; });
+        if (stop) return;
+        seen = gen;
+      }
+      run();
+      finished.fetch_add(1);
+    }
+  }
+  void copy() {  // jobs filled by the caller
+    {
+      std::lock_guard<std::mutex> l(m);
+      next = 0;
+      finished = 0;
+      ++gen;
+    }
+    cv.notify_all();
+    run();
+    while (finished.load() < (int)th.size()) std::this_thread::yield();
+  }
+};
+
+constexpr int kStageGroup = 8;  // frames per staging group; two groups of pinned slots
+
 struct klt_hip_ctx {
   int device = 0;
   hipStream_t own = nullptr;
@@ -3030,6 +3096,14 @@ struct klt_hip_ctx {
   size_t ring_cap = 0;
   hipStream_t cstream = nullptr;
   hipEvent_t ev_ring_ready[2] = {}, ev_ring_free[2] = {};
+  // klt_hip_track_frames_host: pinned staging for the caller's pageable
+  // frames, 2 groups of kStageGroup slots (host copy by the pool, then DMA)
+  CopyPool *pool = nullptr;
+  int copy_threads = 4;            // pool workers besides the caller; 0: runtime staging (hipMemcpyAsync from pageable)
+  unsigned char *h_stage = nullptr;
+  size_t stage_frame = 0;          // bytes per slot
+  hipEvent_t ev_stage[2] = {};     // DMA out of group g done
+  int stage_next = 0;
 #ifdef KLT_TRACK_PROF
   unsigned long long *prof = nullptr;
 #endif
@@ -3513,6 +3587,7 @@ KLT_API klt_hip_ctx *klt_hip_ctx_create(int device) {
   if (const char *m = getenv("KLT_AMD_TRACK_MERGE")) c->track_merge = atoi(m) != 0;  // A/B switch for tools
   if (const char *m = getenv("KLT_AMD_UPLOAD_PIECE_KB")) c->upload_piece = (size_t)atol(m) * 1024;  // A/B switch
   if (const char *m = getenv("KLT_AMD_FEAT_ZERO_COPY")) c->feat_zero_copy = atoi(m) != 0;          // A/B switch
+  if (const char *m = getenv("KLT_AMD_COPY_THREADS")) c->copy_threads = atoi(m) > 0 ? atoi(m) : 0;  // A/B switch
   if (const char *m = getenv("KLT_AMD_TRACK_ORDER")) c->track_order = atoi(m) != 0;                // A/B switch
   if (device < 0) {
     if (hipGetDevice(&device) != hipSuccess) device = 0;
@@ -3570,6 +3645,10 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
     if (c->ev_ring_free[k]) hipEventDestroy(c->ev_ring_free[k]);
   }
   hipFree(c->d_ring);
+  delete c->pool;
+  if (c->h_stage) hipHostFree(c->h_stage);
+  for (int k = 0; k < 2; ++k)
+    if (c->ev_stage[k]) hipEventDestroy(c->ev_stage[k]);
   hipFree(c->d_hs);
   hipFree(c->d_feat);
   if (c->h_feat) hipHostFree(c->h_feat);
@@ -4294,16 +4373,49 @@ KLT_API int klt_hip_track_frames_host(klt_hip_ctx *c, const klt_hip_pyr_desc *pd
       HIPCHK(c, hipEventCreateWithFlags(&c->ev_ring_free[k], hipEventDisableTiming));
     }
   }
+  if (c->copy_threads > 0 && (!c->pool || c->stage_frame < (size_t)fb)) {
+    if (c->h_stage) {
+      for (int k = 0; k < 2; ++k) HIPCHK(c, hipEventSynchronize(c->ev_stage[k]));
+      HIPCHK(c, hipHostFree(c->h_stage));
+      c->h_stage = nullptr;
+    }
+    HIPCHK(c, hipHostMalloc((void **)&c->h_stage, (size_t)2 * kStageGroup * fb, hipHostMallocDefault));
+    c->stage_frame = (size_t)fb;
+    for (int k = 0; k < 2; ++k)
+      if (!c->ev_stage[k]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_stage[k], hipEventDisableTiming));
+    if (!c->pool) c->pool = new CopyPool(c->copy_threads);
+  }
   // the ring may still be read by earlier work on the context stream
   HIPCHK(c, hipEventRecord(c->ev_ring_free[0], c->stream));
   HIPCHK(c, hipEventRecord(c->ev_ring_free[1], c->stream));
   auto upload = [&](int j0, int k) -> int {
     const int nf = F < nframes - j0 ? F : nframes - j0;
     HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_ring_free[k], 0));
-    for (int f = 0; f < nf; ++f) {
+    for (int f = 0; f < nf; ++f)
       if (!frames[j0 + f]) return fail(c, "track_frames_host: frame %d is NULL", j0 + f);
-      HIPCHK(c, hipMemcpyAsync(c->d_ring + (size_t)(k * F + f) * fb, frames[j0 + f], (size_t)fb,
+    if (!c->pool) {
+      for (int f = 0; f < nf; ++f)
+        HIPCHK(c, hipMemcpyAsync(c->d_ring + (size_t)(k * F + f) * fb, frames[j0 + f], (size_t)fb,
+                                 hipMemcpyHostToDevice, c->cstream));
+    }
+    for (int g0 = 0; c->pool && g0 < nf; g0 += kStageGroup) {
+      // a group of frames: wait until this group's slots are out of their
+      // last DMA, copy in parallel, then one DMA per frame
+      const int ng = kStageGroup < nf - g0 ? kStageGroup : nf - g0;
+      const int sg = c->stage_next;
+      c->stage_next ^= 1;
+      HIPCHK(c, hipEventSynchronize(c->ev_stage[sg]));
+      unsigned char *slots = c->h_stage + (size_t)sg * kStageGroup * fb;
+      const size_t piece = 512 << 10;
+      c->pool->jobs.clear();
+      for (int f = 0; f < ng; ++f)
+        for (size_t o = 0; o < (size_t)fb; o += piece)
+          c->pool->jobs.push_back({slots + (size_t)f * fb + o, frames[j0 + g0 + f] + o,
+                                   (size_t)fb - o < piece ? (size_t)fb - o : piece});
+      c->pool->copy();
+      HIPCHK(c, hipMemcpyAsync(c->d_ring + (size_t)(k * F + g0) * fb, slots, (size_t)ng * fb,
                                hipMemcpyHostToDevice, c->cstream));
+      HIPCHK(c, hipEventRecord(c->ev_stage[sg], c->cstream));
     }
     HIPCHK(c, hipEventRecord(c->ev_ring_ready[k], c->cstream));
     return 0;
