@@ -274,6 +274,12 @@ int klt_hip_get_timing(klt_hip_ctx *ctx, klt_hip_timing *out);
 /* numerics self-checks used by the tests: f64 sqrt and f32 divide on device */
 int klt_hip_selftest_sqrt(klt_hip_ctx *ctx, const double *in, double *out, int n);
 int klt_hip_selftest_div(klt_hip_ctx *ctx, const float *a, const float *b, float *out, int n);
+/* host-only self-check of the copy pool behind klt_hip_track_frames_host's
+   pinned staging: `rounds` back-to-back groups of pieces (sizes and offsets
+   varying per round, up to max_bytes) copied by `workers` threads plus the
+   caller, each verified byte for byte.  0 on success, else the failing round
+   + 1.  Needs no device. */
+int klt_hip_selftest_copy_pool(int workers, int rounds, size_t max_bytes);
 
 #ifdef __cplusplus
 }

@@ -4566,6 +4566,30 @@ KLT_API int klt_hip_selftest_sqrt(klt_hip_ctx *c, const double *in, double *out,
   return 0;
 }
 
+KLT_API int klt_hip_selftest_copy_pool(int workers, int rounds, size_t max_bytes) {
+  if (workers < 0 || rounds < 0 || max_bytes < 1) return -1;
+  std::vector<unsigned char> src(max_bytes), dst(max_bytes);
+  CopyPool pool(workers);
+  unsigned long long r64 = 0x9E3779B97F4A7C15ull;
+  auto rnd = [&]() {
+    r64 ^= r64 << 13;
+    r64 ^= r64 >> 7;
+    r64 ^= r64 << 17;
+    return r64;
+  };
+  for (int r = 0; r < rounds; ++r) {
+    const size_t n = 1 + rnd() % max_bytes;
+    const size_t piece = 1 + rnd() % (n < 65536 ? n : 65536);
+    for (size_t i = 0; i < n; ++i) src[i] = (unsigned char)(rnd() >> 29);
+    memset(dst.data(), 0, n);
+    pool.jobs.clear();
+    for (size_t o = 0; o < n; o += piece) pool.jobs.push_back({dst.data() + o, src.data() + o, n - o < piece ? n - o : piece});
+    pool.copy();
+    if (memcmp(dst.data(), src.data(), n) != 0) return r + 1;
+  }
+  return 0;
+}
+
 KLT_API int klt_hip_selftest_div(klt_hip_ctx *c, const float *a, const float *b, float *out, int n) {
   if (use_device(c)) return -1;
   float *d = nullptr;

@@ -91,6 +91,7 @@ DEVICE_PROTOS = {
     "klt_hip_get_timing": (C.c_int, [V, C.POINTER(Timing)]),
     "klt_hip_selftest_sqrt": (C.c_int, [V, DP, DP, C.c_int]),
     "klt_hip_selftest_div": (C.c_int, [V, FP, FP, FP, C.c_int]),
+    "klt_hip_selftest_copy_pool": (C.c_int, [C.c_int, C.c_int, C.c_size_t]),
     # klt_api.c hooks
     "klt_amd_device_context": (V, [V]),
     "klt_amd_pyr_desc": (None, [V, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(PyrDesc)]),

@@ -144,3 +144,12 @@ def test_no_gpu_path_fails_loudly():
     if r.returncode == 3:
         pytest.skip("a GPU is visible")
     assert r.returncode == 1 and "KLT Error" in r.stderr, (r.returncode, r.stderr[-500:])
+
+
+@pytest.mark.parametrize("workers", [0, 1, 3, 4, 8])
+def test_copy_pool_selftest(amd, workers):
+    """Host-only: the copy pool behind KLTTrackSequence's pinned staging copies
+    every byte of many back-to-back groups (random sizes and piece lengths),
+    with the job list refilled between groups while the workers are parked."""
+    assert amd.klt_hip_selftest_copy_pool(workers, 400, 1 << 20) == 0
+    assert amd.klt_hip_selftest_copy_pool(workers, 2000, 4096) == 0
