@@ -61,8 +61,13 @@ def parse():
     p.add_argument("--no-4k", action="store_true", help="skip the 4K pyramid-pass roofline line (rank 0, N=1)")
     p.add_argument("--reduction", choices=["exact", "fast"], default="exact")
     p.add_argument("--chunk", type=int, default=None,
-                   help="frames per batched pyramid/track launch (klt_hip_track_frames; default 64, sharded 32); "
-                        "0 = the per-frame pipelined path (klt_hip_track_sequence)")
+                   help="frames per batched pyramid/track launch (klt_hip_track_frames; default 64, sharded 32; "
+                        "capped at ceil(steps/2) so that the timed region always holds >= 2 chunks and the "
+                        "overlapped schedule really runs); 0 = the per-frame pipelined path (klt_hip_track_sequence)")
+    p.add_argument("--api-frames", type=int, default=200,
+                   help="host frames for the klt.h API legs (KLTTrackFeatures per call, KLTTrackSequence); "
+                        "rank 0, N=1; 0 = skip")
+    p.add_argument("--no-fast", action="store_true", help="skip the fast (wave-shuffle) reduction replay")
     p.add_argument("--serial", action="store_true",
                    help="build and track on one stream; default: chunk c+1's pyramids are built on a second "
                         "stream while chunk c is tracked (they fill the CUs the tracker's last waves leave idle)")
@@ -74,6 +79,9 @@ def parse():
                          ("features", 5000, 20000), ("seed", 1080, 2160), ("chunk", 64, 32)):
         if getattr(a, k) is None:
             setattr(a, k, shd if sharded else dflt)
+    a.chunk_requested = a.chunk
+    if a.chunk > 0 and a.steps > 0:
+        a.chunk = min(a.chunk, max(1, -(-a.steps // 2)))  # >= 2 chunks in the timed region
     return a
 
 
@@ -196,6 +204,7 @@ def main() -> None:
     check(lib, ctx, lib.klt_hip_get_timing(ctx, C.byref(tm)), "timing")
     lib.klt_hip_set_timing(ctx, 0)
     tracker = None
+    exact_tab = [t[t_start - 1:t_start - 1 + args.steps].clone() for t in tab]
     if args.chunk > 0:
         # tracker work counters (Newton iterations, gather passes) in a replay
         # of their own, so that neither timed run carries the counting atomics
@@ -209,6 +218,13 @@ def main() -> None:
         # feature-frames: features live when frame j starts (table row j-1 holds the list after j-1)
         ff = int((tab[2][t_start - 1:t_start - 1 + args.steps] >= 0).sum().item())
         tracker = tracker_line(solves.value, passes.value, ff, tm)
+
+    fast = None
+    if args.chunk > 0 and args.reduction == "exact" and not args.no_fast and rank == 0:
+        # the same timed region with the wave-shuffle reduction (KLT_HIP_FAST):
+        # its own wall clock, then a one-stream replay for the tracker's events
+        fast = fast_leg(lib, ctx, td, tab, exact_tab, xs, ys, vs, x, y, v, build0, run, t_start, args)
+        check(lib, ctx, lib.klt_hip_set_frames_overlap(ctx, 0 if args.serial else 1), "overlap")
 
     dt_max = dt
     if world > 1:
@@ -246,10 +262,12 @@ def main() -> None:
         "dtype": "f32",
         "data": f"synthetic: include/klt_synth.h value-noise frames, (0.7,0.3) px/frame, seed {args.seed}+rank",
         "config": {"workload": f"{W}x{H}, {NF} features, sequential KLTTrackFeatures pass + KLTStoreFeatureList "
-                               f"per frame, {nframes} frames per GPU (BASELINE config 3; config 5 at N>1)",
-                   "chunk": args.chunk,
-                   "schedule": "one stream" if args.serial else
-                               "pyramids of chunk c+1 on a second stream while chunk c is tracked",
+                               f"per frame, {nframes} frames per GPU (BASELINE config 3; config 5 at N>1); "
+                               "device-resident: frames in HBM before timing, features and table stay on "
+                               "the device (the API-inclusive figure is the `api` key)",
+                   "chunk": args.chunk, "chunk_requested": args.chunk_requested,
+                   "launches_timed": (-(-args.steps // args.chunk)) if args.chunk > 0 else args.steps,
+                   "schedule": schedule_name(args),
                    "resolution": f"{W}x{H}", "features": NF, "frames": nframes,
                    "parallelism": "independent sequence per GPU" if world > 1 else "single GPU",
                    "reduction": args.reduction, "pyramid_path": "fused" if fused else "generic"},
@@ -259,8 +277,11 @@ def main() -> None:
         "frames_per_launch": fpl,
         "live_features": {"after_warmup": live_before, "at_end": live_after},
     }
+    result["value_kind"] = "device_only"
     if tracker:
         result["tracker"] = tracker
+    if fast:
+        result["fast"] = fast
     if pass_us:
         ach = pass_bytes / (pass_us * 1e-6) / 1e9
         result["roofline"] = {
@@ -288,6 +309,9 @@ def main() -> None:
 
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"], result["parity"] = cpu_leg(lib, frames, W, H, NF, args, tc, ctx, dev)
+
+    if rank == 0 and world == 1 and args.api_frames > 0:
+        result["api"] = api_leg(lib, frames, W, H, NF, args)
 
     lib.KLTFreeTrackingContext(tc)
     del frames, tab
@@ -441,6 +465,126 @@ def pass_4k(lib, dev, chunk=64, reps=2):
             "event_timing": "HIP events on the launch stream, one stream"}
 
 
+def schedule_name(args) -> str:
+    """What the timed region actually launched."""
+    if args.chunk == 0:
+        return "per-frame pipeline: frame t+1's pyramid on a second stream while frame t is tracked"
+    n = -(-args.steps // args.chunk)
+    if args.serial or n < 2:
+        return f"{n} chunk(s) of <= {args.chunk} frames, pyramids and tracker on one stream"
+    return (f"{n} chunks of <= {args.chunk} frames; pyramids of chunk c+1 on a second stream while chunk c is "
+            "tracked (the first chunk's pyramids are not overlapped)")
+
+
+def fast_leg(lib, ctx, td, tab, exact_tab, xs, ys, vs, x, y, v, build0, run, t_start, args):
+    """The timed region again with KLT_HIP_FAST: the tracker's five window
+    sums by a wave butterfly instead of the reference's sequential 49-term
+    sums (trackFeatures.c:241-248, :271-278).  Not bit-exact: reported with its
+    distance from the exact run over the same frames (val mismatches, max
+    |dx|,|dy| over cells tracked by both); the tolerance it is held to is
+    tests/test_gpu_long.py::test_fast_reduction_tolerance."""
+    import torch
+    from kltamd.device import FAST, Timing, check
+    saved = td.reduction
+    td.reduction = FAST
+    try:
+        x.copy_(xs); y.copy_(ys); v.copy_(vs)
+        build0(t_start - 1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(t_start, args.steps)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        ft = [t[t_start - 1:t_start - 1 + args.steps].clone() for t in tab]
+        # per-kernel events in a one-stream replay, as for the exact line
+        x.copy_(xs); y.copy_(ys); v.copy_(vs)
+        check(lib, ctx, lib.klt_hip_set_frames_overlap(ctx, 0), "overlap")
+        build0(t_start - 1)
+        lib.klt_hip_set_timing(ctx, 1)
+        run(t_start, args.steps)
+        tm = Timing()
+        check(lib, ctx, lib.klt_hip_get_timing(ctx, C.byref(tm)), "timing")
+        lib.klt_hip_set_timing(ctx, 0)
+    finally:
+        td.reduction = saved
+    ev, fv = exact_tab[2], ft[2]
+    both = (ev == 0) & (fv == 0)
+    dx = (exact_tab[0][both].double() - ft[0][both].double()).abs()
+    dy = (exact_tab[1][both].double() - ft[1][both].double()).abs()
+    return {"value": args.steps / dt, "unit": "frames/s", "ms_per_step": 1000.0 * dt / args.steps,
+            "k_track_us_per_frame": 1000.0 * tm.ms_track / tm.frames_track if tm.frames_track else None,
+            "vs_exact": {"cells": int(ev.numel()), "val_mismatches": int((ev != fv).sum().item()),
+                         "max_dx": float(dx.max().item()) if dx.numel() else 0.0,
+                         "max_dy": float(dy.max().item()) if dy.numel() else 0.0,
+                         "tracked_in_both": int(both.sum().item())},
+            "note": "wave-shuffle window sums (KLT_HIP_FAST); not bit-exact, see vs_exact"}
+
+
+def api_leg(lib, frames, W, H, NF, args):
+    """SURVEY 8(d)'s frames/sec through the klt.h API, host frames in pageable
+    memory, PCIe and the feature-list round trip inside the timed region:
+      per_call: one KLTTrackFeatures call per frame, wall clock around each
+                call as example3.c:61-63 times it; the first call (two pyramids)
+                is excluded, as the reference's steady state;
+      sequence: KLTTrackSequence over the same frames with a feature table
+                (the example3.c loop + KLTStoreFeatureList in one call;
+                klt_amd.h), after a warm-up call of its own for allocations.
+    Both select on frame 0 of the same sequence the device line tracks."""
+    import torch
+    from kltabi import fl_to_arrays
+    U8P = C.POINTER(C.c_ubyte)
+    n = min(args.api_frames, frames.shape[0] - 1)
+    host = [np.ascontiguousarray(frames[t].cpu().numpy()) for t in range(n + 1)]
+    torch.cuda.synchronize()
+    u8 = lambda a: a.ctypes.data_as(U8P)  # noqa: E731
+
+    tc = lib.KLTCreateTrackingContext()
+    tc.contents.sequentialMode = 1
+    fl = lib.KLTCreateFeatureList(NF)
+    lib.KLTSelectGoodFeatures(tc, u8(host[0]), W, H, fl)
+    lib.KLTTrackFeatures(tc, u8(host[0]), u8(host[1]), W, H, fl)  # builds both pyramids: not steady state
+    times = []
+    for t in range(2, n + 1):
+        a = time.perf_counter()
+        lib.KLTTrackFeatures(tc, u8(host[t - 1]), u8(host[t]), W, H, fl)
+        times.append(time.perf_counter() - a)
+    pc = fl_to_arrays(fl)
+    lib.KLTFreeFeatureList(fl)
+    lib.KLTFreeTrackingContext(tc)
+
+    arr = (U8P * (n + 1))(*[u8(a) for a in host])
+
+    def sequence(m):
+        tc = lib.KLTCreateTrackingContext()
+        tc.contents.sequentialMode = 1
+        fl = lib.KLTCreateFeatureList(NF)
+        lib.KLTSelectGoodFeatures(tc, u8(host[0]), W, H, fl)
+        ft = lib.KLTCreateFeatureTable(m, NF)
+        a = time.perf_counter()
+        lib.KLTTrackSequence(tc, arr, m + 1, W, H, fl, ft, 0)
+        dt = time.perf_counter() - a
+        out = fl_to_arrays(fl)
+        lib.KLTFreeFeatureTable(ft)
+        lib.KLTFreeFeatureList(fl)
+        lib.KLTFreeTrackingContext(tc)
+        return dt, out
+
+    sequence(min(n, 40))  # warm-up: staging, banks, copy pool
+    dt, sq = sequence(n)
+    same = all(np.array_equal(np.asarray(p).view(np.int32), np.asarray(q).view(np.int32)) for p, q in zip(pc, sq))
+    return {
+        "per_call": {"value": len(times) / sum(times), "unit": "frames/s", "calls": len(times),
+                     "us_per_call_median": 1e6 * float(np.median(times)),
+                     "region": "wall clock around each KLTTrackFeatures call (example3.c:61-63): host u8 frame "
+                               "H2D, both device kernels, feature list in/out"},
+        "sequence": {"value": n / dt, "unit": "frames/s", "frames": n,
+                     "region": "one KLTTrackSequence call over host frames 0..n with a KLT_FeatureTable "
+                               "(frame uploads, pyramids of frame 0..n, tracking, table download)"},
+        "frames": f"{W}x{H} u8 host frames (pageable numpy), {NF} features, seed {args.seed}",
+        "per_call_equals_sequence": bool(same),
+    }
+
+
 def tracker_line(solves, passes, feature_frames, tm):
     """the LK tracker is gather/latency and VALU bound, not an HBM
     roofline kernel; report its work rate as feature-iterations per second.
@@ -498,6 +642,7 @@ def cpu_leg(lib, frames, W, H, NF, args, tc, ctx, dev):
     host = [frames[t].cpu().numpy() for t in range(S)]
     kind = "reference" if REF_LIB.exists() else "port"
     rl = bind_klt(REF_LIB) if kind == "reference" else None
+    cols = []  # the list after every frame (example3.c's KLTStoreFeatureList columns)
     sel_t = time.perf_counter()
     if rl is not None:
         rl.KLTSetVerbosity(0)
@@ -508,14 +653,14 @@ def cpu_leg(lib, frames, W, H, NF, args, tc, ctx, dev):
         rl.KLTSelectGoodFeatures(rtc, u8(host[0]), W, H, fl)
         sel_s = time.perf_counter() - sel_t
         times, ctimes = [], []
+        lx, ly, lv = list_view(fl)
         for t in range(1, S):
             a, ca = time.perf_counter(), time.process_time()
             rl.KLTTrackFeatures(rtc, u8(host[t - 1]), u8(host[t]), W, H, fl)
             times.append(time.perf_counter() - a)
             ctimes.append(time.process_time() - ca)
-        cx = np.array([fl.contents.feature[k].contents.x for k in range(NF)], np.float32)
-        cy = np.array([fl.contents.feature[k].contents.y for k in range(NF)], np.float32)
-        cv = np.array([fl.contents.feature[k].contents.val for k in range(NF)], np.int32)
+            cols.append((lx.copy(), ly.copy(), lv.copy()))  # KLTStoreFeatureList, outside the timed call
+        cx, cy, cv = cols[-1]
         rl.KLTFreeFeatureList(fl)
         rl.KLTFreeTrackingContext(rtc)
     else:
@@ -530,35 +675,53 @@ def cpu_leg(lib, frames, W, H, NF, args, tc, ctx, dev):
             ot.track(host[t - 1], host[t], cx, cy, cv)
             times.append(time.perf_counter() - a)
             ctimes.append(time.process_time() - ca)
+            cols.append((cx.copy(), cy.copy(), cv.copy()))
     steady = times[1:] if len(times) > 1 else times  # first call builds two pyramids
     csteady = ctimes[1:] if len(ctimes) > 1 else ctimes
     cpu_fps = len(steady) / sum(steady)
     # the reference harness's own metric is clock() (example3.c:61-63): process CPU time
     clock_fps = len(csteady) / sum(csteady) if sum(csteady) > 0 else None
 
-    # the timed GPU path on the same frames: value-by-value parity
-    gx, gy, gv = gpu_sequence(lib, host, NF, args.chunk, not args.serial)
-    mism = int((gx.view(np.int32) != cx.view(np.int32)).sum() + (gy.view(np.int32) != cy.view(np.int32)).sum()
-               + (gv != cv).sum())
+    # the timed GPU path on the same frames (same reduction): cell-by-cell parity
+    # over every column of the feature table
+    TX, TY, TV = gpu_sequence(lib, host, NF, args.chunk, not args.serial, args.reduction)
+    mism = 0
+    for j, (cx_, cy_, cv_) in enumerate(cols):
+        mism += int((TX[j].view(np.int32) != cx_.view(np.int32)).sum() +
+                    (TY[j].view(np.int32) != cy_.view(np.int32)).sum() + (TV[j] != cv_).sum())
     cpu = {"value": cpu_fps, "unit": "frames/s", "cores": 1, "kind": kind, "value_clock": clock_fps,
            "sample": f"first {S} frames of the same {W}x{H} sequence, {NF} features, sequential mode; "
                      f"{len(steady)} steady-state KLTTrackFeatures calls timed (wall clock), "
                      f"selection {sel_s:.2f}s not included",
            "cpu_model": cpu_model(), "nproc": os.cpu_count()}
-    par = {"frames": S, "features": NF, "mismatched_values": mism,
-           "live_at_end": int((cv >= 0).sum()), "against": kind}
+    par = {"frames": S, "features": NF, "cells": 3 * NF * len(cols), "mismatched_values": mism,
+           "compared": "x, y (bit patterns) and val of every (feature, frame) cell of the feature table",
+           "reduction": args.reduction, "live_at_end": int((cv >= 0).sum()), "against": kind}
     return cpu, par
 
 
-def gpu_sequence(lib, host, NF, chunk, overlap):
+def list_view(fl):
+    """(x, y, val) views of a klt.h feature list whose 64-byte records are one
+    block (KLTCreateFeatureList, klt.c:143-170)."""
+    n = fl.contents.nFeatures
+    base = C.addressof(fl.contents.feature[0].contents)
+    assert C.addressof(fl.contents.feature[n - 1].contents) == base + 64 * (n - 1)
+    raw = np.ctypeslib.as_array((C.c_uint8 * (64 * n)).from_address(base)).view(np.int32).reshape(n, 16)
+    return raw[:, 0].view(np.float32), raw[:, 1].view(np.float32), raw[:, 2]
+
+
+def gpu_sequence(lib, host, NF, chunk, overlap, reduction="exact"):
     """The timed path (klt_hip_track_frames -- or klt_hip_track_sequence for
     chunk 0 -- frames + features in HBM) on the CPU sample's frames: select on
-    frame 0, then track frames 1..S-1."""
+    frame 0, then track frames 1..S-1.  Returns the feature table [S-1, NF]
+    (row j = the list after frame j+1; for chunk 0 only the last row is real)."""
+    from kltamd.device import EXACT, FAST
     import torch
     from kltamd.device import PyrDesc, TrackDesc, check, use_torch_stream
     H, W = host[0].shape
     tc = lib.KLTCreateTrackingContext()
     tc.contents.sequentialMode = 1
+    lib.klt_amd_set_reduction(tc, EXACT if reduction == "exact" else FAST)
     ctx = lib.klt_amd_device_context(tc)
     dev = torch.device("cuda", torch.cuda.current_device())
     use_torch_stream(lib, ctx, dev)
@@ -573,12 +736,15 @@ def gpu_sequence(lib, host, NF, chunk, overlap):
     pd, td = PyrDesc(), TrackDesc()
     lib.klt_amd_pyr_desc(tc, W, H, tc.contents.nPyramidLevels, 1, C.byref(pd))
     lib.klt_amd_track_desc(tc, C.byref(td))
+    T = len(host) - 1
+    tab = [torch.zeros((T, NF), dtype=dt, device=dev) for dt in (torch.float32, torch.float32, torch.int32)]
     if chunk > 0:
+        tp = [C.c_void_p(a.data_ptr()) for a in tab]
         check(lib, ctx, lib.klt_hip_frames_begin(ctx, C.byref(pd), C.c_void_p(fr.data_ptr()), W), "begin")
         check(lib, ctx, lib.klt_hip_track_frames(ctx, C.byref(pd), C.byref(td), C.c_void_p(fr.data_ptr() + W * H), W,
-                                                 W * H, len(host) - 1, chunk, C.c_void_p(x.data_ptr()),
-                                                 C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()), NF, None,
-                                                 None, None, 0), "frames")
+                                                 W * H, T, chunk, C.c_void_p(x.data_ptr()),
+                                                 C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()), NF, tp[0],
+                                                 tp[1], tp[2], NF), "frames")
     else:
         check(lib, ctx, lib.klt_hip_build_pyramid(ctx, 0, C.byref(pd), C.c_void_p(fr.data_ptr()), W, 0), "build")
         slot = C.c_int(0)
@@ -587,7 +753,9 @@ def gpu_sequence(lib, host, NF, chunk, overlap):
                                                    C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()), NF,
                                                    C.byref(slot)), "sequence")
     torch.cuda.synchronize()
-    out = (x.cpu().numpy(), y.cpu().numpy(), v.cpu().numpy())
+    if chunk == 0:  # the pipelined path keeps no table: its final list is the last row
+        tab[0][-1].copy_(x), tab[1][-1].copy_(y), tab[2][-1].copy_(v)
+    out = tuple(a.cpu().numpy() for a in tab)
     lib.KLTFreeTrackingContext(tc)
     return out
 

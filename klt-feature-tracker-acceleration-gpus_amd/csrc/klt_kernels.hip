@@ -3038,6 +3038,7 @@ struct CopyPool {
 };
 
 constexpr int kStageGroup = 8;  // frames per staging group; two groups of pinned slots
+constexpr int kMaxCopyThreads = 16;  // copy-pool workers per device context, at most
 
 struct klt_hip_ctx {
   int device = 0;
@@ -3587,7 +3588,7 @@ KLT_API klt_hip_ctx *klt_hip_ctx_create(int device) {
   if (const char *m = getenv("KLT_AMD_TRACK_MERGE")) c->track_merge = atoi(m) != 0;  // A/B switch for tools
   if (const char *m = getenv("KLT_AMD_UPLOAD_PIECE_KB")) c->upload_piece = (size_t)atol(m) * 1024;  // A/B switch
   if (const char *m = getenv("KLT_AMD_FEAT_ZERO_COPY")) c->feat_zero_copy = atoi(m) != 0;          // A/B switch
-  if (const char *m = getenv("KLT_AMD_COPY_THREADS")) c->copy_threads = atoi(m) > 0 ? atoi(m) : 0;  // A/B switch
+  if (const char *m = getenv("KLT_AMD_COPY_THREADS")) c->copy_threads = clampi(atoi(m), 0, kMaxCopyThreads);  // A/B
   if (const char *m = getenv("KLT_AMD_TRACK_ORDER")) c->track_order = atoi(m) != 0;                // A/B switch
   if (device < 0) {
     if (hipGetDevice(&device) != hipSuccess) device = 0;
@@ -4383,7 +4384,16 @@ KLT_API int klt_hip_track_frames_host(klt_hip_ctx *c, const klt_hip_pyr_desc *pd
     c->stage_frame = (size_t)fb;
     for (int k = 0; k < 2; ++k)
       if (!c->ev_stage[k]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_stage[k], hipEventDisableTiming));
-    if (!c->pool) c->pool = new CopyPool(c->copy_threads);
+    if (!c->pool) {
+      // thread creation can throw (std::system_error, bad_alloc): no exception
+      // crosses this extern "C" entry; without a pool the runtime stages the copies
+      try {
+        c->pool = new CopyPool(c->copy_threads);
+      } catch (...) {
+        c->pool = nullptr;
+        c->copy_threads = 0;
+      }
+    }
   }
   // the ring may still be read by earlier work on the context stream
   HIPCHK(c, hipEventRecord(c->ev_ring_free[0], c->stream));
@@ -4407,11 +4417,15 @@ KLT_API int klt_hip_track_frames_host(klt_hip_ctx *c, const klt_hip_pyr_desc *pd
       HIPCHK(c, hipEventSynchronize(c->ev_stage[sg]));
       unsigned char *slots = c->h_stage + (size_t)sg * kStageGroup * fb;
       const size_t piece = 512 << 10;
-      c->pool->jobs.clear();
-      for (int f = 0; f < ng; ++f)
-        for (size_t o = 0; o < (size_t)fb; o += piece)
-          c->pool->jobs.push_back({slots + (size_t)f * fb + o, frames[j0 + g0 + f] + o,
-                                   (size_t)fb - o < piece ? (size_t)fb - o : piece});
+      try {
+        c->pool->jobs.clear();
+        for (int f = 0; f < ng; ++f)
+          for (size_t o = 0; o < (size_t)fb; o += piece)
+            c->pool->jobs.push_back({slots + (size_t)f * fb + o, frames[j0 + g0 + f] + o,
+                                     (size_t)fb - o < piece ? (size_t)fb - o : piece});
+      } catch (...) {
+        return fail(c, "track_frames_host: out of memory filling the copy jobs");
+      }
       c->pool->copy();
       HIPCHK(c, hipMemcpyAsync(c->d_ring + (size_t)(k * F + g0) * fb, slots, (size_t)ng * fb,
                                hipMemcpyHostToDevice, c->cstream));

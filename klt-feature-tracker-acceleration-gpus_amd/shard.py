@@ -10,8 +10,10 @@ owner's value bit for bit.  A feature whose window would leave a rank's built
 rows raises the chunk's escape flag; all ranks then redo that chunk from
 full-frame pyramids, so the result never depends on the margin.
 
-The data path has one collective per chunk (3*n int32, 240 KB at 20k
-features) -- the position exchange the path really has -- and no other.
+The data path has one collective per chunk: 3*n+1 int32 (240 KB at 20k
+features) -- the position exchange the path really has, with the escape flag
+riding along as its last element -- and one host read of that flag after it.
+Only a chunk that escaped costs a second build and a second exchange.
 """
 from __future__ import annotations
 
@@ -46,18 +48,25 @@ def owned_mask(y0: torch.Tensor, v0: torch.Tensor, band: Band) -> torch.Tensor:
     return (v0 >= 0) & (y0 >= band.own_lo) & (y0 < band.own_hi)
 
 
-def merge_chunk(x, y, v, y0, v0, band: Band, rank: int, all_reduce) -> None:
+def merge_chunk(x, y, v, y0, v0, band: Band, rank: int, all_reduce, escape=None):
     """In place, after one chunk: every rank ends with the owners' (x, y, val).
     y0/v0 are the chunk-start state (ownership); lost features, which nobody
-    tracks, are contributed by rank 0."""
+    tracks, are contributed by rank 0.  escape (a 1-element int32 device
+    tensor, optional) is summed over the ranks in the same collective; the sum
+    is returned (None without it)."""
+    n = x.numel()
     owned = owned_mask(y0, v0, band)
     keep = owned | (v0 < 0) if rank == 0 else owned
     bits = torch.stack([x.view(torch.int32), y.view(torch.int32), v.view(torch.int32)])
     bits = torch.where(keep.unsqueeze(0), bits, torch.zeros_like(bits))
+    if escape is not None:
+        bits = torch.cat([bits.reshape(-1), escape.reshape(1).to(torch.int32)])
     all_reduce(bits)
-    x.view(torch.int32).copy_(bits[0])
-    y.view(torch.int32).copy_(bits[1])
-    v.copy_(bits[2])
+    flat = bits[:3 * n].reshape(3, n)
+    x.view(torch.int32).copy_(flat[0])
+    y.view(torch.int32).copy_(flat[1])
+    v.copy_(flat[2])
+    return bits[3 * n:] if escape is not None else None
 
 
 class ShardedSequence:
@@ -106,13 +115,15 @@ class ShardedSequence:
             xs, ys, vs = self.x.clone(), self.y.clone(), self.v.clone()
             self.escape.zero_()
             self._band_call(c0, n, self.band.row_lo, self.band.row_hi)
-            flag = self.escape.clone()
-            self.all_reduce(flag)  # any rank escaped?
+            # one collective: the owners' results and the escape flag summed over ranks
+            flag = merge_chunk(self.x, self.y, self.v, ys, vs, self.band, self.rank, self.all_reduce,
+                               escape=self.escape)
             if int(flag.item()) != 0:
-                # redo the chunk from full-frame pyramids (exact whatever the motion)
+                # some rank's window left its built rows: redo the chunk from
+                # full-frame pyramids (exact whatever the motion), merge again
                 self.redone += 1
                 self.x.copy_(xs), self.y.copy_(ys), self.v.copy_(vs)
                 self.begin(c0 - 1)
                 self.escape.zero_()
                 self._band_call(c0, n, 0, self.H)
-            merge_chunk(self.x, self.y, self.v, ys, vs, self.band, self.rank, self.all_reduce)
+                merge_chunk(self.x, self.y, self.v, ys, vs, self.band, self.rank, self.all_reduce)

@@ -21,7 +21,7 @@ ROOT = Path(__file__).resolve().parents[1]
 PKG = ROOT / "klt-feature-tracker-acceleration-gpus_amd"
 AMD_LIB = PKG / "lib" / "libklt_amd.so"
 REF_LIB = ROOT / "oracle" / "_ref" / "libklt_ref.so"
-ORACLE_LIB = ROOT / "oracle" / "build" / "libklt_oracle.so"
+ORACLE_LIB = Path(os.environ.get("KLT_ORACLE_LIB", ROOT / "oracle" / "build" / "libklt_oracle.so"))  # env: sanitizer builds
 GOLDEN = ROOT / "tests" / "golden"
 
 import sys as _sys

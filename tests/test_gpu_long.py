@@ -1,0 +1,207 @@
+"""Full-length BASELINE sequences on the GPU against the reference itself.
+
+tests/golden/long_config{2,3,4}.json hold, per feature-table column, the
+sha256 of the reference's output (oracle/_ref, src/V3 compiled from its own
+sources; tests/golden/make_long.py) on the synthetic sequences of BASELINE
+configs 2 (640x480, 1000 features, 100 frames), 3 (1920x1080, 5000, 500) and
+4 (3840x2160, 20000, 1000).  The frames are regenerated on the device from the
+seed (include/klt_synth.h, bit-identical to the host generator), so nothing of
+the reference travels to the GPU box.
+
+Paths covered, each over the whole sequence:
+  * the batched device path bench.py times (klt_hip_track_frames, 64-frame
+    chunks, next chunk's pyramids on a second stream) -- every column;
+  * KLTTrackSequence on host frames (the klt.h extension) -- every column;
+  * KLTTrackFeatures once per host frame (config 2; example3.c:54-74);
+  * the feature-sharded schedule (config 4, 2/4/8 simulated ranks);
+  * the fast (wave-shuffle) reduction, against the exact path, with the
+    tolerance it is held to.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import hashlib
+import json
+
+import numpy as np
+import pytest
+
+from kltabi import GOLDEN, u8ptr
+
+pytestmark = pytest.mark.gpu
+
+FAST_MAX_FLIP_FRACTION = 1e-3  # val mismatches / cells (SURVEY 8c expects ~13 per 100k)
+FAST_MAX_DRIFT_PX = 0.5        # max |dx|, |dy| over cells tracked in both (<= 0.41 px)
+
+
+def fixture(name: str) -> dict:
+    return json.loads((GOLDEN / f"long_{name}.json").read_text())
+
+
+def digest(x, y, v) -> str:
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(x, "<f4").tobytes())
+    h.update(np.ascontiguousarray(y, "<f4").tobytes())
+    h.update(np.ascontiguousarray(v, "<i4").tobytes())
+    return h.hexdigest()
+
+
+def first_mismatch(X, Y, V, want: list[str]) -> int | None:
+    """Index of the first table row whose digest differs from the reference's."""
+    for j in range(len(want)):
+        if digest(X[j], Y[j], V[j]) != want[j]:
+            return j
+    return None
+
+
+def device_run(gpu, cfg: dict, nframes: int | None = None, reduction: int = 0, chunk: int = 64,
+               overlap: int = 1):
+    """Frames synthesised into HBM, selection on frame 0 through KLTSelectGoodFeatures,
+    then klt_hip_frames_begin + klt_hip_track_frames with the feature table on the
+    device (the bench's path).  Returns the table [T, n] (row j = list after frame j+1)."""
+    from kltabi import fl_to_arrays
+    from kltamd.device import D2H, H2D, PyrDesc, TrackDesc, check
+    w, h, n, seed = cfg["w"], cfg["h"], cfg["features"], cfg["seed"]
+    nframes = nframes or cfg["frames"]
+    T = nframes - 1
+    tc = gpu.KLTCreateTrackingContext()
+    tc.contents.sequentialMode = 1
+    gpu.klt_amd_set_reduction(tc, reduction)
+    ctx = gpu.klt_amd_device_context(tc)
+    check(gpu, ctx, gpu.klt_hip_set_frames_overlap(ctx, overlap), "overlap")
+    dfr = gpu.klt_hip_malloc(ctx, nframes * w * h)
+    check(gpu, ctx, gpu.klt_hip_synth_frames(ctx, seed, 0, nframes, w, h, dfr, w, w * h), "synth")
+    f0 = np.empty((h, w), np.uint8)
+    check(gpu, ctx, gpu.klt_hip_memcpy(ctx, f0.ctypes.data, dfr, f0.nbytes, D2H), "d2h")
+    fl = gpu.KLTCreateFeatureList(n)
+    gpu.KLTSelectGoodFeatures(tc, u8ptr(f0), w, h, fl)
+    x, y, v = fl_to_arrays(fl)
+    gpu.KLTFreeFeatureList(fl)
+    dx, dy, dv = (gpu.klt_hip_malloc(ctx, 4 * n) for _ in range(3))
+    tx, ty, tv = (gpu.klt_hip_malloc(ctx, 4 * n * T) for _ in range(3))
+    for d, a in ((dx, x), (dy, y), (dv, v)):
+        check(gpu, ctx, gpu.klt_hip_memcpy(ctx, d, a.ctypes.data, a.nbytes, H2D), "h2d")
+    pd, td = PyrDesc(), TrackDesc()
+    gpu.klt_amd_pyr_desc(tc, w, h, tc.contents.nPyramidLevels, 1, C.byref(pd))
+    gpu.klt_amd_track_desc(tc, C.byref(td))
+    check(gpu, ctx, gpu.klt_hip_frames_begin(ctx, C.byref(pd), dfr, w), "begin")
+    check(gpu, ctx, gpu.klt_hip_track_frames(ctx, C.byref(pd), C.byref(td), dfr + w * h, w, w * h, T, chunk,
+                                             dx, dy, dv, n, tx, ty, tv, n), "frames")
+    X = np.empty((T, n), np.float32)
+    Y = np.empty((T, n), np.float32)
+    V = np.empty((T, n), np.int32)
+    for d, a in ((tx, X), (ty, Y), (tv, V)):
+        check(gpu, ctx, gpu.klt_hip_memcpy(ctx, a.ctypes.data, d, a.nbytes, D2H), "d2h")
+    for d in (dfr, dx, dy, dv, tx, ty, tv):
+        gpu.klt_hip_free(ctx, d)
+    gpu.KLTFreeTrackingContext(tc)
+    return X, Y, V
+
+
+def host_frames(gpu, cfg: dict, nframes: int) -> list[np.ndarray]:
+    out = []
+    for t in range(nframes):
+        a = np.empty((cfg["h"], cfg["w"]), np.uint8)
+        gpu.klt_synth_frame(cfg["seed"], t, cfg["w"], cfg["h"], a.ctypes.data)
+        out.append(a)
+    return out
+
+
+def table_view(ft, T: int, n: int):
+    """(x, y, val) [T, n] of a feature table from KLTCreateFeatureTable (one
+    record block, record (feature j, frame i) at j*nFrames + i, 64 bytes each)."""
+    nfr = ft.contents.nFrames
+    base = C.addressof(ft.contents.feature[0][0].contents)
+    assert C.addressof(ft.contents.feature[n - 1][nfr - 1].contents) == base + 64 * (n * nfr - 1)
+    raw = np.ctypeslib.as_array((C.c_uint8 * (64 * n * nfr)).from_address(base)).view(np.int32)
+    raw = raw.reshape(n, nfr, 16)[:, :T]
+    return (raw[:, :, 0].view(np.float32).T.copy(), raw[:, :, 1].view(np.float32).T.copy(),
+            raw[:, :, 2].T.copy())
+
+
+@pytest.mark.parametrize("name", ["config2", "config3", "config4"])
+def test_batched_full_sequence_vs_reference(gpu, name):
+    """Every column of the full-length sequence, on the bench's schedule."""
+    cfg = fixture(name)
+    X, Y, V = device_run(gpu, cfg)
+    assert len(cfg["columns"]) == X.shape[0] == cfg["frames"] - 1
+    j = first_mismatch(X, Y, V, cfg["columns"])
+    assert j is None, f"{name}: table differs from the reference from frame {j + 1}"
+    assert [int((V[k] >= 0).sum()) for k in range(0, X.shape[0], 50)] == cfg["live"][::50]
+
+
+@pytest.mark.parametrize("name,chunk,overlap", [("config2", 1, 0), ("config2", 7, 1), ("config4", 32, 0)])
+def test_batched_schedules_vs_reference(gpu, name, chunk, overlap):
+    """Other chunk sizes / one stream: the same columns (config 4 on 200 frames)."""
+    cfg = fixture(name)
+    nframes = min(cfg["frames"], 201)
+    X, Y, V = device_run(gpu, cfg, nframes=nframes, chunk=chunk, overlap=overlap)
+    j = first_mismatch(X, Y, V, cfg["columns"][:nframes - 1])
+    assert j is None, f"{name} chunk {chunk}: differs from frame {j + 1}"
+
+
+@pytest.mark.parametrize("name", ["config2", "config3"])
+def test_track_sequence_full_vs_reference(gpu, name):
+    """KLTTrackSequence(tc, host frames, ...) + its feature table, whole sequence."""
+    from kltabi import fl_to_arrays
+    cfg = fixture(name)
+    w, h, n, nfr = cfg["w"], cfg["h"], cfg["features"], cfg["frames"]
+    frames = host_frames(gpu, cfg, nfr)
+    tc = gpu.KLTCreateTrackingContext()
+    tc.contents.sequentialMode = 1
+    fl = gpu.KLTCreateFeatureList(n)
+    gpu.KLTSelectGoodFeatures(tc, u8ptr(frames[0]), w, h, fl)
+    T = nfr - 1
+    ft = gpu.KLTCreateFeatureTable(T, n)
+    arr = (C.POINTER(C.c_ubyte) * nfr)(*[u8ptr(f) for f in frames])
+    gpu.KLTTrackSequence(tc, arr, nfr, w, h, fl, ft, 0)
+    X, Y, V = table_view(ft, T, n)
+    x, y, v = fl_to_arrays(fl)
+    gpu.KLTFreeFeatureTable(ft)
+    gpu.KLTFreeFeatureList(fl)
+    gpu.KLTFreeTrackingContext(tc)
+    j = first_mismatch(X, Y, V, cfg["columns"])
+    assert j is None, f"{name}: KLTTrackSequence differs from frame {j + 1}"
+    assert hashlib.sha256(v.tobytes()).hexdigest() == cfg["final"]["val"]
+
+
+def test_track_features_per_call_config2(gpu):
+    """The reference harness loop itself: one KLTTrackFeatures call per host frame."""
+    from kltabi import KLTRunner
+    cfg = fixture("config2")
+    frames = host_frames(gpu, cfg, cfg["frames"])
+    X, Y, V = KLTRunner(gpu).harness(frames, cfg["features"], cfg["frames"], first=frames[0])
+    T = cfg["frames"] - 1
+    j = first_mismatch(X[:, :T].T, Y[:, :T].T, V[:, :T].T, cfg["columns"])
+    assert j is None, f"per-call path differs from frame {j + 1}"
+
+
+def fast_vs_exact(Xe, Ye, Ve, Xf, Yf, Vf) -> dict:
+    cells = Ve.size
+    flips = int((Ve != Vf).sum())
+    both = (Ve == 0) & (Vf == 0)
+    dx = np.abs(Xe[both].astype(np.float64) - Xf[both])
+    dy = np.abs(Ye[both].astype(np.float64) - Yf[both])
+    return {"cells": cells, "val_mismatches": flips, "flip_fraction": flips / cells,
+            "tracked_in_both": int(both.sum()), "max_dx": float(dx.max(initial=0.0)),
+            "max_dy": float(dy.max(initial=0.0)), "cells_moved": int(((dx > 0) | (dy > 0)).sum())}
+
+
+@pytest.mark.parametrize("name", ["config2", "config3"])
+def test_fast_reduction_tolerance(gpu, name, tmp_path_factory):
+    """KLT_HIP_FAST (butterfly sums instead of the reference's sequential 49-term
+    sums, trackFeatures.c:241-248 and :271-278): not bit-exact, held to a stated
+    tolerance over the whole sequence against the exact path, which the same
+    test pins to the reference column by column."""
+    cfg = fixture(name)
+    Xe, Ye, Ve = device_run(gpu, cfg)
+    assert first_mismatch(Xe, Ye, Ve, cfg["columns"]) is None
+    Xf, Yf, Vf = device_run(gpu, cfg, reduction=1)
+    st = fast_vs_exact(Xe, Ye, Ve, Xf, Yf, Vf)
+    print(f"\nfast reduction {name}: {json.dumps(st)}")
+    out = GOLDEN.parents[1] / "gpurun_out"
+    if out.is_dir():
+        (out / f"fast_tolerance_{name}.json").write_text(json.dumps(st, indent=1) + "\n")
+    assert st["flip_fraction"] <= FAST_MAX_FLIP_FRACTION, st
+    assert st["max_dx"] <= FAST_MAX_DRIFT_PX and st["max_dy"] <= FAST_MAX_DRIFT_PX, st
+    assert st["tracked_in_both"] > 0.5 * st["cells"]

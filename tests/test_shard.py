@@ -57,8 +57,9 @@ def _merge_worker(rank, world, port, q):
         x[owned] = x0[owned] + 1000 * (rank + 1)
         y[owned] = -1.0
         v[owned] = -3 - rank
-        merge_chunk(x, y, v, y0.clone(), v0.clone(), band, rank, lambda t: dist.all_reduce(t))
-        q.put((rank, x.numpy(), y.numpy(), v.numpy()))
+        flag = merge_chunk(x, y, v, y0.clone(), v0.clone(), band, rank, lambda t: dist.all_reduce(t),
+                           escape=torch.tensor([rank + 1], dtype=torch.int32))
+        q.put((rank, x.numpy(), y.numpy(), v.numpy(), int(flag.item())))
     finally:
         dist.destroy_process_group()
 
@@ -75,8 +76,10 @@ def test_merge_chunk_gloo_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     res.sort(key=lambda t: t[0])
+    # the escape flags ride along in the same collective: summed on every rank
+    assert [r[4] for r in res] == [3, 3]
     # both ranks hold identical arrays ...
-    for a, b in zip(res[0][1:], res[1][1:]):
+    for a, b in zip(res[0][1:4], res[1][1:4]):
         assert np.array_equal(a.view(np.int32), b.view(np.int32))
     # ... equal to the owners' values
     n = 64
@@ -201,3 +204,23 @@ def test_sharded_equals_single_gpu(gpu, oracle, world, chunk, margin):
     assert np.array_equal(y.view(np.int32), Y[:, k].view(np.int32))
     if margin == 0:
         assert redone > 0  # no margin: features near band edges must escape and be redone
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_sharded_4k_20k_equals_reference(gpu, world):
+    """BASELINE config 4 (3840x2160, 20000 features): the feature-sharded
+    schedule with 2/4/8 simulated ranks (32-frame chunks, 128-row margin)
+    reproduces the reference's list after 64 frames -- the digest of column 63
+    of tests/golden/long_config4.json (oracle/_ref on the full sequence)."""
+    import hashlib
+    import json
+    from kltabi import GOLDEN
+    cfg = json.loads((GOLDEN / "long_config4.json").read_text())
+    T = 64
+    frames = synth(gpu, cfg["seed"], cfg["w"], cfg["h"], T + 1)
+    x, y, v, redone = sharded_sequence(gpu, frames, cfg["features"], world, 32, 128)
+    h = hashlib.sha256()
+    for a, dt in ((x, "<f4"), (y, "<f4"), (v, "<i4")):
+        h.update(np.ascontiguousarray(a, dt).tobytes())
+    assert h.hexdigest() == cfg["columns"][T - 1], f"world {world}: sharded list differs (redone {redone})"
