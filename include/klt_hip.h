@@ -118,9 +118,6 @@ int klt_hip_build_pyramid(klt_hip_ctx *ctx, int slot, const klt_hip_pyr_desc *de
 /* test hook: 1 forces the generic one-pass-per-launch path even when the
    fused kernels apply (they must agree bit for bit) */
 int klt_hip_set_path(klt_hip_ctx *ctx, int force_generic);
-/* tuning hook: features per wavefront for windows of <= 64 pixels (1, 2 or
-   4; 0 restores the default).  Results do not depend on it. */
-int klt_hip_set_track_group(klt_hip_ctx *ctx, int features_per_wave);
 /* tuning hook: 1 tracks features in input order; 0 (default) in row-band
    order with each XCD given one band (L2 locality).  Results do not depend on it. */
 int klt_hip_set_track_order(klt_hip_ctx *ctx, int input_order);
@@ -145,16 +142,9 @@ int klt_hip_get_track_count(klt_hip_ctx *ctx, unsigned long long *solves, unsign
 /* tuning hook: 0 disables the lane-patch gather of one-feature waves (default
    1: on where (ww+1)*(wh+1) <= 64).  Results do not depend on it. */
 int klt_hip_set_track_patch(klt_hip_ctx *ctx, int on);
-/* tuning hook: the level-0 kernel of the fused pyramid.  mode 0 (default):
-   64x32 tiles, one workgroup each (k_pyr_l0); 1: rolling 64-column strips that
-   keep the rows shared by consecutive steps in LDS (k_pyr_l0s, needs width % 8
-   == 0 and 4-byte aligned rows; strip_steps 16-row steps per strip, <= 0 keeps
-   the current value, default 8); 2: persistent tiles fed by an LDS-DMA loading
-   wave (k_pyr_l0p, 4-byte aligned rows); 3: persistent tiles whose gx/gy
-   stores are deferred into the next tile's phases (k_pyr_l0q).  Shapes a mode
-   cannot take use tiles.
-   Results do not depend on it (tests/test_gpu_pyramid.py). */
-int klt_hip_set_pyr_l0(klt_hip_ctx *ctx, int mode, int strip_steps);
+/* instrumented build only (make -C csrc prof): device buffer receiving 10
+   u64 phase counters per tracker wave; a no-op buffer in the product build */
+int klt_hip_set_prof(klt_hip_ctx *ctx, void *dev);
 /* klt_hip_track_frames scheduling: 1 builds chunk c+1's pyramids on a second
    stream while chunk c is tracked; 0 (default) runs both on the context stream. */
 int klt_hip_set_frames_overlap(klt_hip_ctx *ctx, int overlap);

@@ -1,0 +1,724 @@
+// pyramid.hip -- gfx950 kernels of the image side of the KLT hot path:
+//   k_pyr_l0 / k_pyr_l1   the fused pyramid for the default parameters
+//                         (_KLTToFloatImage + _KLTComputeSmoothedImage +
+//                          _KLTComputePyramid + _KLTComputeGradients,
+//                          convolve.c:37-53,273-314; pyramid.c:87-131)
+//   k_u8_to_f32 / k_rows / k_cols / k_subsample   the generic path (any sigma,
+//                         levels, subsampling), one 1-D pass per launch
+//   k_min_eigen           the trackability map (selectGoodFeatures.c:375-424)
+//   k_synth               synthetic frames (include/klt_synth.h)
+//
+// Parity contract: every output is bit-identical to the reference CPU path
+// (src/V3).  That needs
+//   * no multiply-add contraction (built with -ffp-contract=off, and the pragma
+//     below): the reference is compiled for x86-64 without FMA;
+//   * every sum accumulated from +0 in the reference's order;
+//   * IEEE division/sqrt (HIP defaults; never -ffast-math);
+//   * the reference's zero borders after every 1-D pass (convolve.c:164-178,
+//     :216-237), its pyramid sampling points (pyramid.c:120-124) and its
+//     x86 float->int conversion for the trackability values.
+//
+// Memory: every pyramid plane is a tight row-major f32 array (pitch = ncols),
+// the layout the reference's _KLT_FloatImage uses (klt_util.c:31-47).
+#pragma clang fp contract(off)
+
+#include <math.h>
+
+#include "klt_dev.h"
+#include "klt_synth.h"
+
+namespace kltdev {
+namespace {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4 ld4(const float *p) { return *reinterpret_cast<const f4 *>(p); }
+__device__ __forceinline__ void st4(float *p, f4 v) { *reinterpret_cast<f4 *>(p) = v; }
+// level-0 HBM stores are nontemporal (measured 1-2 % faster than plain stores)
+__device__ __forceinline__ void st4_out(float *p, f4 v) { __builtin_nontemporal_store(v, reinterpret_cast<f4 *>(p)); }
+__device__ __forceinline__ void st2_out(float *p, f2 v) { __builtin_nontemporal_store(v, reinterpret_cast<f2 *>(p)); }
+
+// acc[i] += v[i + off] * k for 4 lanes, as two packed-f32 pairs
+__device__ __forceinline__ void mac4(f4 &acc, const float *v, float k) {
+  f2 lo = {v[0], v[1]}, hi = {v[2], v[3]};
+  f2 kk = {k, k};
+  f2 alo = {acc.x, acc.y}, ahi = {acc.z, acc.w};
+  alo += lo * kk;
+  ahi += hi * kk;
+  acc = f4{alo.x, alo.y, ahi.x, ahi.y};
+}
+
+// v[i] * k for 4 lanes: the first term of a sum whose terms are all >= +0
+// (u8 or smoothed values times a positive gauss tap), where 0 + t == t bit
+// for bit and the reference's +0 start can be left out
+__device__ __forceinline__ f4 mul4(const float *v, float k) {
+  f2 lo = {v[0], v[1]}, hi = {v[2], v[3]};
+  f2 kk = {k, k};
+  lo = lo * kk;
+  hi = hi * kk;
+  return f4{lo.x, lo.y, hi.x, hi.y};
+}
+
+// The derivative's centre tap is exactly +0 (-0 * g / sum, convolve.c:92;
+// fused_ok checks it).  A product with it is +-0, and an ordered sum started
+// from +0 is never -0 (x + (-x) rounds to +0), so acc + v * d[kDC] == acc bit
+// for bit and the derivative passes leave that term out: 6 of 7 multiply-adds.
+
+// ---------------------------------------------------------------------------
+// k_pyr_l0: one 256-thread workgroup per 64x32 tile of level 0 produces
+//   img0 = cols_s(rows_s(float(u8)))                  _KLTComputeSmoothedImage
+//   gx0  = cols_g(rows_d(img0)), gy0 = cols_d(rows_g(img0))  _KLTComputeGradients
+//   hs   = rows_p(img0) at columns 4X+2 only          first half of pyramid.c:114
+// All intermediates stay in LDS.  Each output is still summed from +0 in the
+// reference's tap order.  Phases (one barrier each):
+//   A  u8 tile + halo -> LDS (bytes)
+//   B  smoothing rows pass -> t1 (8 outputs per item from 4 staged dwords)
+//   C  smoothing columns pass -> img0 (LDS), 4 rows x 4 columns per thread
+//   D  img0 -> HBM; gradient rows passes -> tx, ty; pyramid rows pass -> hs
+//   E  gradient columns passes -> gx0, gy0 (4 rows x 2 columns per thread)
+// ---------------------------------------------------------------------------
+namespace l0 {
+constexpr int RS = kRS, RG = kRG, RP = kRP, SS = kSS, TW = geom::L0_TW, TH = geom::L0_TH;
+constexpr int UQ = 24;                        // staged u8 dwords per row: global [C0-12, C0+84)
+constexpr int UH = TH + 2 * RG + 2 * RS + 2;  // 44 rows: global R0-5 ..  (2 spare for 4-row blocks)
+constexpr int NG = 21;                        // 4-column groups of t1 / img0: global [C0-8, C0+76)
+constexpr int IH = TH + 2 * RG;               // 38 img0 rows used (global R0-3 ..)
+constexpr int IHB = (IH + 3) / 4;             // 4-row blocks of img0 computed
+// LDS pitches (floats) chosen with tools/lds_banks.py so that the 16-lane
+// groups of each ds_read_b128 hit (nearly) distinct bank slots; a few bank
+// conflicts were traded for a 4th workgroup per CU
+constexpr int PT = 88, PI = 92, PX = TW;
+constexpr int PUB = 24;                   // staged u8 row pitch in dwords (96 bytes)
+constexpr int U_WORDS = UH * PUB;
+constexpr int REG_A = U_WORDS > IH * PI ? U_WORDS : IH * PI;  // u during A-B, then img0 during C-D
+constexpr int REG_B = 2 * IH * PX;                            // t1 during B-C, then tx|ty during D-E
+constexpr int LDS = REG_A + REG_B;
+static_assert(IH * PI <= REG_A && UH * PT <= REG_B, "LDS aliasing");
+static_assert(TH % 4 == 0 && TH * TW / 16 <= kBlock && TW % 16 == 0, "tile shape");
+// interior tiles: one 16-byte chunk per thread covers the staged rows
+constexpr int NQ = UQ / 4, NR = TH + 2 * RG + 2 * RS;
+static_assert(NR * NQ <= kBlock && NR <= UH, "one 16-byte load per thread");
+}  // namespace l0
+
+// XCD-aware tile order: consecutive workgroups are dealt to the 8 XCDs in
+// turn, so workgroup w takes tile (w % 8) * per + w / 8 (grid.x = 8 * per) and
+// each XCD's L2 sees one contiguous band of rows -- the halo rows a tile
+// shares with its neighbours above and below are then mostly L2 hits.
+__device__ __forceinline__ bool xcd_tile(int tiles_x, int tiles_y, int &bx, int &by) {
+  const int per = (int)gridDim.x / 8;
+  const int t = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+  if (t >= tiles_x * tiles_y) return false;
+  by = t / tiles_x;
+  bx = t - by * tiles_x;
+  return true;
+}
+
+// Edge tiles (INT false) clamp their loads and apply the zero-border rules per
+// element; interior tiles (~90 % at 1080p, 94 % at 4K) need neither.
+template <bool INT>
+__device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8_t *__restrict__ src, int spitch,
+                                            int W, int H, const DefTaps &T, int vec_u8,
+                                            float *__restrict__ img0, float *__restrict__ gx0,
+                                            float *__restrict__ gy0, float *__restrict__ hs, int hsW,
+                                            int do_hs, int vec_out, int C0, int R0, int tid) {
+  using namespace l0;
+  float *u = lds;            // [UH][PUB] staged bytes
+  float *im = lds;           // [IHB*4][PI]   (after u is dead)
+  float *t1 = lds + REG_A;   // [UH][PT]
+  float *tx = lds + REG_A;   // [IH][PX]      (after t1 is dead)
+  float *ty = tx + IH * PX;
+
+  // A. u8 tile + halo -> LDS; every load issued before the first is used
+  if constexpr (INT) {
+    // interior tile: one 16-byte load per thread, 6 per staged row at
+    // C0-12+16q (dword-aligned: vec_u8 guarantees a 4-byte pitch and base),
+    // rows R0-5 .. R0+36 -- the 42 rows any stored output reads.  Rows 42-43
+    // of the staging area keep stale bytes: they feed only img0 rows 38-39,
+    // which are computed for the 4-row blocks and never used.  Threads past
+    // the 252 chunks repeat the last one (same bytes, same LDS slot), so the
+    // loads stay branch-free.
+    const int i = min(tid, NR * NQ - 1);
+    const int r = i / NQ, q = i - r * NQ;
+    const uint4 c = *reinterpret_cast<const uint4 *>(src + (unsigned)((R0 - RG - RS + r) * spitch + C0 - 12 + 16 * q));
+    *reinterpret_cast<uint4 *>(reinterpret_cast<uint32_t *>(u) + r * PUB + 4 * q) = c;
+  } else {
+    constexpr int NA = UH * UQ, PER = (NA + kBlock - 1) / kBlock;
+    uint32_t w[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      // unconditional: items past NA reload the last dword and land in LDS
+      // past the staged rows (unused), so no load sits under a branch -- the
+      // compiler's wait counting then stays exact
+      const int i = min(tid + k * kBlock, NA - 1);
+      const int r = i / UQ, q = i - r * UQ;
+      const int x = C0 - 12 + 4 * q;
+      const unsigned rowp = (unsigned)(clampi(R0 - RG - RS + r, 0, H - 1) * spitch);
+      if (vec_u8) {
+        w[k] = *reinterpret_cast<const uint32_t *>(src + rowp + clampi(x, 0, W - 4));
+      } else {
+        w[k] = (uint32_t)src[rowp + clampi(x, 0, W - 1)] | ((uint32_t)src[rowp + clampi(x + 1, 0, W - 1)] << 8) |
+               ((uint32_t)src[rowp + clampi(x + 2, 0, W - 1)] << 16) |
+               ((uint32_t)src[rowp + clampi(x + 3, 0, W - 1)] << 24);
+      }
+    }
+    static_assert(PER * kBlock <= REG_A, "phase A spill-over stays inside region A");
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + k * kBlock;
+      const int r = i / UQ, q = i - r * UQ;
+      reinterpret_cast<uint32_t *>(u)[r * PUB + q] = w[k];
+    }
+  }
+  __syncthreads();
+
+  // B. rows pass of the smoothing: t1 idx k <-> global C0-8+k; zero unless RS <= x < W-RS.
+  //    23 rows of 11 eight-column groups per pass (t1 idx 0..87): bytes [8j, 8j+16) of a staged row
+  {
+    const int j = tid % 11, r0 = tid / 11;
+#pragma unroll
+    for (int k = 0; k < (UH + 22) / 23; ++k) {
+      const int r = r0 + 23 * k;
+      if (r0 >= 23 || r >= UH) break;
+      const uint32_t *row = reinterpret_cast<const uint32_t *>(u) + r * PUB + 2 * j;
+      const uint2 d01 = *reinterpret_cast<const uint2 *>(row), d23 = *reinterpret_cast<const uint2 *>(row + 2);
+      const uint32_t d[4] = {d01.x, d01.y, d23.x, d23.y};
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[4 * q + 0] = (float)(d[q] & 0xFF);
+        v[4 * q + 1] = (float)((d[q] >> 8) & 0xFF);
+        v[4 * q + 2] = (float)((d[q] >> 16) & 0xFF);
+        v[4 * q + 3] = (float)(d[q] >> 24);
+      }
+      f4 a0 = mul4(v + 2, T.s[0]), a1 = mul4(v + 6, T.s[0]);
+#pragma unroll
+      for (int m = 1; m < 5; ++m) {
+        mac4(a0, v + 2 + m, T.s[m]);
+        mac4(a1, v + 6 + m, T.s[m]);
+      }
+      if (!INT) {
+        const int x = C0 - 8 + 8 * j;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (!(x + e >= RS && x + e < W - RS)) a0[e] = 0.0f;
+          if (!(x + 4 + e >= RS && x + 4 + e < W - RS)) a1[e] = 0.0f;
+        }
+      }
+      st4(t1 + r * PT + 8 * j, a0);
+      st4(t1 + r * PT + 8 * j + 4, a1);
+    }
+  }
+  __syncthreads();
+
+  // C. columns pass -> img0, 4 rows x 4 columns per thread; zero unless RS <= y < H-RS
+  const int g21 = tid % NG, r21 = tid / NG;
+  if (r21 < IHB) {  // IHB x 21 items, one per thread
+    const int b = r21, g = g21;
+    const float *col = t1 + (4 * b) * PT + 4 * g;
+    f4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = ld4(col + k * PT);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      f4 acc = mul4(reinterpret_cast<const float *>(&v[rr]), T.s[0]);
+#pragma unroll
+      for (int m = 1; m < 5; ++m) mac4(acc, reinterpret_cast<const float *>(&v[rr + m]), T.s[m]);
+      if (!INT) {
+        const int y = R0 - RG + 4 * b + rr;
+        if (!(y >= RS && y < H - RS)) acc = f4{0.0f, 0.0f, 0.0f, 0.0f};
+      }
+      if (IH % 4 == 0 || 4 * b + rr < IH) st4(im + (4 * b + rr) * PI + 4 * g, acc);  // rows >= IH unused
+    }
+  }
+  __syncthreads();
+
+  // D1. img0 tile -> HBM
+  const int g16 = tid & 15, r16 = tid >> 4;
+#pragma unroll
+  for (int k = 0; k < TH / 16; ++k) {
+    const int r = r16 + 16 * k, g = g16;
+    const int y = R0 + r, x = C0 + 4 * g;
+    const f4 val = ld4(im + (r + RG) * PI + 8 + 4 * g);
+    if (INT) {
+      st4_out(img0 + (unsigned)(y * W + x), val);
+    } else {
+      if (y >= H || x >= W) continue;
+      float *dst = img0 + (unsigned)(y * W + x);
+      if (vec_out && x + 3 < W) st4(dst, val);
+      else
+        for (int e = 0; e < 4 && x + e < W; ++e) dst[e] = val[e];
+    }
+  }
+  // D2. rows passes of both gradients; zero unless RG <= x < W-RG
+#pragma unroll
+  for (int k = 0; k < (IH + 15) / 16; ++k) {
+    const int r = r16 + 16 * k, g = g16;
+    if (r >= IH) break;
+    const float *row = im + r * PI + 4 * g + 4;  // img0 idx c0+4 <-> global C0+c0-4
+    float v[12];
+    *reinterpret_cast<f4 *>(v) = ld4(row);
+    *reinterpret_cast<f4 *>(v + 4) = ld4(row + 4);
+    *reinterpret_cast<f4 *>(v + 8) = ld4(row + 8);
+    // ay: img0 >= +0 and gauss taps > 0, so every term is >= +0 and the +0
+    // start can be left out (mul4); ax has signed taps and keeps it
+    f4 ax = {0.0f, 0.0f, 0.0f, 0.0f}, ay = mul4(v + 1, T.g[0]);
+#pragma unroll
+    for (int m = 0; m < 7; ++m) {
+      if (m != kDC) mac4(ax, v + 1 + m, T.d[m]);  // zero centre tap: exact to skip (see kDC)
+      if (m > 0) mac4(ay, v + 1 + m, T.g[m]);
+    }
+    if (!INT) {
+      const int x = C0 + 4 * g;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (!(x + e >= RG && x + e < W - RG)) {
+          ax[e] = 0.0f;
+          ay[e] = 0.0f;
+        }
+      }
+    }
+    st4(tx + r * PX + 4 * g, ax);
+    st4(ty + r * PX + 4 * g, ay);
+  }
+  // D3. pyramid rows pass at columns 4X+2; zero unless RP <= c < W-RP.  Four
+  // outputs per item (36 values read for 4 outputs), TH*TW/16 items on the
+  // upper threads, which take one gradient row group fewer in D2
+  if (do_hs && tid >= kBlock - TH * (TW / 16)) {
+    const int i = tid - (kBlock - TH * (TW / 16));
+    const int r = i / (TW / 16), q = i - r * (TW / 16);
+    const float *row = im + (r + RG) * PI + 16 * q;  // idx 16q <-> global C0+16q-8
+    float v[36];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) *reinterpret_cast<f4 *>(v + 4 * k) = ld4(row + 4 * k);
+    f2 a01 = f2{v[0], v[4]} * f2{T.p[0], T.p[0]};  // terms >= +0
+    f2 a23 = f2{v[8], v[12]} * f2{T.p[0], T.p[0]};
+#pragma unroll
+    for (int m = 1; m < 21; ++m) {
+      const f2 kk = {T.p[m], T.p[m]};
+      a01 += f2{v[m], v[m + 4]} * kk;
+      a23 += f2{v[m + 8], v[m + 12]} * kk;
+    }
+    const int y = R0 + r;
+    const int X = C0 / SS + 4 * q;
+    if (INT) {
+      *reinterpret_cast<f4 *>(hs + hs_at(y, X, H)) = f4{a01.x, a01.y, a23.x, a23.y};
+    } else if (y < H) {
+      const float o[4] = {a01.x, a01.y, a23.x, a23.y};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = C0 + 16 * q + 4 * e + 2;
+        if (X + e < hsW) hs[hs_at(y, X + e, H)] = (c >= RP && c < W - RP) ? o[e] : 0.0f;
+      }
+    }
+  }
+  __syncthreads();
+
+  // E. columns passes of both gradients; zero unless RG <= y < H-RG.  4 rows x
+  //    2 columns per thread from 8-byte LDS reads (10 rows read for 4 outputs)
+  for (int i = tid; i < (TH / 4) * (TW / 2); i += kBlock) {
+    const int b = i / (TW / 2), g = i - b * (TW / 2);
+    f2 vx[10], vy[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      vx[k] = *reinterpret_cast<const f2 *>(tx + (4 * b + k) * PX + 2 * g);
+      vy[k] = *reinterpret_cast<const f2 *>(ty + (4 * b + k) * PX + 2 * g);
+    }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      f2 ax = {0.0f, 0.0f}, ay = {0.0f, 0.0f};
+#pragma unroll
+      for (int m = 0; m < 7; ++m) {
+        ax += vx[rr + m] * f2{T.g[m], T.g[m]};
+        if (m != kDC) ay += vy[rr + m] * f2{T.d[m], T.d[m]};
+      }
+      const int y = R0 + 4 * b + rr, x = C0 + 2 * g;
+      if (INT) {
+        st2_out(gx0 + (unsigned)(y * W + x), ax);
+        st2_out(gy0 + (unsigned)(y * W + x), ay);
+      } else {
+        if (y >= H || x >= W) continue;
+        if (!(y >= RG && y < H - RG)) {
+          ax = f2{0.0f, 0.0f};
+          ay = ax;
+        }
+        float *px = gx0 + (unsigned)(y * W + x);
+        float *py = gy0 + (unsigned)(y * W + x);
+        if (vec_out && x + 1 < W) {
+          *reinterpret_cast<f2 *>(px) = ax;
+          *reinterpret_cast<f2 *>(py) = ay;
+        } else {
+          px[0] = ax.x;
+          py[0] = ay.x;
+          if (x + 1 < W) {
+            px[1] = ax.y;
+            py[1] = ay.y;
+          }
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ src, int spitch, int W, int H,
+                                                   DefTaps T, int vec_u8, float *__restrict__ img0,
+                                                   float *__restrict__ gx0, float *__restrict__ gy0,
+                                                   float *__restrict__ hs, int hsW, int do_hs, int vec_out,
+                                                   long fs_src, long fs0, long fs_hs, int ty0, int tiles_x,
+                                                   int tiles_y) {
+  __shared__ __attribute__((aligned(16))) float lds[l0::LDS];
+  int bx, by;
+  if (!xcd_tile(tiles_x, tiles_y, bx, by)) return;  // whole workgroup: no barrier is skipped
+  const int C0 = bx * l0::TW, R0 = (by + ty0) * l0::TH;
+  // blockIdx.z: frame of a batch (frame strides in elements; 0 for one frame)
+  src += blockIdx.z * fs_src;
+  img0 += blockIdx.z * fs0;
+  gx0 += blockIdx.z * fs0;
+  gy0 += blockIdx.z * fs0;
+  hs += blockIdx.z * fs_hs;
+  // interior: unclamped aligned loads, no zero-border rule applies, all stores in bounds
+  const bool interior = vec_u8 && vec_out && (hsW * l0::SS == W) && (hsW % 2 == 0) && C0 >= 12 && C0 + 84 <= W &&
+                        R0 >= 5 && R0 + l0::TH + 7 <= H;
+  if (interior)
+    pyr_l0_tile<true>(lds, src, spitch, W, H, T, vec_u8, img0, gx0, gy0, hs, hsW, do_hs, vec_out, C0, R0,
+                      threadIdx.x);
+  else
+    pyr_l0_tile<false>(lds, src, spitch, W, H, T, vec_u8, img0, gx0, gy0, hs, hsW, do_hs, vec_out, C0, R0,
+                       threadIdx.x);
+}
+
+// ---------------------------------------------------------------------------
+// k_pyr_l1: img1 = cols_p(hs) sampled at rows 4Y+2 (rest of pyramid.c:114-124)
+// and its gradients.  One 256-thread workgroup per 32x32 tile of level 1.
+// ---------------------------------------------------------------------------
+namespace l1 {
+constexpr int RG = kRG, RP = kRP, SS = kSS, TW = geom::L1_TW, TH = geom::L1_TH, NT = 256;
+constexpr int JW = 40;                          // img1 / hs columns: X in [x0-4, x0+36)
+constexpr int JH = TH + 2 * RG;                 // img1 rows: Y in [y0-3, y0+TH+3)
+constexpr int HR = SS * (JH - 1) + 2 * RP + 1;  // hs rows: [4y0-20, 4y0-20+HR)
+constexpr int LDS_H = HR * JW, LDS_J = JH * JW, LDS_X = JH * TW;
+constexpr int LDS = LDS_H + LDS_J;
+static_assert(2 * LDS_X <= LDS_H, "tx/ty reuse the hs region");
+static_assert(HR == geom::L1_HR, "geometry");
+}  // namespace l1
+
+__global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs, int W1, int H, int H1,
+                                                   DefTaps T, int vec, float *__restrict__ img1,
+                                                   float *__restrict__ gx1, float *__restrict__ gy1,
+                                                   long fs_hs, long fs1, int ty0, int tiles_x, int tiles_y) {
+  using namespace l1;
+  hs += blockIdx.z * fs_hs;
+  img1 += blockIdx.z * fs1;
+  gx1 += blockIdx.z * fs1;
+  gy1 += blockIdx.z * fs1;
+  __shared__ __attribute__((aligned(16))) float lds[LDS];
+  float *hl = lds;          // [HR][JW]
+  float *im = lds + LDS_H;  // [JH][JW]
+  float *tx = lds;          // [JH][TW]
+  float *ty = lds + LDS_X;
+
+  int bx, by;
+  if (!xcd_tile(tiles_x, tiles_y, bx, by)) return;
+  const int x0 = bx * TW, y0 = (by + ty0) * TH;
+  const int tid = threadIdx.x;
+
+  {
+    constexpr int NQ = JW / 4, NA = HR * NQ, PER = (NA + NT - 1) / NT;
+    f4 v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + k * NT;
+      if (i < NA) {
+        const int r = i / NQ, q = i - r * NQ;
+        const int row = clampi(SS * y0 - 20 + r, 0, H - 1);
+        const int X = x0 - 4 + 4 * q;
+        if (vec) {  // a 4-aligned group never straddles a slab
+          v[k] = ld4(hs + hs_at(row, clampi(X, 0, W1 - 4), H));
+        } else {
+          v[k] = f4{hs[hs_at(row, clampi(X, 0, W1 - 1), H)], hs[hs_at(row, clampi(X + 1, 0, W1 - 1), H)],
+                    hs[hs_at(row, clampi(X + 2, 0, W1 - 1), H)], hs[hs_at(row, clampi(X + 3, 0, W1 - 1), H)]};
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + k * NT;
+      if (i < NA) st4(hl + 4 * i, v[k]);
+    }
+  }
+  __syncthreads();
+
+  // img1 row i <-> Y = y0-3+i reads hs rows 4i..4i+20; zero unless 0<=Y<H1, 0<=X<W1, RP<=4Y+2<H-RP
+  for (int i = tid; i < JH * (JW / 4); i += NT) {
+    const int r = i / (JW / 4), g = i - r * (JW / 4);
+    const float *col = hl + (SS * r) * JW + 4 * g;
+    f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int m = 0; m < 21; ++m) {
+      const f4 v = ld4(col + m * JW);
+      mac4(acc, reinterpret_cast<const float *>(&v), T.p[m]);
+    }
+    const int Y = y0 - RG + r, X = x0 - 4 + 4 * g, rr = SS * Y + SS / 2;
+    const bool rowok = Y >= 0 && Y < H1 && rr >= RP && rr < H - RP;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (!(rowok && X + e >= 0 && X + e < W1)) acc[e] = 0.0f;
+    st4(im + r * JW + 4 * g, acc);
+  }
+  __syncthreads();
+
+  for (int i = tid; i < TH * (TW / 4); i += NT) {  // img1 tile out
+    const int r = i / (TW / 4), g = i - r * (TW / 4);
+    const int Y = y0 + r, X = x0 + 4 * g;
+    if (Y >= H1 || X >= W1) continue;
+    const f4 v = ld4(im + (r + RG) * JW + 4 + 4 * g);
+    float *dst = img1 + (long)Y * W1 + X;
+    if (vec && X + 3 < W1) st4(dst, v);
+    else
+      for (int e = 0; e < 4 && X + e < W1; ++e) dst[e] = v[e];
+  }
+  for (int i = tid; i < JH * (TW / 4); i += NT) {  // gradient rows passes
+    const int r = i / (TW / 4), g = i - r * (TW / 4);
+    const float *row = im + r * JW + 4 * g;  // idx 4g <-> X = x0+4g-4
+    float v[12];
+    *reinterpret_cast<f4 *>(v) = ld4(row);
+    *reinterpret_cast<f4 *>(v + 4) = ld4(row + 4);
+    *reinterpret_cast<f4 *>(v + 8) = ld4(row + 8);
+    f4 ax = {0.0f, 0.0f, 0.0f, 0.0f}, ay = mul4(v + 1, T.g[0]);  // level-1 img >= +0: as k_pyr_l0's D2
+#pragma unroll
+    for (int m = 0; m < 7; ++m) {
+      if (m != kDC) mac4(ax, v + 1 + m, T.d[m]);
+      if (m > 0) mac4(ay, v + 1 + m, T.g[m]);
+    }
+    const int X = x0 + 4 * g;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (!(X + e >= RG && X + e < W1 - RG)) {
+        ax[e] = 0.0f;
+        ay[e] = 0.0f;
+      }
+    }
+    st4(tx + r * TW + 4 * g, ax);
+    st4(ty + r * TW + 4 * g, ay);
+  }
+  __syncthreads();
+
+  for (int i = tid; i < TH * (TW / 4); i += NT) {  // gradient columns passes
+    const int r = i / (TW / 4), g = i - r * (TW / 4);
+    f4 ax = {0.0f, 0.0f, 0.0f, 0.0f}, ay = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int m = 0; m < 7; ++m) {
+      const f4 a = ld4(tx + (r + m) * TW + 4 * g), b = ld4(ty + (r + m) * TW + 4 * g);
+      mac4(ax, reinterpret_cast<const float *>(&a), T.g[m]);
+      if (m != kDC) mac4(ay, reinterpret_cast<const float *>(&b), T.d[m]);
+    }
+    const int Y = y0 + r, X = x0 + 4 * g;
+    if (Y >= H1 || X >= W1) continue;
+    if (!(Y >= RG && Y < H1 - RG)) {
+      ax = f4{0.0f, 0.0f, 0.0f, 0.0f};
+      ay = ax;
+    }
+    float *px = gx1 + (long)Y * W1 + X;
+    float *py = gy1 + (long)Y * W1 + X;
+    if (vec && X + 3 < W1) {
+      st4(px, ax);
+      st4(py, ay);
+    } else {
+      for (int e = 0; e < 4 && X + e < W1; ++e) {
+        px[e] = ax[e];
+        py[e] = ay[e];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Generic path (any sigma / levels / subsampling): one 1-D pass per launch,
+// the reference's own pass structure (convolve.c:137-266, pyramid.c:87-131).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_u8_to_f32(const uint8_t *__restrict__ src, long spitch,
+                                                      int W, int H, float *__restrict__ out) {
+  const long i = (long)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= (long)W * H) return;
+  const int y = (int)(i / W), x = (int)(i - (long)y * W);
+  out[i] = (float)src[(long)y * spitch + x];
+}
+
+__global__ __launch_bounds__(kBlock) void k_rows(const float *__restrict__ in, int W, int H, RTaps t,
+                                                 float *__restrict__ out) {
+  const long i = (long)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= (long)W * H) return;
+  const int y = (int)(i / W), x = (int)(i - (long)y * W);
+  const int r = t.w / 2;
+  float acc = 0.0f;
+  if (x >= r && x < W - r) {
+    const float *p = in + (long)y * W + x - r;
+    for (int m = 0; m < t.w; ++m) acc += p[m] * t.k[m];
+  }
+  out[i] = acc;
+}
+
+__global__ __launch_bounds__(kBlock) void k_cols(const float *__restrict__ in, int W, int H, RTaps t,
+                                                 float *__restrict__ out) {
+  const long i = (long)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= (long)W * H) return;
+  const int y = (int)(i / W), x = (int)(i - (long)y * W);
+  const int r = t.w / 2;
+  float acc = 0.0f;
+  if (y >= r && y < H - r) {
+    const float *p = in + (long)(y - r) * W + x;
+    for (int m = 0; m < t.w; ++m) acc += p[(long)m * W] * t.k[m];
+  }
+  out[i] = acc;
+}
+
+__global__ __launch_bounds__(kBlock) void k_subsample(const float *__restrict__ in, int W, int ss,
+                                                      float *__restrict__ out, int W1, int H1) {
+  const long i = (long)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= (long)W1 * H1) return;
+  const int y = (int)(i / W1), x = (int)(i - (long)y * W1);
+  out[i] = in[(long)(ss * y + ss / 2) * W + (ss * x + ss / 2)];
+}
+
+// ---------------------------------------------------------------------------
+// Trackability map (selectGoodFeatures.c:396-423): one thread per grid point,
+// window sums in row-major order, _minEigenvalue with a double sqrt, then
+// the x86-64 float->int conversion the reference binary performs.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int x86_ftoi(float v) {
+  // cvttss2si: NaN / out of range -> INT_MIN
+  if (!(v > -2147483904.0f && v < 2147483648.0f)) return (int)0x80000000u;
+  return (int)v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_min_eigen(const float *__restrict__ gx,
+                                                      const float *__restrict__ gy, int W, int bx,
+                                                      int by, int step, int nx, int ny, int hw, int hh,
+                                                      int *__restrict__ out) {
+  const long i = (long)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= (long)nx * ny) return;
+  const int iy = (int)(i / nx), ix = (int)(i - (long)iy * nx);
+  const int x = bx + ix * step, y = by + iy * step;
+  float sxx = 0.0f, sxy = 0.0f, syy = 0.0f;
+  for (int v = y - hh; v <= y + hh; ++v) {
+    const float *px = gx + (long)v * W;
+    const float *py = gy + (long)v * W;
+    for (int u = x - hw; u <= x + hw; ++u) {
+      const float a = px[u], b = py[u];
+      sxx += a * a;
+      sxy += a * b;
+      syy += b * b;
+    }
+  }
+  // (float)((gxx + gyy - sqrt((gxx-gyy)^2 + 4*gxy*gxy)) / 2.0f), :289-292
+  const float disc = (sxx - syy) * (sxx - syy) + 4.0f * sxy * sxy;
+  float val = (float)(((double)(sxx + syy) - sqrt((double)disc)) / 2.0);
+  if (val > 2147483648.0f) val = 2147483648.0f;  // (float)limit, :415-420
+  out[i] = x86_ftoi(val);
+}
+
+// synthetic frames (include/klt_synth.h), one thread per pixel
+__global__ __launch_bounds__(kBlock) void k_synth(unsigned long long seed, int t0, int W, int H,
+                                                  uint8_t *__restrict__ out, long pitch, long fstride) {
+  const long i = (long)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= (long)W * H) return;
+  const int y = (int)(i / W), x = (int)(i - (long)y * W);
+  const int t = t0 + blockIdx.y;
+  out[(long)blockIdx.y * fstride + (long)y * pitch + x] = klt_synth_pixel(seed, t, x, y);
+}
+
+__global__ void k_selftest_sqrt(const double *in, double *out, int n) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) out[i] = sqrt(in[i]);
+}
+
+__global__ void k_selftest_div(const float *a, const float *b, float *out, int n) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) out[i] = a[i] / b[i];
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+hipError_t launch_pyr_l0(hipStream_t st, const uint8_t *src, int pitch, long stride, int W, int H, const DefTaps &T,
+                         int vec_u8, int vec_out, float *img, float *gx, float *gy, float *hs, int W1, int do_hs,
+                         long fs0, long fsh, int F, int ty0, int ty1) {
+  const int tx = (W + l0::TW - 1) / l0::TW;
+  if (F <= 0 || ty1 <= ty0) return hipSuccess;
+  hipLaunchKernelGGL(k_pyr_l0, dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(kBlock), 0, st, src, pitch, W, H, T,
+                     vec_u8, img, gx, gy, hs, W1, do_hs, vec_out, stride, fs0, fsh, ty0, tx, ty1 - ty0);
+  return hipGetLastError();
+}
+
+hipError_t launch_pyr_l1(hipStream_t st, const float *hs, int W1, int H, int H1, const DefTaps &T, int vec,
+                         float *img1, float *gx1, float *gy1, long fsh, long fs1, int F, int ty0, int ty1) {
+  const int tx = (W1 + l1::TW - 1) / l1::TW;
+  if (F <= 0 || ty1 <= ty0) return hipSuccess;
+  hipLaunchKernelGGL(k_pyr_l1, dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(l1::NT), 0, st, hs, W1, H, H1, T, vec,
+                     img1, gx1, gy1, fsh, fs1, ty0, tx, ty1 - ty0);
+  return hipGetLastError();
+}
+
+hipError_t launch_u8_to_f32(hipStream_t st, const uint8_t *src, long pitch, int W, int H, float *out) {
+  const long n = (long)W * H;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_u8_to_f32, dim3(blocks_for(n)), dim3(kBlock), 0, st, src, pitch, W, H, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_rows(hipStream_t st, const float *in, int W, int H, const RTaps &t, float *out) {
+  const long n = (long)W * H;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rows, dim3(blocks_for(n)), dim3(kBlock), 0, st, in, W, H, t, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_cols(hipStream_t st, const float *in, int W, int H, const RTaps &t, float *out) {
+  const long n = (long)W * H;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_cols, dim3(blocks_for(n)), dim3(kBlock), 0, st, in, W, H, t, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_subsample(hipStream_t st, const float *in, int W, int ss, float *out, int W1, int H1) {
+  const long n = (long)W1 * H1;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_subsample, dim3(blocks_for(n)), dim3(kBlock), 0, st, in, W, ss, out, W1, H1);
+  return hipGetLastError();
+}
+
+hipError_t launch_min_eigen(hipStream_t st, const float *gx, const float *gy, int W, int bx, int by, int step, int nx,
+                            int ny, int hw, int hh, int *out) {
+  const long np = (long)nx * ny;
+  if (np == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_min_eigen, dim3(blocks_for(np)), dim3(kBlock), 0, st, gx, gy, W, bx, by, step, nx, ny, hw, hh,
+                     out);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth(hipStream_t st, unsigned long long seed, int t0, int n, int W, int H, uint8_t *out,
+                        long pitch, long fstride) {
+  const long np = (long)W * H;
+  for (int f0 = 0; f0 < n && np > 0; f0 += 65535) {
+    const int cnt = (n - f0) < 65535 ? (n - f0) : 65535;
+    hipLaunchKernelGGL(k_synth, dim3(blocks_for(np), cnt), dim3(kBlock), 0, st, seed, t0 + f0, W, H,
+                       out + (long)f0 * fstride, pitch, fstride);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_selftest_sqrt(const double *in, double *out, int n) {
+  hipLaunchKernelGGL(k_selftest_sqrt, dim3(blocks_for(n)), dim3(kBlock), 0, 0, in, out, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_selftest_div(const float *a, const float *b, float *out, int n) {
+  hipLaunchKernelGGL(k_selftest_div, dim3(blocks_for(n)), dim3(kBlock), 0, 0, a, b, out, n);
+  return hipGetLastError();
+}
+
+}  // namespace kltdev

@@ -1,0 +1,1546 @@
+// runtime.hip -- host side of libklt_amd.so: device contexts (stream, pyramid
+// slots, banks of batched pyramids, feature buffers), the pipelines that drive
+// the kernels of pyramid.hip / track.hip / affine.hip, and the klt_hip_* C ABI
+// declared in include/klt_hip.h.  No kernels here.
+#include <math.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "klt_dev.h"
+#include "klt_hip.h"
+
+#define KLT_API extern "C" __attribute__((visibility("default")))
+
+using namespace kltdev;
+
+// ===========================================================================
+// host side
+// ===========================================================================
+struct Level {
+  int w = 0, h = 0;
+  float *img = nullptr, *gx = nullptr, *gy = nullptr;
+  size_t cap = 0;  // floats per plane
+};
+
+struct Slot {
+  int nlev = 0;
+  int ss = 1;
+  int fused = -1;
+  Level lv[KLT_HIP_MAX_LEVELS];
+};
+
+enum TimerClass { T_L0 = 0, T_L1, T_TRACK, T_EIG, T_GEN, T_N };
+
+// a batch of same-size pyramids: plane l of frame f at lv[l].img + f * w*h
+struct Bank {
+  int frames = 0;  // capacity in frames
+  int nlev = 0;
+  int ss = 1;
+  Level lv[KLT_HIP_MAX_LEVELS];
+  float *hs = nullptr;  // per-frame row pass of the sigma-3.6 smoothing (fused path)
+  size_t hs_cap = 0;
+  int vlo[KLT_HIP_MAX_LEVELS] = {}, vhi[KLT_HIP_MAX_LEVELS] = {};  // rows built (band mode: a subset)
+};
+
+// where the pyramid preceding the next batch lives
+struct PrevRef {
+  int bank = -1;  // -1: pyramid slot `slot`
+  int frame = 0;
+  int slot = KLT_HIP_MAX_SLOTS;  // the batch seed slot unless klt_hip_frames_begin_slot
+};
+
+// Host copies of caller frames into pinned staging (klt_hip_track_frames_host):
+// a few worker threads and the calling thread split a group of frames into
+// 512 KB pieces.  Every worker takes part in every generation, and copy()
+// returns only when all of them have finished it, so no worker can still be
+// reading the job list when the caller refills it for the next group.
+struct CopyPool {
+  struct Job {
+    unsigned char *dst;
+    const unsigned char *src;
+    size_t n;
+  };
+  std::vector<std::thread> th;
+  std::mutex m;
+  std::condition_variable cv;
+  std::vector<Job> jobs;
+  std::atomic<size_t> next{0};
+  std::atomic<int> finished{0};
+  unsigned gen = 0;
+  bool stop = false;
+
+  explicit CopyPool(int workers) {
+    for (int i = 0; i < workers; ++i) th.emplace_back([this] { worker(); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> l(m);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto &t : th) t.join();
+  }
+  void run() {
+    for (size_t i; (i = next.fetch_add(1)) < jobs.size();) memcpy(jobs[i].dst, jobs[i].src, jobs[i].n);
+  }
+  void worker() {
+    unsigned seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> l(m);
+        cv.wait(l, [&] { return stop || gen != seen; });
+        if (stop) return;
+        seen = gen;
+      }
+      run();
+      finished.fetch_add(1);
+    }
+  }
+  void copy() {  // jobs filled by the caller
+    {
+      std::lock_guard<std::mutex> l(m);
+      next = 0;
+      finished = 0;
+      ++gen;
+    }
+    cv.notify_all();
+    run();
+    while (finished.load() < (int)th.size()) std::this_thread::yield();
+  }
+};
+
+constexpr int kStageGroup = 8;  // frames per staging group; two groups of pinned slots
+constexpr int kMaxCopyThreads = 16;  // copy-pool workers per device context, at most
+
+struct klt_hip_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  hipStream_t pstream = nullptr;  // pyramid stream of the pipelined sequence
+  hipEvent_t ev_built[KLT_HIP_MAX_SLOTS] = {};
+  hipEvent_t ev_free[KLT_HIP_MAX_SLOTS] = {};
+  hipEvent_t ev_start = nullptr;
+  Slot slot[KLT_HIP_MAX_SLOTS + 2];  // + the batch seed and scratch slots
+  uint8_t *d_u8[2] = {nullptr, nullptr};
+  uint8_t *h_u8[2] = {nullptr, nullptr};
+  hipEvent_t u8_done[2] = {nullptr, nullptr};
+  size_t u8_cap = 0;
+  int u8_w[2] = {0, 0}, u8_h[2] = {0, 0};
+  float *d_hs = nullptr;
+  size_t hs_cap = 0;
+  float *d_tmp[2] = {nullptr, nullptr};
+  size_t tmp_cap[2] = {0, 0};
+  // host-array tracking (klt.h calls): x | y | val in one device block and one
+  // pinned host block, so a call moves its feature list in one copy each way
+  float *d_fx = nullptr, *d_fy = nullptr;  // views into d_feat
+  int *d_fv = nullptr;
+  float *d_feat = nullptr, *h_feat = nullptr;
+  size_t upload_piece = 512 << 10;  // klt_hip_upload_frame: bytes per host-copy/DMA piece (0: whole frame)
+  int feat_zero_copy = 1;   // klt_hip_track on host lists: kernels use h_feat in place (0: copies)
+  size_t f_cap = 0;
+  int *d_eig = nullptr;
+  size_t eig_cap = 0;
+  // affine consistency check: stored windows (3*aff_S floats per feature) and per-call arrays
+  float *d_aff_store = nullptr;
+  size_t aff_store_cap = 0;
+  int aff_S = 0;
+  float *d_aff = nullptr, *d_xp = nullptr, *d_yp = nullptr, *d_astage = nullptr;
+  size_t aff_cap = 0, xp_cap = 0, yp_cap = 0, astage_cap = 0;
+  int *d_astate = nullptr, *d_aidx = nullptr;
+  size_t astate_cap = 0, aidx_cap = 0;
+  std::string err;
+  int force_generic = 0;
+  int track_order = 0;  // 0: band-sorted, XCD-major processing order; 1: input order
+  int track_patch = 1;  // one-feature waves gather through a lane patch when the window fits
+  int track_merge = 1;   // defer finest-level residues into the next frame's first pass (ResCarry)
+  int serial_frames = 1;  // klt_hip_track_frames: 1 builds and tracks on one stream (default: the
+                          // tracker and the pyramid kernels compete for the same CUs; overlap buys ~3 %)
+  int *d_perm = nullptr;
+  size_t perm_cap = 0;
+  int *d_count = nullptr;  // band mode: features owned in this chunk
+  unsigned long long *d_trk_count = nullptr;  // klt_hip_set_track_count: {solves, passes}, null when off
+  unsigned char *d_ring = nullptr;  // klt_hip_track_frames_host: 2 chunks of uploaded frames
+  size_t ring_cap = 0;
+  hipStream_t cstream = nullptr;
+  hipEvent_t ev_ring_ready[2] = {}, ev_ring_free[2] = {};
+  // klt_hip_track_frames_host: pinned staging for the caller's pageable
+  // frames, 2 groups of kStageGroup slots (host copy by the pool, then DMA)
+  CopyPool *pool = nullptr;
+  int copy_threads = 4;            // pool workers besides the caller; 0: runtime staging (hipMemcpyAsync from pageable)
+  unsigned char *h_stage = nullptr;
+  size_t stage_frame = 0;          // bytes per slot
+  hipEvent_t ev_stage[2] = {};     // DMA out of group g done
+  int stage_next = 0;
+  unsigned long long *prof = nullptr;  // instrumented build: per-wave tracker phase counters
+  Bank bank[3];
+  int bank_next = 0;
+  PrevRef prev;
+  bool frames_ready = false;
+  hipEvent_t ev_bbuilt[3] = {}, ev_bfree[3] = {};
+  bool timing = false;
+  long frames_timed[T_N] = {};
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_used[T_N];
+};
+
+namespace {
+
+int fail(klt_hip_ctx *c, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return -1;
+}
+
+#define HIPCHK(c, expr)                                                                \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess) return fail((c), "%s: %s", #expr, hipGetErrorString(e_));    \
+  } while (0)
+
+int use_device(klt_hip_ctx *c) {
+  HIPCHK(c, hipSetDevice(c->device));
+  return 0;
+}
+
+template <class T>
+int grow(klt_hip_ctx *c, T **p, size_t *cap, size_t n) {
+  if (*cap >= n && *p) return 0;
+  if (*p) HIPCHK(c, hipFree(*p));
+  *p = nullptr;
+  HIPCHK(c, hipMalloc((void **)p, sizeof(T) * (n ? n : 1)));
+  *cap = n;
+  return 0;
+}
+
+hipEvent_t take_event(klt_hip_ctx *c) {
+  if (!c->ev_pool.empty()) {
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// HIP events around one launch, recorded on the stream the kernel runs on
+struct TimedScope {
+  klt_hip_ctx *c;
+  int cls;
+  hipStream_t st;
+  hipEvent_t a = nullptr, b = nullptr;
+  TimedScope(klt_hip_ctx *c_, int cls_, hipStream_t st_, int frames = 1) : c(c_), cls(cls_), st(st_) {
+    if (!c->timing) return;
+    c->frames_timed[cls] += frames;
+    a = take_event(c);
+    b = take_event(c);
+    if (a) hipEventRecord(a, st);
+  }
+  ~TimedScope() {
+    if (!c->timing || !a || !b) return;
+    hipEventRecord(b, st);
+    c->ev_used[cls].push_back({a, b});
+  }
+};
+
+
+unsigned xcd_grid(int tiles) { return (unsigned)(8 * ((tiles + 7) / 8)); }
+
+int launched(klt_hip_ctx *c, const char *what, hipError_t e) {
+  if (e != hipSuccess) return fail(c, "launch %s: %s", what, hipGetErrorString(e));
+  return 0;
+}
+
+bool fused_ok(const klt_hip_pyr_desc *d) {
+  return d->smooth_input && d->smooth.width == 2 * kRS + 1 && d->grad_gauss.width == 2 * kRG + 1 &&
+         d->grad_deriv.width == 2 * kRG + 1 && d->grad_deriv.k[kRG] == 0.0f && kDC == kRG &&
+         (d->nlevels == 1 || (d->nlevels == 2 && d->subsampling == kSS && d->pyr.width == 2 * kRP + 1));
+}
+
+int ensure_slot(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d) {
+  Slot &S = c->slot[s];
+  int w = d->ncols, h = d->nrows;
+  S.nlev = d->nlevels;
+  S.ss = d->nlevels > 1 ? d->subsampling : 1;
+  for (int l = 0; l < d->nlevels; ++l) {
+    Level &L = S.lv[l];
+    L.w = w;
+    L.h = h;
+    size_t n = (size_t)w * h;
+    if (L.cap < n || !L.img) {
+      if (L.img) hipFree(L.img);
+      if (L.gx) hipFree(L.gx);
+      if (L.gy) hipFree(L.gy);
+      L.img = L.gx = L.gy = nullptr;
+      size_t m = n ? n : 1;
+      HIPCHK(c, hipMalloc((void **)&L.img, m * sizeof(float)));
+      HIPCHK(c, hipMalloc((void **)&L.gx, m * sizeof(float)));
+      HIPCHK(c, hipMalloc((void **)&L.gy, m * sizeof(float)));
+      L.cap = n;
+    }
+    w /= d->subsampling > 0 ? d->subsampling : 1;
+    h /= d->subsampling > 0 ? d->subsampling : 1;
+  }
+  return 0;
+}
+
+
+
+int build_generic(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
+                  hipStream_t st) {
+  Slot &S = c->slot[s];
+  const long n0 = (long)d->ncols * d->nrows;
+  if (grow(c, &c->d_tmp[0], &c->tmp_cap[0], (size_t)n0)) return -1;
+  if (grow(c, &c->d_tmp[1], &c->tmp_cap[1], (size_t)n0)) return -1;
+  TimedScope ts(c, T_GEN, st);
+  const RTaps sm = reverse_taps(d->smooth), py = reverse_taps(d->pyr);
+  const RTaps gg = reverse_taps(d->grad_gauss), gd = reverse_taps(d->grad_deriv);
+  Level &L0 = S.lv[0];
+  float *t0 = c->d_tmp[0], *t1 = c->d_tmp[1];
+  if (n0 > 0) {
+    if (d->smooth_input) {
+      if (launched(c, "k_u8_to_f32", launch_u8_to_f32(st, src, pitch, d->ncols, d->nrows, t1)) ||
+          launched(c, "k_rows", launch_rows(st, t1, d->ncols, d->nrows, sm, t0)) ||
+          launched(c, "k_cols", launch_cols(st, t0, d->ncols, d->nrows, sm, L0.img)))
+        return -1;
+    } else {
+      if (launched(c, "k_u8_to_f32", launch_u8_to_f32(st, src, pitch, d->ncols, d->nrows, L0.img))) return -1;
+    }
+  }
+  for (int l = 1; l < d->nlevels; ++l) {
+    Level &P = S.lv[l - 1], &L = S.lv[l];
+    if ((long)P.w * P.h == 0) continue;
+    if (launched(c, "k_rows", launch_rows(st, P.img, P.w, P.h, py, t0)) ||
+        launched(c, "k_cols", launch_cols(st, t0, P.w, P.h, py, t1)) ||
+        launched(c, "k_subsample", launch_subsample(st, t1, P.w, d->subsampling, L.img, L.w, L.h)))
+      return -1;
+  }
+  for (int l = 0; l < d->nlevels; ++l) {
+    Level &L = S.lv[l];
+    if (launched(c, "k_rows", launch_rows(st, L.img, L.w, L.h, gd, t0)) ||
+        launched(c, "k_cols", launch_cols(st, t0, L.w, L.h, gg, L.gx)) ||
+        launched(c, "k_rows", launch_rows(st, L.img, L.w, L.h, gg, t0)) ||
+        launched(c, "k_cols", launch_cols(st, t0, L.w, L.h, gd, L.gy)))
+      return -1;
+  }
+  return 0;
+}
+
+DefTaps default_taps(const klt_hip_pyr_desc *d) {
+  DefTaps T;
+  const RTaps s = reverse_taps(d->smooth), g = reverse_taps(d->grad_gauss);
+  const RTaps dd = reverse_taps(d->grad_deriv), p = reverse_taps(d->pyr);
+  for (int m = 0; m < 5; ++m) T.s[m] = s.k[m];
+  for (int m = 0; m < 7; ++m) {
+    T.g[m] = g.k[m];
+    T.d[m] = dd.k[m];
+  }
+  for (int m = 0; m < 21; ++m) T.p[m] = d->nlevels > 1 ? p.k[m] : 0.0f;
+  return T;
+}
+
+// Level 0 of the fused pyramid for F frames, rows [r0, r1) (global
+// coordinates; every built value is the full-frame value).  Whole 32-row tiles:
+// the rows actually built are returned in r0/r1.
+int launch_l0(klt_hip_ctx *c, hipStream_t st, const uint8_t *src, long pitch, long stride, int W, int H,
+              const DefTaps &T, int vec_u8, int vec_out, float *img, float *gx, float *gy, float *hs, int W1,
+              int do_hs, long fs0, long fsh, int F, int &r0, int &r1) {
+  if (r1 <= r0 || F <= 0) return 0;
+  const int TH = geom::L0_TH;
+  const int nty = (H + TH - 1) / TH;
+  const int ty0 = r0 / TH, ty1 = r1 >= H ? nty : clampi((r1 + TH - 1) / TH, ty0, nty);
+  r0 = ty0 * TH;
+  r1 = ty1 >= nty ? H : ty1 * TH;
+  return launched(c, "k_pyr_l0", launch_pyr_l0(st, src, (int)pitch, stride, W, H, T, vec_u8, vec_out, img, gx, gy,
+                                               hs, W1, do_hs, fs0, fsh, F, ty0, ty1));
+}
+
+int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
+                hipStream_t st) {
+  Slot &S = c->slot[s];
+  const int W = d->ncols, H = d->nrows;
+  const DefTaps T = default_taps(d);
+  const bool two = d->nlevels == 2;
+  const int W1 = two ? S.lv[1].w : 0, H1 = two ? S.lv[1].h : 0;
+  if (two && grow(c, &c->d_hs, &c->hs_cap, (size_t)hs_size(W1 > 0 ? W1 : 1, H))) return -1;
+  if ((long)W * H == 0) return 0;
+  const int vec_u8 = (W % 4 == 0 && W >= 16 && pitch % 4 == 0 && ((uintptr_t)src & 3) == 0) ? 1 : 0;
+  const int vec_out = (W % 4 == 0) ? 1 : 0;
+  {
+    TimedScope ts(c, T_L0, st);
+    int r0 = 0, r1 = H;
+    if (launch_l0(c, st, src, pitch, 0L, W, H, T, vec_u8, vec_out, S.lv[0].img, S.lv[0].gx, S.lv[0].gy, c->d_hs,
+                  W1, (two && W1 > 0) ? 1 : 0, 0L, 0L, 1, r0, r1))
+      return -1;
+  }
+  if (two && (long)W1 * H1 > 0) {
+    TimedScope ts(c, T_L1, st);
+    const int vec = (W1 % 4 == 0 && W1 >= 8) ? 1 : 0;
+    const int ty = (H1 + geom::L1_TH - 1) / geom::L1_TH;
+    if (launched(c, "k_pyr_l1", launch_pyr_l1(st, c->d_hs, W1, H, H1, T, vec, S.lv[1].img, S.lv[1].gx, S.lv[1].gy,
+                                              0L, 0L, 1, 0, ty)))
+      return -1;
+  }
+  return 0;
+}
+
+int check_window(klt_hip_ctx *c, const klt_hip_track_desc *d) {
+  const int npx = d->window_width * d->window_height;
+  if (d->window_width < 1 || d->window_height < 1 || npx > 16 * kWave)
+    return fail(c, "track: window %dx%d unsupported (max %d pixels)", d->window_width, d->window_height,
+                16 * kWave);
+  return 0;
+}
+
+void fill_trk_args(const klt_hip_track_desc *d, int nlev, int ss, int ncols, int nrows, TrkArgs &a) {
+  memset(&a, 0, sizeof a);
+  const int npx = d->window_width * d->window_height;
+  a.nlev = nlev;
+  a.ss = (float)ss;
+  a.ww = d->window_width;
+  a.wh = d->window_height;
+  a.max_it = d->max_iterations;
+  a.min_det = d->min_determinant;
+  a.min_disp = d->min_displacement;
+  a.max_res = d->max_residue;
+  a.step = d->step_factor;
+  a.borderx = d->borderx;
+  a.bordery = d->bordery;
+  a.ncols = ncols;
+  a.nrows = nrows;
+  a.li = d->lighting_insensitive;
+  int rp = (npx + 3) & ~3;  // 16-byte rows with an odd slot count: distinct banks per sum
+  if (((rp / 4) & 1) == 0) rp += 4;
+  a.red_pitch = rp;
+}
+
+// fewer features than this: input order (the sort launch would not pay)
+constexpr int kOrderMin = 2048;
+
+// own != nullptr (band mode): only live features with own[0] <= y < own[1]
+int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc *d, const TrkArgs &a,
+                        const TrkFramesArgs &b, float *x, float *y, int *v, int n, const float *own = nullptr) {
+  TimedScope ts(c, T_TRACK, st, b.nframes);
+  const int npx = d->window_width * d->window_height;
+  const bool exact = d->reduction == KLT_HIP_EXACT, li = d->lighting_insensitive != 0;
+  const bool patch = c->track_patch && (d->window_width + 1) * (d->window_height + 1) <= kWave;
+  // the default 7x7 window gets compile-time window geometry (unrolled ordered sums)
+  const bool win7 = d->window_width == 7 && d->window_height == 7;
+  TrkFramesArgs bb = b;
+  if (own || (c->track_order == 0 && n >= kOrderMin)) {
+    if (grow(c, &c->d_perm, &c->perm_cap, (size_t)n)) return -1;
+    if (own && !c->d_count) HIPCHK(c, hipMalloc((void **)&c->d_count, sizeof(int)));
+    if (launched(c, "k_band_order", launch_band_order(st, y, v, n, a.nrows, c->d_perm, own ? own[0] : 0.0f,
+                                                      own ? own[1] : 0.0f, own ? c->d_count : (int *)nullptr)))
+      return -1;
+    if (own) bb.n_dev = c->d_count;
+    const int per = kBlock / kWave, nb = (n + per - 1) / per;
+    bb.perm = c->d_perm;
+    bb.xcd_per = (nb + 7) / 8;
+  }
+  bb.prof = c->prof;
+  bb.count = c->d_trk_count;
+  const TrkFramesArgs &b2 = bb;
+  TrkArgs aa = a;
+  aa.merge_res = c->track_merge;
+  return launched(c, "k_track_frames", launch_track_frames(st, exact, li, patch, win7, npx, aa, b2, x, y, v, n));
+}
+
+// allocate bank k for `frames` pyramids shaped like desc d
+int ensure_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, int frames) {
+  int w = d->ncols, h = d->nrows;
+  K.nlev = d->nlevels;
+  K.ss = d->nlevels > 1 ? d->subsampling : 1;
+  for (int l = 0; l < d->nlevels; ++l) {
+    Level &L = K.lv[l];
+    L.w = w;
+    L.h = h;
+    const size_t need = (size_t)(w > 0 ? w : 1) * (h > 0 ? h : 1) * frames;
+    if (L.cap < need || !L.img) {
+      hipFree(L.img);
+      hipFree(L.gx);
+      hipFree(L.gy);
+      L.img = L.gx = L.gy = nullptr;
+      L.cap = 0;
+      HIPCHK(c, hipMalloc((void **)&L.img, need * sizeof(float)));
+      HIPCHK(c, hipMalloc((void **)&L.gx, need * sizeof(float)));
+      HIPCHK(c, hipMalloc((void **)&L.gy, need * sizeof(float)));
+      L.cap = need;
+    }
+    w /= K.ss;
+    h /= K.ss;
+  }
+  if (d->nlevels == 2) {
+    const size_t need = (size_t)hs_size(K.lv[1].w > 0 ? K.lv[1].w : 1, d->nrows) * frames;
+    if (K.hs_cap < need || !K.hs) {
+      hipFree(K.hs);
+      K.hs = nullptr;
+      K.hs_cap = 0;
+      HIPCHK(c, hipMalloc((void **)&K.hs, need * sizeof(float)));
+      K.hs_cap = need;
+    }
+  }
+  K.frames = frames;
+  return 0;
+}
+
+// fused pyramids of F frames (src + f*stride) into bank K, two launches.
+// Level-0 rows [row_lo, row_hi) are built (whole 32-row tiles, global
+// coordinates, so every built value is the full-frame value) and the level-1
+// tiles whose sigma-3.6 inputs lie inside them; K.vlo/vhi record what is valid.
+int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
+                     long stride, int F, hipStream_t st, int row_lo = 0, int row_hi = 1 << 30) {
+  const int W = d->ncols, H = d->nrows;
+  const DefTaps T = default_taps(d);
+  const bool two = d->nlevels == 2;
+  const int W1 = two ? K.lv[1].w : 0, H1 = two ? K.lv[1].h : 0;
+  if ((long)W * H == 0 || F <= 0) return 0;
+  const int vec_u8 =
+      (W % 4 == 0 && W >= 16 && pitch % 4 == 0 && stride % 4 == 0 && ((uintptr_t)src & 3) == 0) ? 1 : 0;
+  const int vec_out = (W % 4 == 0) ? 1 : 0;
+  const long fs0 = (long)W * H, fsh = hs_size(W1, H), fs1 = (long)W1 * H1;
+  int r0 = clampi(row_lo, 0, H), r1 = row_hi >= H ? H : clampi(row_hi, r0, H);
+  {
+    TimedScope ts(c, T_L0, st, F);
+    if (launch_l0(c, st, src, pitch, stride, W, H, T, vec_u8, vec_out, K.lv[0].img, K.lv[0].gx, K.lv[0].gy, K.hs,
+                  W1, (two && W1 > 0) ? 1 : 0, fs0, fsh, F, r0, r1))
+      return -1;
+  }
+  K.vlo[0] = r0;
+  K.vhi[0] = r1 >= H ? (1 << 30) : r1;
+  if (two && (long)W1 * H1 > 0) {
+    // an L1 tile at rows [y0, y0+TH) reads hs rows [4*y0-20, 4*y0-20+HR) (clamped to the image)
+    const int TH1 = geom::L1_TH;
+    const int nt1 = (H1 + TH1 - 1) / TH1;
+    const int last = geom::L1_HR - 20;  // 4*y0 + last is the last hs row read
+    const int t1lo = r0 == 0 ? 0 : (r0 + 20 + 4 * TH1 - 1) / (4 * TH1);
+    const int t1hi = r1 >= H ? nt1 : (r1 > last ? clampi((r1 - last - 1) / (4 * TH1) + 1, 0, nt1) : 0);
+    K.vlo[1] = t1lo * TH1;
+    K.vhi[1] = t1hi >= nt1 ? (1 << 30) : t1hi * TH1;
+    if (t1hi > t1lo) {
+      TimedScope ts(c, T_L1, st, F);
+      const int vec = (W1 % 4 == 0 && W1 >= 8) ? 1 : 0;
+      if (launched(c, "k_pyr_l1", launch_pyr_l1(st, K.hs, W1, H, H1, T, vec, K.lv[1].img, K.lv[1].gx, K.lv[1].gy,
+                                                fsh, fs1, F, t1lo, t1hi)))
+        return -1;
+    }
+  }
+  return 0;
+}
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+KLT_API int klt_hip_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+KLT_API klt_hip_ctx *klt_hip_ctx_create(int device) {
+  klt_hip_ctx *c = new klt_hip_ctx();
+  if (device < 0) {
+    if (hipGetDevice(&device) != hipSuccess) device = 0;
+  }
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return nullptr;
+  }
+  c->stream = c->own;
+  for (int i = 0; i < 2; ++i) hipEventCreateWithFlags(&c->u8_done[i], hipEventDisableTiming);
+  return c;
+}
+
+KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  if (c->own) hipStreamSynchronize(c->own);
+  if (c->pstream) hipStreamSynchronize(c->pstream);
+  for (auto &S : c->slot)
+    for (auto &L : S.lv) {
+      hipFree(L.img);
+      hipFree(L.gx);
+      hipFree(L.gy);
+    }
+  for (int i = 0; i < 2; ++i) {
+    hipFree(c->d_u8[i]);
+    if (c->h_u8[i]) hipHostFree(c->h_u8[i]);
+    if (c->u8_done[i]) hipEventDestroy(c->u8_done[i]);
+    hipFree(c->d_tmp[i]);
+  }
+  for (auto &K : c->bank) {
+    for (auto &L : K.lv) {
+      hipFree(L.img);
+      hipFree(L.gx);
+      hipFree(L.gy);
+    }
+    hipFree(K.hs);
+  }
+  for (int k = 0; k < 3; ++k) {
+    if (c->ev_bbuilt[k]) hipEventDestroy(c->ev_bbuilt[k]);
+    if (c->ev_bfree[k]) hipEventDestroy(c->ev_bfree[k]);
+  }
+  hipFree(c->d_perm);
+  hipFree(c->d_count);
+  hipFree(c->d_trk_count);
+  if (c->cstream) {
+    hipStreamSynchronize(c->cstream);
+    hipStreamDestroy(c->cstream);
+  }
+  for (int k = 0; k < 2; ++k) {
+    if (c->ev_ring_ready[k]) hipEventDestroy(c->ev_ring_ready[k]);
+    if (c->ev_ring_free[k]) hipEventDestroy(c->ev_ring_free[k]);
+  }
+  hipFree(c->d_ring);
+  delete c->pool;
+  if (c->h_stage) hipHostFree(c->h_stage);
+  for (int k = 0; k < 2; ++k)
+    if (c->ev_stage[k]) hipEventDestroy(c->ev_stage[k]);
+  hipFree(c->d_hs);
+  hipFree(c->d_feat);
+  if (c->h_feat) hipHostFree(c->h_feat);
+  hipFree(c->d_eig);
+  for (void *p : {(void *)c->d_aff_store, (void *)c->d_aff, (void *)c->d_xp, (void *)c->d_yp, (void *)c->d_astage,
+                  (void *)c->d_astate, (void *)c->d_aidx})
+    hipFree(p);
+  for (auto e : c->ev_pool) hipEventDestroy(e);
+  for (auto &v : c->ev_used)
+    for (auto &p : v) {
+      hipEventDestroy(p.first);
+      hipEventDestroy(p.second);
+    }
+  if (c->pstream) {
+    hipStreamSynchronize(c->pstream);
+    hipStreamDestroy(c->pstream);
+  }
+  for (int k = 0; k < KLT_HIP_MAX_SLOTS; ++k) {
+    if (c->ev_built[k]) hipEventDestroy(c->ev_built[k]);
+    if (c->ev_free[k]) hipEventDestroy(c->ev_free[k]);
+  }
+  if (c->ev_start) hipEventDestroy(c->ev_start);
+  if (c->own) hipStreamDestroy(c->own);
+  delete c;
+}
+
+KLT_API const char *klt_hip_last_error(klt_hip_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+KLT_API int klt_hip_set_stream(klt_hip_ctx *c, void *stream) {
+  if (!c) return -1;
+  c->stream = stream ? (hipStream_t)stream : c->own;
+  return 0;
+}
+
+KLT_API void *klt_hip_get_stream(klt_hip_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+KLT_API int klt_hip_sync(klt_hip_ctx *c) {
+  if (use_device(c)) return -1;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+KLT_API int klt_hip_upload_frame(klt_hip_ctx *c, int buf, const unsigned char *host, int ncols,
+                                 int nrows) {
+  if (buf < 0 || buf > 1 || !host || ncols < 0 || nrows < 0) return fail(c, "upload: bad arguments");
+  if (use_device(c)) return -1;
+  const size_t n = (size_t)ncols * nrows;
+  if (n > c->u8_cap) {
+    for (int i = 0; i < 2; ++i) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      hipFree(c->d_u8[i]);
+      if (c->h_u8[i]) hipHostFree(c->h_u8[i]);
+      c->d_u8[i] = nullptr;
+      c->h_u8[i] = nullptr;
+      HIPCHK(c, hipMalloc((void **)&c->d_u8[i], n));
+      HIPCHK(c, hipHostMalloc((void **)&c->h_u8[i], n, hipHostMallocDefault));
+    }
+    c->u8_cap = n;
+  }
+  // the previous copy out of this bounce buffer must have finished
+  HIPCHK(c, hipEventSynchronize(c->u8_done[buf]));
+  // in pieces: the DMA of piece k runs while the host copies piece k+1
+  const size_t piece = c->upload_piece > 0 ? c->upload_piece : n;
+  for (size_t o = 0; o < n; o += piece) {
+    const size_t m = n - o < piece ? n - o : piece;
+    memcpy(c->h_u8[buf] + o, host + o, m);
+    HIPCHK(c, hipMemcpyAsync(c->d_u8[buf] + o, c->h_u8[buf] + o, m, hipMemcpyHostToDevice, c->stream));
+  }
+  HIPCHK(c, hipEventRecord(c->u8_done[buf], c->stream));
+  c->u8_w[buf] = ncols;
+  c->u8_h[buf] = nrows;
+  return 0;
+}
+
+static int build_pyramid_on(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const unsigned char *frame,
+                            long pitch, int buf, hipStream_t st);
+
+KLT_API int klt_hip_build_pyramid(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d,
+                                  const unsigned char *frame, long pitch, int buf) {
+  if (!c) return fail(c, "build_pyramid: null context");
+  if (s < 0 || s >= KLT_HIP_MAX_SLOTS) return fail(c, "build_pyramid: bad slot %d", s);
+  return build_pyramid_on(c, s, d, frame, pitch, buf, c->stream);
+}
+
+static int build_pyramid_on(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const unsigned char *frame,
+                            long pitch, int buf, hipStream_t st) {
+  if (!c || !d) return fail(c, "build_pyramid: null argument");
+  if (s < 0 || s >= KLT_HIP_MAX_SLOTS + 2) return fail(c, "build_pyramid: bad slot %d", s);
+  if (d->nlevels < 1 || d->nlevels > KLT_HIP_MAX_LEVELS) return fail(c, "bad nlevels %d", d->nlevels);
+  if (d->nlevels > 1 && d->subsampling < 2) return fail(c, "bad subsampling %d", d->subsampling);
+  for (const klt_hip_taps *t : {&d->smooth, &d->pyr, &d->grad_gauss, &d->grad_deriv})
+    if (t->width < 0 || t->width > KLT_HIP_MAX_TAPS || (t->width % 2) != 1)
+      if (!(t == &d->pyr && d->nlevels == 1) && !(t == &d->smooth && !d->smooth_input))
+        return fail(c, "build_pyramid: bad tap width %d", t->width);
+  if (use_device(c)) return -1;
+  const uint8_t *src = frame;
+  if (!src) {
+    if (buf < 0 || buf > 1 || !c->d_u8[buf]) return fail(c, "build_pyramid: no uploaded frame");
+    if (c->u8_w[buf] != d->ncols || c->u8_h[buf] != d->nrows)
+      return fail(c, "build_pyramid: uploaded frame is %dx%d, desc %dx%d", c->u8_w[buf], c->u8_h[buf],
+                  d->ncols, d->nrows);
+    src = c->d_u8[buf];
+    pitch = d->ncols;
+  }
+  if (pitch < d->ncols) return fail(c, "build_pyramid: pitch %ld < ncols %d", pitch, d->ncols);
+  if (ensure_slot(c, s, d)) return -1;
+  const bool fz = fused_ok(d) && !c->force_generic;
+  c->slot[s].fused = fz ? 1 : 0;
+  return fz ? build_fused(c, s, d, src, pitch, st) : build_generic(c, s, d, src, pitch, st);
+}
+
+KLT_API int klt_hip_set_path(klt_hip_ctx *c, int force_generic) {
+  if (!c) return -1;
+  c->force_generic = force_generic != 0;
+  return 0;
+}
+
+
+
+KLT_API int klt_hip_set_prof(klt_hip_ctx *c, void *dev) {
+  if (!c) return fail(c, "set_prof: null context");
+  c->prof = (unsigned long long *)dev;  // written by the instrumented tracker only (KLT_TRACK_PROF)
+  return 0;
+}
+
+KLT_API int klt_hip_set_frames_overlap(klt_hip_ctx *c, int overlap) {
+  if (!c) return fail(c, "set_frames_overlap: null context");
+  c->serial_frames = overlap ? 0 : 1;
+  return 0;
+}
+
+KLT_API int klt_hip_set_track_patch(klt_hip_ctx *c, int on) {
+  if (!c) return fail(c, "set_track_patch: null context");
+  c->track_patch = on ? 1 : 0;
+  return 0;
+}
+
+
+KLT_API int klt_hip_set_track_merge(klt_hip_ctx *c, int on) {
+  if (!c) return fail(c, "set_track_merge: null context");
+  c->track_merge = on ? 1 : 0;
+  return 0;
+}
+
+KLT_API int klt_hip_set_track_count(klt_hip_ctx *c, int on) {
+  if (!c) return fail(c, "set_track_count: null context");
+  if (use_device(c)) return -1;
+  HIPCHK(c, hipDeviceSynchronize());  // no tracker launch still holds the old pointer
+  if (!on) {
+    hipFree(c->d_trk_count);
+    c->d_trk_count = nullptr;
+    return 0;
+  }
+  const size_t bytes = 2 * kCountSlots * sizeof(unsigned long long);
+  if (!c->d_trk_count) HIPCHK(c, hipMalloc((void **)&c->d_trk_count, bytes));
+  HIPCHK(c, hipMemset(c->d_trk_count, 0, bytes));
+  return 0;
+}
+
+KLT_API int klt_hip_get_track_count(klt_hip_ctx *c, unsigned long long *solves, unsigned long long *passes,
+                                    int reset) {
+  if (!c || !solves || !passes) return fail(c, "get_track_count: null argument");
+  if (!c->d_trk_count) return fail(c, "get_track_count: counting is off (klt_hip_set_track_count)");
+  if (use_device(c)) return -1;
+  unsigned long long h[2 * kCountSlots];
+  HIPCHK(c, hipDeviceSynchronize());  // every stream the tracker may have run on
+  HIPCHK(c, hipMemcpy(h, c->d_trk_count, sizeof h, hipMemcpyDeviceToHost));
+  *solves = *passes = 0;
+  for (int k = 0; k < kCountSlots; ++k) {
+    *solves += h[k];
+    *passes += h[kCountSlots + k];
+  }
+  if (reset) HIPCHK(c, hipMemset(c->d_trk_count, 0, sizeof h));
+  return 0;
+}
+
+KLT_API int klt_hip_set_track_order(klt_hip_ctx *c, int input_order) {
+  if (!c) return fail(c, "set_track_order: null context");
+  c->track_order = input_order ? 1 : 0;
+  return 0;
+}
+
+KLT_API int klt_hip_fused_path(klt_hip_ctx *c, const klt_hip_pyr_desc *d) {
+  if (!c || !d) return fail(c, "fused_path: null argument");
+  return fused_ok(d) && !c->force_generic ? 1 : 0;
+}
+
+KLT_API int klt_hip_pyramid_path(klt_hip_ctx *c, int s) {
+  if (!c || s < 0 || s >= KLT_HIP_MAX_SLOTS) return -1;
+  return c->slot[s].fused;
+}
+
+KLT_API int klt_hip_level_dims(klt_hip_ctx *c, int s, int l, int *w, int *h) {
+  if (!c || s < 0 || s >= KLT_HIP_MAX_SLOTS || l < 0 || l >= c->slot[s].nlev) return fail(c, "bad slot/level");
+  *w = c->slot[s].lv[l].w;
+  *h = c->slot[s].lv[l].h;
+  return 0;
+}
+
+KLT_API const float *klt_hip_level_ptr(klt_hip_ctx *c, int s, int l, int which) {
+  if (!c || s < 0 || s >= KLT_HIP_MAX_SLOTS || l < 0 || l >= c->slot[s].nlev) return nullptr;
+  const Level &L = c->slot[s].lv[l];
+  return which == 0 ? L.img : (which == 1 ? L.gx : L.gy);
+}
+
+KLT_API int klt_hip_download_level(klt_hip_ctx *c, int s, int l, int which, float *host) {
+  const float *p = klt_hip_level_ptr(c, s, l, which);
+  if (!p) return fail(c, "download_level: bad slot/level");
+  if (use_device(c)) return -1;
+  const Level &L = c->slot[s].lv[l];
+  HIPCHK(c, hipMemcpyAsync(host, p, sizeof(float) * L.w * L.h, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// A host feature list packed into the context's pinned block h_feat
+// (x | y | val).  The kernels of the per-call path read and write it in place
+// (pinned host memory is mapped into the device's address space): no copy
+// engine, no copy-to-kernel handoff.  The previous call is complete (every
+// host-list call ends with a stream synchronize).
+int feat_pack(klt_hip_ctx *c, const float *x, const float *y, const int *val, int n) {
+  if (n <= 0) return 0;
+  if ((size_t)n > c->f_cap) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(c->d_feat);
+    if (c->h_feat) hipHostFree(c->h_feat);
+    c->d_feat = c->h_feat = nullptr;
+    c->d_fx = c->d_fy = nullptr;
+    c->d_fv = nullptr;
+    c->f_cap = 0;
+    HIPCHK(c, hipMalloc((void **)&c->d_feat, 3 * sizeof(float) * n));
+    HIPCHK(c, hipHostMalloc((void **)&c->h_feat, 3 * sizeof(float) * n, hipHostMallocDefault));
+    c->f_cap = (size_t)n;
+  }
+  c->d_fx = c->d_feat;
+  c->d_fy = c->d_feat + n;
+  c->d_fv = reinterpret_cast<int *>(c->d_feat + 2 * (size_t)n);
+  memcpy(c->h_feat, x, sizeof(float) * n);
+  memcpy(c->h_feat + n, y, sizeof(float) * n);
+  memcpy(c->h_feat + 2 * (size_t)n, val, sizeof(int) * n);
+  return 0;
+}
+
+// ... or copied into the device block (d_fx | d_fy | d_fv) in one H2D copy
+int feat_stage_in(klt_hip_ctx *c, const float *x, const float *y, const int *val, int n) {
+  if (n <= 0) return 0;
+  if (feat_pack(c, x, y, val, n)) return -1;
+  HIPCHK(c, hipMemcpyAsync(c->d_feat, c->h_feat, 3 * sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+  return 0;
+}
+
+// the pinned block back into the host list once the stream is done with it
+int feat_unpack(klt_hip_ctx *c, float *x, float *y, int *val, int n) {
+  if (n <= 0) return 0;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  memcpy(x, c->h_feat, sizeof(float) * n);
+  memcpy(y, c->h_feat + n, sizeof(float) * n);
+  memcpy(val, c->h_feat + 2 * (size_t)n, sizeof(int) * n);
+  return 0;
+}
+
+KLT_API int klt_hip_track(klt_hip_ctx *c, int s1, int s2, const klt_hip_track_desc *d, float *x, float *y,
+                          int *val, int n, int on_device) {
+  if (!c || !d) return fail(c, "track: null argument");
+  if (s1 < 0 || s1 >= KLT_HIP_MAX_SLOTS || s2 < 0 || s2 >= KLT_HIP_MAX_SLOTS) return fail(c, "track: bad slot");
+  const Slot &A = c->slot[s1], &B = c->slot[s2];
+  if (A.nlev < 1 || A.nlev != B.nlev) return fail(c, "track: slots not built / level mismatch");
+  for (int l = 0; l < A.nlev; ++l)
+    if (A.lv[l].w != B.lv[l].w || A.lv[l].h != B.lv[l].h) return fail(c, "track: slot size mismatch");
+  if (check_window(c, d)) return -1;
+  const int npx = d->window_width * d->window_height;
+  if (n <= 0) return 0;
+  if (use_device(c)) return -1;
+  TrkArgs a;
+  fill_trk_args(d, A.nlev, A.ss, A.lv[0].w, A.lv[0].h, a);
+  for (int l = 0; l < A.nlev; ++l) {
+    a.A[l] = {A.lv[l].img, A.lv[l].gx, A.lv[l].gy, A.lv[l].w, A.lv[l].h};
+    a.B[l] = {B.lv[l].img, B.lv[l].gx, B.lv[l].gy, B.lv[l].w, B.lv[l].h};
+  }
+
+  float *x_d = x, *y_d = y;
+  int *v_d = val;
+  if (!on_device) {
+    if (c->feat_zero_copy) {
+      if (feat_pack(c, x, y, val, n)) return -1;
+      x_d = c->h_feat;
+      y_d = c->h_feat + n;
+      v_d = reinterpret_cast<int *>(c->h_feat + 2 * (size_t)n);
+    } else {
+      if (feat_stage_in(c, x, y, val, n)) return -1;
+      x_d = c->d_fx;
+      y_d = c->d_fy;
+      v_d = c->d_fv;
+    }
+  }
+  {
+    // one frame through the batched kernels: frame 0 tracks a.A -> a.B, no table
+    TrkFramesArgs b;
+    memset(&b, 0, sizeof b);
+    b.nframes = 1;
+    if (track_frames_launch(c, c->stream, d, a, b, x_d, y_d, v_d, n)) return -1;
+  }
+  if (!on_device) {
+    if (!c->feat_zero_copy)
+      HIPCHK(c, hipMemcpyAsync(c->h_feat, c->d_feat, 3 * sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+    return feat_unpack(c, x, y, val, n);
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// affine consistency check (include/klt_hip.h)
+// ---------------------------------------------------------------------------
+KLT_API int klt_hip_affine_reserve(klt_hip_ctx *c, int n, int ww, int wh) {
+  if (!c) return fail(c, "affine_reserve: null context");
+  if (n < 0 || ww < 1 || wh < 1) return fail(c, "affine_reserve: bad size");
+  if (use_device(c)) return -1;
+  const int S = (ww + 2) * (wh + 2);
+  const size_t need = (size_t)(n ? n : 1) * 3 * S;
+  if (c->d_aff_store && c->aff_S == S && c->aff_store_cap >= need) return 0;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  hipFree(c->d_aff_store);
+  c->d_aff_store = nullptr;
+  c->aff_store_cap = 0;
+  HIPCHK(c, hipMalloc((void **)&c->d_aff_store, sizeof(float) * need));
+  c->aff_store_cap = need;
+  c->aff_S = S;
+  return 1;
+}
+
+static int affine_move(klt_hip_ctx *c, int dir, const int *idx, int m, float *win) {
+  if (!c || (m > 0 && (!idx || !win))) return fail(c, "affine windows: null argument");
+  if (m <= 0) return 0;
+  if (!c->d_aff_store) return fail(c, "affine windows: no store (klt_hip_affine_reserve)");
+  const int s3 = 3 * c->aff_S;
+  const size_t cap_feat = c->aff_store_cap / s3;
+  for (int j = 0; j < m; ++j)
+    if (idx[j] < 0 || (size_t)idx[j] >= cap_feat) return fail(c, "affine windows: index %d out of range", idx[j]);
+  if (use_device(c)) return -1;
+  if (grow(c, &c->d_astage, &c->astage_cap, (size_t)m * s3) || grow(c, &c->d_aidx, &c->aidx_cap, (size_t)m))
+    return -1;
+  HIPCHK(c, hipMemcpyAsync(c->d_aidx, idx, sizeof(int) * m, hipMemcpyHostToDevice, c->stream));
+  if (dir == 0)
+    HIPCHK(c, hipMemcpyAsync(c->d_astage, win, sizeof(float) * m * s3, hipMemcpyHostToDevice, c->stream));
+  if (launched(c, "k_affine_move", launch_affine_move(c->stream, dir, c->d_aidx, m, s3, c->d_astage, c->d_aff_store)))
+    return -1;
+  if (dir == 1)
+    HIPCHK(c, hipMemcpyAsync(win, c->d_astage, sizeof(float) * m * s3, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+KLT_API int klt_hip_affine_put(klt_hip_ctx *c, const int *idx, int m, const float *win) {
+  return affine_move(c, 0, idx, m, const_cast<float *>(win));
+}
+
+KLT_API int klt_hip_affine_get(klt_hip_ctx *c, const int *idx, int m, float *win) {
+  return affine_move(c, 1, idx, m, win);
+}
+
+KLT_API int klt_hip_track_affine(klt_hip_ctx *c, int s1, int s2, const klt_hip_track_desc *d,
+                                 const klt_hip_affine_desc *ad, float *x, float *y, int *val, float *aff,
+                                 int *state, int n) {
+  if (!c || !d || !ad || (n > 0 && (!x || !y || !val || !aff || !state)))
+    return fail(c, "track_affine: null argument");
+  if (ad->mode < 0 || ad->mode > 2) return fail(c, "track_affine: mode %d (0, 1 or 2)", ad->mode);
+  if (ad->window_width < 3 || ad->window_height < 3 || ad->window_width % 2 == 0 || ad->window_height % 2 == 0)
+    return fail(c, "track_affine: affine window %dx%d must be odd and >= 3", ad->window_width,
+                ad->window_height);
+  if (n <= 0) return 0;
+  if (s1 < 0 || s1 >= KLT_HIP_MAX_SLOTS || s2 < 0 || s2 >= KLT_HIP_MAX_SLOTS)
+    return fail(c, "track_affine: bad slot");
+  const int S = (ad->window_width + 2) * (ad->window_height + 2);
+  if (!c->d_aff_store || c->aff_S != S || c->aff_store_cap < (size_t)n * 3 * S)
+    return fail(c, "track_affine: window store not reserved for %d features (klt_hip_affine_reserve)", n);
+  if (use_device(c)) return -1;
+  if (grow(c, &c->d_aff, &c->aff_cap, (size_t)n * 6) || grow(c, &c->d_astate, &c->astate_cap, (size_t)n) ||
+      grow(c, &c->d_xp, &c->xp_cap, (size_t)n) || grow(c, &c->d_yp, &c->yp_cap, (size_t)n))
+    return -1;
+  // positions before the translation track: the window is stored around them
+  HIPCHK(c, hipMemcpyAsync(c->d_xp, x, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_yp, y, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_aff, aff, sizeof(float) * n * 6, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_astate, state, sizeof(int) * n, hipMemcpyHostToDevice, c->stream));
+  if (feat_stage_in(c, x, y, val, n)) return -1;
+  if (klt_hip_track(c, s1, s2, d, c->d_fx, c->d_fy, c->d_fv, n, 1)) return -1;
+  const Slot &A = c->slot[s1], &B = c->slot[s2];
+  AffArgs a;
+  memset(&a, 0, sizeof a);
+  a.ai = A.lv[0].img;
+  a.agx = A.lv[0].gx;
+  a.agy = A.lv[0].gy;
+  a.aw = A.lv[0].w;
+  a.ah = A.lv[0].h;
+  a.bi = B.lv[0].img;
+  a.bgx = B.lv[0].gx;
+  a.bgy = B.lv[0].gy;
+  a.bw = B.lv[0].w;
+  a.bh = B.lv[0].h;
+  a.xp = c->d_xp;
+  a.yp = c->d_yp;
+  a.x = c->d_fx;
+  a.y = c->d_fy;
+  a.v = c->d_fv;
+  a.xo = c->d_fx;
+  a.yo = c->d_fy;
+  a.aff = c->d_aff;
+  a.state = c->d_astate;
+  a.store = c->d_aff_store;
+  a.n = n;
+  a.mode = ad->mode;
+  a.ww = ad->window_width;
+  a.wh = ad->window_height;
+  a.max_it = ad->max_iterations;
+  a.li = ad->lighting_insensitive;
+  a.min_det = ad->min_determinant;
+  a.th = ad->min_displacement;
+  a.th_aff = ad->affine_min_displacement;
+  a.max_res = ad->max_residue;
+  a.mdd = ad->max_displacement_differ;
+  a.step = ad->step_factor;
+  if (launched(c, "k_affine", launch_affine(c->stream, a))) return -1;
+  HIPCHK(c, hipMemcpyAsync(x, c->d_fx, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(y, c->d_fy, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(val, c->d_fv, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(aff, c->d_aff, sizeof(float) * n * 6, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(state, c->d_astate, sizeof(int) * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// Pipelined sequence: pyramids are built on a second stream one frame ahead of
+// the tracker.  Three slots rotate: frame t's pyramid goes into the slot that
+// held frame t-3, which the tracker released after tracking t-3 -> t-2.
+KLT_API int klt_hip_track_sequence(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
+                                   const unsigned char *frames, long pitch, long stride, int t0, int nsteps,
+                                   float *x, float *y, int *val, int n, int *cur_slot) {
+  if (!c || !pd || !td || !frames || !cur_slot) return fail(c, "track_sequence: null argument");
+  if (*cur_slot < 0 || *cur_slot > 2) return fail(c, "track_sequence: cur_slot must be 0, 1 or 2");
+  if (nsteps <= 0) return 0;
+  if (use_device(c)) return -1;
+  if (!c->pstream) {
+    HIPCHK(c, hipStreamCreateWithFlags(&c->pstream, hipStreamNonBlocking));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
+    for (int k = 0; k < 3; ++k) {
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_built[k], hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_free[k], hipEventDisableTiming));
+    }
+  }
+  // the pyramid stream starts behind everything already queued on the tracking stream
+  HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
+  HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_start, 0));
+  hipStream_t track_stream = c->stream;
+  for (int k = 0; k < nsteps; ++k) {
+    const int prev = *cur_slot, next = (prev + 1) % 3;
+    HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_free[next], 0));
+    if (build_pyramid_on(c, next, pd, frames + (long)(t0 + k) * stride, pitch, 0, c->pstream)) return -1;
+    HIPCHK(c, hipEventRecord(c->ev_built[next], c->pstream));
+    HIPCHK(c, hipStreamWaitEvent(track_stream, c->ev_built[next], 0));
+    if (klt_hip_track(c, prev, next, td, x, y, val, n, 1)) return -1;
+    HIPCHK(c, hipEventRecord(c->ev_free[prev], track_stream));
+    *cur_slot = next;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// batched frames: pyramids of `chunk` frames per pair of launches into one of
+// three banks on the pyramid stream, one k_track_frames launch per chunk on
+// the tracking stream.  Bank k is rebuilt only after the chunk that used its
+// last frame as the previous pyramid has been tracked (ev_bfree[k]).
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int kSeedSlot = KLT_HIP_MAX_SLOTS, kScratchSlot = KLT_HIP_MAX_SLOTS + 1;
+
+TrkLevel prev_level(klt_hip_ctx *c, int l) {
+  if (c->prev.bank < 0) {
+    const Level &L = c->slot[c->prev.slot].lv[l];
+    return TrkLevel{L.img, L.gx, L.gy, L.w, L.h};
+  }
+  const Bank &K = c->bank[c->prev.bank];
+  const Level &L = K.lv[l];
+  const long off = (long)c->prev.frame * L.w * L.h;
+  return TrkLevel{L.img + off, L.gx + off, L.gy + off, L.w, L.h, K.vlo[l], K.vhi[l]};
+}
+
+bool bank_fits(const Bank &K, const klt_hip_pyr_desc *d, int F) {
+  if (K.nlev != d->nlevels) return false;
+  int w = d->ncols, h = d->nrows;
+  for (int l = 0; l < d->nlevels; ++l) {
+    const Level &L = K.lv[l];
+    if (L.w != w || L.h != h || !L.img || L.cap < (size_t)(w > 0 ? w : 1) * (h > 0 ? h : 1) * F) return false;
+    w /= K.ss;
+    h /= K.ss;
+  }
+  if (d->nlevels == 2 && K.hs_cap < (size_t)(K.lv[1].w > 0 ? K.lv[1].w : 1) * d->nrows * F) return false;
+  return true;
+}
+
+int copy_level_planes(klt_hip_ctx *c, const Level &from, float *img, float *gx, float *gy, hipStream_t st) {
+  const size_t b = sizeof(float) * (size_t)from.w * from.h;
+  if (!b) return 0;
+  HIPCHK(c, hipMemcpyAsync(img, from.img, b, hipMemcpyDeviceToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(gx, from.gx, b, hipMemcpyDeviceToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(gy, from.gy, b, hipMemcpyDeviceToDevice, st));
+  return 0;
+}
+}  // namespace
+
+KLT_API int klt_hip_frames_begin(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const unsigned char *frame,
+                                 long pitch) {
+  if (!c || !pd || !frame) return fail(c, "frames_begin: null argument");
+  if (use_device(c)) return -1;
+  if (build_pyramid_on(c, kSeedSlot, pd, frame, pitch, 0, c->stream)) return -1;
+  c->prev = PrevRef{-1, 0, kSeedSlot};
+  c->frames_ready = true;
+  return 0;
+}
+
+KLT_API int klt_hip_frames_begin_slot(klt_hip_ctx *c, int slot) {
+  if (!c) return fail(c, "frames_begin_slot: null context");
+  if (slot < 0 || slot >= KLT_HIP_MAX_SLOTS || c->slot[slot].nlev < 1)
+    return fail(c, "frames_begin_slot: slot %d is not built", slot);
+  c->prev = PrevRef{-1, 0, slot};
+  c->frames_ready = true;
+  return 0;
+}
+
+namespace {
+struct BandSpec {
+  float own[2];        // features owned: own[0] <= y < own[1] (level-0 rows) at the chunk start
+  int row_lo, row_hi;  // level-0 rows to build
+  int *escape;         // device flag
+};
+
+int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
+                      const unsigned char *frames, long pitch, long stride, int nframes, int chunk, float *x,
+                      float *y, int *val, int n, float *tab_x, float *tab_y, int *tab_val, long tab_stride,
+                      const BandSpec *band) {
+  if (!c || !pd || !td) return fail(c, "track_frames: null argument");
+  if (!c->frames_ready) return fail(c, "track_frames: no previous pyramid (call klt_hip_frames_begin)");
+  if (nframes < 0 || chunk < 1 || n < 0) return fail(c, "track_frames: bad nframes/chunk/n");
+  if (nframes > 0 && !frames) return fail(c, "track_frames: null frames");
+  if (n > 0 && (!x || !y || !val)) return fail(c, "track_frames: null feature arrays");
+  const int ntab = (tab_x != nullptr) + (tab_y != nullptr) + (tab_val != nullptr);
+  if (ntab != 0 && ntab != 3) return fail(c, "track_frames: give all three table arrays or none");
+  if (ntab && tab_stride < n) return fail(c, "track_frames: table stride %ld < n %d", tab_stride, n);
+  if (pitch < pd->ncols) return fail(c, "track_frames: pitch %ld < ncols %d", pitch, pd->ncols);
+  if (check_window(c, td)) return -1;
+  {
+    const TrkLevel p0 = prev_level(c, 0);
+    int nl = c->prev.bank < 0 ? c->slot[c->prev.slot].nlev : c->bank[c->prev.bank].nlev;
+    if (p0.w != pd->ncols || p0.h != pd->nrows || nl != pd->nlevels)
+      return fail(c, "track_frames: frames are %dx%d/%d levels, previous pyramid %dx%d/%d", pd->ncols,
+                  pd->nrows, pd->nlevels, p0.w, p0.h, nl);
+  }
+  if (nframes == 0) return 0;
+  if (use_device(c)) return -1;
+  if (!c->pstream) {
+    HIPCHK(c, hipStreamCreateWithFlags(&c->pstream, hipStreamNonBlocking));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
+    for (int k = 0; k < 3; ++k) {
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_built[k], hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_free[k], hipEventDisableTiming));
+    }
+  }
+  if (!c->ev_bbuilt[0])
+    for (int k = 0; k < 3; ++k) {
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_bbuilt[k], hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_bfree[k], hipEventDisableTiming));
+    }
+  const int F = chunk < nframes ? chunk : nframes;
+  // banks hold `chunk` frames whatever this call's length, so a short first
+  // call does not force a reallocation (and a drain) in the next one
+  if (!(bank_fits(c->bank[0], pd, chunk) && bank_fits(c->bank[1], pd, chunk) &&
+        bank_fits(c->bank[2], pd, chunk))) {
+    // (re)allocation: drain both streams; a previous pyramid living in a bank
+    // moves to the seed slot first
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->pstream));
+    if (c->prev.bank >= 0) {
+      if (ensure_slot(c, kSeedSlot, pd)) return -1;
+      for (int l = 0; l < pd->nlevels; ++l) {
+        const TrkLevel p = prev_level(c, l);
+        Level from;
+        from.w = p.w;
+        from.h = p.h;
+        from.img = const_cast<float *>(p.img);
+        from.gx = const_cast<float *>(p.gx);
+        from.gy = const_cast<float *>(p.gy);
+        const Level &to = c->slot[kSeedSlot].lv[l];
+        if (copy_level_planes(c, from, to.img, to.gx, to.gy, c->stream)) return -1;
+      }
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      c->prev = PrevRef{-1, 0, kSeedSlot};
+    }
+    for (auto &K : c->bank)
+      if (ensure_bank(c, K, pd, chunk)) return -1;
+  }
+  // the pyramid stream starts behind everything already queued on the tracking stream
+  if (!c->serial_frames) {
+    HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_start, 0));
+  }
+  const bool fz = fused_ok(pd) && !c->force_generic;
+  if (band && !fz) return fail(c, "track_frames_band: needs the fused (default-parameter) pyramid path");
+  TrkArgs a;
+  fill_trk_args(td, pd->nlevels, pd->nlevels > 1 ? pd->subsampling : 1, pd->ncols, pd->nrows, a);
+  if (band) a.escape = band->escape;
+  for (int j0 = 0; j0 < nframes; j0 += F) {
+    const int Fc = F < nframes - j0 ? F : nframes - j0;
+    const int bi = c->bank_next;
+    c->bank_next = (bi + 1) % 3;
+    Bank &K = c->bank[bi];
+    const unsigned char *src = frames + (long)j0 * stride;
+    // overlapped: the pyramid stream builds chunk c+1 while chunk c is tracked;
+    // serial: both on the tracking stream (no two kernels share the CUs)
+    const bool serial = c->serial_frames != 0;
+    hipStream_t ps = serial ? c->stream : c->pstream;
+    // one stream: stream order is the dependency (an event wait would add a queue barrier)
+    if (!serial) HIPCHK(c, hipStreamWaitEvent(ps, c->ev_bfree[bi], 0));
+    if (fz) {
+      if (band ? build_fused_bank(c, K, pd, src, pitch, stride, Fc, ps, band->row_lo, band->row_hi)
+               : build_fused_bank(c, K, pd, src, pitch, stride, Fc, ps))
+        return -1;
+    } else {
+      for (int f = 0; f < Fc; ++f) {
+        if (build_pyramid_on(c, kScratchSlot, pd, src + (long)f * stride, pitch, 0, ps)) return -1;
+        for (int l = 0; l < pd->nlevels; ++l) {
+          const Level &L = c->slot[kScratchSlot].lv[l];
+          const long off = (long)f * L.w * L.h;
+          if (copy_level_planes(c, L, K.lv[l].img + off, K.lv[l].gx + off, K.lv[l].gy + off, ps))
+            return -1;
+        }
+      }
+    }
+    if (!serial) {
+      HIPCHK(c, hipEventRecord(c->ev_bbuilt[bi], ps));
+      HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_bbuilt[bi], 0));
+    }
+    TrkFramesArgs b;
+    memset(&b, 0, sizeof b);
+    for (int l = 0; l < pd->nlevels; ++l) {
+      a.A[l] = prev_level(c, l);
+      a.B[l] = TrkLevel{K.lv[l].img, K.lv[l].gx, K.lv[l].gy, K.lv[l].w, K.lv[l].h, fz ? K.vlo[l] : 0,
+                        fz ? K.vhi[l] : (1 << 30)};
+      b.lfs[l] = (long)K.lv[l].w * K.lv[l].h;
+    }
+    b.nframes = Fc;
+    if (ntab) {
+      b.tx = tab_x + (long)j0 * tab_stride;
+      b.ty = tab_y + (long)j0 * tab_stride;
+      b.tv = tab_val + (long)j0 * tab_stride;
+      b.tstride = tab_stride;
+    }
+    if (n > 0 && track_frames_launch(c, c->stream, td, a, b, x, y, val, n, band ? band->own : nullptr))
+      return -1;
+    if (!serial && c->prev.bank >= 0) HIPCHK(c, hipEventRecord(c->ev_bfree[c->prev.bank], c->stream));
+    c->prev = PrevRef{bi, Fc - 1};
+  }
+  return 0;
+}
+}  // namespace
+
+KLT_API int klt_hip_track_frames(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
+                                 const unsigned char *frames, long pitch, long stride, int nframes, int chunk,
+                                 float *x, float *y, int *val, int n, float *tab_x, float *tab_y, int *tab_val,
+                                 long tab_stride) {
+  return track_frames_impl(c, pd, td, frames, pitch, stride, nframes, chunk, x, y, val, n, tab_x, tab_y, tab_val,
+                           tab_stride, nullptr);
+}
+
+// Host frames: uploaded chunk by chunk into a two-slot device ring on a copy
+// stream (pageable sources, staged by the runtime), so the upload of chunk
+// c+1 overlaps the pyramids and tracking of chunk c.
+KLT_API int klt_hip_track_frames_host(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
+                                      const unsigned char *const *frames, int nframes, int chunk, float *x,
+                                      float *y, int *val, int n, float *tab_x, float *tab_y, int *tab_val,
+                                      long tab_stride) {
+  if (!c || !pd || !td || (nframes > 0 && !frames)) return fail(c, "track_frames_host: null argument");
+  if (chunk < 1 || nframes < 0) return fail(c, "track_frames_host: bad nframes/chunk");
+  if (nframes == 0) return 0;
+  if (use_device(c)) return -1;
+  const long fb = (long)pd->ncols * pd->nrows;
+  const int F = chunk < nframes ? chunk : nframes;
+  if (grow(c, &c->d_ring, &c->ring_cap, (size_t)(2 * F * fb))) return -1;
+  if (!c->cstream) {
+    HIPCHK(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    for (int k = 0; k < 2; ++k) {
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_ring_ready[k], hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_ring_free[k], hipEventDisableTiming));
+    }
+  }
+  if (c->copy_threads > 0 && (!c->pool || c->stage_frame < (size_t)fb)) {
+    if (c->h_stage) {
+      for (int k = 0; k < 2; ++k) HIPCHK(c, hipEventSynchronize(c->ev_stage[k]));
+      HIPCHK(c, hipHostFree(c->h_stage));
+      c->h_stage = nullptr;
+    }
+    HIPCHK(c, hipHostMalloc((void **)&c->h_stage, (size_t)2 * kStageGroup * fb, hipHostMallocDefault));
+    c->stage_frame = (size_t)fb;
+    for (int k = 0; k < 2; ++k)
+      if (!c->ev_stage[k]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_stage[k], hipEventDisableTiming));
+    if (!c->pool) {
+      // thread creation can throw (std::system_error, bad_alloc): no exception
+      // crosses this extern "C" entry; without a pool the runtime stages the copies
+      try {
+        c->pool = new CopyPool(c->copy_threads);
+      } catch (...) {
+        c->pool = nullptr;
+        c->copy_threads = 0;
+      }
+    }
+  }
+  // the ring may still be read by earlier work on the context stream
+  HIPCHK(c, hipEventRecord(c->ev_ring_free[0], c->stream));
+  HIPCHK(c, hipEventRecord(c->ev_ring_free[1], c->stream));
+  auto upload = [&](int j0, int k) -> int {
+    const int nf = F < nframes - j0 ? F : nframes - j0;
+    HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_ring_free[k], 0));
+    for (int f = 0; f < nf; ++f)
+      if (!frames[j0 + f]) return fail(c, "track_frames_host: frame %d is NULL", j0 + f);
+    if (!c->pool) {
+      for (int f = 0; f < nf; ++f)
+        HIPCHK(c, hipMemcpyAsync(c->d_ring + (size_t)(k * F + f) * fb, frames[j0 + f], (size_t)fb,
+                                 hipMemcpyHostToDevice, c->cstream));
+    }
+    for (int g0 = 0; c->pool && g0 < nf; g0 += kStageGroup) {
+      // a group of frames: wait until this group's slots are out of their
+      // last DMA, copy in parallel, then one DMA per frame
+      const int ng = kStageGroup < nf - g0 ? kStageGroup : nf - g0;
+      const int sg = c->stage_next;
+      c->stage_next ^= 1;
+      HIPCHK(c, hipEventSynchronize(c->ev_stage[sg]));
+      unsigned char *slots = c->h_stage + (size_t)sg * kStageGroup * fb;
+      const size_t piece = 512 << 10;
+      try {
+        c->pool->jobs.clear();
+        for (int f = 0; f < ng; ++f)
+          for (size_t o = 0; o < (size_t)fb; o += piece)
+            c->pool->jobs.push_back({slots + (size_t)f * fb + o, frames[j0 + g0 + f] + o,
+                                     (size_t)fb - o < piece ? (size_t)fb - o : piece});
+      } catch (...) {
+        return fail(c, "track_frames_host: out of memory filling the copy jobs");
+      }
+      c->pool->copy();
+      HIPCHK(c, hipMemcpyAsync(c->d_ring + (size_t)(k * F + g0) * fb, slots, (size_t)ng * fb,
+                               hipMemcpyHostToDevice, c->cstream));
+      HIPCHK(c, hipEventRecord(c->ev_stage[sg], c->cstream));
+    }
+    HIPCHK(c, hipEventRecord(c->ev_ring_ready[k], c->cstream));
+    return 0;
+  };
+  if (upload(0, 0)) return -1;
+  for (int j0 = 0, k = 0; j0 < nframes; j0 += F, k ^= 1) {
+    const int nf = F < nframes - j0 ? F : nframes - j0;
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_ring_ready[k], 0));
+    const long off = (long)j0 * tab_stride;
+    if (track_frames_impl(c, pd, td, c->d_ring + (size_t)k * F * fb, pd->ncols, fb, nf, F, x, y, val, n,
+                          tab_x ? tab_x + off : nullptr, tab_y ? tab_y + off : nullptr,
+                          tab_val ? tab_val + off : nullptr, tab_stride, nullptr))
+      return -1;
+    HIPCHK(c, hipEventRecord(c->ev_ring_free[k], c->stream));
+    if (j0 + F < nframes && upload(j0 + F, k ^ 1)) return -1;  // overlaps the chunk just queued
+  }
+  return 0;
+}
+
+KLT_API int klt_hip_track_frames_band(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
+                                      const unsigned char *frames, long pitch, long stride, int nframes,
+                                      float *x, float *y, int *val, int n, float own_lo, float own_hi,
+                                      int row_lo, int row_hi, int *escape) {
+  if (!escape) return fail(c, "track_frames_band: null escape flag");
+  BandSpec bs{{own_lo, own_hi}, row_lo, row_hi, escape};
+  return track_frames_impl(c, pd, td, frames, pitch, stride, nframes, nframes > 0 ? nframes : 1, x, y, val, n,
+                           nullptr, nullptr, nullptr, 0, &bs);
+}
+
+KLT_API int klt_hip_min_eigen(klt_hip_ctx *c, int s, const klt_hip_select_desc *d, int *vals, int *nx,
+                              int *ny) {
+  if (!c || !d) return fail(c, "min_eigen: null argument");
+  if (s < 0 || s >= KLT_HIP_MAX_SLOTS || c->slot[s].nlev < 1) return fail(c, "min_eigen: bad slot");
+  const Level &L = c->slot[s].lv[0];
+  const int hw = d->window_width / 2, hh = d->window_height / 2;
+  const int step = d->nSkippedPixels + 1;
+  if (step < 1) return fail(c, "min_eigen: bad nSkippedPixels");
+  const int bx = d->borderx, by = d->bordery;
+  if (bx < hw || by < hh) return fail(c, "min_eigen: border smaller than window half size");
+  const int cx = L.w - 2 * bx, cy = L.h - 2 * by;
+  const int gx = cx > 0 ? (cx + step - 1) / step : 0;
+  const int gy = cy > 0 ? (cy + step - 1) / step : 0;
+  *nx = gx;
+  *ny = gy;
+  if (!vals) return 0;
+  const long np = (long)gx * gy;
+  if (np == 0) return 0;
+  if (use_device(c)) return -1;
+  if (grow(c, &c->d_eig, &c->eig_cap, (size_t)np)) return -1;
+  {
+    TimedScope ts(c, T_EIG, c->stream);
+    if (launched(c, "k_min_eigen", launch_min_eigen(c->stream, L.gx, L.gy, L.w, bx, by, step, gx, gy, hw, hh,
+                                                    c->d_eig)))
+      return -1;
+  }
+  HIPCHK(c, hipMemcpyAsync(vals, c->d_eig, sizeof(int) * np, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+KLT_API int klt_hip_synth_frames(klt_hip_ctx *c, unsigned long long seed, int t0, int n, int ncols, int nrows,
+                                 unsigned char *dev, long pitch, long fstride) {
+  if (!c || !dev || n < 0 || pitch < ncols) return fail(c, "synth: bad arguments");
+  if (use_device(c)) return -1;
+  const long np = (long)ncols * nrows;
+  if (np == 0 || n == 0) return 0;
+  return launched(c, "k_synth", launch_synth(c->stream, seed, t0, n, ncols, nrows, dev, pitch, fstride));
+}
+
+KLT_API void *klt_hip_malloc(klt_hip_ctx *c, size_t bytes) {
+  void *p = nullptr;
+  if (!c || use_device(c)) return nullptr;
+  if (hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) {
+    fail(c, "hipMalloc(%zu) failed", bytes);
+    return nullptr;
+  }
+  return p;
+}
+
+KLT_API void klt_hip_free(klt_hip_ctx *c, void *p) {
+  if (!c || !p) return;
+  use_device(c);
+  hipFree(p);
+}
+
+KLT_API int klt_hip_memcpy(klt_hip_ctx *c, void *dst, const void *src, size_t bytes, int kind) {
+  if (use_device(c)) return -1;
+  HIPCHK(c, hipMemcpyAsync(dst, src, bytes, (hipMemcpyKind)kind, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+KLT_API int klt_hip_set_timing(klt_hip_ctx *c, int on) {
+  if (!c) return -1;
+  c->timing = on != 0;
+  return 0;
+}
+
+KLT_API int klt_hip_get_timing(klt_hip_ctx *c, klt_hip_timing *out) {
+  if (!c || !out) return -1;
+  if (klt_hip_sync(c)) return -1;
+  double ms[T_N] = {0, 0, 0, 0, 0};
+  int cnt[T_N] = {0, 0, 0, 0, 0};
+  for (int k = 0; k < T_N; ++k) {
+    for (auto &p : c->ev_used[k]) {
+      float t = 0.0f;
+      if (hipEventElapsedTime(&t, p.first, p.second) == hipSuccess) {
+        ms[k] += t;
+        cnt[k]++;
+      }
+      c->ev_pool.push_back(p.first);
+      c->ev_pool.push_back(p.second);
+    }
+    c->ev_used[k].clear();
+  }
+  out->n_pyr_l0 = cnt[T_L0];
+  out->ms_pyr_l0 = ms[T_L0];
+  out->n_pyr_l1 = cnt[T_L1];
+  out->ms_pyr_l1 = ms[T_L1];
+  out->n_track = cnt[T_TRACK];
+  out->ms_track = ms[T_TRACK];
+  out->n_eigen = cnt[T_EIG];
+  out->ms_eigen = ms[T_EIG];
+  out->n_generic = cnt[T_GEN];
+  out->ms_generic = ms[T_GEN];
+  out->frames_pyr_l0 = c->frames_timed[T_L0];
+  out->frames_pyr_l1 = c->frames_timed[T_L1];
+  out->frames_track = c->frames_timed[T_TRACK];
+  for (auto &f : c->frames_timed) f = 0;
+  return 0;
+}
+
+KLT_API int klt_hip_selftest_sqrt(klt_hip_ctx *c, const double *in, double *out, int n) {
+  if (use_device(c)) return -1;
+  double *d = nullptr;
+  HIPCHK(c, hipMalloc((void **)&d, sizeof(double) * 2 * (n ? n : 1)));
+  hipMemcpy(d, in, sizeof(double) * n, hipMemcpyHostToDevice);
+  hipError_t e = launch_selftest_sqrt(d, d + n, n);
+  if (e == hipSuccess) e = hipMemcpy(out, d + n, sizeof(double) * n, hipMemcpyDeviceToHost);
+  hipFree(d);
+  if (e != hipSuccess) return fail(c, "selftest_sqrt: %s", hipGetErrorString(e));
+  return 0;
+}
+
+KLT_API int klt_hip_selftest_copy_pool(int workers, int rounds, size_t max_bytes) {
+  if (workers < 0 || rounds < 0 || max_bytes < 1) return -1;
+  std::vector<unsigned char> src(max_bytes), dst(max_bytes);
+  CopyPool pool(workers);
+  unsigned long long r64 = 0x9E3779B97F4A7C15ull;
+  auto rnd = [&]() {
+    r64 ^= r64 << 13;
+    r64 ^= r64 >> 7;
+    r64 ^= r64 << 17;
+    return r64;
+  };
+  for (int r = 0; r < rounds; ++r) {
+    const size_t n = 1 + rnd() % max_bytes;
+    const size_t piece = 1 + rnd() % (n < 65536 ? n : 65536);
+    for (size_t i = 0; i < n; ++i) src[i] = (unsigned char)(rnd() >> 29);
+    memset(dst.data(), 0, n);
+    pool.jobs.clear();
+    for (size_t o = 0; o < n; o += piece) pool.jobs.push_back({dst.data() + o, src.data() + o, n - o < piece ? n - o : piece});
+    pool.copy();
+    if (memcmp(dst.data(), src.data(), n) != 0) return r + 1;
+  }
+  return 0;
+}
+
+KLT_API int klt_hip_selftest_div(klt_hip_ctx *c, const float *a, const float *b, float *out, int n) {
+  if (use_device(c)) return -1;
+  float *d = nullptr;
+  HIPCHK(c, hipMalloc((void **)&d, sizeof(float) * 3 * (n ? n : 1)));
+  hipMemcpy(d, a, sizeof(float) * n, hipMemcpyHostToDevice);
+  hipMemcpy(d + n, b, sizeof(float) * n, hipMemcpyHostToDevice);
+  hipError_t e = launch_selftest_div(d, d + n, d + 2 * n, n);
+  if (e == hipSuccess) e = hipMemcpy(out, d + 2 * n, sizeof(float) * n, hipMemcpyDeviceToHost);
+  hipFree(d);
+  if (e != hipSuccess) return fail(c, "selftest_div: %s", hipGetErrorString(e));
+  return 0;
+}

@@ -61,13 +61,12 @@ DEVICE_PROTOS = {
     "klt_hip_build_pyramid": (C.c_int, [V, C.c_int, C.POINTER(PyrDesc), V, C.c_long, C.c_int]),
     "klt_hip_pyramid_path": (C.c_int, [V, C.c_int]),
     "klt_hip_fused_path": (C.c_int, [V, C.POINTER(PyrDesc)]),
-    "klt_hip_set_track_group": (C.c_int, [V, C.c_int]),
     "klt_hip_set_track_order": (C.c_int, [V, C.c_int]),
     "klt_hip_set_track_merge": (C.c_int, [V, C.c_int]),
     "klt_hip_set_track_patch": (C.c_int, [V, C.c_int]),
     "klt_hip_set_track_count": (C.c_int, [V, C.c_int]),
     "klt_hip_get_track_count": (C.c_int, [V, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong), C.c_int]),
-    "klt_hip_set_pyr_l0": (C.c_int, [V, C.c_int, C.c_int]),
+    "klt_hip_set_prof": (C.c_int, [V, V]),
     "klt_hip_set_frames_overlap": (C.c_int, [V, C.c_int]),
     "klt_hip_set_path": (C.c_int, [V, C.c_int]),
     "klt_hip_level_dims": (C.c_int, [V, C.c_int, C.c_int, IP, IP]),

@@ -297,15 +297,14 @@ def test_batched_frames_vs_oracle(gpu, oracle, chunks, calls):
 
 
 @pytest.mark.parametrize("merge", [1, 0])
-def test_track_counts_vs_oracle(gpu, oracle, merge, monkeypatch):
+def test_track_counts_vs_oracle(gpu, oracle, merge):
     """klt_hip_set_track_count: the device's count of 2x2 systems formed equals
     the oracle's Newton loop bodies (both levels, SMALL_DET included) over the
     same sequence, with the deferred residue on and off; the gather passes are
     at least one per system."""
-    monkeypatch.setenv("KLT_AMD_TRACK_MERGE", str(merge))  # read when the device context is created
     frames = synth(gpu, 5150, 640, 480, 12)
     counts = []
-    X, Y, V = batch_sequence(gpu, frames, 1000, [5], counts=counts)
+    X, Y, V = batch_sequence_opts(gpu, frames, 1000, 5, dict(merge=merge), counts=counts)
     oracle.orc_solve_count(1)
     OX, OY, OV = OracleTracker(oracle).harness(frames, 1000, 12, first=frames[0])
     assert_table_equal(X, Y, V, OX, OY, OV)
@@ -419,14 +418,13 @@ def test_patch_gather_edge_positions(gpu, oracle, patch):
     assert np.array_equal(gy.view(np.int32), oy.view(np.int32))
 
 
-@pytest.mark.parametrize("opts", [dict(group=1, patch=0), dict(group=2, patch=1), dict(group=4, patch=1),
-                                  dict(order=1, patch=1), dict(l0=2), dict(l0=3), dict(l0=3, chunk=7),
-                                  dict(merge=0), dict(merge=0, patch=0)])
+@pytest.mark.parametrize("opts", [dict(patch=0), dict(order=1, patch=1), dict(chunk=7), dict(merge=0),
+                                  dict(merge=0, patch=0), dict(order=1, patch=0, chunk=3)])
 def test_tracker_tuning_hooks_do_not_change_results(gpu, oracle, opts):
-    """Features per wave, lane patch, processing order and the level-0 kernel
-    (batched over a chunk's frames) only reorganise work."""
+    """Lane patch, processing order, deferred residue and chunking only
+    reorganise work."""
     frames = synth(gpu, 5151, 640, 480, 8)
-    X, Y, V = batch_sequence_opts(gpu, frames, 3000, opts.get("chunk", 4), opts)
+    X, Y, V = batch_sequence_opts(gpu, frames, 3000, 4, opts)
     assert_table_equal(X, Y, V, *OracleTracker(oracle).harness(frames, 3000, 8, first=frames[0]))
 
 
@@ -440,23 +438,21 @@ def test_overlapped_schedule_1080p(gpu, oracle, opts):
     assert_table_equal(X, Y, V, *OracleTracker(oracle).harness(frames, 5000, 11, first=frames[0]))
 
 
-def batch_sequence_opts(gpu, frames, nfeat, chunk, opts):
+def batch_sequence_opts(gpu, frames, nfeat, chunk, opts, counts=None):
     """batch_sequence with the tuning hooks applied to its device context."""
     orig = gpu.klt_amd_device_context
 
     def hooked(tc):
         ctx = orig(tc)
-        assert gpu.klt_hip_set_track_group(ctx, opts.get("group", 0)) == 0
         assert gpu.klt_hip_set_track_patch(ctx, opts.get("patch", 1)) == 0
         assert gpu.klt_hip_set_track_order(ctx, opts.get("order", 0)) == 0
-        assert gpu.klt_hip_set_pyr_l0(ctx, opts.get("l0", 0), 0) == 0
         assert gpu.klt_hip_set_frames_overlap(ctx, opts.get("overlap", 0)) == 0
         assert gpu.klt_hip_set_track_merge(ctx, opts.get("merge", 1)) == 0
         return ctx
 
     gpu.klt_amd_device_context = hooked
     try:
-        return batch_sequence(gpu, frames, nfeat, [chunk])
+        return batch_sequence(gpu, frames, nfeat, [opts.get("chunk", chunk)], counts=counts)
     finally:
         gpu.klt_amd_device_context = orig
 

@@ -35,7 +35,6 @@ def main():
     ap.add_argument("--input-order", action="store_true", help="tracker: no band ordering")
     ap.add_argument("--no-merge", action="store_true", help="tracker: residue passes of their own")
     ap.add_argument("--table", action="store_true", help="frames: write the feature table (as bench.py does)")
-    ap.add_argument("--group", type=int, default=0, help="tracker: features per wave (0 default, 1, 2, 4)")
     ap.add_argument("--chunk", type=int, default=16, help="frames: frames per batch")
     ap.add_argument("--pyr-only", action="store_true", help="frames: build the batched pyramids, track nothing")
     ap.add_argument("--width", type=int, default=1920)
@@ -48,11 +47,6 @@ def main():
     ap.add_argument("--max-it", type=int, default=0, help="tracker: override max_iterations")
     ap.add_argument("--lost", action="store_true", help="tracker: mark every feature lost (launch floor)")
     ap.add_argument("--window", type=int, default=0, help="tracker: override window width/height")
-    ap.add_argument("--l0prof", action="store_true",
-                    help="k_pyr_l0s pass cycles per workgroup (needs KLT_AMD_LIB=.../lib/prof/libklt_amd.so)")
-    ap.add_argument("--l0-tiles", action="store_true", help="pyramid level 0 by 64x32 tiles (k_pyr_l0)")
-    ap.add_argument("--l0-mode", type=int, default=-1, help="level-0 kernel: 0 tiles, 1 strips, 2 persistent, 3 deferred stores")
-    ap.add_argument("--strip-steps", type=int, default=0, help="k_pyr_l0s steps per strip (0: default)")
     a = ap.parse_args()
 
     import kltamd
@@ -66,13 +60,10 @@ def main():
     lib.klt_amd_set_reduction(tc, 0 if a.reduction == "exact" else 1)
     ctx = lib.klt_amd_device_context(tc)
     lib.klt_hip_set_path(ctx, 1 if a.generic else 0)
-    check(lib, ctx, lib.klt_hip_set_track_group(ctx, a.group), "group")
     check(lib, ctx, lib.klt_hip_set_track_order(ctx, 1 if a.input_order else 0), "order")
     check(lib, ctx, lib.klt_hip_set_track_merge(ctx, 0 if a.no_merge else 1), "merge")
     check(lib, ctx, lib.klt_hip_set_track_patch(ctx, 0 if a.no_patch else 1), "patch")
     check(lib, ctx, lib.klt_hip_set_frames_overlap(ctx, 1 if a.overlap else 0), "overlap")
-    if a.l0_mode >= 0 or a.l0_tiles:
-        check(lib, ctx, lib.klt_hip_set_pyr_l0(ctx, 0 if a.l0_tiles else a.l0_mode, a.strip_steps), "pyr_l0")
     nf = max(a.frames, 2)
     frames = lib.klt_hip_malloc(ctx, nf * W * H)
     check(lib, ctx, lib.klt_hip_synth_frames(ctx, 1080, 0, nf, W, H, frames, W, W * H), "synth")
@@ -206,37 +197,10 @@ def main():
         if a.prof:
             nslot = (n + 64) * 10
             pbuf = lib.klt_hip_malloc(ctx, 8 * nslot)
-            lib.klt_hip_set_prof.restype = C.c_int
-            lib.klt_hip_set_prof.argtypes = [C.c_void_p, C.c_void_p]
             check(lib, ctx, lib.klt_hip_memcpy(ctx, pbuf, np.zeros(nslot, np.uint64).ctypes.data, 8 * nslot, H2D),
                   "zero")
             lib.klt_hip_set_prof(ctx, pbuf)
-        if a.l0prof:
-            lib.klt_hip_l0s_prof.restype = C.c_int
-            lib.klt_hip_l0s_prof.argtypes = [C.c_void_p, C.c_int]
-            lib.klt_hip_sync(ctx)
-            lib.klt_hip_l0s_prof(None, 1)
         rep()
-        if a.l0prof:
-            lib.klt_hip_sync(ctx)
-            g = np.zeros(64, np.uint64)
-            lib.klt_hip_l0s_prof(g.ctypes.data, 0)
-            nwg = max(int(g[5]), 1)
-            out["l0s_workgroups"] = nwg
-            out["l0s_cycles_per_wg"] = {"prologue": float(g[0]) / nwg,
-                                        **{f"pass{k}": float(g[1 + k]) / nwg for k in range(4)}}
-            out["l0s_work_cycles_per_wg"] = {f"wave{wv}": [float(g[8 + 4 * wv + k]) / nwg for k in range(4)]
-                                             for wv in range(5)}
-            nt = max(int(g[21]), 1)
-            out["l0_tiles"] = int(g[21])
-            out["l0_tile_cycles"] = {ph: float(g[16 + k]) / nt for k, ph in enumerate("ABCD")}
-            out["l0_tile_work_cycles"] = {ph: float(g[24 + k]) / nt for k, ph in enumerate("ABCDE")}
-            npt = max(int(g[53]), 1)
-            out["l0p_tiles"] = int(g[53])
-            out["l0p_tile_cycles"] = {ph: float(g[49 + k]) / npt for k, ph in enumerate("BCD")}
-            out["l0p_tile_work_cycles"] = {ph: float(g[57 + k]) / npt for k, ph in enumerate("BCDE")}
-            out["l0p_wave_work"] = {f"wave{w}": [float(g[4 * w + k]) / npt for k in range(1, 4)] for w in range(1, 5)}
-            out["l0p_end"] = {"loader_wait": float(g[62]) / npt, "wave0_to_next": float(g[63]) / npt}
         if a.prof:
             lib.klt_hip_sync(ctx)
             pr = np.empty(nslot, np.uint64)
