@@ -100,6 +100,12 @@ typedef struct klt_hip_ctx klt_hip_ctx;
 /* device < 0: the calling thread's current HIP device */
 klt_hip_ctx *klt_hip_ctx_create(int device);
 void klt_hip_ctx_destroy(klt_hip_ctx *ctx);
+/* back to a fresh context's settings (own stream, default tuning, no timing
+   or counters, no current pyramid), keeping its allocations for reuse */
+int klt_hip_ctx_reset(klt_hip_ctx *ctx);
+int klt_hip_ctx_device(klt_hip_ctx *ctx);
+/* the calling thread's current HIP device, -1 on error */
+int klt_hip_current_device(void);
 const char *klt_hip_last_error(klt_hip_ctx *ctx);
 /* stream: a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL
    restores the context's own non-blocking stream */
@@ -145,6 +151,9 @@ int klt_hip_set_track_patch(klt_hip_ctx *ctx, int on);
 /* instrumented build only (make -C csrc prof): device buffer receiving 10
    u64 phase counters per tracker wave; a no-op buffer in the product build */
 int klt_hip_set_prof(klt_hip_ctx *ctx, void *dev);
+/* host threads of klt_hip_track_frames_host besides the caller (frame copies
+   into pinned staging, table-row delivery); 0..16, default 7 */
+int klt_hip_set_host_threads(klt_hip_ctx *ctx, int workers);
 /* klt_hip_track_frames scheduling: 1 builds chunk c+1's pyramids on a second
    stream while chunk c is tracked; 0 (default) runs both on the context stream. */
 int klt_hip_set_frames_overlap(klt_hip_ctx *ctx, int overlap);
@@ -218,15 +227,31 @@ int klt_hip_track_frames(klt_hip_ctx *ctx, const klt_hip_pyr_desc *pdesc, const 
 /* start the next klt_hip_track_frames* call from pyramid slot `slot` (built by
    klt_hip_build_pyramid) instead of klt_hip_frames_begin's seed */
 int klt_hip_frames_begin_slot(klt_hip_ctx *ctx, int slot);
-/* klt_hip_track_frames for frames in HOST memory (frames[f]: ncols*nrows u8,
-   tight rows): chunks are uploaded on a copy stream into a two-chunk device
-   ring, overlapping the upload of chunk c+1 with the work on chunk c.
-   x/y/val and tab_* are device arrays.  Asynchronous: the host frames must
-   stay valid until the context stream is synchronized (klt_hip_sync). */
+/* copy the pyramid the next klt_hip_track_frames* call would start from (the
+   last tracked frame's) into pyramid slot `slot` (device-to-device) */
+int klt_hip_frames_end_slot(klt_hip_ctx *ctx, int slot);
+
+/* feature-table rows handed back by klt_hip_track_frames_host: tracked frames
+   frame0 .. frame0+nframes-1 (row j at x + j*stride), features [f0, f1).
+   Called from several threads at once, on disjoint feature ranges. */
+typedef void (*klt_hip_rows_fn)(void *user, int frame0, int nframes, int f0, int f1, const float *x,
+                                const float *y, const int *val, long stride);
+/* The batched sequence for frames in HOST memory (frames[f]: ncols*nrows u8,
+   tight rows, pageable): chunk by chunk, a few host threads copy the chunk's
+   frames into pinned staging, one DMA per chunk moves them into a device ring
+   (copy stream), the chunk's pyramids and tracking run on the context stream,
+   its feature-table rows come back by one D2H (a third stream) and are handed
+   to `rows` (optional) -- the upload of chunk c+1 and the delivery of chunk
+   c-1 overlap the device work on chunk c.  seed_first != 0: frames[0] is the
+   image before the first tracked one (its pyramid is built from the uploaded
+   copy) and frames[1..] are tracked; 0: the pyramid of klt_hip_frames_begin*
+   or the previous call is the start and every frame is tracked.  x/y/val are
+   HOST arrays of n features, updated in place.  Returns when every row has
+   been delivered and x/y/val are written. */
 int klt_hip_track_frames_host(klt_hip_ctx *ctx, const klt_hip_pyr_desc *pdesc,
                               const klt_hip_track_desc *tdesc, const unsigned char *const *frames,
-                              int nframes, int chunk, float *x, float *y, int *val, int n, float *tab_x,
-                              float *tab_y, int *tab_val, long tab_stride);
+                              int nframes, int seed_first, int chunk, float *x, float *y, int *val, int n,
+                              klt_hip_rows_fn rows, void *user);
 
 /* one chunk of the feature-sharded sequence (BASELINE config 4), for one rank
    of a row-band decomposition: like klt_hip_track_frames over nframes frames
@@ -264,7 +289,7 @@ int klt_hip_get_timing(klt_hip_ctx *ctx, klt_hip_timing *out);
 /* numerics self-checks used by the tests: f64 sqrt and f32 divide on device */
 int klt_hip_selftest_sqrt(klt_hip_ctx *ctx, const double *in, double *out, int n);
 int klt_hip_selftest_div(klt_hip_ctx *ctx, const float *a, const float *b, float *out, int n);
-/* host-only self-check of the copy pool behind klt_hip_track_frames_host's
+/* host-only self-check of the thread pool behind klt_hip_track_frames_host's
    pinned staging: `rounds` back-to-back groups of pieces (sizes and offsets
    varying per round, up to max_bytes) copied by `workers` threads plus the
    caller, each verified byte for byte.  0 on success, else the failing round

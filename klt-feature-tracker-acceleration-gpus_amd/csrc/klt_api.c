@@ -59,16 +59,50 @@ typedef struct {
 
 enum { SLOT_A = 0, SLOT_B = 1, SLOT_SELECT = 2 };
 
+/* Device contexts of freed tracking contexts are kept (reset, allocations
+   intact) and handed to the next tracking context on the same device, so a
+   caller that creates a context per sequence does not pay for device memory,
+   pinned staging and host threads every time. */
+#define DEV_CACHE 4
+static pthread_mutex_t g_dev_lock = PTHREAD_MUTEX_INITIALIZER;
+static klt_hip_ctx *g_dev_free[DEV_CACHE];
+static int g_dev_nfree;
+
 static klt_hip_ctx *device_of(KLT_TrackingContext tc)
 {
   klt_ctx_full *f = FULL(tc);
   if (!f->dev) {
+    int cur, i;
     if (klt_hip_device_count() <= 0)
       KLTError("(KLT) no HIP device available: libklt_amd runs the tracker on the GPU only");
-    f->dev = klt_hip_ctx_create(-1);
+    cur = klt_hip_current_device();
+    pthread_mutex_lock(&g_dev_lock);
+    for (i = g_dev_nfree - 1; i >= 0; i--)
+      if (klt_hip_ctx_device(g_dev_free[i]) == cur) {
+        f->dev = g_dev_free[i];
+        g_dev_free[i] = g_dev_free[--g_dev_nfree];
+        break;
+      }
+    pthread_mutex_unlock(&g_dev_lock);
+    if (!f->dev) f->dev = klt_hip_ctx_create(-1);
     if (!f->dev) KLTError("(KLT) could not create the HIP context");
   }
   return f->dev;
+}
+
+static void release_device(klt_hip_ctx *dev)
+{
+  int kept = 0;
+  if (!dev) return;
+  if (klt_hip_ctx_reset(dev) == 0) {
+    pthread_mutex_lock(&g_dev_lock);
+    if (g_dev_nfree < DEV_CACHE) {
+      g_dev_free[g_dev_nfree++] = dev;
+      kept = 1;
+    }
+    pthread_mutex_unlock(&g_dev_lock);
+  }
+  if (!kept) klt_hip_ctx_destroy(dev);
 }
 
 static void dev_check(KLT_TrackingContext tc, int rc, const char *what)
@@ -289,7 +323,7 @@ EXPORT void KLTFreeTrackingContext(KLT_TrackingContext tc)
   klt_ctx_full *f;
   if (!tc) return;
   f = FULL(tc);
-  if (f->dev) klt_hip_ctx_destroy(f->dev);
+  release_device(f->dev);
   free(f->aff_owner);
   free(f);
 }
@@ -841,16 +875,31 @@ static int taps_state_eq(const taps_state *a, const taps_state *b)
          !memcmp(&a->deriv, &b->deriv, sizeof a->deriv);
 }
 
-/* KLTStoreFeatureList (storeFeatures.c:15-35) for one column: x, y, val only */
-static void store_column(KLT_FeatureTable ft, int col, int n, const float *x, const float *y, const int *v)
+/* KLTStoreFeatureList (storeFeatures.c:15-35: x, y, val only) for the rows
+   klt_hip_track_frames_host hands back: tracked frame t goes to column
+   col + t.  Called concurrently on disjoint feature ranges; each feature's
+   records are one row of the table, written in frame order. */
+typedef struct {
+  KLT_FeatureTable ft;
+  int col;
+} store_rows_ctx;
+
+static void store_rows(void *user, int frame0, int nframes, int f0, int f1, const float *x, const float *y,
+                       const int *v, long stride)
 {
-  int k;
-  for (k = 0; k < n; k++) {
-    ft->feature[k][col]->x = x[k];
-    ft->feature[k][col]->y = y[k];
-    ft->feature[k][col]->val = v[k];
+  const store_rows_ctx *s = (const store_rows_ctx *)user;
+  int k, j;
+  for (k = f0; k < f1; k++) {
+    KLT_Feature *row = s->ft->feature[k] + s->col + frame0;
+    for (j = 0; j < nframes; j++) {
+      row[j]->x = x[(size_t)j * stride + k];
+      row[j]->y = y[(size_t)j * stride + k];
+      row[j]->val = v[(size_t)j * stride + k];
+    }
   }
 }
+
+#define SEQ_CHUNK 16 /* frames per upload / pyramid / tracking chunk of KLTTrackSequence */
 
 EXPORT void KLTTrackSequence(KLT_TrackingContext tc, KLT_PixelType **frames, int nframes, int ncols, int nrows,
                              KLT_FeatureList fl, KLT_FeatureTable ft, int ft_col)
@@ -860,10 +909,11 @@ EXPORT void KLTTrackSequence(KLT_TrackingContext tc, KLT_PixelType **frames, int
   klt_hip_pyr_desc d1, d2, e1, e2;
   klt_hip_track_desc td;
   taps_state st, after1;
-  int k, i, seq_start, steady, n = fl->nFeatures, T = nframes - 1;
-  float *hx, *hy, *tx = NULL, *ty = NULL;
-  int *hv, *tv = NULL;
-  void *dx, *dy, *dv, *dtx = NULL, *dty = NULL, *dtv = NULL;
+  store_rows_ctx sr;
+  int k, i, seq_start, steady, seed_first, n = fl->nFeatures, T = nframes - 1;
+  const unsigned char *const *src;
+  float *hx, *hy;
+  int *hv;
 
   if (nframes < 2) return;
   window_fix(tc, NULL);
@@ -906,11 +956,20 @@ EXPORT void KLTTrackSequence(KLT_TrackingContext tc, KLT_PixelType **frames, int
     fflush(stderr);
   }
 
+  /* where the first tracked frame starts from: the kept pyramid (sequential
+     mode), or frames[0] -- built from its uploaded copy when the first call's
+     description is the steady one, else here from the host with its own */
+  seed_first = 0;
+  src = (const unsigned char *const *)frames;
   if (seq_start) {
     dev_check(tc, klt_hip_frames_begin_slot(dev, f->last_slot), "sequence start");
+    src++;
+  } else if (!memcmp(&d1, &d2, sizeof d2)) {
+    seed_first = 1;
   } else {
     build_from_host(tc, SLOT_A, 0, frames[0], &d1);
     dev_check(tc, klt_hip_frames_begin_slot(dev, SLOT_A), "sequence start");
+    src++;
   }
   klt_amd_track_desc(tc, &td);
 
@@ -923,39 +982,11 @@ EXPORT void KLTTrackSequence(KLT_TrackingContext tc, KLT_PixelType **frames, int
     hy[k] = fl->feature[k]->y;
     hv[k] = fl->feature[k]->val;
   }
-  dx = klt_hip_malloc(dev, sizeof(float) * (n + 1));
-  dy = klt_hip_malloc(dev, sizeof(float) * (n + 1));
-  dv = klt_hip_malloc(dev, sizeof(int) * (n + 1));
-  if (!dx || !dy || !dv) KLTError("(KLTTrackSequence) device allocation failed");
-  dev_check(tc, klt_hip_memcpy(dev, dx, hx, sizeof(float) * n, 1), "upload");
-  dev_check(tc, klt_hip_memcpy(dev, dy, hy, sizeof(float) * n, 1), "upload");
-  dev_check(tc, klt_hip_memcpy(dev, dv, hv, sizeof(int) * n, 1), "upload");
-  if (ft) {
-    const size_t cells = (size_t)T * (n > 0 ? n : 1);
-    dtx = klt_hip_malloc(dev, sizeof(float) * cells);
-    dty = klt_hip_malloc(dev, sizeof(float) * cells);
-    dtv = klt_hip_malloc(dev, sizeof(int) * cells);
-    tx = (float *)malloc(sizeof(float) * cells);
-    ty = (float *)malloc(sizeof(float) * cells);
-    tv = (int *)malloc(sizeof(int) * cells);
-    if (!dtx || !dty || !dtv || !tx || !ty || !tv) KLTError("(KLTTrackSequence) Out of memory");
-  }
-  dev_check(tc, klt_hip_track_frames_host(dev, &d2, &td, (const unsigned char *const *)(frames + 1), T, 32,
-                                          (float *)dx, (float *)dy, (int *)dv, n, (float *)dtx, (float *)dty,
-                                          (int *)dtv, n),
+  sr.ft = ft;
+  sr.col = ft_col;
+  dev_check(tc, klt_hip_track_frames_host(dev, &d2, &td, src, seed_first ? nframes : nframes - 1, seed_first,
+                                          SEQ_CHUNK, hx, hy, hv, n, ft ? store_rows : NULL, &sr),
             "sequence tracking");
-  dev_check(tc, klt_hip_sync(dev), "sequence tracking");
-  dev_check(tc, klt_hip_memcpy(dev, hx, dx, sizeof(float) * n, 2), "download");
-  dev_check(tc, klt_hip_memcpy(dev, hy, dy, sizeof(float) * n, 2), "download");
-  dev_check(tc, klt_hip_memcpy(dev, hv, dv, sizeof(int) * n, 2), "download");
-  if (ft) {
-    const size_t cells = (size_t)T * n;
-    dev_check(tc, klt_hip_memcpy(dev, tx, dtx, sizeof(float) * cells, 2), "download");
-    dev_check(tc, klt_hip_memcpy(dev, ty, dty, sizeof(float) * cells, 2), "download");
-    dev_check(tc, klt_hip_memcpy(dev, tv, dtv, sizeof(int) * cells, 2), "download");
-    for (i = 0; i < T; i++) store_column(ft, ft_col + i, n, tx + (size_t)i * n, ty + (size_t)i * n,
-                                         tv + (size_t)i * n);
-  }
   for (k = 0; k < n; k++) {
     KLT_Feature ftr = fl->feature[k];
     if (ftr->val < 0) continue; /* untouched, like the reference (:1346) */
@@ -964,26 +995,18 @@ EXPORT void KLTTrackSequence(KLT_TrackingContext tc, KLT_PixelType **frames, int
     ftr->val = hv[k];
     if (hv[k] != KLT_TRACKED) drop_affine(ftr);
   }
-  klt_hip_free(dev, dx);
-  klt_hip_free(dev, dy);
-  klt_hip_free(dev, dv);
-  klt_hip_free(dev, dtx);
-  klt_hip_free(dev, dty);
-  klt_hip_free(dev, dtv);
   free(hx);
   free(hy);
   free(hv);
-  free(tx);
-  free(ty);
-  free(tv);
 
   /* the kernel cache ends where the per-frame loop would leave it */
   pthread_mutex_lock(&g_taps_lock);
   g_taps = st;
   pthread_mutex_unlock(&g_taps_lock);
   if (tc->sequentialMode) { /* the last frame's pyramid carries over, as after the loop */
-    const int slot = f->last_slot == SLOT_A ? SLOT_B : SLOT_A;
-    build_from_host(tc, slot, 1, frames[nframes - 1], &d2);
+    const int slot = (seq_start && f->last_slot == SLOT_A) ? SLOT_B : SLOT_A;
+    dev_check(tc, klt_hip_frames_end_slot(dev, slot), "sequence end");
+    dev_check(tc, klt_hip_sync(dev), "sequence end");
     f->last_slot = slot;
     f->last_w = ncols;
     f->last_h = nrows;

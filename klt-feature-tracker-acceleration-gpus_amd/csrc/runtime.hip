@@ -8,10 +8,12 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <emmintrin.h>
 
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -60,30 +62,27 @@ struct PrevRef {
   int slot = KLT_HIP_MAX_SLOTS;  // the batch seed slot unless klt_hip_frames_begin_slot
 };
 
-// Host copies of caller frames into pinned staging (klt_hip_track_frames_host):
-// a few worker threads and the calling thread split a group of frames into
-// 512 KB pieces.  Every worker takes part in every generation, and copy()
-// returns only when all of them have finished it, so no worker can still be
-// reading the job list when the caller refills it for the next group.
-struct CopyPool {
-  struct Job {
-    unsigned char *dst;
-    const unsigned char *src;
-    size_t n;
-  };
+// Host-side parallel work of klt_hip_track_frames_host: copies of the
+// caller's pageable frames into pinned staging and the delivery of table rows
+// to the caller's callback.  A few worker threads and the calling thread pull
+// task indices of one generation; parallel() returns only when every worker
+// has finished the generation, so no worker still runs the task function when
+// the caller moves on to the next one.
+struct HostPool {
   std::vector<std::thread> th;
   std::mutex m;
   std::condition_variable cv;
-  std::vector<Job> jobs;
+  const std::function<void(size_t)> *fn = nullptr;
+  size_t ntasks = 0;
   std::atomic<size_t> next{0};
   std::atomic<int> finished{0};
   unsigned gen = 0;
   bool stop = false;
 
-  explicit CopyPool(int workers) {
+  explicit HostPool(int workers) {
     for (int i = 0; i < workers; ++i) th.emplace_back([this] { worker(); });
   }
-  ~CopyPool() {
+  ~HostPool() {
     {
       std::lock_guard<std::mutex> l(m);
       stop = true;
@@ -92,7 +91,7 @@ struct CopyPool {
     for (auto &t : th) t.join();
   }
   void run() {
-    for (size_t i; (i = next.fetch_add(1)) < jobs.size();) memcpy(jobs[i].dst, jobs[i].src, jobs[i].n);
+    for (size_t i; (i = next.fetch_add(1)) < ntasks;) (*fn)(i);
   }
   void worker() {
     unsigned seen = 0;
@@ -107,9 +106,12 @@ struct CopyPool {
       finished.fetch_add(1);
     }
   }
-  void copy() {  // jobs filled by the caller
+  // fn(0) .. fn(n-1), on the workers and the calling thread
+  void parallel(size_t n, const std::function<void(size_t)> &f) {
     {
       std::lock_guard<std::mutex> l(m);
+      fn = &f;
+      ntasks = n;
       next = 0;
       finished = 0;
       ++gen;
@@ -120,7 +122,6 @@ struct CopyPool {
   }
 };
 
-constexpr int kStageGroup = 8;  // frames per staging group; two groups of pinned slots
 constexpr int kMaxCopyThreads = 16;  // copy-pool workers per device context, at most
 
 struct klt_hip_ctx {
@@ -146,7 +147,6 @@ struct klt_hip_ctx {
   float *d_fx = nullptr, *d_fy = nullptr;  // views into d_feat
   int *d_fv = nullptr;
   float *d_feat = nullptr, *h_feat = nullptr;
-  size_t upload_piece = 512 << 10;  // klt_hip_upload_frame: bytes per host-copy/DMA piece (0: whole frame)
   int feat_zero_copy = 1;   // klt_hip_track on host lists: kernels use h_feat in place (0: copies)
   size_t f_cap = 0;
   int *d_eig = nullptr;
@@ -168,20 +168,20 @@ struct klt_hip_ctx {
                           // tracker and the pyramid kernels compete for the same CUs; overlap buys ~3 %)
   int *d_perm = nullptr;
   size_t perm_cap = 0;
+  int perm_n = -1, perm_age = 0;  // features of the order in d_perm (-1: none), calls since it was sorted
   int *d_count = nullptr;  // band mode: features owned in this chunk
   unsigned long long *d_trk_count = nullptr;  // klt_hip_set_track_count: {solves, passes}, null when off
-  unsigned char *d_ring = nullptr;  // klt_hip_track_frames_host: 2 chunks of uploaded frames
-  size_t ring_cap = 0;
-  hipStream_t cstream = nullptr;
-  hipEvent_t ev_ring_ready[2] = {}, ev_ring_free[2] = {};
-  // klt_hip_track_frames_host: pinned staging for the caller's pageable
-  // frames, 2 groups of kStageGroup slots (host copy by the pool, then DMA)
-  CopyPool *pool = nullptr;
-  int copy_threads = 4;            // pool workers besides the caller; 0: runtime staging (hipMemcpyAsync from pageable)
-  unsigned char *h_stage = nullptr;
-  size_t stage_frame = 0;          // bytes per slot
-  hipEvent_t ev_stage[2] = {};     // DMA out of group g done
-  int stage_next = 0;
+  // klt_hip_track_frames_host: frames uploaded chunk by chunk.  Two slots per
+  // stage: pinned staging (filled by the pool), the device ring (one DMA per
+  // chunk on cstream), device table rows (written by the tracker) and pinned
+  // table rows (one D2H per chunk on dstream, then handed to the caller)
+  unsigned char *d_ring = nullptr, *h_stage = nullptr;
+  float *d_rows = nullptr, *h_rows = nullptr;
+  size_t ring_cap = 0, stage_cap = 0, drows_cap = 0, hrows_cap = 0;  // bytes
+  hipStream_t cstream = nullptr, dstream = nullptr;
+  hipEvent_t ev_ring_free[2] = {}, ev_dma[2] = {}, ev_tracked[2] = {}, ev_rows[2] = {};
+  HostPool *pool = nullptr;
+  int copy_threads = 7;  // pool workers besides the caller (0: the caller alone)
   unsigned long long *prof = nullptr;  // instrumented build: per-wave tracker phase counters
   Bank bank[3];
   int bank_next = 0;
@@ -260,6 +260,57 @@ struct TimedScope {
 
 
 unsigned xcd_grid(int tiles) { return (unsigned)(8 * ((tiles + 7) / 8)); }
+
+// copy into pinned staging with non-temporal stores: the destination is read
+// only by the DMA engine, so its lines need not be fetched (no read-for-
+// ownership) nor kept in the CPU caches
+void copy_stream(unsigned char *dst, const unsigned char *src, size_t n) {
+  size_t i = 0;
+  const size_t head = (16 - ((uintptr_t)dst & 15)) & 15;
+  if (head) {
+    memcpy(dst, src, head < n ? head : n);
+    i = head < n ? head : n;
+  }
+  for (; i + 64 <= n; i += 64) {
+    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i));
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i + 16));
+    const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i + 32));
+    const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + i + 48));
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i), a);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i + 16), b);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i + 32), c);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(dst + i + 48), d);
+  }
+  if (i < n) memcpy(dst + i, src + i, n - i);
+  _mm_sfence();  // the stores are globally visible before the DMA is queued
+}
+
+// the context's host pool, created on first use (thread creation can throw:
+// no exception crosses an extern "C" entry; without a pool the caller works alone)
+void ensure_pool(klt_hip_ctx *c) {
+  if (c->pool || c->copy_threads <= 0) return;
+  try {
+    c->pool = new HostPool(c->copy_threads);
+  } catch (...) {
+    c->pool = nullptr;
+    c->copy_threads = 0;
+  }
+}
+
+template <class Fn>
+int host_parallel(klt_hip_ctx *c, size_t n, Fn fn) {
+  try {
+    if (c->pool) {
+      const std::function<void(size_t)> f = fn;
+      c->pool->parallel(n, f);
+    } else {
+      for (size_t i = 0; i < n; ++i) fn(i);
+    }
+  } catch (...) {
+    return fail(c, "track_frames_host: host task failed (out of memory?)");
+  }
+  return 0;
+}
 
 int launched(klt_hip_ctx *c, const char *what, hipError_t e) {
   if (e != hipSuccess) return fail(c, "launch %s: %s", what, hipGetErrorString(e));
@@ -431,6 +482,8 @@ void fill_trk_args(const klt_hip_track_desc *d, int nlev, int ss, int ncols, int
 
 // fewer features than this: input order (the sort launch would not pay)
 constexpr int kOrderMin = 2048;
+// one-frame launches re-sort the processing order every this many calls
+constexpr int kOrderReuse = 8;
 
 // own != nullptr (band mode): only live features with own[0] <= y < own[1]
 int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc *d, const TrkArgs &a,
@@ -443,11 +496,21 @@ int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc
   const bool win7 = d->window_width == 7 && d->window_height == 7;
   TrkFramesArgs bb = b;
   if (own || (c->track_order == 0 && n >= kOrderMin)) {
-    if (grow(c, &c->d_perm, &c->perm_cap, (size_t)n)) return -1;
-    if (own && !c->d_count) HIPCHK(c, hipMalloc((void **)&c->d_count, sizeof(int)));
-    if (launched(c, "k_band_order", launch_band_order(st, y, v, n, a.nrows, c->d_perm, own ? own[0] : 0.0f,
-                                                      own ? own[1] : 0.0f, own ? c->d_count : (int *)nullptr)))
-      return -1;
+    // one-frame launches (KLTTrackFeatures) reuse the order of a recent call
+    // with the same feature count: any permutation gives the same results,
+    // and features move little from one frame to the next
+    const bool reuse = !own && b.nframes == 1 && c->perm_n == n && c->perm_age < kOrderReuse;
+    if (reuse) {
+      ++c->perm_age;
+    } else {
+      if (grow(c, &c->d_perm, &c->perm_cap, (size_t)n)) return -1;
+      if (own && !c->d_count) HIPCHK(c, hipMalloc((void **)&c->d_count, sizeof(int)));
+      if (launched(c, "k_band_order", launch_band_order(st, y, v, n, a.nrows, c->d_perm, own ? own[0] : 0.0f,
+                                                        own ? own[1] : 0.0f, own ? c->d_count : (int *)nullptr)))
+        return -1;
+      c->perm_n = own ? -1 : n;  // a band's order lists only the band's features
+      c->perm_age = 0;
+    }
     if (own) bb.n_dev = c->d_count;
     const int per = kBlock / kWave, nb = (n + per - 1) / per;
     bb.perm = c->d_perm;
@@ -602,19 +665,19 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
   hipFree(c->d_perm);
   hipFree(c->d_count);
   hipFree(c->d_trk_count);
-  if (c->cstream) {
-    hipStreamSynchronize(c->cstream);
-    hipStreamDestroy(c->cstream);
-  }
-  for (int k = 0; k < 2; ++k) {
-    if (c->ev_ring_ready[k]) hipEventDestroy(c->ev_ring_ready[k]);
-    if (c->ev_ring_free[k]) hipEventDestroy(c->ev_ring_free[k]);
-  }
+  for (hipStream_t st : {c->cstream, c->dstream})
+    if (st) {
+      hipStreamSynchronize(st);
+      hipStreamDestroy(st);
+    }
+  for (int k = 0; k < 2; ++k)
+    for (hipEvent_t e : {c->ev_ring_free[k], c->ev_dma[k], c->ev_tracked[k], c->ev_rows[k]})
+      if (e) hipEventDestroy(e);
   hipFree(c->d_ring);
+  hipFree(c->d_rows);
   delete c->pool;
   if (c->h_stage) hipHostFree(c->h_stage);
-  for (int k = 0; k < 2; ++k)
-    if (c->ev_stage[k]) hipEventDestroy(c->ev_stage[k]);
+  if (c->h_rows) hipHostFree(c->h_rows);
   hipFree(c->d_hs);
   hipFree(c->d_feat);
   if (c->h_feat) hipHostFree(c->h_feat);
@@ -639,6 +702,43 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
   if (c->ev_start) hipEventDestroy(c->ev_start);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
+}
+
+KLT_API int klt_hip_current_device(void) {
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) return -1;
+  return d;
+}
+
+KLT_API int klt_hip_ctx_device(klt_hip_ctx *c) { return c ? c->device : -1; }
+
+KLT_API int klt_hip_ctx_reset(klt_hip_ctx *c) {
+  if (!c) return -1;
+  if (use_device(c)) return -1;
+  HIPCHK(c, hipDeviceSynchronize());  // nothing of the previous owner is still running
+  c->stream = c->own;
+  c->force_generic = 0;
+  c->track_order = 0;
+  c->track_patch = 1;
+  c->track_merge = 1;
+  c->serial_frames = 1;
+  c->prof = nullptr;
+  c->frames_ready = false;
+  c->timing = false;
+  for (int k = 0; k < T_N; ++k) {
+    for (auto &p : c->ev_used[k]) {
+      c->ev_pool.push_back(p.first);
+      c->ev_pool.push_back(p.second);
+    }
+    c->ev_used[k].clear();
+    c->frames_timed[k] = 0;
+  }
+  hipFree(c->d_trk_count);
+  c->d_trk_count = nullptr;
+  c->perm_n = -1;
+  for (auto &S : c->slot) S.fused = -1;
+  c->err.clear();
+  return 0;
 }
 
 KLT_API const char *klt_hip_last_error(klt_hip_ctx *c) { return c ? c->err.c_str() : "null context"; }
@@ -676,12 +776,20 @@ KLT_API int klt_hip_upload_frame(klt_hip_ctx *c, int buf, const unsigned char *h
   }
   // the previous copy out of this bounce buffer must have finished
   HIPCHK(c, hipEventSynchronize(c->u8_done[buf]));
-  // in pieces: the DMA of piece k runs while the host copies piece k+1
-  const size_t piece = c->upload_piece > 0 ? c->upload_piece : n;
-  for (size_t o = 0; o < n; o += piece) {
-    const size_t m = n - o < piece ? n - o : piece;
-    memcpy(c->h_u8[buf] + o, host + o, m);
-    HIPCHK(c, hipMemcpyAsync(c->d_u8[buf] + o, c->h_u8[buf] + o, m, hipMemcpyHostToDevice, c->stream));
+  // in groups: the host pool copies group g+1 into pinned memory while group
+  // g's DMA runs
+  ensure_pool(c);
+  const size_t group = n >= (1u << 20) ? (n + 3) / 4 : n, piece = 64 << 10;
+  for (size_t o = 0; o < n; o += group) {
+    const size_t m = n - o < group ? n - o : group;
+    unsigned char *dst = c->h_u8[buf] + o;
+    const unsigned char *src = host + o;
+    if (host_parallel(c, (m + piece - 1) / piece, [&](size_t t) {
+          const size_t q = t * piece;
+          copy_stream(dst + q, src + q, m - q < piece ? m - q : piece);
+        }))
+      return -1;
+    HIPCHK(c, hipMemcpyAsync(c->d_u8[buf] + o, dst, m, hipMemcpyHostToDevice, c->stream));
   }
   HIPCHK(c, hipEventRecord(c->u8_done[buf], c->stream));
   c->u8_w[buf] = ncols;
@@ -737,6 +845,18 @@ KLT_API int klt_hip_set_path(klt_hip_ctx *c, int force_generic) {
 KLT_API int klt_hip_set_prof(klt_hip_ctx *c, void *dev) {
   if (!c) return fail(c, "set_prof: null context");
   c->prof = (unsigned long long *)dev;  // written by the instrumented tracker only (KLT_TRACK_PROF)
+  return 0;
+}
+
+KLT_API int klt_hip_set_host_threads(klt_hip_ctx *c, int workers) {
+  if (!c) return fail(c, "set_host_threads: null context");
+  if (workers < 0 || workers > kMaxCopyThreads)
+    return fail(c, "set_host_threads: %d workers (0..%d)", workers, kMaxCopyThreads);
+  if (workers != c->copy_threads) {
+    delete c->pool;  // its workers are idle between calls; joined here
+    c->pool = nullptr;
+    c->copy_threads = workers;
+  }
   return 0;
 }
 
@@ -1143,6 +1263,39 @@ KLT_API int klt_hip_frames_begin_slot(klt_hip_ctx *c, int slot) {
   return 0;
 }
 
+KLT_API int klt_hip_frames_end_slot(klt_hip_ctx *c, int slot) {
+  if (!c) return fail(c, "frames_end_slot: null context");
+  if (slot < 0 || slot >= KLT_HIP_MAX_SLOTS) return fail(c, "frames_end_slot: bad slot %d", slot);
+  if (!c->frames_ready) return fail(c, "frames_end_slot: no current pyramid");
+  if (c->prev.bank < 0 && c->prev.slot == slot) return 0;
+  if (use_device(c)) return -1;
+  const int nl = c->prev.bank < 0 ? c->slot[c->prev.slot].nlev : c->bank[c->prev.bank].nlev;
+  const int ss = c->prev.bank < 0 ? c->slot[c->prev.slot].ss : c->bank[c->prev.bank].ss;
+  const TrkLevel p0 = prev_level(c, 0);
+  klt_hip_pyr_desc d;
+  memset(&d, 0, sizeof d);
+  d.ncols = p0.w;
+  d.nrows = p0.h;
+  d.nlevels = nl;
+  d.subsampling = ss > 1 ? ss : 2;
+  if (ensure_slot(c, slot, &d)) return -1;
+  Slot &S = c->slot[slot];
+  S.ss = ss;
+  S.fused = 1;
+  for (int l = 0; l < nl; ++l) {
+    const TrkLevel p = prev_level(c, l);
+    Level from;
+    from.w = p.w;
+    from.h = p.h;
+    from.img = const_cast<float *>(p.img);
+    from.gx = const_cast<float *>(p.gx);
+    from.gy = const_cast<float *>(p.gy);
+    if (from.w != S.lv[l].w || from.h != S.lv[l].h) return fail(c, "frames_end_slot: level %d size mismatch", l);
+    if (copy_level_planes(c, from, S.lv[l].img, S.lv[l].gx, S.lv[l].gy, c->stream)) return -1;
+  }
+  return 0;
+}
+
 namespace {
 struct BandSpec {
   float own[2];        // features owned: own[0] <= y < own[1] (level-0 rows) at the chunk start
@@ -1287,98 +1440,158 @@ KLT_API int klt_hip_track_frames(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, con
                            tab_stride, nullptr);
 }
 
-// Host frames: uploaded chunk by chunk into a two-slot device ring on a copy
-// stream (pageable sources, staged by the runtime), so the upload of chunk
-// c+1 overlaps the pyramids and tracking of chunk c.
-KLT_API int klt_hip_track_frames_host(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
-                                      const unsigned char *const *frames, int nframes, int chunk, float *x,
-                                      float *y, int *val, int n, float *tab_x, float *tab_y, int *tab_val,
-                                      long tab_stride) {
-  if (!c || !pd || !td || (nframes > 0 && !frames)) return fail(c, "track_frames_host: null argument");
-  if (chunk < 1 || nframes < 0) return fail(c, "track_frames_host: bad nframes/chunk");
-  if (nframes == 0) return 0;
-  if (use_device(c)) return -1;
-  const long fb = (long)pd->ncols * pd->nrows;
-  const int F = chunk < nframes ? chunk : nframes;
-  if (grow(c, &c->d_ring, &c->ring_cap, (size_t)(2 * F * fb))) return -1;
-  if (!c->cstream) {
-    HIPCHK(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
-    for (int k = 0; k < 2; ++k) {
-      HIPCHK(c, hipEventCreateWithFlags(&c->ev_ring_ready[k], hipEventDisableTiming));
-      HIPCHK(c, hipEventCreateWithFlags(&c->ev_ring_free[k], hipEventDisableTiming));
-    }
-  }
-  if (c->copy_threads > 0 && (!c->pool || c->stage_frame < (size_t)fb)) {
-    if (c->h_stage) {
-      for (int k = 0; k < 2; ++k) HIPCHK(c, hipEventSynchronize(c->ev_stage[k]));
-      HIPCHK(c, hipHostFree(c->h_stage));
+// Host frames (klt_hip_track_frames_host): the caller's pageable frames go up
+// chunk by chunk.  Per chunk: the pool copies the frames into a pinned staging
+// slot, one DMA moves the slot into a device ring slot (copy stream), the
+// batched pyramids + tracker run on the context stream and write the chunk's
+// table rows into a device rows slot, one D2H brings the rows into a pinned
+// host slot (a third stream), and the pool hands them to the caller's
+// callback.  Two slots of each: the upload of chunk c+1 and the delivery of
+// chunk c-1 run on the host while chunk c is on the device.
+namespace {
+int host_pipeline_prepare(klt_hip_ctx *c, size_t stage_bytes, size_t rows_bytes) {
+  for (hipStream_t *st : {&c->cstream, &c->dstream})
+    if (!*st) HIPCHK(c, hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+  for (int k = 0; k < 2; ++k)
+    for (hipEvent_t *e : {&c->ev_ring_free[k], &c->ev_dma[k], &c->ev_tracked[k], &c->ev_rows[k]})
+      if (!*e) HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
+  if (c->stage_cap < stage_bytes || c->hrows_cap < rows_bytes) {
+    HIPCHK(c, hipDeviceSynchronize());  // no copy still reads the old pinned buffers
+    if (c->stage_cap < stage_bytes) {
+      if (c->h_stage) HIPCHK(c, hipHostFree(c->h_stage));
       c->h_stage = nullptr;
+      c->stage_cap = 0;
+      HIPCHK(c, hipHostMalloc((void **)&c->h_stage, stage_bytes, hipHostMallocDefault));
+      c->stage_cap = stage_bytes;
     }
-    HIPCHK(c, hipHostMalloc((void **)&c->h_stage, (size_t)2 * kStageGroup * fb, hipHostMallocDefault));
-    c->stage_frame = (size_t)fb;
-    for (int k = 0; k < 2; ++k)
-      if (!c->ev_stage[k]) HIPCHK(c, hipEventCreateWithFlags(&c->ev_stage[k], hipEventDisableTiming));
-    if (!c->pool) {
-      // thread creation can throw (std::system_error, bad_alloc): no exception
-      // crosses this extern "C" entry; without a pool the runtime stages the copies
-      try {
-        c->pool = new CopyPool(c->copy_threads);
-      } catch (...) {
-        c->pool = nullptr;
-        c->copy_threads = 0;
-      }
+    if (c->hrows_cap < rows_bytes) {
+      if (c->h_rows) HIPCHK(c, hipHostFree(c->h_rows));
+      c->h_rows = nullptr;
+      c->hrows_cap = 0;
+      HIPCHK(c, hipHostMalloc((void **)&c->h_rows, rows_bytes, hipHostMallocDefault));
+      c->hrows_cap = rows_bytes;
     }
   }
-  // the ring may still be read by earlier work on the context stream
-  HIPCHK(c, hipEventRecord(c->ev_ring_free[0], c->stream));
-  HIPCHK(c, hipEventRecord(c->ev_ring_free[1], c->stream));
-  auto upload = [&](int j0, int k) -> int {
-    const int nf = F < nframes - j0 ? F : nframes - j0;
+  if (c->ring_cap < stage_bytes) {
+    HIPCHK(c, hipDeviceSynchronize());
+    hipFree(c->d_ring);
+    c->d_ring = nullptr;
+    c->ring_cap = 0;
+    HIPCHK(c, hipMalloc((void **)&c->d_ring, stage_bytes));
+    c->ring_cap = stage_bytes;
+  }
+  if (c->drows_cap < rows_bytes) {
+    HIPCHK(c, hipDeviceSynchronize());
+    hipFree(c->d_rows);
+    c->d_rows = nullptr;
+    c->drows_cap = 0;
+    HIPCHK(c, hipMalloc((void **)&c->d_rows, rows_bytes));
+    c->drows_cap = rows_bytes;
+  }
+  ensure_pool(c);
+  return 0;
+}
+}  // namespace
+
+KLT_API int klt_hip_track_frames_host(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
+                                      const unsigned char *const *frames, int nframes, int seed_first, int chunk,
+                                      float *x, float *y, int *val, int n, klt_hip_rows_fn rows, void *user) {
+  if (!c || !pd || !td || (nframes > 0 && !frames)) return fail(c, "track_frames_host: null argument");
+  if (chunk < 1 || nframes < 0 || n < 0) return fail(c, "track_frames_host: bad nframes/chunk/n");
+  if (n > 0 && (!x || !y || !val)) return fail(c, "track_frames_host: null feature arrays");
+  for (int f = 0; f < nframes; ++f)
+    if (!frames[f]) return fail(c, "track_frames_host: frame %d is NULL", f);
+  if (nframes - (seed_first ? 1 : 0) <= 0) return 0;
+  if (use_device(c)) return -1;
+  const size_t fb = (size_t)pd->ncols * pd->nrows;
+  const int F = chunk < nframes ? chunk : nframes;
+  const size_t rows_slot = (size_t)3 * F * (n > 0 ? n : 1);  // floats: x | y | val rows of one chunk
+  if (host_pipeline_prepare(c, 2 * F * fb, 2 * rows_slot * sizeof(float))) return -1;
+  if (n > 0 && feat_stage_in(c, x, y, val, n)) return -1;
+  float *dx = c->d_fx, *dy = c->d_fy;
+  int *dv = c->d_fv;
+  // the ring and the rows slots may still be read by earlier work on the context stream
+  for (int k = 0; k < 2; ++k) {
+    HIPCHK(c, hipEventRecord(c->ev_ring_free[k], c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_rows[k], c->stream));
+  }
+  const int nchunks = (nframes + F - 1) / F;
+  auto upload = [&](int ci) -> int {
+    const int k = ci & 1, f0 = ci * F, nf = F < nframes - f0 ? F : nframes - f0;
+    unsigned char *stage = c->h_stage + (size_t)k * F * fb;
+    HIPCHK(c, hipEventSynchronize(c->ev_dma[k]));  // the slot's previous DMA is done
+    const size_t piece = 512 << 10, per = (fb + piece - 1) / piece;
+    if (host_parallel(c, (size_t)nf * per, [&](size_t t) {
+          const size_t f = t / per, o = (t - f * per) * piece;
+          copy_stream(stage + f * fb + o, frames[f0 + f] + o, fb - o < piece ? fb - o : piece);
+        }))
+      return -1;
     HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_ring_free[k], 0));
-    for (int f = 0; f < nf; ++f)
-      if (!frames[j0 + f]) return fail(c, "track_frames_host: frame %d is NULL", j0 + f);
-    if (!c->pool) {
-      for (int f = 0; f < nf; ++f)
-        HIPCHK(c, hipMemcpyAsync(c->d_ring + (size_t)(k * F + f) * fb, frames[j0 + f], (size_t)fb,
-                                 hipMemcpyHostToDevice, c->cstream));
-    }
-    for (int g0 = 0; c->pool && g0 < nf; g0 += kStageGroup) {
-      // a group of frames: wait until this group's slots are out of their
-      // last DMA, copy in parallel, then one DMA per frame
-      const int ng = kStageGroup < nf - g0 ? kStageGroup : nf - g0;
-      const int sg = c->stage_next;
-      c->stage_next ^= 1;
-      HIPCHK(c, hipEventSynchronize(c->ev_stage[sg]));
-      unsigned char *slots = c->h_stage + (size_t)sg * kStageGroup * fb;
-      const size_t piece = 512 << 10;
-      try {
-        c->pool->jobs.clear();
-        for (int f = 0; f < ng; ++f)
-          for (size_t o = 0; o < (size_t)fb; o += piece)
-            c->pool->jobs.push_back({slots + (size_t)f * fb + o, frames[j0 + g0 + f] + o,
-                                     (size_t)fb - o < piece ? (size_t)fb - o : piece});
-      } catch (...) {
-        return fail(c, "track_frames_host: out of memory filling the copy jobs");
-      }
-      c->pool->copy();
-      HIPCHK(c, hipMemcpyAsync(c->d_ring + (size_t)(k * F + g0) * fb, slots, (size_t)ng * fb,
-                               hipMemcpyHostToDevice, c->cstream));
-      HIPCHK(c, hipEventRecord(c->ev_stage[sg], c->cstream));
-    }
-    HIPCHK(c, hipEventRecord(c->ev_ring_ready[k], c->cstream));
+    HIPCHK(c, hipMemcpyAsync(c->d_ring + (size_t)k * F * fb, stage, (size_t)nf * fb, hipMemcpyHostToDevice,
+                             c->cstream));
+    HIPCHK(c, hipEventRecord(c->ev_dma[k], c->cstream));
     return 0;
   };
-  if (upload(0, 0)) return -1;
-  for (int j0 = 0, k = 0; j0 < nframes; j0 += F, k ^= 1) {
-    const int nf = F < nframes - j0 ? F : nframes - j0;
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_ring_ready[k], 0));
-    const long off = (long)j0 * tab_stride;
-    if (track_frames_impl(c, pd, td, c->d_ring + (size_t)k * F * fb, pd->ncols, fb, nf, F, x, y, val, n,
-                          tab_x ? tab_x + off : nullptr, tab_y ? tab_y + off : nullptr,
-                          tab_val ? tab_val + off : nullptr, tab_stride, nullptr))
+  auto ring_ready = [&](int k) -> int {
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_dma[k], 0));
+    return 0;
+  };
+  // tracked frames of chunk ci: input frames [f0+skip, f0+nf), table rows from t0
+  auto span = [&](int ci, int &t0, int &nt, int &skip) {
+    const int f0 = ci * F, nf = F < nframes - f0 ? F : nframes - f0;
+    skip = (ci == 0 && seed_first) ? 1 : 0;
+    nt = nf - skip;
+    t0 = f0 + skip - (seed_first ? 1 : 0);
+  };
+  auto deliver = [&](int ci) -> int {
+    int t0, nt, skip;
+    span(ci, t0, nt, skip);
+    if (!rows || nt <= 0 || n <= 0) return 0;
+    const int k = ci & 1;
+    HIPCHK(c, hipEventSynchronize(c->ev_rows[k]));
+    const float *hx = c->h_rows + k * rows_slot, *hy = hx + (size_t)F * n;
+    const int *hv = reinterpret_cast<const int *>(hy + (size_t)F * n);
+    const int per = 256;
+    return host_parallel(c, (size_t)(n + per - 1) / per, [&](size_t t) {
+      const int a = (int)t * per, b = a + per < n ? a + per : n;
+      rows(user, t0, nt, a, b, hx, hy, hv, n);
+    });
+  };
+  if (upload(0)) return -1;
+  if (seed_first) {  // frames[0]'s pyramid, built from its uploaded copy
+    if (ring_ready(0)) return -1;
+    if (klt_hip_frames_begin(c, pd, c->d_ring, pd->ncols)) return -1;
+  }
+  for (int ci = 0; ci < nchunks; ++ci) {
+    const int k = ci & 1;
+    int t0, nt, skip;
+    span(ci, t0, nt, skip);
+    float *rx = c->d_rows + k * rows_slot, *ry = rx + (size_t)F * n;
+    int *rv = reinterpret_cast<int *>(ry + (size_t)F * n);
+    if (ring_ready(k)) return -1;
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_rows[k], 0));  // the rows slot's last D2H is done
+    if (nt > 0 && track_frames_impl(c, pd, td, c->d_ring + (size_t)k * F * fb + skip * fb, pd->ncols, fb, nt, F,
+                                    dx, dy, dv, n, rows ? rx : nullptr, rows ? ry : nullptr, rows ? rv : nullptr,
+                                    n, nullptr))
       return -1;
     HIPCHK(c, hipEventRecord(c->ev_ring_free[k], c->stream));
-    if (j0 + F < nframes && upload(j0 + F, k ^ 1)) return -1;  // overlaps the chunk just queued
+    if (rows && n > 0 && nt > 0) {
+      HIPCHK(c, hipEventRecord(c->ev_tracked[k], c->stream));
+      HIPCHK(c, hipStreamWaitEvent(c->dstream, c->ev_tracked[k], 0));
+      float *hx = c->h_rows + k * rows_slot;
+      const size_t b = sizeof(float) * (size_t)nt * n;
+      HIPCHK(c, hipMemcpyAsync(hx, rx, b, hipMemcpyDeviceToHost, c->dstream));
+      HIPCHK(c, hipMemcpyAsync(hx + (size_t)F * n, ry, b, hipMemcpyDeviceToHost, c->dstream));
+      HIPCHK(c, hipMemcpyAsync(hx + (size_t)2 * F * n, rv, b, hipMemcpyDeviceToHost, c->dstream));
+      HIPCHK(c, hipEventRecord(c->ev_rows[k], c->dstream));
+    }
+    if (ci + 1 < nchunks && upload(ci + 1)) return -1;  // overlaps chunk ci on the device
+    if (ci >= 1 && deliver(ci - 1)) return -1;          // and the rows of chunk ci-1
+  }
+  if (deliver(nchunks - 1)) return -1;
+  if (n > 0) {
+    HIPCHK(c, hipMemcpyAsync(c->h_feat, c->d_feat, 3 * sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+    if (feat_unpack(c, x, y, val, n)) return -1;
   }
   return 0;
 }
@@ -1511,7 +1724,7 @@ KLT_API int klt_hip_selftest_sqrt(klt_hip_ctx *c, const double *in, double *out,
 KLT_API int klt_hip_selftest_copy_pool(int workers, int rounds, size_t max_bytes) {
   if (workers < 0 || rounds < 0 || max_bytes < 1) return -1;
   std::vector<unsigned char> src(max_bytes), dst(max_bytes);
-  CopyPool pool(workers);
+  HostPool pool(workers);
   unsigned long long r64 = 0x9E3779B97F4A7C15ull;
   auto rnd = [&]() {
     r64 ^= r64 << 13;
@@ -1524,9 +1737,11 @@ KLT_API int klt_hip_selftest_copy_pool(int workers, int rounds, size_t max_bytes
     const size_t piece = 1 + rnd() % (n < 65536 ? n : 65536);
     for (size_t i = 0; i < n; ++i) src[i] = (unsigned char)(rnd() >> 29);
     memset(dst.data(), 0, n);
-    pool.jobs.clear();
-    for (size_t o = 0; o < n; o += piece) pool.jobs.push_back({dst.data() + o, src.data() + o, n - o < piece ? n - o : piece});
-    pool.copy();
+    const std::function<void(size_t)> copy = [&](size_t t) {
+      const size_t o = t * piece;
+      memcpy(dst.data() + o, src.data() + o, n - o < piece ? n - o : piece);
+    };
+    pool.parallel((n + piece - 1) / piece, copy);
     if (memcmp(dst.data(), src.data(), n) != 0) return r + 1;
   }
   return 0;

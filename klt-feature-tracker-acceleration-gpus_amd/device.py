@@ -68,6 +68,7 @@ DEVICE_PROTOS = {
     "klt_hip_get_track_count": (C.c_int, [V, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong), C.c_int]),
     "klt_hip_set_prof": (C.c_int, [V, V]),
     "klt_hip_set_frames_overlap": (C.c_int, [V, C.c_int]),
+    "klt_hip_set_host_threads": (C.c_int, [V, C.c_int]),
     "klt_hip_set_path": (C.c_int, [V, C.c_int]),
     "klt_hip_level_dims": (C.c_int, [V, C.c_int, C.c_int, IP, IP]),
     "klt_hip_download_level": (C.c_int, [V, C.c_int, C.c_int, C.c_int, V]),
@@ -76,6 +77,8 @@ DEVICE_PROTOS = {
     "klt_hip_track_sequence": (C.c_int, [V, C.POINTER(PyrDesc), C.POINTER(TrackDesc), V, C.c_long,
                                          C.c_long, C.c_int, C.c_int, V, V, V, C.c_int, IP]),
     "klt_hip_frames_begin": (C.c_int, [V, C.POINTER(PyrDesc), V, C.c_long]),
+    "klt_hip_frames_begin_slot": (C.c_int, [V, C.c_int]),
+    "klt_hip_frames_end_slot": (C.c_int, [V, C.c_int]),
     "klt_hip_track_frames": (C.c_int, [V, C.POINTER(PyrDesc), C.POINTER(TrackDesc), V, C.c_long, C.c_long,
                                        C.c_int, C.c_int, V, V, V, C.c_int, V, V, V, C.c_long]),
     "klt_hip_track_frames_band": (C.c_int, [V, C.POINTER(PyrDesc), C.POINTER(TrackDesc), V, C.c_long, C.c_long,

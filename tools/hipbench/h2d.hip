@@ -11,6 +11,8 @@
 #include <stdlib.h>
 #include <string.h>
 #include <chrono>
+#include <thread>
+#include <atomic>
 #include <vector>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
@@ -116,6 +118,39 @@ int main(int argc, char **argv) {
     t0 = now();
     for (int i = 0; i < n; ++i) memcpy(pin + (i & 1) * fb, fr[i], fb);
     if (rep) report("f_memcpy_only", now() - t0);
+    {  // g: DMA from pinned over two streams (two copy engines?)
+      static hipStream_t s2 = nullptr;
+      if (!s2) CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+      t0 = now();
+      for (int i = 0; i < n; ++i)
+        CK(hipMemcpyAsync(dev + (i & 1) * fb, pin + (i & 1) * fb, fb, hipMemcpyHostToDevice, (i & 1) ? s2 : s));
+      CK(hipStreamSynchronize(s));
+      CK(hipStreamSynchronize(s2));
+      if (rep) report("g_dma_pinned_two_streams", now() - t0);
+    }
+    {  // h: DMA from pinned while 4 host threads memcpy (host memory contention)
+      std::atomic<bool> stop{false};
+      std::vector<std::thread> th;
+      for (int w = 0; w < 4; ++w)
+        th.emplace_back([&, w] {
+          std::vector<unsigned char> a(fb), b(fb);
+          while (!stop.load()) memcpy(b.data(), fr[w], fb);
+        });
+      t0 = now();
+      for (int i = 0; i < n; ++i) CK(hipMemcpyAsync(dev + (i & 1) * fb, pin + (i & 1) * fb, fb, hipMemcpyHostToDevice, s));
+      CK(hipStreamSynchronize(s));
+      if (rep) report("h_dma_pinned_under_4_memcpy_threads", now() - t0);
+      stop = true;
+      for (auto &t : th) t.join();
+    }
+    {  // i: one big DMA of 8 frames from a pinned group (as the copy pool's groups)
+      static unsigned char *grp = nullptr, *dgrp = nullptr;
+      if (!grp) { CK(hipHostMalloc((void **)&grp, 8 * fb, hipHostMallocDefault)); CK(hipMalloc(&dgrp, 8 * fb)); memset(grp, 3, 8 * fb); }
+      t0 = now();
+      for (int i = 0; i < n; i += 8) CK(hipMemcpyAsync(dgrp, grp, 8 * fb, hipMemcpyHostToDevice, s));
+      CK(hipStreamSynchronize(s));
+      if (rep) report("i_dma_pinned_groups_of_8", now() - t0);
+    }
   }
   return 0;
 }

@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--frames", type=int, default=8)
     ap.add_argument("--reduction", choices=["exact", "fast"], default="exact")
+    ap.add_argument("--no-table", action="store_true", help="apiseq: no feature table")
+    ap.add_argument("--host-threads", type=int, default=-1, help="apiseq: host pool workers (-1: default)")
     ap.add_argument("--generic", action="store_true")
     ap.add_argument("--max-it", type=int, default=0, help="tracker: override max_iterations")
     ap.add_argument("--lost", action="store_true", help="tracker: mark every feature lost (launch floor)")
@@ -64,6 +66,8 @@ def main():
     check(lib, ctx, lib.klt_hip_set_track_merge(ctx, 0 if a.no_merge else 1), "merge")
     check(lib, ctx, lib.klt_hip_set_track_patch(ctx, 0 if a.no_patch else 1), "patch")
     check(lib, ctx, lib.klt_hip_set_frames_overlap(ctx, 1 if a.overlap else 0), "overlap")
+    if a.host_threads >= 0:
+        check(lib, ctx, lib.klt_hip_set_host_threads(ctx, a.host_threads), "host_threads")
     nf = max(a.frames, 2)
     frames = lib.klt_hip_malloc(ctx, nf * W * H)
     check(lib, ctx, lib.klt_hip_synth_frames(ctx, 1080, 0, nf, W, H, frames, W, W * H), "synth")
@@ -135,16 +139,16 @@ def main():
         fl = lib.KLTCreateFeatureList(a.features)
         lib.KLTSelectGoodFeatures(tc, u8(host[0]), W, H, fl)
         ft = lib.KLTCreateFeatureTable(nh - 1, a.features)
-        lib.KLTTrackSequence(tc, arr, min(nh, 40), W, H, fl, ft, 0)  # warm-up (allocations)
-        lib.KLTFreeFeatureList(fl)
-        fl = lib.KLTCreateFeatureList(a.features)
-        lib.KLTSelectGoodFeatures(tc, u8(host[0]), W, H, fl)
-        t0 = time.perf_counter()
-        lib.KLTTrackSequence(tc, arr, nh, W, H, fl, ft, 0)
-        dt = time.perf_counter() - t0
-        live = sum(1 for k in range(a.features) if fl.contents.feature[k].contents.val >= 0)
+        for rep in range(3):
+            fl = lib.KLTCreateFeatureList(a.features)
+            lib.KLTSelectGoodFeatures(tc, u8(host[0]), W, H, fl)
+            t0 = time.perf_counter()
+            lib.KLTTrackSequence(tc, arr, nh, W, H, fl, ft if not a.no_table else None, 0)
+            dt = time.perf_counter() - t0
+            print(f"apiseq rep {rep}: {(nh - 1) / dt:.0f} fps", file=sys.stderr, flush=True)
+            live = sum(1 for k in range(a.features) if fl.contents.feature[k].contents.val >= 0)
+            lib.KLTFreeFeatureList(fl)
         lib.KLTFreeFeatureTable(ft)
-        lib.KLTFreeFeatureList(fl)
         out.update({"features": a.features, "frames_tracked": nh - 1, "fps": (nh - 1) / dt,
                     "us_per_frame": 1e6 * dt / (nh - 1), "live_at_end": live,
                     "note": "host frames, PCIe upload and feature-table download included"})
