@@ -647,6 +647,9 @@ hipError_t launch_pyr_l0(hipStream_t st, const uint8_t *src, int pitch, long str
                          long fs0, long fsh, int F, int ty0, int ty1) {
   const int tx = (W + l0::TW - 1) / l0::TW;
   if (F <= 0 || ty1 <= ty0) return hipSuccess;
+#ifdef KLT_EXP_NOHS  // timing experiment only: level 0 without the sigma-3.6 rows pass
+  do_hs = 0;
+#endif
   hipLaunchKernelGGL(k_pyr_l0, dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(kBlock), 0, st, src, pitch, W, H, T,
                      vec_u8, img, gx, gy, hs, W1, do_hs, vec_out, stride, fs0, fsh, ty0, tx, ty1 - ty0);
   return hipGetLastError();

@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--frames", type=int, default=8)
     ap.add_argument("--reduction", choices=["exact", "fast"], default="exact")
     ap.add_argument("--no-table", action="store_true", help="apiseq: no feature table")
+    ap.add_argument("--count", action="store_true", help="frames: count Newton iterations / passes of the timed rep")
     ap.add_argument("--host-threads", type=int, default=-1, help="apiseq: host pool workers (-1: default)")
     ap.add_argument("--generic", action="store_true")
     ap.add_argument("--max-it", type=int, default=0, help="tracker: override max_iterations")
@@ -204,7 +205,13 @@ def main():
             check(lib, ctx, lib.klt_hip_memcpy(ctx, pbuf, np.zeros(nslot, np.uint64).ctypes.data, 8 * nslot, H2D),
                   "zero")
             lib.klt_hip_set_prof(ctx, pbuf)
+        if a.count:
+            check(lib, ctx, lib.klt_hip_set_track_count(ctx, 1), "count")
         rep()
+        if a.count:
+            solves, passes = C.c_ulonglong(0), C.c_ulonglong(0)
+            check(lib, ctx, lib.klt_hip_get_track_count(ctx, C.byref(solves), C.byref(passes), 0), "count")
+            out["newton_iterations"], out["gather_passes"] = solves.value, passes.value
         if a.prof:
             lib.klt_hip_sync(ctx)
             pr = np.empty(nslot, np.uint64)
