@@ -238,17 +238,11 @@ def main() -> None:
     l1 = us(tm.ms_pyr_l1, tm.n_pyr_l1)
     trk = us(tm.ms_track, tm.n_track)
     gen = us(tm.ms_generic, tm.n_generic)
-    stp = us(tm.ms_pyr_strip, tm.n_pyr_strip)
     l0f = us(tm.ms_pyr_l0, tm.frames_pyr_l0)
     l1f = us(tm.ms_pyr_l1, tm.frames_pyr_l1)
-    stpf = us(tm.ms_pyr_strip, tm.frames_pyr_strip)
     trkf = us(tm.ms_track, tm.frames_track)
-    strip = bool(tm.n_pyr_strip)  # both levels in one k_pyr_strip launch (the batched default)
-    if strip:
-        fpl = tm.frames_pyr_strip / tm.n_pyr_strip  # frames per pyramid launch
-    else:
-        fpl = (tm.frames_pyr_l0 / tm.n_pyr_l0) if tm.n_pyr_l0 else 1.0
-    pass_us = (stpf if strip else (l0f or 0) + (l1f or 0)) if fused else gen
+    fpl = (tm.frames_pyr_l0 / tm.n_pyr_l0) if tm.n_pyr_l0 else 1.0  # frames per pyramid launch
+    pass_us = (l0f or 0) + (l1f or 0) if fused else gen
     px = W * H
     W1, H1 = W // 4, H // 4
     pass_bytes = px * 13 + W1 * H1 * 12  # u8 in; img/gx/gy out at L0 and L1
@@ -278,9 +272,8 @@ def main() -> None:
                    "parallelism": "independent sequence per GPU" if world > 1 else "single GPU",
                    "reduction": args.reduction, "pyramid_path": "fused" if fused else "generic"},
         "pyramid_gpix_s": (px / (pass_us * 1e-6) / 1e9) if pass_us else None,
-        "kernels_us_per_launch": {"k_pyr_strip": stp, "k_pyr_l0": l0, "k_pyr_l1": l1, "k_track": trk,
-                                  "generic_pass": gen},
-        "kernels_us_per_frame": {"k_pyr_strip": stpf, "k_pyr_l0": l0f, "k_pyr_l1": l1f, "k_track": trkf},
+        "kernels_us_per_launch": {"k_pyr_l0": l0, "k_pyr_l1": l1, "k_track": trk, "generic_pass": gen},
+        "kernels_us_per_frame": {"k_pyr_l0": l0f, "k_pyr_l1": l1f, "k_track": trkf},
         "frames_per_launch": fpl,
         "live_features": {"after_warmup": live_before, "at_end": live_after},
     }
@@ -292,14 +285,13 @@ def main() -> None:
     if pass_us:
         ach = pass_bytes / (pass_us * 1e-6) / 1e9
         result["roofline"] = {
-            "kernel": "pyramid pass (k_pyr_strip: both levels, one launch)" if strip else
-                      "pyramid pass (k_pyr_l0 + k_pyr_l1)", "bound": "hbm", "achieved": ach,
+            "kernel": "pyramid pass (k_pyr_l0 + k_pyr_l1)", "bound": "hbm", "achieved": ach,
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
             "traffic": None, "algorithmic_bytes_per_frame": pass_bytes,
             "algorithmic_bytes_per_launch": pass_bytes * fpl, "frames_per_launch": fpl,
             "us_per_frame": pass_us,
-            "k_pyr_l0": ({"achieved": (l0_bytes / (l0f * 1e-6) / 1e9) if l0f else None,
-                          "algorithmic_bytes_per_frame": l0_bytes} if not strip else None),
+            "k_pyr_l0": {"achieved": (l0_bytes / (l0f * 1e-6) / 1e9) if l0f else None,
+                         "algorithmic_bytes_per_frame": l0_bytes},
             "event_timing": "timed region" if timed_events else
                             "replay of the timed region on one stream (each kernel's own duration)",
         }
@@ -461,19 +453,15 @@ def pass_4k(lib, dev, chunk=64, reps=2):
     lib.KLTFreeTrackingContext(tc)
     del fr
     torch.cuda.empty_cache()
-    per = lambda ms, fr: 1000.0 * ms / fr if fr else None  # noqa: E731
-    l0, l1 = per(tm.ms_pyr_l0, tm.frames_pyr_l0), per(tm.ms_pyr_l1, tm.frames_pyr_l1)
-    sp = per(tm.ms_pyr_strip, tm.frames_pyr_strip)
-    pus = sp if sp is not None else (l0 or 0) + (l1 or 0)
+    l0 = 1000.0 * tm.ms_pyr_l0 / tm.frames_pyr_l0
+    l1 = 1000.0 * tm.ms_pyr_l1 / tm.frames_pyr_l1
     by = W * H * 13 + (W // 4) * (H // 4) * 12
-    ach = by / (pus * 1e-6) / 1e9
+    ach = by / ((l0 + l1) * 1e-6) / 1e9
     return {"workload": f"{W}x{H} pyramid pass, batched {chunk} frames per launch, pyramids only",
-            "kernel": "k_pyr_strip (both levels, one launch)" if sp is not None else "k_pyr_l0 + k_pyr_l1",
             "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-            "algorithmic_bytes_per_frame": by, "us_per_frame": pus,
-            "kernels_us_per_frame": {"k_pyr_strip": sp, "k_pyr_l0": l0, "k_pyr_l1": l1},
-            "frames_timed": int(tm.frames_pyr_strip or tm.frames_pyr_l0),
-            "pyramid_gpix_s": W * H / (pus * 1e-6) / 1e9,
+            "algorithmic_bytes_per_frame": by, "us_per_frame": l0 + l1,
+            "kernels_us_per_frame": {"k_pyr_l0": l0, "k_pyr_l1": l1}, "frames_timed": int(tm.frames_pyr_l0),
+            "pyramid_gpix_s": W * H / ((l0 + l1) * 1e-6) / 1e9,
             "event_timing": "HIP events on the launch stream, one stream"}
 
 

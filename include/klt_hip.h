@@ -93,9 +93,6 @@ typedef struct {
   int n_pyr_l0, n_pyr_l1, n_track, n_eigen, n_generic;
   double ms_pyr_l0, ms_pyr_l1, ms_track, ms_eigen, ms_generic;
   long frames_pyr_l0, frames_pyr_l1, frames_track; /* frames covered by the timed launches */
-  int n_pyr_strip;                                   /* k_pyr_strip: both levels in one launch */
-  double ms_pyr_strip;
-  long frames_pyr_strip;
 } klt_hip_timing;
 
 typedef struct klt_hip_ctx klt_hip_ctx;
@@ -127,13 +124,6 @@ int klt_hip_build_pyramid(klt_hip_ctx *ctx, int slot, const klt_hip_pyr_desc *de
 /* test hook: 1 forces the generic one-pass-per-launch path even when the
    fused kernels apply (they must agree bit for bit) */
 int klt_hip_set_path(klt_hip_ctx *ctx, int force_generic);
-/* fused pyramid kernels: mode 0 (default) builds batched launches of enough
-   frames with k_pyr_strip (both levels in one pass over 128-column strips,
-   LDS line buffers) and single frames with the k_pyr_l0 + k_pyr_l1 tiles;
-   1 always tiles; 2 strips wherever the shape allows (two levels, width a
-   multiple of 4, 4-byte aligned rows).  seg_blocks: 4-row blocks per strip
-   workgroup (0: the whole height).  Results do not depend on either. */
-int klt_hip_set_pyr_strips(klt_hip_ctx *ctx, int mode, int seg_blocks);
 /* tuning hook: 1 tracks features in input order; 0 (default) in row-band
    order with each XCD given one band (L2 locality).  Results do not depend on it. */
 int klt_hip_set_track_order(klt_hip_ctx *ctx, int input_order);

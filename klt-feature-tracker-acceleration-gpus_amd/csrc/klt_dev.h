@@ -147,12 +147,6 @@ hipError_t launch_pyr_l0(hipStream_t st, const uint8_t *src, int pitch, long str
 // k_pyr_l1 over F frames, level-1 tile rows [ty0, ty1)
 hipError_t launch_pyr_l1(hipStream_t st, const float *hs, int W1, int H, int H1, const DefTaps &T, int vec,
                          float *img1, float *gx1, float *gy1, long fsh, long fs1, int F, int ty0, int ty1);
-// k_pyr_strip over F frames: both levels of the fused pyramid in one pass
-// (W % 4 == 0, 4-byte aligned rows; v16: W, pitch, stride and base multiples
-// of 16); seg_blocks 4-row blocks per workgroup (<= 0: the whole height)
-hipError_t launch_pyr_strip(hipStream_t st, const uint8_t *src, int pitch, long stride, int W, int H,
-                            const DefTaps &T, bool v16, float *img0, float *gx0, float *gy0, float *img1,
-                            float *gx1, float *gy1, long fs0, long fs1, int F, int seg_blocks);
 // generic one-pass kernels (any sigma / levels / subsampling)
 hipError_t launch_u8_to_f32(hipStream_t st, const uint8_t *src, long pitch, int W, int H, float *out);
 hipError_t launch_rows(hipStream_t st, const float *in, int W, int H, const RTaps &t, float *out);

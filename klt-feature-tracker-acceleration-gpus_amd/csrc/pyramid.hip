@@ -533,518 +533,6 @@ __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs,
 }
 
 // ---------------------------------------------------------------------------
-// k_pyr_strip: both levels in one pass, by line buffers in LDS.  One 256-thread
-// workgroup owns a 128-column strip of level 0 (32 columns of level 1) and a
-// segment of 4-row blocks, and walks down it one block per step: block b is
-// level-0 rows 4b..4b+3, and level-1 row b (whose sigma-3.6 sample row is
-// 4b+2).  Every row of every intermediate is computed once per strip and kept
-// in a ring of LDS rows for as long as a later pass needs it, so the sigma-3.6
-// row pass (k_pyr_l0's `hs`) never leaves the chip and there is no level-1
-// launch.  The stages of step s, each reading only ring rows written in
-// earlier steps, so that a step ends with one barrier:
-//   U  u8 rows of block s -> sigma-0.7 rows pass (t1)        [u8 prefetch: block s+PF]
-//   I  sigma-0.7 columns pass -> img0, block s-2               (HBM + ring)
-//   G  gradient rows passes of img0 (tx, ty), block s-3
-//   H  sigma-3.6 rows pass of img0 at columns 4X+2 (hs), block s-3
-//   C  gradient columns passes -> gx0, gy0, block s-5          (HBM)
-//   P  sigma-3.6 columns pass at row 4Y+2 -> img1, Y = s-7     (HBM + ring)
-//   Q  level-1 gradient rows passes, Y = s-8
-//   R  level-1 gradient columns passes -> gx1, gy1, Y = s-12   (HBM)
-// The four waves pair them by the taps they use: U+H, I+P, G+R, C+Q.
-// Each output is the same ordered sum as in k_pyr_l0 / k_pyr_l1 (and so the
-// reference's), with the same zero-border rules.  A segment of blocks [b0, b1)
-// runs steps b0-6 .. b1+11: the leading steps rebuild the rows above the
-// segment that its outputs read (12 blocks of warm-up for level 1's 21+7-row
-// reach), so segments are independent.
-// Column coordinates: staged u8 byte c <-> global x = C0-32+c (192 per row);
-// t1 / img0 column k <-> x = C0-20+k (172); hs / img1 column i <-> X = X0-3+i
-// (38 used; X0 = C0/4).  Needs W % 4 == 0 (4-byte u8 rows; V16: 16-byte).
-// ---------------------------------------------------------------------------
-namespace st {
-constexpr int SW = 128, SW1 = SW / 4;
-constexpr int UROW = SW + 64;  // staged u8 bytes per row
-constexpr int UW = UROW / 4;   // ... as dwords (48)
-constexpr int UQ = UROW / 16;  // 16-byte chunks per row (12)
-constexpr int NK = SW + 44;    // t1 / img0 columns (172)
-constexpr int NJ = SW1 + 8;    // img1 ring pitch (40; 38 used)
-constexpr int NH = SW1 + 6;    // hs ring pitch (38)
-constexpr int TR = 16;         // t1 ring rows (10 read + 4 written, 14 apart)
-constexpr int XRN = 16;        // tx/ty ring rows (10 read + 4 written, 15 apart)
-constexpr int HRN = 32;        // hs ring rows (24 read + 4 written)
-constexpr int LRN = 8;         // level-1 tx/ty ring rows (7 read + 1 written)
-constexpr int PF = 4;          // u8 prefetch distance (steps); the step loop is unrolled by it
-constexpr int WARM = 6, TAIL = 12;  // steps before b0 / after b1 (see above)
-constexpr int O_U = 0;
-constexpr int O_T = O_U + 4 * UW;
-constexpr int O_I = O_T + TR * NK;
-constexpr int O_X = O_I + 8 * NK;
-constexpr int O_Y = O_X + XRN * SW;
-constexpr int O_H = O_Y + XRN * SW;
-constexpr int O_J = O_H + HRN * NH;
-constexpr int O_X1 = O_J + 2 * NJ;
-constexpr int O_Y1 = O_X1 + LRN * SW1;
-constexpr int LDS = O_Y1 + LRN * SW1;
-static_assert(4 * UQ <= kWave && 4 * 22 <= 2 * kWave, "u8 staging / t1 items");
-static_assert(O_J % 4 == 0 && O_X1 % 4 == 0 && O_T % 4 == 0 && O_I % 4 == 0, "16-byte LDS rows");
-static_assert(LDS * 4 <= 40 * 1024, "four workgroups per CU");
-__device__ __forceinline__ int rt(int y) { return y & (TR - 1); }  // ring row of global row y
-}  // namespace st
-
-template <bool V16>
-__device__ __forceinline__ uint4 strip_u8_load(const uint8_t *__restrict__ src, int spitch, int W, int H, int C0,
-                                               int blk, int lane) {
-  using namespace st;
-  const int l = min(lane, 4 * UQ - 1);
-  const int r = l / UQ, q = l - r * UQ;
-  const int y = clampi(4 * blk + r, 0, H - 1);
-  const int x = C0 - 32 + 16 * q;
-  const uint8_t *row = src + (unsigned)(y * spitch);
-  if (V16) return *reinterpret_cast<const uint4 *>(row + clampi(x, 0, W - 16));
-  uint4 v;
-  v.x = *reinterpret_cast<const uint32_t *>(row + clampi(x, 0, W - 4));
-  v.y = *reinterpret_cast<const uint32_t *>(row + clampi(x + 4, 0, W - 4));
-  v.z = *reinterpret_cast<const uint32_t *>(row + clampi(x + 8, 0, W - 4));
-  v.w = *reinterpret_cast<const uint32_t *>(row + clampi(x + 12, 0, W - 4));
-  return v;
-}
-
-// Every wave runs the same steps with one barrier each, so the barrier counts
-// match; a stage's LDS writes of step s are read by other stages after that
-// step's barrier.
-struct StripArgs {
-  const uint8_t *src;
-  int spitch, W, H, W1, H1, C0, X0, b0, b1, l1hi;
-  float *img0, *gx0, *gy0, *img1, *gx1, *gy1;
-};
-
-// a tap copied into a vector register: the packed multiplies then take their
-// broadcast operand from VGPRs, which the strip kernel has to spare, instead
-// of SGPR pairs, which it has not (40 taps)
-__device__ __forceinline__ float vtap(float k) {
-  float v;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(k));
-  return v;
-}
-
-#ifdef KLT_STRIP_NOSTORE  // timing experiment only: level-0 planes not stored
-#define STRIP_ST(v) ((v) == 1234.5f)
-#else
-#define STRIP_ST(v) true
-#endif
-
-__device__ __forceinline__ void strip_barrier() {
-  // LDS writes of this step complete; global stores and the u8 prefetch stay in flight
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-// Stages of the strip walk (see above), each for step s
-// U: t1 rows of block s from the u8 rows loaded PF steps before (pf)
-template <bool E, bool V16>
-__device__ __forceinline__ void strip_U(float *__restrict__ lds, const StripArgs &A, const DefTaps &T, int s,
-                                        uint4 &pf, int lane) {
-  using namespace st;
-  float *U = lds + O_U, *Tt = lds + O_T;
-  if (!E || s < A.b1 + 7) {
-    if (lane < 4 * UQ) {
-      const int r = lane / UQ, q = lane - r * UQ;
-      *reinterpret_cast<uint4 *>(reinterpret_cast<uint32_t *>(U) + r * UW + 4 * q) = pf;
-    }
-    // the same wave reads the staging back: the LDS ops of one wave complete in order
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int i = lane + kWave * k;
-      if (i >= 4 * 22) break;
-      const int r = i / 22, j = i - r * 22;
-      const uint32_t *row = reinterpret_cast<const uint32_t *>(U) + r * UW + 2 + 2 * j;  // byte 8j+8
-      const uint2 d01 = *reinterpret_cast<const uint2 *>(row), d23 = *reinterpret_cast<const uint2 *>(row + 2);
-      const uint32_t d[4] = {d01.x, d01.y, d23.x, d23.y};
-      float v[16];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[4 * e + 0] = (float)(d[e] & 0xFF);
-        v[4 * e + 1] = (float)((d[e] >> 8) & 0xFF);
-        v[4 * e + 2] = (float)((d[e] >> 16) & 0xFF);
-        v[4 * e + 3] = (float)(d[e] >> 24);
-      }
-      f4 a0 = mul4(v + 2, T.s[0]), a1 = mul4(v + 6, T.s[0]);
-#pragma unroll
-      for (int m = 1; m < 5; ++m) {
-        mac4(a0, v + 2 + m, T.s[m]);
-        mac4(a1, v + 6 + m, T.s[m]);
-      }
-      if (E) {
-        const int x = A.C0 - 20 + 8 * j;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (!(x + e >= kRS && x + e < A.W - kRS)) a0[e] = 0.0f;
-          if (!(x + 4 + e >= kRS && x + 4 + e < A.W - kRS)) a1[e] = 0.0f;
-        }
-      }
-      float *dst = Tt + rt(4 * s + r) * NK + 8 * j;
-      st4(dst, a0);
-      if (8 * j + 4 < NK) st4(dst + 4, a1);  // item 21 holds columns 168 .. 171 only
-    }
-  }
-  pf = strip_u8_load<V16>(A.src, A.spitch, A.W, A.H, A.C0, s + PF, lane);
-}
-
-// Q: level-1 gradient rows passes of level-1 row s-8
-template <bool E>
-__device__ __forceinline__ void strip_Q(float *__restrict__ lds, const StripArgs &A, const DefTaps &T, int s,
-                                        int lane) {
-  using namespace st;
-  const float *J = lds + O_J;
-  float *X1 = lds + O_X1, *Y1 = lds + O_Y1;
-  const int Yq = s - 8;
-  if ((!E || (Yq >= A.b0 - 3 && Yq < A.b1 + 3)) && lane < SW1 / 4) {
-    const int g = lane;
-    const float *row = J + (Yq & 1) * NJ + 4 * g;  // i = 4g <-> X = X0+4g-3
-    float v[12];
-    *reinterpret_cast<f4 *>(v) = ld4(row);
-    *reinterpret_cast<f4 *>(v + 4) = ld4(row + 4);
-    *reinterpret_cast<f4 *>(v + 8) = ld4(row + 8);
-    f4 ax = {0.0f, 0.0f, 0.0f, 0.0f}, ay = mul4(v, T.g[0]);  // level-1 img >= +0 (k_pyr_l1)
-#pragma unroll
-    for (int m = 0; m < 7; ++m) {
-      if (m != kDC) mac4(ax, v + m, T.d[m]);
-      if (m > 0) mac4(ay, v + m, T.g[m]);
-    }
-    const int Xg = A.X0 + 4 * g;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      if (E && !(Xg + e >= kRG && Xg + e < A.W1 - kRG)) {
-        ax[e] = 0.0f;
-        ay[e] = 0.0f;
-      }
-    }
-    st4(X1 + (Yq & (LRN - 1)) * SW1 + 4 * g, ax);
-    st4(Y1 + (Yq & (LRN - 1)) * SW1 + 4 * g, ay);
-  }
-}
-
-// I: img0 block s-2 from t1 rows 4b-2 .. 4b+5
-template <bool E>
-__device__ __forceinline__ void strip_I(float *__restrict__ lds, const StripArgs &A, const DefTaps &T, int s,
-                                        int lane) {
-  using namespace st;
-  const float *Tt = lds + O_T;
-  float *I = lds + O_I;
-  const int b = s - 2;
-  if ((!E || (b >= A.b0 - 5 && b < A.b1 + 6)) && lane < NK / 4) {
-    const int g = lane;
-    f4 v[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = ld4(Tt + rt(4 * b - 2 + k) * NK + 4 * g);
-    const int x = A.C0 - 20 + 4 * g;
-    const bool out = (!E || (b >= A.b0 && b < A.b1 && x < A.W)) && g >= 5 && g < 5 + SW / 4;
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      f4 acc = mul4(reinterpret_cast<const float *>(&v[rr]), T.s[0]);
-#pragma unroll
-      for (int m = 1; m < 5; ++m) mac4(acc, reinterpret_cast<const float *>(&v[rr + m]), T.s[m]);
-      const int y = 4 * b + rr;
-      if (E && !(y >= kRS && y < A.H - kRS)) acc = f4{0.0f, 0.0f, 0.0f, 0.0f};
-      st4(I + ((b & 1) * 4 + rr) * NK + 4 * g, acc);
-      if (out && (!E || y < A.H) && STRIP_ST(acc.x)) st4_out(A.img0 + (unsigned)(y * A.W + x), acc);
-    }
-  }
-}
-
-// P: img1 row s-7, the sigma-3.6 columns pass over hs rows 4Y-8 .. 4Y+12
-template <bool E>
-__device__ __forceinline__ void strip_P(float *__restrict__ lds, const StripArgs &A, const DefTaps &T, int s,
-                                        int lane) {
-  using namespace st;
-  const float *Hs = lds + O_H;
-  float *J = lds + O_J;
-  const int Yp = s - 7;
-  if ((!E || (Yp >= A.b0 - 3 && Yp < A.b1 + 3)) && lane < 19) {
-    const int P = lane;
-    // terms >= +0: k_pyr_l1's +0 start is exact to leave out
-    f2 acc = *reinterpret_cast<const f2 *>(Hs + ((4 * Yp - 8) & (HRN - 1)) * NH + 2 * P) * f2{T.p[0], T.p[0]};
-#pragma unroll
-    for (int m = 1; m < 21; ++m)
-      acc += *reinterpret_cast<const f2 *>(Hs + ((4 * Yp - 8 + m) & (HRN - 1)) * NH + 2 * P) * f2{T.p[m], T.p[m]};
-    const int rr = kSS * Yp + kSS / 2;
-    if (E && !(rr >= kRP && rr < A.H - kRP)) acc = f2{0.0f, 0.0f};
-    *reinterpret_cast<f2 *>(J + (Yp & 1) * NJ + 2 * P) = acc;
-    if (!E || (Yp >= A.b0 && Yp < A.l1hi)) {
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int Xo = A.X0 - 3 + 2 * P + e;
-        if (Xo >= A.X0 && Xo < A.X0 + SW1 && (!E || Xo < A.W1)) A.img1[(unsigned)(Yp * A.W1 + Xo)] = acc[e];
-      }
-    }
-  }
-}
-
-// G: gradient rows passes of img0 block s-3 (columns C0 .. C0+127)
-template <bool E>
-__device__ __forceinline__ void strip_G(float *__restrict__ lds, const StripArgs &A, const DefTaps &T, int s,
-                                        int lane) {
-  using namespace st;
-  const float *I = lds + O_I;
-  float *X = lds + O_X, *Y = lds + O_Y;
-  const int b = s - 3;
-  if (E && !(b >= A.b0 - 5 && b < A.b1 + 6)) return;
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int i = lane + kWave * k;
-    const int rr = i / (SW / 4), g = i - rr * (SW / 4);
-    const float *row = I + ((b & 1) * 4 + rr) * NK + 4 * g + 16;  // k = 4g+16 <-> x = C0+4g-4
-    float v[12];
-    *reinterpret_cast<f4 *>(v) = ld4(row);
-    *reinterpret_cast<f4 *>(v + 4) = ld4(row + 4);
-    *reinterpret_cast<f4 *>(v + 8) = ld4(row + 8);
-    f4 ax = {0.0f, 0.0f, 0.0f, 0.0f}, ay = mul4(v + 1, T.g[0]);  // img0 >= +0 (k_pyr_l0's D2)
-#pragma unroll
-    for (int m = 0; m < 7; ++m) {
-      if (m != kDC) mac4(ax, v + 1 + m, T.d[m]);
-      if (m > 0) mac4(ay, v + 1 + m, T.g[m]);
-    }
-    const int x = A.C0 + 4 * g;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      if (E && !(x + e >= kRG && x + e < A.W - kRG)) {
-        ax[e] = 0.0f;
-        ay[e] = 0.0f;
-      }
-    }
-    const int yr = (4 * b + rr) & (XRN - 1);
-    st4(X + yr * SW + 4 * g, ax);
-    st4(Y + yr * SW + 4 * g, ay);
-  }
-}
-
-// H: the sigma-3.6 rows pass of img0 block s-3 at columns 4X+2, X = X0-3 .. X0+34
-template <bool E>
-__device__ __forceinline__ void strip_H(float *__restrict__ lds, const StripArgs &A, const DefTaps &T, int s,
-                                        int lane) {
-  using namespace st;
-  const float *I = lds + O_I;
-  float *Hs = lds + O_H;
-  const int b = s - 3;
-  if (E && !(b >= A.b0 - 5 && b < A.b1 + 6)) return;
-  if (lane < 38) {
-    const int P = lane % 19, h2 = lane / 19;
-    const int Xp = A.X0 - 3 + 2 * P;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int rr = 2 * h2 + q;
-      const float *row = I + ((b & 1) * 4 + rr) * NK + 8 * P;  // k = 8P <-> x = 4*Xp - 8
-      float v[28];
-#pragma unroll
-      for (int k = 0; k < 7; ++k) *reinterpret_cast<f4 *>(v + 4 * k) = ld4(row + 4 * k);
-      f2 a = f2{v[0], v[4]} * f2{T.p[0], T.p[0]};  // terms >= +0
-#pragma unroll
-      for (int m = 1; m < 21; ++m) a += f2{v[m], v[m + 4]} * f2{T.p[m], T.p[m]};
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int c = kSS * (Xp + e) + kSS / 2;
-        if (E && !(c >= kRP && c < A.W - kRP)) a[e] = 0.0f;
-      }
-      *reinterpret_cast<f2 *>(Hs + ((4 * b + rr) & (HRN - 1)) * NH + 2 * P) = a;
-      __builtin_amdgcn_sched_barrier(0);  // one row's 28 values live at a time
-    }
-  }
-}
-
-// C: gradient columns passes of block s-5 (tx/ty rows 4b-3 .. 4b+6), 4 rows x 2 columns per lane
-template <bool E>
-__device__ __forceinline__ void strip_C(float *__restrict__ lds, const StripArgs &A, const DefTaps &T, int s,
-                                        int lane) {
-  using namespace st;
-  const float *X = lds + O_X, *Y = lds + O_Y;
-  const int b = s - 5;
-  if (!E || (b >= A.b0 && b < A.b1)) {
-    const int g = lane;
-    f2 vx[10], vy[10];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) {
-      const int yr = (4 * b - 3 + k) & (XRN - 1);
-      vx[k] = *reinterpret_cast<const f2 *>(X + yr * SW + 2 * g);
-      vy[k] = *reinterpret_cast<const f2 *>(Y + yr * SW + 2 * g);
-    }
-    const int x = A.C0 + 2 * g;
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      f2 ax = {0.0f, 0.0f}, ay = {0.0f, 0.0f};
-#pragma unroll
-      for (int m = 0; m < 7; ++m) {
-        ax += vx[rr + m] * f2{T.g[m], T.g[m]};
-        if (m != kDC) ay += vy[rr + m] * f2{T.d[m], T.d[m]};
-      }
-      const int y = 4 * b + rr;
-      if (E && !(y >= kRG && y < A.H - kRG)) {
-        ax = f2{0.0f, 0.0f};
-        ay = ax;
-      }
-      if (!E || (y < A.H && x < A.W)) {
-        if (STRIP_ST(ax.x)) {
-          st2_out(A.gx0 + (unsigned)(y * A.W + x), ax);
-          st2_out(A.gy0 + (unsigned)(y * A.W + x), ay);
-        }
-      }
-    }
-  }
-}
-
-// R: level-1 gradient columns passes of level-1 row s-12 (level-1 tx/ty rows Y-3 .. Y+3)
-template <bool E>
-__device__ __forceinline__ void strip_R(float *__restrict__ lds, const StripArgs &A, const DefTaps &T, int s,
-                                        int lane) {
-  using namespace st;
-  const float *X1 = lds + O_X1, *Y1 = lds + O_Y1;
-  const int Yr = s - 12;
-  if ((!E || (Yr >= A.b0 && Yr < A.l1hi)) && lane < SW1 / 2) {  // 2 columns per lane
-    const int g = lane;
-    f2 ax = {0.0f, 0.0f}, ay = {0.0f, 0.0f};
-#pragma unroll
-    for (int m = 0; m < 7; ++m) {
-      const int yr = (Yr - 3 + m) & (LRN - 1);
-      const f2 a = *reinterpret_cast<const f2 *>(X1 + yr * SW1 + 2 * g);
-      const f2 c = *reinterpret_cast<const f2 *>(Y1 + yr * SW1 + 2 * g);
-      ax += a * f2{T.g[m], T.g[m]};
-      if (m != kDC) ay += c * f2{T.d[m], T.d[m]};
-    }
-    if (E && !(Yr >= kRG && Yr < A.H1 - kRG)) {
-      ax = f2{0.0f, 0.0f};
-      ay = ax;
-    }
-    const int Xg = A.X0 + 2 * g;
-    float *px = A.gx1 + (unsigned)(Yr * A.W1 + Xg), *py = A.gy1 + (unsigned)(Yr * A.W1 + Xg);
-    if (!E || Xg + 1 < A.W1) {
-      *reinterpret_cast<f2 *>(px) = ax;
-      *reinterpret_cast<f2 *>(py) = ay;
-    } else if (Xg < A.W1) {
-      px[0] = ax.x;
-      py[0] = ay.x;
-    }
-  }
-}
-
-// one wave's stage pair over steps [sa, sb) (a whole number of PF groups);
-// E: with the edge rules and range tests
-template <int ROLE, bool E, bool V16>
-__device__ __forceinline__ void strip_walk(float *__restrict__ lds, const StripArgs &A, const DefTaps &V, int sa,
-                                           int sb, uint4 (&pf)[st::PF], int lane) {
-  using namespace st;
-  for (int s = sa; s < sb; s += PF) {
-#pragma unroll
-    for (int d = 0; d < PF; ++d) {
-      if (ROLE == 3) {
-        strip_U<E, V16>(lds, A, V, s + d, pf[d], lane);
-        __builtin_amdgcn_sched_barrier(0);  // keep the stages' registers apart
-        strip_H<E>(lds, A, V, s + d, lane);
-      } else if (ROLE == 1) {
-        strip_I<E>(lds, A, V, s + d, lane);
-        strip_P<E>(lds, A, V, s + d, lane);
-      } else if (ROLE == 2) {
-        strip_G<E>(lds, A, V, s + d, lane);
-        strip_R<E>(lds, A, V, s + d, lane);
-      } else {
-        strip_C<E>(lds, A, V, s + d, lane);
-        strip_Q<E>(lds, A, V, s + d, lane);
-      }
-      strip_barrier();
-    }
-  }
-}
-
-template <bool V16>
-__global__ __launch_bounds__(kBlock) void k_pyr_strip(const uint8_t *__restrict__ src, int spitch, int W, int H,
-                                                      DefTaps T, float *__restrict__ img0, float *__restrict__ gx0,
-                                                      float *__restrict__ gy0, float *__restrict__ img1,
-                                                      float *__restrict__ gx1, float *__restrict__ gy1, long fs_src,
-                                                      long fs0, long fs1, int nstrips, int nseg, int seg_len) {
-  using namespace st;
-  __shared__ __attribute__((aligned(16))) float lds[LDS];
-  int sx, sg;
-  if (!xcd_tile(nstrips, nseg, sx, sg)) return;  // whole workgroup
-  const int nb = (H + 3) / 4;
-  StripArgs A;
-  A.b0 = sg * seg_len;
-  A.b1 = min(nb, A.b0 + seg_len);
-  if (A.b0 >= A.b1) return;  // whole workgroup
-  A.W = W;
-  A.H = H;
-  A.W1 = W / kSS;
-  A.H1 = H / kSS;
-  A.l1hi = min(A.b1, A.H1);
-  A.spitch = spitch;
-  A.src = src + blockIdx.z * fs_src;
-  A.img0 = img0 + blockIdx.z * fs0;
-  A.gx0 = gx0 + blockIdx.z * fs0;
-  A.gy0 = gy0 + blockIdx.z * fs0;
-  A.img1 = img1 + blockIdx.z * fs1;
-  A.gx1 = gx1 + blockIdx.z * fs1;
-  A.gy1 = gy1 + blockIdx.z * fs1;
-  A.C0 = sx * SW;
-  A.X0 = sx * SW1;
-  // the stage pairs differ in cost: rotate them over the waves of consecutive
-  // workgroups, so that each SIMD of a CU gets a mix
-  const int lane = threadIdx.x & (kWave - 1), wave = (threadIdx.x / kWave + blockIdx.x) & 3;
-  const int s0 = A.b0 - WARM, s1 = A.b1 + TAIL;
-  // every role walks the same steps (a multiple of PF; the extra ones do
-  // nothing).  Roles pair stages by the taps they use (fewer live scalar
-  // registers) and keep the u8 prefetch on a wave without global stores.
-  // Steps [sA, sB) of an interior strip need none of the zero-border rules,
-  // bounds or stage-range tests (every stage is active on interior rows):
-  // they run the E = false stages.  Both ends are whole groups of PF steps.
-  int sA = s0, sB = s0;
-  if (A.C0 >= 22 && A.C0 + 156 <= W && A.X0 + SW1 + 3 <= A.W1) {
-    const int lo = max(A.b0 + 12, 15);
-    const int hi = min(min(A.b1 + 5, A.l1hi + 7), min(min((H + 2) / 4, (H + 13) / 4 - 3), A.H1 + 9));
-    sA = s0 + PF * ((lo - s0 + PF - 1) / PF);
-    sB = hi > sA ? sA + PF * ((hi - sA) / PF) : sA;
-  }
-  const int s1r = sB + PF * ((s1 - sB + PF - 1) / PF);
-  DefTaps V;  // the taps a wave's stages use, in VGPRs
-  if (wave == 3) {  // U + H (sigma 0.7 / 3.6 taps)
-    for (int m = 0; m < 5; ++m) V.s[m] = T.s[m];
-#ifdef KLT_STRIP_H_SCALAR_TAPS
-    for (int m = 0; m < 21; ++m) V.p[m] = T.p[m];
-#else
-    for (int m = 0; m < 21; ++m) V.p[m] = vtap(T.p[m]);
-#endif
-    uint4 pf[PF];  // register set d holds the u8 rows of block s, s = s0+d (mod PF)
-    // issued in step order (the compiler must not reorder them): the loop's
-    // wait for set d then counts the PF-1 loads issued after it
-#pragma unroll
-    for (int d = 0; d < PF; ++d) {
-      pf[d] = strip_u8_load<V16>(A.src, spitch, W, H, A.C0, s0 + d, lane);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    strip_walk<3, true, V16>(lds, A, V, s0, sA, pf, lane);
-    strip_walk<3, false, V16>(lds, A, V, sA, sB, pf, lane);
-    strip_walk<3, true, V16>(lds, A, V, sB, s1r, pf, lane);
-  } else {
-    uint4 none[PF];
-    if (wave == 1) {  // I + P (sigma 0.7 / 3.6 taps): img0, img1 out
-      for (int m = 0; m < 5; ++m) V.s[m] = T.s[m];
-      for (int m = 0; m < 21; ++m) V.p[m] = vtap(T.p[m]);
-      strip_walk<1, true, V16>(lds, A, V, s0, sA, none, lane);
-      strip_walk<1, false, V16>(lds, A, V, sA, sB, none, lane);
-      strip_walk<1, true, V16>(lds, A, V, sB, s1r, none, lane);
-    } else {
-      for (int m = 0; m < 7; ++m) {
-        V.g[m] = vtap(T.g[m]);
-        V.d[m] = vtap(T.d[m]);
-      }
-      if (wave == 2) {  // G + R (gradient taps): gx1, gy1 out
-        strip_walk<2, true, V16>(lds, A, V, s0, sA, none, lane);
-        strip_walk<2, false, V16>(lds, A, V, sA, sB, none, lane);
-        strip_walk<2, true, V16>(lds, A, V, sB, s1r, none, lane);
-      } else {  // C + Q (gradient taps): gx0, gy0 out
-        strip_walk<0, true, V16>(lds, A, V, s0, sA, none, lane);
-        strip_walk<0, false, V16>(lds, A, V, sA, sB, none, lane);
-        strip_walk<0, true, V16>(lds, A, V, sB, s1r, none, lane);
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Generic path (any sigma / levels / subsampling): one 1-D pass per launch,
 // the reference's own pass structure (convolve.c:137-266, pyramid.c:87-131).
 // ---------------------------------------------------------------------------
@@ -1173,23 +661,6 @@ hipError_t launch_pyr_l1(hipStream_t st, const float *hs, int W1, int H, int H1,
   if (F <= 0 || ty1 <= ty0) return hipSuccess;
   hipLaunchKernelGGL(k_pyr_l1, dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(l1::NT), 0, st, hs, W1, H, H1, T, vec,
                      img1, gx1, gy1, fsh, fs1, ty0, tx, ty1 - ty0);
-  return hipGetLastError();
-}
-
-hipError_t launch_pyr_strip(hipStream_t st, const uint8_t *src, int pitch, long stride, int W, int H,
-                            const DefTaps &T, bool v16, float *img0, float *gx0, float *gy0, float *img1,
-                            float *gx1, float *gy1, long fs0, long fs1, int F, int seg_blocks) {
-  if (F <= 0 || W <= 0 || H <= 0) return hipSuccess;
-  const int nstrips = (W + st::SW - 1) / st::SW, nb = (H + 3) / 4;
-  const int seg = seg_blocks > 0 ? (seg_blocks < nb ? seg_blocks : nb) : nb;
-  const int nseg = (nb + seg - 1) / seg;
-  const dim3 grid(xcd_grid(nstrips * nseg), 1, F);
-  if (v16)
-    hipLaunchKernelGGL(k_pyr_strip<true>, grid, dim3(kBlock), 0, st, src, pitch, W, H, T, img0, gx0, gy0, img1, gx1,
-                       gy1, stride, fs0, fs1, nstrips, nseg, seg);
-  else
-    hipLaunchKernelGGL(k_pyr_strip<false>, grid, dim3(kBlock), 0, st, src, pitch, W, H, T, img0, gx0, gy0, img1, gx1,
-                       gy1, stride, fs0, fs1, nstrips, nseg, seg);
   return hipGetLastError();
 }
 

@@ -42,7 +42,7 @@ struct Slot {
   Level lv[KLT_HIP_MAX_LEVELS];
 };
 
-enum TimerClass { T_L0 = 0, T_L1, T_TRACK, T_EIG, T_GEN, T_STRIP, T_N };
+enum TimerClass { T_L0 = 0, T_L1, T_TRACK, T_EIG, T_GEN, T_N };
 
 // a batch of same-size pyramids: plane l of frame f at lv[l].img + f * w*h
 struct Bank {
@@ -161,8 +161,6 @@ struct klt_hip_ctx {
   size_t astate_cap = 0, aidx_cap = 0;
   std::string err;
   int force_generic = 0;
-  int pyr_strips = 0;      // fused pyramids: 0 auto (k_pyr_strip for batched launches), 1 tiles, 2 strips
-  int strip_seg = 0;       // k_pyr_strip blocks per workgroup (0: the whole height)
   int track_order = 0;  // 0: band-sorted, XCD-major processing order; 1: input order
   int track_patch = 1;  // one-feature waves gather through a lane patch when the window fits
   int track_merge = 1;   // defer finest-level residues into the next frame's first pass (ResCarry)
@@ -423,32 +421,6 @@ int launch_l0(klt_hip_ctx *c, hipStream_t st, const uint8_t *src, long pitch, lo
                                                hs, W1, do_hs, fs0, fsh, F, ty0, ty1));
 }
 
-// k_pyr_strip (both levels in one pass) applies to two-level default
-// pyramids of frames with 4-byte aligned rows; auto mode takes it for batched
-// launches (F frames of at least a few hundred strips in all), where its
-// per-strip warm-up is small and the frames give the parallelism
-bool strip_ok(const klt_hip_pyr_desc *d, const uint8_t *src, long pitch, long stride) {
-  return d->nlevels == 2 && d->subsampling == kSS && d->ncols % 4 == 0 && d->ncols >= 16 && d->nrows >= 4 &&
-         pitch % 4 == 0 && stride % 4 == 0 && ((uintptr_t)src & 3) == 0;
-}
-
-bool use_strips(klt_hip_ctx *c, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch, long stride, int F) {
-  if (c->pyr_strips == 1 || !strip_ok(d, src, pitch, stride)) return false;
-  if (c->pyr_strips == 2) return true;
-  const int nstrips = (d->ncols + 127) / 128;
-  return (long)F * nstrips >= 256;
-}
-
-int launch_strip(klt_hip_ctx *c, hipStream_t st, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
-                 long stride, Level *lv, long fs0, long fs1, int F) {
-  const int W = d->ncols, H = d->nrows;
-  const bool v16 = W % 16 == 0 && pitch % 16 == 0 && stride % 16 == 0 && ((uintptr_t)src & 15) == 0;
-  TimedScope ts(c, T_STRIP, st, F);
-  return launched(c, "k_pyr_strip", launch_pyr_strip(st, src, (int)pitch, stride, W, H, default_taps(d), v16,
-                                                     lv[0].img, lv[0].gx, lv[0].gy, lv[1].img, lv[1].gx, lv[1].gy,
-                                                     fs0, fs1, F, c->strip_seg));
-}
-
 int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
                 hipStream_t st) {
   Slot &S = c->slot[s];
@@ -456,9 +428,8 @@ int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t 
   const DefTaps T = default_taps(d);
   const bool two = d->nlevels == 2;
   const int W1 = two ? S.lv[1].w : 0, H1 = two ? S.lv[1].h : 0;
-  if ((long)W * H == 0) return 0;
-  if (use_strips(c, d, src, pitch, 0L, 1)) return launch_strip(c, st, d, src, pitch, 0L, S.lv, 0L, 0L, 1);
   if (two && grow(c, &c->d_hs, &c->hs_cap, (size_t)hs_size(W1 > 0 ? W1 : 1, H))) return -1;
+  if ((long)W * H == 0) return 0;
   const int vec_u8 = (W % 4 == 0 && W >= 16 && pitch % 4 == 0 && ((uintptr_t)src & 3) == 0) ? 1 : 0;
   const int vec_out = (W % 4 == 0) ? 1 : 0;
   {
@@ -577,21 +548,17 @@ int ensure_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, int frames) 
     w /= K.ss;
     h /= K.ss;
   }
-  K.frames = frames;
-  return 0;
-}
-
-// the tile path's sigma-3.6 row-pass buffer for the whole of bank K, on first
-// use (k_pyr_strip needs none); it changes size only with the bank
-int ensure_bank_hs(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d) {
-  const size_t need = (size_t)hs_size(K.lv[1].w > 0 ? K.lv[1].w : 1, d->nrows) * K.frames;
-  if (K.hs_cap < need || !K.hs) {
-    hipFree(K.hs);
-    K.hs = nullptr;
-    K.hs_cap = 0;
-    HIPCHK(c, hipMalloc((void **)&K.hs, need * sizeof(float)));
-    K.hs_cap = need;
+  if (d->nlevels == 2) {
+    const size_t need = (size_t)hs_size(K.lv[1].w > 0 ? K.lv[1].w : 1, d->nrows) * frames;
+    if (K.hs_cap < need || !K.hs) {
+      hipFree(K.hs);
+      K.hs = nullptr;
+      K.hs_cap = 0;
+      HIPCHK(c, hipMalloc((void **)&K.hs, need * sizeof(float)));
+      K.hs_cap = need;
+    }
   }
+  K.frames = frames;
   return 0;
 }
 
@@ -611,14 +578,6 @@ int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const u
   const int vec_out = (W % 4 == 0) ? 1 : 0;
   const long fs0 = (long)W * H, fsh = hs_size(W1, H), fs1 = (long)W1 * H1;
   int r0 = clampi(row_lo, 0, H), r1 = row_hi >= H ? H : clampi(row_hi, r0, H);
-  if (r0 == 0 && r1 >= H && use_strips(c, d, src, pitch, stride, F)) {
-    for (int l = 0; l < d->nlevels; ++l) {
-      K.vlo[l] = 0;
-      K.vhi[l] = 1 << 30;
-    }
-    return launch_strip(c, st, d, src, pitch, stride, K.lv, fs0, fs1, F);
-  }
-  if (two && ensure_bank_hs(c, K, d)) return -1;
   {
     TimedScope ts(c, T_L0, st, F);
     if (launch_l0(c, st, src, pitch, stride, W, H, T, vec_u8, vec_out, K.lv[0].img, K.lv[0].gx, K.lv[0].gy, K.hs,
@@ -759,8 +718,6 @@ KLT_API int klt_hip_ctx_reset(klt_hip_ctx *c) {
   HIPCHK(c, hipDeviceSynchronize());  // nothing of the previous owner is still running
   c->stream = c->own;
   c->force_generic = 0;
-  c->pyr_strips = 0;
-  c->strip_seg = 0;
   c->track_order = 0;
   c->track_patch = 1;
   c->track_merge = 1;
@@ -880,15 +837,6 @@ static int build_pyramid_on(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, co
 KLT_API int klt_hip_set_path(klt_hip_ctx *c, int force_generic) {
   if (!c) return -1;
   c->force_generic = force_generic != 0;
-  return 0;
-}
-
-KLT_API int klt_hip_set_pyr_strips(klt_hip_ctx *c, int mode, int seg_blocks) {
-  if (!c) return -1;
-  if (mode < 0 || mode > 2) return fail(c, "set_pyr_strips: mode %d (0 auto, 1 tiles, 2 strips)", mode);
-  if (seg_blocks < 0) return fail(c, "set_pyr_strips: seg_blocks %d < 0", seg_blocks);
-  c->pyr_strips = mode;
-  c->strip_seg = seg_blocks;
   return 0;
 }
 
@@ -1282,6 +1230,7 @@ bool bank_fits(const Bank &K, const klt_hip_pyr_desc *d, int F) {
     w /= K.ss;
     h /= K.ss;
   }
+  if (d->nlevels == 2 && K.hs_cap < (size_t)(K.lv[1].w > 0 ? K.lv[1].w : 1) * d->nrows * F) return false;
   return true;
 }
 
@@ -1729,8 +1678,8 @@ KLT_API int klt_hip_set_timing(klt_hip_ctx *c, int on) {
 KLT_API int klt_hip_get_timing(klt_hip_ctx *c, klt_hip_timing *out) {
   if (!c || !out) return -1;
   if (klt_hip_sync(c)) return -1;
-  double ms[T_N] = {};
-  int cnt[T_N] = {};
+  double ms[T_N] = {0, 0, 0, 0, 0};
+  int cnt[T_N] = {0, 0, 0, 0, 0};
   for (int k = 0; k < T_N; ++k) {
     for (auto &p : c->ev_used[k]) {
       float t = 0.0f;
@@ -1756,9 +1705,6 @@ KLT_API int klt_hip_get_timing(klt_hip_ctx *c, klt_hip_timing *out) {
   out->frames_pyr_l0 = c->frames_timed[T_L0];
   out->frames_pyr_l1 = c->frames_timed[T_L1];
   out->frames_track = c->frames_timed[T_TRACK];
-  out->n_pyr_strip = cnt[T_STRIP];
-  out->ms_pyr_strip = ms[T_STRIP];
-  out->frames_pyr_strip = c->frames_timed[T_STRIP];
   for (auto &f : c->frames_timed) f = 0;
   return 0;
 }

@@ -41,8 +41,7 @@ class Timing(C.Structure):
                 ("n_eigen", C.c_int), ("n_generic", C.c_int), ("ms_pyr_l0", C.c_double),
                 ("ms_pyr_l1", C.c_double), ("ms_track", C.c_double), ("ms_eigen", C.c_double),
                 ("ms_generic", C.c_double), ("frames_pyr_l0", C.c_long), ("frames_pyr_l1", C.c_long),
-                ("frames_track", C.c_long),
-                ("n_pyr_strip", C.c_int), ("ms_pyr_strip", C.c_double), ("frames_pyr_strip", C.c_long)]
+                ("frames_track", C.c_long)]
 
 
 V = C.c_void_p
@@ -71,7 +70,6 @@ DEVICE_PROTOS = {
     "klt_hip_set_frames_overlap": (C.c_int, [V, C.c_int]),
     "klt_hip_set_host_threads": (C.c_int, [V, C.c_int]),
     "klt_hip_set_path": (C.c_int, [V, C.c_int]),
-    "klt_hip_set_pyr_strips": (C.c_int, [V, C.c_int, C.c_int]),
     "klt_hip_level_dims": (C.c_int, [V, C.c_int, C.c_int, IP, IP]),
     "klt_hip_download_level": (C.c_int, [V, C.c_int, C.c_int, C.c_int, V]),
     "klt_hip_level_ptr": (V, [V, C.c_int, C.c_int, C.c_int]),

@@ -38,14 +38,12 @@ class Dev:
         self.lib.klt_amd_pyr_desc(self.tc, w, h, n, smooth, C.byref(d))
         return d
 
-    def build(self, img: np.ndarray, slot=0, nlevels=None, smooth=1, force_generic=False, strips=(0, 0)):
-        """strips: (mode, seg_blocks) of klt_hip_set_pyr_strips (2 = k_pyr_strip wherever it applies)"""
+    def build(self, img: np.ndarray, slot=0, nlevels=None, smooth=1, force_generic=False):
         lib, ctx = self.lib, self.ctx
         h, w = img.shape
         d = self.desc(w, h, nlevels, smooth)
         img = np.ascontiguousarray(img)
         check(lib, ctx, lib.klt_hip_set_path(ctx, 1 if force_generic else 0), "set_path")
-        check(lib, ctx, lib.klt_hip_set_pyr_strips(ctx, strips[0], strips[1]), "set_pyr_strips")
         check(lib, ctx, lib.klt_hip_upload_frame(ctx, 0, img.ctypes.data, w, h), "upload")
         check(lib, ctx, lib.klt_hip_build_pyramid(ctx, slot, C.byref(d), None, 0, 0), "build")
         return d

@@ -62,36 +62,6 @@ def test_fused_pyramid_shapes_vs_oracle(gpu, oracle, shape):
     assert_planes_equal(dev.levels(0, 2), oracle_for(oracle, dev.tc).frame_pyramid(img), f"tiles {shape}")
 
 
-# k_pyr_strip (both levels in one pass, 128-column strips walked in 4-row
-# blocks): widths multiple of 4 incl. 16-byte (v16) and 4-byte row paths,
-# strips partly outside the frame, heights not multiple of 4, and segments
-# of 1 .. 17 blocks (each with its own warm-up rows) as well as whole strips
-STRIP_KERNEL_CASES = [((240, 320), 0), ((480, 640), 0), ((480, 640), 1), ((1080, 1920), 0), ((1080, 1920), 17),
-                      ((67, 136), 0), ((67, 136), 3), ((31, 40), 0), ((9, 64), 1), ((200, 72), 5), ((113, 516), 2),
-                      ((251, 332), 0), ((150, 200), 7), ((4, 16), 0), ((7, 20), 1)]
-
-
-@pytest.mark.parametrize("shape,seg", STRIP_KERNEL_CASES, ids=[f"{h}x{w}-seg{s}" for (h, w), s in STRIP_KERNEL_CASES])
-def test_strip_pyramid_vs_oracle(gpu, oracle, shape, seg):
-    h, w = shape
-    img = synth(gpu, 6060 + w + h, w, h, 1)[0]
-    dev = Dev(gpu)
-    dev.build(img, strips=(2, seg))
-    assert dev.path(0) == 1
-    assert_planes_equal(dev.levels(0, 2), oracle_for(oracle, dev.tc).frame_pyramid(img), f"strips {shape} seg {seg}")
-
-
-@pytest.mark.parametrize("seg", [0, 9])
-def test_strip_pyramid_4k_equals_tiles(gpu, seg):
-    """k_pyr_strip == k_pyr_l0 + k_pyr_l1 (themselves pinned to the oracle at 4K above), bit for bit."""
-    h, w = 2160, 3840
-    img = synth(gpu, 3840 + seg, w, h, 1)[0]
-    dev = Dev(gpu)
-    dev.build(img, slot=0, strips=(1, 0))
-    dev.build(img, slot=1, strips=(2, seg))
-    assert_planes_equal(dev.levels(1, 2), dev.levels(0, 2), f"strips 4K seg {seg}")
-
-
 @pytest.mark.parametrize("shape", [(240, 320), (251, 333), (67, 129)])
 def test_generic_equals_fused(gpu, shape):
     h, w = shape

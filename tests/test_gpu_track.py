@@ -428,18 +428,6 @@ def test_tracker_tuning_hooks_do_not_change_results(gpu, oracle, opts):
     assert_table_equal(X, Y, V, *OracleTracker(oracle).harness(frames, 3000, 8, first=frames[0]))
 
 
-@pytest.mark.parametrize("opts", [dict(strips=(2, 0)), dict(strips=(2, 5), overlap=1), dict(strips=(1, 0)),
-                                  dict(strips=(2, 0), chunk=1)], ids=["strips", "strips-seg5-overlap", "tiles",
-                                                                      "strips-chunk1"])
-def test_batched_pyramid_kernels_vs_oracle(gpu, oracle, opts):
-    """The batched path with each pyramid kernel forced: k_pyr_strip (whole
-    strips, 5-block segments) and the k_pyr_l0 + k_pyr_l1 tiles give the
-    oracle's tracks, bit for bit."""
-    frames = synth(gpu, 5152, 640, 480, 10)
-    X, Y, V = batch_sequence_opts(gpu, frames, 1500, 4, opts)
-    assert_table_equal(X, Y, V, *OracleTracker(oracle).harness(frames, 1500, 10, first=frames[0]))
-
-
 @pytest.mark.parametrize("opts", [dict(overlap=1), dict(overlap=0), dict(overlap=1, merge=0)])
 def test_overlapped_schedule_1080p(gpu, oracle, opts):
     """The bench's overlapped schedule -- pyramids of chunk c+1 built on their
@@ -460,7 +448,6 @@ def batch_sequence_opts(gpu, frames, nfeat, chunk, opts, counts=None):
         assert gpu.klt_hip_set_track_order(ctx, opts.get("order", 0)) == 0
         assert gpu.klt_hip_set_frames_overlap(ctx, opts.get("overlap", 0)) == 0
         assert gpu.klt_hip_set_track_merge(ctx, opts.get("merge", 1)) == 0
-        assert gpu.klt_hip_set_pyr_strips(ctx, *opts.get("strips", (0, 0))) == 0
         return ctx
 
     gpu.klt_amd_device_context = hooked

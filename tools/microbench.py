@@ -47,8 +47,6 @@ def main():
     ap.add_argument("--count", action="store_true", help="frames: count Newton iterations / passes of the timed rep")
     ap.add_argument("--host-threads", type=int, default=-1, help="apiseq: host pool workers (-1: default)")
     ap.add_argument("--generic", action="store_true")
-    ap.add_argument("--strips", type=int, default=0, help="pyramid kernels: 0 auto, 1 tiles, 2 k_pyr_strip")
-    ap.add_argument("--strip-seg", type=int, default=0, help="k_pyr_strip blocks per workgroup (0: whole height)")
     ap.add_argument("--max-it", type=int, default=0, help="tracker: override max_iterations")
     ap.add_argument("--lost", action="store_true", help="tracker: mark every feature lost (launch floor)")
     ap.add_argument("--window", type=int, default=0, help="tracker: override window width/height")
@@ -65,7 +63,6 @@ def main():
     lib.klt_amd_set_reduction(tc, 0 if a.reduction == "exact" else 1)
     ctx = lib.klt_amd_device_context(tc)
     lib.klt_hip_set_path(ctx, 1 if a.generic else 0)
-    check(lib, ctx, lib.klt_hip_set_pyr_strips(ctx, a.strips, a.strip_seg), "strips")
     check(lib, ctx, lib.klt_hip_set_track_order(ctx, 1 if a.input_order else 0), "order")
     check(lib, ctx, lib.klt_hip_set_track_merge(ctx, 0 if a.no_merge else 1), "merge")
     check(lib, ctx, lib.klt_hip_set_track_patch(ctx, 0 if a.no_patch else 1), "patch")
@@ -243,9 +240,6 @@ def main():
                     "us_per_frame_wall": 1e6 * wall / done,
                     "l0_us_per_frame": 1e3 * tm.ms_pyr_l0 / max(tm.frames_pyr_l0, 1),
                     "l1_us_per_frame": 1e3 * tm.ms_pyr_l1 / max(tm.frames_pyr_l1, 1),
-                    "strip_us_per_frame": 1e3 * tm.ms_pyr_strip / max(tm.frames_pyr_strip, 1),
-                    "pass_us_per_frame": 1e3 * (tm.ms_pyr_l0 + tm.ms_pyr_l1 + tm.ms_pyr_strip)
-                                         / max(tm.frames_pyr_l0 + tm.frames_pyr_strip, 1),
                     "track_us_per_frame": 1e3 * tm.ms_track / max(tm.frames_track, 1),
                     "status_hist": {int(k): int(c) for k, c in zip(*np.unique(vv, return_counts=True))}})
     else:
