@@ -54,14 +54,15 @@ def parse():
     p.add_argument("--height", type=int, default=None, help="default 1080 (sharded 2160)")
     p.add_argument("--features", type=int, default=None, help="default 5000 (sharded 20000)")
     p.add_argument("--seed", type=int, default=None, help="default 1080 (sharded 2160)")
-    p.add_argument("--margin", type=int, default=128, help="sharded: level-0 rows built beyond a band")
+    p.add_argument("--margin", type=int, default=64, help="sharded: level-0 rows built beyond a band")
     p.add_argument("--cpu-frames", type=int, default=160,
                    help="frames of the bounded CPU-baseline sample (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-4k", action="store_true", help="skip the 4K pyramid-pass roofline line (rank 0, N=1)")
     p.add_argument("--reduction", choices=["exact", "fast"], default="exact")
     p.add_argument("--chunk", type=int, default=None,
-                   help="frames per batched pyramid/track launch (klt_hip_track_frames; default 64, sharded 32; "
+                   help="frames per batched pyramid/track launch (klt_hip_track_frames; default 64; sharded: frames "
+                        "per exchange, 64; "
                         "capped at ceil(steps/2) so that the timed region always holds >= 2 chunks and the "
                         "overlapped schedule really runs); 0 = the per-frame pipelined path (klt_hip_track_sequence)")
     p.add_argument("--api-frames", type=int, default=200,
@@ -76,7 +77,7 @@ def parse():
     a = p.parse_args()
     sharded = a.mode == "sharded"
     for k, dflt, shd in (("steps", 489, 490), ("warmup", 10, 64), ("width", 1920, 3840), ("height", 1080, 2160),
-                         ("features", 5000, 20000), ("seed", 1080, 2160), ("chunk", 64, 32)):
+                         ("features", 5000, 20000), ("seed", 1080, 2160), ("chunk", 64, 64)):
         if getattr(a, k) is None:
             setattr(a, k, shd if sharded else dflt)
     a.chunk_requested = a.chunk
@@ -218,6 +219,21 @@ def main() -> None:
         # feature-frames: features live when frame j starts (table row j-1 holds the list after j-1)
         ff = int((tab[2][t_start - 1:t_start - 1 + args.steps] >= 0).sum().item())
         tracker = tracker_line(solves.value, passes.value, ff, tm)
+        pmc = ROOT / "profiles" / "pmc_tracker.json"
+        if pmc.exists():
+            try:
+                d = json.loads(pmc.read_text())
+                if d.get("workload", "").startswith(f"{W}x{H}, {NF} features"):
+                    # the tracker's bound is instruction issue, not HBM; its VALU
+                    # instructions per iteration (PMC) set an issue ceiling beside the measured rate
+                    tracker["pmc"] = {k: d[k] for k in ("per_iteration", "valu_issue_busy", "wave_time_split",
+                                                        "issue_ceiling_iterations_per_s", "clock_hz_assumed")}
+                    tracker["pmc"]["source"] = str(pmc.relative_to(ROOT))
+                    if tracker.get("feature_iterations_per_s"):
+                        tracker["frac_of_issue_ceiling"] = (tracker["feature_iterations_per_s"]
+                                                            / d["issue_ceiling_iterations_per_s"])
+            except Exception:
+                pass
 
     fast = None
     if args.chunk > 0 and args.reduction == "exact" and not args.no_fast and rank == 0:

@@ -256,17 +256,23 @@ int klt_hip_track_frames_host(klt_hip_ctx *ctx, const klt_hip_pyr_desc *pdesc,
 /* one chunk of the feature-sharded sequence (BASELINE config 4), for one rank
    of a row-band decomposition: like klt_hip_track_frames over nframes frames
    (one chunk), but the pyramids are built only for level-0 rows
-   [row_lo, row_hi) (whole tiles, full-frame values) and only live features
+   [row_lo, row_hi) (whole tiles, full-frame values; level-1 rows are valid
+   where their sigma-3.6 support lies inside them) and only live features
    with own_lo <= y < own_hi at the chunk start are tracked (updated in place;
    the others are left untouched for the caller's exchange).  A feature whose
    window needs rows outside the built ones sets *escape (device int, caller
    zeroes it) and its result is invalid: the caller then redoes the chunk from
    full-frame pyramids (klt_hip_frames_begin on the frame before the chunk,
-   row_lo = 0, row_hi = nrows).  Needs the default (fused) pyramid parameters. */
+   row_lo = 0, row_hi = nrows).  next_frames (optional, next_nframes frames
+   at the same pitch/stride): the next chunk, whose band pyramids are then
+   built on the context's pyramid stream while this chunk is tracked and the
+   caller exchanges results; the next call with exactly those frames and rows
+   uses them.  Needs the default (fused) pyramid parameters. */
 int klt_hip_track_frames_band(klt_hip_ctx *ctx, const klt_hip_pyr_desc *pdesc,
                               const klt_hip_track_desc *tdesc, const unsigned char *frames, long pitch,
                               long stride, int nframes, float *x, float *y, int *val, int n, float own_lo,
-                              float own_hi, int row_lo, int row_hi, int *escape);
+                              float own_hi, int row_lo, int row_hi, int *escape,
+                              const unsigned char *next_frames, int next_nframes);
 
 /* trackability map of level 0 of `slot`: nx*ny int values, row-major over the
    border-trimmed grid; vals == NULL only reports nx, ny.  Synchronous. */

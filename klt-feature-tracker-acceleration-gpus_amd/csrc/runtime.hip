@@ -185,6 +185,13 @@ struct klt_hip_ctx {
   unsigned long long *prof = nullptr;  // instrumented build: per-wave tracker phase counters
   Bank bank[3];
   int bank_next = 0;
+  // band mode: a bank whose pyramids were built ahead, during the previous
+  // call's tracking (klt_hip_track_frames_band's next_frames); -1: none
+  struct {
+    int bank = -1, F = 0, row_lo = 0, row_hi = 0;
+    const unsigned char *src = nullptr;
+    long stride = 0;
+  } pre;
   PrevRef prev;
   bool frames_ready = false;
   hipEvent_t ev_bbuilt[3] = {}, ev_bfree[3] = {};
@@ -587,15 +594,19 @@ int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const u
   K.vlo[0] = r0;
   K.vhi[0] = r1 >= H ? (1 << 30) : r1;
   if (two && (long)W1 * H1 > 0) {
-    // an L1 tile at rows [y0, y0+TH) reads hs rows [4*y0-20, 4*y0-20+HR) (clamped to the image)
+    // level-1 row Y (img1 and its gradients) reads hs rows 4Y-20 .. 4Y+24:
+    // it is exact when those lie inside the built level-0 rows (or past an
+    // image edge, where the zero rules apply).  The L1 tiles covering the
+    // valid rows are launched whole; their rows outside [vlo, vhi) read stale
+    // hs rows and are never used (the tracker's band test stops at vlo/vhi).
     const int TH1 = geom::L1_TH;
     const int nt1 = (H1 + TH1 - 1) / TH1;
-    const int last = geom::L1_HR - 20;  // 4*y0 + last is the last hs row read
-    const int t1lo = r0 == 0 ? 0 : (r0 + 20 + 4 * TH1 - 1) / (4 * TH1);
-    const int t1hi = r1 >= H ? nt1 : (r1 > last ? clampi((r1 - last - 1) / (4 * TH1) + 1, 0, nt1) : 0);
-    K.vlo[1] = t1lo * TH1;
-    K.vhi[1] = t1hi >= nt1 ? (1 << 30) : t1hi * TH1;
-    if (t1hi > t1lo) {
+    const int ylo = r0 == 0 ? 0 : (r0 + 20 + 3) / 4;
+    const int yhi = r1 >= H ? H1 : (r1 >= 25 ? (r1 - 25) / 4 + 1 : 0);
+    K.vlo[1] = ylo;
+    K.vhi[1] = yhi >= H1 ? (1 << 30) : yhi;
+    if (yhi > ylo) {
+      const int t1lo = ylo / TH1, t1hi = clampi((yhi + TH1 - 1) / TH1, t1lo, nt1);
       TimedScope ts(c, T_L1, st, F);
       const int vec = (W1 % 4 == 0 && W1 >= 8) ? 1 : 0;
       if (launched(c, "k_pyr_l1", launch_pyr_l1(st, K.hs, W1, H, H1, T, vec, K.lv[1].img, K.lv[1].gx, K.lv[1].gy,
@@ -724,6 +735,7 @@ KLT_API int klt_hip_ctx_reset(klt_hip_ctx *c) {
   c->serial_frames = 1;
   c->prof = nullptr;
   c->frames_ready = false;
+  c->pre.bank = -1;
   c->timing = false;
   for (int k = 0; k < T_N; ++k) {
     for (auto &p : c->ev_used[k]) {
@@ -1301,6 +1313,8 @@ struct BandSpec {
   float own[2];        // features owned: own[0] <= y < own[1] (level-0 rows) at the chunk start
   int row_lo, row_hi;  // level-0 rows to build
   int *escape;         // device flag
+  const unsigned char *next;  // optional: the next chunk's frames, built ahead on the pyramid stream
+  int next_n;
 };
 
 int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
@@ -1366,9 +1380,13 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     }
     for (auto &K : c->bank)
       if (ensure_bank(c, K, pd, chunk)) return -1;
+    c->pre.bank = -1;
   }
+  // band calls always use both streams: the next chunk's band pyramids are
+  // built on the pyramid stream while this chunk is tracked and exchanged
+  const bool serial = band ? false : c->serial_frames != 0;
   // the pyramid stream starts behind everything already queued on the tracking stream
-  if (!c->serial_frames) {
+  if (!serial) {
     HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_start, 0));
   }
@@ -1385,11 +1403,15 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     const unsigned char *src = frames + (long)j0 * stride;
     // overlapped: the pyramid stream builds chunk c+1 while chunk c is tracked;
     // serial: both on the tracking stream (no two kernels share the CUs)
-    const bool serial = c->serial_frames != 0;
     hipStream_t ps = serial ? c->stream : c->pstream;
+    const bool prebuilt = band && c->pre.bank == bi && c->pre.src == src && c->pre.F == Fc &&
+                          c->pre.stride == stride && c->pre.row_lo == band->row_lo && c->pre.row_hi == band->row_hi;
+    if (c->pre.bank == bi) c->pre.bank = -1;  // taken now, or about to be overwritten
     // one stream: stream order is the dependency (an event wait would add a queue barrier)
-    if (!serial) HIPCHK(c, hipStreamWaitEvent(ps, c->ev_bfree[bi], 0));
-    if (fz) {
+    if (!serial && !prebuilt) HIPCHK(c, hipStreamWaitEvent(ps, c->ev_bfree[bi], 0));
+    if (prebuilt) {
+      // ev_bbuilt[bi] was recorded after that build: the wait below orders it
+    } else if (fz) {
       if (band ? build_fused_bank(c, K, pd, src, pitch, stride, Fc, ps, band->row_lo, band->row_hi)
                : build_fused_bank(c, K, pd, src, pitch, stride, Fc, ps))
         return -1;
@@ -1405,7 +1427,7 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
       }
     }
     if (!serial) {
-      HIPCHK(c, hipEventRecord(c->ev_bbuilt[bi], ps));
+      if (!prebuilt) HIPCHK(c, hipEventRecord(c->ev_bbuilt[bi], ps));
       HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_bbuilt[bi], 0));
     }
     TrkFramesArgs b;
@@ -1427,6 +1449,22 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
       return -1;
     if (!serial && c->prev.bank >= 0) HIPCHK(c, hipEventRecord(c->ev_bfree[c->prev.bank], c->stream));
     c->prev = PrevRef{bi, Fc - 1};
+  }
+  if (band && band->next && band->next_n > 0 && fz) {
+    // the next chunk's band pyramids, into the bank it will take, on the
+    // pyramid stream: they depend on frames only, not on this chunk's result
+    const int bj = c->bank_next;
+    const int Fn = band->next_n < chunk ? band->next_n : chunk;
+    HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_bfree[bj], 0));
+    if (build_fused_bank(c, c->bank[bj], pd, band->next, pitch, stride, Fn, c->pstream, band->row_lo, band->row_hi))
+      return -1;
+    HIPCHK(c, hipEventRecord(c->ev_bbuilt[bj], c->pstream));
+    c->pre.bank = bj;
+    c->pre.src = band->next;
+    c->pre.F = Fn;
+    c->pre.stride = stride;
+    c->pre.row_lo = band->row_lo;
+    c->pre.row_hi = band->row_hi;
   }
   return 0;
 }
@@ -1599,9 +1637,10 @@ KLT_API int klt_hip_track_frames_host(klt_hip_ctx *c, const klt_hip_pyr_desc *pd
 KLT_API int klt_hip_track_frames_band(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
                                       const unsigned char *frames, long pitch, long stride, int nframes,
                                       float *x, float *y, int *val, int n, float own_lo, float own_hi,
-                                      int row_lo, int row_hi, int *escape) {
+                                      int row_lo, int row_hi, int *escape, const unsigned char *next_frames,
+                                      int next_nframes) {
   if (!escape) return fail(c, "track_frames_band: null escape flag");
-  BandSpec bs{{own_lo, own_hi}, row_lo, row_hi, escape};
+  BandSpec bs{{own_lo, own_hi}, row_lo, row_hi, escape, next_frames, next_nframes};
   return track_frames_impl(c, pd, td, frames, pitch, stride, nframes, nframes > 0 ? nframes : 1, x, y, val, n,
                            nullptr, nullptr, nullptr, 0, &bs);
 }

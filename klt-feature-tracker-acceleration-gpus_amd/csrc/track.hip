@@ -715,8 +715,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KLT_TRAC
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   // consecutive workgroups land on the 8 XCDs round-robin: give each XCD a
   // contiguous run of the (band-sorted) order so its L2 sees one image band
-  const int blk = b.xcd_per > 0 ? (int)(blockIdx.x % 8) * b.xcd_per + (int)(blockIdx.x / 8) : (int)blockIdx.x;
   if (b.n_dev) n = *b.n_dev;
+  // band mode: the grid is sized for every feature, but only the n_dev kept
+  // ones are processed -- spread THEIR blocks over the 8 XCDs (a per-XCD run
+  // sized for all features would put a small band on one XCD)
+  const int xcd_per = b.n_dev && b.xcd_per > 0 ? ((n + kBlock / kWave * G - 1) / (kBlock / kWave * G) + 7) / 8
+                                                 : b.xcd_per;
+  if (xcd_per > 0 && (int)(blockIdx.x / 8) >= xcd_per) return;  // past this XCD's run: no duplicate slots
+  const int blk = xcd_per > 0 ? (int)(blockIdx.x % 8) * xcd_per + (int)(blockIdx.x / 8) : (int)blockIdx.x;
   const int s0 = (blk * (kBlock / kWave) + wave) * G;
   if (s0 >= n) return;  // whole wave; the kernel has no workgroup barrier
   const int g = lane / LG, slot = s0 + g;
@@ -742,7 +748,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KLT_TRAC
   const unsigned long long wall0 = wall_clock64();
 #endif
   // deferred residues (ResCarry): one-feature waves, exact sums, default gain
-  const bool merge = G == 1 && EXACT && !LI && a.merge_res && a.nlev >= 2 && !a.escape;
+  // (band mode too: the residue's rows were checked against the band at frame
+  // j's final position, and an escape voids the whole chunk anyway)
+  const bool merge = G == 1 && EXACT && !LI && a.merge_res && a.nlev >= 2;
   ResCarry<PPL> rc;
   TrkCount cnt;
   for (int j = 0; j < b.nframes; ++j) {

@@ -13,7 +13,10 @@ full-frame pyramids, so the result never depends on the margin.
 The data path has one collective per chunk: 3*n+1 int32 (240 KB at 20k
 features) -- the position exchange the path really has, with the escape flag
 riding along as its last element -- and one host read of that flag after it.
-Only a chunk that escaped costs a second build and a second exchange.
+Only a chunk that escaped costs a second build and a second exchange.  The
+next chunk's band pyramids depend on frames only, so each call hands the
+library the next chunk's frames: it builds them on its pyramid stream while
+this chunk is tracked and exchanged.
 """
 from __future__ import annotations
 
@@ -22,9 +25,12 @@ from dataclasses import dataclass
 
 import torch
 
-# level-0 rows built beyond the band: L1 tiles need ~52 rows of sigma-3.6
-# input on each side, the L1 window 4*(hh+1) more, plus a chunk of motion
-DEFAULT_MARGIN = 128
+# level-0 rows built beyond the band: a level-1 row needs sigma-3.6 input 20
+# rows above and 24 below its level-0 rows (the library marks exactly those
+# rows valid), the level-1 window 4*(hh+1) more, plus a chunk of motion;
+# tools/shard_sim.py: 48 and 64 never escaped at 4K/20k features (32- and
+# 64-frame chunks), 32 did
+DEFAULT_MARGIN = 64
 
 
 @dataclass(frozen=True)
@@ -80,7 +86,7 @@ class ShardedSequence:
     """
 
     def __init__(self, lib, ctx, pd, td, frames: torch.Tensor, x, y, v, rank: int, world: int, all_reduce,
-                 chunk: int = 32, margin: int = DEFAULT_MARGIN):
+                 chunk: int = 64, margin: int = DEFAULT_MARGIN):
         from .device import check
         self.lib, self.ctx, self.pd, self.td = lib, ctx, pd, td
         self.frames, self.x, self.y, self.v = frames, x, y, v
@@ -99,22 +105,24 @@ class ShardedSequence:
         self._check(self.lib, self.ctx, self.lib.klt_hip_frames_begin(self.ctx, C.byref(self.pd), self._ptr(t),
                                                                       self.W), "frames_begin")
 
-    def _band_call(self, t0: int, n: int, row_lo: int, row_hi: int) -> None:
+    def _band_call(self, t0: int, n: int, row_lo: int, row_hi: int, next_t0: int = 0, next_n: int = 0) -> None:
         b = self.band
         self._check(self.lib, self.ctx, self.lib.klt_hip_track_frames_band(
             self.ctx, C.byref(self.pd), C.byref(self.td), self._ptr(t0), self.W, self.H * self.W, n,
             C.c_void_p(self.x.data_ptr()), C.c_void_p(self.y.data_ptr()), C.c_void_p(self.v.data_ptr()),
-            self.x.numel(), b.own_lo, b.own_hi, row_lo, row_hi, C.c_void_p(self.escape.data_ptr())),
-            "track_frames_band")
+            self.x.numel(), b.own_lo, b.own_hi, row_lo, row_hi, C.c_void_p(self.escape.data_ptr()),
+            self._ptr(next_t0) if next_n > 0 else None, next_n), "track_frames_band")
 
     def run(self, t0: int, nframes: int) -> None:
         """Track frames t0 .. t0+nframes-1 (the pyramid of t0-1 must be current:
         begin(t0-1) first, or a previous run ending at t0-1)."""
-        for c0 in range(t0, t0 + nframes, self.chunk):
-            n = min(self.chunk, t0 + nframes - c0)
+        end = t0 + nframes
+        for c0 in range(t0, end, self.chunk):
+            n = min(self.chunk, end - c0)
+            nn = min(self.chunk, end - c0 - n)  # the next chunk, built ahead
             xs, ys, vs = self.x.clone(), self.y.clone(), self.v.clone()
             self.escape.zero_()
-            self._band_call(c0, n, self.band.row_lo, self.band.row_hi)
+            self._band_call(c0, n, self.band.row_lo, self.band.row_hi, c0 + n, nn)
             # one collective: the owners' results and the escape flag summed over ranks
             flag = merge_chunk(self.x, self.y, self.v, ys, vs, self.band, self.rank, self.all_reduce,
                                escape=self.escape)
@@ -125,5 +133,5 @@ class ShardedSequence:
                 self.x.copy_(xs), self.y.copy_(ys), self.v.copy_(vs)
                 self.begin(c0 - 1)
                 self.escape.zero_()
-                self._band_call(c0, n, 0, self.H)
+                self._band_call(c0, n, 0, self.H, c0 + n, nn)
                 merge_chunk(self.x, self.y, self.v, ys, vs, self.band, self.rank, self.all_reduce)

@@ -135,17 +135,20 @@ class _Rank:
     def begin(self, t):
         assert self.gpu.klt_hip_frames_begin(self.ctx, C.byref(self.pd), self.ptr(t), self.W) == 0
 
-    def chunk(self, t0, n, x, y, v, esc, full=False):
+    def chunk(self, t0, n, x, y, v, esc, full=False, next_n=0):
+        """next_n > 0: frames t0+n .. are the next chunk, built ahead (klt_hip_track_frames_band's next_frames)"""
         b = self.band
         rc = self.gpu.klt_hip_track_frames_band(
             self.ctx, C.byref(self.pd), C.byref(self.td), self.ptr(t0), self.W, self.H * self.W, n,
             C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()), x.numel(),
-            b.own_lo, b.own_hi, 0 if full else b.row_lo, self.H if full else b.row_hi, C.c_void_p(esc.data_ptr()))
+            b.own_lo, b.own_hi, 0 if full else b.row_lo, self.H if full else b.row_hi, C.c_void_p(esc.data_ptr()),
+            self.ptr(t0 + n) if next_n > 0 else None, next_n)
         assert rc == 0, self.gpu.klt_hip_last_error(self.ctx)
 
 
-def sharded_sequence(gpu, frames, nfeat, world, chunk, margin):
-    """Frames[0] selects; frames[1:] are tracked by `world` simulated ranks."""
+def sharded_sequence(gpu, frames, nfeat, world, chunk, margin, ahead=True):
+    """Frames[0] selects; frames[1:] are tracked by `world` simulated ranks
+    (ahead: each call builds the next chunk's band pyramids ahead)."""
     H, W = frames[0].shape
     dev = torch.device("cuda", 0)
     dfr = torch.from_numpy(np.ascontiguousarray(np.stack(frames))).to(dev)
@@ -158,12 +161,13 @@ def sharded_sequence(gpu, frames, nfeat, world, chunk, margin):
     T = len(frames) - 1
     for c0 in range(1, 1 + T, chunk):
         n = min(chunk, 1 + T - c0)
+        nn = min(chunk, 1 + T - c0 - n) if ahead else 0
         state = (x.clone(), y.clone(), v.clone())
         outs, esc_any = [], 0
         for rk in ranks:
             xr, yr, vr = (s.clone() for s in state)
             esc = torch.zeros(1, dtype=torch.int32, device=dev)
-            rk.chunk(c0, n, xr, yr, vr, esc)
+            rk.chunk(c0, n, xr, yr, vr, esc, next_n=nn)
             esc_any += int(esc.item())
             outs.append((xr, yr, vr))
         if esc_any:
@@ -173,7 +177,7 @@ def sharded_sequence(gpu, frames, nfeat, world, chunk, margin):
                 xr, yr, vr = (s.clone() for s in state)
                 esc = torch.zeros(1, dtype=torch.int32, device=dev)
                 rk.begin(c0 - 1)
-                rk.chunk(c0, n, xr, yr, vr, esc, full=True)
+                rk.chunk(c0, n, xr, yr, vr, esc, full=True, next_n=nn)
                 assert int(esc.item()) == 0
                 outs.append((xr, yr, vr))
         # the all-reduce, done by hand: sum of the ranks' kept bit patterns
@@ -192,11 +196,12 @@ def sharded_sequence(gpu, frames, nfeat, world, chunk, margin):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,chunk,margin", [(2, 4, 128), (3, 5, 128), (4, 3, 40), (2, 4, 0)])
-def test_sharded_equals_single_gpu(gpu, oracle, world, chunk, margin):
+@pytest.mark.parametrize("world,chunk,margin,ahead", [(2, 4, 128, True), (3, 5, 64, True), (4, 3, 40, True),
+                                                      (2, 4, 0, True), (3, 4, 64, False), (4, 3, 0, False)])
+def test_sharded_equals_single_gpu(gpu, oracle, world, chunk, margin, ahead):
     from kltabi import OracleTracker
     frames = synth(gpu, 2160 + world, 640, 480, 11)
-    x, y, v, redone = sharded_sequence(gpu, frames, 1500, world, chunk, margin)
+    x, y, v, redone = sharded_sequence(gpu, frames, 1500, world, chunk, margin, ahead)
     X, Y, V = OracleTracker(oracle).harness(frames, 1500, 11, first=frames[0])
     k = 11 - 2
     assert np.array_equal(v, V[:, k])
@@ -210,7 +215,7 @@ def test_sharded_equals_single_gpu(gpu, oracle, world, chunk, margin):
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_sharded_4k_20k_equals_reference(gpu, world):
     """BASELINE config 4 (3840x2160, 20000 features): the feature-sharded
-    schedule with 2/4/8 simulated ranks (32-frame chunks, 128-row margin)
+    schedule with 2/4/8 simulated ranks (32-frame chunks, 64-row margin, next chunk built ahead)
     reproduces the reference's list after 64 frames -- the digest of column 63
     of tests/golden/long_config4.json (oracle/_ref on the full sequence)."""
     import hashlib
@@ -219,7 +224,7 @@ def test_sharded_4k_20k_equals_reference(gpu, world):
     cfg = json.loads((GOLDEN / "long_config4.json").read_text())
     T = 64
     frames = synth(gpu, cfg["seed"], cfg["w"], cfg["h"], T + 1)
-    x, y, v, redone = sharded_sequence(gpu, frames, cfg["features"], world, 32, 128)
+    x, y, v, redone = sharded_sequence(gpu, frames, cfg["features"], world, 32, 64)
     h = hashlib.sha256()
     for a, dt in ((x, "<f4"), (y, "<f4"), (v, "<i4")):
         h.update(np.ascontiguousarray(a, dt).tobytes())
