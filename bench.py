@@ -348,14 +348,16 @@ def main() -> None:
 
 def run_sharded(args, world, rank, dev) -> None:
     """BASELINE config 4: one sequence (default 4K, 20k features); every rank
-    builds pyramids for its row band (+margin) and tracks the features it owns;
-    one all-reduce of the owners' (x, y, val) per chunk (kltamd.shard)."""
+    holds only the rows of each frame its band build reads (its band, margin
+    and tile halo: kltamd.shard.BandFrames, synthesized in place of its
+    ingest), builds pyramids for its row band (+margin) and tracks the features
+    it owns; one all-reduce of the owners' (x, y, val) per chunk (kltamd.shard)."""
     import torch
     import torch.distributed as dist
 
     import kltamd
     from kltamd.device import EXACT, FAST, PyrDesc, TrackDesc, check, use_torch_stream
-    from kltamd.shard import ShardedSequence
+    from kltamd.shard import BandFrames, ShardedSequence, band_of
 
     lib = kltamd.load()
     lib.KLTSetVerbosity(0)
@@ -366,11 +368,14 @@ def run_sharded(args, world, rank, dev) -> None:
     lib.klt_amd_set_reduction(tc, EXACT if args.reduction == "exact" else FAST)
     ctx = lib.klt_amd_device_context(tc)
     use_torch_stream(lib, ctx, dev)  # library kernels and torch ops ordered on one stream
-    frames = torch.empty((nframes, H, W), dtype=torch.uint8, device=dev)  # the same sequence on every rank
-    check(lib, ctx, lib.klt_hip_synth_frames(ctx, args.seed, 0, nframes, W, H, C.c_void_p(frames.data_ptr()),
-                                             W, W * H), "synth")
+    def load(t0, n, row0, nrows, dst, stride):  # this rank's ingest of rows row0 .. row0+nrows-1
+        check(lib, ctx, lib.klt_hip_synth_rows(ctx, args.seed, t0, n, W, row0, nrows, C.c_void_p(dst), W, stride),
+              "synth")
+
+    frames = BandFrames(nframes, H, W, band_of(H, world, rank, args.margin), load, dev)
     torch.cuda.synchronize()
-    f0 = frames[0].cpu().numpy()
+    f0 = np.empty((H, W), np.uint8)  # frame 0 whole, for the selection every rank makes
+    lib.klt_synth_frame(args.seed, 0, W, H, f0.ctypes.data)
     fl = lib.KLTCreateFeatureList(NF)
     lib.KLTSelectGoodFeatures(tc, f0.ctypes.data_as(C.POINTER(C.c_ubyte)), W, H, fl)
     sel = np.array([[fl.contents.feature[k].contents.x, fl.contents.feature[k].contents.y,
@@ -422,7 +427,8 @@ def run_sharded(args, world, rank, dev) -> None:
         "config": {"workload": f"{W}x{H}, {NF} features, one sequence, features sharded by row band over "
                                f"{world} GPU(s) (BASELINE config 4)",
                    "resolution": f"{W}x{H}", "features": NF, "frames": nframes, "chunk": args.chunk,
-                   "margin_rows": args.margin, "parallelism": f"row-band feature sharding x{world}"},
+                   "margin_rows": args.margin, "parallelism": f"row-band feature sharding x{world}",
+                   "rank_frame_rows": [frames.ra, frames.rb]},
         "live_features": {"after_warmup": live_before, "at_end": int((v >= 0).sum().item())},
         "chunks_redone_full_frame": seq.redone,
         "state_digest": digest,

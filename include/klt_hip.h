@@ -282,6 +282,10 @@ int klt_hip_min_eigen(klt_hip_ctx *ctx, int slot, const klt_hip_select_desc *des
 /* synthetic frames t0..t0+n-1 (include/klt_synth.h) into device memory */
 int klt_hip_synth_frames(klt_hip_ctx *ctx, unsigned long long seed, int t0, int n, int ncols,
                          int nrows, unsigned char *dev, long pitch, long frame_stride);
+/* rows row0 .. row0+nrows-1 of the same frames (one rank's band of a
+   row-sharded sequence): row row0 of frame t0+f lands at dev + f*frame_stride */
+int klt_hip_synth_rows(klt_hip_ctx *ctx, unsigned long long seed, int t0, int n, int ncols, int row0,
+                       int nrows, unsigned char *dev, long pitch, long frame_stride);
 
 /* device memory helpers (for callers without torch) */
 void *klt_hip_malloc(klt_hip_ctx *ctx, size_t bytes);

@@ -155,7 +155,7 @@ hipError_t launch_subsample(hipStream_t st, const float *in, int W, int ss, floa
 // trackability map over the nx x ny grid from (bx, by), step apart
 hipError_t launch_min_eigen(hipStream_t st, const float *gx, const float *gy, int W, int bx, int by, int step, int nx,
                             int ny, int hw, int hh, int *out);
-hipError_t launch_synth(hipStream_t st, unsigned long long seed, int t0, int n, int W, int H, uint8_t *out,
+hipError_t launch_synth(hipStream_t st, unsigned long long seed, int t0, int n, int W, int H, int row0, uint8_t *out,
                         long pitch, long fstride);
 hipError_t launch_selftest_sqrt(const double *in, double *out, int n);
 hipError_t launch_selftest_div(const float *a, const float *b, float *out, int n);

@@ -618,13 +618,14 @@ __global__ __launch_bounds__(kBlock) void k_min_eigen(const float *__restrict__ 
 }
 
 // synthetic frames (include/klt_synth.h), one thread per pixel
-__global__ __launch_bounds__(kBlock) void k_synth(unsigned long long seed, int t0, int W, int H,
+// rows row0 .. row0+H-1 of the frames (row row0 lands in row 0 of `out`)
+__global__ __launch_bounds__(kBlock) void k_synth(unsigned long long seed, int t0, int W, int H, int row0,
                                                   uint8_t *__restrict__ out, long pitch, long fstride) {
   const long i = (long)blockIdx.x * kBlock + threadIdx.x;
   if (i >= (long)W * H) return;
   const int y = (int)(i / W), x = (int)(i - (long)y * W);
   const int t = t0 + blockIdx.y;
-  out[(long)blockIdx.y * fstride + (long)y * pitch + x] = klt_synth_pixel(seed, t, x, y);
+  out[(long)blockIdx.y * fstride + (long)y * pitch + x] = klt_synth_pixel(seed, t, x, row0 + y);
 }
 
 __global__ void k_selftest_sqrt(const double *in, double *out, int n) {
@@ -701,12 +702,12 @@ hipError_t launch_min_eigen(hipStream_t st, const float *gx, const float *gy, in
   return hipGetLastError();
 }
 
-hipError_t launch_synth(hipStream_t st, unsigned long long seed, int t0, int n, int W, int H, uint8_t *out,
+hipError_t launch_synth(hipStream_t st, unsigned long long seed, int t0, int n, int W, int H, int row0, uint8_t *out,
                         long pitch, long fstride) {
   const long np = (long)W * H;
   for (int f0 = 0; f0 < n && np > 0; f0 += 65535) {
     const int cnt = (n - f0) < 65535 ? (n - f0) : 65535;
-    hipLaunchKernelGGL(k_synth, dim3(blocks_for(np), cnt), dim3(kBlock), 0, st, seed, t0 + f0, W, H,
+    hipLaunchKernelGGL(k_synth, dim3(blocks_for(np), cnt), dim3(kBlock), 0, st, seed, t0 + f0, W, H, row0,
                        out + (long)f0 * fstride, pitch, fstride);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -1682,7 +1682,15 @@ KLT_API int klt_hip_synth_frames(klt_hip_ctx *c, unsigned long long seed, int t0
   if (use_device(c)) return -1;
   const long np = (long)ncols * nrows;
   if (np == 0 || n == 0) return 0;
-  return launched(c, "k_synth", launch_synth(c->stream, seed, t0, n, ncols, nrows, dev, pitch, fstride));
+  return launched(c, "k_synth", launch_synth(c->stream, seed, t0, n, ncols, nrows, 0, dev, pitch, fstride));
+}
+
+KLT_API int klt_hip_synth_rows(klt_hip_ctx *c, unsigned long long seed, int t0, int n, int ncols, int row0,
+                               int nrows, unsigned char *dev, long pitch, long fstride) {
+  if (!c || !dev || n < 0 || pitch < ncols || row0 < 0 || nrows < 0) return fail(c, "synth_rows: bad arguments");
+  if (use_device(c)) return -1;
+  if ((long)ncols * nrows == 0 || n == 0) return 0;
+  return launched(c, "k_synth", launch_synth(c->stream, seed, t0, n, ncols, nrows, row0, dev, pitch, fstride));
 }
 
 KLT_API void *klt_hip_malloc(klt_hip_ctx *c, size_t bytes) {

@@ -85,6 +85,8 @@ DEVICE_PROTOS = {
                                             C.c_int, V, V, V, C.c_int, C.c_float, C.c_float, C.c_int, C.c_int, V,
                                             V, C.c_int]),
     "klt_hip_min_eigen": (C.c_int, [V, C.c_int, C.POINTER(SelectDesc), V, IP, IP]),
+    "klt_hip_synth_rows": (C.c_int, [V, C.c_ulonglong, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, V,
+                                     C.c_long, C.c_long]),
     "klt_hip_synth_frames": (C.c_int, [V, C.c_ulonglong, C.c_int, C.c_int, C.c_int, C.c_int, V,
                                        C.c_long, C.c_long]),
     "klt_hip_malloc": (V, [V, C.c_size_t]),

@@ -49,6 +49,62 @@ def band_of(nrows: int, world: int, rank: int, margin: int = DEFAULT_MARGIN) -> 
     return Band(own_lo, own_hi, max(0, lo - margin), min(nrows, hi + margin))
 
 
+def band_rows(nrows: int, band: Band, tile: int = 32, halo: int = 8) -> tuple[int, int]:
+    """The u8 rows [ra, rb) a rank's band build reads: its level-0 build rows
+    rounded out to whole tiles, plus the tiles' halo (k_pyr_l0 reads 5 rows
+    above and 7 below a 32-row tile)."""
+    lo = (band.row_lo // tile) * tile
+    hi = -(-band.row_hi // tile) * tile
+    return max(0, lo - halo), min(nrows, hi + halo)
+
+
+class FullFrames:
+    """Every frame whole in device memory (a uint8 tensor [T, H, W])."""
+
+    def __init__(self, frames: torch.Tensor):
+        self.frames = frames
+        self.T, self.H, self.W = frames.shape
+        self.stride = self.H * self.W  # bytes between band frames
+
+    def band(self, t: int) -> int:
+        """Device address of row 0 of frame t (only the band's rows are read)."""
+        return self.frames.data_ptr() + t * self.stride
+
+    def full(self, t0: int, n: int) -> tuple[int, int]:
+        """Device address of frame t0 and the frame stride, frames t0 .. t0+n-1 whole."""
+        return self.frames.data_ptr() + t0 * self.stride, self.stride
+
+
+class BandFrames:
+    """A rank's frames as SURVEY 8e has them: only the rows its band build
+    reads (band_rows: its band, margin and tile halo), for every frame; whole
+    frames only on demand -- the sequence start and a redone chunk -- into a
+    scratch buffer.  load(t0, n, row0, nrows, dst, stride) writes rows row0 ..
+    row0+nrows-1 of frames t0 .. t0+n-1 to the device address dst (frame
+    stride `stride` bytes, pitch W): the rank's ingest (an H2D copy of its
+    band of host frames, or synthesis)."""
+
+    def __init__(self, T: int, H: int, W: int, band: Band, load, device):
+        self.T, self.H, self.W, self.load = T, H, W, load
+        self.ra, self.rb = band_rows(H, band)
+        self.stride = (self.rb - self.ra) * W
+        self.buf = torch.empty((T, self.rb - self.ra, W), dtype=torch.uint8, device=device)
+        load(0, T, self.ra, self.rb - self.ra, self.buf.data_ptr(), self.stride)
+        self._scratch = None
+
+    def band(self, t: int) -> int:
+        # row y of frame t is at this address + y*W for ra <= y < rb; the band
+        # build reads no other rows
+        return self.buf.data_ptr() + t * self.stride - self.ra * self.W
+
+    def full(self, t0: int, n: int) -> tuple[int, int]:
+        fb = self.H * self.W
+        if self._scratch is None or self._scratch.numel() < n * fb:
+            self._scratch = torch.empty(n * fb, dtype=torch.uint8, device=self.buf.device)
+        self.load(t0, n, 0, self.H, self._scratch.data_ptr(), fb)
+        return self._scratch.data_ptr(), fb
+
+
 def owned_mask(y0: torch.Tensor, v0: torch.Tensor, band: Band) -> torch.Tensor:
     """The features klt_hip_track_frames_band tracks for this band (same tests as k_band_order)."""
     return (v0 >= 0) & (y0 >= band.own_lo) & (y0 < band.own_hi)
@@ -79,9 +135,11 @@ class ShardedSequence:
     """Drives klt_hip_track_frames_band chunk by chunk for one rank.
 
     lib/ctx: the loaded library and a device context; pd/td: descriptors;
-    frames: device u8 frames (uint8 tensor [T, H, W]); x/y/v: device feature
-    arrays (identical on every rank at the start), on the stream the context
-    uses.  all_reduce(tensor) sums a device tensor over the ranks in place
+    frames: device u8 frames -- a uint8 tensor [T, H, W] (every rank holds
+    them whole) or a BandFrames (the rank's rows only; build it with
+    band_of(H, world, rank, margin)); x/y/v: device feature arrays (identical
+    on every rank at the start), on the stream the context uses.
+    all_reduce(tensor) sums a device tensor over the ranks in place
     (torch.distributed.all_reduce in production).
     """
 
@@ -89,29 +147,32 @@ class ShardedSequence:
                  chunk: int = 64, margin: int = DEFAULT_MARGIN):
         from .device import check
         self.lib, self.ctx, self.pd, self.td = lib, ctx, pd, td
-        self.frames, self.x, self.y, self.v = frames, x, y, v
+        self.src = frames if isinstance(frames, (FullFrames, BandFrames)) else FullFrames(frames)
+        self.x, self.y, self.v = x, y, v
         self.rank, self.world, self.all_reduce, self.chunk = rank, world, all_reduce, chunk
-        T, H, W = frames.shape
+        H, W = self.src.H, self.src.W
         self.H, self.W = H, W
         self.band = band_of(H, world, rank, margin)
-        self.escape = torch.zeros(1, dtype=torch.int32, device=frames.device)
+        if isinstance(self.src, BandFrames):
+            ra, rb = band_rows(H, self.band)
+            assert self.src.ra <= ra and self.src.rb >= rb, "BandFrames built for another band"
+        self.escape = torch.zeros(1, dtype=torch.int32, device=x.device)
         self.redone = 0
         self._check = check
 
-    def _ptr(self, t: int) -> C.c_void_p:
-        return C.c_void_p(self.frames.data_ptr() + t * self.H * self.W)
-
     def begin(self, t: int) -> None:
-        self._check(self.lib, self.ctx, self.lib.klt_hip_frames_begin(self.ctx, C.byref(self.pd), self._ptr(t),
+        ptr, _ = self.src.full(t, 1)
+        self._check(self.lib, self.ctx, self.lib.klt_hip_frames_begin(self.ctx, C.byref(self.pd), C.c_void_p(ptr),
                                                                       self.W), "frames_begin")
 
-    def _band_call(self, t0: int, n: int, row_lo: int, row_hi: int, next_t0: int = 0, next_n: int = 0) -> None:
+    def _band_call(self, ptr: int, stride: int, n: int, row_lo: int, row_hi: int, next_ptr: int = 0,
+                   next_n: int = 0) -> None:
         b = self.band
         self._check(self.lib, self.ctx, self.lib.klt_hip_track_frames_band(
-            self.ctx, C.byref(self.pd), C.byref(self.td), self._ptr(t0), self.W, self.H * self.W, n,
+            self.ctx, C.byref(self.pd), C.byref(self.td), C.c_void_p(ptr), self.W, stride, n,
             C.c_void_p(self.x.data_ptr()), C.c_void_p(self.y.data_ptr()), C.c_void_p(self.v.data_ptr()),
             self.x.numel(), b.own_lo, b.own_hi, row_lo, row_hi, C.c_void_p(self.escape.data_ptr()),
-            self._ptr(next_t0) if next_n > 0 else None, next_n), "track_frames_band")
+            C.c_void_p(next_ptr) if next_n > 0 else None, next_n), "track_frames_band")
 
     def run(self, t0: int, nframes: int) -> None:
         """Track frames t0 .. t0+nframes-1 (the pyramid of t0-1 must be current:
@@ -122,7 +183,9 @@ class ShardedSequence:
             nn = min(self.chunk, end - c0 - n)  # the next chunk, built ahead
             xs, ys, vs = self.x.clone(), self.y.clone(), self.v.clone()
             self.escape.zero_()
-            self._band_call(c0, n, self.band.row_lo, self.band.row_hi, c0 + n, nn)
+            src = self.src
+            self._band_call(src.band(c0), src.stride, n, self.band.row_lo, self.band.row_hi,
+                            src.band(c0 + n) if nn > 0 else 0, nn)
             # one collective: the owners' results and the escape flag summed over ranks
             flag = merge_chunk(self.x, self.y, self.v, ys, vs, self.band, self.rank, self.all_reduce,
                                escape=self.escape)
@@ -131,7 +194,9 @@ class ShardedSequence:
                 # full-frame pyramids (exact whatever the motion), merge again
                 self.redone += 1
                 self.x.copy_(xs), self.y.copy_(ys), self.v.copy_(vs)
-                self.begin(c0 - 1)
+                ptr, fb = self.src.full(c0 - 1, n + 1)  # whole frames c0-1 .. c0+n-1
+                self._check(self.lib, self.ctx, self.lib.klt_hip_frames_begin(
+                    self.ctx, C.byref(self.pd), C.c_void_p(ptr), self.W), "frames_begin")
                 self.escape.zero_()
-                self._band_call(c0, n, 0, self.H, c0 + n, nn)
+                self._band_call(ptr + fb, fb, n, 0, self.H)
                 merge_chunk(self.x, self.y, self.v, ys, vs, self.band, self.rank, self.all_reduce)

@@ -128,32 +128,61 @@ class _Rank:
         gpu.klt_amd_track_desc(self.tc, C.byref(self.td))
         self.band = band_of(H, world, rank, margin)
         self.rank = rank
+        self.src = None
+
+    def band_only(self):
+        """Hold only the band's rows of every frame (kltamd.shard.BandFrames), copied from the full frames."""
+        from kltamd.shard import BandFrames
+        dfr, W = self.dfr, self.W
+
+        def load(t0, n, row0, nrows, dst, stride):
+            from kltamd.device import D2D, check
+            part = dfr[t0:t0 + n, row0:row0 + nrows].contiguous()  # [n, nrows, W]
+            for f in range(n):
+                check(self.gpu, self.ctx, self.gpu.klt_hip_memcpy(
+                    self.ctx, C.c_void_p(dst + f * stride), C.c_void_p(part[f].data_ptr()), nrows * W, D2D), "d2d")
+            self.gpu.klt_hip_sync(self.ctx)
+
+        self.src = BandFrames(dfr.shape[0], self.H, W, self.band, load, dfr.device)
 
     def ptr(self, t):
+        if self.src is not None:
+            return C.c_void_p(self.src.band(t))
         return C.c_void_p(self.dfr.data_ptr() + t * self.H * self.W)
 
     def begin(self, t):
-        assert self.gpu.klt_hip_frames_begin(self.ctx, C.byref(self.pd), self.ptr(t), self.W) == 0
+        ptr = self.src.full(t, 1)[0] if self.src is not None else self.dfr.data_ptr() + t * self.H * self.W
+        assert self.gpu.klt_hip_frames_begin(self.ctx, C.byref(self.pd), C.c_void_p(ptr), self.W) == 0
 
     def chunk(self, t0, n, x, y, v, esc, full=False, next_n=0):
         """next_n > 0: frames t0+n .. are the next chunk, built ahead (klt_hip_track_frames_band's next_frames)"""
         b = self.band
+        if full and self.src is not None:  # a redone chunk: whole frames from the source's scratch
+            ptr, stride = self.src.full(t0, n)
+            first, nxt, next_n = C.c_void_p(ptr), None, 0
+        else:
+            stride = self.src.stride if self.src is not None else self.H * self.W
+            first, nxt = self.ptr(t0), (self.ptr(t0 + n) if next_n > 0 else None)
         rc = self.gpu.klt_hip_track_frames_band(
-            self.ctx, C.byref(self.pd), C.byref(self.td), self.ptr(t0), self.W, self.H * self.W, n,
+            self.ctx, C.byref(self.pd), C.byref(self.td), first, self.W, stride, n,
             C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()), x.numel(),
             b.own_lo, b.own_hi, 0 if full else b.row_lo, self.H if full else b.row_hi, C.c_void_p(esc.data_ptr()),
-            self.ptr(t0 + n) if next_n > 0 else None, next_n)
+            nxt, next_n)
         assert rc == 0, self.gpu.klt_hip_last_error(self.ctx)
 
 
-def sharded_sequence(gpu, frames, nfeat, world, chunk, margin, ahead=True):
+def sharded_sequence(gpu, frames, nfeat, world, chunk, margin, ahead=True, band_only=False):
     """Frames[0] selects; frames[1:] are tracked by `world` simulated ranks
-    (ahead: each call builds the next chunk's band pyramids ahead)."""
+    (ahead: each call builds the next chunk's band pyramids ahead; band_only:
+    each rank holds only its band's rows, whole frames only to redo a chunk)."""
     H, W = frames[0].shape
     dev = torch.device("cuda", 0)
     dfr = torch.from_numpy(np.ascontiguousarray(np.stack(frames))).to(dev)
     x0, y0, v0 = (torch.from_numpy(a).to(dev) for a in _select(gpu, frames[0], nfeat))
     ranks = [_Rank(gpu, dfr, H, W, world, r, margin) for r in range(world)]
+    if band_only:
+        for rk in ranks:
+            rk.band_only()
     for rk in ranks:
         rk.begin(0)
     x, y, v = x0.clone(), y0.clone(), v0.clone()
@@ -196,12 +225,14 @@ def sharded_sequence(gpu, frames, nfeat, world, chunk, margin, ahead=True):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,chunk,margin,ahead", [(2, 4, 128, True), (3, 5, 64, True), (4, 3, 40, True),
-                                                      (2, 4, 0, True), (3, 4, 64, False), (4, 3, 0, False)])
-def test_sharded_equals_single_gpu(gpu, oracle, world, chunk, margin, ahead):
+@pytest.mark.parametrize("world,chunk,margin,ahead,band_only",
+                         [(2, 4, 128, True, False), (3, 5, 64, True, False), (4, 3, 40, True, False),
+                          (2, 4, 0, True, False), (3, 4, 64, False, False), (4, 3, 0, False, False),
+                          (3, 5, 64, True, True), (4, 3, 0, True, True)])
+def test_sharded_equals_single_gpu(gpu, oracle, world, chunk, margin, ahead, band_only):
     from kltabi import OracleTracker
     frames = synth(gpu, 2160 + world, 640, 480, 11)
-    x, y, v, redone = sharded_sequence(gpu, frames, 1500, world, chunk, margin, ahead)
+    x, y, v, redone = sharded_sequence(gpu, frames, 1500, world, chunk, margin, ahead, band_only)
     X, Y, V = OracleTracker(oracle).harness(frames, 1500, 11, first=frames[0])
     k = 11 - 2
     assert np.array_equal(v, V[:, k])
