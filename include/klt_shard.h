@@ -1,0 +1,78 @@
+/*
+ * klt_shard.h -- feature-sharded tracking of ONE sequence over N GPUs
+ * (BASELINE config 4) for C callers: one process (or thread) per GPU, the
+ * exchange over RCCL (xGMI).  Extension of the klt.h drop-in; the reference
+ * has no multi-GPU path (its V3 harness, example3.c:54-76, tracks one
+ * sequence on one device).
+ *
+ * Rank r of N owns the features whose y lies in its row band
+ * [r*H/N, (r+1)*H/N) at the start of a chunk, builds band-limited pyramids
+ * (its band +/- margin rows; klt_hip_track_frames_band) and tracks them;
+ * after each chunk one RCCL all-reduce of the int32 bit patterns of
+ * (x, y, val) -- every feature has exactly one contributor: its owner, rank 0
+ * for lost features -- leaves every rank with the same list, bit-identical
+ * to one GPU's.  A window that needs rows a rank did not build raises an
+ * escape flag that rides in the same all-reduce; every rank then redoes the
+ * chunk from whole frames (obtained through the caller's callback).
+ *
+ * Usage, per rank:
+ *   rank 0: klt_shard_unique_id(id); distribute id (MPI, a file, a socket);
+ *   s = klt_shard_create(ctx, rank, N, id, nrows, margin);
+ *   klt_shard_rows(s, &lo, &hi): upload only rows [lo, hi) of each frame;
+ *   klt_hip_frames_begin(ctx, pdesc, whole first frame, pitch);
+ *   for each chunk: klt_shard_track(...);   (x/y/val: device arrays, same on every rank)
+ *   klt_shard_destroy(s);
+ */
+#ifndef KLT_SHARD_H
+#define KLT_SHARD_H
+
+#include "klt_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KLT_SHARD_ID_BYTES 128
+
+typedef struct klt_shard klt_shard;
+
+/* whole frames t0-1 .. t0+n-1 of the chunk being redone (t0: its first
+   frame): *frames = device address of frame t0-1, *stride = bytes between
+   frames (row pitch as in klt_shard_track).  Returns 0, or < 0 to fail. */
+typedef int (*klt_shard_frames_fn)(void *user, const unsigned char **frames, long *stride);
+
+/* a new communicator id (ncclGetUniqueId); 0 on success */
+int klt_shard_unique_id(unsigned char id[KLT_SHARD_ID_BYTES]);
+/* rank `rank` of `world` on the device of `ctx` (ncclCommInitRank; every
+   rank must call it); nrows: the frame height, margin: level-0 rows built
+   beyond the band (64 suits the synthetic sequences; any value is exact) */
+klt_shard *klt_shard_create(klt_hip_ctx *ctx, int rank, int world, const unsigned char id[KLT_SHARD_ID_BYTES],
+                            int nrows, int margin);
+/* single-process rehearsal (tests): the band of rank/world, but the exchange
+   runs over a communicator of this rank alone, so klt_shard_track leaves only
+   this rank's contribution (its owned features, rank 0 also the lost ones;
+   0 elsewhere) and redoes a chunk only when this rank escaped.  The caller
+   sums the ranks' int32 bit patterns to get the merged list. */
+klt_shard *klt_shard_create_local(klt_hip_ctx *ctx, int rank, int world, int nrows, int margin);
+void klt_shard_destroy(klt_shard *s);
+const char *klt_shard_last_error(klt_shard *s);
+/* rows [*lo, *hi) of every frame this rank's band build reads: the only rows
+   klt_shard_track's frames must hold (its band, margin and tile halo) */
+int klt_shard_rows(const klt_shard *s, int *lo, int *hi);
+/* one chunk: frames + f*stride holds frame f of the chunk, addressed as whole
+   frames (row y at + y*pitch; only rows [lo, hi) are read); next_frames
+   (optional, next_nframes frames, same pitch/stride): the next chunk, whose
+   band pyramids are built while this one is exchanged.  x/y/val: n device
+   features, updated in place to the merged list.  full: whole frames for a
+   redone chunk (required when the chunk escapes).  Returns 0, 1 when the
+   chunk was redone from whole frames, < 0 on error. */
+int klt_shard_track(klt_shard *s, const klt_hip_pyr_desc *pdesc, const klt_hip_track_desc *tdesc,
+                    const unsigned char *frames, long pitch, long stride, int nframes,
+                    const unsigned char *next_frames, int next_nframes, float *x, float *y, int *val, int n,
+                    klt_shard_frames_fn full, void *user);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,241 @@
+// shard.hip -- feature-sharded tracking over N GPUs for C callers
+// (include/klt_shard.h): the row-band decomposition of BASELINE config 4 on
+// top of klt_hip_track_frames_band, with the per-chunk exchange as one RCCL
+// all-reduce on the context's stream.  kltamd/shard.py is the same schedule
+// for torch.distributed callers; both merge bit for bit.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+
+#include "klt_dev.h"
+#include "klt_shard.h"
+
+#define KLT_API extern "C" __attribute__((visibility("default")))
+
+struct klt_shard {
+  klt_hip_ctx *ctx = nullptr;
+  int rank = 0, world = 1, nrows = 0;
+  float own_lo = 0.0f, own_hi = 0.0f;   // features owned: own_lo <= y < own_hi at the chunk start
+  int row_lo = 0, row_hi = 0;           // level-0 rows built
+  int load_lo = 0, load_hi = 0;         // u8 rows the band build reads
+  ncclComm_t comm = nullptr;
+  int *d_buf = nullptr;                 // 3n+1 int32: x | y | val bit patterns, escape flag
+  float *d_x0 = nullptr, *d_y0 = nullptr;
+  int *d_v0 = nullptr;                  // chunk-start state (ownership, redo)
+  size_t cap = 0;
+  int *h_flag = nullptr;                // pinned: the summed escape flag
+  std::string err;
+};
+
+namespace {
+
+int sfail(klt_shard *s, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (s) s->err = buf;
+  return -1;
+}
+
+#define SHIP(s, call)                                                                     \
+  do {                                                                                    \
+    hipError_t e_ = (call);                                                               \
+    if (e_ != hipSuccess) return sfail(s, "%s: %s", #call, hipGetErrorString(e_));        \
+  } while (0)
+#define SNCCL(s, call)                                                                    \
+  do {                                                                                    \
+    ncclResult_t r_ = (call);                                                             \
+    if (r_ != ncclSuccess) return sfail(s, "%s: %s", #call, ncclGetErrorString(r_));      \
+  } while (0)
+
+// the owners' bit patterns, zero elsewhere (rank 0 also contributes the lost
+// features, which nobody tracks); the escape flag as the last element
+__global__ void k_shard_pack(const float *__restrict__ x, const float *__restrict__ y, const int *__restrict__ v,
+                             const float *__restrict__ y0, const int *__restrict__ v0, float own_lo, float own_hi,
+                             int rank0, const int *__restrict__ escape, int *__restrict__ buf, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const bool owned = v0[i] >= 0 && y0[i] >= own_lo && y0[i] < own_hi;  // k_band_order's test
+    const bool keep = owned || (rank0 && v0[i] < 0);
+    buf[i] = keep ? __float_as_int(x[i]) : 0;
+    buf[n + i] = keep ? __float_as_int(y[i]) : 0;
+    buf[2 * n + i] = keep ? v[i] : 0;
+  }
+  if (i == 0) buf[3 * n] = escape ? *escape : 0;
+}
+
+__global__ void k_shard_unpack(const int *__restrict__ buf, float *__restrict__ x, float *__restrict__ y,
+                               int *__restrict__ v, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  x[i] = __int_as_float(buf[i]);
+  y[i] = __int_as_float(buf[n + i]);
+  v[i] = buf[2 * n + i];
+}
+
+int grow_buffers(klt_shard *s, int n) {
+  if ((size_t)n <= s->cap && s->d_buf) return 0;
+  hipFree(s->d_buf);
+  hipFree(s->d_x0);
+  hipFree(s->d_y0);
+  hipFree(s->d_v0);
+  s->d_buf = nullptr;
+  s->d_x0 = s->d_y0 = nullptr;
+  s->d_v0 = nullptr;
+  s->cap = 0;
+  const size_t m = n > 0 ? (size_t)n : 1;
+  SHIP(s, hipMalloc((void **)&s->d_buf, (3 * m + 1) * sizeof(int)));
+  SHIP(s, hipMalloc((void **)&s->d_x0, m * sizeof(float)));
+  SHIP(s, hipMalloc((void **)&s->d_y0, m * sizeof(float)));
+  SHIP(s, hipMalloc((void **)&s->d_v0, m * sizeof(int)));
+  s->cap = m;
+  return 0;
+}
+
+// pack this rank's results, all-reduce them with every rank's, unpack; the
+// summed escape flag lands in *s->h_flag (synchronous)
+int exchange(klt_shard *s, hipStream_t st, float *x, float *y, int *v, int n, const int *escape) {
+  const int nb = (n + 255) / 256 > 0 ? (n + 255) / 256 : 1;
+  hipLaunchKernelGGL(k_shard_pack, dim3(nb), dim3(256), 0, st, x, y, v, s->d_y0, s->d_v0, s->own_lo, s->own_hi,
+                     s->rank == 0 ? 1 : 0, escape, s->d_buf, n);
+  SHIP(s, hipGetLastError());
+  SNCCL(s, ncclAllReduce(s->d_buf, s->d_buf, (size_t)3 * n + 1, ncclInt32, ncclSum, s->comm, st));
+  if (n > 0) {
+    hipLaunchKernelGGL(k_shard_unpack, dim3(nb), dim3(256), 0, st, s->d_buf, x, y, v, n);
+    SHIP(s, hipGetLastError());
+  }
+  SHIP(s, hipMemcpyAsync(s->h_flag, s->d_buf + (size_t)3 * n, sizeof(int), hipMemcpyDeviceToHost, st));
+  SHIP(s, hipStreamSynchronize(st));
+  return 0;
+}
+
+}  // namespace
+
+KLT_API int klt_shard_unique_id(unsigned char id[KLT_SHARD_ID_BYTES]) {
+  if (!id) return -1;
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return -1;
+  static_assert(sizeof u == KLT_SHARD_ID_BYTES, "id size");
+  memcpy(id, &u, sizeof u);
+  return 0;
+}
+
+namespace {
+
+// rank/world's band (kltamd/shard.py band_of and band_rows) and a
+// communicator of `cranks` ranks in which this one is `crank`
+klt_shard *make_shard(klt_hip_ctx *ctx, int rank, int world, const unsigned char *id, int cranks, int crank,
+                      int nrows, int margin) {
+  if (!ctx || !id || world < 1 || rank < 0 || rank >= world || nrows < 1 || margin < 0) return nullptr;
+  klt_shard *s = new klt_shard();
+  s->ctx = ctx;
+  s->rank = rank;
+  s->world = world;
+  s->nrows = nrows;
+  const int lo = (int)((long)rank * nrows / world), hi = (int)((long)(rank + 1) * nrows / world);
+  s->own_lo = rank == 0 ? -INFINITY : (float)lo;
+  s->own_hi = rank == world - 1 ? INFINITY : (float)hi;
+  s->row_lo = lo - margin > 0 ? lo - margin : 0;
+  s->row_hi = hi + margin < nrows ? hi + margin : nrows;
+  const int TH = kltdev::geom::L0_TH, halo = 8;
+  const int t_lo = (s->row_lo / TH) * TH, t_hi = ((s->row_hi + TH - 1) / TH) * TH;
+  s->load_lo = t_lo - halo > 0 ? t_lo - halo : 0;
+  s->load_hi = t_hi + halo < nrows ? t_hi + halo : nrows;
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof u);
+  if (hipSetDevice(klt_hip_ctx_device(ctx)) != hipSuccess || ncclCommInitRank(&s->comm, cranks, u, crank) != ncclSuccess ||
+      hipHostMalloc((void **)&s->h_flag, sizeof(int), hipHostMallocDefault) != hipSuccess) {
+    if (s->comm) ncclCommDestroy(s->comm);
+    delete s;
+    return nullptr;
+  }
+  return s;
+}
+
+}  // namespace
+
+KLT_API klt_shard *klt_shard_create(klt_hip_ctx *ctx, int rank, int world, const unsigned char id[KLT_SHARD_ID_BYTES],
+                                    int nrows, int margin) {
+  return make_shard(ctx, rank, world, id, world, rank, nrows, margin);
+}
+
+KLT_API klt_shard *klt_shard_create_local(klt_hip_ctx *ctx, int rank, int world, int nrows, int margin) {
+  unsigned char id[KLT_SHARD_ID_BYTES];
+  if (klt_shard_unique_id(id)) return nullptr;
+  return make_shard(ctx, rank, world, id, 1, 0, nrows, margin);  // a communicator of this rank alone
+}
+
+KLT_API void klt_shard_destroy(klt_shard *s) {
+  if (!s) return;
+  if (s->ctx) klt_hip_sync(s->ctx);
+  if (s->comm) ncclCommDestroy(s->comm);
+  hipFree(s->d_buf);
+  hipFree(s->d_x0);
+  hipFree(s->d_y0);
+  hipFree(s->d_v0);
+  if (s->h_flag) hipHostFree(s->h_flag);
+  delete s;
+}
+
+KLT_API const char *klt_shard_last_error(klt_shard *s) { return s ? s->err.c_str() : "null shard"; }
+
+KLT_API int klt_shard_rows(const klt_shard *s, int *lo, int *hi) {
+  if (!s || !lo || !hi) return -1;
+  *lo = s->load_lo;
+  *hi = s->load_hi;
+  return 0;
+}
+
+KLT_API int klt_shard_track(klt_shard *s, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
+                            const unsigned char *frames, long pitch, long stride, int nframes,
+                            const unsigned char *next_frames, int next_nframes, float *x, float *y, int *val, int n,
+                            klt_shard_frames_fn full, void *user) {
+  if (!s || !pd || !td) return sfail(s, "shard_track: null argument");
+  if (pd->nrows != s->nrows) return sfail(s, "shard_track: frames have %d rows, the shard %d", pd->nrows, s->nrows);
+  if (n < 0 || nframes < 1 || !frames || (n > 0 && (!x || !y || !val)))
+    return sfail(s, "shard_track: bad frames or feature arrays");
+  if (hipSetDevice(klt_hip_ctx_device(s->ctx)) != hipSuccess) return sfail(s, "shard_track: device");
+  hipStream_t st = (hipStream_t)klt_hip_get_stream(s->ctx);
+  if (grow_buffers(s, n)) return -1;
+  // the chunk-start state: ownership (y0, v0) and the redo's starting point
+  const size_t fb = sizeof(float) * (size_t)n;
+  if (n > 0) {
+    SHIP(s, hipMemcpyAsync(s->d_x0, x, fb, hipMemcpyDeviceToDevice, st));
+    SHIP(s, hipMemcpyAsync(s->d_y0, y, fb, hipMemcpyDeviceToDevice, st));
+    SHIP(s, hipMemcpyAsync(s->d_v0, val, fb, hipMemcpyDeviceToDevice, st));
+  }
+  int *escape = s->d_buf + (size_t)3 * s->cap;  // the buffer's last slot doubles as the device flag
+  SHIP(s, hipMemsetAsync(escape, 0, sizeof(int), st));
+  if (klt_hip_track_frames_band(s->ctx, pd, td, frames, pitch, stride, nframes, x, y, val, n, s->own_lo, s->own_hi,
+                                s->row_lo, s->row_hi, escape, next_frames, next_nframes))
+    return sfail(s, "shard_track: %s", klt_hip_last_error(s->ctx));
+  if (exchange(s, st, x, y, val, n, escape)) return -1;
+  if (*s->h_flag == 0) return 0;
+  // some rank's window left its built rows: every rank redoes the chunk from
+  // whole frames (exact whatever the motion) and exchanges again
+  if (!full) return sfail(s, "shard_track: chunk escaped its band and no whole-frame callback was given");
+  const unsigned char *whole = nullptr;
+  long wstride = 0;
+  if (full(user, &whole, &wstride) || !whole) return sfail(s, "shard_track: whole-frame callback failed");
+  if (n > 0) {
+    SHIP(s, hipMemcpyAsync(x, s->d_x0, fb, hipMemcpyDeviceToDevice, st));
+    SHIP(s, hipMemcpyAsync(y, s->d_y0, fb, hipMemcpyDeviceToDevice, st));
+    SHIP(s, hipMemcpyAsync(val, s->d_v0, fb, hipMemcpyDeviceToDevice, st));
+  }
+  if (klt_hip_frames_begin(s->ctx, pd, whole, pitch))
+    return sfail(s, "shard_track: redo: %s", klt_hip_last_error(s->ctx));
+  SHIP(s, hipMemsetAsync(escape, 0, sizeof(int), st));
+  if (klt_hip_track_frames_band(s->ctx, pd, td, whole + wstride, pitch, wstride, nframes, x, y, val, n, s->own_lo,
+                                s->own_hi, 0, s->nrows, escape, nullptr, 0))
+    return sfail(s, "shard_track: redo: %s", klt_hip_last_error(s->ctx));
+  if (exchange(s, st, x, y, val, n, nullptr)) return -1;
+  return 1;
+}

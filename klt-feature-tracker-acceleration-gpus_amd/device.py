@@ -84,6 +84,14 @@ DEVICE_PROTOS = {
     "klt_hip_track_frames_band": (C.c_int, [V, C.POINTER(PyrDesc), C.POINTER(TrackDesc), V, C.c_long, C.c_long,
                                             C.c_int, V, V, V, C.c_int, C.c_float, C.c_float, C.c_int, C.c_int, V,
                                             V, C.c_int]),
+    "klt_shard_unique_id": (C.c_int, [V]),
+    "klt_shard_create": (V, [V, C.c_int, C.c_int, V, C.c_int, C.c_int]),
+    "klt_shard_create_local": (V, [V, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "klt_shard_destroy": (None, [V]),
+    "klt_shard_last_error": (C.c_char_p, [V]),
+    "klt_shard_rows": (C.c_int, [V, IP, IP]),
+    "klt_shard_track": (C.c_int, [V, C.POINTER(PyrDesc), C.POINTER(TrackDesc), V, C.c_long, C.c_long, C.c_int, V,
+                                  C.c_int, V, V, V, C.c_int, V, V]),
     "klt_hip_min_eigen": (C.c_int, [V, C.c_int, C.POINTER(SelectDesc), V, IP, IP]),
     "klt_hip_synth_rows": (C.c_int, [V, C.c_ulonglong, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, V,
                                      C.c_long, C.c_long]),

@@ -260,3 +260,91 @@ def test_sharded_4k_20k_equals_reference(gpu, world):
     for a, dt in ((x, "<f4"), (y, "<f4"), (v, "<i4")):
         h.update(np.ascontiguousarray(a, dt).tobytes())
     assert h.hexdigest() == cfg["columns"][T - 1], f"world {world}: sharded list differs (redone {redone})"
+
+
+# ---------------------------------------------------------------------------
+# GPU: the C-ABI driver (include/klt_shard.h) -- ranks rehearsed in one process
+# ---------------------------------------------------------------------------
+_FRAMES_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_long))
+
+
+def c_sharded_sequence(gpu, frames, nfeat, world, chunk, margin, band_only=False, real_comm=False):
+    """klt_shard_track per chunk for every rank (klt_shard_create_local: the
+    rank's band, a communicator of its own), then the all-reduce done by hand:
+    the sum of the ranks' int32 contributions.  real_comm (world 1): the
+    RCCL path proper, klt_shard_unique_id + klt_shard_create."""
+    H, W = frames[0].shape
+    dev = torch.device("cuda", 0)
+    dfr = torch.from_numpy(np.ascontiguousarray(np.stack(frames))).to(dev)
+    x, y, v = (torch.from_numpy(a).to(dev) for a in _select(gpu, frames[0], nfeat))
+    ranks, shards, keep = [], [], []
+    for r in range(world):
+        rk = _Rank(gpu, dfr, H, W, world, r, margin)
+        if real_comm:
+            assert world == 1
+            uid = (C.c_ubyte * 128)()
+            assert gpu.klt_shard_unique_id(uid) == 0
+            s = gpu.klt_shard_create(rk.ctx, 0, 1, uid, H, margin)
+        else:
+            s = gpu.klt_shard_create_local(rk.ctx, r, world, H, margin)
+        assert s
+        lo, hi = C.c_int(), C.c_int()
+        assert gpu.klt_shard_rows(s, C.byref(lo), C.byref(hi)) == 0
+        b = band_of(H, world, r, margin)
+        assert lo.value <= b.row_lo and hi.value >= b.row_hi
+        if band_only:  # only rows [lo, hi) of each frame on this rank, addressed as whole frames
+            part = dfr[:, lo.value:hi.value].contiguous()
+            base, stride = part.data_ptr() - lo.value * W, (hi.value - lo.value) * W
+            keep.append(part)
+        else:
+            base, stride = dfr.data_ptr(), H * W
+        rk.base, rk.stride = base, stride
+        assert gpu.klt_hip_frames_begin(rk.ctx, C.byref(rk.pd), C.c_void_p(dfr.data_ptr()), W) == 0
+        ranks.append(rk)
+        shards.append(s)
+    redone, cur = [0], [0]
+
+    def whole(user, frames_out, stride_out):  # frames t0-1 .. of the chunk being redone
+        frames_out[0] = dfr.data_ptr() + (cur[0] - 1) * H * W
+        stride_out[0] = H * W
+        redone[0] += 1
+        return 0
+    cb = _FRAMES_FN(whole)
+    T = len(frames) - 1
+    for c0 in range(1, 1 + T, chunk):
+        n = min(chunk, 1 + T - c0)
+        nn = min(chunk, 1 + T - c0 - n)
+        cur[0] = c0
+        acc = None
+        for rk, s in zip(ranks, shards):
+            xr, yr, vr = x.clone(), y.clone(), v.clone()
+            nxt = C.c_void_p(rk.base + (c0 + n) * rk.stride) if nn else None
+            rc = gpu.klt_shard_track(s, C.byref(rk.pd), C.byref(rk.td), C.c_void_p(rk.base + c0 * rk.stride), W,
+                                     rk.stride, n, nxt, nn, C.c_void_p(xr.data_ptr()), C.c_void_p(yr.data_ptr()),
+                                     C.c_void_p(vr.data_ptr()), x.numel(), cb, None)
+            assert rc in (0, 1), gpu.klt_shard_last_error(s)
+            part = torch.stack([xr.view(torch.int32), yr.view(torch.int32), vr])
+            acc = part if acc is None else acc + part
+        x.view(torch.int32).copy_(acc[0]), y.view(torch.int32).copy_(acc[1]), v.copy_(acc[2])
+    for rk, s in zip(ranks, shards):
+        gpu.klt_shard_destroy(s)
+        gpu.KLTFreeTrackingContext(rk.tc)
+    del keep
+    return x.cpu().numpy(), y.cpu().numpy(), v.cpu().numpy(), redone[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,chunk,margin,band_only,real_comm",
+                         [(1, 4, 64, False, True), (3, 5, 64, False, False), (4, 3, 0, True, False),
+                          (2, 4, 64, True, False)])
+def test_c_shard_equals_single_gpu(gpu, oracle, world, chunk, margin, band_only, real_comm):
+    from kltabi import OracleTracker
+    frames = synth(gpu, 2160 + world, 640, 480, 11)
+    x, y, v, redone = c_sharded_sequence(gpu, frames, 1500, world, chunk, margin, band_only, real_comm)
+    X, Y, V = OracleTracker(oracle).harness(frames, 1500, 11, first=frames[0])
+    k = 11 - 2
+    assert np.array_equal(v, V[:, k])
+    assert np.array_equal(x.view(np.int32), X[:, k].view(np.int32))
+    assert np.array_equal(y.view(np.int32), Y[:, k].view(np.int32))
+    if margin == 0:
+        assert redone > 0  # no margin: band-edge features escape; the callback supplies whole frames
