@@ -279,6 +279,15 @@ int klt_hip_track_frames_band(klt_hip_ctx *ctx, const klt_hip_pyr_desc *pdesc,
 int klt_hip_min_eigen(klt_hip_ctx *ctx, int slot, const klt_hip_select_desc *desc, int *vals,
                       int *nx, int *ny);
 
+/* the trackability map rows of the last tracked frame (the previous pyramid,
+   as sequential-mode replacement reads it: selectGoodFeatures.c:342-348)
+   whose pixel row lies in [row_lo, row_hi): grid rows [*r0, *r1) of the
+   nx*ny map, written into dev_map (device, the whole map's layout; other rows
+   untouched; NULL: only the sizes).  Returns 1 without writing when those
+   rows' windows reach rows a band-built pyramid does not hold. */
+int klt_hip_min_eigen_rows(klt_hip_ctx *ctx, const klt_hip_select_desc *desc, int row_lo, int row_hi, int *dev_map,
+                           int *nx, int *ny, int *r0, int *r1);
+
 /* synthetic frames t0..t0+n-1 (include/klt_synth.h) into device memory */
 int klt_hip_synth_frames(klt_hip_ctx *ctx, unsigned long long seed, int t0, int n, int ncols,
                          int nrows, unsigned char *dev, long pitch, long frame_stride);

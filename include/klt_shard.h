@@ -71,6 +71,29 @@ int klt_shard_track(klt_shard *s, const klt_hip_pyr_desc *pdesc, const klt_hip_t
                     const unsigned char *next_frames, int next_nframes, float *x, float *y, int *val, int n,
                     klt_shard_frames_fn full, void *user);
 
+/* KLTReplaceLostFeatures across the ranks (selectGoodFeatures.c:514-541 in
+   sequential mode, which reads the last tracked frame's pyramid, :342-348),
+   between two klt_shard_track calls.  Each rank computes the trackability map
+   rows of its own band from its band pyramid, the rows are broadcast to every
+   rank (RCCL, one broadcast per owner), and every rank runs the same host
+   selection over the whole map: x/y/val (device, the merged list) come back
+   identical on every rank and equal to one GPU's.  When the selection window
+   reaches rows the band pyramid lacks, `full` is asked for the last frame
+   whole (*frames = its device address).  pitch: that frame's row pitch.
+   tc-equivalent parameters: sd (window, borders, nSkippedPixels), mindist,
+   min_eigenvalue.  Returns 0, < 0 on error. */
+int klt_shard_replace(klt_shard *s, const klt_hip_pyr_desc *pdesc, const klt_hip_select_desc *sd, long pitch,
+                      int mindist, int min_eigenvalue, float *x, float *y, int *val, int n,
+                      klt_shard_frames_fn full, void *user);
+/* its two halves, for callers with their own collective (and the local
+   rehearsal): this rank's map rows into dev_map (the whole map's layout,
+   klt_hip_min_eigen_rows; 1 when the whole frame was needed) ... */
+int klt_shard_eigen(klt_shard *s, const klt_hip_pyr_desc *pdesc, const klt_hip_select_desc *sd, long pitch,
+                    int *dev_map, klt_shard_frames_fn full, void *user);
+/* ... and the host selection over a complete map (synchronous) */
+int klt_shard_select(klt_shard *s, const klt_hip_pyr_desc *pdesc, const klt_hip_select_desc *sd, int mindist,
+                     int min_eigenvalue, const int *dev_map, float *x, float *y, int *val, int n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1676,6 +1676,36 @@ KLT_API int klt_hip_min_eigen(klt_hip_ctx *c, int s, const klt_hip_select_desc *
   return 0;
 }
 
+KLT_API int klt_hip_min_eigen_rows(klt_hip_ctx *c, const klt_hip_select_desc *d, int row_lo, int row_hi,
+                                   int *dev_map, int *nx, int *ny, int *r0, int *r1) {
+  if (!c || !d || !nx || !ny || !r0 || !r1) return fail(c, "min_eigen_rows: null argument");
+  if (!c->frames_ready) return fail(c, "min_eigen_rows: no tracked frame (call klt_hip_frames_begin)");
+  const TrkLevel L = prev_level(c, 0);
+  const int hw = d->window_width / 2, hh = d->window_height / 2;
+  const int step = d->nSkippedPixels + 1;
+  if (step < 1) return fail(c, "min_eigen_rows: bad nSkippedPixels");
+  const int bx = d->borderx, by = d->bordery;
+  if (bx < hw || by < hh) return fail(c, "min_eigen_rows: border smaller than window half size");
+  const int cx = L.w - 2 * bx, cy = L.h - 2 * by;
+  const int gx = cx > 0 ? (cx + step - 1) / step : 0;
+  const int gy = cy > 0 ? (cy + step - 1) / step : 0;
+  // grid rows j with by + j*step in [row_lo, row_hi)
+  auto first_at = [&](int y) { return clampi(y <= by ? 0 : (y - by + step - 1) / step, 0, gy); };
+  const int j0 = first_at(row_lo), j1 = first_at(row_hi) > j0 ? first_at(row_hi) : j0;
+  *nx = gx;
+  *ny = gy;
+  *r0 = j0;
+  *r1 = j1;
+  if (!dev_map || j1 == j0 || gx == 0) return 0;
+  // the window's gradient rows must have been built (a band pyramid holds [vlo, vhi))
+  const int ylo = by + j0 * step - hh, yhi = by + (j1 - 1) * step + hh + 1;
+  if (ylo < L.vlo || (yhi > L.vhi && L.vhi < L.h)) return 1;
+  if (use_device(c)) return -1;
+  TimedScope ts(c, T_EIG, c->stream);
+  return launched(c, "k_min_eigen", launch_min_eigen(c->stream, L.gx, L.gy, L.w, bx, by + j0 * step, step, gx, j1 - j0,
+                                                     hw, hh, dev_map + (long)j0 * gx));
+}
+
 KLT_API int klt_hip_synth_frames(klt_hip_ctx *c, unsigned long long seed, int t0, int n, int ncols, int nrows,
                                  unsigned char *dev, long pitch, long fstride) {
   if (!c || !dev || n < 0 || pitch < ncols) return fail(c, "synth: bad arguments");

@@ -12,15 +12,21 @@
 #include <string.h>
 
 #include <string>
+#include <vector>
 
 #include "klt_dev.h"
 #include "klt_shard.h"
+
+extern "C" {
+#include "klt_select.h"
+}
 
 #define KLT_API extern "C" __attribute__((visibility("default")))
 
 struct klt_shard {
   klt_hip_ctx *ctx = nullptr;
   int rank = 0, world = 1, nrows = 0;
+  int cranks = 1;                       // ranks in the communicator (1 for a local shard)
   float own_lo = 0.0f, own_hi = 0.0f;   // features owned: own_lo <= y < own_hi at the chunk start
   int row_lo = 0, row_hi = 0;           // level-0 rows built
   int load_lo = 0, load_hi = 0;         // u8 rows the band build reads
@@ -30,6 +36,8 @@ struct klt_shard {
   int *d_v0 = nullptr;                  // chunk-start state (ownership, redo)
   size_t cap = 0;
   int *h_flag = nullptr;                // pinned: the summed escape flag
+  int *d_map = nullptr;                 // the trackability map (replacement)
+  size_t map_cap = 0;
   std::string err;
 };
 
@@ -140,6 +148,7 @@ klt_shard *make_shard(klt_hip_ctx *ctx, int rank, int world, const unsigned char
   s->rank = rank;
   s->world = world;
   s->nrows = nrows;
+  s->cranks = cranks;
   const int lo = (int)((long)rank * nrows / world), hi = (int)((long)(rank + 1) * nrows / world);
   s->own_lo = rank == 0 ? -INFINITY : (float)lo;
   s->own_hi = rank == world - 1 ? INFINITY : (float)hi;
@@ -181,6 +190,7 @@ KLT_API void klt_shard_destroy(klt_shard *s) {
   hipFree(s->d_x0);
   hipFree(s->d_y0);
   hipFree(s->d_v0);
+  hipFree(s->d_map);
   if (s->h_flag) hipHostFree(s->h_flag);
   delete s;
 }
@@ -238,4 +248,125 @@ KLT_API int klt_shard_track(klt_shard *s, const klt_hip_pyr_desc *pd, const klt_
     return sfail(s, "shard_track: redo: %s", klt_hip_last_error(s->ctx));
   if (exchange(s, st, x, y, val, n, nullptr)) return -1;
   return 1;
+}
+
+namespace {
+
+// rank r's own pixel rows [lo, hi) (rank 0 from row 0, the last to the bottom)
+void own_rows(const klt_shard *s, int r, int *lo, int *hi) {
+  *lo = r == 0 ? 0 : (int)((long)r * s->nrows / s->world);
+  *hi = r == s->world - 1 ? s->nrows : (int)((long)(r + 1) * s->nrows / s->world);
+}
+
+}  // namespace
+
+KLT_API int klt_shard_eigen(klt_shard *s, const klt_hip_pyr_desc *pd, const klt_hip_select_desc *sd, long pitch,
+                            int *dev_map, klt_shard_frames_fn full, void *user) {
+  if (!s || !pd || !sd || !dev_map) return sfail(s, "shard_eigen: null argument");
+  if (pd->nrows != s->nrows) return sfail(s, "shard_eigen: frames have %d rows, the shard %d", pd->nrows, s->nrows);
+  if (hipSetDevice(klt_hip_ctx_device(s->ctx)) != hipSuccess) return sfail(s, "shard_eigen: device");
+  int lo, hi, nx, ny, j0, j1;
+  own_rows(s, s->rank, &lo, &hi);
+  int rc = klt_hip_min_eigen_rows(s->ctx, sd, lo, hi, dev_map, &nx, &ny, &j0, &j1);
+  if (rc < 0) return sfail(s, "shard_eigen: %s", klt_hip_last_error(s->ctx));
+  if (rc == 0) return 0;
+  // the windows reach rows the band pyramid does not hold: rebuild the last
+  // frame's pyramid whole (it becomes the previous pyramid; same values)
+  if (!full) return sfail(s, "shard_eigen: band too narrow for the selection window and no whole-frame callback");
+  const unsigned char *whole = nullptr;
+  long wstride = 0;
+  if (full(user, &whole, &wstride) || !whole) return sfail(s, "shard_eigen: whole-frame callback failed");
+  if (klt_hip_frames_begin(s->ctx, pd, whole, pitch)) return sfail(s, "shard_eigen: %s", klt_hip_last_error(s->ctx));
+  rc = klt_hip_min_eigen_rows(s->ctx, sd, lo, hi, dev_map, &nx, &ny, &j0, &j1);
+  if (rc != 0) return sfail(s, "shard_eigen: %s", rc < 0 ? klt_hip_last_error(s->ctx) : "rows still missing");
+  return 1;
+}
+
+KLT_API int klt_shard_select(klt_shard *s, const klt_hip_pyr_desc *pd, const klt_hip_select_desc *sd, int mindist,
+                             int min_eigenvalue, const int *dev_map, float *x, float *y, int *val, int n) {
+  if (!s || !pd || !sd || !dev_map || n < 0 || (n > 0 && (!x || !y || !val)))
+    return sfail(s, "shard_select: bad argument");
+  if (hipSetDevice(klt_hip_ctx_device(s->ctx)) != hipSuccess) return sfail(s, "shard_select: device");
+  int nx, ny, j0, j1;
+  if (klt_hip_min_eigen_rows(s->ctx, sd, 0, 0, nullptr, &nx, &ny, &j0, &j1) < 0)
+    return sfail(s, "shard_select: %s", klt_hip_last_error(s->ctx));
+  hipStream_t st = (hipStream_t)klt_hip_get_stream(s->ctx);
+  std::vector<int> map((size_t)nx * ny + 1);
+  std::vector<float> hx(n > 0 ? n : 1), hy(n > 0 ? n : 1);
+  std::vector<int> hv(n > 0 ? n : 1);
+  if ((size_t)nx * ny) SHIP(s, hipMemcpyAsync(map.data(), dev_map, sizeof(int) * (size_t)nx * ny, hipMemcpyDeviceToHost, st));
+  if (n > 0) {
+    SHIP(s, hipMemcpyAsync(hx.data(), x, sizeof(float) * n, hipMemcpyDeviceToHost, st));
+    SHIP(s, hipMemcpyAsync(hy.data(), y, sizeof(float) * n, hipMemcpyDeviceToHost, st));
+    SHIP(s, hipMemcpyAsync(hv.data(), val, sizeof(int) * n, hipMemcpyDeviceToHost, st));
+  }
+  SHIP(s, hipStreamSynchronize(st));
+  // the host half of KLTReplaceLostFeatures (klt_api.c select_features), the
+  // same code on every rank over the same map and list: identical results
+  KLT_FeatureList fl = KLTCreateFeatureList(n);
+  for (int i = 0; i < n; ++i) {
+    fl->feature[i]->x = hx[i];
+    fl->feature[i]->y = hy[i];
+    fl->feature[i]->val = hv[i];
+  }
+  klt_select_from_map(map.data(), nx, ny, sd->borderx, sd->bordery, sd->nSkippedPixels + 1, pd->ncols, pd->nrows, fl,
+                      mindist < 0 ? 0 : mindist, min_eigenvalue, 0);
+  for (int i = 0; i < n; ++i) {
+    hx[i] = fl->feature[i]->x;
+    hy[i] = fl->feature[i]->y;
+    hv[i] = fl->feature[i]->val;
+  }
+  KLTFreeFeatureList(fl);
+  if (n > 0) {
+    SHIP(s, hipMemcpyAsync(x, hx.data(), sizeof(float) * n, hipMemcpyHostToDevice, st));
+    SHIP(s, hipMemcpyAsync(y, hy.data(), sizeof(float) * n, hipMemcpyHostToDevice, st));
+    SHIP(s, hipMemcpyAsync(val, hv.data(), sizeof(int) * n, hipMemcpyHostToDevice, st));
+    SHIP(s, hipStreamSynchronize(st));
+  }
+  return 0;
+}
+
+KLT_API int klt_shard_replace(klt_shard *s, const klt_hip_pyr_desc *pd, const klt_hip_select_desc *sd, long pitch,
+                              int mindist, int min_eigenvalue, float *x, float *y, int *val, int n,
+                              klt_shard_frames_fn full, void *user) {
+  if (!s || !pd || !sd) return sfail(s, "shard_replace: null argument");
+  if (s->cranks != s->world)
+    return sfail(s, "shard_replace: a local shard has no peers (use klt_shard_eigen and klt_shard_select)");
+  if (hipSetDevice(klt_hip_ctx_device(s->ctx)) != hipSuccess) return sfail(s, "shard_replace: device");
+  int nx, ny, j0, j1;
+  if (klt_hip_min_eigen_rows(s->ctx, sd, 0, 0, nullptr, &nx, &ny, &j0, &j1) < 0)
+    return sfail(s, "shard_replace: %s", klt_hip_last_error(s->ctx));
+  const size_t np = (size_t)nx * ny;
+  if (np > s->map_cap) {
+    hipFree(s->d_map);
+    s->d_map = nullptr;
+    s->map_cap = 0;
+    SHIP(s, hipMalloc((void **)&s->d_map, np * sizeof(int)));
+    s->map_cap = np;
+  }
+  const int rc = np ? klt_shard_eigen(s, pd, sd, pitch, s->d_map, full, user) : 0;
+  if (rc < 0) return rc;
+  // every rank's grid rows to every rank: one broadcast per owner, grouped
+  hipStream_t st = (hipStream_t)klt_hip_get_stream(s->ctx);
+  if (np) {
+    SNCCL(s, ncclGroupStart());
+    for (int r = 0; r < s->world; ++r) {
+      int lo, hi;
+      own_rows(s, r, &lo, &hi);
+      if (klt_hip_min_eigen_rows(s->ctx, sd, lo, hi, nullptr, &nx, &ny, &j0, &j1) < 0) {
+        ncclGroupEnd();
+        return sfail(s, "shard_replace: %s", klt_hip_last_error(s->ctx));
+      }
+      if (j1 > j0) {
+        int *p = s->d_map + (size_t)j0 * nx;
+        const ncclResult_t e = ncclBroadcast(p, p, (size_t)(j1 - j0) * nx, ncclInt32, r, s->comm, st);
+        if (e != ncclSuccess) {
+          ncclGroupEnd();
+          return sfail(s, "shard_replace: ncclBroadcast: %s", ncclGetErrorString(e));
+        }
+      }
+    }
+    SNCCL(s, ncclGroupEnd());
+  }
+  return klt_shard_select(s, pd, sd, mindist, min_eigenvalue, s->d_map, x, y, val, n);
 }

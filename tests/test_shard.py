@@ -268,11 +268,15 @@ def test_sharded_4k_20k_equals_reference(gpu, world):
 _FRAMES_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_long))
 
 
-def c_sharded_sequence(gpu, frames, nfeat, world, chunk, margin, band_only=False, real_comm=False):
+def c_sharded_sequence(gpu, frames, nfeat, world, chunk, margin, band_only=False, real_comm=False, replace=False):
     """klt_shard_track per chunk for every rank (klt_shard_create_local: the
     rank's band, a communicator of its own), then the all-reduce done by hand:
     the sum of the ranks' int32 contributions.  real_comm (world 1): the
-    RCCL path proper, klt_shard_unique_id + klt_shard_create."""
+    RCCL path proper, klt_shard_unique_id + klt_shard_create.  replace: lost
+    features replaced after every chunk -- klt_shard_replace over the real
+    communicator, else every rank's klt_shard_eigen rows into one map and
+    klt_shard_select over it."""
+    from kltamd.device import SelectDesc
     H, W = frames[0].shape
     dev = torch.device("cuda", 0)
     dfr = torch.from_numpy(np.ascontiguousarray(np.stack(frames))).to(dev)
@@ -302,10 +306,10 @@ def c_sharded_sequence(gpu, frames, nfeat, world, chunk, margin, band_only=False
         assert gpu.klt_hip_frames_begin(rk.ctx, C.byref(rk.pd), C.c_void_p(dfr.data_ptr()), W) == 0
         ranks.append(rk)
         shards.append(s)
-    redone, cur = [0], [0]
+    redone, cur, rebuilt = [0], [0], [0]
 
-    def whole(user, frames_out, stride_out):  # frames t0-1 .. of the chunk being redone
-        frames_out[0] = dfr.data_ptr() + (cur[0] - 1) * H * W
+    def whole(user, frames_out, stride_out):  # whole frames from frame cur[0] on
+        frames_out[0] = dfr.data_ptr() + cur[0] * H * W
         stride_out[0] = H * W
         redone[0] += 1
         return 0
@@ -314,7 +318,7 @@ def c_sharded_sequence(gpu, frames, nfeat, world, chunk, margin, band_only=False
     for c0 in range(1, 1 + T, chunk):
         n = min(chunk, 1 + T - c0)
         nn = min(chunk, 1 + T - c0 - n)
-        cur[0] = c0
+        cur[0] = c0 - 1
         acc = None
         for rk, s in zip(ranks, shards):
             xr, yr, vr = x.clone(), y.clone(), v.clone()
@@ -326,10 +330,36 @@ def c_sharded_sequence(gpu, frames, nfeat, world, chunk, margin, band_only=False
             part = torch.stack([xr.view(torch.int32), yr.view(torch.int32), vr])
             acc = part if acc is None else acc + part
         x.view(torch.int32).copy_(acc[0]), y.view(torch.int32).copy_(acc[1]), v.copy_(acc[2])
+        if replace:
+            tc = ranks[0].tc.contents
+            sd = SelectDesc(tc.window_width, tc.window_height, max(tc.borderx, tc.window_width // 2),
+                            max(tc.bordery, tc.window_height // 2), tc.nSkippedPixels)
+            cur[0] = c0 + n - 1  # the last tracked frame, whole, when a band is too narrow
+            xyz = (C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()), x.numel())
+            if real_comm:
+                rk, s = ranks[0], shards[0]
+                rc = gpu.klt_shard_replace(s, C.byref(rk.pd), C.byref(sd), W, tc.mindist, tc.min_eigenvalue,
+                                           *xyz, cb, None)
+                assert rc == 0, gpu.klt_shard_last_error(s)
+            else:
+                nx, ny, j0, j1 = (C.c_int() for _ in range(4))
+                assert gpu.klt_hip_min_eigen_rows(ranks[0].ctx, C.byref(sd), 0, 0, None, C.byref(nx), C.byref(ny),
+                                                  C.byref(j0), C.byref(j1)) == 0
+                emap = torch.full((nx.value * ny.value,), -7, dtype=torch.int32, device=dev)
+                for rk, s in zip(ranks, shards):
+                    rc = gpu.klt_shard_eigen(s, C.byref(rk.pd), C.byref(sd), W, C.c_void_p(emap.data_ptr()), cb, None)
+                    assert rc in (0, 1), gpu.klt_shard_last_error(s)
+                    rebuilt[0] += rc
+                assert not bool((emap == -7).any())  # the ranks' rows tile the map
+                rc = gpu.klt_shard_select(shards[0], C.byref(ranks[0].pd), C.byref(sd), tc.mindist,
+                                          tc.min_eigenvalue, C.c_void_p(emap.data_ptr()), *xyz)
+                assert rc == 0, gpu.klt_shard_last_error(shards[0])
     for rk, s in zip(ranks, shards):
         gpu.klt_shard_destroy(s)
         gpu.KLTFreeTrackingContext(rk.tc)
     del keep
+    if replace:
+        c_sharded_sequence.rebuilt = rebuilt[0]
     return x.cpu().numpy(), y.cpu().numpy(), v.cpu().numpy(), redone[0]
 
 
@@ -348,3 +378,89 @@ def test_c_shard_equals_single_gpu(gpu, oracle, world, chunk, margin, band_only,
     assert np.array_equal(y.view(np.int32), Y[:, k].view(np.int32))
     if margin == 0:
         assert redone > 0  # no margin: band-edge features escape; the callback supplies whole frames
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,margin,real_comm", [(1, 64, True), (3, 64, False), (4, 0, False), (2, 2, False)])
+def test_c_shard_replace_equals_single_gpu(gpu, oracle, world, margin, real_comm):
+    """KLTReplaceLostFeatures after every frame (the harness with REPLACE):
+    ranks' band trackability rows + the same host selection on every rank
+    equal the oracle's sequence bit for bit (margin 0: band pyramids too short
+    for the selection window, or chunks redone)."""
+    from kltabi import OracleTracker
+    frames = synth(gpu, 3160 + world, 640, 480, 9)
+    x, y, v, redone = c_sharded_sequence(gpu, frames, 800, world, 1, margin, False, real_comm, replace=True)
+    X, Y, V = OracleTracker(oracle).harness(frames, 800, 9, first=frames[0], replace=True)
+    k = 9 - 2
+    assert (V[:, :k + 1] >= 0).sum() > 0 and (V[:, k] > 0).any()  # replacements happened (val = eigenvalue)
+    assert np.array_equal(v, V[:, k])
+    assert np.array_equal(x.view(np.int32), X[:, k].view(np.int32))
+    assert np.array_equal(y.view(np.int32), Y[:, k].view(np.int32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,rank,margin", [(4, 1, 0), (3, 2, 0), (3, 0, 64), (15, 1, 0), (15, 14, 0), (15, 7, 1)])
+def test_eigen_rows_of_band_pyramid(gpu, world, rank, margin):
+    """klt_hip_min_eigen_rows on a band-built pyramid: the rank's grid rows
+    equal the whole frame's map (klt_hip_min_eigen), or it reports 1 (nothing
+    written) when the 7x7 window reaches rows the band does not hold;
+    klt_shard_eigen then rebuilds the frame whole through the callback
+    (15 ranks of 480 rows: 32-row bands on tile edges, no margin)."""
+    from kltamd.device import SelectDesc
+    frames = synth(gpu, 4242, 640, 480, 2)
+    H, W = frames[0].shape
+    dev = torch.device("cuda", 0)
+    dfr = torch.from_numpy(np.ascontiguousarray(np.stack(frames))).to(dev)
+    rk = _Rank(gpu, dfr, H, W, world, rank, margin)
+    tc = rk.tc.contents
+    sd = SelectDesc(tc.window_width, tc.window_height, max(tc.borderx, tc.window_width // 2),
+                    max(tc.bordery, tc.window_height // 2), tc.nSkippedPixels)
+    # whole-frame map of frame 1
+    assert gpu.klt_hip_frames_begin(rk.ctx, C.byref(rk.pd), C.c_void_p(dfr.data_ptr() + H * W), W) == 0
+    nx, ny, j0, j1 = (C.c_int() for _ in range(4))
+    assert gpu.klt_hip_min_eigen_rows(rk.ctx, C.byref(sd), 0, H, None, C.byref(nx), C.byref(ny),
+                                      C.byref(j0), C.byref(j1)) == 0
+    full_map = torch.zeros(nx.value * ny.value, dtype=torch.int32, device=dev)
+    assert gpu.klt_hip_min_eigen_rows(rk.ctx, C.byref(sd), 0, H, C.c_void_p(full_map.data_ptr()), C.byref(nx),
+                                      C.byref(ny), C.byref(j0), C.byref(j1)) == 0
+    assert (j0.value, j1.value) == (0, ny.value)
+    # band pyramid of frame 1 (a band call with no features builds it and makes it the previous pyramid)
+    rk.begin(0)
+    esc = torch.zeros(1, dtype=torch.int32, device=dev)
+    e = torch.zeros(0, device=dev)
+    b = rk.band
+    assert gpu.klt_hip_track_frames_band(rk.ctx, C.byref(rk.pd), C.byref(rk.td), C.c_void_p(dfr.data_ptr() + H * W),
+                                         W, H * W, 1, C.c_void_p(e.data_ptr()), C.c_void_p(e.data_ptr()),
+                                         C.c_void_p(e.data_ptr()), 0, b.own_lo, b.own_hi, b.row_lo, b.row_hi,
+                                         C.c_void_p(esc.data_ptr()), None, 0) == 0
+    lo = 0 if rank == 0 else rank * H // world
+    hi = H if rank == world - 1 else (rank + 1) * H // world
+    got = torch.full_like(full_map, -7)
+    rc = gpu.klt_hip_min_eigen_rows(rk.ctx, C.byref(sd), lo, hi, C.c_void_p(got.data_ptr()), C.byref(nx),
+                                    C.byref(ny), C.byref(j0), C.byref(j1))
+    by, step, hh = sd.bordery, sd.nSkippedPixels + 1, sd.window_height // 2
+    rows = slice(j0.value * nx.value, j1.value * nx.value)
+    assert j1.value > j0.value and all(lo <= by + j * step < hi for j in (j0.value, j1.value - 1))
+    # a band build runs whole 32-row level-0 tiles: those rows are valid
+    vlo, vhi = b.row_lo // 32 * 32, (H if b.row_hi >= H else min(H, -(-b.row_hi // 32) * 32))
+    needs = (by + j0.value * step - hh < vlo) or (by + (j1.value - 1) * step + hh >= vhi)
+    assert rc == (1 if needs else 0)
+    if rc == 0:
+        assert torch.equal(got[rows], full_map[rows])
+        assert bool((got[:rows.start] == -7).all()) and bool((got[rows.stop:] == -7).all())
+    else:
+        assert bool((got == -7).all())
+        # the shard rebuilds the frame whole and then succeeds
+        s = gpu.klt_shard_create_local(rk.ctx, rank, world, H, margin)
+        calls = []
+
+        def whole(user, frames_out, stride_out):
+            calls.append(1)
+            frames_out[0] = dfr.data_ptr() + H * W
+            stride_out[0] = H * W
+            return 0
+        cb = _FRAMES_FN(whole)
+        assert gpu.klt_shard_eigen(s, C.byref(rk.pd), C.byref(sd), W, C.c_void_p(got.data_ptr()), cb, None) == 1
+        assert calls == [1] and torch.equal(got[rows], full_map[rows])
+        gpu.klt_shard_destroy(s)
+    gpu.KLTFreeTrackingContext(rk.tc)
