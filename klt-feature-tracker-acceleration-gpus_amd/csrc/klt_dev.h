@@ -116,7 +116,7 @@ struct TrkFramesArgs {
   unsigned long long *count;  // non-null: [kCountSlots] 2x2 systems formed, [kCountSlots] gather round trips
 };
 constexpr int kCountSlots = 64;  // counter pairs (the host sums them)
-constexpr int kProfN = 10;       // instrumented build: counters per wave
+constexpr int kProfN = 12;       // instrumented build: counters per wave
 
 // ---------------------------------------------------------------------------
 // affine consistency check arguments (affine.hip)

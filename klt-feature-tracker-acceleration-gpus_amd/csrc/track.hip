@@ -59,7 +59,8 @@ __device__ __forceinline__ TrkLevel at_frame(const TrkLevel &L, long off) {
 // ---------------------------------------------------------------------------
 // Instrumented build (make prof): per-wave shader-clock cycles per phase
 #ifdef KLT_TRACK_PROF
-// kProfN counters: 0 gather+interp, 1 sums, 2 solve, 3 residue, 4 frame, 5 iterations, 6 passes, 7 wall ticks, 8/9 wall start/end
+// kProfN counters: 0 gather+interp, 1 sums, 2 solve, 3 residue, 4 frame, 5 iterations, 6 passes, 7 wall ticks,
+// 8/9 wall start/end, 10 levels (track_level_g calls), 11 pass-top tests (window/escape/hand-over)
 struct Prof {
   unsigned long long c[kProfN] = {};
 };
@@ -470,6 +471,7 @@ __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, 
   int it = 0, status = kTracked;
   bool first = true, deferred = false;
   while (true) {
+    PROF_T(t_top);
     // window test: top of an iteration, or the post-loop test for a finished one
     if (act && ((first && x1_out) || window_out(x2, y2, hw, hh, nc, nr))) {
       status = kOOB;
@@ -500,6 +502,7 @@ __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, 
       for (int k = 0; k < PPL; ++k) rc.aim[k] = a_im[k];
       act = false;
     }
+    PROF_ADD(11, t_top);
     if (!wave_any(act) && !job) break;
     PROF_INC(6);
     if (act || job) ++cnt.passes;
@@ -679,9 +682,11 @@ __device__ __forceinline__ void track_feature_g(PROF_DECL const TrkArgs &a, cons
       yo = uni<G>(yo * a.ss);
     }
     const bool lj = job && r == a.nlev - 1;
+    PROF_T(t_l0);
     const int v = track_level_g<G, PPL, PATCH, WIN, EXACT, LI>(PROF_ARG a, w, LA(r), LB(r), xl, yl, xo, yo, go,
                                                                lane, red, r == 0, rc, lj, defer && r == 0, R,
                                                                rstat, cnt);
+    PROF_ADD(10, t_l0);
     if (lj && rstat != kTracked) return;
     if (go) {
       val = v;

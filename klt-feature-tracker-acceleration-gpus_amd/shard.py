@@ -41,12 +41,33 @@ class Band:
     row_hi: int
 
 
-def band_of(nrows: int, world: int, rank: int, margin: int = DEFAULT_MARGIN) -> Band:
-    lo = rank * nrows // world
-    hi = (rank + 1) * nrows // world
+def band_of(nrows: int, world: int, rank: int, margin: int = DEFAULT_MARGIN, edges=None) -> Band:
+    """Rank r's band: rows [r*H/N, (r+1)*H/N), or [edges[r], edges[r+1]) when
+    edges (N+1 row boundaries, balanced_edges) are given."""
+    if edges is not None:
+        assert len(edges) == world + 1 and edges[0] == 0 and edges[-1] == nrows
+        lo, hi = int(edges[rank]), int(edges[rank + 1])
+    else:
+        lo = rank * nrows // world
+        hi = (rank + 1) * nrows // world
     own_lo = float("-inf") if rank == 0 else float(lo)
     own_hi = float("inf") if rank == world - 1 else float(hi)
     return Band(own_lo, own_hi, max(0, lo - margin), min(nrows, hi + margin))
+
+
+def balanced_edges(y: torch.Tensor, v: torch.Tensor, nrows: int, world: int) -> list[int]:
+    """Row boundaries that give every rank about the same number of live
+    features (quantiles of their y), for the tracker's share of a rank's time:
+    a rank with a dense band gets fewer rows.  Deterministic in (y, v), so
+    every rank computes the same edges from the same list."""
+    ys = torch.sort(y[v >= 0].float().cpu()).values
+    m = ys.numel()
+    edges = [0]
+    for r in range(1, world):
+        e = int(ys[min(m - 1, r * m // world)].item()) if m else r * nrows // world
+        edges.append(min(max(e, edges[-1]), nrows))
+    edges.append(nrows)
+    return edges
 
 
 def band_rows(nrows: int, band: Band, tile: int = 32, halo: int = 8) -> tuple[int, int]:
@@ -137,14 +158,15 @@ class ShardedSequence:
     lib/ctx: the loaded library and a device context; pd/td: descriptors;
     frames: device u8 frames -- a uint8 tensor [T, H, W] (every rank holds
     them whole) or a BandFrames (the rank's rows only; build it with
-    band_of(H, world, rank, margin)); x/y/v: device feature arrays (identical
-    on every rank at the start), on the stream the context uses.
+    band_of(H, world, rank, margin, edges)); x/y/v: device feature arrays
+    (identical on every rank at the start), on the stream the context uses.
+    edges: row boundaries of the bands (balanced_edges), default equal rows.
     all_reduce(tensor) sums a device tensor over the ranks in place
     (torch.distributed.all_reduce in production).
     """
 
     def __init__(self, lib, ctx, pd, td, frames: torch.Tensor, x, y, v, rank: int, world: int, all_reduce,
-                 chunk: int = 64, margin: int = DEFAULT_MARGIN):
+                 chunk: int = 64, margin: int = DEFAULT_MARGIN, edges=None):
         from .device import check
         self.lib, self.ctx, self.pd, self.td = lib, ctx, pd, td
         self.src = frames if isinstance(frames, (FullFrames, BandFrames)) else FullFrames(frames)
@@ -152,7 +174,7 @@ class ShardedSequence:
         self.rank, self.world, self.all_reduce, self.chunk = rank, world, all_reduce, chunk
         H, W = self.src.H, self.src.W
         self.H, self.W = H, W
-        self.band = band_of(H, world, rank, margin)
+        self.band = band_of(H, world, rank, margin, edges)
         if isinstance(self.src, BandFrames):
             ra, rb = band_rows(H, self.band)
             assert self.src.ra <= ra and self.src.rb >= rb, "BandFrames built for another band"

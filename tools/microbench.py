@@ -200,7 +200,7 @@ def main():
         lib.klt_hip_set_timing(ctx, 1)  # one more pass with per-launch events
         pbuf = None
         if a.prof:
-            nslot = (n + 64) * 10
+            nslot = (n + 64) * 12
             pbuf = lib.klt_hip_malloc(ctx, 8 * nslot)
             check(lib, ctx, lib.klt_hip_memcpy(ctx, pbuf, np.zeros(nslot, np.uint64).ctypes.data, 8 * nslot, H2D),
                   "zero")
@@ -216,12 +216,14 @@ def main():
             lib.klt_hip_sync(ctx)
             pr = np.empty(nslot, np.uint64)
             check(lib, ctx, lib.klt_hip_memcpy(ctx, pr.ctypes.data, pbuf, 8 * nslot, 2), "prof")
-            pr = pr.reshape(-1, 10).astype(np.float64)
+            pr = pr.reshape(-1, 12).astype(np.float64)
             pr = pr[pr[:, 4] > 0]  # waves that ran frames
-            names = ["gather_interp", "sums", "solve", "residue", "frame", "iterations", "passes", "wall_ticks"]
+            names = ["gather_interp", "sums", "solve", "residue", "frame", "iterations", "passes", "wall_ticks",
+                     "-", "-", "levels", "pass_top"]
             # accumulated over the timed rep's launches (last launch overwrites per slot): per wave per frame
             fr = a.chunk
-            out["prof_cycles_per_wave_frame"] = {nm: float(pr[:, k].mean() / fr) for k, nm in enumerate(names)}
+            out["prof_cycles_per_wave_frame"] = {nm: float(pr[:, k].mean() / fr) for k, nm in enumerate(names)
+                                                 if nm != "-"}
             out["prof_cycles_per_wave_frame"].pop("wall_ticks")
             out["prof_waves"] = int(pr.shape[0])
             rate = C.c_int(0)

@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--worlds", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--margins", type=int, nargs="+", default=[64])
     ap.add_argument("--seed", type=int, default=2160)
+    ap.add_argument("--balanced", action="store_true", help="bands of equal feature counts (balanced_edges)")
     ap.add_argument("--no-ahead", action="store_true", help="pass 2 without building the next chunk ahead")
     ap.add_argument("--own-streams", action="store_true",
                     help="pass 2: the library on its own streams (not a torch pool stream), synchronized by host")
@@ -54,7 +55,7 @@ def main():
     import torch
     import kltamd
     from kltamd.device import PyrDesc, Timing, TrackDesc, check, use_torch_stream
-    from kltamd.shard import band_of, merge_chunk
+    from kltamd.shard import balanced_edges, band_of, merge_chunk
     from kltabi import fl_to_arrays, u8ptr
 
     lib = kltamd.load()
@@ -85,7 +86,7 @@ def main():
             self.pd, self.td = PyrDesc(), TrackDesc()
             lib.klt_amd_pyr_desc(self.tc, W, H, self.tc.contents.nPyramidLevels, 1, C.byref(self.pd))
             lib.klt_amd_track_desc(self.tc, C.byref(self.td))
-            self.band = band_of(H, world, rank, margin)
+            self.band = band_of(H, world, rank, margin, balanced_edges(ys, vs, H, world) if a.balanced else None)
             self.rank = rank
 
         def ptr(self, t):
@@ -110,7 +111,8 @@ def main():
         world = int(np.load(a.replay)["world"])
         margin = int(np.load(a.replay)["margin"])
         st = np.load(a.replay)
-        rk = Rank(world, a.rank, margin, a.own_streams)
+        own = a.own_streams
+        rk = Rank(world, a.rank, margin, own)
         xr, yr, vr = xs.clone(), ys.clone(), vs.clone()
         esc = torch.zeros(1, dtype=torch.int32, device=dev)
         sx, sy, sv = (torch.from_numpy(st[k]).to(dev) for k in ("x", "y", "v"))
@@ -122,10 +124,10 @@ def main():
                 nn = chunks[ci + 1][1] if ci + 1 < len(chunks) and not a.no_ahead else 0
                 xr.copy_(sx[ci]), yr.copy_(sy[ci]), vr.copy_(sv[ci])
                 esc.zero_()
-                if a.own_streams:
+                if own:
                     torch.cuda.current_stream().synchronize()
                 rk.chunk(c0, n, xr, yr, vr, esc, next_n=nn)
-                if a.own_streams:
+                if own:
                     check(lib, rk.ctx, lib.klt_hip_sync(rk.ctx), "sync")
                 int(esc.item())  # the host's read of the escape flag (merge_chunk)
             torch.cuda.synchronize()
@@ -133,7 +135,8 @@ def main():
         print(json.dumps({"rank": a.rank, "us_per_frame": 1e6 * (time.perf_counter() - t_start) / frames_timed}))
         return
 
-    out = {"workload": f"{W}x{H}, {NF} features, {a.frames - 1} tracked frames, {a.chunk}-frame chunks",
+    out = {"workload": f"{W}x{H}, {NF} features, {a.frames - 1} tracked frames, {a.chunk}-frame chunks"
+                       + (", bands of equal feature counts" if a.balanced else ""),
            "exchange_us_assumed": a.exchange_us, "runs": []}
     base_fps = None
     for margin in a.margins:
@@ -195,7 +198,7 @@ def main():
                     cmd = [sys.executable, __file__, "--replay", f, "--rank", str(r), "--width", str(W), "--height",
                            str(H), "--features", str(NF), "--frames", str(a.frames), "--chunk", str(a.chunk),
                            "--seed", str(a.seed)] + (["--no-ahead"] if a.no_ahead else []) + \
-                          (["--own-streams"] if a.own_streams else [])
+                          (["--own-streams"] if a.own_streams else []) + (["--balanced"] if a.balanced else [])
                     res = subprocess.run(cmd, check=True, capture_output=True, text=True)
                     rank_us.append(json.loads(res.stdout.strip().splitlines()[-1])["us_per_frame"])
             nch = len(chunks)
