@@ -92,6 +92,7 @@ struct TrkArgs {
   TrkLevel B[KLT_HIP_MAX_LEVELS];  // current image (img2)
   int nlev;
   float ss;
+  float ss_inv;       // 1/ss when ss is a power of two (x / ss == x * ss_inv bit for bit), else 0
   int ww, wh, max_it;
   float min_det, min_disp, max_res, step;
   int borderx, bordery, ncols, nrows;

@@ -470,6 +470,7 @@ void fill_trk_args(const klt_hip_track_desc *d, int nlev, int ss, int ncols, int
   const int npx = d->window_width * d->window_height;
   a.nlev = nlev;
   a.ss = (float)ss;
+  a.ss_inv = ss > 0 && (ss & (ss - 1)) == 0 ? 1.0f / (float)ss : 0.0f;
   a.ww = d->window_width;
   a.wh = d->window_height;
   a.max_it = d->max_iterations;

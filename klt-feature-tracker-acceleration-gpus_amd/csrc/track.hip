@@ -667,8 +667,10 @@ __device__ __forceinline__ void track_feature_g(PROF_DECL const TrkArgs &a, cons
   // loss).  defer: this frame's own finest-level residue may be handed on.
   float xl = fx, yl = fy;
   for (int r = a.nlev - 1; r >= 0; --r) {
-    xl = uni<G>(xl / a.ss);
-    yl = uni<G>(yl / a.ss);
+    // xloc /= subsampling (trackFeatures.c:1353): a power of two divides
+    // exactly, so the reciprocal's product is the same float
+    xl = uni<G>(a.ss_inv != 0.0f ? xl * a.ss_inv : xl / a.ss);
+    yl = uni<G>(a.ss_inv != 0.0f ? yl * a.ss_inv : yl / a.ss);
   }
   float xo = xl, yo = yl;
   int val = kTracked;
