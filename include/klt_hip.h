@@ -288,6 +288,14 @@ int klt_hip_min_eigen(klt_hip_ctx *ctx, int slot, const klt_hip_select_desc *des
 int klt_hip_min_eigen_rows(klt_hip_ctx *ctx, const klt_hip_select_desc *desc, int row_lo, int row_hi, int *dev_map,
                            int *nx, int *ny, int *r0, int *r1);
 
+/* the host half of KLTReplaceLostFeatures (selectGoodFeatures.c:514-541 ->
+   _KLTSelectGoodFeatures' sort and minimum-distance fill, :425-453) over a
+   complete trackability map in device memory (dev_map, nx*ny values as
+   klt_hip_min_eigen_rows lays them out): fills the lost slots of the device
+   feature arrays.  Synchronous.  The sharded drivers run it on every rank. */
+int klt_hip_select_map(klt_hip_ctx *ctx, int ncols, int nrows, const klt_hip_select_desc *desc, int mindist,
+                       int min_eigenvalue, const int *dev_map, float *x, float *y, int *val, int n);
+
 /* synthetic frames t0..t0+n-1 (include/klt_synth.h) into device memory */
 int klt_hip_synth_frames(klt_hip_ctx *ctx, unsigned long long seed, int t0, int n, int ncols,
                          int nrows, unsigned char *dev, long pitch, long frame_stride);

@@ -282,25 +282,25 @@ KLT_API int klt_shard_eigen(klt_shard *s, const klt_hip_pyr_desc *pd, const klt_
   return 1;
 }
 
-KLT_API int klt_shard_select(klt_shard *s, const klt_hip_pyr_desc *pd, const klt_hip_select_desc *sd, int mindist,
-                             int min_eigenvalue, const int *dev_map, float *x, float *y, int *val, int n) {
-  if (!s || !pd || !sd || !dev_map || n < 0 || (n > 0 && (!x || !y || !val)))
-    return sfail(s, "shard_select: bad argument");
-  if (hipSetDevice(klt_hip_ctx_device(s->ctx)) != hipSuccess) return sfail(s, "shard_select: device");
+KLT_API int klt_hip_select_map(klt_hip_ctx *ctx, int ncols, int nrows, const klt_hip_select_desc *sd, int mindist,
+                               int min_eigenvalue, const int *dev_map, float *x, float *y, int *val, int n) {
+  if (!ctx || !sd || !dev_map || ncols < 1 || nrows < 1 || n < 0 || (n > 0 && (!x || !y || !val))) return -1;
+  if (hipSetDevice(klt_hip_ctx_device(ctx)) != hipSuccess) return -1;
   int nx, ny, j0, j1;
-  if (klt_hip_min_eigen_rows(s->ctx, sd, 0, 0, nullptr, &nx, &ny, &j0, &j1) < 0)
-    return sfail(s, "shard_select: %s", klt_hip_last_error(s->ctx));
-  hipStream_t st = (hipStream_t)klt_hip_get_stream(s->ctx);
+  if (klt_hip_min_eigen_rows(ctx, sd, 0, 0, nullptr, &nx, &ny, &j0, &j1) < 0) return -1;
+  hipStream_t st = (hipStream_t)klt_hip_get_stream(ctx);
   std::vector<int> map((size_t)nx * ny + 1);
   std::vector<float> hx(n > 0 ? n : 1), hy(n > 0 ? n : 1);
   std::vector<int> hv(n > 0 ? n : 1);
-  if ((size_t)nx * ny) SHIP(s, hipMemcpyAsync(map.data(), dev_map, sizeof(int) * (size_t)nx * ny, hipMemcpyDeviceToHost, st));
+  bool ok = true;
+  if ((size_t)nx * ny)
+    ok = ok && hipMemcpyAsync(map.data(), dev_map, sizeof(int) * (size_t)nx * ny, hipMemcpyDeviceToHost, st) == hipSuccess;
   if (n > 0) {
-    SHIP(s, hipMemcpyAsync(hx.data(), x, sizeof(float) * n, hipMemcpyDeviceToHost, st));
-    SHIP(s, hipMemcpyAsync(hy.data(), y, sizeof(float) * n, hipMemcpyDeviceToHost, st));
-    SHIP(s, hipMemcpyAsync(hv.data(), val, sizeof(int) * n, hipMemcpyDeviceToHost, st));
+    ok = ok && hipMemcpyAsync(hx.data(), x, sizeof(float) * n, hipMemcpyDeviceToHost, st) == hipSuccess;
+    ok = ok && hipMemcpyAsync(hy.data(), y, sizeof(float) * n, hipMemcpyDeviceToHost, st) == hipSuccess;
+    ok = ok && hipMemcpyAsync(hv.data(), val, sizeof(int) * n, hipMemcpyDeviceToHost, st) == hipSuccess;
   }
-  SHIP(s, hipStreamSynchronize(st));
+  if (!ok || hipStreamSynchronize(st) != hipSuccess) return -1;
   // the host half of KLTReplaceLostFeatures (klt_api.c select_features), the
   // same code on every rank over the same map and list: identical results
   KLT_FeatureList fl = KLTCreateFeatureList(n);
@@ -309,7 +309,7 @@ KLT_API int klt_shard_select(klt_shard *s, const klt_hip_pyr_desc *pd, const klt
     fl->feature[i]->y = hy[i];
     fl->feature[i]->val = hv[i];
   }
-  klt_select_from_map(map.data(), nx, ny, sd->borderx, sd->bordery, sd->nSkippedPixels + 1, pd->ncols, pd->nrows, fl,
+  klt_select_from_map(map.data(), nx, ny, sd->borderx, sd->bordery, sd->nSkippedPixels + 1, ncols, nrows, fl,
                       mindist < 0 ? 0 : mindist, min_eigenvalue, 0);
   for (int i = 0; i < n; ++i) {
     hx[i] = fl->feature[i]->x;
@@ -318,11 +318,20 @@ KLT_API int klt_shard_select(klt_shard *s, const klt_hip_pyr_desc *pd, const klt
   }
   KLTFreeFeatureList(fl);
   if (n > 0) {
-    SHIP(s, hipMemcpyAsync(x, hx.data(), sizeof(float) * n, hipMemcpyHostToDevice, st));
-    SHIP(s, hipMemcpyAsync(y, hy.data(), sizeof(float) * n, hipMemcpyHostToDevice, st));
-    SHIP(s, hipMemcpyAsync(val, hv.data(), sizeof(int) * n, hipMemcpyHostToDevice, st));
-    SHIP(s, hipStreamSynchronize(st));
+    ok = hipMemcpyAsync(x, hx.data(), sizeof(float) * n, hipMemcpyHostToDevice, st) == hipSuccess &&
+         hipMemcpyAsync(y, hy.data(), sizeof(float) * n, hipMemcpyHostToDevice, st) == hipSuccess &&
+         hipMemcpyAsync(val, hv.data(), sizeof(int) * n, hipMemcpyHostToDevice, st) == hipSuccess &&
+         hipStreamSynchronize(st) == hipSuccess;
+    if (!ok) return -1;
   }
+  return 0;
+}
+
+KLT_API int klt_shard_select(klt_shard *s, const klt_hip_pyr_desc *pd, const klt_hip_select_desc *sd, int mindist,
+                             int min_eigenvalue, const int *dev_map, float *x, float *y, int *val, int n) {
+  if (!s || !pd) return sfail(s, "shard_select: null argument");
+  if (klt_hip_select_map(s->ctx, pd->ncols, pd->nrows, sd, mindist, min_eigenvalue, dev_map, x, y, val, n))
+    return sfail(s, "shard_select: %s", klt_hip_last_error(s->ctx));
   return 0;
 }
 

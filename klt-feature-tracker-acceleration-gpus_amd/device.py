@@ -92,6 +92,7 @@ DEVICE_PROTOS = {
     "klt_shard_rows": (C.c_int, [V, IP, IP]),
     "klt_shard_track": (C.c_int, [V, C.POINTER(PyrDesc), C.POINTER(TrackDesc), V, C.c_long, C.c_long, C.c_int, V,
                                   C.c_int, V, V, V, C.c_int, V, V]),
+    "klt_hip_select_map": (C.c_int, [V, C.c_int, C.c_int, V, C.c_int, C.c_int, V, V, V, V, C.c_int]),
     "klt_hip_min_eigen_rows": (C.c_int, [V, V, C.c_int, C.c_int, V, IP, IP, IP, IP]),
     "klt_shard_eigen": (C.c_int, [V, C.POINTER(PyrDesc), V, C.c_long, V, V, V]),
     "klt_shard_select": (C.c_int, [V, C.POINTER(PyrDesc), V, C.c_int, C.c_int, V, V, V, V, C.c_int]),

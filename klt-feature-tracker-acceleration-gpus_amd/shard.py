@@ -174,15 +174,19 @@ class ShardedSequence:
         self.rank, self.world, self.all_reduce, self.chunk = rank, world, all_reduce, chunk
         H, W = self.src.H, self.src.W
         self.H, self.W = H, W
+        self.edges = edges
         self.band = band_of(H, world, rank, margin, edges)
         if isinstance(self.src, BandFrames):
             ra, rb = band_rows(H, self.band)
             assert self.src.ra <= ra and self.src.rb >= rb, "BandFrames built for another band"
         self.escape = torch.zeros(1, dtype=torch.int32, device=x.device)
         self.redone = 0
+        self.rebuilt = 0  # replacements whose band pyramid was too short for the selection window
+        self.t_last = None  # last tracked frame
         self._check = check
 
     def begin(self, t: int) -> None:
+        self.t_last = t
         ptr, _ = self.src.full(t, 1)
         self._check(self.lib, self.ctx, self.lib.klt_hip_frames_begin(self.ctx, C.byref(self.pd), C.c_void_p(ptr),
                                                                       self.W), "frames_begin")
@@ -222,3 +226,58 @@ class ShardedSequence:
                 self.escape.zero_()
                 self._band_call(ptr + fb, fb, n, 0, self.H)
                 merge_chunk(self.x, self.y, self.v, ys, vs, self.band, self.rank, self.all_reduce)
+            self.t_last = c0 + n - 1
+
+    # -- KLTReplaceLostFeatures across the ranks (selectGoodFeatures.c:514-541,
+    # sequential mode: the last tracked frame's pyramid, :342-348) ------------
+    def own_rows(self, rank: int | None = None) -> tuple[int, int]:
+        """Pixel rows [lo, hi) whose trackability map rows rank computes."""
+        b = self.band if rank is None else band_of(self.H, self.world, rank, 0, self.edges)
+        lo = 0 if b.own_lo == float("-inf") else int(b.own_lo)
+        hi = self.H if b.own_hi == float("inf") else int(b.own_hi)
+        return lo, hi
+
+    def _map_rows(self, sd, lo: int, hi: int, dev_map=None) -> tuple[int, int, int, int, int]:
+        nx, ny, j0, j1 = (C.c_int() for _ in range(4))
+        rc = self.lib.klt_hip_min_eigen_rows(self.ctx, C.byref(sd), lo, hi,
+                                             C.c_void_p(dev_map) if dev_map is not None else None, C.byref(nx),
+                                             C.byref(ny), C.byref(j0), C.byref(j1))
+        if rc < 0:
+            self._check(self.lib, self.ctx, rc, "min_eigen_rows")
+        return rc, nx.value, ny.value, j0.value, j1.value
+
+    def replace_rows(self, sd) -> torch.Tensor:
+        """This rank's rows of the trackability map of the last tracked frame
+        (a device int32 tensor in the whole map's layout; other rows 0).  A band
+        pyramid too short for the selection window is rebuilt from the whole
+        frame first (it becomes the previous pyramid; same values)."""
+        _, nx, ny, _, _ = self._map_rows(sd, 0, 0)
+        emap = torch.zeros(nx * ny, dtype=torch.int32, device=self.x.device)
+        lo, hi = self.own_rows()
+        rc = self._map_rows(sd, lo, hi, emap.data_ptr())[0]
+        if rc == 1:
+            self.rebuilt += 1
+            self.begin(self.t_last)
+            rc = self._map_rows(sd, lo, hi, emap.data_ptr())[0]
+            assert rc == 0, "trackability rows still missing after a whole-frame build"
+        return emap
+
+    def replace_select(self, sd, mindist: int, min_eigenvalue: int, emap: torch.Tensor) -> None:
+        """The host selection over the complete map (the same on every rank)."""
+        self._check(self.lib, self.ctx, self.lib.klt_hip_select_map(
+            self.ctx, self.W, self.H, C.byref(sd), mindist, min_eigenvalue, C.c_void_p(emap.data_ptr()),
+            C.c_void_p(self.x.data_ptr()), C.c_void_p(self.y.data_ptr()), C.c_void_p(self.v.data_ptr()),
+            self.x.numel()), "select_map")
+
+    def replace(self, sd, mindist: int, min_eigenvalue: int, broadcast) -> None:
+        """KLTReplaceLostFeatures between two run() calls: each rank's map rows
+        to every rank (broadcast(tensor, src) in place, torch.distributed.broadcast
+        in production), then the same selection everywhere."""
+        emap = self.replace_rows(sd)
+        _, nx, _, _, _ = self._map_rows(sd, 0, 0)
+        for r in range(self.world):
+            _, _, _, j0, j1 = self._map_rows(sd, *self.own_rows(r))
+            if j1 > j0:
+                part = emap[j0 * nx:j1 * nx]
+                broadcast(part, r)
+        self.replace_select(sd, mindist, min_eigenvalue, emap)

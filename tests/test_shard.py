@@ -464,3 +464,184 @@ def test_eigen_rows_of_band_pyramid(gpu, world, rank, margin):
         assert calls == [1] and torch.equal(got[rows], full_map[rows])
         gpu.klt_shard_destroy(s)
     gpu.KLTFreeTrackingContext(rk.tc)
+
+
+@pytest.mark.gpu
+def test_c_shard_errors(gpu):
+    """klt_shard.h error behaviour: bad geometry refused at create, a frame
+    height that differs from the shard's, an escaped chunk with no whole-frame
+    callback, and klt_shard_replace on a local shard (no peers) all fail with
+    a message, without touching the feature arrays."""
+    from kltamd.device import SelectDesc
+    frames = synth(gpu, 77, 640, 480, 3)
+    H, W = frames[0].shape
+    dev = torch.device("cuda", 0)
+    dfr = torch.from_numpy(np.ascontiguousarray(np.stack(frames))).to(dev)
+    rk = _Rank(gpu, dfr, H, W, 4, 1, 0)
+    assert not gpu.klt_shard_create_local(rk.ctx, 4, 4, H, 0)   # rank out of range
+    assert not gpu.klt_shard_create_local(rk.ctx, 0, 0, H, 0)   # no ranks
+    assert not gpu.klt_shard_create_local(rk.ctx, 0, 2, H, -1)  # negative margin
+    s = gpu.klt_shard_create_local(rk.ctx, 1, 4, H, 0)
+    assert s
+    x, y, v = (torch.from_numpy(a).to(dev) for a in _select(gpu, frames[0], 800))
+    x0, y0, v0 = x.clone(), y.clone(), v.clone()
+    ptrs = (C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()), x.numel())
+    assert gpu.klt_hip_frames_begin(rk.ctx, C.byref(rk.pd), C.c_void_p(dfr.data_ptr()), W) == 0
+    from kltamd.device import PyrDesc
+    bad = PyrDesc()
+    gpu.klt_amd_pyr_desc(rk.tc, W, H - 32, rk.tc.contents.nPyramidLevels, 1, C.byref(bad))
+    rc = gpu.klt_shard_track(s, C.byref(bad), C.byref(rk.td), C.c_void_p(dfr.data_ptr() + H * W), W, H * W, 2,
+                             None, 0, *ptrs, None, None)
+    assert rc < 0 and b"rows" in gpu.klt_shard_last_error(s)
+    # margin 0 over two frames: some owned feature's window leaves the band -> escape; no callback -> error
+    rc = gpu.klt_shard_track(s, C.byref(rk.pd), C.byref(rk.td), C.c_void_p(dfr.data_ptr() + H * W), W, H * W, 2,
+                             None, 0, *ptrs, None, None)
+    assert rc < 0 and b"callback" in gpu.klt_shard_last_error(s)
+    tc = rk.tc.contents
+    sd = SelectDesc(tc.window_width, tc.window_height, max(tc.borderx, 3), max(tc.bordery, 3), tc.nSkippedPixels)
+    x.copy_(x0), y.copy_(y0), v.copy_(v0)
+    rc = gpu.klt_shard_replace(s, C.byref(rk.pd), C.byref(sd), W, tc.mindist, tc.min_eigenvalue, *ptrs, None, None)
+    assert rc < 0 and b"local" in gpu.klt_shard_last_error(s)
+    assert torch.equal(x, x0) and torch.equal(v, v0)
+    gpu.klt_shard_destroy(s)
+    gpu.KLTFreeTrackingContext(rk.tc)
+
+
+# ---------------------------------------------------------------------------
+# GPU: kltamd.shard.ShardedSequence itself, one thread per rank on one GPU,
+# the collectives done by a thread group (sum / copy between the ranks' tensors)
+# ---------------------------------------------------------------------------
+class _ThreadGroup:
+    def __init__(self, world):
+        import threading
+        self.world, self.bar, self.slots, self.out = world, threading.Barrier(world), [None] * world, None
+
+    def all_reduce(self, rank, t):
+        torch.cuda.current_stream().synchronize()
+        self.slots[rank] = t
+        self.bar.wait()
+        if rank == 0:
+            acc = self.slots[0].clone()
+            for o in self.slots[1:]:
+                acc += o
+            torch.cuda.current_stream().synchronize()
+            self.out = acc
+        self.bar.wait()
+        t.copy_(self.out)
+        torch.cuda.current_stream().synchronize()
+        self.bar.wait()
+
+    def broadcast(self, rank, t, src):
+        torch.cuda.current_stream().synchronize()
+        if rank == src:
+            self.slots[src] = t
+        self.bar.wait()
+        if rank != src:
+            t.copy_(self.slots[src])
+            torch.cuda.current_stream().synchronize()
+        self.bar.wait()
+
+
+def threaded_sequence(gpu, frames, nfeat, world, chunk, margin, replace=False, band_only=False):
+    """frames[0] selects; world ShardedSequence ranks (threads, one context
+    each) track frames[1:] -- with replace: one frame per run() and
+    ShardedSequence.replace after each, as the REPLACE harness does."""
+    import threading
+    from kltamd.device import D2D, PyrDesc, SelectDesc, TrackDesc, check, use_torch_stream
+    from kltamd.shard import BandFrames, FullFrames, ShardedSequence, band_of
+    H, W = frames[0].shape
+    T = len(frames) - 1
+    dev = torch.device("cuda", 0)
+    dfr = torch.from_numpy(np.ascontiguousarray(np.stack(frames))).to(dev)
+    sel = _select(gpu, frames[0], nfeat)
+    grp = _ThreadGroup(world)
+    tcs = [gpu.KLTCreateTrackingContext() for _ in range(world)]
+    for tc in tcs:
+        tc.contents.sequentialMode = 1
+    ctxs = [gpu.klt_amd_device_context(tc) for tc in tcs]
+    out, errs, stats = [None] * world, [], [None] * world
+
+    def worker(rank):
+        try:
+            torch.cuda.set_device(dev)
+            ctx, tc = ctxs[rank], tcs[rank]
+            use_torch_stream(gpu, ctx, dev)
+            pd, td = PyrDesc(), TrackDesc()
+            gpu.klt_amd_pyr_desc(tc, W, H, tc.contents.nPyramidLevels, 1, C.byref(pd))
+            gpu.klt_amd_track_desc(tc, C.byref(td))
+            x, y, v = (torch.from_numpy(a).to(dev) for a in sel)
+            if band_only:
+                def load(t0, n, row0, nrows, dst, stride):
+                    part = dfr[t0:t0 + n, row0:row0 + nrows].contiguous()
+                    for f in range(n):
+                        check(gpu, ctx, gpu.klt_hip_memcpy(ctx, C.c_void_p(dst + f * stride),
+                                                           C.c_void_p(part[f].data_ptr()), nrows * W, D2D), "d2d")
+                    gpu.klt_hip_sync(ctx)
+                src = BandFrames(T + 1, H, W, band_of(H, world, rank, margin), load, dev)
+            else:
+                src = FullFrames(dfr)
+            seq = ShardedSequence(gpu, ctx, pd, td, src, x, y, v, rank, world, lambda t: grp.all_reduce(rank, t),
+                                  chunk=chunk, margin=margin)
+            seq.begin(0)
+            if replace:
+                c = tc.contents
+                sd = SelectDesc(c.window_width, c.window_height, max(c.borderx, c.window_width // 2),
+                                max(c.bordery, c.window_height // 2), c.nSkippedPixels)
+                for t in range(1, T + 1):
+                    seq.run(t, 1)
+                    seq.replace(sd, c.mindist, c.min_eigenvalue, lambda tt, s: grp.broadcast(rank, tt, s))
+            else:
+                seq.run(1, T)
+            torch.cuda.current_stream().synchronize()
+            out[rank] = (x.cpu().numpy(), y.cpu().numpy(), v.cpu().numpy())
+            stats[rank] = (seq.redone, seq.rebuilt)
+        except BaseException as e:  # surface in the main thread; release the others
+            errs.append(e)
+            grp.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=180)
+    for tc in tcs:
+        gpu.KLTFreeTrackingContext(tc)
+    if errs:
+        raise errs[0]
+    for r in range(1, world):  # every rank ends with the same list
+        for a, b in zip(out[0], out[r]):
+            assert np.array_equal(a.view(np.int32), b.view(np.int32))
+    return out[0], stats
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,chunk,margin,band_only", [(1, 4, 64, False), (3, 4, 64, False), (3, 3, 0, True),
+                                                         (4, 5, 40, True)])
+def test_sharded_sequence_threads_equal_oracle(gpu, oracle, world, chunk, margin, band_only):
+    from kltabi import OracleTracker
+    frames = synth(gpu, 2170 + world, 640, 480, 11)
+    (x, y, v), stats = threaded_sequence(gpu, frames, 1500, world, chunk, margin, band_only=band_only)
+    X, Y, V = OracleTracker(oracle).harness(frames, 1500, 11, first=frames[0])
+    k = 11 - 2
+    assert np.array_equal(v, V[:, k])
+    assert np.array_equal(x.view(np.int32), X[:, k].view(np.int32))
+    assert np.array_equal(y.view(np.int32), Y[:, k].view(np.int32))
+    if margin == 0:
+        assert stats[0][0] > 0  # chunks redone from whole frames
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,margin,band_only", [(1, 64, False), (3, 64, True), (4, 0, False)])
+def test_sharded_sequence_replace_equals_oracle(gpu, oracle, world, margin, band_only):
+    """ShardedSequence.replace after every frame (the REPLACE harness): the
+    ranks' trackability rows, broadcast per owner, and the same selection on
+    every rank equal the oracle's list bit for bit."""
+    from kltabi import OracleTracker
+    frames = synth(gpu, 3170 + world, 640, 480, 9)
+    (x, y, v), stats = threaded_sequence(gpu, frames, 800, world, 1, margin, replace=True, band_only=band_only)
+    X, Y, V = OracleTracker(oracle).harness(frames, 800, 9, first=frames[0], replace=True)
+    k = 9 - 2
+    assert (V[:, k] > 0).any()  # some slots hold replacements (val = their eigenvalue)
+    assert np.array_equal(v, V[:, k])
+    assert np.array_equal(x.view(np.int32), X[:, k].view(np.int32))
+    assert np.array_equal(y.view(np.int32), Y[:, k].view(np.int32))
