@@ -450,7 +450,7 @@ struct TrkCount {
 // trips instead of k+2.  The order of tests is the reference's: window test
 // at the top of each iteration and once after the loop (same x2, same test),
 // SMALL_DET ends the loop before x2 moves, residue only for TRACKED.
-template <int G, int PPL, bool PATCH, int WIN, bool EXACT, bool LI>
+template <int G, int PPL, bool PATCH, int WIN, bool EXACT, bool LI, bool BAND>
 __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, PATCH, WIN> &w, const TrkLevel &A,
                              const TrkLevel &B, float x1, float y1, float &x2, float &y2, bool live, int lane,
                              float *red, bool residue, ResCarry<PPL> &rc, bool job, bool defer, const TrkLevel &R,
@@ -477,7 +477,7 @@ __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, 
       status = kOOB;
       act = false;
     }
-    if (a.escape && act) {
+    if (BAND && act) {
       // band-built pyramids: every row the bilinear window touches must exist
       const bool bad = (int)(y2 - hh) < B.vlo || (int)(y2 + hh) + 1 >= B.vhi ||
                        (first && ((int)(y1 - hh) < A.vlo || (int)(y1 + hh) + 1 >= A.vhi));
@@ -654,7 +654,7 @@ __device__ int track_level_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, 
 }
 
 // one frame of KLTTrackFeatures for the feature of this lane's group (:1348-1437)
-template <int G, int PPL, bool PATCH, int WIN, bool EXACT, bool LI, class LevA, class LevB>
+template <int G, int PPL, bool PATCH, int WIN, bool EXACT, bool LI, bool BAND, class LevA, class LevB>
 __device__ __forceinline__ void track_feature_g(PROF_DECL const TrkArgs &a, const GroupWin<G, PPL, PATCH, WIN> &w,
                                                 LevA LA,
                                                 LevB LB,
@@ -685,7 +685,7 @@ __device__ __forceinline__ void track_feature_g(PROF_DECL const TrkArgs &a, cons
     }
     const bool lj = job && r == a.nlev - 1;
     PROF_T(t_l0);
-    const int v = track_level_g<G, PPL, PATCH, WIN, EXACT, LI>(PROF_ARG a, w, LA(r), LB(r), xl, yl, xo, yo, go,
+    const int v = track_level_g<G, PPL, PATCH, WIN, EXACT, LI, BAND>(PROF_ARG a, w, LA(r), LB(r), xl, yl, xo, yo, go,
                                                                lane, red, r == 0, rc, lj, defer && r == 0, R,
                                                                rstat, cnt);
     PROF_ADD(10, t_l0);
@@ -714,7 +714,8 @@ __device__ __forceinline__ void track_feature_g(PROF_DECL const TrkArgs &a, cons
   }
 }
 
-template <int G, int PPL, bool PATCH, int WIN, bool EXACT, bool LI>
+// BAND: band-built pyramids (klt_hip_track_frames_band) -- the escape checks
+template <int G, int PPL, bool PATCH, int WIN, bool EXACT, bool LI, bool BAND>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KLT_TRACK_WAVES))) void k_track_frames_g(TrkArgs a, TrkFramesArgs b, float *__restrict__ fx,
                                                            float *__restrict__ fy, int *__restrict__ fv, int n) {
   constexpr int LG = kWave / G;
@@ -768,7 +769,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KLT_TRAC
     PROF_T(t_f0);
     if (wave_any(live)) {
       auto LA = [&](int r) { return j == 0 ? a.A[r] : at_frame(a.B[r], (long)(j - 1) * b.lfs[r]); };
-      track_feature_g<G, PPL, PATCH, WIN, EXACT, LI>(
+      track_feature_g<G, PPL, PATCH, WIN, EXACT, LI, BAND>(
           PROF_ARG a, w, LA, [&](int r) { return at_frame(a.B[r], (long)j * b.lfs[r]); }, x, y, v, live, lane,
           red_all[wave], rc, job, merge && j + 1 < b.nframes, LA(0), rstat, cnt);
     }
@@ -852,19 +853,22 @@ __global__ __launch_bounds__(kSortThreads) void k_band_order(const float *__rest
   }
 }
 
-template <int G, int PPL, bool PATCH, int WIN, bool EXACT, bool LI>
+template <int G, int PPL, bool PATCH, int WIN, bool EXACT, bool LI, bool BAND = true>
 void launch_g(hipStream_t st, const TrkArgs &a, const TrkFramesArgs &b, float *x, float *y, int *v, int n) {
   const int per = (kBlock / kWave) * G;  // features per workgroup
   const int nb = (n + per - 1) / per;
   const int grid = b.xcd_per > 0 ? 8 * b.xcd_per : nb;
-  hipLaunchKernelGGL((k_track_frames_g<G, PPL, PATCH, WIN, EXACT, LI>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y,
+  hipLaunchKernelGGL((k_track_frames_g<G, PPL, PATCH, WIN, EXACT, LI, BAND>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y,
                      v, n);
 }
 
 template <bool EXACT, bool LI>
 void launch_sel(bool patch, bool win7, int npx, hipStream_t st, const TrkArgs &a, const TrkFramesArgs &b, float *x,
                 float *y, int *v, int n) {
-  if (patch && win7) launch_g<1, 1, true, 7, EXACT, LI>(st, a, b, x, y, v, n);
+  // the default configuration has an instance without the band checks (its
+  // escape test and the spilled scalar registers it costs: -1.5..3 % per frame)
+  if (patch && win7 && !a.escape) launch_g<1, 1, true, 7, EXACT, LI, false>(st, a, b, x, y, v, n);
+  else if (patch && win7) launch_g<1, 1, true, 7, EXACT, LI>(st, a, b, x, y, v, n);
   else if (patch) launch_g<1, 1, true, 0, EXACT, LI>(st, a, b, x, y, v, n);
   else if (win7) launch_g<1, 1, false, 7, EXACT, LI>(st, a, b, x, y, v, n);
   else if (npx <= kWave) launch_g<1, 1, false, 0, EXACT, LI>(st, a, b, x, y, v, n);
