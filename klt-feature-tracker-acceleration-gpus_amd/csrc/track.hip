@@ -358,6 +358,38 @@ __device__ __forceinline__ void residue_sample(const TrkLevel &R, const GroupWin
   residue_direct(R, w, rx, ry, r_b);
 }
 
+// The lane patch's rare per-pixel fallback, one plane at a time: each plane's
+// corners are loaded and interpolated before the next plane's loads go out, so
+// the fallback's register peak stays below the patch path's (with all six
+// planes' corners in flight it set the kernel's allocation and cost 5-9 % on
+// every pass); the extra round trips are paid only in the passes that need it.
+__device__ __forceinline__ float direct_one(const float *__restrict__ P, const Bil &q, unsigned w, bool on) {
+  float r = sel(on, corner_interp(q, corner_load(P, q, w)));
+  asm volatile("" : "+v"(r));  // complete before the next plane's loads are issued
+  return r;
+}
+
+template <int G, int PPL, bool PATCH, int WIN>
+__device__ __forceinline__ void gather_direct_seq(const TrkLevel &A, const TrkLevel &B,
+                                                  const GroupWin<G, PPL, PATCH, WIN> &w, float x1, float y1,
+                                                  float x2, float y2, bool first, bool grads, float (&a_im)[PPL],
+                                                  float (&a_gx)[PPL], float (&a_gy)[PPL], float (&b_im)[PPL],
+                                                  float (&b_gx)[PPL], float (&b_gy)[PPL]) {
+#pragma unroll
+  for (int k = 0; k < PPL; ++k) {
+    const Bil qb = bil_at(B.w, B.h, x2 + w.oi[k], y2 + w.oj[k]);
+    b_im[k] = direct_one(B.img, qb, B.w, w.on[k]);
+    b_gx[k] = grads ? direct_one(B.gx, qb, B.w, w.on[k]) : 0.0f;
+    b_gy[k] = grads ? direct_one(B.gy, qb, B.w, w.on[k]) : 0.0f;
+    if (first) {
+      const Bil qa = bil_at(A.w, A.h, x1 + w.oi[k], y1 + w.oj[k]);
+      a_im[k] = direct_one(A.img, qa, A.w, w.on[k]);
+      a_gx[k] = direct_one(A.gx, qa, A.w, w.on[k]);
+      a_gy[k] = direct_one(A.gy, qa, A.w, w.on[k]);
+    }
+  }
+}
+
 template <int G, int PPL, bool PATCH, int WIN>
 __device__ __forceinline__ void gather_pass(const TrkLevel &A, const TrkLevel &B, const GroupWin<G, PPL, PATCH, WIN> &w,
                                             float x1, float y1, float x2, float y2, bool first, bool grads,
@@ -408,7 +440,8 @@ __device__ __forceinline__ void gather_pass(const TrkLevel &A, const TrkLevel &B
     }
   }
   pc.valid = false;
-  gather_direct2(A, B, w, x1, y1, x2, y2, first, grads, a_im, a_gx, a_gy, b_im, b_gx, b_gy);
+  if constexpr (PATCH) gather_direct_seq(A, B, w, x1, y1, x2, y2, first, grads, a_im, a_gx, a_gy, b_im, b_gx, b_gy);
+  else gather_direct2(A, B, w, x1, y1, x2, y2, first, grads, a_im, a_gx, a_gy, b_im, b_gx, b_gy);
   if (rjob) {
     float t[PPL];
     residue_direct(*R, w, rx, ry, t);
