@@ -54,6 +54,7 @@ klt_shard *klt_shard_create(klt_hip_ctx *ctx, int rank, int world, const unsigne
    0 elsewhere) and redoes a chunk only when this rank escaped.  The caller
    sums the ranks' int32 bit patterns to get the merged list. */
 klt_shard *klt_shard_create_local(klt_hip_ctx *ctx, int rank, int world, int nrows, int margin);
+/* before the tracking context that owns ctx is freed (it synchronizes ctx) */
 void klt_shard_destroy(klt_shard *s);
 const char *klt_shard_last_error(klt_shard *s);
 /* rows [*lo, *hi) of every frame this rank's band build reads: the only rows
