@@ -65,6 +65,10 @@ def parse():
                         "per exchange, 64; "
                         "capped at ceil(steps/2) so that the timed region always holds >= 2 chunks and the "
                         "overlapped schedule really runs); 0 = the per-frame pipelined path (klt_hip_track_sequence)")
+    p.add_argument("--replay-frames", type=int, default=489,
+                   help="frames of the per-kernel event replay and the tracker-count replay (at least --steps); "
+                        "they run at the production chunk (--chunk, default 64) whatever --steps caps the timed "
+                        "region's chunk at")
     p.add_argument("--api-frames", type=int, default=200,
                    help="host frames for the klt.h API legs (KLTTrackFeatures per call, KLTTrackSequence); "
                         "rank 0, N=1; 0 = skip")
@@ -116,7 +120,12 @@ def main() -> None:
     lib = kltamd.load()
     lib.KLTSetVerbosity(0)
     W, H, NF = args.width, args.height, args.features
-    nframes = 1 + args.warmup + args.steps
+    # the timed region covers `steps` frames; the event and count replays cover
+    # `replay` frames at the production chunk, so that the roofline and tracker
+    # lines measure 64-frame launches even when --steps caps the timed chunk
+    replay = max(args.steps, args.replay_frames)
+    rchunk = args.chunk_requested
+    nframes = 1 + args.warmup + replay
     seed = args.seed + rank
 
     tc = lib.KLTCreateTrackingContext()
@@ -161,11 +170,12 @@ def main() -> None:
               "build")
         slot.value = 0
 
-    def run(t0, n):
-        if args.chunk > 0:
+    def run(t0, n, chunk=None):
+        chunk = args.chunk if chunk is None else chunk
+        if chunk > 0:
             tp = [C.c_void_p(a.data_ptr() + a.element_size() * t0 * NF) for a in tab]
             check(lib, ctx, lib.klt_hip_track_frames(ctx, C.byref(pd), C.byref(td), C.c_void_p(fptr + t0 * W * H),
-                                                     W, W * H, n, args.chunk, C.c_void_p(x.data_ptr()),
+                                                     W, W * H, n, chunk, C.c_void_p(x.data_ptr()),
                                                      C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()), NF,
                                                      tp[0], tp[1], tp[2], NF), "track_frames")
             return
@@ -193,31 +203,34 @@ def main() -> None:
     live_after = int((v >= 0).sum().item())
 
     tm = Timing()
+    exact_tab = [t[t_start - 1:t_start - 1 + args.steps].clone() for t in tab]
     if not timed_events:
-        # replay the same frames from the same state with events on, on one
-        # stream: each kernel's duration is then its own (the roofline), not
-        # time shared with a kernel overlapping it on the other stream
+        # replay from the same state with events on, on one stream, at the
+        # production chunk over `replay` frames: each kernel's duration is then
+        # its own (the roofline), not time shared with a kernel overlapping it
+        # on the other stream, and the launches are 64-frame launches
         x.copy_(xs); y.copy_(ys); v.copy_(vs)
         check(lib, ctx, lib.klt_hip_set_frames_overlap(ctx, 0), "overlap")
         build0(t_start - 1)
         lib.klt_hip_set_timing(ctx, 1)
-        run(t_start, args.steps)
+        run(t_start, replay, rchunk)
     check(lib, ctx, lib.klt_hip_get_timing(ctx, C.byref(tm)), "timing")
     lib.klt_hip_set_timing(ctx, 0)
     tracker = None
-    exact_tab = [t[t_start - 1:t_start - 1 + args.steps].clone() for t in tab]
     if args.chunk > 0:
         # tracker work counters (Newton iterations, gather passes) in a replay
-        # of their own, so that neither timed run carries the counting atomics
+        # of their own over the same frames and chunk as the event replay, so
+        # that no timed run carries the counting atomics
         x.copy_(xs); y.copy_(ys); v.copy_(vs)
         build0(t_start - 1)
         check(lib, ctx, lib.klt_hip_set_track_count(ctx, 1), "track_count")
-        run(t_start, args.steps)
+        nrep = args.steps if timed_events else replay
+        run(t_start, nrep, args.chunk if timed_events else rchunk)
         solves, passes = C.c_ulonglong(0), C.c_ulonglong(0)
         check(lib, ctx, lib.klt_hip_get_track_count(ctx, C.byref(solves), C.byref(passes), 0), "track_count")
         lib.klt_hip_set_track_count(ctx, 0)
         # feature-frames: features live when frame j starts (table row j-1 holds the list after j-1)
-        ff = int((tab[2][t_start - 1:t_start - 1 + args.steps] >= 0).sum().item())
+        ff = int((tab[2][t_start - 1:t_start - 1 + nrep] >= 0).sum().item())
         tracker = tracker_line(solves.value, passes.value, ff, tm)
         pmc = ROOT / "profiles" / "pmc_tracker.json"
         if pmc.exists():
@@ -290,6 +303,9 @@ def main() -> None:
         "pyramid_gpix_s": (px / (pass_us * 1e-6) / 1e9) if pass_us else None,
         "kernels_us_per_launch": {"k_pyr_l0": l0, "k_pyr_l1": l1, "k_track": trk, "generic_pass": gen},
         "kernels_us_per_frame": {"k_pyr_l0": l0f, "k_pyr_l1": l1f, "k_track": trkf},
+        "replay": {"frames": replay if not timed_events else args.steps,
+                   "chunk": rchunk if not timed_events else args.chunk,
+                   "what": "per-kernel HIP events and tracker counters come from replays of this length and chunk"},
         "frames_per_launch": fpl,
         "live_features": {"after_warmup": live_before, "at_end": live_after},
     }
@@ -309,19 +325,10 @@ def main() -> None:
             "k_pyr_l0": {"achieved": (l0_bytes / (l0f * 1e-6) / 1e9) if l0f else None,
                          "algorithmic_bytes_per_frame": l0_bytes},
             "event_timing": "timed region" if timed_events else
-                            "replay of the timed region on one stream (each kernel's own duration)",
+                            f"replay on one stream from the timed region's start state: {replay} frames at chunk "
+                            f"{rchunk} (each kernel's own duration, production launch length)",
         }
-        pmc = ROOT / "profiles" / "pmc_latest.json"
-        if pmc.exists():
-            try:
-                d = json.loads(pmc.read_text())
-                if d.get("resolution") == f"{W}x{H}":
-                    # per launch, like `achieved` (a launch covers frames_per_launch frames)
-                    result["roofline"]["traffic"] = d["pass_hbm_bytes_per_frame"] * fpl
-                    result["roofline"]["traffic_per_frame"] = d["pass_hbm_bytes_per_frame"]
-                    result["roofline"]["traffic_source"] = str(pmc.relative_to(ROOT))
-            except Exception:
-                pass
+        attach_traffic(result["roofline"], ROOT / "profiles" / "pmc_latest.json", f"{W}x{H}", fpl)
 
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"], result["parity"] = cpu_leg(lib, frames, W, H, NF, args, tc, ctx, dev)
@@ -333,6 +340,8 @@ def main() -> None:
     del frames, tab
     if rank == 0 and world == 1 and not args.no_4k:
         result["roofline_4k"] = pass_4k(lib, dev)
+        attach_traffic(result["roofline_4k"], ROOT / "profiles" / "pmc_4k_latest.json", "3840x2160",
+                       result["roofline_4k"]["frames_per_launch"])
     if rank == 0 and world == 1:
         # the fraction also against a measured copy peak
         mp = measured_peaks(dev)
@@ -450,6 +459,10 @@ def pass_4k(lib, dev, chunk=64, reps=2):
     import torch
     from kltamd.device import PyrDesc, TrackDesc, Timing, check, use_torch_stream
     W, H = 3840, 2160
+    # the earlier legs' parked device contexts and torch's cached blocks go
+    # back to the driver first, so the 4K banks are not laid out in their holes
+    lib.klt_amd_release_cached_devices()
+    torch.cuda.empty_cache()
     tc = lib.KLTCreateTrackingContext()
     ctx = lib.klt_amd_device_context(tc)
     use_torch_stream(lib, ctx, dev)
@@ -481,10 +494,33 @@ def pass_4k(lib, dev, chunk=64, reps=2):
     ach = by / ((l0 + l1) * 1e-6) / 1e9
     return {"workload": f"{W}x{H} pyramid pass, batched {chunk} frames per launch, pyramids only",
             "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "traffic": None, "frames_per_launch": tm.frames_pyr_l0 / tm.n_pyr_l0,
             "algorithmic_bytes_per_frame": by, "us_per_frame": l0 + l1,
             "kernels_us_per_frame": {"k_pyr_l0": l0, "k_pyr_l1": l1}, "frames_timed": int(tm.frames_pyr_l0),
             "pyramid_gpix_s": W * H / ((l0 + l1) * 1e-6) / 1e9,
             "event_timing": "HIP events on the launch stream, one stream"}
+
+
+def attach_traffic(line, pmc, resolution, fpl) -> None:
+    """roofline.traffic: HBM bytes per launch from the committed PMC summary of
+    the same kernels (tools/pmc_traffic.sh + tools/pmc_traffic_json.py), when
+    it was taken at this resolution.  Static: rocprofv3 counters cannot be
+    read from inside this process."""
+    if not pmc.exists():
+        return
+    try:
+        d = json.loads(pmc.read_text())
+    except ValueError:
+        return
+    if d.get("resolution") != resolution:
+        return
+    line["traffic"] = d["pass_hbm_bytes_per_frame"] * fpl  # per launch, like `achieved`
+    line["traffic_per_frame"] = d["pass_hbm_bytes_per_frame"]
+    line["traffic_over_algorithmic"] = d["pass_hbm_bytes_per_frame"] / d["pass_algorithmic_bytes_per_frame"]
+    line["traffic_source"] = str(pmc.relative_to(ROOT))
+    line["traffic_kind"] = ("static: FETCH_SIZE (x2, gfx950) + WRITE_SIZE from separate rocprofv3 --pmc passes over "
+                            f"the same kernels at {resolution}, {d.get('frames_per_launch', '?')} frames per launch "
+                            "(tools/pmc_traffic.sh); counters cannot be read inside this process")
 
 
 def schedule_name(args) -> str:
@@ -523,7 +559,7 @@ def fast_leg(lib, ctx, td, tab, exact_tab, xs, ys, vs, x, y, v, build0, run, t_s
         check(lib, ctx, lib.klt_hip_set_frames_overlap(ctx, 0), "overlap")
         build0(t_start - 1)
         lib.klt_hip_set_timing(ctx, 1)
-        run(t_start, args.steps)
+        run(t_start, max(args.steps, args.replay_frames), args.chunk_requested)  # as the exact line's replay
         tm = Timing()
         check(lib, ctx, lib.klt_hip_get_timing(ctx, C.byref(tm)), "timing")
         lib.klt_hip_set_timing(ctx, 0)

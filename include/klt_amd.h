@@ -17,6 +17,10 @@ extern "C" {
 
 /* the device context behind a tracking context (created on first use) */
 klt_hip_ctx *klt_amd_device_context(KLT_TrackingContext tc);
+/* Device contexts of freed tracking contexts are parked (at most 4, each
+   trimmed to 2 GiB) for the next KLTCreateTrackingContext on the same device.
+   This destroys the parked ones and returns their memory; returns how many. */
+int klt_amd_release_cached_devices(void);
 /* the descriptors KLTTrackFeatures would build for this context */
 void klt_amd_pyr_desc(KLT_TrackingContext tc, int ncols, int nrows, int nlevels, int smooth,
                       klt_hip_pyr_desc *desc);

@@ -100,8 +100,10 @@ typedef struct klt_hip_ctx klt_hip_ctx;
 /* device < 0: the calling thread's current HIP device */
 klt_hip_ctx *klt_hip_ctx_create(int device);
 void klt_hip_ctx_destroy(klt_hip_ctx *ctx);
-/* back to a fresh context's settings (own stream, default tuning, no timing
-   or counters, no current pyramid), keeping its allocations for reuse */
+/* back to a fresh context's settings (own stream, default tuning and host
+   threads, no timing or counters, no current pyramid), after its own streams
+   drain; it keeps its allocations for reuse unless they exceed 2 GiB, in which
+   case the pyramid banks, the upload ring and the pinned staging are freed */
 int klt_hip_ctx_reset(klt_hip_ctx *ctx);
 int klt_hip_ctx_device(klt_hip_ctx *ctx);
 /* the calling thread's current HIP device, -1 on error */
@@ -154,6 +156,20 @@ int klt_hip_set_prof(klt_hip_ctx *ctx, void *dev);
 /* host threads of klt_hip_track_frames_host besides the caller (frame copies
    into pinned staging, table-row delivery); 0..16, default 7 */
 int klt_hip_set_host_threads(klt_hip_ctx *ctx, int workers);
+int klt_hip_get_host_threads(klt_hip_ctx *ctx);
+/* Byte budget of the three pyramid banks of klt_hip_track_frames* (one device
+   arena per context; 0 restores the default: a quarter of the device memory,
+   at most 64 GiB).  A klt_hip_track_frames call whose chunk does not fit runs
+   with the largest chunk that does (results do not depend on the chunk); a
+   klt_hip_track_frames_band call fails instead, before allocating.  Either
+   fails cleanly when not even one frame fits, or when the arena exceeds the
+   device's free memory. */
+int klt_hip_set_bank_budget(klt_hip_ctx *ctx, size_t bytes);
+size_t klt_hip_get_bank_budget(klt_hip_ctx *ctx);
+/* frames per bank (launch) of the last klt_hip_track_frames* call */
+int klt_hip_frames_chunk(klt_hip_ctx *ctx);
+/* device bytes the context holds (pyramid slots, banks, upload ring, maps) */
+size_t klt_hip_ctx_footprint(klt_hip_ctx *ctx);
 /* klt_hip_track_frames scheduling: 1 builds chunk c+1's pyramids on a second
    stream while chunk c is tracked; 0 (default) runs both on the context stream. */
 int klt_hip_set_frames_overlap(klt_hip_ctx *ctx, int overlap);

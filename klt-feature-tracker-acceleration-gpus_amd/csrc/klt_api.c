@@ -105,6 +105,19 @@ static void release_device(klt_hip_ctx *dev)
   if (!kept) klt_hip_ctx_destroy(dev);
 }
 
+int klt_amd_release_cached_devices(void)
+{
+  klt_hip_ctx *park[DEV_CACHE];
+  int i, n;
+  pthread_mutex_lock(&g_dev_lock);
+  n = g_dev_nfree;
+  for (i = 0; i < n; i++) park[i] = g_dev_free[i];
+  g_dev_nfree = 0;
+  pthread_mutex_unlock(&g_dev_lock);
+  for (i = 0; i < n; i++) klt_hip_ctx_destroy(park[i]);
+  return n;
+}
+
 static void dev_check(KLT_TrackingContext tc, int rc, const char *what)
 {
   if (rc != 0) KLTError("(KLT) %s failed: %s", what, klt_hip_last_error(FULL(tc)->dev));

@@ -183,7 +183,11 @@ struct klt_hip_ctx {
   HostPool *pool = nullptr;
   int copy_threads = 7;  // pool workers besides the caller (0: the caller alone)
   unsigned long long *prof = nullptr;  // instrumented build: per-wave tracker phase counters
-  Bank bank[3];
+  Bank bank[3];  // views into bank_arena
+  void *bank_arena = nullptr;
+  size_t bank_arena_bytes = 0;
+  size_t bank_budget = 0;  // bytes the bank arena may take (klt_hip_set_bank_budget; 0: the default)
+  int chunk_used = 0;      // frames per bank of the last klt_hip_track_frames* call (budget-capped)
   int bank_next = 0;
   // band mode: a bank whose pyramids were built ahead, during the previous
   // call's tracking (klt_hip_track_frames_band's next_frames); -1: none
@@ -532,41 +536,150 @@ int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc
   return launched(c, "k_track_frames", launch_track_frames(st, exact, li, patch, win7, npx, aa, b2, x, y, v, n));
 }
 
-// allocate bank k for `frames` pyramids shaped like desc d
-int ensure_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, int frames) {
+// The three banks live in one device arena per context: for each bank, level
+// l's img | gx | gy planes (each `frames` pyramids long) and the sigma-3.6 row
+// pass, every plane on a 64 KiB boundary.  One allocation instead of 21 keeps
+// the physical placement of the banks independent of what the process
+// allocated and freed before: separate plane allocations made after a smaller
+// context's banks were freed ran the 4K pass 7 % slower (staggering
+// the planes' offsets by 256 B .. 16 KiB changed nothing).
+size_t bank_plane_floats(const klt_hip_pyr_desc *d, int l, int frames) {
   int w = d->ncols, h = d->nrows;
-  K.nlev = d->nlevels;
-  K.ss = d->nlevels > 1 ? d->subsampling : 1;
-  for (int l = 0; l < d->nlevels; ++l) {
-    Level &L = K.lv[l];
-    L.w = w;
-    L.h = h;
-    const size_t need = (size_t)(w > 0 ? w : 1) * (h > 0 ? h : 1) * frames;
-    if (L.cap < need || !L.img) {
-      hipFree(L.img);
-      hipFree(L.gx);
-      hipFree(L.gy);
+  for (int k = 0; k < l; ++k) {
+    w /= d->subsampling;
+    h /= d->subsampling;
+  }
+  return (size_t)(w > 0 ? w : 1) * (h > 0 ? h : 1) * frames;
+}
+
+size_t bank_hs_floats(const klt_hip_pyr_desc *d, int frames) {
+  const int W1 = d->nlevels == 2 ? d->ncols / d->subsampling : 0;
+  return d->nlevels == 2 ? (size_t)hs_size(W1 > 0 ? W1 : 1, d->nrows) * frames : 0;
+}
+
+constexpr size_t kPlaneAlign = 64 << 10;
+
+size_t bank_arena_bytes(const klt_hip_pyr_desc *d, int frames) {
+  size_t total = 0;
+  auto add = [&](size_t floats) { total = (total + kPlaneAlign - 1) / kPlaneAlign * kPlaneAlign + floats * sizeof(float); };
+  for (int b = 0; b < 3; ++b) {
+    for (int l = 0; l < d->nlevels; ++l)
+      for (int p = 0; p < 3; ++p) add(bank_plane_floats(d, l, frames));
+    if (d->nlevels == 2) add(bank_hs_floats(d, frames));
+  }
+  return total;
+}
+
+size_t env_size(const char *name, size_t dflt) {
+  const char *v = getenv(name);
+  return v && *v ? (size_t)strtoull(v, nullptr, 10) : dflt;
+}
+
+void free_banks(klt_hip_ctx *c) {
+  for (auto &K : c->bank) {
+    for (auto &L : K.lv) {
+      if (!c->bank_arena) {
+        hipFree(L.img);
+        hipFree(L.gx);
+        hipFree(L.gy);
+      }
       L.img = L.gx = L.gy = nullptr;
       L.cap = 0;
-      HIPCHK(c, hipMalloc((void **)&L.img, need * sizeof(float)));
-      HIPCHK(c, hipMalloc((void **)&L.gx, need * sizeof(float)));
-      HIPCHK(c, hipMalloc((void **)&L.gy, need * sizeof(float)));
-      L.cap = need;
     }
-    w /= K.ss;
-    h /= K.ss;
+    if (!c->bank_arena) hipFree(K.hs);
+    K.hs = nullptr;
+    K.hs_cap = 0;
+    K.frames = 0;
   }
-  if (d->nlevels == 2) {
-    const size_t need = (size_t)hs_size(K.lv[1].w > 0 ? K.lv[1].w : 1, d->nrows) * frames;
-    if (K.hs_cap < need || !K.hs) {
-      hipFree(K.hs);
-      K.hs = nullptr;
-      K.hs_cap = 0;
-      HIPCHK(c, hipMalloc((void **)&K.hs, need * sizeof(float)));
-      K.hs_cap = need;
+  hipFree(c->bank_arena);
+  c->bank_arena = nullptr;
+  c->bank_arena_bytes = 0;
+}
+
+// Default bank budget: a quarter of the device's memory, at most 64 GiB --
+// three 64-frame banks of 4K pyramids take 21 GB, of 1080p 5.3 GB.
+size_t bank_budget_of(klt_hip_ctx *c) {
+  if (c->bank_budget) return c->bank_budget;
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess || tot == 0) tot = (size_t)64 << 30;
+  const size_t q = tot / 4, cap = (size_t)64 << 30;
+  return q < cap ? q : cap;
+}
+
+// the largest chunk whose three banks fit the budget (0: not even one frame)
+int budget_chunk(klt_hip_ctx *c, const klt_hip_pyr_desc *d) {
+  const size_t budget = bank_budget_of(c), one = bank_arena_bytes(d, 1);
+  if (one > budget) return 0;
+  int lo = 1, hi = 1 << 16;
+  while (lo < hi) {  // bank_arena_bytes grows with frames
+    const int mid = lo + (hi - lo + 1) / 2;
+    if (bank_arena_bytes(d, mid) <= budget) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// (re)lay out the three banks for `frames` pyramids shaped like desc d.  The
+// caller has drained both streams.
+int ensure_banks(klt_hip_ctx *c, const klt_hip_pyr_desc *d, int frames) {
+  const bool arena = env_size("KLT_BANK_ARENA", 1) != 0;  // 0: the old per-plane allocations (A/B only)
+  const size_t need = bank_arena_bytes(d, frames);
+  if (!arena || need > c->bank_arena_bytes || !c->bank_arena) free_banks(c);
+  if (!arena) {  // one allocation per plane (the round-1/2 layout; experiments only)
+    for (auto &K : c->bank) {
+      for (int l = 0; l < d->nlevels; ++l) {
+        const size_t n = bank_plane_floats(d, l, frames);
+        HIPCHK(c, hipMalloc((void **)&K.lv[l].img, n * sizeof(float)));
+        HIPCHK(c, hipMalloc((void **)&K.lv[l].gx, n * sizeof(float)));
+        HIPCHK(c, hipMalloc((void **)&K.lv[l].gy, n * sizeof(float)));
+      }
+      if (d->nlevels == 2) HIPCHK(c, hipMalloc((void **)&K.hs, bank_hs_floats(d, frames) * sizeof(float)));
     }
+  } else if (!c->bank_arena) {
+    size_t fr = 0, tot = 0;
+    HIPCHK(c, hipMemGetInfo(&fr, &tot));
+    if (need > fr)
+      return fail(c, "track_frames: the bank arena for %d-frame chunks of %dx%d needs %zu bytes, %zu free on the device",
+                  frames, d->ncols, d->nrows, need, fr);
+    // physically contiguous when the driver can (experiment hook KLT_BANK_CONTIG=1)
+    if (!(env_size("KLT_BANK_CONTIG", 0) &&
+          hipExtMallocWithFlags(&c->bank_arena, need, hipDeviceMallocContiguous) == hipSuccess)) {
+      (void)hipGetLastError();
+      c->bank_arena = nullptr;
+      HIPCHK(c, hipMalloc(&c->bank_arena, need));
+    }
+    c->bank_arena_bytes = need;
   }
-  K.frames = frames;
+  size_t off = 0;
+  auto take = [&](size_t floats) {
+    off = (off + kPlaneAlign - 1) / kPlaneAlign * kPlaneAlign;
+    float *p = reinterpret_cast<float *>(static_cast<char *>(c->bank_arena) + off);
+    off += floats * sizeof(float);
+    return p;
+  };
+  for (auto &K : c->bank) {
+    int w = d->ncols, h = d->nrows;
+    K.nlev = d->nlevels;
+    K.ss = d->nlevels > 1 ? d->subsampling : 1;
+    for (int l = 0; l < d->nlevels; ++l) {
+      Level &L = K.lv[l];
+      L.w = w;
+      L.h = h;
+      L.cap = bank_plane_floats(d, l, frames);
+      if (arena) {
+        L.img = take(L.cap);
+        L.gx = take(L.cap);
+        L.gy = take(L.cap);
+      }
+      w /= K.ss;
+      h /= K.ss;
+    }
+    if (d->nlevels == 2) {
+      K.hs_cap = bank_hs_floats(d, frames);
+      if (arena) K.hs = take(K.hs_cap);
+    }
+    K.frames = frames;
+  }
   return 0;
 }
 
@@ -662,14 +775,7 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
     if (c->u8_done[i]) hipEventDestroy(c->u8_done[i]);
     hipFree(c->d_tmp[i]);
   }
-  for (auto &K : c->bank) {
-    for (auto &L : K.lv) {
-      hipFree(L.img);
-      hipFree(L.gx);
-      hipFree(L.gy);
-    }
-    hipFree(K.hs);
-  }
+  free_banks(c);
   for (int k = 0; k < 3; ++k) {
     if (c->ev_bbuilt[k]) hipEventDestroy(c->ev_bbuilt[k]);
     if (c->ev_bfree[k]) hipEventDestroy(c->ev_bfree[k]);
@@ -724,10 +830,53 @@ KLT_API int klt_hip_current_device(void) {
 
 KLT_API int klt_hip_ctx_device(klt_hip_ctx *c) { return c ? c->device : -1; }
 
+// Device bytes a cached context keeps at most (klt_hip_ctx_reset): larger
+// bank arenas, upload rings and staging are freed when it is parked.
+constexpr size_t kKeepBytes = (size_t)2 << 30;
+
+KLT_API size_t klt_hip_ctx_footprint(klt_hip_ctx *c) {
+  if (!c) return 0;
+  size_t b = c->bank_arena_bytes + c->ring_cap + c->drows_cap + c->hs_cap * sizeof(float) +
+             c->eig_cap * sizeof(int) + c->u8_cap * 2 + (c->tmp_cap[0] + c->tmp_cap[1]) * sizeof(float);
+  for (const auto &S : c->slot)
+    for (const auto &L : S.lv) b += 3 * L.cap * sizeof(float);
+  if (!c->bank_arena)
+    for (const auto &K : c->bank) {
+      for (const auto &L : K.lv) b += 3 * L.cap * sizeof(float);
+      b += K.hs_cap * sizeof(float);
+    }
+  return b;
+}
+
 KLT_API int klt_hip_ctx_reset(klt_hip_ctx *c) {
   if (!c) return -1;
   if (use_device(c)) return -1;
-  HIPCHK(c, hipDeviceSynchronize());  // nothing of the previous owner is still running
+  // nothing of the previous owner is still running: the context's own streams
+  // (a caller's stream set with klt_hip_set_stream is the caller's to drain)
+  for (hipStream_t st : {c->stream, c->own, c->pstream, c->cstream, c->dstream})
+    if (st) HIPCHK(c, hipStreamSynchronize(st));
+  if (klt_hip_ctx_footprint(c) > kKeepBytes) {
+    free_banks(c);
+    hipFree(c->d_ring);
+    hipFree(c->d_rows);
+    c->d_ring = nullptr;
+    c->d_rows = nullptr;
+    c->ring_cap = c->drows_cap = 0;
+    if (c->h_stage) hipHostFree(c->h_stage);
+    if (c->h_rows) hipHostFree(c->h_rows);
+    c->h_stage = nullptr;
+    c->h_rows = nullptr;
+    c->stage_cap = c->hrows_cap = 0;
+    c->prev = PrevRef{};
+  }
+  if (c->copy_threads != 7) {
+    delete c->pool;  // idle between calls; joined here
+    c->pool = nullptr;
+    c->copy_threads = 7;
+  }
+  c->feat_zero_copy = 1;
+  c->bank_budget = 0;
+  c->chunk_used = 0;
   c->stream = c->own;
   c->force_generic = 0;
   c->track_order = 0;
@@ -872,6 +1021,18 @@ KLT_API int klt_hip_set_host_threads(klt_hip_ctx *c, int workers) {
   }
   return 0;
 }
+
+KLT_API int klt_hip_set_bank_budget(klt_hip_ctx *c, size_t bytes) {
+  if (!c) return fail(c, "set_bank_budget: null context");
+  c->bank_budget = bytes;
+  return 0;
+}
+
+KLT_API size_t klt_hip_get_bank_budget(klt_hip_ctx *c) { return c ? bank_budget_of(c) : 0; }
+
+KLT_API int klt_hip_frames_chunk(klt_hip_ctx *c) { return c ? c->chunk_used : -1; }
+
+KLT_API int klt_hip_get_host_threads(klt_hip_ctx *c) { return c ? c->copy_threads : -1; }
 
 KLT_API int klt_hip_set_frames_overlap(klt_hip_ctx *c, int overlap) {
   if (!c) return fail(c, "set_frames_overlap: null context");
@@ -1354,6 +1515,23 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
       HIPCHK(c, hipEventCreateWithFlags(&c->ev_bbuilt[k], hipEventDisableTiming));
       HIPCHK(c, hipEventCreateWithFlags(&c->ev_bfree[k], hipEventDisableTiming));
     }
+  // the banks' byte budget caps the chunk: a plain call runs shorter launches
+  // (results do not depend on the chunk), a band call -- whose chunk is the
+  // caller's exchange span -- fails before allocating anything
+  {
+    const int fit = budget_chunk(c, pd);
+    if (fit < 1)
+      return fail(c, "track_frames: one %dx%d pyramid per bank exceeds the bank budget of %zu bytes", pd->ncols,
+                  pd->nrows, bank_budget_of(c));
+    if (chunk > fit) {
+      if (band)
+        return fail(c, "track_frames_band: %d frames per chunk of %dx%d need %zu bytes of banks, over the budget of "
+                    "%zu (klt_hip_set_bank_budget); at most %d frames fit", chunk, pd->ncols, pd->nrows,
+                    bank_arena_bytes(pd, chunk), bank_budget_of(c), fit);
+      chunk = fit;
+    }
+  }
+  c->chunk_used = chunk;
   const int F = chunk < nframes ? chunk : nframes;
   // banks hold `chunk` frames whatever this call's length, so a short first
   // call does not force a reallocation (and a drain) in the next one
@@ -1379,8 +1557,7 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
       HIPCHK(c, hipStreamSynchronize(c->stream));
       c->prev = PrevRef{-1, 0, kSeedSlot};
     }
-    for (auto &K : c->bank)
-      if (ensure_bank(c, K, pd, chunk)) return -1;
+    if (ensure_banks(c, pd, chunk)) return -1;
     c->pre.bank = -1;
   }
   // band calls always use both streams: the next chunk's band pyramids are

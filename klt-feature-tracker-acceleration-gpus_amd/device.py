@@ -69,7 +69,13 @@ DEVICE_PROTOS = {
     "klt_hip_set_prof": (C.c_int, [V, V]),
     "klt_hip_set_frames_overlap": (C.c_int, [V, C.c_int]),
     "klt_hip_set_host_threads": (C.c_int, [V, C.c_int]),
+    "klt_hip_get_host_threads": (C.c_int, [V]),
     "klt_hip_set_path": (C.c_int, [V, C.c_int]),
+    "klt_hip_set_bank_budget": (C.c_int, [V, C.c_size_t]),
+    "klt_hip_get_bank_budget": (C.c_size_t, [V]),
+    "klt_hip_frames_chunk": (C.c_int, [V]),
+    "klt_hip_ctx_footprint": (C.c_size_t, [V]),
+    "klt_hip_ctx_reset": (C.c_int, [V]),
     "klt_hip_level_dims": (C.c_int, [V, C.c_int, C.c_int, IP, IP]),
     "klt_hip_download_level": (C.c_int, [V, C.c_int, C.c_int, C.c_int, V]),
     "klt_hip_level_ptr": (V, [V, C.c_int, C.c_int, C.c_int]),
@@ -115,6 +121,7 @@ DEVICE_PROTOS = {
     "klt_amd_pyr_desc": (None, [V, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(PyrDesc)]),
     "klt_amd_track_desc": (None, [V, C.POINTER(TrackDesc)]),
     "klt_amd_set_reduction": (None, [V, C.c_int]),
+    "klt_amd_release_cached_devices": (C.c_int, []),
     # host helpers
     "klt_synth_frame": (None, [C.c_uint64, C.c_int, C.c_int, C.c_int, V]),
     "klt_sort_pairs_full": (None, [IP, IP, C.c_int]),

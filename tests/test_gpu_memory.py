@@ -1,0 +1,109 @@
+"""Device memory bounds of the batched path:
+the bank budget (klt_hip_set_bank_budget) caps the chunk of a plain
+klt_hip_track_frames call -- with results identical to the uncapped run, the
+tracker being chunk-independent -- and fails a band call or a one-frame
+over-budget request cleanly, before allocating; a parked device context is
+trimmed and restored to its defaults (klt_hip_ctx_reset), and
+klt_amd_release_cached_devices frees the parked ones."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from conftest import synth
+from kltabi import OracleTracker
+from test_gpu_track import assert_table_equal, batch_sequence
+
+pytestmark = pytest.mark.gpu
+
+
+def test_budget_caps_chunk_results_unchanged(gpu, oracle):
+    frames = synth(gpu, 5151, 640, 480, 14)
+    seen = {}
+
+    def hook(ctx, done=False):
+        if not done:
+            # room for three banks of 5 frames, not of the 13 asked for
+            from kltamd.device import PyrDesc
+            one = 3 * (640 * 480 * 12 + 160 * 120 * 12 + 160 * 480 * 4) + 14 * (64 << 10)
+            assert gpu.klt_hip_set_bank_budget(ctx, 5 * one) == 0
+            assert gpu.klt_hip_get_bank_budget(ctx) == 5 * one
+        else:
+            seen["chunk"] = gpu.klt_hip_frames_chunk(ctx)
+            seen["foot"] = gpu.klt_hip_ctx_footprint(ctx)
+
+    X, Y, V = batch_sequence(gpu, frames, 1000, [13], ctx_hook=hook)
+    assert 1 <= seen["chunk"] < 13, seen
+    OX, OY, OV = OracleTracker(oracle).harness(frames, 1000, 14, first=frames[0])
+    assert_table_equal(X, Y, V, OX, OY, OV)
+    X2, Y2, V2 = batch_sequence(gpu, frames, 1000, [13])
+    assert np.array_equal(X.view(np.int32), X2.view(np.int32)) and np.array_equal(V, V2)
+
+
+def test_budget_errors_are_clean(gpu):
+    from kltamd.device import PyrDesc, TrackDesc, check
+    W, H = 640, 480
+    tc = gpu.KLTCreateTrackingContext()
+    ctx = gpu.klt_amd_device_context(tc)
+    pd, td = PyrDesc(), TrackDesc()
+    gpu.klt_amd_pyr_desc(tc, W, H, tc.contents.nPyramidLevels, 1, C.byref(pd))
+    gpu.klt_amd_track_desc(tc, C.byref(td))
+    fr = gpu.klt_hip_malloc(ctx, 9 * W * H)
+    check(gpu, ctx, gpu.klt_hip_synth_frames(ctx, 7, 0, 9, W, H, fr, W, W * H), "synth")
+    check(gpu, ctx, gpu.klt_hip_frames_begin(ctx, C.byref(pd), fr, W), "begin")
+    foot0 = gpu.klt_hip_ctx_footprint(ctx)
+    # not even one frame per bank
+    assert gpu.klt_hip_set_bank_budget(ctx, 1 << 20) == 0
+    assert gpu.klt_hip_track_frames(ctx, C.byref(pd), C.byref(td), fr + W * H, W, W * H, 8, 8, None, None, None, 0,
+                                    None, None, None, 0) < 0
+    assert b"bank budget" in gpu.klt_hip_last_error(ctx)
+    assert gpu.klt_hip_ctx_footprint(ctx) == foot0  # nothing was allocated
+    # a band call whose chunk does not fit fails instead of shortening its exchange span
+    one = 3 * (W * H * 12 + (W // 4) * (H // 4) * 12 + (W // 4) * H * 4) + 14 * (64 << 10)
+    assert gpu.klt_hip_set_bank_budget(ctx, 3 * one) == 0
+    esc = gpu.klt_hip_malloc(ctx, 4)
+    check(gpu, ctx, gpu.klt_hip_memcpy(ctx, esc, np.zeros(1, np.int32).ctypes.data, 4, 1), "h2d")
+    assert gpu.klt_hip_track_frames_band(ctx, C.byref(pd), C.byref(td), fr + W * H, W, W * H, 8, None, None, None,
+                                         0, 0.0, float(H), 0, H, esc, None, 0) < 0
+    assert b"over the budget" in gpu.klt_hip_last_error(ctx)
+    # within the budget the same call runs
+    assert gpu.klt_hip_set_bank_budget(ctx, 0) == 0
+    check(gpu, ctx, gpu.klt_hip_track_frames(ctx, C.byref(pd), C.byref(td), fr + W * H, W, W * H, 8, 8, None, None,
+                                             None, 0, None, None, None, 0), "frames")
+    assert gpu.klt_hip_frames_chunk(ctx) == 8
+    gpu.klt_hip_free(ctx, esc)
+    gpu.klt_hip_free(ctx, fr)
+    gpu.KLTFreeTrackingContext(tc)
+
+
+def test_reset_trims_and_restores_defaults(gpu):
+    """A context holding more than 2 GiB is trimmed when parked; a host-thread
+    setting does not leak into the next tracking context."""
+    from kltamd.device import PyrDesc, TrackDesc, check
+    gpu.klt_amd_release_cached_devices()
+    W, H = 1920, 1080
+    tc = gpu.KLTCreateTrackingContext()
+    ctx = gpu.klt_amd_device_context(tc)
+    check(gpu, ctx, gpu.klt_hip_set_host_threads(ctx, 2), "threads")
+    pd, td = PyrDesc(), TrackDesc()
+    gpu.klt_amd_pyr_desc(tc, W, H, tc.contents.nPyramidLevels, 1, C.byref(pd))
+    gpu.klt_amd_track_desc(tc, C.byref(td))
+    n = 34
+    fr = gpu.klt_hip_malloc(ctx, n * W * H)
+    check(gpu, ctx, gpu.klt_hip_synth_frames(ctx, 7, 0, n, W, H, fr, W, W * H), "synth")
+    check(gpu, ctx, gpu.klt_hip_frames_begin(ctx, C.byref(pd), fr, W), "begin")
+    check(gpu, ctx, gpu.klt_hip_track_frames(ctx, C.byref(pd), C.byref(td), fr + W * H, W, W * H, n - 1, 32, None,
+                                             None, None, 0, None, None, None, 0), "frames")
+    assert gpu.klt_hip_ctx_footprint(ctx) > (2 << 30)
+    gpu.klt_hip_free(ctx, fr)
+    gpu.KLTFreeTrackingContext(tc)  # parked, trimmed
+    tc2 = gpu.KLTCreateTrackingContext()
+    ctx2 = gpu.klt_amd_device_context(tc2)
+    assert ctx2 == ctx  # the parked context is handed on
+    assert gpu.klt_hip_ctx_footprint(ctx2) <= (2 << 30)
+    assert gpu.klt_hip_get_host_threads(ctx2) == 7
+    gpu.KLTFreeTrackingContext(tc2)
+    assert gpu.klt_amd_release_cached_devices() >= 1
+    assert gpu.klt_amd_release_cached_devices() == 0

@@ -220,11 +220,13 @@ def test_pipelined_generic_path_vs_oracle(gpu, oracle):
     assert np.array_equal(x.view(np.int32), X[:, 5].view(np.int32)) and np.array_equal(v, V[:, 5])
 
 
-def batch_sequence(gpu, frames, nfeat, chunks, setup=None, calls=None, counts=None):
+def batch_sequence(gpu, frames, nfeat, chunks, setup=None, calls=None, counts=None, ctx_hook=None):
     """Select on frames[0], then klt_hip_frames_begin + klt_hip_track_frames over
     frames[1:] (split into `calls` pieces, one chunk size per call), returning
     the device feature table: row j = the list after frame j+1.  counts (a
-    list): the tracker's work counters (klt_hip_set_track_count) are appended."""
+    list): the tracker's work counters (klt_hip_set_track_count) are appended.
+    ctx_hook(ctx) runs before the first call and after the last (with
+    done=True)."""
     from kltabi import fl_to_arrays, u8ptr
     from kltamd.device import D2H, H2D, PyrDesc, TrackDesc, check
     h, w = frames[0].shape
@@ -249,6 +251,8 @@ def batch_sequence(gpu, frames, nfeat, chunks, setup=None, calls=None, counts=No
     gpu.klt_amd_pyr_desc(tc, w, h, tc.contents.nPyramidLevels, 1, C.byref(pd))
     gpu.klt_amd_track_desc(tc, C.byref(td))
     check(gpu, ctx, gpu.klt_hip_frames_begin(ctx, C.byref(pd), dfr, w), "begin")
+    if ctx_hook:
+        ctx_hook(ctx)
     if counts is not None:
         check(gpu, ctx, gpu.klt_hip_set_track_count(ctx, 1), "count on")
     calls = calls or [T]
@@ -260,6 +264,8 @@ def batch_sequence(gpu, frames, nfeat, chunks, setup=None, calls=None, counts=No
                                                  nf, ch, dx, dy, dv, nfeat, tx + off, ty + off, tv + off,
                                                  nfeat), "frames")
         j0 += nf
+    if ctx_hook:
+        ctx_hook(ctx, done=True)
     if counts is not None:
         solves, passes = C.c_ulonglong(0), C.c_ulonglong(0)
         check(gpu, ctx, gpu.klt_hip_get_track_count(ctx, C.byref(solves), C.byref(passes), 1), "count")

@@ -19,6 +19,7 @@ import sys
 root, W, H = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 out = sys.argv[4] if len(sys.argv) > 4 else "profiles/pmc_latest.json"
 per = {}
+fpl = set()
 threads_l0 = ((W + 63) // 64) * ((H + 31) // 32) * 256
 W1, H1 = W // 4, H // 4
 threads_l1 = ((W1 + 31) // 32) * ((H1 + 31) // 32) * 256
@@ -32,6 +33,7 @@ for path in glob.glob(f"{root}/*/**/*counter_collection.csv", recursive=True):
         if frames < 2:
             continue  # single-frame launches (sequence starts) are not the batched pass
         per.setdefault((kern, r["Counter_Name"]), []).append(float(r["Counter_Value"]) * 1024 / frames)
+        fpl.add(frames)
 avg = {k: sum(v) / len(v) for k, v in per.items()}
 px = W * H
 alg_l0_read, alg_l0_write = px, px * 12 + W1 * H * 4
@@ -40,6 +42,7 @@ l0r, l0w = 2 * avg[("l0", "FETCH_SIZE")], avg[("l0", "WRITE_SIZE")]
 l1r, l1w = 2 * avg[("l1", "FETCH_SIZE")], avg[("l1", "WRITE_SIZE")]
 res = {
     "resolution": f"{W}x{H}",
+    "frames_per_launch": sorted(fpl),
     "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), tools/pmc_traffic.sh, batched launches",
     "per_frame_bytes": {"k_pyr_l0": {"read": l0r, "write": l0w, "alg_read": alg_l0_read, "alg_write": alg_l0_write},
                         "k_pyr_l1": {"read": l1r, "write": l1w, "alg_read": alg_l1_read, "alg_write": alg_l1_write}},
