@@ -73,6 +73,8 @@ def parse():
                    help="host frames for the klt.h API legs (KLTTrackFeatures per call, KLTTrackSequence); "
                         "rank 0, N=1; 0 = skip")
     p.add_argument("--no-fast", action="store_true", help="skip the fast (wave-shuffle) reduction replay")
+    p.add_argument("--replace-frames", type=int, default=59,
+                   help="frames of the api.replace leg (REPLACE harness, rank 0, N=1); 0 = skip")
     p.add_argument("--serial", action="store_true",
                    help="build and track on one stream; default: chunk c+1's pyramids are built on a second "
                         "stream while chunk c is tracked (they fill the CUs the tracker's last waves leave idle)")
@@ -610,6 +612,8 @@ def api_leg(lib, frames, W, H, NF, args):
     lib.KLTFreeFeatureList(fl)
     lib.KLTFreeTrackingContext(tc)
 
+    replace = replace_leg(lib, host, W, H, NF, args)
+
     arr = (U8P * (n + 1))(*[u8(a) for a in host])
     ft = lib.KLTCreateFeatureTable(n, NF)
 
@@ -647,9 +651,69 @@ def api_leg(lib, frames, W, H, NF, args):
                      "first_call_value": n / dt_cold,
                      "first_call": "the process's first KLTTrackSequence: device allocations, pinned staging, "
                                    "host threads, the table's first touch"},
+        "replace": replace,
         "frames": f"{W}x{H} u8 host frames (pageable numpy), {NF} features, seed {args.seed}",
         "per_call_equals_sequence": bool(same),
     }
+
+
+def replace_leg(lib, host, W, H, NF, args):
+    """The REPLACE harness (example3.c:62-71 with REPLACE): KLTTrackFeatures
+    then KLTReplaceLostFeatures on the new frame, per host frame; wall clock
+    around each call.  Parity: the list after each frame against the
+    reference's digests of the same sequence (tests/golden/long_config3r.json,
+    the reference compiled from its own sources) where the workload matches."""
+    import hashlib
+    from kltabi import fl_to_arrays
+    U8P = C.POINTER(C.c_ubyte)
+    u8 = lambda a: a.ctypes.data_as(U8P)  # noqa: E731
+    n = min(args.replace_frames, len(host) - 1)
+    if n < 2:
+        return None
+    fix = ROOT / "tests" / "golden" / "long_config3r.json"
+    want = None
+    if fix.exists():
+        d = json.loads(fix.read_text())
+        if (d["w"], d["h"], d["features"], d["seed"]) == (W, H, NF, args.seed):
+            want = d["columns"]
+    tc = lib.KLTCreateTrackingContext()
+    tc.contents.sequentialMode = 1
+    fl = lib.KLTCreateFeatureList(NF)
+    lib.KLTSelectGoodFeatures(tc, u8(host[0]), W, H, fl)
+    trk, rep, cols, replaced = [], [], [], 0
+    for t in range(1, n + 1):
+        a = time.perf_counter()
+        lib.KLTTrackFeatures(tc, u8(host[t - 1]), u8(host[t]), W, H, fl)
+        b = time.perf_counter()
+        lost = NF - lib.KLTCountRemainingFeatures(fl)
+        c = time.perf_counter()
+        lib.KLTReplaceLostFeatures(tc, u8(host[t]), W, H, fl)
+        e = time.perf_counter()
+        trk.append(b - a)
+        rep.append(e - c)
+        x, y, v = fl_to_arrays(fl)
+        replaced += lost - (NF - int((v >= 0).sum()))
+        h = hashlib.sha256()
+        for arr, dt in ((x, "<f4"), (y, "<f4"), (v, "<i4")):
+            h.update(np.ascontiguousarray(arr, dt).tobytes())
+        cols.append(h.hexdigest())
+    lib.KLTFreeFeatureList(fl)
+    lib.KLTFreeTrackingContext(tc)
+    steady = slice(1, None)  # the first track call builds two pyramids
+    per_frame = [p + q for p, q in zip(trk, rep)][steady]
+    out = {"value": len(per_frame) / sum(per_frame), "unit": "frames/s", "frames": n,
+           "us_per_replace_median": 1e6 * float(np.median(rep[steady])),
+           "us_per_track_median": 1e6 * float(np.median(trk[steady])),
+           "features_replaced": replaced,
+           "region": "wall clock around KLTTrackFeatures + KLTReplaceLostFeatures per frame (example3.c:61-69 "
+                     "with REPLACE), host u8 frames; first frame excluded"}
+    if want is not None:
+        m = min(len(want), len(cols))
+        bad = [j for j in range(m) if cols[j] != want[j]]
+        out["parity"] = {"against": "tests/golden/long_config3r.json (reference, oracle/_ref)",
+                         "columns_compared": m, "columns_mismatched": len(bad),
+                         "first_mismatch": bad[0] + 1 if bad else None}
+    return out
 
 
 def tracker_line(solves, passes, feature_frames, tm):

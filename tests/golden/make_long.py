@@ -20,6 +20,8 @@ Output: tests/golden/long_<name>.json
   config3: 1920x1080, 5000 features,  500 frames, seed 1080    (configs[2])
   config4: 3840x2160, 20000 features, 1000 frames, seed 2160   (configs[3]; the
            single-GPU result the sharded run must equal)
+  config3r: config 3's sequence (60 frames) through the REPLACE harness:
+           KLTReplaceLostFeatures after every KLTTrackFeatures
 """
 from __future__ import annotations
 
@@ -40,6 +42,9 @@ CONFIGS = {
     "config2": dict(w=640, h=480, features=1000, frames=100, seed=640480),
     "config3": dict(w=1920, h=1080, features=5000, frames=500, seed=1080),
     "config4": dict(w=3840, h=2160, features=20000, frames=1000, seed=2160),
+    # the REPLACE harness (example3.c:67-69: KLTReplaceLostFeatures after every
+    # KLTTrackFeatures, before KLTStoreFeatureList) at the config-3 size
+    "config3r": dict(w=1920, h=1080, features=5000, frames=60, seed=1080, replace=True),
 }
 
 
@@ -67,6 +72,7 @@ def run(name: str) -> dict:
     amd = kltamd.load()  # host-side synthetic generator only (klt_synth_frame)
     p = CONFIGS[name]
     w, h, nf, nframes, seed = p["w"], p["h"], p["features"], p["frames"], p["seed"]
+    p = dict(p)
     ref = bind_klt(REF_LIB)
     ref.KLTSetVerbosity(0)
 
@@ -87,6 +93,8 @@ def run(name: str) -> dict:
     for i in range(1, nframes):
         img2 = frame(i)
         ref.KLTTrackFeatures(tc, u8ptr(img1), u8ptr(img2), w, h, fl)
+        if p.get("replace"):
+            ref.KLTReplaceLostFeatures(tc, u8ptr(img2), w, h, fl)
         cols.append(column_digest(x, y, v))
         live.append(int((v >= 0).sum()))
         img1 = img2

@@ -13,6 +13,8 @@ Paths covered, each over the whole sequence:
     chunks, next chunk's pyramids on a second stream) -- every column;
   * KLTTrackSequence on host frames (the klt.h extension) -- every column;
   * KLTTrackFeatures once per host frame (config 2; example3.c:54-74);
+  * the REPLACE harness at the config-3 size (KLTReplaceLostFeatures after
+    every KLTTrackFeatures, 60 frames, long_config3r.json);
   * the feature-sharded schedule (config 4, 2/4/8 simulated ranks);
   * the fast (wave-shuffle) reduction, against the exact path, with the
     tolerance it is held to.
@@ -174,6 +176,21 @@ def test_track_features_per_call_config2(gpu):
     T = cfg["frames"] - 1
     j = first_mismatch(X[:, :T].T, Y[:, :T].T, V[:, :T].T, cfg["columns"])
     assert j is None, f"per-call path differs from frame {j + 1}"
+
+
+def test_replace_harness_config3r(gpu):
+    """The REPLACE harness (example3.c:62-71 with REPLACE defined): every
+    KLTTrackFeatures is followed by KLTReplaceLostFeatures on the new frame,
+    at the config-3 size (1080p, 5000 features), 60 frames, against the
+    reference's per-column digests (long_config3r.json)."""
+    from kltabi import KLTRunner
+    cfg = fixture("config3r")
+    frames = host_frames(gpu, cfg, cfg["frames"])
+    X, Y, V = KLTRunner(gpu).harness(frames, cfg["features"], cfg["frames"], first=frames[0], replace=True)
+    T = cfg["frames"] - 1
+    j = first_mismatch(X[:, :T].T, Y[:, :T].T, V[:, :T].T, cfg["columns"])
+    assert j is None, f"REPLACE harness differs from frame {j + 1}"
+    assert [int((V[:, i] >= 0).sum()) for i in range(T)] == cfg["live"]
 
 
 def fast_vs_exact(Xe, Ye, Ve, Xf, Yf, Vf) -> dict:
