@@ -681,6 +681,8 @@ def replace_leg(lib, host, W, H, NF, args):
     fl = lib.KLTCreateFeatureList(NF)
     lib.KLTSelectGoodFeatures(tc, u8(host[0]), W, H, fl)
     trk, rep, cols, replaced = [], [], [], 0
+    sel_stats = []
+    ctx = lib.klt_amd_device_context(tc)
     for t in range(1, n + 1):
         a = time.perf_counter()
         lib.KLTTrackFeatures(tc, u8(host[t - 1]), u8(host[t]), W, H, fl)
@@ -691,6 +693,11 @@ def replace_leg(lib, host, W, H, NF, args):
         e = time.perf_counter()
         trk.append(b - a)
         rep.append(e - c)
+        if lost > 0:
+            st = [C.c_long() for _ in range(3)]
+            us = (C.c_double * 4)()
+            lib.klt_hip_select_stats(ctx, *[C.byref(q) for q in st], us)
+            sel_stats.append([q.value for q in st] + list(us))
         x, y, v = fl_to_arrays(fl)
         replaced += lost - (NF - int((v >= 0).sum()))
         h = hashlib.sha256()
@@ -705,6 +712,10 @@ def replace_leg(lib, host, W, H, NF, args):
            "us_per_replace_median": 1e6 * float(np.median(rep[steady])),
            "us_per_track_median": 1e6 * float(np.median(trk[steady])),
            "features_replaced": replaced,
+           "select_median": dict(zip(("map_points_downloaded", "device_partition_steps", "sorted_positions_visited",
+                                      "us_map_init", "us_device_splits", "us_downloads", "us_select_total"),
+                                     (float(np.median([q[k] for q in sel_stats])) for k in range(7))))
+           if sel_stats else None,
            "region": "wall clock around KLTTrackFeatures + KLTReplaceLostFeatures per frame (example3.c:61-69 "
                      "with REPLACE), host u8 frames; first frame excluded"}
     if want is not None:

@@ -290,6 +290,31 @@ int klt_hip_track_frames_band(klt_hip_ctx *ctx, const klt_hip_pyr_desc *pdesc,
                               float own_hi, int row_lo, int row_hi, int *escape,
                               const unsigned char *next_frames, int next_nframes);
 
+/* Feature selection on the device (selectGoodFeatures.c:297-453 after the
+   smoothing): the trackability map of slot `slot`'s level 0, then the
+   reference's quicksort order produced lazily -- the top-level partition steps
+   on the device, exactly (parallel form of the same step), the segments the
+   walk reaches on the host -- and the minimum-distance walk.  x/y/val: the
+   host feature list (in/out); overwrite_all 1 = KLTSelectGoodFeatures
+   (every slot), 0 = KLTReplaceLostFeatures (slots with val < 0, live
+   features' squares blocked).  changed[k] = 1 for every slot written (a new
+   feature or NOT_FOUND; the caller resets its affine fields).  mindist as in
+   the tracking context (the walk uses mindist-1, :157). */
+int klt_hip_select(klt_hip_ctx *ctx, int slot, const klt_hip_select_desc *sd, int ncols, int nrows, int mindist,
+                   int min_eigenvalue, int overwrite_all, float *x, float *y, int *val, unsigned char *changed,
+                   int n);
+/* the same walk over a device trackability map (nx x ny grid) */
+int klt_hip_select_dev_map(klt_hip_ctx *ctx, const int *dev_map, int nx, int ny, const klt_hip_select_desc *sd,
+                           int ncols, int nrows, int mindist, int min_eigenvalue, int overwrite_all, float *x,
+                           float *y, int *val, unsigned char *changed, int n);
+/* segments longer than `threshold` map points are split on the device (default 32768) */
+int klt_hip_select_tune(klt_hip_ctx *ctx, int threshold);
+/* last selection: map points copied to the host, device partition steps, sorted positions visited;
+   host_us (optional, 4 values): wall clock of the map + init (queued and drained), the device
+   splits, the segment downloads, and the whole walk */
+int klt_hip_select_stats(klt_hip_ctx *ctx, long *downloaded, long *device_steps, long *visited, double *host_us);
+/* test hook: the whole lazy order of host vals[0..n) as klt_sort_pairs_full gives it */
+int klt_hip_select_sort_test(klt_hip_ctx *ctx, const int *vals, int n, int *out_val, int *out_idx);
 /* trackability map of level 0 of `slot`: nx*ny int values, row-major over the
    border-trimmed grid; vals == NULL only reports nx, ny.  Synchronous. */
 int klt_hip_min_eigen(klt_hip_ctx *ctx, int slot, const klt_hip_select_desc *desc, int *vals,

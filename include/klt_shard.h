@@ -57,6 +57,17 @@ klt_shard *klt_shard_create_local(klt_hip_ctx *ctx, int rank, int world, int nro
 /* before the tracking context that owns ctx is freed (it synchronizes ctx) */
 void klt_shard_destroy(klt_shard *s);
 const char *klt_shard_last_error(klt_shard *s);
+/* Failures and the collectives.  Argument errors (null pointers, a frame
+   height that differs from the shard's) return before any collective; a
+   caller passes every rank the same geometry, so every rank returns there.
+   A failure after that point (a device call, the whole-frame callback, the
+   band build) does not skip the rank's collectives: klt_shard_track sends a
+   failure count with its all-reduce and klt_shard_replace agrees on one
+   before its broadcasts, so every rank returns < 0 together ("peer rank(s)
+   failed" on the others) and none waits for a rank that left.  A rank that
+   cannot take part at all (its exchange buffers cannot be allocated) aborts
+   the communicator (ncclCommAbort) so that its peers' collectives fail; the
+   shard is then unusable.  Entry points restore the caller's current device. */
 /* rows [*lo, *hi) of every frame this rank's band build reads: the only rows
    klt_shard_track's frames must hold (its band, margin and tile halo) */
 int klt_shard_rows(const klt_shard *s, int *lo, int *hi);
@@ -76,8 +87,8 @@ int klt_shard_track(klt_shard *s, const klt_hip_pyr_desc *pdesc, const klt_hip_t
    sequential mode, which reads the last tracked frame's pyramid, :342-348),
    between two klt_shard_track calls.  Each rank computes the trackability map
    rows of its own band from its band pyramid, the rows are broadcast to every
-   rank (RCCL, one broadcast per owner), and every rank runs the same host
-   selection over the whole map: x/y/val (device, the merged list) come back
+   rank (RCCL, one broadcast per owner), and every rank runs the same
+   selection (klt_hip_select_dev_map) over the whole map: x/y/val (device, the merged list) come back
    identical on every rank and equal to one GPU's.  When the selection window
    reaches rows the band pyramid lacks, `full` is asked for the last frame
    whole (*frames = its device address).  pitch: that frame's row pitch.
@@ -91,7 +102,7 @@ int klt_shard_replace(klt_shard *s, const klt_hip_pyr_desc *pdesc, const klt_hip
    klt_hip_min_eigen_rows; 1 when the whole frame was needed) ... */
 int klt_shard_eigen(klt_shard *s, const klt_hip_pyr_desc *pdesc, const klt_hip_select_desc *sd, long pitch,
                     int *dev_map, klt_shard_frames_fn full, void *user);
-/* ... and the host selection over a complete map (synchronous) */
+/* ... and the selection over a complete device map (synchronous) */
 int klt_shard_select(klt_shard *s, const klt_hip_pyr_desc *pdesc, const klt_hip_select_desc *sd, int mindist,
                      int min_eigenvalue, const int *dev_map, float *x, float *y, int *val, int n);
 

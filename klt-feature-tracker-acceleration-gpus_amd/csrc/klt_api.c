@@ -573,7 +573,7 @@ static void select_features(KLT_TrackingContext tc, KLT_PixelType *img, int ncol
   klt_ctx_full *f = FULL(tc);
   klt_hip_ctx *dev;
   klt_hip_select_desc sd;
-  int slot, nx = 0, ny = 0, *vals;
+  int slot;
 
   window_fix(tc, NULL);
   dev = device_of(tc);
@@ -595,19 +595,34 @@ static void select_features(KLT_TrackingContext tc, KLT_PixelType *img, int ncol
   sd.borderx = tc->borderx < tc->window_width / 2 ? tc->window_width / 2 : tc->borderx;
   sd.bordery = tc->bordery < tc->window_height / 2 ? tc->window_height / 2 : tc->bordery;
   sd.nSkippedPixels = tc->nSkippedPixels;
-  dev_check(tc, klt_hip_min_eigen(dev, slot, &sd, NULL, &nx, &ny), "trackability map");
-  vals = (int *)malloc(sizeof(int) * ((size_t)nx * ny + 1));
-  if (!vals) KLTError("(KLTSelectGoodFeatures) Out of memory");
-  dev_check(tc, klt_hip_min_eigen(dev, slot, &sd, vals, &nx, &ny), "trackability map");
   if (tc->mindist < 0) {
     KLTWarning("(_KLTSelectGoodFeatures) Tracking context field tc->mindist is negative (%d); "
                "setting to zero",
                tc->mindist);
     tc->mindist = 0;
   }
-  klt_select_from_map(vals, nx, ny, sd.borderx, sd.bordery, tc->nSkippedPixels + 1, ncols, nrows, fl,
-                      tc->mindist, tc->min_eigenvalue, !replacing);
-  free(vals);
+  {
+    /* the map, the reference's sort order and the walk (klt_hip_select);
+       written slots get klt_select.c's mark_found treatment */
+    const int n = fl->nFeatures;
+    float *x = (float *)malloc(sizeof(float) * (n + 1)), *y = (float *)malloc(sizeof(float) * (n + 1));
+    int *v = (int *)malloc(sizeof(int) * (n + 1)), k;
+    unsigned char *changed = (unsigned char *)malloc((size_t)n + 1);
+    if (!x || !y || !v || !changed) KLTError("(KLTSelectGoodFeatures) Out of memory");
+    for (k = 0; k < n; k++) {
+      x[k] = fl->feature[k]->x;
+      y[k] = fl->feature[k]->y;
+      v[k] = fl->feature[k]->val;
+    }
+    dev_check(tc, klt_hip_select(dev, slot, &sd, ncols, nrows, tc->mindist, tc->min_eigenvalue, !replacing, x, y,
+                                 v, changed, n),
+              "feature selection");
+    klt_select_apply(fl, x, y, v, changed);
+    free(x);
+    free(y);
+    free(v);
+    free(changed);
+  }
 }
 
 EXPORT void KLTSelectGoodFeatures(KLT_TrackingContext tc, KLT_PixelType *img, int ncols, int nrows,

@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "klt_hip.h"
 
 namespace kltdev {
@@ -23,7 +25,7 @@ constexpr int kWave = 64;
 constexpr int kBlock = 256;
 
 // status codes (klt.h:28-33)
-constexpr int kTracked = 0, kSmallDet = -2, kMaxIter = -3, kOOB = -4, kLargeResidue = -5;
+constexpr int kTracked = 0, kNotFound = -1, kSmallDet = -2, kMaxIter = -3, kOOB = -4, kLargeResidue = -5;
 
 __host__ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
@@ -171,6 +173,23 @@ hipError_t launch_band_order(hipStream_t st, const float *fy, const int *fv, int
                              float own_lo, float own_hi, int *count);
 
 hipError_t launch_affine(hipStream_t st, const AffArgs &a);
+
+// runtime.hip: record a failure in the context's error message (klt_hip_last_error); returns -1
+int ctx_fail(klt_hip_ctx *c, const char *fmt, ...);
+
+// select.hip: exact lazy selection (the reference's quicksort order) with the
+// top-level partition steps on the device
+struct SelEngine;
+constexpr int kSelDefaultThreshold = 32768;  // map points: longer segments are split on the device
+SelEngine *sel_engine_create();
+void sel_engine_destroy(SelEngine *e);
+void sel_engine_set_threshold(SelEngine *e, int threshold);
+void sel_engine_stats(const SelEngine *e, long *downloaded, long *steps, long *visited, double *us);
+int sel_engine_run(SelEngine *e, hipStream_t st, const int *dev_vals, int nx, int ny, int bx, int by, int step,
+                   int W, int H, int mindist, int min_eigenvalue, int overwrite_all, float *x, float *y, int *val,
+                   unsigned char *changed, int n, std::string *err);
+int sel_engine_sort(SelEngine *e, hipStream_t st, const int *dev_vals, int n, int *out_val, int *out_idx,
+                    std::string *err);
 hipError_t launch_affine_move(hipStream_t st, int dir, const int *idx, int m, int s3, float *staging, float *store);
 
 }  // namespace kltdev

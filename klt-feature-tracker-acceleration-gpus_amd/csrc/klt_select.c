@@ -146,6 +146,14 @@ static void mark_found(KLT_Feature f, int x, int y, int val)
   f->aff_Ayy = 1.0;
 }
 
+void klt_select_apply(KLT_FeatureList fl, const float *x, const float *y, const int *val,
+                      const unsigned char *changed)
+{
+  int k;
+  for (k = 0; k < fl->nFeatures; k++)
+    if (changed[k]) mark_found(fl->feature[k], (int)x[k], (int)y[k], val[k]);
+}
+
 void klt_select_from_map(const int *vals, int gx, int gy, int bx, int by, int step, int W, int H,
                          KLT_FeatureList fl, int mindist, int min_eigenvalue, int overwrite_all)
 {

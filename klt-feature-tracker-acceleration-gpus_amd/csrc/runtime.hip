@@ -151,6 +151,7 @@ struct klt_hip_ctx {
   size_t f_cap = 0;
   int *d_eig = nullptr;
   size_t eig_cap = 0;
+  SelEngine *sel = nullptr;  // select.hip: the lazy exact selection
   // affine consistency check: stored windows (3*aff_S floats per feature) and per-call arrays
   float *d_aff_store = nullptr;
   size_t aff_store_cap = 0;
@@ -216,6 +217,20 @@ int fail(klt_hip_ctx *c, const char *fmt, ...) {
   if (c) c->err = buf;
   return -1;
 }
+
+}  // namespace
+
+int kltdev::ctx_fail(klt_hip_ctx *c, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return -1;
+}
+
+namespace {
 
 #define HIPCHK(c, expr)                                                                \
   do {                                                                                 \
@@ -800,6 +815,7 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
   hipFree(c->d_feat);
   if (c->h_feat) hipHostFree(c->h_feat);
   hipFree(c->d_eig);
+  sel_engine_destroy(c->sel);
   for (void *p : {(void *)c->d_aff_store, (void *)c->d_aff, (void *)c->d_xp, (void *)c->d_yp, (void *)c->d_astage,
                   (void *)c->d_astate, (void *)c->d_aidx})
     hipFree(p);
@@ -875,6 +891,7 @@ KLT_API int klt_hip_ctx_reset(klt_hip_ctx *c) {
     c->copy_threads = 7;
   }
   c->feat_zero_copy = 1;
+  if (c->sel) sel_engine_set_threshold(c->sel, kSelDefaultThreshold);
   c->bank_budget = 0;
   c->chunk_used = 0;
   c->stream = c->own;
@@ -1851,6 +1868,80 @@ KLT_API int klt_hip_min_eigen(klt_hip_ctx *c, int s, const klt_hip_select_desc *
   }
   HIPCHK(c, hipMemcpyAsync(vals, c->d_eig, sizeof(int) * np, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// the trackability map of slot s into d_eig (k_min_eigen), grid nx x ny
+static int eigen_to_dev(klt_hip_ctx *c, int s, const klt_hip_select_desc *d, int *nx, int *ny) {
+  if (klt_hip_min_eigen(c, s, d, nullptr, nx, ny)) return -1;
+  const long np = (long)*nx * *ny;
+  if (np == 0) return 0;
+  const Level &L = c->slot[s].lv[0];
+  if (grow(c, &c->d_eig, &c->eig_cap, (size_t)np)) return -1;
+  TimedScope ts(c, T_EIG, c->stream);
+  return launched(c, "k_min_eigen", launch_min_eigen(c->stream, L.gx, L.gy, L.w, d->borderx, d->bordery,
+                                                     d->nSkippedPixels + 1, *nx, *ny, d->window_width / 2,
+                                                     d->window_height / 2, c->d_eig));
+}
+
+static SelEngine *sel_of(klt_hip_ctx *c) {
+  if (!c->sel) c->sel = sel_engine_create();
+  return c->sel;
+}
+
+KLT_API int klt_hip_select(klt_hip_ctx *c, int s, const klt_hip_select_desc *d, int ncols, int nrows, int mindist,
+                           int min_eigenvalue, int overwrite_all, float *x, float *y, int *val,
+                           unsigned char *changed, int n) {
+  if (!c || !d || (n > 0 && (!x || !y || !val || !changed))) return fail(c, "select: null argument");
+  if (s < 0 || s >= KLT_HIP_MAX_SLOTS || c->slot[s].nlev < 1) return fail(c, "select: bad slot");
+  if (c->slot[s].lv[0].w != ncols || c->slot[s].lv[0].h != nrows)
+    return fail(c, "select: slot %d is %dx%d, image %dx%d", s, c->slot[s].lv[0].w, c->slot[s].lv[0].h, ncols, nrows);
+  if (use_device(c)) return -1;
+  int nx = 0, ny = 0;
+  if (eigen_to_dev(c, s, d, &nx, &ny)) return -1;
+  std::string e;
+  if (sel_engine_run(sel_of(c), c->stream, c->d_eig, nx, ny, d->borderx, d->bordery, d->nSkippedPixels + 1, ncols,
+                     nrows, mindist < 0 ? 0 : mindist, min_eigenvalue, overwrite_all, x, y, val, changed, n, &e))
+    return fail(c, "select: %s", e.c_str());
+  return 0;
+}
+
+KLT_API int klt_hip_select_dev_map(klt_hip_ctx *c, const int *dev_map, int nx, int ny,
+                                   const klt_hip_select_desc *d, int ncols, int nrows, int mindist,
+                                   int min_eigenvalue, int overwrite_all, float *x, float *y, int *val,
+                                   unsigned char *changed, int n) {
+  if (!c || !d || (nx * ny > 0 && !dev_map) || (n > 0 && (!x || !y || !val || !changed)))
+    return fail(c, "select_dev_map: null argument");
+  if (use_device(c)) return -1;
+  std::string e;
+  if (sel_engine_run(sel_of(c), c->stream, dev_map, nx, ny, d->borderx, d->bordery, d->nSkippedPixels + 1, ncols,
+                     nrows, mindist < 0 ? 0 : mindist, min_eigenvalue, overwrite_all, x, y, val, changed, n, &e))
+    return fail(c, "select: %s", e.c_str());
+  return 0;
+}
+
+KLT_API int klt_hip_select_tune(klt_hip_ctx *c, int threshold) {
+  if (!c) return fail(c, "select_tune: null context");
+  sel_engine_set_threshold(sel_of(c), threshold);
+  return 0;
+}
+
+KLT_API int klt_hip_select_stats(klt_hip_ctx *c, long *downloaded, long *device_steps, long *visited,
+                                 double *host_us) {
+  if (!c || !downloaded || !device_steps || !visited) return fail(c, "select_stats: null argument");
+  sel_engine_stats(sel_of(c), downloaded, device_steps, visited, host_us);
+  return 0;
+}
+
+KLT_API int klt_hip_select_sort_test(klt_hip_ctx *c, const int *vals, int n, int *out_val, int *out_idx) {
+  if (!c || n < 0 || (n > 0 && (!vals || !out_val || !out_idx))) return fail(c, "select_sort_test: bad argument");
+  if (use_device(c)) return -1;
+  if (n == 0) return 0;
+  if (grow(c, &c->d_eig, &c->eig_cap, (size_t)n)) return -1;
+  HIPCHK(c, hipMemcpyAsync(c->d_eig, vals, sizeof(int) * n, hipMemcpyHostToDevice, c->stream));
+  std::string e;
+  if (sel_engine_sort(sel_of(c), c->stream, c->d_eig, n, out_val, out_idx, &e))
+    return fail(c, "select_sort_test: %s", e.c_str());
   return 0;
 }
 

@@ -1,0 +1,618 @@
+// select.hip -- feature selection after the trackability map, on the device
+// where the reference's order allows it (selectGoodFeatures.c:62-96 quicksort,
+// :135-239 minimum-distance walk).
+//
+// The reference sorts every grid point {x, y, val} with its own unstable
+// quicksort and walks the sorted list greedily.  The walk reads only a prefix
+// of the sorted order, and the quicksort's two partitions are sorted
+// independently, so the order is produced lazily, left to right: a segment is
+// split by exactly the reference's partition step only when the walk reaches
+// it.  Ties make the permutation depend on every element of a segment, so the
+// large top-level segments (the whole map: 1.9 M points at 1080p, 8 M at 4K)
+// are split here on the device, and only the leftmost small segment -- the
+// one the walk reads first -- goes to the host, where the remaining splits and
+// the walk run as in klt_select.c.
+//
+// The partition step (klt_select.c partition_step, the reference's _quicksort
+// body) on a[0..n) with pivot a[n/2] swapped to the front:
+//   j walks down from n and stops at values >= pv, i walks up from 0 and stops
+//   at values <= pv (or at j); while i < j the two swap.
+// Swaps only exchange a left stop with a right stop, and i never reaches a
+// swapped right stop, so the k-th left stop l_k (k-th position >= 1 with value
+// <= pv, ascending) meets the k-th right stop r_k (k-th position >= 1 with
+// value >= pv, descending).  They swap for k = 1..m, m = the number of k with
+// l_k < r_k (true for a prefix of k).  j's last scan stops at the first value
+// >= pv below r_m: the next original right stop r_{m+1} (position 0, the pivot
+// itself, when there is none) or l_m, which holds r_m's value after the last
+// swap -- whichever is higher; the pivot swaps with it.  With per-position
+// ranks from two scans every swap pair is known at once: that is the parallel
+// step below, equal to the sequential one element for element (the model in
+// tools/exp/partition_model.py checks it exhaustively on small arrays).
+//
+// Grid point i of the map is the pair {val, idx}; idx carries bit 31 when the
+// point lies inside the painted square of a feature that is already live
+// (REPLACE mode, selectGoodFeatures.c:160-166 / _fillFeaturemap), so the host
+// walk never needs the full-frame feature map.  The partition reads val only.
+#pragma clang fp contract(off)
+
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <string>
+#include <vector>
+
+#include "klt_dev.h"
+
+namespace kltdev {
+namespace {
+
+constexpr int kSelThreads = 256;
+constexpr int kSelPer = 8;                          // elements per thread in the count / rank kernels
+constexpr int kSelBS = kSelThreads * kSelPer;       // elements per block
+constexpr int kSelStack = 512;                      // segments a device refinement may push
+constexpr int kSelScanThreads = 1024;
+constexpr unsigned kBlockedBit = 0x80000000u;
+
+struct SelState {
+  int start, len;  // the leftmost segment still to split
+  int pv;          // its pivot value
+  int done;        // 1 once len <= the host threshold
+  int m;           // swap pairs of the current step
+  int totL, totR;  // left / right stops of the current step
+  int nstack;      // segments pushed (start, len), in push order
+  int stack[2 * kSelStack];
+};
+
+__device__ __forceinline__ void swap2(int2 *a, int i, int j) {
+  const int2 t = a[i];
+  a[i] = a[j];
+  a[j] = t;
+}
+
+// block-wide exclusive scan of one int per thread (kSelThreads threads); returns
+// the exclusive prefix and writes the block total
+__device__ __forceinline__ int block_exscan(int v, int *tmp, int &total) {
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int y = __shfl_up(x, o, kWave);
+    if (lane >= o) x += y;
+  }
+  if (lane == kWave - 1) tmp[w] = x;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < kSelThreads / kWave; ++k) {
+    const int t = tmp[k];
+    if (k < w) base += t;
+    tot += t;
+  }
+  __syncthreads();
+  total = tot;
+  return base + x - v;
+}
+
+// kv[i] = {val, i | blocked}: blocked when the grid point lies in a square
+// painted around a live feature (map != null, REPLACE mode)
+__global__ __launch_bounds__(kSelThreads) void k_sel_init(const int *__restrict__ vals, int nx, int n, int bx, int by,
+                                                         int step, int W, const uint8_t *__restrict__ map,
+                                                         int2 *__restrict__ kv) {
+  const int i = blockIdx.x * kSelThreads + threadIdx.x;
+  if (i >= n) return;
+  unsigned idx = (unsigned)i;
+  if (map) {
+    const int iy = i / nx, ix = i - iy * nx;
+    if (map[(size_t)(by + iy * step) * W + bx + ix * step]) idx |= kBlockedBit;
+  }
+  kv[i] = make_int2(vals[i], (int)idx);
+}
+
+// _fillFeaturemap around every live feature (selectGoodFeatures.c:102-115):
+// the square [x-r, x+r] x [y-r, y+r] of (int) coordinates, clipped
+__global__ __launch_bounds__(kSelThreads) void k_sel_paint(const float *__restrict__ x, const float *__restrict__ y,
+                                                          const int *__restrict__ v, int n, int r, int W, int H,
+                                                          uint8_t *__restrict__ map) {
+  const int side = 2 * r + 1, cells = side * side;
+  const long t = (long)blockIdx.x * kSelThreads + threadIdx.x;
+  if (t >= (long)n * cells) return;
+  const int f = (int)(t / cells), c = (int)(t - (long)f * cells);
+  if (v[f] < 0) return;
+  const int px = (int)x[f] - r + c % side, py = (int)y[f] - r + c / side;
+  if (px >= 0 && px < W && py >= 0 && py < H) map[(size_t)py * W + px] = 1;
+}
+
+// step 0: pivot a[n/2] to the front (or stop: the segment is small enough)
+__global__ void k_sel_pivot(SelState *s, int2 *kv, int threshold) {
+  if (s->done) return;
+  if (s->len <= threshold) {
+    s->done = 1;
+    return;
+  }
+  const int st = s->start;
+  swap2(kv, st, st + s->len / 2);
+  s->pv = kv[st].x;
+  s->m = 0;
+}
+
+// step 1: left / right stop counts per block (positions 1 .. len-1)
+__global__ __launch_bounds__(kSelThreads) void k_sel_count(const SelState *s, const int2 *__restrict__ kv,
+                                                          int *__restrict__ cnt) {
+  __shared__ int tmp[kSelThreads / kWave];
+  if (s->done) return;
+  const int len = s->len, b = blockIdx.x;
+  if (b * kSelBS >= len) return;
+  const int2 *a = kv + s->start;
+  const int pv = s->pv;
+  int l = 0, r = 0;
+#pragma unroll
+  for (int e = 0; e < kSelPer; ++e) {
+    const int p = b * kSelBS + e * kSelThreads + threadIdx.x;
+    if (p >= 1 && p < len) {
+      const int v = a[p].x;
+      l += v <= pv;
+      r += v >= pv;
+    }
+  }
+  int tl, tr;
+  block_exscan(l, tmp, tl);
+  block_exscan(r, tmp, tr);
+  if (threadIdx.x == 0) {
+    cnt[2 * b] = tl;
+    cnt[2 * b + 1] = tr;
+  }
+}
+
+// step 2 (one block): exclusive prefix of the left counts, exclusive suffix
+// (blocks after b) of the right counts, totals
+__global__ __launch_bounds__(kSelScanThreads) void k_sel_scan(SelState *s, const int *__restrict__ cnt,
+                                                             int *__restrict__ off) {
+  __shared__ int sl[kSelScanThreads], sr[kSelScanThreads];
+  if (s->done) return;
+  const int nb = (s->len + kSelBS - 1) / kSelBS;
+  const int per = (nb + kSelScanThreads - 1) / kSelScanThreads;
+  const int t = threadIdx.x, b0 = t * per;
+  int l = 0, r = 0;
+  for (int k = 0; k < per; ++k)
+    if (b0 + k < nb) {
+      l += cnt[2 * (b0 + k)];
+      r += cnt[2 * (b0 + k) + 1];
+    }
+  sl[t] = l;
+  sr[t] = r;
+  __syncthreads();
+  for (int o = 1; o < kSelScanThreads; o <<= 1) {  // inclusive Hillis-Steele scans
+    const int a = t >= o ? sl[t - o] : 0, c = t >= o ? sr[t - o] : 0;
+    __syncthreads();
+    sl[t] += a;
+    sr[t] += c;
+    __syncthreads();
+  }
+  const int totL = sl[kSelScanThreads - 1], totR = sr[kSelScanThreads - 1];
+  int pl = sl[t] - l, pr = sr[t] - r;  // exclusive: blocks before b0
+  for (int k = 0; k < per; ++k) {
+    const int b = b0 + k;
+    if (b >= nb) break;
+    off[2 * b] = pl;                                  // left stops in blocks < b
+    pr += cnt[2 * b + 1];
+    off[2 * b + 1] = totR - pr;                       // right stops in blocks > b
+    pl += cnt[2 * b];
+  }
+  if (t == 0) {
+    s->totL = totL;
+    s->totR = totR;
+  }
+}
+
+// step 3: per position, its rank among the left stops (ascending) and the right
+// stops (descending); left stop k pairs with right stop k when the latter lies
+// further right.  posL[k-1] / posR[k-1] collect the pairs' positions; m counts
+// them.
+__global__ __launch_bounds__(kSelThreads) void k_sel_rank(SelState *s, const int2 *__restrict__ kv,
+                                                         const int *__restrict__ off, int *__restrict__ posL,
+                                                         int *__restrict__ posR) {
+  __shared__ int tmp[kSelThreads / kWave];
+  if (s->done) return;
+  const int len = s->len, b = blockIdx.x;
+  if (b * kSelBS >= len) return;
+  const int2 *a = kv + s->start;
+  const int pv = s->pv, totL = s->totL;
+  // a thread owns kSelPer consecutive positions, in order
+  const int p0 = b * kSelBS + threadIdx.x * kSelPer;
+  int v[kSelPer];
+  int l = 0, r = 0;
+#pragma unroll
+  for (int e = 0; e < kSelPer; ++e) {
+    const int p = p0 + e;
+    v[e] = (p >= 1 && p < len) ? a[p].x : 0;
+    const bool in = p >= 1 && p < len;
+    l += in && v[e] <= pv;
+    r += in && v[e] >= pv;
+  }
+  int bl, br;
+  int lx = block_exscan(l, tmp, bl);
+  int rx = block_exscan(r, tmp, br);
+  const int preL = off[2 * b], sufR = off[2 * b + 1];
+  int rankL = preL + lx;           // left stops before this thread's run
+  int rafter = sufR + (br - rx);   // right stops at or after the run's start
+  int sat = 0;
+#pragma unroll
+  for (int e = 0; e < kSelPer; ++e) {
+    const int p = p0 + e;
+    if (!(p >= 1 && p < len)) continue;
+    const bool isl = v[e] <= pv, isr = v[e] >= pv;
+    if (isr) --rafter;  // now: right stops strictly after p
+    if (isl) {
+      ++rankL;
+      if (rafter >= rankL) {
+        posL[rankL - 1] = p;
+        ++sat;
+      }
+    }
+    if (isr && rafter + 1 <= totL + 1) posR[rafter] = p;  // rank rafter+1
+  }
+  int tot;
+  block_exscan(sat, tmp, tot);
+  if (threadIdx.x == 0 && tot) atomicAdd(&s->m, tot);
+}
+
+// step 4: the m swaps, the pivot into its slot, and the split: right part and
+// pivot pushed (the order in which klt_select.c's lazy sort pushes them), the
+// left part becomes the current segment.  The thread of the last swap also
+// moves the pivot (its slot may be that swap's left position).
+__global__ __launch_bounds__(kSelThreads) void k_sel_swap(SelState *s, int2 *__restrict__ kv,
+                                                         const int *__restrict__ posL, const int *__restrict__ posR) {
+  if (s->done) return;
+  const int m = s->m, st = s->start;
+  const int k = blockIdx.x * kSelThreads + threadIdx.x;
+  if (k < m) swap2(kv, st + posL[k], st + posR[k]);
+  if (k == (m > 0 ? m - 1 : 0)) {
+    const int len = s->len;
+    const int jr = m < s->totR ? posR[m] : 0, jl = m > 0 ? posL[m - 1] : 0;
+    const int jf = jr > jl ? jr : jl;
+    swap2(kv, st + jf, st);
+    int ns = s->nstack;
+    if (len - jf - 1 > 0 && ns < kSelStack) {
+      s->stack[2 * ns] = st + jf + 1;
+      s->stack[2 * ns + 1] = len - jf - 1;
+      ++ns;
+    }
+    if (ns < kSelStack) {
+      s->stack[2 * ns] = st + jf;
+      s->stack[2 * ns + 1] = 1;
+      ++ns;
+    }
+    s->nstack = ns;
+    s->len = jf;
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// host driver
+// ---------------------------------------------------------------------------
+struct SelEngine {
+  int2 *d_kv = nullptr;
+  size_t kv_cap = 0;
+  int *d_cnt = nullptr, *d_off = nullptr, *d_posL = nullptr, *d_posR = nullptr;
+  size_t cnt_cap = 0, off_cap = 0, posL_cap = 0, posR_cap = 0;
+  SelState *d_state = nullptr, *h_state = nullptr;
+  int2 *h_kv = nullptr;  // pinned host mirror (segments are copied in as the walk reaches them)
+  size_t hkv_cap = 0;
+  uint8_t *d_map = nullptr;
+  size_t map_cap = 0;
+  float *d_fx = nullptr, *d_fy = nullptr;
+  int *d_fv = nullptr;
+  size_t fx_cap = 0, fy_cap = 0, fv_cap = 0;
+  int threshold = kSelDefaultThreshold;  // segments at most this long go to the host
+  // statistics of the last run
+  long downloaded = 0, device_steps = 0, visited = 0;
+  double us[4] = {};  // host wall clock: map + paint + init queued and drained, device splits, downloads, total
+};
+
+double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+namespace {
+
+#define SELCHK(expr)                                                          \
+  do {                                                                        \
+    hipError_t e_ = (expr);                                                   \
+    if (e_ != hipSuccess) {                                                   \
+      if (err) *err = std::string(#expr) + ": " + hipGetErrorString(e_);     \
+      return -1;                                                              \
+    }                                                                         \
+  } while (0)
+
+template <class T>
+int sel_grow(T **p, size_t *cap, size_t n, std::string *err) {
+  if (*cap >= n && *p) return 0;
+  hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  SELCHK(hipMalloc((void **)p, sizeof(T) * (n ? n : 1)));
+  *cap = n;
+  return 0;
+}
+
+struct Seg {
+  int start, len;
+  bool host;
+};
+
+// the exact partition step of klt_select.c (the reference's _quicksort body)
+// on host pairs {val, idx}
+unsigned host_partition(int2 *a, unsigned n) {
+  unsigned i = 0, j = n;
+  std::swap(a[0], a[n / 2]);
+  const int pv = a[0].x;
+  for (;;) {
+    do --j;
+    while (a[j].x < pv);
+    do ++i;
+    while (i < j && a[i].x > pv);
+    if (i >= j) break;
+    std::swap(a[i], a[j]);
+  }
+  std::swap(a[j], a[0]);
+  return j;
+}
+
+// split device segment g on the device until its leftmost part is at most the
+// threshold; the resulting segments are pushed onto stk (device-resident)
+int dev_refine(SelEngine *e, hipStream_t st, Seg g, std::vector<Seg> &stk, std::string *err) {
+  const double t0 = now_us();
+  struct Acc {
+    SelEngine *e;
+    double t0;
+    ~Acc() { e->us[1] += now_us() - t0; }
+  } acc{e, t0};
+  const int T = e->threshold;
+  const int nb = (g.len + kSelBS - 1) / kSelBS;
+  if (sel_grow(&e->d_cnt, &e->cnt_cap, 2 * (size_t)nb, err) || sel_grow(&e->d_off, &e->off_cap, 2 * (size_t)nb, err) ||
+      sel_grow(&e->d_posL, &e->posL_cap, (size_t)g.len + 1, err) ||
+      sel_grow(&e->d_posR, &e->posR_cap, (size_t)g.len + 1, err))
+    return -1;
+  for (;;) {
+    memset(e->h_state, 0, sizeof(SelState));
+    e->h_state->start = g.start;
+    e->h_state->len = g.len;
+    SELCHK(hipMemcpyAsync(e->d_state, e->h_state, offsetof(SelState, stack), hipMemcpyHostToDevice, st));
+    // splits expected to reach the threshold, plus slack; the loop below
+    // continues if the pivots were unlucky
+    int levels = 2;
+    for (long l = g.len; l > T; l /= 2) ++levels;
+    const int sw = (g.len / 2 + kSelThreads) / kSelThreads;
+    for (int l = 0; l < levels; ++l) {
+      hipLaunchKernelGGL(k_sel_pivot, dim3(1), dim3(1), 0, st, e->d_state, e->d_kv, T);
+      hipLaunchKernelGGL(k_sel_count, dim3(nb), dim3(kSelThreads), 0, st, e->d_state, e->d_kv, e->d_cnt);
+      hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(kSelScanThreads), 0, st, e->d_state, e->d_cnt, e->d_off);
+      hipLaunchKernelGGL(k_sel_rank, dim3(nb), dim3(kSelThreads), 0, st, e->d_state, e->d_kv, e->d_off, e->d_posL,
+                         e->d_posR);
+      hipLaunchKernelGGL(k_sel_swap, dim3(sw), dim3(kSelThreads), 0, st, e->d_state, e->d_kv, e->d_posL, e->d_posR);
+      e->device_steps++;
+    }
+    SELCHK(hipGetLastError());
+    SELCHK(hipMemcpyAsync(e->h_state, e->d_state, sizeof(SelState), hipMemcpyDeviceToHost, st));
+    SELCHK(hipStreamSynchronize(st));
+    const SelState &S = *e->h_state;
+    if (S.nstack >= kSelStack) {
+      if (err) *err = "select: device partition stack overflow";
+      return -1;
+    }
+    for (int k = 0; k < S.nstack; ++k) stk.push_back(Seg{S.stack[2 * k], S.stack[2 * k + 1], false});
+    if (S.done || S.len <= T) {
+      stk.push_back(Seg{S.start, S.len, false});
+      return 0;
+    }
+    g = Seg{S.start, S.len, false};  // unlucky pivots: more steps on what is left
+  }
+}
+
+// the lazy sort: next position in sorted order, or -1 when exhausted
+struct LazySort {
+  SelEngine *e;
+  hipStream_t st;
+  std::vector<Seg> stk;
+  std::string *err;
+  int failed = 0;
+
+  long next() {
+    while (!stk.empty()) {
+      Seg g = stk.back();
+      stk.pop_back();
+      if (g.len <= 0) continue;
+      if (!g.host) {
+        if (g.len > e->threshold) {
+          if (dev_refine(e, st, g, stk, err)) {
+            failed = 1;
+            return -1;
+          }
+          continue;
+        }
+        const double t0 = now_us();
+        if (hipMemcpyAsync(e->h_kv + g.start, e->d_kv + g.start, sizeof(int2) * (size_t)g.len,
+                           hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) {
+          if (err) *err = "select: segment download failed";
+          failed = 1;
+          return -1;
+        }
+        e->downloaded += g.len;
+        e->us[2] += now_us() - t0;
+        g.host = true;
+      }
+      if (g.len == 1) return g.start;
+      const unsigned j = host_partition(e->h_kv + g.start, (unsigned)g.len);
+      stk.push_back(Seg{g.start + (int)j + 1, g.len - (int)j - 1, true});
+      stk.push_back(Seg{g.start + (int)j, 1, true});
+      stk.push_back(Seg{g.start, (int)j, true});
+    }
+    return -1;
+  }
+};
+
+// features accepted during this walk, bucketed for the minimum-distance test
+struct NearGrid {
+  int r, cs, gw, gh;
+  std::vector<std::vector<int2>> cell;
+  NearGrid(int r_, int W, int H) : r(r_) {
+    cs = std::max(2 * r + 1, 32);
+    gw = W / cs + 1;
+    gh = H / cs + 1;
+    cell.resize((size_t)gw * gh);
+  }
+  bool near(int x, int y) const {
+    if (r < 0) return false;
+    const int cx = x / cs, cy = y / cs;
+    for (int j = std::max(cy - 1, 0); j <= std::min(cy + 1, gh - 1); ++j)
+      for (int i = std::max(cx - 1, 0); i <= std::min(cx + 1, gw - 1); ++i)
+        for (const int2 &p : cell[(size_t)j * gw + i])
+          if (abs(p.x - x) <= r && abs(p.y - y) <= r) return true;
+    return false;
+  }
+  void add(int x, int y) { cell[(size_t)(y / cs) * gw + x / cs].push_back(make_int2(x, y)); }
+};
+
+}  // namespace
+
+SelEngine *sel_engine_create() { return new SelEngine(); }
+
+void sel_engine_destroy(SelEngine *e) {
+  if (!e) return;
+  for (void *p : {(void *)e->d_kv, (void *)e->d_cnt, (void *)e->d_off, (void *)e->d_posL, (void *)e->d_posR,
+                  (void *)e->d_state, (void *)e->d_map, (void *)e->d_fx, (void *)e->d_fy, (void *)e->d_fv})
+    hipFree(p);
+  if (e->h_state) hipHostFree(e->h_state);
+  if (e->h_kv) hipHostFree(e->h_kv);
+  delete e;
+}
+
+void sel_engine_set_threshold(SelEngine *e, int t) { e->threshold = t < 1 ? 1 : t; }
+
+void sel_engine_stats(const SelEngine *e, long *downloaded, long *steps, long *visited, double *us) {
+  *downloaded = e->downloaded;
+  *steps = e->device_steps;
+  *visited = e->visited;
+  if (us)
+    for (int k = 0; k < 4; ++k) us[k] = e->us[k];
+}
+
+static int sel_prepare(SelEngine *e, hipStream_t st, const int *dev_vals, int nx, int ny, int bx, int by, int step,
+                       int W, const uint8_t *map, std::string *err) {
+  const size_t n = (size_t)nx * ny;
+  if (sel_grow(&e->d_kv, &e->kv_cap, n, err)) return -1;
+  if (!e->d_state) SELCHK(hipMalloc((void **)&e->d_state, sizeof(SelState)));
+  if (!e->h_state) SELCHK(hipHostMalloc((void **)&e->h_state, sizeof(SelState), hipHostMallocDefault));
+  if (e->hkv_cap < n) {
+    if (e->h_kv) hipHostFree(e->h_kv);
+    e->h_kv = nullptr;
+    e->hkv_cap = 0;
+    SELCHK(hipHostMalloc((void **)&e->h_kv, sizeof(int2) * (n ? n : 1), hipHostMallocDefault));
+    e->hkv_cap = n;
+  }
+  e->downloaded = e->device_steps = e->visited = 0;
+  for (double &u : e->us) u = 0.0;
+  if (n) {
+    hipLaunchKernelGGL(k_sel_init, dim3((unsigned)((n + kSelThreads - 1) / kSelThreads)), dim3(kSelThreads), 0, st,
+                       dev_vals, nx, (int)n, bx, by, step, W, map, e->d_kv);
+    SELCHK(hipGetLastError());
+  }
+  return 0;
+}
+
+// The selection walk of _KLTSelectGoodFeatures (selectGoodFeatures.c:135-239)
+// over the lazily sorted map: x/y/val are the host feature list (in/out);
+// changed[k] = 1 for slots written (a new feature or NOT_FOUND).
+int sel_engine_run(SelEngine *e, hipStream_t st, const int *dev_vals, int nx, int ny, int bx, int by, int step,
+                   int W, int H, int mindist, int min_eigenvalue, int overwrite_all, float *x, float *y, int *val,
+                   unsigned char *changed, int n, std::string *err) {
+  const int r = mindist - 1;  // :157
+  if (min_eigenvalue < 1) min_eigenvalue = 1;
+  for (int k = 0; k < n; ++k) changed[k] = 0;
+  const uint8_t *map = nullptr;
+  if (!overwrite_all && n > 0 && r >= 0) {
+    // the squares of the live features, painted on the device (:160-166)
+    if (sel_grow(&e->d_map, &e->map_cap, (size_t)W * H, err) || sel_grow(&e->d_fx, &e->fx_cap, (size_t)n, err) ||
+        sel_grow(&e->d_fy, &e->fy_cap, (size_t)n, err) || sel_grow(&e->d_fv, &e->fv_cap, (size_t)n, err))
+      return -1;
+    SELCHK(hipMemsetAsync(e->d_map, 0, (size_t)W * H, st));
+    SELCHK(hipMemcpyAsync(e->d_fx, x, sizeof(float) * n, hipMemcpyHostToDevice, st));
+    SELCHK(hipMemcpyAsync(e->d_fy, y, sizeof(float) * n, hipMemcpyHostToDevice, st));
+    SELCHK(hipMemcpyAsync(e->d_fv, val, sizeof(int) * n, hipMemcpyHostToDevice, st));
+    const long cells = (long)n * (2 * r + 1) * (2 * r + 1);
+    hipLaunchKernelGGL(k_sel_paint, dim3((unsigned)((cells + kSelThreads - 1) / kSelThreads)), dim3(kSelThreads), 0,
+                       st, e->d_fx, e->d_fy, e->d_fv, n, r, W, H, e->d_map);
+    SELCHK(hipGetLastError());
+    map = e->d_map;
+  }
+  const double t_start = now_us();
+  if (sel_prepare(e, st, dev_vals, nx, ny, bx, by, step, W, map, err)) return -1;
+  SELCHK(hipStreamSynchronize(st));
+  e->us[0] = now_us() - t_start;
+  const int np = nx * ny;
+  LazySort ls{e, st, {}, err};
+  ls.stk.push_back(Seg{0, np, false});
+  NearGrid near(r, W, H);
+  int k = 0;
+  bool filled = false;
+  for (;;) {
+    const long p = ls.next();
+    if (p < 0) break;
+    e->visited++;
+    const int2 kv = e->h_kv[p];
+    if (kv.x < min_eigenvalue) break;  // descending: nothing else can be accepted
+    const int idx = (int)((unsigned)kv.y & ~kBlockedBit);
+    const int gx = bx + (idx % nx) * step, gy = by + (idx / nx) * step;
+    while (!overwrite_all && k < n && val[k] >= 0) ++k;
+    if (k >= n) {
+      filled = true;
+      break;
+    }
+    if (((unsigned)kv.y & kBlockedBit) || near.near(gx, gy)) continue;
+    x[k] = (float)gx;
+    y[k] = (float)gy;
+    val[k] = kv.x;
+    changed[k] = 1;
+    ++k;
+    if (r >= 0) near.add(gx, gy);
+  }
+  if (ls.failed) return -1;
+  e->us[3] = now_us() - t_start;
+  if (!filled)  // list exhausted: remaining slots become NOT_FOUND (:175-195)
+    for (; k < n; ++k)
+      if (overwrite_all || val[k] < 0) {
+        x[k] = -1.0f;
+        y[k] = -1.0f;
+        val[k] = kNotFound;
+        changed[k] = 1;
+      }
+  return 0;
+}
+
+// test hook: the whole lazy order of vals[0..n) (device array), as
+// klt_sort_pairs_full produces it on the host
+int sel_engine_sort(SelEngine *e, hipStream_t st, const int *dev_vals, int n, int *out_val, int *out_idx,
+                    std::string *err) {
+  if (sel_prepare(e, st, dev_vals, n, 1, 0, 0, 1, n, nullptr, err)) return -1;
+  LazySort ls{e, st, {}, err};
+  ls.stk.push_back(Seg{0, n, false});
+  int k = 0;
+  for (long p; (p = ls.next()) >= 0;) {
+    out_val[k] = e->h_kv[p].x;
+    out_idx[k] = e->h_kv[p].y;
+    ++k;
+  }
+  if (ls.failed) return -1;
+  if (k != n) {
+    if (err) *err = "select: lazy order lost elements";
+    return -1;
+  }
+  return 0;
+}
+
+}  // namespace kltdev

@@ -31,11 +31,12 @@ struct klt_shard {
   int row_lo = 0, row_hi = 0;           // level-0 rows built
   int load_lo = 0, load_hi = 0;         // u8 rows the band build reads
   ncclComm_t comm = nullptr;
-  int *d_buf = nullptr;                 // 3n+1 int32: x | y | val bit patterns, escape flag
+  int *d_buf = nullptr;                 // 3n+2 int32: x | y | val bit patterns, escape flag, error count
   float *d_x0 = nullptr, *d_y0 = nullptr;
   int *d_v0 = nullptr;                  // chunk-start state (ownership, redo)
   size_t cap = 0;
-  int *h_flag = nullptr;                // pinned: the summed escape flag
+  int *h_flag = nullptr;                // pinned: the summed escape flag and error count
+  bool dead = false;                    // the communicator was aborted (a rank could not take part)
   int *d_map = nullptr;                 // the trackability map (replacement)
   size_t map_cap = 0;
   std::string err;
@@ -64,20 +65,44 @@ int sfail(klt_shard *s, const char *fmt, ...) {
     if (r_ != ncclSuccess) return sfail(s, "%s: %s", #call, ncclGetErrorString(r_));      \
   } while (0)
 
+// The caller's current device is restored when an entry point returns.
+struct DeviceGuard {
+  int dev = -1;
+  DeviceGuard() {
+    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  }
+  ~DeviceGuard() {
+    if (dev >= 0) (void)hipSetDevice(dev);
+  }
+};
+
+// A rank that cannot take part in the next collective (its buffers could not
+// be allocated) aborts the communicator, so that its peers' collectives fail
+// instead of waiting for it; the shard is unusable afterwards.
+int abort_comm(klt_shard *s, const char *what) {
+  if (s->comm && !s->dead) ncclCommAbort(s->comm);
+  s->comm = nullptr;
+  s->dead = true;
+  return sfail(s, "%s (communicator aborted)", what);
+}
+
 // the owners' bit patterns, zero elsewhere (rank 0 also contributes the lost
 // features, which nobody tracks); the escape flag as the last element
 __global__ void k_shard_pack(const float *__restrict__ x, const float *__restrict__ y, const int *__restrict__ v,
                              const float *__restrict__ y0, const int *__restrict__ v0, float own_lo, float own_hi,
-                             int rank0, const int *__restrict__ escape, int *__restrict__ buf, int n) {
+                             int rank0, const int *__restrict__ escape, int failed, int *__restrict__ buf, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
-    const bool owned = v0[i] >= 0 && y0[i] >= own_lo && y0[i] < own_hi;  // k_band_order's test
-    const bool keep = owned || (rank0 && v0[i] < 0);
+    const bool owned = !failed && v0[i] >= 0 && y0[i] >= own_lo && y0[i] < own_hi;  // k_band_order's test
+    const bool keep = owned || (!failed && rank0 && v0[i] < 0);
     buf[i] = keep ? __float_as_int(x[i]) : 0;
     buf[n + i] = keep ? __float_as_int(y[i]) : 0;
     buf[2 * n + i] = keep ? v[i] : 0;
   }
-  if (i == 0) buf[3 * n] = escape ? *escape : 0;
+  if (i == 0) {
+    buf[3 * n] = escape && !failed ? *escape : 0;
+    buf[3 * n + 1] = failed;
+  }
 }
 
 __global__ void k_shard_unpack(const int *__restrict__ buf, float *__restrict__ x, float *__restrict__ y,
@@ -100,7 +125,7 @@ int grow_buffers(klt_shard *s, int n) {
   s->d_v0 = nullptr;
   s->cap = 0;
   const size_t m = n > 0 ? (size_t)n : 1;
-  SHIP(s, hipMalloc((void **)&s->d_buf, (3 * m + 1) * sizeof(int)));
+  SHIP(s, hipMalloc((void **)&s->d_buf, (3 * m + 2) * sizeof(int)));
   SHIP(s, hipMalloc((void **)&s->d_x0, m * sizeof(float)));
   SHIP(s, hipMalloc((void **)&s->d_y0, m * sizeof(float)));
   SHIP(s, hipMalloc((void **)&s->d_v0, m * sizeof(int)));
@@ -109,19 +134,34 @@ int grow_buffers(klt_shard *s, int n) {
 }
 
 // pack this rank's results, all-reduce them with every rank's, unpack; the
-// summed escape flag lands in *s->h_flag (synchronous)
-int exchange(klt_shard *s, hipStream_t st, float *x, float *y, int *v, int n, const int *escape) {
+// summed escape flag lands in h_flag[0], the number of ranks that failed this
+// step (failed != 0: this one, which contributes nothing else) in h_flag[1].
+// Every rank calls it at the same point whatever went wrong locally, so no
+// peer waits in the collective for a rank that returned early; a nonzero
+// error count makes every rank return an error.  Synchronous.
+int exchange(klt_shard *s, hipStream_t st, float *x, float *y, int *v, int n, const int *escape, int failed) {
   const int nb = (n + 255) / 256 > 0 ? (n + 255) / 256 : 1;
   hipLaunchKernelGGL(k_shard_pack, dim3(nb), dim3(256), 0, st, x, y, v, s->d_y0, s->d_v0, s->own_lo, s->own_hi,
-                     s->rank == 0 ? 1 : 0, escape, s->d_buf, n);
+                     s->rank == 0 ? 1 : 0, escape, failed ? 1 : 0, s->d_buf, n);
   SHIP(s, hipGetLastError());
-  SNCCL(s, ncclAllReduce(s->d_buf, s->d_buf, (size_t)3 * n + 1, ncclInt32, ncclSum, s->comm, st));
-  if (n > 0) {
+  SNCCL(s, ncclAllReduce(s->d_buf, s->d_buf, (size_t)3 * n + 2, ncclInt32, ncclSum, s->comm, st));
+  SHIP(s, hipMemcpyAsync(s->h_flag, s->d_buf + (size_t)3 * n, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+  SHIP(s, hipStreamSynchronize(st));
+  if (s->h_flag[1] == 0 && n > 0) {
     hipLaunchKernelGGL(k_shard_unpack, dim3(nb), dim3(256), 0, st, s->d_buf, x, y, v, n);
     SHIP(s, hipGetLastError());
   }
-  SHIP(s, hipMemcpyAsync(s->h_flag, s->d_buf + (size_t)3 * n, sizeof(int), hipMemcpyDeviceToHost, st));
+  return 0;
+}
+
+// one int32 all-reduce of this rank's failure flag: how many ranks failed
+int agree(klt_shard *s, hipStream_t st, int failed, int *failed_ranks) {
+  int *w = s->d_buf + (size_t)3 * s->cap + 1;
+  SHIP(s, hipMemcpyAsync(w, &failed, sizeof(int), hipMemcpyHostToDevice, st));
+  SNCCL(s, ncclAllReduce(w, w, 1, ncclInt32, ncclSum, s->comm, st));
+  SHIP(s, hipMemcpyAsync(s->h_flag + 1, w, sizeof(int), hipMemcpyDeviceToHost, st));
   SHIP(s, hipStreamSynchronize(st));
+  *failed_ranks = s->h_flag[1];
   return 0;
 }
 
@@ -161,7 +201,7 @@ klt_shard *make_shard(klt_hip_ctx *ctx, int rank, int world, const unsigned char
   ncclUniqueId u;
   memcpy(&u, id, sizeof u);
   if (hipSetDevice(klt_hip_ctx_device(ctx)) != hipSuccess || ncclCommInitRank(&s->comm, cranks, u, crank) != ncclSuccess ||
-      hipHostMalloc((void **)&s->h_flag, sizeof(int), hipHostMallocDefault) != hipSuccess) {
+      hipHostMalloc((void **)&s->h_flag, 2 * sizeof(int), hipHostMallocDefault) != hipSuccess) {
     if (s->comm) ncclCommDestroy(s->comm);
     delete s;
     return nullptr;
@@ -208,45 +248,59 @@ KLT_API int klt_shard_track(klt_shard *s, const klt_hip_pyr_desc *pd, const klt_
                             const unsigned char *frames, long pitch, long stride, int nframes,
                             const unsigned char *next_frames, int next_nframes, float *x, float *y, int *val, int n,
                             klt_shard_frames_fn full, void *user) {
+  // argument errors return before any collective: they are the same on every
+  // rank of a caller that passes every rank the same frames and features
   if (!s || !pd || !td) return sfail(s, "shard_track: null argument");
+  if (s->dead) return sfail(s, "shard_track: the communicator was aborted");
   if (pd->nrows != s->nrows) return sfail(s, "shard_track: frames have %d rows, the shard %d", pd->nrows, s->nrows);
   if (n < 0 || nframes < 1 || !frames || (n > 0 && (!x || !y || !val)))
     return sfail(s, "shard_track: bad frames or feature arrays");
-  if (hipSetDevice(klt_hip_ctx_device(s->ctx)) != hipSuccess) return sfail(s, "shard_track: device");
+  DeviceGuard guard;
+  if (hipSetDevice(klt_hip_ctx_device(s->ctx)) != hipSuccess) return abort_comm(s, "shard_track: device");
   hipStream_t st = (hipStream_t)klt_hip_get_stream(s->ctx);
-  if (grow_buffers(s, n)) return -1;
+  if (grow_buffers(s, n)) return abort_comm(s, ("shard_track: " + s->err).c_str());
   // the chunk-start state: ownership (y0, v0) and the redo's starting point
   const size_t fb = sizeof(float) * (size_t)n;
-  if (n > 0) {
-    SHIP(s, hipMemcpyAsync(s->d_x0, x, fb, hipMemcpyDeviceToDevice, st));
-    SHIP(s, hipMemcpyAsync(s->d_y0, y, fb, hipMemcpyDeviceToDevice, st));
-    SHIP(s, hipMemcpyAsync(s->d_v0, val, fb, hipMemcpyDeviceToDevice, st));
-  }
-  int *escape = s->d_buf + (size_t)3 * s->cap;  // the buffer's last slot doubles as the device flag
-  SHIP(s, hipMemsetAsync(escape, 0, sizeof(int), st));
-  if (klt_hip_track_frames_band(s->ctx, pd, td, frames, pitch, stride, nframes, x, y, val, n, s->own_lo, s->own_hi,
+  std::string local;  // this rank's failure, if any: it still takes part in every exchange
+  if (n > 0 &&
+      (hipMemcpyAsync(s->d_x0, x, fb, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+       hipMemcpyAsync(s->d_y0, y, fb, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+       hipMemcpyAsync(s->d_v0, val, fb, hipMemcpyDeviceToDevice, st) != hipSuccess))
+    local = "chunk-start copy failed";
+  int *escape = s->d_buf + (size_t)3 * s->cap;  // the buffer's slot after the features doubles as the device flag
+  if (local.empty() && hipMemsetAsync(escape, 0, sizeof(int), st) != hipSuccess) local = "escape flag reset failed";
+  if (local.empty() &&
+      klt_hip_track_frames_band(s->ctx, pd, td, frames, pitch, stride, nframes, x, y, val, n, s->own_lo, s->own_hi,
                                 s->row_lo, s->row_hi, escape, next_frames, next_nframes))
-    return sfail(s, "shard_track: %s", klt_hip_last_error(s->ctx));
-  if (exchange(s, st, x, y, val, n, escape)) return -1;
-  if (*s->h_flag == 0) return 0;
+    local = klt_hip_last_error(s->ctx);
+  if (exchange(s, st, x, y, val, n, escape, !local.empty())) return abort_comm(s, ("shard_track: " + s->err).c_str());
+  if (s->h_flag[1]) {
+    return local.empty() ? sfail(s, "shard_track: %d peer rank(s) failed this chunk", s->h_flag[1])
+                         : sfail(s, "shard_track: %s", local.c_str());
+  }
+  if (s->h_flag[0] == 0) return 0;
   // some rank's window left its built rows: every rank redoes the chunk from
   // whole frames (exact whatever the motion) and exchanges again
-  if (!full) return sfail(s, "shard_track: chunk escaped its band and no whole-frame callback was given");
   const unsigned char *whole = nullptr;
   long wstride = 0;
-  if (full(user, &whole, &wstride) || !whole) return sfail(s, "shard_track: whole-frame callback failed");
-  if (n > 0) {
-    SHIP(s, hipMemcpyAsync(x, s->d_x0, fb, hipMemcpyDeviceToDevice, st));
-    SHIP(s, hipMemcpyAsync(y, s->d_y0, fb, hipMemcpyDeviceToDevice, st));
-    SHIP(s, hipMemcpyAsync(val, s->d_v0, fb, hipMemcpyDeviceToDevice, st));
-  }
-  if (klt_hip_frames_begin(s->ctx, pd, whole, pitch))
-    return sfail(s, "shard_track: redo: %s", klt_hip_last_error(s->ctx));
-  SHIP(s, hipMemsetAsync(escape, 0, sizeof(int), st));
-  if (klt_hip_track_frames_band(s->ctx, pd, td, whole + wstride, pitch, wstride, nframes, x, y, val, n, s->own_lo,
+  if (!full) local = "chunk escaped its band and no whole-frame callback was given";
+  else if (full(user, &whole, &wstride) || !whole) local = "whole-frame callback failed";
+  if (local.empty() && n > 0 &&
+      (hipMemcpyAsync(x, s->d_x0, fb, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+       hipMemcpyAsync(y, s->d_y0, fb, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+       hipMemcpyAsync(val, s->d_v0, fb, hipMemcpyDeviceToDevice, st) != hipSuccess))
+    local = "redo: chunk-start copy failed";
+  if (local.empty() && klt_hip_frames_begin(s->ctx, pd, whole, pitch))
+    local = std::string("redo: ") + klt_hip_last_error(s->ctx);
+  if (local.empty() && hipMemsetAsync(escape, 0, sizeof(int), st) != hipSuccess) local = "redo: escape flag reset failed";
+  if (local.empty() &&
+      klt_hip_track_frames_band(s->ctx, pd, td, whole + wstride, pitch, wstride, nframes, x, y, val, n, s->own_lo,
                                 s->own_hi, 0, s->nrows, escape, nullptr, 0))
-    return sfail(s, "shard_track: redo: %s", klt_hip_last_error(s->ctx));
-  if (exchange(s, st, x, y, val, n, nullptr)) return -1;
+    local = std::string("redo: ") + klt_hip_last_error(s->ctx);
+  if (exchange(s, st, x, y, val, n, nullptr, !local.empty())) return abort_comm(s, ("shard_track: " + s->err).c_str());
+  if (s->h_flag[1])
+    return local.empty() ? sfail(s, "shard_track: %d peer rank(s) failed the redo", s->h_flag[1])
+                         : sfail(s, "shard_track: %s", local.c_str());
   return 1;
 }
 
@@ -264,6 +318,7 @@ KLT_API int klt_shard_eigen(klt_shard *s, const klt_hip_pyr_desc *pd, const klt_
                             int *dev_map, klt_shard_frames_fn full, void *user) {
   if (!s || !pd || !sd || !dev_map) return sfail(s, "shard_eigen: null argument");
   if (pd->nrows != s->nrows) return sfail(s, "shard_eigen: frames have %d rows, the shard %d", pd->nrows, s->nrows);
+  DeviceGuard guard;
   if (hipSetDevice(klt_hip_ctx_device(s->ctx)) != hipSuccess) return sfail(s, "shard_eigen: device");
   int lo, hi, nx, ny, j0, j1;
   own_rows(s, s->rank, &lo, &hi);
@@ -284,45 +339,35 @@ KLT_API int klt_shard_eigen(klt_shard *s, const klt_hip_pyr_desc *pd, const klt_
 
 KLT_API int klt_hip_select_map(klt_hip_ctx *ctx, int ncols, int nrows, const klt_hip_select_desc *sd, int mindist,
                                int min_eigenvalue, const int *dev_map, float *x, float *y, int *val, int n) {
-  if (!ctx || !sd || !dev_map || ncols < 1 || nrows < 1 || n < 0 || (n > 0 && (!x || !y || !val))) return -1;
-  if (hipSetDevice(klt_hip_ctx_device(ctx)) != hipSuccess) return -1;
+  if (!ctx || !sd || !dev_map || ncols < 1 || nrows < 1 || n < 0 || (n > 0 && (!x || !y || !val)))
+    return ctx ? kltdev::ctx_fail(ctx, "select_map: bad argument") : -1;
+  DeviceGuard guard;
+  if (hipSetDevice(klt_hip_ctx_device(ctx)) != hipSuccess) return kltdev::ctx_fail(ctx, "select_map: hipSetDevice failed");
   int nx, ny, j0, j1;
-  if (klt_hip_min_eigen_rows(ctx, sd, 0, 0, nullptr, &nx, &ny, &j0, &j1) < 0) return -1;
+  if (klt_hip_min_eigen_rows(ctx, sd, 0, 0, nullptr, &nx, &ny, &j0, &j1) < 0) return -1;  // its own message
   hipStream_t st = (hipStream_t)klt_hip_get_stream(ctx);
-  std::vector<int> map((size_t)nx * ny + 1);
   std::vector<float> hx(n > 0 ? n : 1), hy(n > 0 ? n : 1);
   std::vector<int> hv(n > 0 ? n : 1);
+  std::vector<unsigned char> changed(n > 0 ? n : 1);
   bool ok = true;
-  if ((size_t)nx * ny)
-    ok = ok && hipMemcpyAsync(map.data(), dev_map, sizeof(int) * (size_t)nx * ny, hipMemcpyDeviceToHost, st) == hipSuccess;
   if (n > 0) {
     ok = ok && hipMemcpyAsync(hx.data(), x, sizeof(float) * n, hipMemcpyDeviceToHost, st) == hipSuccess;
     ok = ok && hipMemcpyAsync(hy.data(), y, sizeof(float) * n, hipMemcpyDeviceToHost, st) == hipSuccess;
     ok = ok && hipMemcpyAsync(hv.data(), val, sizeof(int) * n, hipMemcpyDeviceToHost, st) == hipSuccess;
   }
-  if (!ok || hipStreamSynchronize(st) != hipSuccess) return -1;
-  // the host half of KLTReplaceLostFeatures (klt_api.c select_features), the
-  // same code on every rank over the same map and list: identical results
-  KLT_FeatureList fl = KLTCreateFeatureList(n);
-  for (int i = 0; i < n; ++i) {
-    fl->feature[i]->x = hx[i];
-    fl->feature[i]->y = hy[i];
-    fl->feature[i]->val = hv[i];
-  }
-  klt_select_from_map(map.data(), nx, ny, sd->borderx, sd->bordery, sd->nSkippedPixels + 1, ncols, nrows, fl,
-                      mindist < 0 ? 0 : mindist, min_eigenvalue, 0);
-  for (int i = 0; i < n; ++i) {
-    hx[i] = fl->feature[i]->x;
-    hy[i] = fl->feature[i]->y;
-    hv[i] = fl->feature[i]->val;
-  }
-  KLTFreeFeatureList(fl);
+  if (!ok || hipStreamSynchronize(st) != hipSuccess) return kltdev::ctx_fail(ctx, "select_map: feature download failed");
+  // the walk of KLTReplaceLostFeatures (klt_api.c select_features) over the
+  // map on the device, the same on every rank over the same map and list:
+  // identical results
+  if (klt_hip_select_dev_map(ctx, dev_map, nx, ny, sd, ncols, nrows, mindist, min_eigenvalue, 0, hx.data(),
+                             hy.data(), hv.data(), changed.data(), n))
+    return -1;
   if (n > 0) {
     ok = hipMemcpyAsync(x, hx.data(), sizeof(float) * n, hipMemcpyHostToDevice, st) == hipSuccess &&
          hipMemcpyAsync(y, hy.data(), sizeof(float) * n, hipMemcpyHostToDevice, st) == hipSuccess &&
          hipMemcpyAsync(val, hv.data(), sizeof(int) * n, hipMemcpyHostToDevice, st) == hipSuccess &&
          hipStreamSynchronize(st) == hipSuccess;
-    if (!ok) return -1;
+    if (!ok) return kltdev::ctx_fail(ctx, "select_map: feature upload failed");
   }
   return 0;
 }
@@ -339,24 +384,33 @@ KLT_API int klt_shard_replace(klt_shard *s, const klt_hip_pyr_desc *pd, const kl
                               int mindist, int min_eigenvalue, float *x, float *y, int *val, int n,
                               klt_shard_frames_fn full, void *user) {
   if (!s || !pd || !sd) return sfail(s, "shard_replace: null argument");
+  if (s->dead) return sfail(s, "shard_replace: the communicator was aborted");
   if (s->cranks != s->world)
     return sfail(s, "shard_replace: a local shard has no peers (use klt_shard_eigen and klt_shard_select)");
-  if (hipSetDevice(klt_hip_ctx_device(s->ctx)) != hipSuccess) return sfail(s, "shard_replace: device");
+  DeviceGuard guard;
+  if (hipSetDevice(klt_hip_ctx_device(s->ctx)) != hipSuccess) return abort_comm(s, "shard_replace: device");
+  if (grow_buffers(s, n)) return abort_comm(s, ("shard_replace: " + s->err).c_str());
+  hipStream_t st = (hipStream_t)klt_hip_get_stream(s->ctx);
   int nx, ny, j0, j1;
-  if (klt_hip_min_eigen_rows(s->ctx, sd, 0, 0, nullptr, &nx, &ny, &j0, &j1) < 0)
-    return sfail(s, "shard_replace: %s", klt_hip_last_error(s->ctx));
-  const size_t np = (size_t)nx * ny;
-  if (np > s->map_cap) {
+  std::string local;  // this rank's failure: it still joins the agreement below
+  if (klt_hip_min_eigen_rows(s->ctx, sd, 0, 0, nullptr, &nx, &ny, &j0, &j1) < 0) local = klt_hip_last_error(s->ctx);
+  const size_t np = local.empty() ? (size_t)nx * ny : 0;
+  if (local.empty() && np > s->map_cap) {
     hipFree(s->d_map);
     s->d_map = nullptr;
     s->map_cap = 0;
-    SHIP(s, hipMalloc((void **)&s->d_map, np * sizeof(int)));
-    s->map_cap = np;
+    if (hipMalloc((void **)&s->d_map, np * sizeof(int)) != hipSuccess) local = "map allocation failed";
+    else s->map_cap = np;
   }
-  const int rc = np ? klt_shard_eigen(s, pd, sd, pitch, s->d_map, full, user) : 0;
-  if (rc < 0) return rc;
+  if (local.empty() && np && klt_shard_eigen(s, pd, sd, pitch, s->d_map, full, user) < 0) local = s->err;
+  // every rank learns whether any rank failed before the broadcasts, so that
+  // none of them waits in a broadcast that a failed rank never joins
+  int failed = 0;
+  if (agree(s, st, local.empty() ? 0 : 1, &failed)) return abort_comm(s, ("shard_replace: " + s->err).c_str());
+  if (failed)
+    return local.empty() ? sfail(s, "shard_replace: %d peer rank(s) failed the trackability map", failed)
+                         : sfail(s, "shard_replace: %s", local.c_str());
   // every rank's grid rows to every rank: one broadcast per owner, grouped
-  hipStream_t st = (hipStream_t)klt_hip_get_stream(s->ctx);
   if (np) {
     SNCCL(s, ncclGroupStart());
     for (int r = 0; r < s->world; ++r) {

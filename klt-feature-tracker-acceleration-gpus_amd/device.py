@@ -57,6 +57,7 @@ DEVICE_PROTOS = {
     "klt_hip_get_stream": (V, [V]),
     "klt_hip_sync": (C.c_int, [V]),
     "klt_hip_device_count": (C.c_int, []),
+    "klt_hip_current_device": (C.c_int, []),
     "klt_hip_upload_frame": (C.c_int, [V, C.c_int, V, C.c_int, C.c_int]),
     "klt_hip_build_pyramid": (C.c_int, [V, C.c_int, C.POINTER(PyrDesc), V, C.c_long, C.c_int]),
     "klt_hip_pyramid_path": (C.c_int, [V, C.c_int]),
@@ -104,6 +105,13 @@ DEVICE_PROTOS = {
     "klt_shard_select": (C.c_int, [V, C.POINTER(PyrDesc), V, C.c_int, C.c_int, V, V, V, V, C.c_int]),
     "klt_shard_replace": (C.c_int, [V, C.POINTER(PyrDesc), V, C.c_long, C.c_int, C.c_int, V, V, V, C.c_int, V, V]),
     "klt_hip_min_eigen": (C.c_int, [V, C.c_int, C.POINTER(SelectDesc), V, IP, IP]),
+    "klt_hip_select": (C.c_int, [V, C.c_int, C.POINTER(SelectDesc), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                 V, V, V, V, C.c_int]),
+    "klt_hip_select_dev_map": (C.c_int, [V, V, C.c_int, C.c_int, C.POINTER(SelectDesc), C.c_int, C.c_int,
+                                         C.c_int, C.c_int, C.c_int, V, V, V, V, C.c_int]),
+    "klt_hip_select_tune": (C.c_int, [V, C.c_int]),
+    "klt_hip_select_stats": (C.c_int, [V, C.POINTER(C.c_long), C.POINTER(C.c_long), C.POINTER(C.c_long), DP]),
+    "klt_hip_select_sort_test": (C.c_int, [V, V, C.c_int, V, V]),
     "klt_hip_synth_rows": (C.c_int, [V, C.c_ulonglong, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, V,
                                      C.c_long, C.c_long]),
     "klt_hip_synth_frames": (C.c_int, [V, C.c_ulonglong, C.c_int, C.c_int, C.c_int, C.c_int, V,

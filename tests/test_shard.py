@@ -497,6 +497,18 @@ def test_c_shard_errors(gpu):
     rc = gpu.klt_shard_track(s, C.byref(rk.pd), C.byref(rk.td), C.c_void_p(dfr.data_ptr() + H * W), W, H * W, 2,
                              None, 0, *ptrs, None, None)
     assert rc < 0 and b"callback" in gpu.klt_shard_last_error(s)
+    # a whole-frame callback that fails: the rank still joins the redo's exchange, then reports it
+    calls = [0]
+
+    def broken(user, frames_out, stride_out):
+        calls[0] += 1
+        return 1
+    cb = _FRAMES_FN(broken)
+    x.copy_(x0), y.copy_(y0), v.copy_(v0)
+    rc = gpu.klt_shard_track(s, C.byref(rk.pd), C.byref(rk.td), C.c_void_p(dfr.data_ptr() + H * W), W, H * W, 2,
+                             None, 0, *ptrs, cb, None)
+    assert rc < 0 and b"whole-frame callback failed" in gpu.klt_shard_last_error(s) and calls[0] == 1
+    assert gpu.klt_hip_current_device() == 0
     tc = rk.tc.contents
     sd = SelectDesc(tc.window_width, tc.window_height, max(tc.borderx, 3), max(tc.bordery, 3), tc.nSkippedPixels)
     x.copy_(x0), y.copy_(y0), v.copy_(v0)
