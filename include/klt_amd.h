@@ -21,6 +21,15 @@ klt_hip_ctx *klt_amd_device_context(KLT_TrackingContext tc);
    trimmed to 2 GiB) for the next KLTCreateTrackingContext on the same device.
    This destroys the parked ones and returns their memory; returns how many. */
 int klt_amd_release_cached_devices(void);
+/* Opt-in for callers that reuse fixed frame buffers (example3.c's img1 and
+   img2): page-lock [ptr, ptr+bytes) once, so that every KLTTrackFeatures /
+   KLTSelectGoodFeatures / KLTReplaceLostFeatures on a frame inside it uploads
+   the frame by one DMA from the caller's pages instead of copying it into
+   pinned staging first.  Results are unchanged.  The buffer stays registered
+   until klt_amd_unregister_buffer or KLTFreeTrackingContext; it must stay
+   allocated that long.  0 on success, -1 (with a KLTWarning) otherwise. */
+int klt_amd_register_buffer(KLT_TrackingContext tc, const void *ptr, size_t bytes);
+int klt_amd_unregister_buffer(KLT_TrackingContext tc, const void *ptr);
 /* the descriptors KLTTrackFeatures would build for this context */
 void klt_amd_pyr_desc(KLT_TrackingContext tc, int ncols, int nrows, int nlevels, int smooth,
                       klt_hip_pyr_desc *desc);

@@ -129,6 +129,10 @@ int klt_hip_set_path(klt_hip_ctx *ctx, int force_generic);
 /* tuning hook: 1 tracks features in input order; 0 (default) in row-band
    order with each XCD given one band (L2 locality).  Results do not depend on it. */
 int klt_hip_set_track_order(klt_hip_ctx *ctx, int input_order);
+/* tracker kernel for the default configuration (7x7 window, exact sums, no
+   gain/bias): 0 (default) the latency-lean k_track7 (track7.hip), 1 the
+   generic k_track_frames_g; identical results (A/B hook) */
+int klt_hip_set_track_impl(klt_hip_ctx *ctx, int impl);
 /* tuning hook: 1 (default) folds the finest level's residue pass of frame j
    into the first pass of frame j+1 within a batched launch (one-feature
    waves, exact sums, default gain): its gather goes out with that pass's and
@@ -157,6 +161,14 @@ int klt_hip_set_prof(klt_hip_ctx *ctx, void *dev);
    into pinned staging, table-row delivery); 0..16, default 7 */
 int klt_hip_set_host_threads(klt_hip_ctx *ctx, int workers);
 int klt_hip_get_host_threads(klt_hip_ctx *ctx);
+/* Page-lock a caller buffer (hipHostRegister) so that frames inside it are
+   uploaded by one DMA from the caller's pages, without the copy into pinned
+   staging; for callers that reuse fixed frame buffers (the reference harness:
+   img1/img2, example3.c:45-46,56,75).  Registered buffers must not overlap;
+   they are released by klt_hip_unregister_host (after the context's streams
+   drain), when the context is reset (parked) or destroyed. */
+int klt_hip_register_host(klt_hip_ctx *ctx, const void *ptr, size_t bytes);
+int klt_hip_unregister_host(klt_hip_ctx *ctx, const void *ptr);
 /* Byte budget of the three pyramid banks of klt_hip_track_frames* (one device
    arena per context; 0 restores the default: a quarter of the device memory,
    at most 64 GiB).  A klt_hip_track_frames call whose chunk does not fit runs

@@ -105,6 +105,26 @@ static void release_device(klt_hip_ctx *dev)
   if (!kept) klt_hip_ctx_destroy(dev);
 }
 
+int klt_amd_register_buffer(KLT_TrackingContext tc, const void *ptr, size_t bytes)
+{
+  klt_hip_ctx *dev = device_of(tc);
+  if (klt_hip_register_host(dev, ptr, bytes) != 0) {
+    KLTWarning("(klt_amd_register_buffer) %s", klt_hip_last_error(dev));
+    return -1;
+  }
+  return 0;
+}
+
+int klt_amd_unregister_buffer(KLT_TrackingContext tc, const void *ptr)
+{
+  klt_hip_ctx *dev = device_of(tc);
+  if (klt_hip_unregister_host(dev, ptr) != 0) {
+    KLTWarning("(klt_amd_unregister_buffer) %s", klt_hip_last_error(dev));
+    return -1;
+  }
+  return 0;
+}
+
 int klt_amd_release_cached_devices(void)
 {
   klt_hip_ctx *park[DEV_CACHE];

@@ -167,6 +167,10 @@ hipError_t launch_selftest_div(const float *a, const float *b, float *out, int n
 // and the compiled-in 7x7 window, npx the pixels-per-lane instance
 hipError_t launch_track_frames(hipStream_t st, bool exact, bool li, bool patch, bool win7, int npx,
                                const TrkArgs &a, const TrkFramesArgs &b, float *x, float *y, int *v, int n);
+// track7.hip: the default configuration (7x7 window, exact sums, no gain/bias,
+// one wave per feature) with the latency-lean pass; band: escape checks
+hipError_t launch_track7(hipStream_t st, bool band, const TrkArgs &a, const TrkFramesArgs &b, float *x, float *y,
+                         int *v, int n);
 // band-sorted processing order (one workgroup); count != nullptr: keep only
 // live features with own_lo <= y < own_hi and store how many
 hipError_t launch_band_order(hipStream_t st, const float *fy, const int *fv, int n, int nrows, int *perm,

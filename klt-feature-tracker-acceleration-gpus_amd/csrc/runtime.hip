@@ -152,6 +152,11 @@ struct klt_hip_ctx {
   int *d_eig = nullptr;
   size_t eig_cap = 0;
   SelEngine *sel = nullptr;  // select.hip: the lazy exact selection
+  // caller buffers registered with klt_hip_register_host (page-locked): frame
+  // uploads from inside one are one DMA from the caller's pages, no staging
+  std::vector<std::pair<const unsigned char *, size_t>> registered;
+  std::vector<const unsigned char *> registered_dev;  // their device-side addresses (mapped)
+  const unsigned char *u8_mapped[2] = {nullptr, nullptr};  // upload slot b reads the caller's pages directly
   // affine consistency check: stored windows (3*aff_S floats per feature) and per-call arrays
   float *d_aff_store = nullptr;
   size_t aff_store_cap = 0;
@@ -165,6 +170,7 @@ struct klt_hip_ctx {
   int track_order = 0;  // 0: band-sorted, XCD-major processing order; 1: input order
   int track_patch = 1;  // one-feature waves gather through a lane patch when the window fits
   int track_merge = 1;   // defer finest-level residues into the next frame's first pass (ResCarry)
+  int track_impl = 0;    // 0: track7.hip for the default configuration, 1: the generic k_track_frames_g
   int serial_frames = 1;  // klt_hip_track_frames: 1 builds and tracks on one stream (default: the
                           // tracker and the pyramid kernels compete for the same CUs; overlap buys ~3 %)
   int *d_perm = nullptr;
@@ -548,6 +554,15 @@ int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc
   const TrkFramesArgs &b2 = bb;
   TrkArgs aa = a;
   aa.merge_res = c->track_merge;
+  // the default configuration: the latency-lean kernel (track7.hip) unless
+  // the context asks for the generic one (klt_hip_set_track_impl, A/B only)
+#ifdef KLT_TRACK_PROF
+  const bool prof_ok = true;  // the instrumented build instruments both kernels
+#else
+  const bool prof_ok = !c->prof;
+#endif
+  if (c->track_impl == 0 && win7 && exact && !li && c->track_patch && prof_ok)
+    return launched(c, "k_track7", launch_track7(st, aa.escape != nullptr, aa, b2, x, y, v, n));
   return launched(c, "k_track_frames", launch_track_frames(st, exact, li, patch, win7, npx, aa, b2, x, y, v, n));
 }
 
@@ -816,6 +831,7 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
   if (c->h_feat) hipHostFree(c->h_feat);
   hipFree(c->d_eig);
   sel_engine_destroy(c->sel);
+  for (auto &r : c->registered) (void)hipHostUnregister(const_cast<unsigned char *>(r.first));
   for (void *p : {(void *)c->d_aff_store, (void *)c->d_aff, (void *)c->d_xp, (void *)c->d_yp, (void *)c->d_astage,
                   (void *)c->d_astate, (void *)c->d_aidx})
     hipFree(p);
@@ -891,6 +907,10 @@ KLT_API int klt_hip_ctx_reset(klt_hip_ctx *c) {
     c->copy_threads = 7;
   }
   c->feat_zero_copy = 1;
+  for (auto &r : c->registered) (void)hipHostUnregister(const_cast<unsigned char *>(r.first));
+  c->registered.clear();
+  c->registered_dev.clear();
+  c->u8_mapped[0] = c->u8_mapped[1] = nullptr;
   if (c->sel) sel_engine_set_threshold(c->sel, kSelDefaultThreshold);
   c->bank_budget = 0;
   c->chunk_used = 0;
@@ -899,6 +919,7 @@ KLT_API int klt_hip_ctx_reset(klt_hip_ctx *c) {
   c->track_order = 0;
   c->track_patch = 1;
   c->track_merge = 1;
+  c->track_impl = 0;
   c->serial_frames = 1;
   c->prof = nullptr;
   c->frames_ready = false;
@@ -953,6 +974,24 @@ KLT_API int klt_hip_upload_frame(klt_hip_ctx *c, int buf, const unsigned char *h
     }
     c->u8_cap = n;
   }
+  c->u8_mapped[buf] = nullptr;
+  // a frame inside a registered caller buffer: one DMA straight from it, or
+  // (KLT_MAPPED_FRAMES=1, experiment) no copy at all: the level-0 kernel reads
+  // the caller's pages over the bus
+  for (size_t i = 0; i < c->registered.size(); ++i) {
+    const auto &r = c->registered[i];
+    if (host >= r.first && n <= r.second && (size_t)(host - r.first) <= r.second - n) {
+      if (c->registered_dev[i] && getenv("KLT_MAPPED_FRAMES") && atoi(getenv("KLT_MAPPED_FRAMES")) == 1) {
+        c->u8_mapped[buf] = c->registered_dev[i] + (host - r.first);
+      } else {
+        HIPCHK(c, hipMemcpyAsync(c->d_u8[buf], host, n, hipMemcpyHostToDevice, c->stream));
+      }
+      HIPCHK(c, hipEventRecord(c->u8_done[buf], c->stream));
+      c->u8_w[buf] = ncols;
+      c->u8_h[buf] = nrows;
+      return 0;
+    }
+  }
   // the previous copy out of this bounce buffer must have finished
   HIPCHK(c, hipEventSynchronize(c->u8_done[buf]));
   // in groups: the host pool copies group g+1 into pinned memory while group
@@ -1003,7 +1042,7 @@ static int build_pyramid_on(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, co
     if (c->u8_w[buf] != d->ncols || c->u8_h[buf] != d->nrows)
       return fail(c, "build_pyramid: uploaded frame is %dx%d, desc %dx%d", c->u8_w[buf], c->u8_h[buf],
                   d->ncols, d->nrows);
-    src = c->d_u8[buf];
+    src = c->u8_mapped[buf] ? c->u8_mapped[buf] : c->d_u8[buf];
     pitch = d->ncols;
   }
   if (pitch < d->ncols) return fail(c, "build_pyramid: pitch %ld < ncols %d", pitch, d->ncols);
@@ -1039,6 +1078,38 @@ KLT_API int klt_hip_set_host_threads(klt_hip_ctx *c, int workers) {
   return 0;
 }
 
+KLT_API int klt_hip_register_host(klt_hip_ctx *c, const void *ptr, size_t bytes) {
+  if (!c || !ptr || !bytes) return fail(c, "register_host: bad argument");
+  const unsigned char *p = static_cast<const unsigned char *>(ptr);
+  for (const auto &r : c->registered)
+    if (p < r.first + r.second && r.first < p + bytes)
+      return fail(c, "register_host: [%p, +%zu) overlaps a registered buffer", ptr, bytes);
+  if (use_device(c)) return -1;
+  HIPCHK(c, hipHostRegister(const_cast<void *>(ptr), bytes, hipHostRegisterMapped));
+  void *dp = nullptr;
+  if (hipHostGetDevicePointer(&dp, const_cast<void *>(ptr), 0) != hipSuccess) dp = nullptr;
+  c->registered.push_back({p, bytes});
+  c->registered_dev.push_back(static_cast<const unsigned char *>(dp));
+  return 0;
+}
+
+KLT_API int klt_hip_unregister_host(klt_hip_ctx *c, const void *ptr) {
+  if (!c || !ptr) return fail(c, "unregister_host: bad argument");
+  for (size_t i = 0; i < c->registered.size(); ++i)
+    if (c->registered[i].first == ptr) {
+      if (use_device(c)) return -1;
+      // no upload still reads it: the context's streams drain first
+      for (hipStream_t st : {c->stream, c->own, c->pstream, c->cstream})
+        if (st) HIPCHK(c, hipStreamSynchronize(st));
+      HIPCHK(c, hipHostUnregister(const_cast<void *>(ptr)));
+      c->registered.erase(c->registered.begin() + (long)i);
+      c->registered_dev.erase(c->registered_dev.begin() + (long)i);
+      c->u8_mapped[0] = c->u8_mapped[1] = nullptr;
+      return 0;
+    }
+  return fail(c, "unregister_host: %p is not registered", ptr);
+}
+
 KLT_API int klt_hip_set_bank_budget(klt_hip_ctx *c, size_t bytes) {
   if (!c) return fail(c, "set_bank_budget: null context");
   c->bank_budget = bytes;
@@ -1067,6 +1138,12 @@ KLT_API int klt_hip_set_track_patch(klt_hip_ctx *c, int on) {
 KLT_API int klt_hip_set_track_merge(klt_hip_ctx *c, int on) {
   if (!c) return fail(c, "set_track_merge: null context");
   c->track_merge = on ? 1 : 0;
+  return 0;
+}
+
+KLT_API int klt_hip_set_track_impl(klt_hip_ctx *c, int impl) {
+  if (!c || impl < 0 || impl > 1) return fail(c, "set_track_impl: 0 (default kernel) or 1 (generic)");
+  c->track_impl = impl;
   return 0;
 }
 

@@ -64,6 +64,7 @@ DEVICE_PROTOS = {
     "klt_hip_fused_path": (C.c_int, [V, C.POINTER(PyrDesc)]),
     "klt_hip_set_track_order": (C.c_int, [V, C.c_int]),
     "klt_hip_set_track_merge": (C.c_int, [V, C.c_int]),
+    "klt_hip_set_track_impl": (C.c_int, [V, C.c_int]),
     "klt_hip_set_track_patch": (C.c_int, [V, C.c_int]),
     "klt_hip_set_track_count": (C.c_int, [V, C.c_int]),
     "klt_hip_get_track_count": (C.c_int, [V, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong), C.c_int]),
@@ -130,6 +131,10 @@ DEVICE_PROTOS = {
     "klt_amd_track_desc": (None, [V, C.POINTER(TrackDesc)]),
     "klt_amd_set_reduction": (None, [V, C.c_int]),
     "klt_amd_release_cached_devices": (C.c_int, []),
+    "klt_amd_register_buffer": (C.c_int, [V, V, C.c_size_t]),
+    "klt_amd_unregister_buffer": (C.c_int, [V, V]),
+    "klt_hip_register_host": (C.c_int, [V, V, C.c_size_t]),
+    "klt_hip_unregister_host": (C.c_int, [V, V]),
     # host helpers
     "klt_synth_frame": (None, [C.c_uint64, C.c_int, C.c_int, C.c_int, V]),
     "klt_sort_pairs_full": (None, [IP, IP, C.c_int]),

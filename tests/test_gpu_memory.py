@@ -107,3 +107,42 @@ def test_reset_trims_and_restores_defaults(gpu):
     gpu.KLTFreeTrackingContext(tc2)
     assert gpu.klt_amd_release_cached_devices() >= 1
     assert gpu.klt_amd_release_cached_devices() == 0
+
+
+def test_registered_buffers_bit_identical(gpu):
+    """klt_amd_register_buffer (klt_amd.h): example3.c's two reused buffers,
+    page-locked once, give the same lists as the staged upload; overlapping
+    registrations and unknown pointers are refused with a warning."""
+    from kltabi import fl_to_arrays, u8ptr
+    frames = synth(gpu, 4242, 640, 480, 6)
+    H, W = frames[0].shape
+
+    def loop(register):
+        img1, img2 = np.empty((H, W), np.uint8), np.empty((H, W), np.uint8)
+        tc = gpu.KLTCreateTrackingContext()
+        tc.contents.sequentialMode = 1
+        if register:
+            assert gpu.klt_amd_register_buffer(tc, img1.ctypes.data, img1.nbytes) == 0
+            assert gpu.klt_amd_register_buffer(tc, img2.ctypes.data, img2.nbytes) == 0
+            assert gpu.klt_amd_register_buffer(tc, img2.ctypes.data + 16, 64) == -1  # overlaps img2
+        fl = gpu.KLTCreateFeatureList(500)
+        img1[:] = frames[0]
+        gpu.KLTSelectGoodFeatures(tc, u8ptr(img1), W, H, fl)
+        cols = []
+        for t in range(1, len(frames)):
+            img2[:] = frames[t]
+            gpu.KLTTrackFeatures(tc, u8ptr(img1), u8ptr(img2), W, H, fl)
+            gpu.KLTReplaceLostFeatures(tc, u8ptr(img2), W, H, fl)
+            cols.append(fl_to_arrays(fl))
+            img1[:] = img2
+        if register:
+            assert gpu.klt_amd_unregister_buffer(tc, img1.ctypes.data) == 0
+            assert gpu.klt_amd_unregister_buffer(tc, img1.ctypes.data) == -1  # no longer registered
+        gpu.KLTFreeFeatureList(fl)
+        gpu.KLTFreeTrackingContext(tc)  # img2 is released with the context
+        return cols
+
+    a, b = loop(False), loop(True)
+    for ca, cb in zip(a, b):
+        for p, q in zip(ca, cb):
+            assert np.array_equal(p.view(np.int32), q.view(np.int32))

@@ -50,6 +50,8 @@ def main():
     ap.add_argument("--max-it", type=int, default=0, help="tracker: override max_iterations")
     ap.add_argument("--lost", action="store_true", help="tracker: mark every feature lost (launch floor)")
     ap.add_argument("--window", type=int, default=0, help="tracker: override window width/height")
+    ap.add_argument("--impl", type=int, default=0, help="tracker kernel for the default configuration: "
+                                                        "0 track7.hip, 1 generic k_track_frames_g")
     a = ap.parse_args()
 
     import kltamd
@@ -67,6 +69,7 @@ def main():
     check(lib, ctx, lib.klt_hip_set_track_merge(ctx, 0 if a.no_merge else 1), "merge")
     check(lib, ctx, lib.klt_hip_set_track_patch(ctx, 0 if a.no_patch else 1), "patch")
     check(lib, ctx, lib.klt_hip_set_frames_overlap(ctx, 1 if a.overlap else 0), "overlap")
+    check(lib, ctx, lib.klt_hip_set_track_impl(ctx, a.impl), "impl")
     if a.host_threads >= 0:
         check(lib, ctx, lib.klt_hip_set_host_threads(ctx, a.host_threads), "host_threads")
     nf = max(a.frames, 2)
