@@ -755,7 +755,7 @@ def replace_leg(lib, host, W, H, NF, args):
            "us_per_track_median": 1e6 * float(np.median(trk[steady])),
            "features_replaced": replaced,
            "select_median": dict(zip(("map_points_downloaded", "device_partition_steps", "sorted_positions_visited",
-                                      "us_map_init", "us_device_splits", "us_downloads", "us_select_total"),
+                                      "us_map_init", "us_device_splits", "us_downloads_and_host_sort", "us_select_total"),
                                      (float(np.median([q[k] for q in sel_stats])) for k in range(7))))
            if sel_stats else None,
            "region": "wall clock around KLTTrackFeatures + KLTReplaceLostFeatures per frame (example3.c:61-69 "

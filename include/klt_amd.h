@@ -44,7 +44,7 @@ void klt_amd_set_reduction(KLT_TrackingContext tc, int reduction);
      }
    with bit-identical results (sequential mode included), run on the batched
    device path: frames uploaded asynchronously in chunks, pyramids built and
-   features tracked 32 frames per launch.  Where one pyramid description
+   features tracked 16 frames per launch.  Where one pyramid description
    cannot serve every frame (a kernel-cache corner case) or internal images are
    requested, it runs exactly that loop instead. */
 void KLTTrackSequence(KLT_TrackingContext tc, KLT_PixelType **frames, int nframes, int ncols, int nrows,

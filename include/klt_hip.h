@@ -140,6 +140,12 @@ int klt_hip_set_track_impl(klt_hip_ctx *ctx, int impl);
    verdict loses frame j's feature.  0: a residue pass of its own.  Results do
    not depend on it. */
 int klt_hip_set_track_merge(klt_hip_ctx *ctx, int on);
+/* tuning hook: 1 (default) raises the tracker waves' issue priority
+   (s_setprio 3) so that, when the next chunk's pyramids are built beside the
+   tracker (overlapped schedule, band calls with build-ahead), a feature's
+   dependent chain issues ahead of the pyramid waves; 0 leaves it at 0.
+   Results do not depend on it. */
+int klt_hip_set_track_prio(klt_hip_ctx *ctx, int on);
 /* measurement hook: on != 0 zeroes (allocating on first use) two device
    counters that every later tracker launch of this context adds to -- the 2x2
    systems formed, i.e. the reference's Newton loop bodies
@@ -323,7 +329,7 @@ int klt_hip_select_dev_map(klt_hip_ctx *ctx, const int *dev_map, int nx, int ny,
 int klt_hip_select_tune(klt_hip_ctx *ctx, int threshold);
 /* last selection: map points copied to the host, device partition steps, sorted positions visited;
    host_us (optional, 4 values): wall clock of the map + init (queued and drained), the device
-   splits, the segment downloads, and the whole walk */
+   splits, the segment downloads with their host sorts, and the whole walk */
 int klt_hip_select_stats(klt_hip_ctx *ctx, long *downloaded, long *device_steps, long *visited, double *host_us);
 /* test hook: the whole lazy order of host vals[0..n) as klt_sort_pairs_full gives it */
 int klt_hip_select_sort_test(klt_hip_ctx *ctx, const int *vals, int n, int *out_val, int *out_idx);

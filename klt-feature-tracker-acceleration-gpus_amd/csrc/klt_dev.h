@@ -102,6 +102,7 @@ struct TrkArgs {
   int red_pitch;     // per-sum row pitch of the reduction staging area (floats)
   int merge_res;     // 1: defer the finest level's residue into the next frame's first pass
   int *escape;       // band mode: set when a window needs rows outside [vlo, vhi)
+  int prio;          // 1: tracker waves raise their issue priority (s_setprio 3) over concurrent pyramid waves
 };
 
 // batched frames: frame j tracks pyramid j-1 -> j of a bank; row j of the

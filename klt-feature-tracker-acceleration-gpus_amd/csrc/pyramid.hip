@@ -114,6 +114,17 @@ __device__ __forceinline__ bool xcd_tile(int tiles_x, int tiles_y, int &bx, int 
   return true;
 }
 
+#ifdef KLT_PYR_PROF
+// timing experiment (tools/hipbench/pyrprof.hip): per workgroup, the shader
+// clock at entry and after each phase, and where it ran
+__device__ unsigned long long *g_pyr_prof;
+#define PYR_STAMP(k)                                                                                  \
+  if (g_pyr_prof && tid == 0)                                                                         \
+    g_pyr_prof[((long)blockIdx.z * gridDim.x + blockIdx.x) * 8 + (k)] = clock64();
+#else
+#define PYR_STAMP(k)
+#endif
+
 // Edge tiles (INT false) clamp their loads and apply the zero-border rules per
 // element; interior tiles (~90 % at 1080p, 94 % at 4K) need neither.
 template <bool INT>
@@ -171,6 +182,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     }
   }
   __syncthreads();
+  PYR_STAMP(1)
 
   // B. rows pass of the smoothing: t1 idx k <-> global C0-8+k; zero unless RS <= x < W-RS.
   //    23 rows of 11 eight-column groups per pass (t1 idx 0..87): bytes [8j, 8j+16) of a staged row
@@ -210,6 +222,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     }
   }
   __syncthreads();
+  PYR_STAMP(2)
 
   // C. columns pass -> img0, 4 rows x 4 columns per thread; zero unless RS <= y < H-RS
   const int g21 = tid % NG, r21 = tid / NG;
@@ -232,6 +245,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     }
   }
   __syncthreads();
+  PYR_STAMP(3)
 
   // D1. img0 tile -> HBM
   const int g16 = tid & 15, r16 = tid >> 4;
@@ -313,6 +327,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     }
   }
   __syncthreads();
+  PYR_STAMP(4)
 
   // E. columns passes of both gradients; zero unless RG <= y < H-RG.  4 rows x
   //    2 columns per thread from 8-byte LDS reads (10 rows read for 4 outputs)
@@ -358,6 +373,16 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
       }
     }
   }
+#ifdef KLT_PYR_PROF
+  __syncthreads();
+  PYR_STAMP(5)
+  if (g_pyr_prof && tid == 0) {
+    const long o = ((long)blockIdx.z * gridDim.x + blockIdx.x) * 8;
+    g_pyr_prof[o + 6] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                        (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);  // XCC_ID : HW_ID
+    g_pyr_prof[o + 7] = INT ? 1 : 0;
+  }
+#endif
 }
 
 __global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ src, int spitch, int W, int H,
@@ -369,6 +394,10 @@ __global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ s
   __shared__ __attribute__((aligned(16))) float lds[l0::LDS];
   int bx, by;
   if (!xcd_tile(tiles_x, tiles_y, bx, by)) return;  // whole workgroup: no barrier is skipped
+#ifdef KLT_PYR_PROF
+  const int tid = threadIdx.x;
+  PYR_STAMP(0)
+#endif
   const int C0 = bx * l0::TW, R0 = (by + ty0) * l0::TH;
   // blockIdx.z: frame of a batch (frame strides in elements; 0 for one frame)
   src += blockIdx.z * fs_src;

@@ -170,6 +170,7 @@ struct klt_hip_ctx {
   int track_order = 0;  // 0: band-sorted, XCD-major processing order; 1: input order
   int track_patch = 1;  // one-feature waves gather through a lane patch when the window fits
   int track_merge = 1;   // defer finest-level residues into the next frame's first pass (ResCarry)
+  int track_prio = 1;    // tracker waves at issue priority 3 (klt_hip_set_track_prio)
   int track_impl = 0;    // 0: track7.hip for the default configuration, 1: the generic k_track_frames_g
   int serial_frames = 1;  // klt_hip_track_frames: 1 builds and tracks on one stream (default: the
                           // tracker and the pyramid kernels compete for the same CUs; overlap buys ~3 %)
@@ -554,6 +555,7 @@ int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc
   const TrkFramesArgs &b2 = bb;
   TrkArgs aa = a;
   aa.merge_res = c->track_merge;
+  aa.prio = c->track_prio;
   // the default configuration: the latency-lean kernel (track7.hip) unless
   // the context asks for the generic one (klt_hip_set_track_impl, A/B only)
 #ifdef KLT_TRACK_PROF
@@ -919,6 +921,7 @@ KLT_API int klt_hip_ctx_reset(klt_hip_ctx *c) {
   c->track_order = 0;
   c->track_patch = 1;
   c->track_merge = 1;
+  c->track_prio = 1;
   c->track_impl = 0;
   c->serial_frames = 1;
   c->prof = nullptr;
@@ -1138,6 +1141,12 @@ KLT_API int klt_hip_set_track_patch(klt_hip_ctx *c, int on) {
 KLT_API int klt_hip_set_track_merge(klt_hip_ctx *c, int on) {
   if (!c) return fail(c, "set_track_merge: null context");
   c->track_merge = on ? 1 : 0;
+  return 0;
+}
+
+KLT_API int klt_hip_set_track_prio(klt_hip_ctx *c, int on) {
+  if (!c) return fail(c, "set_track_prio: null context");
+  c->track_prio = on ? 1 : 0;
   return 0;
 }
 

@@ -41,6 +41,7 @@
 #include <algorithm>
 #include <chrono>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "klt_dev.h"
@@ -54,6 +55,8 @@ constexpr int kSelBS = kSelThreads * kSelPer;       // elements per block
 constexpr int kSelStack = 512;                      // segments a device refinement may push
 constexpr int kSelScanThreads = 1024;
 constexpr unsigned kBlockedBit = 0x80000000u;
+constexpr unsigned kSelParMin = 2048;               // host sort: parts at least this long go to a second thread
+constexpr int kSelParDepth = 3;                     // host sort: up to 2^3 threads
 
 struct SelState {
   int start, len;  // the leftmost segment still to split
@@ -310,7 +313,7 @@ struct SelEngine {
   int threshold = kSelDefaultThreshold;  // segments at most this long go to the host
   // statistics of the last run
   long downloaded = 0, device_steps = 0, visited = 0;
-  double us[4] = {};  // host wall clock: map + paint + init queued and drained, device splits, downloads, total
+  double us[4] = {};  // host wall clock: map + paint + init queued and drained, device splits, segment downloads + host sorts, total
 };
 
 double now_us() {
@@ -342,6 +345,7 @@ int sel_grow(T **p, size_t *cap, size_t n, std::string *err) {
 struct Seg {
   int start, len;
   bool host;
+  bool sorted = false;  // host segment already in its final order
 };
 
 // the exact partition step of klt_select.c (the reference's _quicksort body)
@@ -360,6 +364,34 @@ unsigned host_partition(int2 *a, unsigned n) {
   }
   std::swap(a[j], a[0]);
   return j;
+}
+
+// the whole quicksort of a[0..n) below one partition step: the left part, then
+// the right part, each sorted the same way.  The two parts are disjoint, so
+// sorting them in any order -- or at once, on two threads -- leaves every
+// element where the sequential recursion (and the lazy walk over it) puts it.
+// The smaller part recurses and the larger one loops, which bounds the
+// recursion depth by log2(n) whatever the pivots.
+void host_sort(int2 *a, unsigned n, int par) {
+  while (n > 1) {
+    const unsigned j = host_partition(a, n);
+    int2 *lo = a, *hi = a + j + 1;
+    unsigned nlo = j, nhi = n - j - 1;
+    if (par > 0 && nlo >= kSelParMin && nhi >= kSelParMin) {
+      std::thread t([=] { host_sort(hi, nhi, par - 1); });
+      host_sort(lo, nlo, par - 1);
+      t.join();
+      return;
+    }
+    if (nlo < nhi) {
+      host_sort(lo, nlo, par);
+      a = hi;
+      n = nhi;
+    } else {
+      host_sort(hi, nhi, par);
+      n = nlo;
+    }
+  }
 }
 
 // split device segment g on the device until its leftmost part is at most the
@@ -447,10 +479,16 @@ struct LazySort {
         g.host = true;
       }
       if (g.len == 1) return g.start;
-      const unsigned j = host_partition(e->h_kv + g.start, (unsigned)g.len);
-      stk.push_back(Seg{g.start + (int)j + 1, g.len - (int)j - 1, true});
-      stk.push_back(Seg{g.start + (int)j, 1, true});
-      stk.push_back(Seg{g.start, (int)j, true});
+      if (!g.sorted) {
+        // a segment the walk has reached is consumed almost whole: sort it
+        // outright (in parallel) and hand its positions out in order
+        const double t0 = now_us();
+        host_sort(e->h_kv + g.start, (unsigned)g.len, kSelParDepth);
+        e->us[2] += now_us() - t0;
+        g.sorted = true;
+      }
+      stk.push_back(Seg{g.start + 1, g.len - 1, true, true});
+      return g.start;
     }
     return -1;
   }

@@ -753,6 +753,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KLT_TRAC
                                                            float *__restrict__ fy, int *__restrict__ fv, int n) {
   constexpr int LG = kWave / G;
   __shared__ __attribute__((aligned(16))) float red_all[kBlock / kWave][6 * G * (LG * PPL + 4) + 16];
+  if (a.prio) __builtin_amdgcn_s_setprio(3);  // the chain issues ahead of co-resident pyramid waves
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   // consecutive workgroups land on the 8 XCDs round-robin: give each XCD a
   // contiguous run of the (band-sorted) order so its L2 sees one image band

@@ -335,6 +335,7 @@ template <bool BAND>
 __global__ __launch_bounds__(kBlock) void k_track7(TrkArgs a, TrkFramesArgs b, float *__restrict__ fx,
                                                    float *__restrict__ fy, int *__restrict__ fv, int n) {
   __shared__ __attribute__((aligned(16))) float red_all[kWaves][kRows * kRow + 4];
+  if (a.prio) __builtin_amdgcn_s_setprio(3);  // the chain issues ahead of co-resident pyramid waves
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   if (b.n_dev) n = *b.n_dev;
   // XCD-major block order over the (band-sorted) features actually processed

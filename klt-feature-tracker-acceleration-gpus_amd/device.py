@@ -64,6 +64,7 @@ DEVICE_PROTOS = {
     "klt_hip_fused_path": (C.c_int, [V, C.POINTER(PyrDesc)]),
     "klt_hip_set_track_order": (C.c_int, [V, C.c_int]),
     "klt_hip_set_track_merge": (C.c_int, [V, C.c_int]),
+    "klt_hip_set_track_prio": (C.c_int, [V, C.c_int]),
     "klt_hip_set_track_impl": (C.c_int, [V, C.c_int]),
     "klt_hip_set_track_patch": (C.c_int, [V, C.c_int]),
     "klt_hip_set_track_count": (C.c_int, [V, C.c_int]),

@@ -434,7 +434,7 @@ def test_tracker_tuning_hooks_do_not_change_results(gpu, oracle, opts):
     assert_table_equal(X, Y, V, *OracleTracker(oracle).harness(frames, 3000, 8, first=frames[0]))
 
 
-@pytest.mark.parametrize("opts", [dict(overlap=1), dict(overlap=0), dict(overlap=1, merge=0)])
+@pytest.mark.parametrize("opts", [dict(overlap=1), dict(overlap=0), dict(overlap=1, merge=0), dict(overlap=1, prio=0)])
 def test_overlapped_schedule_1080p(gpu, oracle, opts):
     """The bench's overlapped schedule -- pyramids of chunk c+1 built on their
     own stream while chunk c is tracked -- over several chunks (chunk 3, 10
@@ -454,6 +454,7 @@ def batch_sequence_opts(gpu, frames, nfeat, chunk, opts, counts=None):
         assert gpu.klt_hip_set_track_order(ctx, opts.get("order", 0)) == 0
         assert gpu.klt_hip_set_frames_overlap(ctx, opts.get("overlap", 0)) == 0
         assert gpu.klt_hip_set_track_merge(ctx, opts.get("merge", 1)) == 0
+        assert gpu.klt_hip_set_track_prio(ctx, opts.get("prio", 1)) == 0
         return ctx
 
     gpu.klt_amd_device_context = hooked
