@@ -233,12 +233,14 @@ def main() -> None:
         lib.klt_hip_set_track_count(ctx, 0)
         # feature-frames: features live when frame j starts (table row j-1 holds the list after j-1)
         ff = int((tab[2][t_start - 1:t_start - 1 + nrep] >= 0).sum().item())
-        tracker = tracker_line(solves.value, passes.value, ff, tm)
+        tracker = tracker_line(solves.value, passes.value, ff, tm,
+                               "kltdev::k_track7<false>" if args.reduction == "exact" else "kltdev::k_track_frames_g")
         pmc = ROOT / "profiles" / "pmc_tracker.json"
         if pmc.exists():
             try:
                 d = json.loads(pmc.read_text())
-                if d.get("workload", "").startswith(f"{W}x{H}, {NF} features"):
+                if (d.get("workload", "").startswith(f"{W}x{H}, {NF} features")
+                        and tracker["kernel"] in d.get("kernel", "")):
                     # the tracker's bound is instruction issue, not HBM; its VALU
                     # instructions per iteration (PMC) set an issue ceiling beside the measured rate
                     tracker["pmc"] = {k: d[k] for k in ("per_iteration", "valu_issue_busy", "wave_time_split",
@@ -769,7 +771,7 @@ def replace_leg(lib, host, W, H, NF, args):
     return out
 
 
-def tracker_line(solves, passes, feature_frames, tm):
+def tracker_line(solves, passes, feature_frames, tm, kernel):
     """the LK tracker is gather/latency and VALU bound, not an HBM
     roofline kernel; report its work rate as feature-iterations per second.
     An iteration is one 2x2 system formed (a body of the reference's Newton
@@ -777,7 +779,7 @@ def tracker_line(solves, passes, feature_frames, tm):
     (klt_hip_set_track_count) over the same frames the kernel events time."""
     s = tm.ms_track * 1e-3
     return {
-        "kernel": "k_track_frames_g", "bound": "VALU / gather latency (no HBM roofline, SURVEY 8d)",
+        "kernel": kernel, "bound": "VALU / gather latency (no HBM roofline, SURVEY 8d)",
         "newton_iterations": solves, "gather_passes": passes, "feature_frames": feature_frames,
         "iterations_per_feature_frame": solves / feature_frames if feature_frames else None,
         "passes_per_feature_frame": passes / feature_frames if feature_frames else None,

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """profiles/pmc_tracker.json from a tools/pmc_track.sh run: the batched
-tracker's (k_track_frames_g) instruction mix per Newton iteration and its VALU
+tracker's (k_track7 for the default configuration, else k_track_frames_g) instruction mix per Newton iteration and its VALU
 issue ceiling (the tracker has no HBM roofline; its bound is
 instruction issue and gather latency).
 
@@ -20,11 +20,12 @@ import sys
 
 root = sys.argv[1]
 out = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_tracker.json"
-per = {}
+per, names = {}, set()
 for path in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(path)):
-        if "k_track_frames" not in r["Kernel_Name"]:
+        if "k_track_frames" not in r["Kernel_Name"] and "k_track7" not in r["Kernel_Name"]:
             continue
+        names.add(r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0])
         per.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
 avg = {k: sum(v) / len(v) for k, v in per.items()}
 cnt = json.load(open(f"{root}/count.json"))
@@ -35,7 +36,7 @@ simd_cycles = cyc * 256 * 4
 valu = avg["SQ_INSTS_VALU"]
 clock_hz = 2.1e9  # sustained shader clock under load (tools: GRBM / wall); nominal 2.4 GHz
 res = {
-    "kernel": "k_track_frames_g<1,1,PATCH,7,EXACT> (one wave per feature)",
+    "kernel": " / ".join(sorted(names)) + " (one wave per feature)",
     "workload": f"{cnt['resolution']}, {cnt['features']} features, {cnt['chunk']}-frame launches, feature table",
     "source": "rocprofv3 --pmc SQ_* / GRBM_GUI_ACTIVE (tools/pmc_track.sh), per dispatch; iterations from the counted replay",
     "newton_iterations_per_launch": it,

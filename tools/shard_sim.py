@@ -46,6 +46,9 @@ def main():
     ap.add_argument("--no-ahead", action="store_true", help="pass 2 without building the next chunk ahead")
     ap.add_argument("--own-streams", action="store_true",
                     help="pass 2: the library on its own streams (not a torch pool stream), synchronized by host")
+    ap.add_argument("--lazy-flag", action="store_true",
+                    help="pass 2: read chunk c's escape flag after chunk c+1 is queued (a speculative driver "
+                         "redoes c and drops c+1 when it is set), so the host never drains the stream per chunk")
     ap.add_argument("--replay", default=None, help=argparse.SUPPRESS)  # internal: pass 2 of one rank (npz of states)
     ap.add_argument("--rank", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--exchange-us", type=float, default=40.0,
@@ -115,6 +118,9 @@ def main():
         rk = Rank(world, a.rank, margin, own)
         xr, yr, vr = xs.clone(), ys.clone(), vs.clone()
         esc = torch.zeros(1, dtype=torch.int32, device=dev)
+        escs = torch.zeros(len(chunks), dtype=torch.int32, device=dev)
+        esc_host = torch.zeros(len(chunks), dtype=torch.int32, pin_memory=True)
+        esc_ev = [torch.cuda.Event() for _ in chunks]
         sx, sy, sv = (torch.from_numpy(st[k]).to(dev) for k in ("x", "y", "v"))
         for rep in range(3):  # the first two warm the device up (allocations, clocks); the last is timed
             rk.begin(0)
@@ -123,13 +129,21 @@ def main():
             for ci, (c0, n) in enumerate(chunks):
                 nn = chunks[ci + 1][1] if ci + 1 < len(chunks) and not a.no_ahead else 0
                 xr.copy_(sx[ci]), yr.copy_(sy[ci]), vr.copy_(sv[ci])
-                esc.zero_()
+                e = escs[ci:ci + 1] if a.lazy_flag else esc
+                e.zero_()
                 if own:
                     torch.cuda.current_stream().synchronize()
-                rk.chunk(c0, n, xr, yr, vr, esc, next_n=nn)
+                rk.chunk(c0, n, xr, yr, vr, e, next_n=nn)
                 if own:
                     check(lib, rk.ctx, lib.klt_hip_sync(rk.ctx), "sync")
-                int(esc.item())  # the host's read of the escape flag (merge_chunk)
+                if not a.lazy_flag:
+                    int(esc.item())  # the host's read of the escape flag (merge_chunk)
+                else:
+                    esc_host[ci:ci + 1].copy_(e, non_blocking=True)
+                    esc_ev[ci].record()
+                    if ci > 0:  # chunk c-1's flag, read while chunk c runs
+                        esc_ev[ci - 1].synchronize()
+                        int(esc_host[ci - 1])
             torch.cuda.synchronize()
         frames_timed = sum(n for _, n in chunks)
         print(json.dumps({"rank": a.rank, "us_per_frame": 1e6 * (time.perf_counter() - t_start) / frames_timed}))
@@ -198,7 +212,8 @@ def main():
                     cmd = [sys.executable, __file__, "--replay", f, "--rank", str(r), "--width", str(W), "--height",
                            str(H), "--features", str(NF), "--frames", str(a.frames), "--chunk", str(a.chunk),
                            "--seed", str(a.seed)] + (["--no-ahead"] if a.no_ahead else []) + \
-                          (["--own-streams"] if a.own_streams else []) + (["--balanced"] if a.balanced else [])
+                          (["--own-streams"] if a.own_streams else []) + (["--balanced"] if a.balanced else []) + \
+                          (["--lazy-flag"] if a.lazy_flag else [])
                     res = subprocess.run(cmd, check=True, capture_output=True, text=True)
                     rank_us.append(json.loads(res.stdout.strip().splitlines()[-1])["us_per_frame"])
             nch = len(chunks)
