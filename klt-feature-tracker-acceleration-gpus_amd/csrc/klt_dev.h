@@ -162,6 +162,8 @@ hipError_t launch_min_eigen(hipStream_t st, const float *gx, const float *gy, in
 hipError_t launch_synth(hipStream_t st, unsigned long long seed, int t0, int n, int W, int H, int row0, uint8_t *out,
                         long pitch, long fstride);
 hipError_t launch_selftest_sqrt(const double *in, double *out, int n);
+// n 32-bit words, 16-byte aligned ends (device or mapped pinned host memory)
+hipError_t launch_copy_words(hipStream_t st, const void *src, void *dst, long n);
 hipError_t launch_selftest_div(const float *a, const float *b, float *out, int n);
 
 // the tracker: one wave per feature; patch/win7 select the lane-patch gather

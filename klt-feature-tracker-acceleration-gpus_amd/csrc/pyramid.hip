@@ -657,6 +657,18 @@ __global__ __launch_bounds__(kBlock) void k_synth(unsigned long long seed, int t
   out[(long)blockIdx.y * fstride + (long)y * pitch + x] = klt_synth_pixel(seed, t, x, row0 + y);
 }
 
+// n 32-bit words from src to dst (16-byte aligned), 16 bytes per thread; one
+// side may be mapped pinned host memory (the per-call feature list)
+__global__ __launch_bounds__(kBlock) void k_copy_words(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
+                                                       long n) {
+  const long i = (long)blockIdx.x * kBlock + threadIdx.x;
+  if (4 * i + 3 < n) {
+    reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(src)[i];
+  } else {
+    for (long k = 4 * i; k < n; ++k) dst[k] = src[k];
+  }
+}
+
 __global__ void k_selftest_sqrt(const double *in, double *out, int n) {
   const int i = blockIdx.x * kBlock + threadIdx.x;
   if (i < n) out[i] = sqrt(in[i]);
@@ -742,6 +754,13 @@ hipError_t launch_synth(hipStream_t st, unsigned long long seed, int t0, int n, 
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+hipError_t launch_copy_words(hipStream_t st, const void *src, void *dst, long n) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_copy_words, dim3(blocks_for((n + 3) / 4)), dim3(kBlock), 0, st,
+                     reinterpret_cast<const uint32_t *>(src), reinterpret_cast<uint32_t *>(dst), n);
+  return hipGetLastError();
 }
 
 hipError_t launch_selftest_sqrt(const double *in, double *out, int n) {

@@ -147,7 +147,12 @@ struct klt_hip_ctx {
   float *d_fx = nullptr, *d_fy = nullptr;  // views into d_feat
   int *d_fv = nullptr;
   float *d_feat = nullptr, *h_feat = nullptr;
-  int feat_zero_copy = 1;   // klt_hip_track on host lists: kernels use h_feat in place (0: copies)
+  // klt_hip_track on host lists: 2 (default) two copy kernels move the pinned
+  // block h_feat to d_feat and back around the tracker (no copy engine, no
+  // copy-to-kernel hand-off, and the tracker's gathers of x/y/val stay on the
+  // device: 111 against 130 us per registered 1080p/5000 call); 1 the kernels
+  // use h_feat in place over the bus; 0 copy-engine copies
+  int feat_mode = 2;
   size_t f_cap = 0;
   int *d_eig = nullptr;
   size_t eig_cap = 0;
@@ -908,7 +913,7 @@ KLT_API int klt_hip_ctx_reset(klt_hip_ctx *c) {
     c->pool = nullptr;
     c->copy_threads = 7;
   }
-  c->feat_zero_copy = 1;
+  c->feat_mode = 2;
   for (auto &r : c->registered) (void)hipHostUnregister(const_cast<unsigned char *>(r.first));
   c->registered.clear();
   c->registered_dev.clear();
@@ -1294,8 +1299,16 @@ KLT_API int klt_hip_track(klt_hip_ctx *c, int s1, int s2, const klt_hip_track_de
 
   float *x_d = x, *y_d = y;
   int *v_d = val;
-  if (!on_device) {
-    if (c->feat_zero_copy) {
+  const bool kstage = !on_device && c->feat_mode == 2;
+  if (kstage) {
+    // the pinned block to the device block by a copy kernel (no copy engine)
+    if (feat_pack(c, x, y, val, n)) return -1;
+    if (launched(c, "k_copy_words", launch_copy_words(c->stream, c->h_feat, c->d_feat, 3L * n))) return -1;
+    x_d = c->d_fx;
+    y_d = c->d_fy;
+    v_d = c->d_fv;
+  } else if (!on_device) {
+    if (c->feat_mode == 1) {
       if (feat_pack(c, x, y, val, n)) return -1;
       x_d = c->h_feat;
       y_d = c->h_feat + n;
@@ -1314,8 +1327,12 @@ KLT_API int klt_hip_track(klt_hip_ctx *c, int s1, int s2, const klt_hip_track_de
     b.nframes = 1;
     if (track_frames_launch(c, c->stream, d, a, b, x_d, y_d, v_d, n)) return -1;
   }
+  if (kstage) {
+    if (launched(c, "k_copy_words", launch_copy_words(c->stream, c->d_feat, c->h_feat, 3L * n))) return -1;
+    return feat_unpack(c, x, y, val, n);
+  }
   if (!on_device) {
-    if (!c->feat_zero_copy)
+    if (c->feat_mode == 0)
       HIPCHK(c, hipMemcpyAsync(c->h_feat, c->d_feat, 3 * sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
     return feat_unpack(c, x, y, val, n);
   }
