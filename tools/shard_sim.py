@@ -124,6 +124,7 @@ def main():
         sx, sy, sv = (torch.from_numpy(st[k]).to(dev) for k in ("x", "y", "v"))
         for rep in range(3):  # the first two warm the device up (allocations, clocks); the last is timed
             rk.begin(0)
+            lib.klt_hip_set_timing(rk.ctx, 1 if rep == 2 else 0)  # per-kernel events of the timed run
             torch.cuda.synchronize()
             t_start = time.perf_counter()
             for ci, (c0, n) in enumerate(chunks):
@@ -146,7 +147,14 @@ def main():
                         int(esc_host[ci - 1])
             torch.cuda.synchronize()
         frames_timed = sum(n for _, n in chunks)
-        print(json.dumps({"rank": a.rank, "us_per_frame": 1e6 * (time.perf_counter() - t_start) / frames_timed}))
+        wall = 1e6 * (time.perf_counter() - t_start) / frames_timed
+        tm = Timing()
+        check(lib, rk.ctx, lib.klt_hip_get_timing(rk.ctx, C.byref(tm)), "timing")
+        # per-kernel event time per frame of the timed run (overlapping kernels share the GPU: with
+        # build-ahead these are contended durations; with --no-ahead each kernel runs alone)
+        kern = {"k_pyr_l0": 1e3 * tm.ms_pyr_l0 / frames_timed, "k_pyr_l1": 1e3 * tm.ms_pyr_l1 / frames_timed,
+                "k_track": 1e3 * tm.ms_track / frames_timed}
+        print(json.dumps({"rank": a.rank, "us_per_frame": wall, "kernels_us_per_frame": kern}))
         return
 
     out = {"workload": f"{W}x{H}, {NF} features, {a.frames - 1} tracked frames, {a.chunk}-frame chunks"
@@ -207,7 +215,7 @@ def main():
                          x=np.stack([t[0].cpu().numpy() for t in starts]),
                          y=np.stack([t[1].cpu().numpy() for t in starts]),
                          v=np.stack([t[2].cpu().numpy() for t in starts]))
-                rank_us = []
+                rank_us, rank_kern = [], []
                 for r in range(world):
                     cmd = [sys.executable, __file__, "--replay", f, "--rank", str(r), "--width", str(W), "--height",
                            str(H), "--features", str(NF), "--frames", str(a.frames), "--chunk", str(a.chunk),
@@ -215,7 +223,9 @@ def main():
                           (["--own-streams"] if a.own_streams else []) + (["--balanced"] if a.balanced else []) + \
                           (["--lazy-flag"] if a.lazy_flag else [])
                     res = subprocess.run(cmd, check=True, capture_output=True, text=True)
-                    rank_us.append(json.loads(res.stdout.strip().splitlines()[-1])["us_per_frame"])
+                    rr = json.loads(res.stdout.strip().splitlines()[-1])
+                    rank_us.append(rr["us_per_frame"])
+                    rank_kern.append(rr["kernels_us_per_frame"])
             nch = len(chunks)
             frames = sum(n for _, n in chunks)
             exch = a.exchange_us * nch / frames if world > 1 else 0.0
@@ -227,7 +237,7 @@ def main():
                    "us_per_frame_exchange": exch, "projected_fps": fps,
                    "projected_speedup": fps / base_fps if base_fps else None,
                    "per_rank_us_per_frame": [{"rank": i, "band_rows": [rk.band.row_lo, rk.band.row_hi],
-                                              "wall": rank_us[i],
+                                              "wall": rank_us[i], "replay_kernels": rank_kern[i],
                                               "k_pyr_l0": p[0] / p[3], "k_pyr_l1": p[1] / p[3], "k_track": p[2] / p[3]}
                                              for i, (rk, p) in enumerate(zip(ranks, per_rank))]}
             out["runs"].append(run)
