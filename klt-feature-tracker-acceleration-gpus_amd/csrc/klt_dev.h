@@ -144,10 +144,11 @@ struct AffArgs {
 // launchers
 // ---------------------------------------------------------------------------
 // k_pyr_l0 over F frames (src + f*stride; outputs + f*fs0, hs + f*fsh), level-0
-// tile rows [ty0, ty1) of 32-row tiles
+// tile rows [ty0, ty1) of 32-row tiles; only tile rows [py0, py1) store the
+// level-0 planes (the others only the sigma-3.6 rows pass, hs)
 hipError_t launch_pyr_l0(hipStream_t st, const uint8_t *src, int pitch, long stride, int W, int H, const DefTaps &T,
                          int vec_u8, int vec_out, float *img, float *gx, float *gy, float *hs, int W1, int do_hs,
-                         long fs0, long fsh, int F, int ty0, int ty1);
+                         long fs0, long fsh, int F, int ty0, int ty1, int py0 = 0, int py1 = 1 << 30);
 // k_pyr_l1 over F frames, level-1 tile rows [ty0, ty1)
 hipError_t launch_pyr_l1(hipStream_t st, const float *hs, int W1, int H, int H1, const DefTaps &T, int vec,
                          float *img1, float *gx1, float *gy1, long fsh, long fs1, int F, int ty0, int ty1);

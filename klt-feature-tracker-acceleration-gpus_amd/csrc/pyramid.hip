@@ -132,7 +132,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
                                             int W, int H, const DefTaps &T, int vec_u8,
                                             float *__restrict__ img0, float *__restrict__ gx0,
                                             float *__restrict__ gy0, float *__restrict__ hs, int hsW,
-                                            int do_hs, int vec_out, int C0, int R0, int tid) {
+                                            int do_hs, int vec_out, int C0, int R0, int tid, bool planes) {
   using namespace l0;
   float *u = lds;            // [UH][PUB] staged bytes
   float *im = lds;           // [IHB*4][PI]   (after u is dead)
@@ -247,10 +247,12 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
   __syncthreads();
   PYR_STAMP(3)
 
-  // D1. img0 tile -> HBM
+  // D1. img0 tile -> HBM (a tile without planes -- a band's outer margin,
+  // where only the sigma-3.6 rows pass is needed -- skips D1, D2 and E)
   const int g16 = tid & 15, r16 = tid >> 4;
 #pragma unroll
   for (int k = 0; k < TH / 16; ++k) {
+    if (!planes) break;
     const int r = r16 + 16 * k, g = g16;
     const int y = R0 + r, x = C0 + 4 * g;
     const f4 val = ld4(im + (r + RG) * PI + 8 + 4 * g);
@@ -268,7 +270,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
 #pragma unroll
   for (int k = 0; k < (IH + 15) / 16; ++k) {
     const int r = r16 + 16 * k, g = g16;
-    if (r >= IH) break;
+    if (r >= IH || !planes) break;
     const float *row = im + r * PI + 4 * g + 4;  // img0 idx c0+4 <-> global C0+c0-4
     float v[12];
     *reinterpret_cast<f4 *>(v) = ld4(row);
@@ -331,7 +333,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
 
   // E. columns passes of both gradients; zero unless RG <= y < H-RG.  4 rows x
   //    2 columns per thread from 8-byte LDS reads (10 rows read for 4 outputs)
-  for (int i = tid; i < (TH / 4) * (TW / 2); i += kBlock) {
+  for (int i = planes ? tid : kBlock; i < (TH / 4) * (TW / 2); i += kBlock) {
     const int b = i / (TW / 2), g = i - b * (TW / 2);
     f2 vx[10], vy[10];
 #pragma unroll
@@ -390,7 +392,7 @@ __global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ s
                                                    float *__restrict__ gx0, float *__restrict__ gy0,
                                                    float *__restrict__ hs, int hsW, int do_hs, int vec_out,
                                                    long fs_src, long fs0, long fs_hs, int ty0, int tiles_x,
-                                                   int tiles_y) {
+                                                   int tiles_y, int py0, int py1) {
   __shared__ __attribute__((aligned(16))) float lds[l0::LDS];
   int bx, by;
   if (!xcd_tile(tiles_x, tiles_y, bx, by)) return;  // whole workgroup: no barrier is skipped
@@ -408,12 +410,13 @@ __global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ s
   // interior: unclamped aligned loads, no zero-border rule applies, all stores in bounds
   const bool interior = vec_u8 && vec_out && (hsW * l0::SS == W) && (hsW % 2 == 0) && C0 >= 12 && C0 + 84 <= W &&
                         R0 >= 5 && R0 + l0::TH + 7 <= H;
+  const bool planes = by + ty0 >= py0 && by + ty0 < py1;  // tile rows [py0, py1) store img0, gx0, gy0
   if (interior)
     pyr_l0_tile<true>(lds, src, spitch, W, H, T, vec_u8, img0, gx0, gy0, hs, hsW, do_hs, vec_out, C0, R0,
-                      threadIdx.x);
+                      threadIdx.x, planes);
   else
     pyr_l0_tile<false>(lds, src, spitch, W, H, T, vec_u8, img0, gx0, gy0, hs, hsW, do_hs, vec_out, C0, R0,
-                       threadIdx.x);
+                       threadIdx.x, planes);
 }
 
 // ---------------------------------------------------------------------------
@@ -686,14 +689,14 @@ __global__ void k_selftest_div(const float *a, const float *b, float *out, int n
 // ---------------------------------------------------------------------------
 hipError_t launch_pyr_l0(hipStream_t st, const uint8_t *src, int pitch, long stride, int W, int H, const DefTaps &T,
                          int vec_u8, int vec_out, float *img, float *gx, float *gy, float *hs, int W1, int do_hs,
-                         long fs0, long fsh, int F, int ty0, int ty1) {
+                         long fs0, long fsh, int F, int ty0, int ty1, int py0, int py1) {
   const int tx = (W + l0::TW - 1) / l0::TW;
   if (F <= 0 || ty1 <= ty0) return hipSuccess;
 #ifdef KLT_EXP_NOHS  // timing experiment only: level 0 without the sigma-3.6 rows pass
   do_hs = 0;
 #endif
   hipLaunchKernelGGL(k_pyr_l0, dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(kBlock), 0, st, src, pitch, W, H, T,
-                     vec_u8, img, gx, gy, hs, W1, do_hs, vec_out, stride, fs0, fsh, ty0, tx, ty1 - ty0);
+                     vec_u8, img, gx, gy, hs, W1, do_hs, vec_out, stride, fs0, fsh, ty0, tx, ty1 - ty0, py0, py1);
   return hipGetLastError();
 }
 

@@ -448,15 +448,23 @@ DefTaps default_taps(const klt_hip_pyr_desc *d) {
 // the rows actually built are returned in r0/r1.
 int launch_l0(klt_hip_ctx *c, hipStream_t st, const uint8_t *src, long pitch, long stride, int W, int H,
               const DefTaps &T, int vec_u8, int vec_out, float *img, float *gx, float *gy, float *hs, int W1,
-              int do_hs, long fs0, long fsh, int F, int &r0, int &r1) {
+              int do_hs, long fs0, long fsh, int F, int &r0, int &r1, int *p0 = nullptr, int *p1 = nullptr) {
   if (r1 <= r0 || F <= 0) return 0;
   const int TH = geom::L0_TH;
   const int nty = (H + TH - 1) / TH;
   const int ty0 = r0 / TH, ty1 = r1 >= H ? nty : clampi((r1 + TH - 1) / TH, ty0, nty);
   r0 = ty0 * TH;
   r1 = ty1 >= nty ? H : ty1 * TH;
+  // planes rows [*p0, *p1) (whole tiles, inside the built ones); null: every built tile
+  int py0 = ty0, py1 = ty1;
+  if (p0 && p1) {
+    py0 = clampi(*p0 / TH, ty0, ty1);
+    py1 = *p1 >= H ? ty1 : clampi((*p1 + TH - 1) / TH, py0, ty1);
+    *p0 = py0 * TH;
+    *p1 = py1 >= nty ? H : py1 * TH;
+  }
   return launched(c, "k_pyr_l0", launch_pyr_l0(st, src, (int)pitch, stride, W, H, T, vec_u8, vec_out, img, gx, gy,
-                                               hs, W1, do_hs, fs0, fsh, F, ty0, ty1));
+                                               hs, W1, do_hs, fs0, fsh, F, ty0, ty1, py0, py1));
 }
 
 int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
@@ -724,8 +732,12 @@ int ensure_banks(klt_hip_ctx *c, const klt_hip_pyr_desc *d, int frames) {
 // Level-0 rows [row_lo, row_hi) are built (whole 32-row tiles, global
 // coordinates, so every built value is the full-frame value) and the level-1
 // tiles whose sigma-3.6 inputs lie inside them; K.vlo/vhi record what is valid.
+// row_lo/row_hi: the level-0 rows to build (the sigma-3.6 rows pass hs over
+// all of them); plane_lo/plane_hi: the rows whose level-0 planes are stored
+// (a band's outer margin feeds only level 1)
 int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
-                     long stride, int F, hipStream_t st, int row_lo = 0, int row_hi = 1 << 30) {
+                     long stride, int F, hipStream_t st, int row_lo = 0, int row_hi = 1 << 30, int plane_lo = 0,
+                     int plane_hi = 1 << 30) {
   const int W = d->ncols, H = d->nrows;
   const DefTaps T = default_taps(d);
   const bool two = d->nlevels == 2;
@@ -736,14 +748,15 @@ int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const u
   const int vec_out = (W % 4 == 0) ? 1 : 0;
   const long fs0 = (long)W * H, fsh = hs_size(W1, H), fs1 = (long)W1 * H1;
   int r0 = clampi(row_lo, 0, H), r1 = row_hi >= H ? H : clampi(row_hi, r0, H);
+  int p0 = clampi(plane_lo, 0, H), p1 = plane_hi >= H ? H : clampi(plane_hi, p0, H);
   {
     TimedScope ts(c, T_L0, st, F);
     if (launch_l0(c, st, src, pitch, stride, W, H, T, vec_u8, vec_out, K.lv[0].img, K.lv[0].gx, K.lv[0].gy, K.hs,
-                  W1, (two && W1 > 0) ? 1 : 0, fs0, fsh, F, r0, r1))
+                  W1, (two && W1 > 0) ? 1 : 0, fs0, fsh, F, r0, r1, &p0, &p1))
       return -1;
   }
-  K.vlo[0] = r0;
-  K.vhi[0] = r1 >= H ? (1 << 30) : r1;
+  K.vlo[0] = p0;
+  K.vhi[0] = p1 >= H ? (1 << 30) : p1;
   if (two && (long)W1 * H1 > 0) {
     // level-1 row Y (img1 and its gradients) reads hs rows 4Y-20 .. 4Y+24:
     // it is exact when those lie inside the built level-0 rows (or past an
@@ -1599,6 +1612,21 @@ struct BandSpec {
   int next_n;
 };
 
+// The rows of a band whose level-0 planes are built.  A feature owned by the
+// band reads level-0 rows within a few of its own (its window and the chunk's
+// motion) but level-1 rows whose sigma-3.6 support reaches 32 rows above and
+// 40 below it, so the outer part of each margin -- all but its first 8 rows,
+// at most 32 -- builds only the rows pass hs (k_pyr_l0 tiles without planes).
+// The tracker's band test still guards level 0 with these rows.
+void band_planes(const BandSpec &b, int &p0, int &p1) {
+  constexpr int kKeep = 8, kSkip = 32;
+  p0 = b.row_lo;
+  p1 = b.row_hi;
+  if (isfinite(b.own[0])) p0 = b.row_lo + clampi((int)b.own[0] - b.row_lo - kKeep, 0, kSkip);
+  if (isfinite(b.own[1])) p1 = b.row_hi - clampi(b.row_hi - (int)ceilf(b.own[1]) - kKeep, 0, kSkip);
+  if (p1 < p0) p1 = p0;
+}
+
 int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
                       const unsigned char *frames, long pitch, long stride, int nframes, int chunk, float *x,
                       float *y, int *val, int n, float *tab_x, float *tab_y, int *tab_val, long tab_stride,
@@ -1710,7 +1738,9 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     if (prebuilt) {
       // ev_bbuilt[bi] was recorded after that build: the wait below orders it
     } else if (fz) {
-      if (band ? build_fused_bank(c, K, pd, src, pitch, stride, Fc, ps, band->row_lo, band->row_hi)
+      int p0 = 0, p1 = 1 << 30;
+      if (band) band_planes(*band, p0, p1);
+      if (band ? build_fused_bank(c, K, pd, src, pitch, stride, Fc, ps, band->row_lo, band->row_hi, p0, p1)
                : build_fused_bank(c, K, pd, src, pitch, stride, Fc, ps))
         return -1;
     } else {
@@ -1754,7 +1784,10 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     const int bj = c->bank_next;
     const int Fn = band->next_n < chunk ? band->next_n : chunk;
     HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_bfree[bj], 0));
-    if (build_fused_bank(c, c->bank[bj], pd, band->next, pitch, stride, Fn, c->pstream, band->row_lo, band->row_hi))
+    int p0 = 0, p1 = 1 << 30;
+    band_planes(*band, p0, p1);
+    if (build_fused_bank(c, c->bank[bj], pd, band->next, pitch, stride, Fn, c->pstream, band->row_lo, band->row_hi,
+                         p0, p1))
       return -1;
     HIPCHK(c, hipEventRecord(c->ev_bbuilt[bj], c->pstream));
     c->pre.bank = bj;
