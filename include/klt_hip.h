@@ -198,7 +198,13 @@ int klt_hip_pyramid_path(klt_hip_ctx *ctx, int slot);
 int klt_hip_level_dims(klt_hip_ctx *ctx, int slot, int level, int *ncols, int *nrows);
 /* synchronous copy of one level plane (which: 0 img, 1 gradx, 2 grady) */
 int klt_hip_download_level(klt_hip_ctx *ctx, int slot, int level, int which, float *host);
-/* device pointer of a level plane (valid until the slot is rebuilt at a new size) */
+/* 1 if the level is stored interleaved ({img, gradx, grady} per pixel: the
+   fused default-parameter pyramid, the layout k_track7 reads), 0 if as three
+   planes (the generic path), -1 for a bad slot/level */
+int klt_hip_level_interleaved(klt_hip_ctx *ctx, int slot, int level);
+/* device pointer of a level plane (valid until the slot is rebuilt at a new
+   size); for an interleaved level: which 0 gives the level's base
+   (pixel i at base + 3 i), 1 and 2 give NULL */
 const float *klt_hip_level_ptr(klt_hip_ctx *ctx, int slot, int level, int which);
 
 /* track n features from slot1 (previous image) to slot2 (current image).

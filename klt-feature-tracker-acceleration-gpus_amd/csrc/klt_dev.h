@@ -84,9 +84,10 @@ inline unsigned blocks_for(long n) { return (unsigned)((n + kBlock - 1) / kBlock
 // tracker arguments (track.hip)
 // ---------------------------------------------------------------------------
 struct TrkLevel {
-  const float *img, *gx, *gy;
+  const float *img, *gx, *gy;  // il: img is the interleaved base ({img, gx, gy} per pixel), gx/gy null
   int w, h;
   int vlo = 0, vhi = 1 << 30;  // rows that hold valid data (a band-built pyramid: fewer)
+  int il = 0;
 };
 
 struct TrkArgs {
@@ -103,6 +104,7 @@ struct TrkArgs {
   int merge_res;     // 1: defer the finest level's residue into the next frame's first pass
   int *escape;       // band mode: set when a window needs rows outside [vlo, vhi)
   int prio;          // 1: tracker waves raise their issue priority (s_setprio 3) over concurrent pyramid waves
+  int aos;           // 1 (k_track7): a level's img is {img, gx, gy} interleaved per pixel (gx/gy unused)
 };
 
 // batched frames: frame j tracks pyramid j-1 -> j of a bank; row j of the
@@ -148,21 +150,25 @@ struct AffArgs {
 // level-0 planes (the others only the sigma-3.6 rows pass, hs)
 hipError_t launch_pyr_l0(hipStream_t st, const uint8_t *src, int pitch, long stride, int W, int H, const DefTaps &T,
                          int vec_u8, int vec_out, float *img, float *gx, float *gy, float *hs, int W1, int do_hs,
-                         long fs0, long fsh, int F, int ty0, int ty1, int py0 = 0, int py1 = 1 << 30);
+                         long fs0, long fsh, int F, int ty0, int ty1, int py0 = 0, int py1 = 1 << 30, int il = 0);
 // k_pyr_l1 over F frames, level-1 tile rows [ty0, ty1)
+// il != 0 (both): the planes interleaved per pixel, {img, gx, gy} at img + 3*(y*w + x); gx/gy unused
 hipError_t launch_pyr_l1(hipStream_t st, const float *hs, int W1, int H, int H1, const DefTaps &T, int vec,
-                         float *img1, float *gx1, float *gy1, long fsh, long fs1, int F, int ty0, int ty1);
+                         float *img1, float *gx1, float *gy1, long fsh, long fs1, int F, int ty0, int ty1, int il = 0);
 // generic one-pass kernels (any sigma / levels / subsampling)
 hipError_t launch_u8_to_f32(hipStream_t st, const uint8_t *src, long pitch, int W, int H, float *out);
 hipError_t launch_rows(hipStream_t st, const float *in, int W, int H, const RTaps &t, float *out);
 hipError_t launch_cols(hipStream_t st, const float *in, int W, int H, const RTaps &t, float *out);
 hipError_t launch_subsample(hipStream_t st, const float *in, int W, int ss, float *out, int W1, int H1);
-// trackability map over the nx x ny grid from (bx, by), step apart
-hipError_t launch_min_eigen(hipStream_t st, const float *gx, const float *gy, int W, int bx, int by, int step, int nx,
-                            int ny, int hw, int hh, int *out);
+// trackability map over the nx x ny grid from (bx, by), step apart; ps: the
+// gradients' pixel stride (1 planes, 3 an interleaved level's gx = base+1, gy = base+2)
+hipError_t launch_min_eigen(hipStream_t st, const float *gx, const float *gy, int W, int ps, int bx, int by, int step,
+                            int nx, int ny, int hw, int hh, int *out);
 hipError_t launch_synth(hipStream_t st, unsigned long long seed, int t0, int n, int W, int H, int row0, uint8_t *out,
                         long pitch, long fstride);
 hipError_t launch_selftest_sqrt(const double *in, double *out, int n);
+// n pixels of an interleaved level into three planes
+hipError_t launch_from_il(hipStream_t st, const float *il, float *img, float *gx, float *gy, long n);
 // n 32-bit words, 16-byte aligned ends (device or mapped pinned host memory)
 hipError_t launch_copy_words(hipStream_t st, const void *src, void *dst, long n);
 hipError_t launch_selftest_div(const float *a, const float *b, float *out, int n);

@@ -127,7 +127,9 @@ __device__ unsigned long long *g_pyr_prof;
 
 // Edge tiles (INT false) clamp their loads and apply the zero-border rules per
 // element; interior tiles (~90 % at 1080p, 94 % at 4K) need neither.
-template <bool INT>
+// IL: the level's planes interleaved per pixel, {img, gx, gy} (12 bytes) at
+// img0 + 3*(y*W + x) -- written in E, where img0 is still in LDS; gx0/gy0 unused
+template <bool INT, bool IL>
 __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8_t *__restrict__ src, int spitch,
                                             int W, int H, const DefTaps &T, int vec_u8,
                                             float *__restrict__ img0, float *__restrict__ gx0,
@@ -252,7 +254,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
   const int g16 = tid & 15, r16 = tid >> 4;
 #pragma unroll
   for (int k = 0; k < TH / 16; ++k) {
-    if (!planes) break;
+    if (!planes || IL) break;
     const int r = r16 + 16 * k, g = g16;
     const int y = R0 + r, x = C0 + 4 * g;
     const f4 val = ld4(im + (r + RG) * PI + 8 + 4 * g);
@@ -350,7 +352,30 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
         if (m != kDC) ay += vy[rr + m] * f2{T.d[m], T.d[m]};
       }
       const int y = R0 + 4 * b + rr, x = C0 + 2 * g;
-      if (INT) {
+      if (IL) {
+        const f2 iv = *reinterpret_cast<const f2 *>(im + (4 * b + rr + RG) * PI + 8 + 2 * g);
+        if (INT) {
+          float *o = img0 + 3u * (unsigned)(y * W + x);
+          st2_out(o, f2{iv.x, ax.x});
+          st2_out(o + 2, f2{ay.x, iv.y});
+          st2_out(o + 4, f2{ax.y, ay.y});
+        } else {
+          if (y >= H || x >= W) continue;
+          if (!(y >= RG && y < H - RG)) {
+            ax = f2{0.0f, 0.0f};
+            ay = ax;
+          }
+          float *o = img0 + 3u * (unsigned)(y * W + x);
+          o[0] = iv.x;
+          o[1] = ax.x;
+          o[2] = ay.x;
+          if (x + 1 < W) {
+            o[3] = iv.y;
+            o[4] = ax.y;
+            o[5] = ay.y;
+          }
+        }
+      } else if (INT) {
         st2_out(gx0 + (unsigned)(y * W + x), ax);
         st2_out(gy0 + (unsigned)(y * W + x), ay);
       } else {
@@ -387,6 +412,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
 #endif
 }
 
+template <bool IL>
 __global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ src, int spitch, int W, int H,
                                                    DefTaps T, int vec_u8, float *__restrict__ img0,
                                                    float *__restrict__ gx0, float *__restrict__ gy0,
@@ -412,10 +438,10 @@ __global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ s
                         R0 >= 5 && R0 + l0::TH + 7 <= H;
   const bool planes = by + ty0 >= py0 && by + ty0 < py1;  // tile rows [py0, py1) store img0, gx0, gy0
   if (interior)
-    pyr_l0_tile<true>(lds, src, spitch, W, H, T, vec_u8, img0, gx0, gy0, hs, hsW, do_hs, vec_out, C0, R0,
+    pyr_l0_tile<true, IL>(lds, src, spitch, W, H, T, vec_u8, img0, gx0, gy0, hs, hsW, do_hs, vec_out, C0, R0,
                       threadIdx.x, planes);
   else
-    pyr_l0_tile<false>(lds, src, spitch, W, H, T, vec_u8, img0, gx0, gy0, hs, hsW, do_hs, vec_out, C0, R0,
+    pyr_l0_tile<false, IL>(lds, src, spitch, W, H, T, vec_u8, img0, gx0, gy0, hs, hsW, do_hs, vec_out, C0, R0,
                        threadIdx.x, planes);
 }
 
@@ -430,10 +456,11 @@ constexpr int JH = TH + 2 * RG;                 // img1 rows: Y in [y0-3, y0+TH+
 constexpr int HR = SS * (JH - 1) + 2 * RP + 1;  // hs rows: [4y0-20, 4y0-20+HR)
 constexpr int LDS_H = HR * JW, LDS_J = JH * JW, LDS_X = JH * TW;
 constexpr int LDS = LDS_H + LDS_J;
-static_assert(2 * LDS_X <= LDS_H, "tx/ty reuse the hs region");
+static_assert(2 * LDS_X + TH * 3 * TW <= LDS_H, "tx/ty and the interleaved output tile reuse the hs region");
 static_assert(HR == geom::L1_HR, "geometry");
 }  // namespace l1
 
+template <bool IL>
 __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs, int W1, int H, int H1,
                                                    DefTaps T, int vec, float *__restrict__ img1,
                                                    float *__restrict__ gx1, float *__restrict__ gy1,
@@ -448,6 +475,7 @@ __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs,
   float *im = lds + LDS_H;  // [JH][JW]
   float *tx = lds;          // [JH][TW]
   float *ty = lds + LDS_X;
+  float *stg = lds + 2 * LDS_X;  // IL: the interleaved output tile [TH][3 TW], past tx/ty
 
   int bx, by;
   if (!xcd_tile(tiles_x, tiles_y, bx, by)) return;
@@ -499,7 +527,7 @@ __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs,
   }
   __syncthreads();
 
-  for (int i = tid; i < TH * (TW / 4); i += NT) {  // img1 tile out
+  for (int i = IL ? TH * (TW / 4) : tid; i < TH * (TW / 4); i += NT) {  // img1 tile out (IL: with the gradients)
     const int r = i / (TW / 4), g = i - r * (TW / 4);
     const int Y = y0 + r, X = x0 + 4 * g;
     if (Y >= H1 || X >= W1) continue;
@@ -550,6 +578,17 @@ __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs,
       ax = f4{0.0f, 0.0f, 0.0f, 0.0f};
       ay = ax;
     }
+    if (IL) {
+      // the tile interleaved in LDS first (the hs region past tx/ty), then
+      // copied out in whole rows: every store instruction writes contiguous
+      // 16-byte pieces (a per-pixel triple stride would split them 3 ways)
+      const f4 iv = ld4(im + (r + RG) * JW + 4 + 4 * g);
+      float *o = stg + r * (3 * TW) + 12 * g;
+      st4(o, f4{iv.x, ax.x, ay.x, iv.y});
+      st4(o + 4, f4{ax.y, ay.y, iv.z, ax.z});
+      st4(o + 8, f4{ay.z, iv.w, ax.w, ay.w});
+      continue;
+    }
     float *px = gx1 + (long)Y * W1 + X;
     float *py = gy1 + (long)Y * W1 + X;
     if (vec && X + 3 < W1) {
@@ -559,6 +598,22 @@ __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs,
       for (int e = 0; e < 4 && X + e < W1; ++e) {
         px[e] = ax[e];
         py[e] = ay[e];
+      }
+    }
+  }
+  if (IL) {
+    __syncthreads();
+    const int nx = min(TW, W1 - x0);  // valid pixels of each tile row
+    float *base = img1 + 3 * (long)x0;
+    if (vec && nx == TW) {
+      for (int i = tid; i < TH * (3 * TW / 4); i += NT) {
+        const int r = i / (3 * TW / 4), q = i - r * (3 * TW / 4);
+        if (y0 + r < H1) st4(base + 3 * (long)(y0 + r) * W1 + 4 * q, ld4(stg + r * (3 * TW) + 4 * q));
+      }
+    } else {
+      for (int i = tid; i < TH * 3 * TW; i += NT) {
+        const int r = i / (3 * TW), q = i - r * (3 * TW);
+        if (y0 + r < H1 && q < 3 * nx) base[3 * (long)(y0 + r) * W1 + q] = stg[r * (3 * TW) + q];
       }
     }
   }
@@ -623,8 +678,9 @@ __device__ __forceinline__ int x86_ftoi(float v) {
   return (int)v;
 }
 
+// gx/gy: the gradient planes, or an interleaved level's gx/gy (base + 1, +2) with ps = 3
 __global__ __launch_bounds__(kBlock) void k_min_eigen(const float *__restrict__ gx,
-                                                      const float *__restrict__ gy, int W, int bx,
+                                                      const float *__restrict__ gy, int W, int ps, int bx,
                                                       int by, int step, int nx, int ny, int hw, int hh,
                                                       int *__restrict__ out) {
   const long i = (long)blockIdx.x * kBlock + threadIdx.x;
@@ -633,10 +689,10 @@ __global__ __launch_bounds__(kBlock) void k_min_eigen(const float *__restrict__ 
   const int x = bx + ix * step, y = by + iy * step;
   float sxx = 0.0f, sxy = 0.0f, syy = 0.0f;
   for (int v = y - hh; v <= y + hh; ++v) {
-    const float *px = gx + (long)v * W;
-    const float *py = gy + (long)v * W;
+    const float *px = gx + (long)v * W * ps;
+    const float *py = gy + (long)v * W * ps;
     for (int u = x - hw; u <= x + hw; ++u) {
-      const float a = px[u], b = py[u];
+      const float a = px[(long)u * ps], b = py[(long)u * ps];
       sxx += a * a;
       sxy += a * b;
       syy += b * b;
@@ -658,6 +714,17 @@ __global__ __launch_bounds__(kBlock) void k_synth(unsigned long long seed, int t
   const int y = (int)(i / W), x = (int)(i - (long)y * W);
   const int t = t0 + blockIdx.y;
   out[(long)blockIdx.y * fstride + (long)y * pitch + x] = klt_synth_pixel(seed, t, x, row0 + y);
+}
+
+// an interleaved level ({img, gx, gy} per pixel) as three planes, for the
+// kernels that read planes (the generic tracker, the affine check)
+__global__ __launch_bounds__(kBlock) void k_from_il(const float *__restrict__ il, float *__restrict__ img,
+                                                    float *__restrict__ gx, float *__restrict__ gy, long n) {
+  const long i = (long)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  img[i] = il[3 * i];
+  gx[i] = il[3 * i + 1];
+  gy[i] = il[3 * i + 2];
 }
 
 // n 32-bit words from src to dst (16-byte aligned), 16 bytes per thread; one
@@ -689,23 +756,31 @@ __global__ void k_selftest_div(const float *a, const float *b, float *out, int n
 // ---------------------------------------------------------------------------
 hipError_t launch_pyr_l0(hipStream_t st, const uint8_t *src, int pitch, long stride, int W, int H, const DefTaps &T,
                          int vec_u8, int vec_out, float *img, float *gx, float *gy, float *hs, int W1, int do_hs,
-                         long fs0, long fsh, int F, int ty0, int ty1, int py0, int py1) {
+                         long fs0, long fsh, int F, int ty0, int ty1, int py0, int py1, int il) {
   const int tx = (W + l0::TW - 1) / l0::TW;
   if (F <= 0 || ty1 <= ty0) return hipSuccess;
 #ifdef KLT_EXP_NOHS  // timing experiment only: level 0 without the sigma-3.6 rows pass
   do_hs = 0;
 #endif
-  hipLaunchKernelGGL(k_pyr_l0, dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(kBlock), 0, st, src, pitch, W, H, T,
-                     vec_u8, img, gx, gy, hs, W1, do_hs, vec_out, stride, fs0, fsh, ty0, tx, ty1 - ty0, py0, py1);
+  if (il)
+    hipLaunchKernelGGL(k_pyr_l0<true>, dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(kBlock), 0, st, src, pitch, W, H,
+                       T, vec_u8, img, gx, gy, hs, W1, do_hs, vec_out, stride, fs0, fsh, ty0, tx, ty1 - ty0, py0, py1);
+  else
+    hipLaunchKernelGGL(k_pyr_l0<false>, dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(kBlock), 0, st, src, pitch, W, H,
+                       T, vec_u8, img, gx, gy, hs, W1, do_hs, vec_out, stride, fs0, fsh, ty0, tx, ty1 - ty0, py0, py1);
   return hipGetLastError();
 }
 
 hipError_t launch_pyr_l1(hipStream_t st, const float *hs, int W1, int H, int H1, const DefTaps &T, int vec,
-                         float *img1, float *gx1, float *gy1, long fsh, long fs1, int F, int ty0, int ty1) {
+                         float *img1, float *gx1, float *gy1, long fsh, long fs1, int F, int ty0, int ty1, int il) {
   const int tx = (W1 + l1::TW - 1) / l1::TW;
   if (F <= 0 || ty1 <= ty0) return hipSuccess;
-  hipLaunchKernelGGL(k_pyr_l1, dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(l1::NT), 0, st, hs, W1, H, H1, T, vec,
-                     img1, gx1, gy1, fsh, fs1, ty0, tx, ty1 - ty0);
+  if (il)
+    hipLaunchKernelGGL(k_pyr_l1<true>, dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(l1::NT), 0, st, hs, W1, H, H1, T,
+                       vec, img1, gx1, gy1, fsh, fs1, ty0, tx, ty1 - ty0);
+  else
+    hipLaunchKernelGGL(k_pyr_l1<false>, dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(l1::NT), 0, st, hs, W1, H, H1, T,
+                       vec, img1, gx1, gy1, fsh, fs1, ty0, tx, ty1 - ty0);
   return hipGetLastError();
 }
 
@@ -737,12 +812,12 @@ hipError_t launch_subsample(hipStream_t st, const float *in, int W, int ss, floa
   return hipGetLastError();
 }
 
-hipError_t launch_min_eigen(hipStream_t st, const float *gx, const float *gy, int W, int bx, int by, int step, int nx,
-                            int ny, int hw, int hh, int *out) {
+hipError_t launch_min_eigen(hipStream_t st, const float *gx, const float *gy, int W, int ps, int bx, int by, int step,
+                            int nx, int ny, int hw, int hh, int *out) {
   const long np = (long)nx * ny;
   if (np == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_min_eigen, dim3(blocks_for(np)), dim3(kBlock), 0, st, gx, gy, W, bx, by, step, nx, ny, hw, hh,
-                     out);
+  hipLaunchKernelGGL(k_min_eigen, dim3(blocks_for(np)), dim3(kBlock), 0, st, gx, gy, W, ps, bx, by, step, nx, ny, hw,
+                     hh, out);
   return hipGetLastError();
 }
 
@@ -763,6 +838,12 @@ hipError_t launch_copy_words(hipStream_t st, const void *src, void *dst, long n)
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_copy_words, dim3(blocks_for((n + 3) / 4)), dim3(kBlock), 0, st,
                      reinterpret_cast<const uint32_t *>(src), reinterpret_cast<uint32_t *>(dst), n);
+  return hipGetLastError();
+}
+
+hipError_t launch_from_il(hipStream_t st, const float *il, float *img, float *gx, float *gy, long n) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_from_il, dim3(blocks_for(n)), dim3(kBlock), 0, st, il, img, gx, gy, n);
   return hipGetLastError();
 }
 

@@ -29,11 +29,24 @@ using namespace kltdev;
 // ===========================================================================
 // host side
 // ===========================================================================
+// A level's storage is one block of 3 * cap floats, img | gx | gy.  Built by
+// the fused kernels it holds the level interleaved (il: {img, gx, gy} per
+// pixel from img on, the form the default tracker reads); built by the
+// generic one-pass kernels it holds the three planes at img, gx and gy.
 struct Level {
   int w = 0, h = 0;
-  float *img = nullptr, *gx = nullptr, *gy = nullptr;
+  float *img = nullptr, *gx = nullptr, *gy = nullptr;  // gx = img + cap, gy = img + 2 cap
   size_t cap = 0;  // floats per plane
+  int il = 0;      // contents interleaved
 };
+
+// a slot's level, or frame f of a bank's (interleaved levels: img is the
+// frame's interleaved base, gx/gy null)
+static TrkLevel level_view(const Level &L, long f = 0, int vlo = 0, int vhi = 1 << 30) {
+  const long n = (long)L.w * L.h;
+  if (L.il) return TrkLevel{L.img + 3 * f * n, nullptr, nullptr, L.w, L.h, vlo, vhi, 1};
+  return TrkLevel{L.img + f * n, L.gx + f * n, L.gy + f * n, L.w, L.h, vlo, vhi, 0};
+}
 
 struct Slot {
   int nlev = 0;
@@ -176,6 +189,10 @@ struct klt_hip_ctx {
   int track_patch = 1;  // one-feature waves gather through a lane patch when the window fits
   int track_merge = 1;   // defer finest-level residues into the next frame's first pass (ResCarry)
   int track_prio = 1;    // tracker waves at issue priority 3 (klt_hip_set_track_prio)
+  // planes of interleaved levels for the kernels that read planes (the generic
+  // tracker, the affine check): [0] image 1, [1] image 2 (a batch of frames)
+  float *pl_scr[2][KLT_HIP_MAX_LEVELS] = {};
+  size_t pl_cap[2][KLT_HIP_MAX_LEVELS] = {};
   int track_impl = 0;    // 0: track7.hip for the default configuration, 1: the generic k_track_frames_g
   int serial_frames = 1;  // klt_hip_track_frames: 1 builds and tracks on one stream (default: the
                           // tracker and the pyramid kernels compete for the same CUs; overlap buys ~3 %)
@@ -373,14 +390,12 @@ int ensure_slot(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d) {
     size_t n = (size_t)w * h;
     if (L.cap < n || !L.img) {
       if (L.img) hipFree(L.img);
-      if (L.gx) hipFree(L.gx);
-      if (L.gy) hipFree(L.gy);
       L.img = L.gx = L.gy = nullptr;
-      size_t m = n ? n : 1;
-      HIPCHK(c, hipMalloc((void **)&L.img, m * sizeof(float)));
-      HIPCHK(c, hipMalloc((void **)&L.gx, m * sizeof(float)));
-      HIPCHK(c, hipMalloc((void **)&L.gy, m * sizeof(float)));
-      L.cap = n;
+      const size_t m = n ? n : 1;
+      HIPCHK(c, hipMalloc((void **)&L.img, 3 * m * sizeof(float)));
+      L.gx = L.img + m;
+      L.gy = L.img + 2 * m;
+      L.cap = m;
     }
     w /= d->subsampling > 0 ? d->subsampling : 1;
     h /= d->subsampling > 0 ? d->subsampling : 1;
@@ -393,6 +408,7 @@ int ensure_slot(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d) {
 int build_generic(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
                   hipStream_t st) {
   Slot &S = c->slot[s];
+  for (int l = 0; l < d->nlevels; ++l) S.lv[l].il = 0;  // planes
   const long n0 = (long)d->ncols * d->nrows;
   if (grow(c, &c->d_tmp[0], &c->tmp_cap[0], (size_t)n0)) return -1;
   if (grow(c, &c->d_tmp[1], &c->tmp_cap[1], (size_t)n0)) return -1;
@@ -448,7 +464,8 @@ DefTaps default_taps(const klt_hip_pyr_desc *d) {
 // the rows actually built are returned in r0/r1.
 int launch_l0(klt_hip_ctx *c, hipStream_t st, const uint8_t *src, long pitch, long stride, int W, int H,
               const DefTaps &T, int vec_u8, int vec_out, float *img, float *gx, float *gy, float *hs, int W1,
-              int do_hs, long fs0, long fsh, int F, int &r0, int &r1, int *p0 = nullptr, int *p1 = nullptr) {
+              int do_hs, long fs0, long fsh, int F, int &r0, int &r1, int *p0 = nullptr, int *p1 = nullptr,
+              int il = 0) {
   if (r1 <= r0 || F <= 0) return 0;
   const int TH = geom::L0_TH;
   const int nty = (H + TH - 1) / TH;
@@ -464,7 +481,7 @@ int launch_l0(klt_hip_ctx *c, hipStream_t st, const uint8_t *src, long pitch, lo
     *p1 = py1 >= nty ? H : py1 * TH;
   }
   return launched(c, "k_pyr_l0", launch_pyr_l0(st, src, (int)pitch, stride, W, H, T, vec_u8, vec_out, img, gx, gy,
-                                               hs, W1, do_hs, fs0, fsh, F, ty0, ty1, py0, py1));
+                                               hs, W1, do_hs, fs0, fsh, F, ty0, ty1, py0, py1, il));
 }
 
 int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
@@ -474,6 +491,7 @@ int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t 
   const DefTaps T = default_taps(d);
   const bool two = d->nlevels == 2;
   const int W1 = two ? S.lv[1].w : 0, H1 = two ? S.lv[1].h : 0;
+  for (int l = 0; l < d->nlevels; ++l) S.lv[l].il = 1;  // interleaved
   if (two && grow(c, &c->d_hs, &c->hs_cap, (size_t)hs_size(W1 > 0 ? W1 : 1, H))) return -1;
   if ((long)W * H == 0) return 0;
   const int vec_u8 = (W % 4 == 0 && W >= 16 && pitch % 4 == 0 && ((uintptr_t)src & 3) == 0) ? 1 : 0;
@@ -482,7 +500,7 @@ int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t 
     TimedScope ts(c, T_L0, st);
     int r0 = 0, r1 = H;
     if (launch_l0(c, st, src, pitch, 0L, W, H, T, vec_u8, vec_out, S.lv[0].img, S.lv[0].gx, S.lv[0].gy, c->d_hs,
-                  W1, (two && W1 > 0) ? 1 : 0, 0L, 0L, 1, r0, r1))
+                  W1, (two && W1 > 0) ? 1 : 0, 0L, 0L, 1, r0, r1, nullptr, nullptr, 1))
       return -1;
   }
   if (two && (long)W1 * H1 > 0) {
@@ -490,7 +508,7 @@ int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t 
     const int vec = (W1 % 4 == 0 && W1 >= 8) ? 1 : 0;
     const int ty = (H1 + geom::L1_TH - 1) / geom::L1_TH;
     if (launched(c, "k_pyr_l1", launch_pyr_l1(st, c->d_hs, W1, H, H1, T, vec, S.lv[1].img, S.lv[1].gx, S.lv[1].gy,
-                                              0L, 0L, 1, 0, ty)))
+                                              0L, 0L, 1, 0, ty, 1)))
       return -1;
   }
   return 0;
@@ -569,6 +587,7 @@ int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc
   TrkArgs aa = a;
   aa.merge_res = c->track_merge;
   aa.prio = c->track_prio;
+  aa.aos = 0;
   // the default configuration: the latency-lean kernel (track7.hip) unless
   // the context asks for the generic one (klt_hip_set_track_impl, A/B only)
 #ifdef KLT_TRACK_PROF
@@ -576,8 +595,27 @@ int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc
 #else
   const bool prof_ok = !c->prof;
 #endif
-  if (c->track_impl == 0 && win7 && exact && !li && c->track_patch && prof_ok)
-    return launched(c, "k_track7", launch_track7(st, aa.escape != nullptr, aa, b2, x, y, v, n));
+  const bool t7 = c->track_impl == 0 && win7 && exact && !li && c->track_patch && prof_ok;
+  // k_track7 reads interleaved levels as built; other kernels (or a mix of
+  // layouts) get planes of the interleaved ones
+  const bool ilA = a.A[0].il != 0, ilB = a.B[0].il != 0;
+  if (t7 && ilA && ilB) {
+    aa.aos = 1;
+  } else if (ilA || ilB) {
+    for (int l = 0; l < a.nlev; ++l) {
+      for (int k = 0; k < 2; ++k) {
+        TrkLevel &L = k == 0 ? aa.A[l] : aa.B[l];
+        if (!L.il) continue;
+        const long np = (long)L.w * L.h, F = k == 0 ? 1 : bb.nframes;
+        if (grow(c, &c->pl_scr[k][l], &c->pl_cap[k][l], (size_t)(3 * np * F))) return -1;
+        float *p = c->pl_scr[k][l];
+        if (launched(c, "k_from_il", launch_from_il(st, L.img, p, p + np * F, p + 2 * np * F, np * F))) return -1;
+        L = TrkLevel{p, p + np * F, p + 2 * np * F, L.w, L.h, L.vlo, L.vhi, 0};
+        if (k == 1) bb.lfs[l] = np;
+      }
+    }
+  }
+  if (t7) return launched(c, "k_track7", launch_track7(st, aa.escape != nullptr, aa, b2, x, y, v, n));
   return launched(c, "k_track_frames", launch_track_frames(st, exact, li, patch, win7, npx, aa, b2, x, y, v, n));
 }
 
@@ -608,8 +646,7 @@ size_t bank_arena_bytes(const klt_hip_pyr_desc *d, int frames) {
   size_t total = 0;
   auto add = [&](size_t floats) { total = (total + kPlaneAlign - 1) / kPlaneAlign * kPlaneAlign + floats * sizeof(float); };
   for (int b = 0; b < 3; ++b) {
-    for (int l = 0; l < d->nlevels; ++l)
-      for (int p = 0; p < 3; ++p) add(bank_plane_floats(d, l, frames));
+    for (int l = 0; l < d->nlevels; ++l) add(3 * bank_plane_floats(d, l, frames));  // one block per level
     if (d->nlevels == 2) add(bank_hs_floats(d, frames));
   }
   return total;
@@ -623,11 +660,7 @@ size_t env_size(const char *name, size_t dflt) {
 void free_banks(klt_hip_ctx *c) {
   for (auto &K : c->bank) {
     for (auto &L : K.lv) {
-      if (!c->bank_arena) {
-        hipFree(L.img);
-        hipFree(L.gx);
-        hipFree(L.gy);
-      }
+      if (!c->bank_arena) hipFree(L.img);  // one block per level
       L.img = L.gx = L.gy = nullptr;
       L.cap = 0;
     }
@@ -674,9 +707,7 @@ int ensure_banks(klt_hip_ctx *c, const klt_hip_pyr_desc *d, int frames) {
     for (auto &K : c->bank) {
       for (int l = 0; l < d->nlevels; ++l) {
         const size_t n = bank_plane_floats(d, l, frames);
-        HIPCHK(c, hipMalloc((void **)&K.lv[l].img, n * sizeof(float)));
-        HIPCHK(c, hipMalloc((void **)&K.lv[l].gx, n * sizeof(float)));
-        HIPCHK(c, hipMalloc((void **)&K.lv[l].gy, n * sizeof(float)));
+        HIPCHK(c, hipMalloc((void **)&K.lv[l].img, 3 * n * sizeof(float)));
       }
       if (d->nlevels == 2) HIPCHK(c, hipMalloc((void **)&K.hs, bank_hs_floats(d, frames) * sizeof(float)));
     }
@@ -711,11 +742,9 @@ int ensure_banks(klt_hip_ctx *c, const klt_hip_pyr_desc *d, int frames) {
       L.w = w;
       L.h = h;
       L.cap = bank_plane_floats(d, l, frames);
-      if (arena) {
-        L.img = take(L.cap);
-        L.gx = take(L.cap);
-        L.gy = take(L.cap);
-      }
+      if (arena) L.img = take(3 * L.cap);
+      L.gx = L.img + L.cap;
+      L.gy = L.img + 2 * L.cap;
       w /= K.ss;
       h /= K.ss;
     }
@@ -749,10 +778,11 @@ int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const u
   const long fs0 = (long)W * H, fsh = hs_size(W1, H), fs1 = (long)W1 * H1;
   int r0 = clampi(row_lo, 0, H), r1 = row_hi >= H ? H : clampi(row_hi, r0, H);
   int p0 = clampi(plane_lo, 0, H), p1 = plane_hi >= H ? H : clampi(plane_hi, p0, H);
+  for (int l = 0; l < d->nlevels; ++l) K.lv[l].il = 1;  // interleaved (frame f at img + 3 f w h)
   {
     TimedScope ts(c, T_L0, st, F);
     if (launch_l0(c, st, src, pitch, stride, W, H, T, vec_u8, vec_out, K.lv[0].img, K.lv[0].gx, K.lv[0].gy, K.hs,
-                  W1, (two && W1 > 0) ? 1 : 0, fs0, fsh, F, r0, r1, &p0, &p1))
+                  W1, (two && W1 > 0) ? 1 : 0, 3 * fs0, fsh, F, r0, r1, &p0, &p1, 1))
       return -1;
   }
   K.vlo[0] = p0;
@@ -774,7 +804,7 @@ int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const u
       TimedScope ts(c, T_L1, st, F);
       const int vec = (W1 % 4 == 0 && W1 >= 8) ? 1 : 0;
       if (launched(c, "k_pyr_l1", launch_pyr_l1(st, K.hs, W1, H, H1, T, vec, K.lv[1].img, K.lv[1].gx, K.lv[1].gy,
-                                                fsh, fs1, F, t1lo, t1hi)))
+                                                fsh, 3 * fs1, F, t1lo, t1hi, 1)))
         return -1;
     }
   }
@@ -814,11 +844,7 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
   if (c->own) hipStreamSynchronize(c->own);
   if (c->pstream) hipStreamSynchronize(c->pstream);
   for (auto &S : c->slot)
-    for (auto &L : S.lv) {
-      hipFree(L.img);
-      hipFree(L.gx);
-      hipFree(L.gy);
-    }
+    for (auto &L : S.lv) hipFree(L.img);  // one block per level
   for (int i = 0; i < 2; ++i) {
     hipFree(c->d_u8[i]);
     if (c->h_u8[i]) hipHostFree(c->h_u8[i]);
@@ -1232,15 +1258,29 @@ KLT_API int klt_hip_level_dims(klt_hip_ctx *c, int s, int l, int *w, int *h) {
 KLT_API const float *klt_hip_level_ptr(klt_hip_ctx *c, int s, int l, int which) {
   if (!c || s < 0 || s >= KLT_HIP_MAX_SLOTS || l < 0 || l >= c->slot[s].nlev) return nullptr;
   const Level &L = c->slot[s].lv[l];
+  if (L.il) return which == 0 ? L.img : nullptr;  // interleaved: the level's base
   return which == 0 ? L.img : (which == 1 ? L.gx : L.gy);
 }
 
+KLT_API int klt_hip_level_interleaved(klt_hip_ctx *c, int s, int l) {
+  if (!c || s < 0 || s >= KLT_HIP_MAX_SLOTS || l < 0 || l >= c->slot[s].nlev) return -1;
+  return c->slot[s].lv[l].il;
+}
+
 KLT_API int klt_hip_download_level(klt_hip_ctx *c, int s, int l, int which, float *host) {
-  const float *p = klt_hip_level_ptr(c, s, l, which);
-  if (!p) return fail(c, "download_level: bad slot/level");
+  if (!c || s < 0 || s >= KLT_HIP_MAX_SLOTS || l < 0 || l >= c->slot[s].nlev || which < 0 || which > 2)
+    return fail(c, "download_level: bad slot/level");
   if (use_device(c)) return -1;
   const Level &L = c->slot[s].lv[l];
-  HIPCHK(c, hipMemcpyAsync(host, p, sizeof(float) * L.w * L.h, hipMemcpyDeviceToHost, c->stream));
+  const long n = (long)L.w * L.h;
+  const float *p = which == 0 ? L.img : (which == 1 ? L.gx : L.gy);
+  if (L.il && n > 0) {  // the plane out of the interleaved level first
+    if (grow(c, &c->d_tmp[0], &c->tmp_cap[0], (size_t)(3 * n))) return -1;
+    float *t = c->d_tmp[0];
+    if (launched(c, "k_from_il", launch_from_il(c->stream, L.img, t, t + n, t + 2 * n, n))) return -1;
+    p = t + which * n;
+  }
+  HIPCHK(c, hipMemcpyAsync(host, p, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return 0;
 }
@@ -1306,8 +1346,8 @@ KLT_API int klt_hip_track(klt_hip_ctx *c, int s1, int s2, const klt_hip_track_de
   TrkArgs a;
   fill_trk_args(d, A.nlev, A.ss, A.lv[0].w, A.lv[0].h, a);
   for (int l = 0; l < A.nlev; ++l) {
-    a.A[l] = {A.lv[l].img, A.lv[l].gx, A.lv[l].gy, A.lv[l].w, A.lv[l].h};
-    a.B[l] = {B.lv[l].img, B.lv[l].gx, B.lv[l].gy, B.lv[l].w, B.lv[l].h};
+    a.A[l] = level_view(A.lv[l]);
+    a.B[l] = level_view(B.lv[l]);
   }
 
   float *x_d = x, *y_d = y;
@@ -1429,18 +1469,29 @@ KLT_API int klt_hip_track_affine(klt_hip_ctx *c, int s1, int s2, const klt_hip_t
   if (feat_stage_in(c, x, y, val, n)) return -1;
   if (klt_hip_track(c, s1, s2, d, c->d_fx, c->d_fy, c->d_fv, n, 1)) return -1;
   const Slot &A = c->slot[s1], &B = c->slot[s2];
+  // k_affine reads level 0 as planes
+  TrkLevel pa = level_view(A.lv[0]), pb = level_view(B.lv[0]);
+  for (int k = 0; k < 2; ++k) {
+    TrkLevel &L = k == 0 ? pa : pb;
+    if (!L.il) continue;
+    const long np = (long)L.w * L.h;
+    if (grow(c, &c->pl_scr[k][0], &c->pl_cap[k][0], (size_t)(3 * np))) return -1;
+    float *p = c->pl_scr[k][0];
+    if (launched(c, "k_from_il", launch_from_il(c->stream, L.img, p, p + np, p + 2 * np, np))) return -1;
+    L = TrkLevel{p, p + np, p + 2 * np, L.w, L.h};
+  }
   AffArgs a;
   memset(&a, 0, sizeof a);
-  a.ai = A.lv[0].img;
-  a.agx = A.lv[0].gx;
-  a.agy = A.lv[0].gy;
-  a.aw = A.lv[0].w;
-  a.ah = A.lv[0].h;
-  a.bi = B.lv[0].img;
-  a.bgx = B.lv[0].gx;
-  a.bgy = B.lv[0].gy;
-  a.bw = B.lv[0].w;
-  a.bh = B.lv[0].h;
+  a.ai = pa.img;
+  a.agx = pa.gx;
+  a.agy = pa.gy;
+  a.aw = pa.w;
+  a.ah = pa.h;
+  a.bi = pb.img;
+  a.bgx = pb.gx;
+  a.bgy = pb.gy;
+  a.bw = pb.w;
+  a.bh = pb.h;
   a.xp = c->d_xp;
   a.yp = c->d_yp;
   a.x = c->d_fx;
@@ -1518,14 +1569,9 @@ namespace {
 constexpr int kSeedSlot = KLT_HIP_MAX_SLOTS, kScratchSlot = KLT_HIP_MAX_SLOTS + 1;
 
 TrkLevel prev_level(klt_hip_ctx *c, int l) {
-  if (c->prev.bank < 0) {
-    const Level &L = c->slot[c->prev.slot].lv[l];
-    return TrkLevel{L.img, L.gx, L.gy, L.w, L.h};
-  }
+  if (c->prev.bank < 0) return level_view(c->slot[c->prev.slot].lv[l]);
   const Bank &K = c->bank[c->prev.bank];
-  const Level &L = K.lv[l];
-  const long off = (long)c->prev.frame * L.w * L.h;
-  return TrkLevel{L.img + off, L.gx + off, L.gy + off, L.w, L.h, K.vlo[l], K.vhi[l]};
+  return level_view(K.lv[l], c->prev.frame, K.vlo[l], K.vhi[l]);
 }
 
 bool bank_fits(const Bank &K, const klt_hip_pyr_desc *d, int F) {
@@ -1541,12 +1587,19 @@ bool bank_fits(const Bank &K, const klt_hip_pyr_desc *d, int F) {
   return true;
 }
 
-int copy_level_planes(klt_hip_ctx *c, const Level &from, float *img, float *gx, float *gy, hipStream_t st) {
-  const size_t b = sizeof(float) * (size_t)from.w * from.h;
+// one level (a view: a slot's, or a bank frame's) into frame f of level `to`
+// (a slot's: f = 0), in its layout
+int copy_level(klt_hip_ctx *c, const TrkLevel &from, Level &to, long f, hipStream_t st) {
+  const size_t n = (size_t)from.w * from.h, b = sizeof(float) * n;
+  to.il = from.il;
   if (!b) return 0;
-  HIPCHK(c, hipMemcpyAsync(img, from.img, b, hipMemcpyDeviceToDevice, st));
-  HIPCHK(c, hipMemcpyAsync(gx, from.gx, b, hipMemcpyDeviceToDevice, st));
-  HIPCHK(c, hipMemcpyAsync(gy, from.gy, b, hipMemcpyDeviceToDevice, st));
+  if (from.il) {
+    HIPCHK(c, hipMemcpyAsync(to.img + 3 * f * n, from.img, 3 * b, hipMemcpyDeviceToDevice, st));
+  } else {
+    HIPCHK(c, hipMemcpyAsync(to.img + f * n, from.img, b, hipMemcpyDeviceToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(to.gx + f * n, from.gx, b, hipMemcpyDeviceToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(to.gy + f * n, from.gy, b, hipMemcpyDeviceToDevice, st));
+  }
   return 0;
 }
 }  // namespace
@@ -1591,14 +1644,8 @@ KLT_API int klt_hip_frames_end_slot(klt_hip_ctx *c, int slot) {
   S.fused = 1;
   for (int l = 0; l < nl; ++l) {
     const TrkLevel p = prev_level(c, l);
-    Level from;
-    from.w = p.w;
-    from.h = p.h;
-    from.img = const_cast<float *>(p.img);
-    from.gx = const_cast<float *>(p.gx);
-    from.gy = const_cast<float *>(p.gy);
-    if (from.w != S.lv[l].w || from.h != S.lv[l].h) return fail(c, "frames_end_slot: level %d size mismatch", l);
-    if (copy_level_planes(c, from, S.lv[l].img, S.lv[l].gx, S.lv[l].gy, c->stream)) return -1;
+    if (p.w != S.lv[l].w || p.h != S.lv[l].h) return fail(c, "frames_end_slot: level %d size mismatch", l);
+    if (copy_level(c, p, S.lv[l], 0, c->stream)) return -1;
   }
   return 0;
 }
@@ -1691,17 +1738,8 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     HIPCHK(c, hipStreamSynchronize(c->pstream));
     if (c->prev.bank >= 0) {
       if (ensure_slot(c, kSeedSlot, pd)) return -1;
-      for (int l = 0; l < pd->nlevels; ++l) {
-        const TrkLevel p = prev_level(c, l);
-        Level from;
-        from.w = p.w;
-        from.h = p.h;
-        from.img = const_cast<float *>(p.img);
-        from.gx = const_cast<float *>(p.gx);
-        from.gy = const_cast<float *>(p.gy);
-        const Level &to = c->slot[kSeedSlot].lv[l];
-        if (copy_level_planes(c, from, to.img, to.gx, to.gy, c->stream)) return -1;
-      }
+      for (int l = 0; l < pd->nlevels; ++l)
+        if (copy_level(c, prev_level(c, l), c->slot[kSeedSlot].lv[l], 0, c->stream)) return -1;
       HIPCHK(c, hipStreamSynchronize(c->stream));
       c->prev = PrevRef{-1, 0, kSeedSlot};
     }
@@ -1746,12 +1784,8 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     } else {
       for (int f = 0; f < Fc; ++f) {
         if (build_pyramid_on(c, kScratchSlot, pd, src + (long)f * stride, pitch, 0, ps)) return -1;
-        for (int l = 0; l < pd->nlevels; ++l) {
-          const Level &L = c->slot[kScratchSlot].lv[l];
-          const long off = (long)f * L.w * L.h;
-          if (copy_level_planes(c, L, K.lv[l].img + off, K.lv[l].gx + off, K.lv[l].gy + off, ps))
-            return -1;
-        }
+        for (int l = 0; l < pd->nlevels; ++l)  // generic levels: planes
+          if (copy_level(c, level_view(c->slot[kScratchSlot].lv[l]), K.lv[l], f, ps)) return -1;
       }
     }
     if (!serial) {
@@ -1762,9 +1796,8 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     memset(&b, 0, sizeof b);
     for (int l = 0; l < pd->nlevels; ++l) {
       a.A[l] = prev_level(c, l);
-      a.B[l] = TrkLevel{K.lv[l].img, K.lv[l].gx, K.lv[l].gy, K.lv[l].w, K.lv[l].h, fz ? K.vlo[l] : 0,
-                        fz ? K.vhi[l] : (1 << 30)};
-      b.lfs[l] = (long)K.lv[l].w * K.lv[l].h;
+      a.B[l] = level_view(K.lv[l], 0, fz ? K.vlo[l] : 0, fz ? K.vhi[l] : (1 << 30));
+      b.lfs[l] = (long)K.lv[l].w * K.lv[l].h * (K.lv[l].il ? 3 : 1);
     }
     b.nframes = Fc;
     if (ntab) {
@@ -1998,8 +2031,8 @@ KLT_API int klt_hip_min_eigen(klt_hip_ctx *c, int s, const klt_hip_select_desc *
   if (grow(c, &c->d_eig, &c->eig_cap, (size_t)np)) return -1;
   {
     TimedScope ts(c, T_EIG, c->stream);
-    if (launched(c, "k_min_eigen", launch_min_eigen(c->stream, L.gx, L.gy, L.w, bx, by, step, gx, gy, hw, hh,
-                                                    c->d_eig)))
+    if (launched(c, "k_min_eigen", launch_min_eigen(c->stream, L.il ? L.img + 1 : L.gx, L.il ? L.img + 2 : L.gy,
+                                                    L.w, L.il ? 3 : 1, bx, by, step, gx, gy, hw, hh, c->d_eig)))
       return -1;
   }
   HIPCHK(c, hipMemcpyAsync(vals, c->d_eig, sizeof(int) * np, hipMemcpyDeviceToHost, c->stream));
@@ -2015,7 +2048,8 @@ static int eigen_to_dev(klt_hip_ctx *c, int s, const klt_hip_select_desc *d, int
   const Level &L = c->slot[s].lv[0];
   if (grow(c, &c->d_eig, &c->eig_cap, (size_t)np)) return -1;
   TimedScope ts(c, T_EIG, c->stream);
-  return launched(c, "k_min_eigen", launch_min_eigen(c->stream, L.gx, L.gy, L.w, d->borderx, d->bordery,
+  return launched(c, "k_min_eigen", launch_min_eigen(c->stream, L.il ? L.img + 1 : L.gx, L.il ? L.img + 2 : L.gy,
+                                                     L.w, L.il ? 3 : 1, d->borderx, d->bordery,
                                                      d->nSkippedPixels + 1, *nx, *ny, d->window_width / 2,
                                                      d->window_height / 2, c->d_eig));
 }
@@ -2107,8 +2141,9 @@ KLT_API int klt_hip_min_eigen_rows(klt_hip_ctx *c, const klt_hip_select_desc *d,
   if (ylo < L.vlo || (yhi > L.vhi && L.vhi < L.h)) return 1;
   if (use_device(c)) return -1;
   TimedScope ts(c, T_EIG, c->stream);
-  return launched(c, "k_min_eigen", launch_min_eigen(c->stream, L.gx, L.gy, L.w, bx, by + j0 * step, step, gx, j1 - j0,
-                                                     hw, hh, dev_map + (long)j0 * gx));
+  return launched(c, "k_min_eigen", launch_min_eigen(c->stream, L.il ? L.img + 1 : L.gx, L.il ? L.img + 2 : L.gy,
+                                                     L.w, L.il ? 3 : 1, bx, by + j0 * step, step, gx, j1 - j0, hw,
+                                                     hh, dev_map + (long)j0 * gx));
 }
 
 KLT_API int klt_hip_synth_frames(klt_hip_ctx *c, unsigned long long seed, int t0, int n, int ncols, int nrows,

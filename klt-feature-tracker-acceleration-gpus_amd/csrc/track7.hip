@@ -9,7 +9,10 @@
 // deferred into the next frame's first pass.  What differs is the shape of
 // the code on the chain that one wave walks for each Newton pass:
 //   * lane p < 49 owns window pixel p (row-major, the reference's order) and
-//     gathers its four bilinear corners itself, two 8-byte loads per plane:
+//     gathers its four bilinear corners itself: from a level stored
+//     interleaved ({img, gx, gy} per pixel, as the fused pyramid kernels
+//     write it) one 24-byte run per row for all three planes, from planes
+//     two 8-byte loads per plane:
 //     no lane shuffles and no patch-fit test, so there is no fallback path;
 //     every load of a pass (img2's three planes, img1's on a level's first
 //     pass, the deferred residue's img2 plane) is issued before any is used;
@@ -52,7 +55,8 @@ __device__ __forceinline__ bool out7(float x, float y, int nc, int nr) {
 
 // _interpolate (trackFeatures.c:31-57) for this lane's pixel: corner offset and weights
 struct Pix {
-  unsigned off;
+  unsigned off;  // byte offset of the top-left corner in a plane
+  unsigned px;   // its pixel index
   float w0, w1, w2, w3;
 };
 
@@ -62,7 +66,8 @@ __device__ __forceinline__ Pix pix_at(int w, int h, float x, float y) {
   xt = clampi(xt, 0, w - 2);  // only guards lanes / positions the bounds test excludes
   yt = clampi(yt, 0, h - 2);
   Pix p;
-  p.off = (unsigned)(yt * w + xt) * 4u;
+  p.px = (unsigned)(yt * w + xt);
+  p.off = p.px * 4u;
   p.w0 = (1.0f - ax) * (1.0f - ay);
   p.w1 = ax * (1.0f - ay);
   p.w2 = (1.0f - ax) * ay;
@@ -81,6 +86,36 @@ __device__ __forceinline__ Quad quad(const float *P, const Pix &p, unsigned rowb
   Quad q;
   q.r0 = *reinterpret_cast<const float2 *>(b + p.off);
   q.r1 = *reinterpret_cast<const float2 *>(b + o1);
+  return q;
+}
+
+// interleaved levels ({img, gx, gy} per pixel, 12 bytes): one 24-byte run per
+// row holds both corners of all three planes
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+struct Tri {
+  Quad i, x, y;
+};
+__device__ __forceinline__ Tri tri(const float *P, const Pix &p, unsigned rowb) {
+  const char *b = reinterpret_cast<const char *>(P) + p.px * 12u;
+  const f4u a0 = *reinterpret_cast<const f4u *>(b), b0 = *reinterpret_cast<const f4u *>(b + rowb);
+  const f2u a1 = *reinterpret_cast<const f2u *>(b + 16), b1 = *reinterpret_cast<const f2u *>(b + rowb + 16);
+  Tri t;
+  t.i.r0 = make_float2(a0.x, a0.w);
+  t.i.r1 = make_float2(b0.x, b0.w);
+  t.x.r0 = make_float2(a0.y, a1.x);
+  t.x.r1 = make_float2(b0.y, b1.x);
+  t.y.r0 = make_float2(a0.z, a1.y);
+  t.y.r1 = make_float2(b0.z, b1.y);
+  return t;
+}
+// img alone from an interleaved level
+__device__ __forceinline__ Quad quad_i(const float *P, const Pix &p, unsigned rowb) {
+  const float *b = reinterpret_cast<const float *>(reinterpret_cast<const char *>(P) + p.px * 12u);
+  const float *c = reinterpret_cast<const float *>(reinterpret_cast<const char *>(P) + p.px * 12u + rowb);
+  Quad q;
+  q.r0 = make_float2(b[0], b[3]);
+  q.r1 = make_float2(c[0], c[3]);
   return q;
 }
 
@@ -186,7 +221,7 @@ enum { kPassAgain = 0, kPassDone = 1, kPassOOB = 2, kPassLostPrev = 3 };
 // level's FIRST pass; the deferred residue's img2 plane with a JOB), the
 // ordered sums, the solve.  Separate instances for the first pass and the
 // rest keep the first pass's addresses out of the loop.
-template <bool BAND, bool FIRST, bool JOB>
+template <bool BAND, bool FIRST, bool JOB, bool AOS>
 __device__ __forceinline__ int pass7(const TrkArgs &a, const Lev &A, const Lev &B, float x1, float y1, bool x1_out,
                                      LevState &ls, int lane, float fi, float fj, bool on, float *red, Pending &pd,
                                      const Lev &R, int &rstat, Counts &cnt) {
@@ -201,7 +236,7 @@ __device__ __forceinline__ int pass7(const TrkArgs &a, const Lev &A, const Lev &
     ls.status = kOOB;
     if (JOB) {  // the previous frame's verdict still needs its own pass
       const Pix q = pix_at(R.w, R.h, pd.x2 + fi, pd.y2 + fj);
-      const float rb = interp(q, quad(R.img, q, (unsigned)R.w * 4u));
+      const float rb = interp(q, AOS ? quad_i(R.img, q, (unsigned)R.w * 12u) : quad(R.img, q, (unsigned)R.w * 4u));
       float v[1] = {on ? fabsf(pd.aim - rb) : 0.0f}, S[1];
       ++cnt.passes;
       sums7<1>(red, lane, on, v, S);
@@ -214,21 +249,38 @@ __device__ __forceinline__ int pass7(const TrkArgs &a, const Lev &A, const Lev &
   T7_ADD(11, t_top);
   T7_T(t_g0);
   ++cnt.passes;
-  const unsigned rowB = (unsigned)B.w * 4u;
+  const unsigned rowB = (unsigned)B.w * (AOS ? 12u : 4u);
   const Pix qb = pix_at(B.w, B.h, ls.x2 + fi, ls.y2 + fj);
-  const Quad bi = quad(B.img, qb, rowB), bx = quad(B.gx, qb, rowB), by = quad(B.gy, qb, rowB);
+  Quad bi, bx, by;
+  if constexpr (AOS) {
+    const Tri t = tri(B.img, qb, rowB);
+    bi = t.i;
+    bx = t.x;
+    by = t.y;
+  } else {
+    bi = quad(B.img, qb, rowB);
+    bx = quad(B.gx, qb, rowB);
+    by = quad(B.gy, qb, rowB);
+  }
   Pix qa = qb, qr = qb;
   Quad ai{}, ax{}, ay{}, ri{};
   if (FIRST) {
-    const unsigned rowA = (unsigned)A.w * 4u;
+    const unsigned rowA = (unsigned)A.w * (AOS ? 12u : 4u);
     qa = pix_at(A.w, A.h, x1 + fi, y1 + fj);
-    ai = quad(A.img, qa, rowA);
-    ax = quad(A.gx, qa, rowA);
-    ay = quad(A.gy, qa, rowA);
+    if constexpr (AOS) {
+      const Tri t = tri(A.img, qa, rowA);
+      ai = t.i;
+      ax = t.x;
+      ay = t.y;
+    } else {
+      ai = quad(A.img, qa, rowA);
+      ax = quad(A.gx, qa, rowA);
+      ay = quad(A.gy, qa, rowA);
+    }
   }
   if (JOB) {
     qr = pix_at(R.w, R.h, pd.x2 + fi, pd.y2 + fj);
-    ri = quad(R.img, qr, (unsigned)R.w * 4u);
+    ri = AOS ? quad_i(R.img, qr, (unsigned)R.w * 12u) : quad(R.img, qr, (unsigned)R.w * 4u);
   }
   if (FIRST) {
     ls.aim = interp(qa, ai);
@@ -284,7 +336,7 @@ __device__ __forceinline__ int pass7(const TrkArgs &a, const Lev &A, const Lev &
 // feature the level stops at once and lost_prev is set).  defer: this
 // (finest) level hands its own residue on (pd) instead of taking a pass for
 // it.  residue: the finest level.
-template <bool BAND>
+template <bool BAND, bool AOS>
 __device__ int level7(const TrkArgs &a, const Lev &A, const Lev &B, float x1, float y1, float &x2, float &y2,
                       int lane, float fi, float fj, bool on, float *red, bool residue, bool defer, Pending &pd,
                       bool job, const Lev &R, int &rstat, bool &lost_prev, Counts &cnt) {
@@ -293,10 +345,10 @@ __device__ int level7(const TrkArgs &a, const Lev &A, const Lev &B, float x1, fl
   LevState ls;
   ls.x2 = x2;
   ls.y2 = y2;
-  int r = job ? pass7<BAND, true, true>(a, A, B, x1, y1, x1_out, ls, lane, fi, fj, on, red, pd, R, rstat, cnt)
-              : pass7<BAND, true, false>(a, A, B, x1, y1, x1_out, ls, lane, fi, fj, on, red, pd, R, rstat, cnt);
+  int r = job ? pass7<BAND, true, true, AOS>(a, A, B, x1, y1, x1_out, ls, lane, fi, fj, on, red, pd, R, rstat, cnt)
+              : pass7<BAND, true, false, AOS>(a, A, B, x1, y1, x1_out, ls, lane, fi, fj, on, red, pd, R, rstat, cnt);
   while (r == kPassAgain)
-    r = pass7<BAND, false, false>(a, A, B, x1, y1, x1_out, ls, lane, fi, fj, on, red, pd, R, rstat, cnt);
+    r = pass7<BAND, false, false, AOS>(a, A, B, x1, y1, x1_out, ls, lane, fi, fj, on, red, pd, R, rstat, cnt);
   x2 = ls.x2;
   y2 = ls.y2;
   if (r == kPassLostPrev) {
@@ -323,7 +375,7 @@ __device__ int level7(const TrkArgs &a, const Lev &A, const Lev &B, float x1, fl
   ++cnt.passes;
   T7_T(t_r0);
   const Pix q = pix_at(B.w, B.h, x2 + fi, y2 + fj);
-  const float rb = interp(q, quad(B.img, q, (unsigned)B.w * 4u));
+  const float rb = interp(q, AOS ? quad_i(B.img, q, (unsigned)B.w * 12u) : quad(B.img, q, (unsigned)B.w * 4u));
   float v[1] = {on ? fabsf(ls.aim - rb) : 0.0f}, S1[1];
   sums7<1>(red, lane, on, v, S1);
   T7_ADD(3, t_r0);
@@ -331,7 +383,7 @@ __device__ int level7(const TrkArgs &a, const Lev &A, const Lev &B, float x1, fl
   return ls.it >= a.max_it ? kMaxIter : kTracked;
 }
 
-template <bool BAND>
+template <bool BAND, bool AOS>
 __global__ __launch_bounds__(kBlock) void k_track7(TrkArgs a, TrkFramesArgs b, float *__restrict__ fx,
                                                    float *__restrict__ fy, int *__restrict__ fv, int n) {
   __shared__ __attribute__((aligned(16))) float red_all[kWaves][kRows * kRow + 4];
@@ -387,7 +439,7 @@ __global__ __launch_bounds__(kBlock) void k_track7(TrkArgs a, TrkFramesArgs b, f
         const Lev LB = lev_of(a.B[r], (long)j * b.lfs[r]);
         const bool lj = job && r == a.nlev - 1;
         T7_T(t_l0);
-        val = level7<BAND>(a, LA, LB, xl, yl, xo, yo, lane, fi, fj, on, red, r == 0,
+        val = level7<BAND, AOS>(a, LA, LB, xl, yl, xo, yo, lane, fi, fj, on, red, r == 0,
                            merge && r == 0 && j + 1 < b.nframes, pd, lj, R, rstat, lost_prev, cnt);
         T7_ADD(10, t_l0);
         if (lost_prev) break;
@@ -458,10 +510,15 @@ hipError_t launch_track7(hipStream_t st, bool band, const TrkArgs &a, const TrkF
                          int *v, int n) {
   const int nb = (n + kWaves - 1) / kWaves;
   const int grid = b.xcd_per > 0 ? 8 * b.xcd_per : nb;
-  if (band)
-    hipLaunchKernelGGL(k_track7<true>, dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
+  // band: escape checks (klt_hip_track_frames_band); aos: interleaved levels
+  if (band && a.aos)
+    hipLaunchKernelGGL((k_track7<true, true>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
+  else if (band)
+    hipLaunchKernelGGL((k_track7<true, false>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
+  else if (a.aos)
+    hipLaunchKernelGGL((k_track7<false, true>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
   else
-    hipLaunchKernelGGL(k_track7<false>, dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
+    hipLaunchKernelGGL((k_track7<false, false>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
   return hipGetLastError();
 }
 

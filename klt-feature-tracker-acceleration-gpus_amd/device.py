@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes
 import ctypes as C
+import os
 
 MAX_TAPS = 71
 MAX_LEVELS = 8
@@ -82,6 +83,7 @@ DEVICE_PROTOS = {
     "klt_hip_level_dims": (C.c_int, [V, C.c_int, C.c_int, IP, IP]),
     "klt_hip_download_level": (C.c_int, [V, C.c_int, C.c_int, C.c_int, V]),
     "klt_hip_level_ptr": (V, [V, C.c_int, C.c_int, C.c_int]),
+    "klt_hip_level_interleaved": (C.c_int, [V, C.c_int, C.c_int]),
     "klt_hip_track": (C.c_int, [V, C.c_int, C.c_int, C.POINTER(TrackDesc), V, V, V, C.c_int, C.c_int]),
     "klt_hip_track_sequence": (C.c_int, [V, C.POINTER(PyrDesc), C.POINTER(TrackDesc), V, C.c_long,
                                          C.c_long, C.c_int, C.c_int, V, V, V, C.c_int, IP]),
@@ -145,7 +147,13 @@ H2D, D2H, D2D = 1, 2, 3  # hipMemcpyKind
 
 
 def bind_device(lib: C.CDLL) -> C.CDLL:
+    # KLT_AMD_LIB may name an older build (same-box A/B tools): its missing
+    # extensions stay unbound; the shipped library exports all of them
+    # (tests/test_abi.py)
+    alt = bool(os.environ.get("KLT_AMD_LIB"))
     for name, (res, args) in DEVICE_PROTOS.items():
+        if alt and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
