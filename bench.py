@@ -15,7 +15,9 @@ no data-path collective; value = total frames / max-over-ranks time.
 
 Extra keys: pyramid_gpix_s, roofline (pyramid pass, HIP events on the launch
 stream; measured_peak: this box's copy/fill GB/s beside the 8 TB/s spec),
-roofline_4k (the same pass at 3840x2160), kernels (avg us per launch), tracker
+roofline_4k (the same pass at 3840x2160 with 20 000 features tracked between
+the launches, BASELINE config 4 on one GPU; pyramids_only: the same frames built
+back to back), kernels (avg us per launch), tracker
 (Newton iterations counted on the device in a separate replay,
 feature-iterations/s over the tracker's own event time), cpu_baseline (the reference compiled
 from its own sources, oracle/_ref, timed on this host), parity (GPU vs that
@@ -453,13 +455,19 @@ def run_sharded(args, world, rank, dev) -> None:
         dist.destroy_process_group()
 
 
-def pass_4k(lib, dev, chunk=64, reps=2):
+def pass_4k(lib, dev, chunk=64, reps=2, nf=20000):
     """The north-star figure (BASELINE.json): the convolve+pyramid pass at
-    3840x2160 against the HBM roofline.  Batched pyramid builds of resident
-    synthetic 4K frames (klt_hip_track_frames with no features: its pyramid
-    launches only), `reps` chunks timed with HIP events on the launch stream
-    after one warm-up chunk.  Algorithmic bytes as for the 1080p line:
-    13.75 B/px (u8 in, img/gx/gy out at both levels)."""
+    3840x2160 against the HBM roofline, in BASELINE config 4's shape on one
+    GPU: resident synthetic 4K frames, `nf` features selected on frame 0 and
+    tracked (klt_hip_track_frames, one stream, 64-frame launches), so every
+    pyramid launch follows a tracker launch as in production.  `reps` chunks
+    are timed with HIP events on the launch stream after one warm-up chunk;
+    each kernel's event time is its own duration (one stream: nothing runs
+    beside it).  The same frames built back to back with no tracking
+    (`pyramids_only`) run the pyramid kernels at the lower clock the chip holds
+    under sustained pyramid load; both are reported.
+    Algorithmic bytes as for the 1080p line: 13.75 B/px (u8 in, img/gx/gy out
+    at both levels)."""
     import torch
     from kltamd.device import PyrDesc, TrackDesc, Timing, check, use_torch_stream
     W, H = 3840, 2160
@@ -468,41 +476,75 @@ def pass_4k(lib, dev, chunk=64, reps=2):
     lib.klt_amd_release_cached_devices()
     torch.cuda.empty_cache()
     tc = lib.KLTCreateTrackingContext()
+    tc.contents.sequentialMode = 1
     ctx = lib.klt_amd_device_context(tc)
     use_torch_stream(lib, ctx, dev)
     n = 1 + chunk * (1 + reps)
     fr = torch.empty((n, H, W), dtype=torch.uint8, device=dev)
     check(lib, ctx, lib.klt_hip_synth_frames(ctx, 2160, 0, n, W, H, C.c_void_p(fr.data_ptr()), W, W * H), "synth")
+    f0 = fr[0].cpu().numpy()
+    fl = lib.KLTCreateFeatureList(nf)
+    lib.KLTSelectGoodFeatures(tc, f0.ctypes.data_as(C.POINTER(C.c_ubyte)), W, H, fl)
+    sel = np.array([[fl.contents.feature[k].contents.x, fl.contents.feature[k].contents.y,
+                     fl.contents.feature[k].contents.val] for k in range(nf)], np.float64)
+    lib.KLTFreeFeatureList(fl)
     pd, td = PyrDesc(), TrackDesc()
     lib.klt_amd_pyr_desc(tc, W, H, tc.contents.nPyramidLevels, 1, C.byref(pd))
     lib.klt_amd_track_desc(tc, C.byref(td))
     base = fr.data_ptr()
 
-    def run(t0, m):
-        check(lib, ctx, lib.klt_hip_track_frames(ctx, C.byref(pd), C.byref(td), C.c_void_p(base + t0 * W * H), W,
-                                                 W * H, m, chunk, None, None, None, 0, None, None, None, 0), "4k")
+    def leg(features):
+        x = torch.from_numpy(sel[:, 0].astype(np.float32)).to(dev)
+        y = torch.from_numpy(sel[:, 1].astype(np.float32)).to(dev)
+        v = torch.from_numpy(sel[:, 2].astype(np.int32)).to(dev)
+        k = nf if features else 0
 
+        def run(t0, m):
+            check(lib, ctx, lib.klt_hip_track_frames(ctx, C.byref(pd), C.byref(td), C.c_void_p(base + t0 * W * H),
+                                                     W, W * H, m, chunk, C.c_void_p(x.data_ptr()),
+                                                     C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()), k, None,
+                                                     None, None, 0), "4k")
+
+        check(lib, ctx, lib.klt_hip_frames_begin(ctx, C.byref(pd), C.c_void_p(base), W), "4k begin")
+        run(1, chunk)
+        torch.cuda.synchronize()
+        lib.klt_hip_set_timing(ctx, 1)
+        run(1 + chunk, chunk * reps)
+        tm = Timing()
+        check(lib, ctx, lib.klt_hip_get_timing(ctx, C.byref(tm)), "4k timing")
+        lib.klt_hip_set_timing(ctx, 0)
+        l0 = 1000.0 * tm.ms_pyr_l0 / tm.frames_pyr_l0
+        l1 = 1000.0 * tm.ms_pyr_l1 / tm.frames_pyr_l1
+        trk = 1000.0 * tm.ms_track / tm.frames_track if tm.frames_track else None
+        return l0, l1, trk, tm, int((v >= 0).sum().item())
+
+    # every bank of the arena is written once before anything is timed (the
+    # legs' timed chunks land in banks their warm-up chunk did not touch)
     check(lib, ctx, lib.klt_hip_frames_begin(ctx, C.byref(pd), C.c_void_p(base), W), "4k begin")
-    run(1, chunk)
+    check(lib, ctx, lib.klt_hip_track_frames(ctx, C.byref(pd), C.byref(td), C.c_void_p(base + W * H), W, W * H,
+                                             n - 1, chunk, None, None, None, 0, None, None, None, 0), "4k touch")
     torch.cuda.synchronize()
-    lib.klt_hip_set_timing(ctx, 1)
-    run(1 + chunk, chunk * reps)
-    tm = Timing()
-    check(lib, ctx, lib.klt_hip_get_timing(ctx, C.byref(tm)), "4k timing")
+    p0, p1, _, ptm, _ = leg(False)
+    l0, l1, trk, tm, live = leg(True)
     lib.KLTFreeTrackingContext(tc)
     del fr
     torch.cuda.empty_cache()
-    l0 = 1000.0 * tm.ms_pyr_l0 / tm.frames_pyr_l0
-    l1 = 1000.0 * tm.ms_pyr_l1 / tm.frames_pyr_l1
     by = W * H * 13 + (W // 4) * (H // 4) * 12
     ach = by / ((l0 + l1) * 1e-6) / 1e9
-    return {"workload": f"{W}x{H} pyramid pass, batched {chunk} frames per launch, pyramids only",
+    pach = by / ((p0 + p1) * 1e-6) / 1e9
+    return {"workload": f"{W}x{H} pyramid pass, batched {chunk} frames per launch, {nf} features tracked between "
+                        "the pyramid launches (BASELINE config 4 on one GPU)",
             "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
             "traffic": None, "frames_per_launch": tm.frames_pyr_l0 / tm.n_pyr_l0,
             "algorithmic_bytes_per_frame": by, "us_per_frame": l0 + l1,
-            "kernels_us_per_frame": {"k_pyr_l0": l0, "k_pyr_l1": l1}, "frames_timed": int(tm.frames_pyr_l0),
+            "kernels_us_per_frame": {"k_pyr_l0": l0, "k_pyr_l1": l1, "k_track": trk}, "frames_timed": int(tm.frames_pyr_l0),
+            "live_features_at_end": live,
             "pyramid_gpix_s": W * H / ((l0 + l1) * 1e-6) / 1e9,
-            "event_timing": "HIP events on the launch stream, one stream"}
+            "event_timing": "HIP events on the launch stream, one stream",
+            "pyramids_only": {"what": "the same frames built back to back with no features tracked",
+                              "achieved": pach, "frac": pach / HBM_PEAK_GBS, "us_per_frame": p0 + p1,
+                              "kernels_us_per_frame": {"k_pyr_l0": p0, "k_pyr_l1": p1},
+                              "frames_timed": int(ptm.frames_pyr_l0)}}
 
 
 def attach_traffic(line, pmc, resolution, fpl) -> None:
