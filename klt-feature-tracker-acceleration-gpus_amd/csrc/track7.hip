@@ -26,11 +26,17 @@
 // Parity: -ffp-contract=off, IEEE division, every expression in the
 // reference's evaluation order.
 #pragma clang fp contract(off)
+// the level loops carry #pragma unroll for the two-level instances; the
+// runtime-depth ones (NL == 0) cannot unroll them, which is expected
+#pragma clang diagnostic ignored "-Wpass-failed"
 
 #include <math.h>
 
 #include "klt_dev.h"
 
+#ifndef KLT_T7_NL2
+#define KLT_T7_NL2 1  // the two-level instances (A/B hook: 0 launches the runtime-depth ones)
+#endif
 #ifndef KLT_T7_BATCH
 #define KLT_T7_BATCH 7  // 16-byte LDS reads in flight per ordered-sum batch (13 per row)
 #endif
@@ -383,7 +389,10 @@ __device__ int level7(const TrkArgs &a, const Lev &A, const Lev &B, float x1, fl
   return ls.it >= a.max_it ? kMaxIter : kTracked;
 }
 
-template <bool BAND, bool AOS>
+// NL > 0: the pyramid depth as a compile-time constant (the default 2), so
+// the level loops unroll and every level's fields are loop-invariant scalars;
+// NL == 0 reads a.nlev
+template <bool BAND, bool AOS, int NL>
 __global__ __launch_bounds__(kBlock) void k_track7(TrkArgs a, TrkFramesArgs b, float *__restrict__ fx,
                                                    float *__restrict__ fy, int *__restrict__ fv, int n) {
   __shared__ __attribute__((aligned(16))) float red_all[kWaves][kRows * kRow + 4];
@@ -408,7 +417,8 @@ __global__ __launch_bounds__(kBlock) void k_track7(TrkArgs a, TrkFramesArgs b, f
 
   float x = u(fx[f]), y = u(fy[f]);
   int v = u(fv[f]);
-  const bool merge = a.merge_res && a.nlev >= 2;
+  const int nlev = NL > 0 ? NL : a.nlev;
+  const bool merge = a.merge_res && nlev >= 2;
   Pending pd;
   Counts cnt;
 #ifdef KLT_TRACK_PROF
@@ -423,21 +433,23 @@ __global__ __launch_bounds__(kBlock) void k_track7(TrkArgs a, TrkFramesArgs b, f
       // one frame of KLTTrackFeatures for this feature (:1348-1437)
       const Lev R = j == 0 ? lev_of(a.A[0], 0) : lev_of(a.B[0], (long)(j - 1) * b.lfs[0]);
       float xl = x, yl = y;
-      for (int r = a.nlev - 1; r >= 0; --r) {  // xloc /= subsampling, nlev times (:1352-1355)
+#pragma unroll
+      for (int r = nlev - 1; r >= 0; --r) {  // xloc /= subsampling, nlev times (:1352-1355)
         xl = u(a.ss_inv != 0.0f ? xl * a.ss_inv : xl / a.ss);
         yl = u(a.ss_inv != 0.0f ? yl * a.ss_inv : yl / a.ss);
       }
       float xo = xl, yo = yl;
       int val = kTracked;
       bool lost_prev = false;
-      for (int r = a.nlev - 1; r >= 0; --r) {
+#pragma unroll
+      for (int r = nlev - 1; r >= 0; --r) {
         xl = u(xl * a.ss);
         yl = u(yl * a.ss);
         xo = u(xo * a.ss);
         yo = u(yo * a.ss);
         const Lev LA = j == 0 ? lev_of(a.A[r], 0) : lev_of(a.B[r], (long)(j - 1) * b.lfs[r]);
         const Lev LB = lev_of(a.B[r], (long)j * b.lfs[r]);
-        const bool lj = job && r == a.nlev - 1;
+        const bool lj = job && r == nlev - 1;
         T7_T(t_l0);
         val = level7<BAND, AOS>(a, LA, LB, xl, yl, xo, yo, lane, fi, fj, on, red, r == 0,
                            merge && r == 0 && j + 1 < b.nframes, pd, lj, R, rstat, lost_prev, cnt);
@@ -511,14 +523,20 @@ hipError_t launch_track7(hipStream_t st, bool band, const TrkArgs &a, const TrkF
   const int nb = (n + kWaves - 1) / kWaves;
   const int grid = b.xcd_per > 0 ? 8 * b.xcd_per : nb;
   // band: escape checks (klt_hip_track_frames_band); aos: interleaved levels
-  if (band && a.aos)
-    hipLaunchKernelGGL((k_track7<true, true>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
+  // (interleaved levels are the fused path's, always two levels deep)
+  const bool two = KLT_T7_NL2 && a.nlev == 2;
+  if (band && a.aos && two)
+    hipLaunchKernelGGL((k_track7<true, true, 2>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
+  else if (a.aos && two)
+    hipLaunchKernelGGL((k_track7<false, true, 2>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
+  else if (band && a.aos)
+    hipLaunchKernelGGL((k_track7<true, true, 0>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
   else if (band)
-    hipLaunchKernelGGL((k_track7<true, false>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
+    hipLaunchKernelGGL((k_track7<true, false, 0>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
   else if (a.aos)
-    hipLaunchKernelGGL((k_track7<false, true>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
+    hipLaunchKernelGGL((k_track7<false, true, 0>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
   else
-    hipLaunchKernelGGL((k_track7<false, false>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
+    hipLaunchKernelGGL((k_track7<false, false, 0>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
   return hipGetLastError();
 }
 
