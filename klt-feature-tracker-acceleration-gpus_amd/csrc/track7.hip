@@ -183,6 +183,18 @@ __device__ __forceinline__ Lev lev_of(const TrkLevel &L, long off) {
   return Lev{L.img + off, L.gx + off, L.gy + off, L.w, L.h, L.vlo, L.vhi};
 }
 
+// image 1 of frame j at level r: the previous pyramid (a.A) for the batch's
+// first frame, else bank frame j-1.  Selected field by field so that both
+// structs' fields stay loop-invariant scalars (a select of the struct's
+// address would load them through a pointer on every frame)
+__device__ __forceinline__ Lev lev_prev(const TrkArgs &a, const TrkFramesArgs &b, int r, int j) {
+  const TrkLevel &P = a.A[r], &Q = a.B[r];
+  const bool f = j == 0;
+  const long off = f ? 0L : (long)(j - 1) * b.lfs[r];
+  return Lev{(f ? P.img : Q.img) + off, (f ? P.gx : Q.gx) + off, (f ? P.gy : Q.gy) + off, f ? P.w : Q.w,
+             f ? P.h : Q.h, f ? P.vlo : Q.vlo, f ? P.vhi : Q.vhi};
+}
+
 // band-built pyramids (klt_hip_track_frames_band): every row the window's
 // bilinear samples touch must have been built
 __device__ __forceinline__ bool band_bad(const Lev &L, float y) {
@@ -431,7 +443,7 @@ __global__ __launch_bounds__(kBlock) void k_track7(TrkArgs a, TrkFramesArgs b, f
     int rstat = kTracked;
     if (v >= 0 || job) {
       // one frame of KLTTrackFeatures for this feature (:1348-1437)
-      const Lev R = j == 0 ? lev_of(a.A[0], 0) : lev_of(a.B[0], (long)(j - 1) * b.lfs[0]);
+      const Lev R = lev_prev(a, b, 0, j);
       float xl = x, yl = y;
 #pragma unroll
       for (int r = nlev - 1; r >= 0; --r) {  // xloc /= subsampling, nlev times (:1352-1355)
@@ -447,7 +459,7 @@ __global__ __launch_bounds__(kBlock) void k_track7(TrkArgs a, TrkFramesArgs b, f
         yl = u(yl * a.ss);
         xo = u(xo * a.ss);
         yo = u(yo * a.ss);
-        const Lev LA = j == 0 ? lev_of(a.A[r], 0) : lev_of(a.B[r], (long)(j - 1) * b.lfs[r]);
+        const Lev LA = lev_prev(a, b, r, j);
         const Lev LB = lev_of(a.B[r], (long)j * b.lfs[r]);
         const bool lj = job && r == nlev - 1;
         T7_T(t_l0);

@@ -118,3 +118,30 @@ def test_selection_images_no_presmoothing(gpu, oracle):
     dev.build(img, nlevels=1, smooth=0)
     a, gx, gy = oracle_for(oracle, dev.tc).select_images(img)
     assert_planes_equal(dev.levels(0, 1), [(a, gx, gy)], "no-presmooth")
+
+
+def test_level_layout_api(gpu):
+    """klt_hip_level_interleaved / klt_hip_level_ptr: fused levels are one
+    {img, gx, gy} record per pixel at the base (gx/gy queries return NULL),
+    generic levels are three planes; both de-interleave to the same planes."""
+    import ctypes as C
+    h, w = 67, 129
+    img = synth(gpu, 31, w, h, 1)[0]
+    dev = Dev(gpu)
+    dev.build(img, slot=0)
+    dev.build(img, slot=1, force_generic=True)
+    lib, ctx = gpu, dev.ctx
+    want = dev.levels(1, 2)
+    for lv in range(2):
+        assert lib.klt_hip_level_interleaved(ctx, 0, lv) == 1
+        assert lib.klt_hip_level_interleaved(ctx, 1, lv) == 0
+        base = lib.klt_hip_level_ptr(ctx, 0, lv, 0)
+        assert base and not lib.klt_hip_level_ptr(ctx, 0, lv, 1) and not lib.klt_hip_level_ptr(ctx, 0, lv, 2)
+        assert all(lib.klt_hip_level_ptr(ctx, 1, lv, k) for k in range(3))
+        lw, lh = want[lv][0].shape[1], want[lv][0].shape[0]
+        rec = np.empty((lh, lw, 3), np.float32)
+        check(lib, ctx, lib.klt_hip_sync(ctx), "sync")
+        check(lib, ctx, lib.klt_hip_memcpy(ctx, rec.ctypes.data, C.c_void_p(base), rec.nbytes, 2), "d2h")
+        for k in range(3):
+            assert np.array_equal(bits(rec[:, :, k]), bits(want[lv][k])), (lv, k)
+    assert lib.klt_hip_level_interleaved(ctx, 0, 5) == -1
