@@ -80,6 +80,9 @@ def parse():
     p.add_argument("--serial", action="store_true",
                    help="build and track on one stream; default: chunk c+1's pyramids are built on a second "
                         "stream while chunk c is tracked (they fill the CUs the tracker's last waves leave idle)")
+    p.add_argument("--min-chunks", type=int, default=2,
+                   help="the timed region holds at least this many chunks (the chunk is capped at "
+                        "ceil(steps / min-chunks)); 1 with --serial: one launch pair over the whole region")
     p.add_argument("--event-timing", choices=["timed", "replay"], default="replay",
                    help="record per-kernel HIP events inside the timed region or in a replay")
     a = p.parse_args()
@@ -90,7 +93,7 @@ def parse():
             setattr(a, k, shd if sharded else dflt)
     a.chunk_requested = a.chunk
     if a.chunk > 0 and a.steps > 0:
-        a.chunk = min(a.chunk, max(1, -(-a.steps // 2)))  # >= 2 chunks in the timed region
+        a.chunk = min(a.chunk, max(1, -(-a.steps // max(1, a.min_chunks))))  # >= min_chunks in the timed region
     return a
 
 

@@ -217,6 +217,7 @@ struct klt_hip_ctx {
   void *bank_arena = nullptr;
   size_t bank_arena_bytes = 0;
   size_t bank_budget = 0;  // bytes the bank arena may take (klt_hip_set_bank_budget; 0: the default)
+  size_t dev_total = 0;    // the device's memory (queried once, for the default budget)
   int chunk_used = 0;      // frames per bank of the last klt_hip_track_frames* call (budget-capped)
   int bank_next = 0;
   // band mode: a bank whose pyramids were built ahead, during the previous
@@ -550,27 +551,24 @@ constexpr int kOrderMin = 2048;
 // one-frame launches re-sort the processing order every this many calls
 constexpr int kOrderReuse = 8;
 
-// own != nullptr (band mode): only live features with own[0] <= y < own[1]
-int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc *d, const TrkArgs &a,
-                        const TrkFramesArgs &b, float *x, float *y, int *v, int n, const float *own = nullptr) {
-  TimedScope ts(c, T_TRACK, st, b.nframes);
-  const int npx = d->window_width * d->window_height;
-  const bool exact = d->reduction == KLT_HIP_EXACT, li = d->lighting_insensitive != 0;
-  const bool patch = c->track_patch && (d->window_width + 1) * (d->window_height + 1) <= kWave;
-  // the default 7x7 window gets compile-time window geometry (unrolled ordered sums)
-  const bool win7 = d->window_width == 7 && d->window_height == 7;
-  TrkFramesArgs bb = b;
+// The processing order of a tracker launch over n features (k_band_order on
+// st, reading y/v as they stand in st's order): bb.perm / xcd_per / n_dev.
+// own != nullptr (band mode): only live features with own[0] <= y < own[1].
+// The batched path queues it before the tracking stream waits for the chunk's
+// pyramids, so the sort runs while they are built.
+int order_features(klt_hip_ctx *c, hipStream_t st, int nrows, const float *y, const int *v, int n, int nframes,
+                   const float *own, TrkFramesArgs &bb) {
   if (own || (c->track_order == 0 && n >= kOrderMin)) {
     // one-frame launches (KLTTrackFeatures) reuse the order of a recent call
     // with the same feature count: any permutation gives the same results,
     // and features move little from one frame to the next
-    const bool reuse = !own && b.nframes == 1 && c->perm_n == n && c->perm_age < kOrderReuse;
+    const bool reuse = !own && nframes == 1 && c->perm_n == n && c->perm_age < kOrderReuse;
     if (reuse) {
       ++c->perm_age;
     } else {
       if (grow(c, &c->d_perm, &c->perm_cap, (size_t)n)) return -1;
       if (own && !c->d_count) HIPCHK(c, hipMalloc((void **)&c->d_count, sizeof(int)));
-      if (launched(c, "k_band_order", launch_band_order(st, y, v, n, a.nrows, c->d_perm, own ? own[0] : 0.0f,
+      if (launched(c, "k_band_order", launch_band_order(st, y, v, n, nrows, c->d_perm, own ? own[0] : 0.0f,
                                                         own ? own[1] : 0.0f, own ? c->d_count : (int *)nullptr)))
         return -1;
       c->perm_n = own ? -1 : n;  // a band's order lists only the band's features
@@ -581,6 +579,21 @@ int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc
     bb.perm = c->d_perm;
     bb.xcd_per = (nb + 7) / 8;
   }
+  return 0;
+}
+
+// ordered: the caller ran order_features into b already
+int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc *d, const TrkArgs &a,
+                        const TrkFramesArgs &b, float *x, float *y, int *v, int n, const float *own = nullptr,
+                        bool ordered = false) {
+  TimedScope ts(c, T_TRACK, st, b.nframes);
+  const int npx = d->window_width * d->window_height;
+  const bool exact = d->reduction == KLT_HIP_EXACT, li = d->lighting_insensitive != 0;
+  const bool patch = c->track_patch && (d->window_width + 1) * (d->window_height + 1) <= kWave;
+  // the default 7x7 window gets compile-time window geometry (unrolled ordered sums)
+  const bool win7 = d->window_width == 7 && d->window_height == 7;
+  TrkFramesArgs bb = b;
+  if (!ordered && order_features(c, st, a.nrows, y, v, n, b.nframes, own, bb)) return -1;
   bb.prof = c->prof;
   bb.count = c->d_trk_count;
   const TrkFramesArgs &b2 = bb;
@@ -678,9 +691,11 @@ void free_banks(klt_hip_ctx *c) {
 // three 64-frame banks of 4K pyramids take 21 GB, of 1080p 5.3 GB.
 size_t bank_budget_of(klt_hip_ctx *c) {
   if (c->bank_budget) return c->bank_budget;
-  size_t fr = 0, tot = 0;
-  if (hipMemGetInfo(&fr, &tot) != hipSuccess || tot == 0) tot = (size_t)64 << 30;
-  const size_t q = tot / 4, cap = (size_t)64 << 30;
+  if (!c->dev_total) {
+    size_t fr = 0, tot = 0;
+    c->dev_total = hipMemGetInfo(&fr, &tot) == hipSuccess && tot ? tot : (size_t)64 << 30;
+  }
+  const size_t q = c->dev_total / 4, cap = (size_t)64 << 30;
   return q < cap ? q : cap;
 }
 
@@ -1768,6 +1783,12 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     // overlapped: the pyramid stream builds chunk c+1 while chunk c is tracked;
     // serial: both on the tracking stream (no two kernels share the CUs)
     hipStream_t ps = serial ? c->stream : c->pstream;
+    // the processing order reads the positions this chunk starts from: queued
+    // on the tracking stream ahead of its wait for the chunk's pyramids (and,
+    // serial, ahead of the build), so the sort is off the chain
+    TrkFramesArgs b;
+    memset(&b, 0, sizeof b);
+    if (n > 0 && order_features(c, c->stream, pd->nrows, y, val, n, Fc, band ? band->own : nullptr, b)) return -1;
     const bool prebuilt = band && c->pre.bank == bi && c->pre.src == src && c->pre.F == Fc &&
                           c->pre.stride == stride && c->pre.row_lo == band->row_lo && c->pre.row_hi == band->row_hi;
     if (c->pre.bank == bi) c->pre.bank = -1;  // taken now, or about to be overwritten
@@ -1792,8 +1813,6 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
       if (!prebuilt) HIPCHK(c, hipEventRecord(c->ev_bbuilt[bi], ps));
       HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_bbuilt[bi], 0));
     }
-    TrkFramesArgs b;
-    memset(&b, 0, sizeof b);
     for (int l = 0; l < pd->nlevels; ++l) {
       a.A[l] = prev_level(c, l);
       a.B[l] = level_view(K.lv[l], 0, fz ? K.vlo[l] : 0, fz ? K.vhi[l] : (1 << 30));
@@ -1806,7 +1825,7 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
       b.tv = tab_val + (long)j0 * tab_stride;
       b.tstride = tab_stride;
     }
-    if (n > 0 && track_frames_launch(c, c->stream, td, a, b, x, y, val, n, band ? band->own : nullptr))
+    if (n > 0 && track_frames_launch(c, c->stream, td, a, b, x, y, val, n, band ? band->own : nullptr, true))
       return -1;
     if (!serial && c->prev.bank >= 0) HIPCHK(c, hipEventRecord(c->ev_bfree[c->prev.bank], c->stream));
     c->prev = PrevRef{bi, Fc - 1};
