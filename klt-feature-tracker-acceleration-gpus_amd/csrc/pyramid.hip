@@ -34,6 +34,12 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f4 ld4(const float *p) { return *reinterpret_cast<const f4 *>(p); }
+// hs_at (klt_dev.h) in 32-bit arithmetic: one frame's hs stays far below 2^32
+// floats, and X >= 0 here, so X / 16 and X % 16 are a shift and a mask
+static_assert(kHsSlab == 16, "hs slab width");
+__device__ __forceinline__ unsigned hs_at32(int y, int X, int H) {
+  return ((unsigned)(X >> 4) * (unsigned)H + (unsigned)y) * 16u + (unsigned)(X & 15);
+}
 __device__ __forceinline__ void st4(float *p, f4 v) { *reinterpret_cast<f4 *>(p) = v; }
 // level-0 HBM stores are nontemporal (measured 1-2 % faster than plain stores)
 __device__ __forceinline__ void st4_out(float *p, f4 v) { __builtin_nontemporal_store(v, reinterpret_cast<f4 *>(p)); }
@@ -320,13 +326,13 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     const int y = R0 + r;
     const int X = C0 / SS + 4 * q;
     if (INT) {
-      *reinterpret_cast<f4 *>(hs + hs_at(y, X, H)) = f4{a01.x, a01.y, a23.x, a23.y};
+      *reinterpret_cast<f4 *>(hs + hs_at32(y, X, H)) = f4{a01.x, a01.y, a23.x, a23.y};
     } else if (y < H) {
       const float o[4] = {a01.x, a01.y, a23.x, a23.y};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int c = C0 + 16 * q + 4 * e + 2;
-        if (X + e < hsW) hs[hs_at(y, X + e, H)] = (c >= RP && c < W - RP) ? o[e] : 0.0f;
+        if (X + e < hsW) hs[hs_at32(y, X + e, H)] = (c >= RP && c < W - RP) ? o[e] : 0.0f;
       }
     }
   }
@@ -493,10 +499,10 @@ __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs,
         const int row = clampi(SS * y0 - 20 + r, 0, H - 1);
         const int X = x0 - 4 + 4 * q;
         if (vec) {  // a 4-aligned group never straddles a slab
-          v[k] = ld4(hs + hs_at(row, clampi(X, 0, W1 - 4), H));
+          v[k] = ld4(hs + hs_at32(row, clampi(X, 0, W1 - 4), H));
         } else {
-          v[k] = f4{hs[hs_at(row, clampi(X, 0, W1 - 1), H)], hs[hs_at(row, clampi(X + 1, 0, W1 - 1), H)],
-                    hs[hs_at(row, clampi(X + 2, 0, W1 - 1), H)], hs[hs_at(row, clampi(X + 3, 0, W1 - 1), H)]};
+          v[k] = f4{hs[hs_at32(row, clampi(X, 0, W1 - 1), H)], hs[hs_at32(row, clampi(X + 1, 0, W1 - 1), H)],
+                    hs[hs_at32(row, clampi(X + 2, 0, W1 - 1), H)], hs[hs_at32(row, clampi(X + 3, 0, W1 - 1), H)]};
         }
       }
     }
@@ -532,7 +538,7 @@ __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs,
     const int Y = y0 + r, X = x0 + 4 * g;
     if (Y >= H1 || X >= W1) continue;
     const f4 v = ld4(im + (r + RG) * JW + 4 + 4 * g);
-    float *dst = img1 + (long)Y * W1 + X;
+    float *dst = img1 + (unsigned)(Y * W1 + X);
     if (vec && X + 3 < W1) st4(dst, v);
     else
       for (int e = 0; e < 4 && X + e < W1; ++e) dst[e] = v[e];
@@ -589,8 +595,8 @@ __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs,
       st4(o + 8, f4{ay.z, iv.w, ax.w, ay.w});
       continue;
     }
-    float *px = gx1 + (long)Y * W1 + X;
-    float *py = gy1 + (long)Y * W1 + X;
+    float *px = gx1 + (unsigned)(Y * W1 + X);
+    float *py = gy1 + (unsigned)(Y * W1 + X);
     if (vec && X + 3 < W1) {
       st4(px, ax);
       st4(py, ay);
@@ -604,16 +610,16 @@ __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs,
   if (IL) {
     __syncthreads();
     const int nx = min(TW, W1 - x0);  // valid pixels of each tile row
-    float *base = img1 + 3 * (long)x0;
+    float *base = img1 + 3u * (unsigned)x0;
     if (vec && nx == TW) {
       for (int i = tid; i < TH * (3 * TW / 4); i += NT) {
         const int r = i / (3 * TW / 4), q = i - r * (3 * TW / 4);
-        if (y0 + r < H1) st4(base + 3 * (long)(y0 + r) * W1 + 4 * q, ld4(stg + r * (3 * TW) + 4 * q));
+        if (y0 + r < H1) st4(base + 3u * (unsigned)((y0 + r) * W1) + 4 * q, ld4(stg + r * (3 * TW) + 4 * q));
       }
     } else {
       for (int i = tid; i < TH * 3 * TW; i += NT) {
         const int r = i / (3 * TW), q = i - r * (3 * TW);
-        if (y0 + r < H1 && q < 3 * nx) base[3 * (long)(y0 + r) * W1 + q] = stg[r * (3 * TW) + q];
+        if (y0 + r < H1 && q < 3 * nx) base[3u * (unsigned)((y0 + r) * W1) + q] = stg[r * (3 * TW) + q];
       }
     }
   }
