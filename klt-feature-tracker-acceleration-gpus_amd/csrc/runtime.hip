@@ -223,7 +223,7 @@ struct klt_hip_ctx {
   // band mode: a bank whose pyramids were built ahead, during the previous
   // call's tracking (klt_hip_track_frames_band's next_frames); -1: none
   struct {
-    int bank = -1, F = 0, row_lo = 0, row_hi = 0;
+    int bank = -1, F = 0, row_lo = 0, row_hi = 0, il = 1;
     const unsigned char *src = nullptr;
     long stride = 0;
   } pre;
@@ -551,6 +551,20 @@ constexpr int kOrderMin = 2048;
 // one-frame launches re-sort the processing order every this many calls
 constexpr int kOrderReuse = 8;
 
+// the default configuration's latency-lean tracker (track7.hip) serves this
+// launch: 7x7 window, exact sums, no gain/bias, the lane-patch path on, and
+// the generic kernel not forced (klt_hip_set_track_impl, A/B only)
+bool t7_tracks(const klt_hip_ctx *c, const klt_hip_track_desc *d) {
+#ifdef KLT_TRACK_PROF
+  const bool prof_ok = true;  // the instrumented build instruments both kernels
+#else
+  const bool prof_ok = !c->prof;
+#endif
+  const bool exact = d->reduction == KLT_HIP_EXACT, li = d->lighting_insensitive != 0;
+  const bool win7 = d->window_width == 7 && d->window_height == 7;
+  return c->track_impl == 0 && win7 && exact && !li && c->track_patch && prof_ok;
+}
+
 // The processing order of a tracker launch over n features (k_band_order on
 // st, reading y/v as they stand in st's order): bb.perm / xcd_per / n_dev.
 // own != nullptr (band mode): only live features with own[0] <= y < own[1].
@@ -601,14 +615,7 @@ int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc
   aa.merge_res = c->track_merge;
   aa.prio = c->track_prio;
   aa.aos = 0;
-  // the default configuration: the latency-lean kernel (track7.hip) unless
-  // the context asks for the generic one (klt_hip_set_track_impl, A/B only)
-#ifdef KLT_TRACK_PROF
-  const bool prof_ok = true;  // the instrumented build instruments both kernels
-#else
-  const bool prof_ok = !c->prof;
-#endif
-  const bool t7 = c->track_impl == 0 && win7 && exact && !li && c->track_patch && prof_ok;
+  const bool t7 = t7_tracks(c, d);
   // k_track7 reads interleaved levels as built; other kernels (or a mix of
   // layouts) get planes of the interleaved ones
   const bool ilA = a.A[0].il != 0, ilB = a.B[0].il != 0;
@@ -781,7 +788,7 @@ int ensure_banks(klt_hip_ctx *c, const klt_hip_pyr_desc *d, int frames) {
 // (a band's outer margin feeds only level 1)
 int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
                      long stride, int F, hipStream_t st, int row_lo = 0, int row_hi = 1 << 30, int plane_lo = 0,
-                     int plane_hi = 1 << 30) {
+                     int plane_hi = 1 << 30, int il = 1) {
   const int W = d->ncols, H = d->nrows;
   const DefTaps T = default_taps(d);
   const bool two = d->nlevels == 2;
@@ -793,11 +800,14 @@ int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const u
   const long fs0 = (long)W * H, fsh = hs_size(W1, H), fs1 = (long)W1 * H1;
   int r0 = clampi(row_lo, 0, H), r1 = row_hi >= H ? H : clampi(row_hi, r0, H);
   int p0 = clampi(plane_lo, 0, H), p1 = plane_hi >= H ? H : clampi(plane_hi, p0, H);
-  for (int l = 0; l < d->nlevels; ++l) K.lv[l].il = 1;  // interleaved (frame f at img + 3 f w h)
+  // il: interleaved (frame f at img + 3 f w h); else planes (frame f at
+  // img / gx / gy + f w h), for a batch that a planes-reading tracker takes
+  const int np = il ? 3 : 1;
+  for (int l = 0; l < d->nlevels; ++l) K.lv[l].il = il;
   {
     TimedScope ts(c, T_L0, st, F);
     if (launch_l0(c, st, src, pitch, stride, W, H, T, vec_u8, vec_out, K.lv[0].img, K.lv[0].gx, K.lv[0].gy, K.hs,
-                  W1, (two && W1 > 0) ? 1 : 0, 3 * fs0, fsh, F, r0, r1, &p0, &p1, 1))
+                  W1, (two && W1 > 0) ? 1 : 0, np * fs0, fsh, F, r0, r1, &p0, &p1, il))
       return -1;
   }
   K.vlo[0] = p0;
@@ -819,7 +829,7 @@ int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const u
       TimedScope ts(c, T_L1, st, F);
       const int vec = (W1 % 4 == 0 && W1 >= 8) ? 1 : 0;
       if (launched(c, "k_pyr_l1", launch_pyr_l1(st, K.hs, W1, H, H1, T, vec, K.lv[1].img, K.lv[1].gx, K.lv[1].gy,
-                                                fsh, 3 * fs1, F, t1lo, t1hi, 1)))
+                                                fsh, np * fs1, F, t1lo, t1hi, il)))
         return -1;
     }
   }
@@ -1771,6 +1781,9 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
   }
   const bool fz = fused_ok(pd) && !c->force_generic;
   if (band && !fz) return fail(c, "track_frames_band: needs the fused (default-parameter) pyramid path");
+  // the banks' layout follows their reader: interleaved for k_track7, planes
+  // for the generic tracker (no per-chunk conversion)
+  const int bil = t7_tracks(c, td) ? 1 : 0;
   TrkArgs a;
   fill_trk_args(td, pd->nlevels, pd->nlevels > 1 ? pd->subsampling : 1, pd->ncols, pd->nrows, a);
   if (band) a.escape = band->escape;
@@ -1790,7 +1803,8 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     memset(&b, 0, sizeof b);
     if (n > 0 && order_features(c, c->stream, pd->nrows, y, val, n, Fc, band ? band->own : nullptr, b)) return -1;
     const bool prebuilt = band && c->pre.bank == bi && c->pre.src == src && c->pre.F == Fc &&
-                          c->pre.stride == stride && c->pre.row_lo == band->row_lo && c->pre.row_hi == band->row_hi;
+                          c->pre.stride == stride && c->pre.row_lo == band->row_lo && c->pre.row_hi == band->row_hi &&
+                          c->pre.il == bil;
     if (c->pre.bank == bi) c->pre.bank = -1;  // taken now, or about to be overwritten
     // one stream: stream order is the dependency (an event wait would add a queue barrier)
     if (!serial && !prebuilt) HIPCHK(c, hipStreamWaitEvent(ps, c->ev_bfree[bi], 0));
@@ -1799,8 +1813,8 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     } else if (fz) {
       int p0 = 0, p1 = 1 << 30;
       if (band) band_planes(*band, p0, p1);
-      if (band ? build_fused_bank(c, K, pd, src, pitch, stride, Fc, ps, band->row_lo, band->row_hi, p0, p1)
-               : build_fused_bank(c, K, pd, src, pitch, stride, Fc, ps))
+      if (band ? build_fused_bank(c, K, pd, src, pitch, stride, Fc, ps, band->row_lo, band->row_hi, p0, p1, bil)
+               : build_fused_bank(c, K, pd, src, pitch, stride, Fc, ps, 0, 1 << 30, 0, 1 << 30, bil))
         return -1;
     } else {
       for (int f = 0; f < Fc; ++f) {
@@ -1839,7 +1853,7 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     int p0 = 0, p1 = 1 << 30;
     band_planes(*band, p0, p1);
     if (build_fused_bank(c, c->bank[bj], pd, band->next, pitch, stride, Fn, c->pstream, band->row_lo, band->row_hi,
-                         p0, p1))
+                         p0, p1, bil))
       return -1;
     HIPCHK(c, hipEventRecord(c->ev_bbuilt[bj], c->pstream));
     c->pre.bank = bj;
@@ -1848,6 +1862,7 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     c->pre.stride = stride;
     c->pre.row_lo = band->row_lo;
     c->pre.row_hi = band->row_hi;
+    c->pre.il = bil;
   }
   return 0;
 }
