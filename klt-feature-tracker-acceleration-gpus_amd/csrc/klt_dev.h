@@ -105,6 +105,7 @@ struct TrkArgs {
   int *escape;       // band mode: set when a window needs rows outside [vlo, vhi)
   int prio;          // 1: tracker waves raise their issue priority (s_setprio 3) over concurrent pyramid waves
   int aos;           // 1 (k_track7): a level's img is {img, gx, gy} interleaved per pixel (gx/gy unused)
+  int fast;          // 1 (k_track7): KLT_HIP_FAST window sums (DPP tree), interleaved two-level pyramids only
 };
 
 // batched frames: frame j tracks pyramid j-1 -> j of a bank; row j of the

@@ -560,9 +560,9 @@ bool t7_tracks(const klt_hip_ctx *c, const klt_hip_track_desc *d) {
 #else
   const bool prof_ok = !c->prof;
 #endif
-  const bool exact = d->reduction == KLT_HIP_EXACT, li = d->lighting_insensitive != 0;
+  const bool li = d->lighting_insensitive != 0;
   const bool win7 = d->window_width == 7 && d->window_height == 7;
-  return c->track_impl == 0 && win7 && exact && !li && c->track_patch && prof_ok;
+  return c->track_impl == 0 && win7 && !li && c->track_patch && prof_ok;  // exact or fast sums
 }
 
 // The processing order of a tracker launch over n features (k_band_order on
@@ -615,12 +615,16 @@ int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc
   aa.merge_res = c->track_merge;
   aa.prio = c->track_prio;
   aa.aos = 0;
-  const bool t7 = t7_tracks(c, d);
+  aa.fast = 0;
   // k_track7 reads interleaved levels as built; other kernels (or a mix of
-  // layouts) get planes of the interleaved ones
+  // layouts) get planes of the interleaved ones.  Its fast-sum instance
+  // covers interleaved two-level pyramids; other fast cases take the generic
+  // kernel's tree sums
   const bool ilA = a.A[0].il != 0, ilB = a.B[0].il != 0;
+  const bool t7 = t7_tracks(c, d) && (exact || (ilA && ilB && a.nlev == 2));
   if (t7 && ilA && ilB) {
     aa.aos = 1;
+    aa.fast = exact ? 0 : 1;
   } else if (ilA || ilB) {
     for (int l = 0; l < a.nlev; ++l) {
       for (int k = 0; k < 2; ++k) {

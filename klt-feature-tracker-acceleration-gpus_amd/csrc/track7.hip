@@ -174,6 +174,43 @@ __device__ __forceinline__ void sums7(float *red, int lane, bool on, const float
   wave_lds_sync();  // the rows are rewritten by the next pass
 }
 
+// KLT_HIP_FAST (not bit-exact; the tolerance is tests/test_gpu_long.py's):
+// the NS sums by DPP within the VALU -- two quad butterflies and two row
+// rotations leave every lane of a 16-lane row its row's sum, then the four
+// row sums are read out and added -- no LDS round trip and no 49-add chain
+constexpr int kQuadXor1 = 0xB1, kQuadXor2 = 0x4E, kRowRor4 = 0x124, kRowRor8 = 0x128;  // DPP controls
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float x) {
+  return x + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+
+template <int NS>
+__device__ __forceinline__ void tree7(bool on, const float (&v)[NS], float (&out)[NS]) {
+  float x[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) x[s] = on ? v[s] : 0.0f;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) x[s] = dpp_add<kQuadXor1>(x[s]);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) x[s] = dpp_add<kQuadXor2>(x[s]);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) x[s] = dpp_add<kRowRor4>(x[s]);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) x[s] = dpp_add<kRowRor8>(x[s]);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int b = __float_as_int(x[s]);
+    out[s] = (__int_as_float(__builtin_amdgcn_readlane(b, 0)) + __int_as_float(__builtin_amdgcn_readlane(b, 16))) +
+             (__int_as_float(__builtin_amdgcn_readlane(b, 32)) + __int_as_float(__builtin_amdgcn_readlane(b, 48)));
+  }
+}
+
+template <int NS, bool FAST>
+__device__ __forceinline__ void sums(float *red, int lane, bool on, const float (&v)[NS], float (&out)[NS]) {
+  if constexpr (FAST) tree7<NS>(on, v, out);
+  else sums7<NS>(red, lane, on, v, out);
+}
+
 struct Lev {
   const float *img, *gx, *gy;
   int w, h, vlo, vhi;
@@ -239,7 +276,7 @@ enum { kPassAgain = 0, kPassDone = 1, kPassOOB = 2, kPassLostPrev = 3 };
 // level's FIRST pass; the deferred residue's img2 plane with a JOB), the
 // ordered sums, the solve.  Separate instances for the first pass and the
 // rest keep the first pass's addresses out of the loop.
-template <bool BAND, bool FIRST, bool JOB, bool AOS>
+template <bool BAND, bool FIRST, bool JOB, bool AOS, bool FAST>
 __device__ __forceinline__ int pass7(const TrkArgs &a, const Lev &A, const Lev &B, float x1, float y1, bool x1_out,
                                      LevState &ls, int lane, float fi, float fj, bool on, float *red, Pending &pd,
                                      const Lev &R, int &rstat, Counts &cnt) {
@@ -257,7 +294,7 @@ __device__ __forceinline__ int pass7(const TrkArgs &a, const Lev &A, const Lev &
       const float rb = interp(q, AOS ? quad_i(R.img, q, (unsigned)R.w * 12u) : quad(R.img, q, (unsigned)R.w * 4u));
       float v[1] = {on ? fabsf(pd.aim - rb) : 0.0f}, S[1];
       ++cnt.passes;
-      sums7<1>(red, lane, on, v, S);
+      sums<1, FAST>(red, lane, on, v, S);
       rstat = S[0] / (float)kNpx > a.max_res ? kLargeResidue : (pd.it >= a.max_it ? kMaxIter : kTracked);
       pd.on = false;
       if (rstat != kTracked) return kPassLostPrev;
@@ -317,14 +354,14 @@ __device__ __forceinline__ int pass7(const TrkArgs &a, const Lev &A, const Lev &
   if (JOB) {
     const float rb = interp(qr, ri);
     float v[6] = {gxs * gxs, gxs * gys, gys * gys, dif * gxs, dif * gys, fabsf(pd.aim - rb)};
-    sums7<6>(red, lane, on, v, S);
+    sums<6, FAST>(red, lane, on, v, S);
     rstat = S[5] / (float)kNpx > a.max_res ? kLargeResidue : (pd.it >= a.max_it ? kMaxIter : kTracked);
     pd.on = false;
     if (rstat != kTracked) return kPassLostPrev;  // that frame's feature is lost: this frame does not happen
   } else {
     float v[5] = {gxs * gxs, gxs * gys, gys * gys, dif * gxs, dif * gys};
     float S5[5];
-    sums7<5>(red, lane, on, v, S5);
+    sums<5, FAST>(red, lane, on, v, S5);
 #pragma unroll
     for (int k = 0; k < 5; ++k) S[k] = S5[k];
   }
@@ -354,7 +391,7 @@ __device__ __forceinline__ int pass7(const TrkArgs &a, const Lev &A, const Lev &
 // feature the level stops at once and lost_prev is set).  defer: this
 // (finest) level hands its own residue on (pd) instead of taking a pass for
 // it.  residue: the finest level.
-template <bool BAND, bool AOS>
+template <bool BAND, bool AOS, bool FAST>
 __device__ int level7(const TrkArgs &a, const Lev &A, const Lev &B, float x1, float y1, float &x2, float &y2,
                       int lane, float fi, float fj, bool on, float *red, bool residue, bool defer, Pending &pd,
                       bool job, const Lev &R, int &rstat, bool &lost_prev, Counts &cnt) {
@@ -363,10 +400,11 @@ __device__ int level7(const TrkArgs &a, const Lev &A, const Lev &B, float x1, fl
   LevState ls;
   ls.x2 = x2;
   ls.y2 = y2;
-  int r = job ? pass7<BAND, true, true, AOS>(a, A, B, x1, y1, x1_out, ls, lane, fi, fj, on, red, pd, R, rstat, cnt)
-              : pass7<BAND, true, false, AOS>(a, A, B, x1, y1, x1_out, ls, lane, fi, fj, on, red, pd, R, rstat, cnt);
+  int r = job ? pass7<BAND, true, true, AOS, FAST>(a, A, B, x1, y1, x1_out, ls, lane, fi, fj, on, red, pd, R, rstat, cnt)
+              : pass7<BAND, true, false, AOS, FAST>(a, A, B, x1, y1, x1_out, ls, lane, fi, fj, on, red, pd, R, rstat,
+                                                    cnt);
   while (r == kPassAgain)
-    r = pass7<BAND, false, false, AOS>(a, A, B, x1, y1, x1_out, ls, lane, fi, fj, on, red, pd, R, rstat, cnt);
+    r = pass7<BAND, false, false, AOS, FAST>(a, A, B, x1, y1, x1_out, ls, lane, fi, fj, on, red, pd, R, rstat, cnt);
   x2 = ls.x2;
   y2 = ls.y2;
   if (r == kPassLostPrev) {
@@ -395,7 +433,7 @@ __device__ int level7(const TrkArgs &a, const Lev &A, const Lev &B, float x1, fl
   const Pix q = pix_at(B.w, B.h, x2 + fi, y2 + fj);
   const float rb = interp(q, AOS ? quad_i(B.img, q, (unsigned)B.w * 12u) : quad(B.img, q, (unsigned)B.w * 4u));
   float v[1] = {on ? fabsf(ls.aim - rb) : 0.0f}, S1[1];
-  sums7<1>(red, lane, on, v, S1);
+  sums<1, FAST>(red, lane, on, v, S1);
   T7_ADD(3, t_r0);
   if (S1[0] / (float)kNpx > a.max_res) return kLargeResidue;
   return ls.it >= a.max_it ? kMaxIter : kTracked;
@@ -404,7 +442,7 @@ __device__ int level7(const TrkArgs &a, const Lev &A, const Lev &B, float x1, fl
 // NL > 0: the pyramid depth as a compile-time constant (the default 2), so
 // the level loops unroll and every level's fields are loop-invariant scalars;
 // NL == 0 reads a.nlev
-template <bool BAND, bool AOS, int NL>
+template <bool BAND, bool AOS, int NL, bool FAST = false>
 __global__ __launch_bounds__(kBlock) void k_track7(TrkArgs a, TrkFramesArgs b, float *__restrict__ fx,
                                                    float *__restrict__ fy, int *__restrict__ fv, int n) {
   __shared__ __attribute__((aligned(16))) float red_all[kWaves][kRows * kRow + 4];
@@ -463,7 +501,7 @@ __global__ __launch_bounds__(kBlock) void k_track7(TrkArgs a, TrkFramesArgs b, f
         const Lev LB = lev_of(a.B[r], (long)j * b.lfs[r]);
         const bool lj = job && r == nlev - 1;
         T7_T(t_l0);
-        val = level7<BAND, AOS>(a, LA, LB, xl, yl, xo, yo, lane, fi, fj, on, red, r == 0,
+        val = level7<BAND, AOS, FAST>(a, LA, LB, xl, yl, xo, yo, lane, fi, fj, on, red, r == 0,
                            merge && r == 0 && j + 1 < b.nframes, pd, lj, R, rstat, lost_prev, cnt);
         T7_ADD(10, t_l0);
         if (lost_prev) break;
@@ -537,7 +575,12 @@ hipError_t launch_track7(hipStream_t st, bool band, const TrkArgs &a, const TrkF
   // band: escape checks (klt_hip_track_frames_band); aos: interleaved levels
   // (interleaved levels are the fused path's, always two levels deep)
   const bool two = KLT_T7_NL2 && a.nlev == 2;
-  if (band && a.aos && two)
+  if (a.fast) {  // KLT_HIP_FAST: the runtime sends only interleaved two-level pyramids here
+    if (band)
+      hipLaunchKernelGGL((k_track7<true, true, 2, true>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
+    else
+      hipLaunchKernelGGL((k_track7<false, true, 2, true>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
+  } else if (band && a.aos && two)
     hipLaunchKernelGGL((k_track7<true, true, 2>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
   else if (a.aos && two)
     hipLaunchKernelGGL((k_track7<false, true, 2>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);
