@@ -1,0 +1,21 @@
+#!/bin/bash
+# HEAD validation + chunk-length probe of the config-4 rank simulation.
+# usage (via gpurun): bash tools/exp/r03f.sh
+set -o pipefail
+OUT=gpurun_out/r03f; mkdir -p $OUT
+export TMPDIR=/tmp
+bash tools/r03_cycle.sh r03f tests prof || exit 1
+for c in "--chunk 64 --margins 64" "--chunk 128 --margins 96"; do
+  timeout -k 10 400 python tools/shard_sim.py --worlds 1 8 --frames 257 $c --lazy-flag > $OUT/s.log 2>&1 || { tail -5 $OUT/s.log; exit 1; }
+  python3 - $OUT/s.log "$c" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith('{"workload')][0])
+out = []
+for r in d["runs"]:
+    q = max(r["per_rank_us_per_frame"], key=lambda q: q["wall"])
+    k = q["replay_kernels"]
+    out.append("w%d max %.2f (l0 %.2f l1 %.2f trk %.2f) x%.2f redo %d digest %d" % (r["world"], q["wall"], k["k_pyr_l0"],
+               k["k_pyr_l1"], k["k_track"], r["projected_speedup"] or 1, r["chunks_redone_full_frame"], r["state_digest"]))
+print(sys.argv[2], " | ".join(out))
+PY
+done
