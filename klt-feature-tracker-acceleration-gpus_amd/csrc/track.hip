@@ -849,8 +849,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KLT_TRAC
 // k_band_order: processing order for the tracker -- live features bucketed by
 // image row band (counting sort, one workgroup), lost features last.  Only
 // the order of work changes; every feature's result is independent of it.
+// It sits between two tracker launches on the tracking stream, so it is
+// shaped for latency: kPer features per thread loaded before any is used, the
+// buckets kept in LDS for the second pass, features outside a rank's band
+// skipped (no atomics), the lost bucket's atomics aggregated per wave, a
+// one-wave scan of the bucket counts.
 // ---------------------------------------------------------------------------
-constexpr int kBands = 128, kSortThreads = 1024;
+constexpr int kBands = 128, kSortThreads = 1024, kPer = 4, kBucketCache = 32768;
+
+// one LDS atomic per wave for the lanes in `mine` (all with the same bucket):
+// returns this lane's slot
+__device__ __forceinline__ int wave_claim(int *ctr, unsigned long long mine) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int leader = __ffsll((long long)mine) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(ctr, __popcll(mine));
+  base = __shfl(base, leader, kWave);
+  return base + __popcll(mine & ((1ull << lane) - 1ull));
+}
 
 __global__ __launch_bounds__(kSortThreads) void k_band_order(const float *__restrict__ fy,
                                                              const int *__restrict__ fv, int n, int nrows,
@@ -859,31 +875,79 @@ __global__ __launch_bounds__(kSortThreads) void k_band_order(const float *__rest
   // count != nullptr: keep only live features with own_lo <= y < own_hi (a
   // rank's band in sharded mode), *count = how many; else every feature
   __shared__ int cnt[kBands + 2];
+  __shared__ unsigned char bk[kBucketCache];
   const int t = threadIdx.x;
   for (int i = t; i <= kBands + 1; i += kSortThreads) cnt[i] = 0;
   __syncthreads();
   const float scale = (float)kBands / (float)(nrows > 0 ? nrows : 1);
-  auto band_of = [&](int i) {
-    if (count && !(fv[i] >= 0 && fy[i] >= own_lo && fy[i] < own_hi)) return kBands + 1;
-    if (fv[i] < 0) return kBands;
-    const float b = fy[i] * scale;
+  auto band_of = [&](float y, int v) {
+    if (count && !(v >= 0 && y >= own_lo && y < own_hi)) return kBands + 1;
+    if (v < 0) return kBands;
+    const float b = y * scale;
     return b >= 0.0f ? (b < (float)kBands ? (int)b : kBands - 1) : 0;  // NaN -> band 0
   };
-  for (int i = t; i < n; i += kSortThreads) atomicAdd(&cnt[band_of(i)], 1);
+  constexpr int kStep = kSortThreads * kPer;
+  // pass 1: bucket counts (the loop bound is uniform, so every lane reaches the ballots)
+  for (int i0 = 0; i0 < n; i0 += kStep) {
+    float y[kPer];
+    int v[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int i = i0 + k * kSortThreads + t;
+      y[k] = i < n ? fy[i] : 0.0f;
+      v[k] = i < n ? fv[i] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int i = i0 + k * kSortThreads + t;
+      const int b = i < n ? band_of(y[k], v[k]) : kBands + 1;
+      if (i < kBucketCache) bk[i] = (unsigned char)b;
+      const unsigned long long lost = __ballot(b == kBands);
+      if (b == kBands) wave_claim(&cnt[kBands], lost);
+      else if (b < kBands) atomicAdd(&cnt[b], 1);
+    }
+  }
   __syncthreads();
-  if (t == 0) {
-    int run = 0;
-    for (int i = 0; i <= kBands + 1; ++i) {
-      const int c = cnt[i];
-      cnt[i] = run;
-      run += c;
+  if (t < kWave) {  // exclusive scan of the kBands + 2 counts by one wave, 3 per lane
+    constexpr int kPerLane = (kBands + 2 + kWave - 1) / kWave;
+    int c[kPerLane], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPerLane; ++k) {
+      const int j = t * kPerLane + k;
+      c[k] = j <= kBands + 1 ? cnt[j] : 0;
+      sum += c[k];
+    }
+    int inc = sum;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const int o = __shfl_up(inc, d, kWave);
+      if (t >= d) inc += o;
+    }
+    int run = inc - sum;
+#pragma unroll
+    for (int k = 0; k < kPerLane; ++k) {
+      const int j = t * kPerLane + k;
+      if (j <= kBands + 1) cnt[j] = run;
+      run += c[k];
     }
   }
   __syncthreads();
   if (count && t == 0) *count = cnt[kBands + 1];  // start of the excluded bucket = kept features
-  for (int i = t; i < n; i += kSortThreads) {
-    const int bnd = band_of(i);
-    if (bnd <= kBands) perm[atomicAdd(&cnt[bnd], 1)] = i;
+  // pass 2: scatter
+  for (int i0 = 0; i0 < n; i0 += kStep) {
+    int b[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int i = i0 + k * kSortThreads + t;
+      b[k] = i >= n ? kBands + 1 : i < kBucketCache ? (int)bk[i] : band_of(fy[i], fv[i]);
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int i = i0 + k * kSortThreads + t;
+      const unsigned long long lost = __ballot(b[k] == kBands);
+      if (b[k] == kBands) perm[wave_claim(&cnt[kBands], lost)] = i;
+      else if (b[k] < kBands) perm[atomicAdd(&cnt[b[k]], 1)] = i;
+    }
   }
 }
 

@@ -527,3 +527,70 @@ def test_track_sequence_then_track_features(gpu, oracle):
     gpu.KLTFreeTrackingContext(tc)
     OX, OY, OV = OracleTracker(oracle).harness(frames, 300, 9, first=frames[0])
     assert np.array_equal(v, OV[:, 7]) and np.array_equal(x.view(np.int32), OX[:, 7].view(np.int32))
+
+
+@pytest.mark.parametrize("band", [False, True])
+def test_processing_order_many_features(gpu, oracle, band):
+    """k_band_order past its LDS bucket cache (40 000 features: a selected list
+    repeated, every fifth copy lost): every live copy tracks exactly like the
+    oracle's single list, lost copies are left alone; in band mode only the
+    copies whose y lies in the band move."""
+    from kltabi import fl_to_arrays, u8ptr
+    from kltamd.device import D2H, H2D, PyrDesc, TrackDesc, check
+    w, h, T, rep = 640, 480, 4, 27
+    frames = synth(gpu, 4242, w, h, T + 1)
+    tc = gpu.KLTCreateTrackingContext()
+    tc.contents.sequentialMode = 1
+    ctx = gpu.klt_amd_device_context(tc)
+    fl = gpu.KLTCreateFeatureList(1500)
+    gpu.KLTSelectGoodFeatures(tc, u8ptr(np.ascontiguousarray(frames[0])), w, h, fl)
+    x1, y1, v1 = fl_to_arrays(fl)
+    gpu.KLTFreeFeatureList(fl)
+    x, y, v = np.tile(x1, rep), np.tile(y1, rep), np.tile(v1, rep)
+    m = len(x1)
+    for c in range(0, rep, 5):
+        v[c * m:(c + 1) * m] = -1
+    n = len(x)
+    assert n > 32768
+    stack = np.ascontiguousarray(np.stack(frames))
+    dfr = gpu.klt_hip_malloc(ctx, stack.nbytes)
+    dx, dy, dv = (gpu.klt_hip_malloc(ctx, 4 * n) for _ in range(3))
+    esc = gpu.klt_hip_malloc(ctx, 4)
+    zero = np.zeros(1, np.int32)
+    check(gpu, ctx, gpu.klt_hip_memcpy(ctx, dfr, stack.ctypes.data, stack.nbytes, H2D), "h2d")
+    check(gpu, ctx, gpu.klt_hip_memcpy(ctx, esc, zero.ctypes.data, 4, H2D), "h2d")
+    for d, a in ((dx, x), (dy, y), (dv, v)):
+        check(gpu, ctx, gpu.klt_hip_memcpy(ctx, d, a.ctypes.data, a.nbytes, H2D), "h2d")
+    pd, td = PyrDesc(), TrackDesc()
+    gpu.klt_amd_pyr_desc(tc, w, h, tc.contents.nPyramidLevels, 1, C.byref(pd))
+    gpu.klt_amd_track_desc(tc, C.byref(td))
+    check(gpu, ctx, gpu.klt_hip_frames_begin(ctx, C.byref(pd), dfr, w), "begin")
+    lo, hi = 120.0, 330.0
+    if band:
+        check(gpu, ctx, gpu.klt_hip_track_frames_band(ctx, C.byref(pd), C.byref(td), dfr + w * h, w, w * h, T, dx, dy,
+                                                      dv, n, lo, hi, 0, h, esc, None, 0), "band")
+    else:
+        check(gpu, ctx, gpu.klt_hip_track_frames(ctx, C.byref(pd), C.byref(td), dfr + w * h, w, w * h, T, 2, dx, dy,
+                                                 dv, n, None, None, None, 0), "frames")
+    gx, gy, gv, ge = np.empty_like(x), np.empty_like(y), np.empty_like(v), np.zeros(1, np.int32)
+    for d, a in ((dx, gx), (dy, gy), (dv, gv), (esc, ge)):
+        check(gpu, ctx, gpu.klt_hip_memcpy(ctx, a.ctypes.data, d, a.nbytes, D2H), "d2h")
+    for d in (dfr, dx, dy, dv, esc):
+        gpu.klt_hip_free(ctx, d)
+    gpu.KLTFreeTrackingContext(tc)
+    ox, oy, ov = x1.copy(), y1.copy(), v1.copy()
+    ot = OracleTracker(oracle)
+    for j in range(T):
+        ot.track(frames[j], frames[j + 1], ox, oy, ov)
+    assert ge[0] == 0
+    for c in range(rep):
+        s = slice(c * m, (c + 1) * m)
+        moved = v[s] >= 0
+        if band:
+            moved &= (y[s] >= lo) & (y[s] < hi)
+        ex = np.where(moved, ox, x[s])
+        ey = np.where(moved, oy, y[s])
+        ev = np.where(moved, ov, v[s])
+        assert np.array_equal(gv[s], ev), c
+        assert np.array_equal(gx[s].view(np.int32), ex.view(np.int32)), c
+        assert np.array_equal(gy[s].view(np.int32), ey.view(np.int32)), c

@@ -19,6 +19,7 @@ usage: python tools/shard_sim.py [--worlds 1 2 4 8] [--margins 64] [--frames 129
 from __future__ import annotations
 
 import argparse
+import os
 import ctypes as C
 import json
 import sys
@@ -49,6 +50,11 @@ def main():
     ap.add_argument("--lazy-flag", action="store_true",
                     help="pass 2: read chunk c's escape flag after chunk c+1 is queued (a speculative driver "
                          "redoes c and drops c+1 when it is set), so the host never drains the stream per chunk")
+    ap.add_argument("--keep-states", default=None,
+                    help="save pass 1's chunk-start states as DIR/states_w<N>.npz (for a profiled --replay)")
+    ap.add_argument("--pass1-shared", action="store_true",
+                    help="pass 1 (the merged states) through one device context for every rank, each chunk "
+                         "started from a whole-frame pyramid: one bank arena instead of N (long chunks at 4K)")
     ap.add_argument("--replay", default=None, help=argparse.SUPPRESS)  # internal: pass 2 of one rank (npz of states)
     ap.add_argument("--rank", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--exchange-us", type=float, default=40.0,
@@ -163,8 +169,17 @@ def main():
     base_fps = None
     for margin in a.margins:
         for world in a.worlds:
-            ranks = [Rank(world, r, margin) for r in range(world)]
-            for rk in ranks:
+            ranks = [Rank(world, r, margin) for r in range(1 if a.pass1_shared else world)]
+            if a.pass1_shared:
+                # one context; each rank's chunk starts from frame c0-1's whole-frame pyramid (band-built
+                # rows equal whole-frame ones, so the states are the same) without build-ahead
+                for r in range(1, world):
+                    rk = Rank.__new__(Rank)
+                    rk.__dict__.update(ranks[0].__dict__)
+                    rk.band = band_of(H, world, r, margin, balanced_edges(ys, vs, H, world) if a.balanced else None)
+                    rk.rank = r
+                    ranks.append(rk)
+            for rk in ranks[:1] if a.pass1_shared else ranks:
                 rk.begin(0)
             x, y, v = xs.clone(), ys.clone(), vs.clone()
             starts, redone, per_rank = [], 0, [[0.0, 0.0, 0.0, 0] for _ in ranks]
@@ -177,7 +192,9 @@ def main():
                     xr, yr, vr = (t.clone() for t in state)
                     esc = torch.zeros(1, dtype=torch.int32, device=dev)
                     lib.klt_hip_set_timing(rk.ctx, 1)
-                    rk.chunk(c0, n, xr, yr, vr, esc, next_n=nn)
+                    if a.pass1_shared:
+                        rk.begin(c0 - 1)
+                    rk.chunk(c0, n, xr, yr, vr, esc, next_n=0 if a.pass1_shared else nn)
                     tm = Timing()
                     check(lib, rk.ctx, lib.klt_hip_get_timing(rk.ctx, C.byref(tm)), "timing")
                     lib.klt_hip_set_timing(rk.ctx, 0)
@@ -195,7 +212,7 @@ def main():
                         xr, yr, vr = (t.clone() for t in state)
                         esc = torch.zeros(1, dtype=torch.int32, device=dev)
                         rk.begin(c0 - 1)
-                        rk.chunk(c0, n, xr, yr, vr, esc, full=True, next_n=nn)
+                        rk.chunk(c0, n, xr, yr, vr, esc, full=True, next_n=0 if a.pass1_shared else nn)
                         outs.append((xr, yr, vr))
                 acc = None
                 for rk, (xr, yr, vr) in zip(ranks, outs):
@@ -215,6 +232,10 @@ def main():
                          x=np.stack([t[0].cpu().numpy() for t in starts]),
                          y=np.stack([t[1].cpu().numpy() for t in starts]),
                          v=np.stack([t[2].cpu().numpy() for t in starts]))
+                if a.keep_states:
+                    import shutil
+                    os.makedirs(a.keep_states, exist_ok=True)
+                    shutil.copy(f, f"{a.keep_states}/states_w{world}.npz")
                 rank_us, rank_kern = [], []
                 for r in range(world):
                     cmd = [sys.executable, __file__, "--replay", f, "--rank", str(r), "--width", str(W), "--height",
@@ -244,7 +265,7 @@ def main():
             print(json.dumps({k: run[k] for k in ("world", "margin_rows", "chunks_redone_full_frame", "state_digest",
                                                   "us_per_frame_max_rank", "projected_fps", "projected_speedup")}),
                   flush=True)
-            for rk in ranks:
+            for rk in ranks[:1] if a.pass1_shared else ranks:
                 lib.KLTFreeTrackingContext(rk.tc)
             torch.cuda.synchronize()
     print(json.dumps(out))
