@@ -114,6 +114,21 @@ __global__ void k_shard_unpack(const int *__restrict__ buf, float *__restrict__ 
   v[i] = buf[2 * n + i];
 }
 
+// the chunk-start state (ownership and the redo's starting point) and the
+// escape flag's reset in one launch: no copy-engine hand-offs between two
+// tracker launches
+__global__ void k_shard_save(const float *__restrict__ x, const float *__restrict__ y, const int *__restrict__ v,
+                             float *__restrict__ x0, float *__restrict__ y0, int *__restrict__ v0,
+                             int *__restrict__ escape, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    x0[i] = x[i];
+    y0[i] = y[i];
+    v0[i] = v[i];
+  }
+  if (i == 0) *escape = 0;
+}
+
 int grow_buffers(klt_shard *s, int n) {
   if ((size_t)n <= s->cap && s->d_buf) return 0;
   hipFree(s->d_buf);
@@ -262,13 +277,10 @@ KLT_API int klt_shard_track(klt_shard *s, const klt_hip_pyr_desc *pd, const klt_
   // the chunk-start state: ownership (y0, v0) and the redo's starting point
   const size_t fb = sizeof(float) * (size_t)n;
   std::string local;  // this rank's failure, if any: it still takes part in every exchange
-  if (n > 0 &&
-      (hipMemcpyAsync(s->d_x0, x, fb, hipMemcpyDeviceToDevice, st) != hipSuccess ||
-       hipMemcpyAsync(s->d_y0, y, fb, hipMemcpyDeviceToDevice, st) != hipSuccess ||
-       hipMemcpyAsync(s->d_v0, val, fb, hipMemcpyDeviceToDevice, st) != hipSuccess))
-    local = "chunk-start copy failed";
   int *escape = s->d_buf + (size_t)3 * s->cap;  // the buffer's slot after the features doubles as the device flag
-  if (local.empty() && hipMemsetAsync(escape, 0, sizeof(int), st) != hipSuccess) local = "escape flag reset failed";
+  hipLaunchKernelGGL(k_shard_save, dim3(n > 0 ? (n + 255) / 256 : 1), dim3(256), 0, st, x, y, val, s->d_x0, s->d_y0,
+                     s->d_v0, escape, n);
+  if (hipGetLastError() != hipSuccess) local = "chunk-start save failed";
   if (local.empty() &&
       klt_hip_track_frames_band(s->ctx, pd, td, frames, pitch, stride, nframes, x, y, val, n, s->own_lo, s->own_hi,
                                 s->row_lo, s->row_hi, escape, next_frames, next_nframes))
