@@ -106,6 +106,10 @@ struct TrkArgs {
   int prio;          // 1: tracker waves raise their issue priority (s_setprio 3) over concurrent pyramid waves
   int aos;           // 1 (k_track7): a level's img is {img, gx, gy} interleaved per pixel (gx/gy unused)
   int fast;          // 1 (k_track7): KLT_HIP_FAST window sums (DPP tree), interleaved two-level pyramids only
+  // k_track7 (set by launch_track7): per level, the bit pattern of the smallest
+  // float x >= 3 with (float)w - (x + 3) < 1.001f (ooby: the same for h), so the
+  // window bounds test is integer compares of x's and y's bit patterns
+  int oobx[KLT_HIP_MAX_LEVELS], ooby[KLT_HIP_MAX_LEVELS];
 };
 
 // batched frames: frame j tracks pyramid j-1 -> j of a bank; row j of the

@@ -31,6 +31,7 @@
 #pragma clang diagnostic ignored "-Wpass-failed"
 
 #include <math.h>
+#include <string.h>
 
 #include "klt_dev.h"
 
@@ -52,11 +53,20 @@ constexpr int kWaves = kBlock / kWave;
 __device__ __forceinline__ float u(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
 __device__ __forceinline__ int u(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// window bounds test (trackFeatures.c:421-427 / :460-462, one_plus_eps 1.001)
-__device__ __forceinline__ bool out7(float x, float y, int nc, int nr) {
-  const float e = 1.001f;
-  if (!(isfinite(x) && isfinite(y))) return true;  // the reference would fault; treat as OOB
-  return x - kHw < 0.0f || nc - (x + kHw) < e || y - kHw < 0.0f || nr - (y + kHw) < e;
+// window bounds test (trackFeatures.c:421-427 / :460-462, one_plus_eps 1.001):
+//   x - 3 < 0 || w - (x + 3) < 1.001 || (the same for y and h)
+// in float arithmetic.  x - 3 < 0 exactly when x < 3, and w - (x + 3) never
+// grows with x, so the second test holds exactly from one float on (tx, found
+// on the host by bisection with the same float operations); IEEE order of
+// non-negative floats is the order of their bit patterns, and a negative
+// float's pattern is a negative int.  So the test is four integer compares
+// of wave-uniform values -- scalar instructions, no VALU round trip --
+// that also send infinities and NaNs out (the reference would fault on them)
+constexpr int kThreeBits = 0x40400000;  // 3.0f
+
+__device__ __forceinline__ bool out7(float x, float y, int tx, int ty) {
+  const int xb = __float_as_int(x), yb = __float_as_int(y);
+  return xb < kThreeBits || xb >= tx || yb < kThreeBits || yb >= ty;
 }
 
 // _interpolate (trackFeatures.c:31-57) for this lane's pixel: corner offset and weights
@@ -214,10 +224,11 @@ __device__ __forceinline__ void sums(float *red, int lane, bool on, const float 
 struct Lev {
   const float *img, *gx, *gy;
   int w, h, vlo, vhi;
+  int tx, ty;  // out7's thresholds for this level's size (TrkArgs::oobx / ooby)
 };
 
-__device__ __forceinline__ Lev lev_of(const TrkLevel &L, long off) {
-  return Lev{L.img + off, L.gx + off, L.gy + off, L.w, L.h, L.vlo, L.vhi};
+__device__ __forceinline__ Lev lev_of(const TrkLevel &L, long off, int tx, int ty) {
+  return Lev{L.img + off, L.gx + off, L.gy + off, L.w, L.h, L.vlo, L.vhi, tx, ty};
 }
 
 // image 1 of frame j at level r: the previous pyramid (a.A) for the batch's
@@ -229,7 +240,7 @@ __device__ __forceinline__ Lev lev_prev(const TrkArgs &a, const TrkFramesArgs &b
   const bool f = j == 0;
   const long off = f ? 0L : (long)(j - 1) * b.lfs[r];
   return Lev{(f ? P.img : Q.img) + off, (f ? P.gx : Q.gx) + off, (f ? P.gy : Q.gy) + off, f ? P.w : Q.w,
-             f ? P.h : Q.h, f ? P.vlo : Q.vlo, f ? P.vhi : Q.vhi};
+             f ? P.h : Q.h, f ? P.vlo : Q.vlo, f ? P.vhi : Q.vhi, a.oobx[r], a.ooby[r]};
 }
 
 // band-built pyramids (klt_hip_track_frames_band): every row the window's
@@ -281,8 +292,7 @@ __device__ __forceinline__ int pass7(const TrkArgs &a, const Lev &A, const Lev &
                                      LevState &ls, int lane, float fi, float fj, bool on, float *red, Pending &pd,
                                      const Lev &R, int &rstat, Counts &cnt) {
   T7_T(t_top);
-  const int nc = A.w, nr = A.h;
-  bool stop = (FIRST && x1_out) || out7(ls.x2, ls.y2, nc, nr);
+  bool stop = (FIRST && x1_out) || out7(ls.x2, ls.y2, A.tx, A.ty);
   if (BAND && !stop && (band_bad(B, ls.y2) || (FIRST && band_bad(A, y1)))) {
     *a.escape = 1;  // the caller redoes the chunk from whole-frame pyramids
     stop = true;
@@ -395,8 +405,7 @@ template <bool BAND, bool AOS, bool FAST>
 __device__ int level7(const TrkArgs &a, const Lev &A, const Lev &B, float x1, float y1, float &x2, float &y2,
                       int lane, float fi, float fj, bool on, float *red, bool residue, bool defer, Pending &pd,
                       bool job, const Lev &R, int &rstat, bool &lost_prev, Counts &cnt) {
-  const int nc = A.w, nr = A.h;
-  const bool x1_out = out7(x1, y1, nc, nr);
+  const bool x1_out = out7(x1, y1, A.tx, A.ty);
   LevState ls;
   ls.x2 = x2;
   ls.y2 = y2;
@@ -413,7 +422,7 @@ __device__ int level7(const TrkArgs &a, const Lev &A, const Lev &B, float x1, fl
   }
   if (r == kPassOOB) return kOOB;
   // after the loop (:460-474)
-  if (out7(x2, y2, nc, nr)) return kOOB;
+  if (out7(x2, y2, A.tx, A.ty)) return kOOB;
   if (BAND && band_bad(B, y2)) {
     *a.escape = 1;
     return kOOB;
@@ -498,7 +507,7 @@ __global__ __launch_bounds__(kBlock) void k_track7(TrkArgs a, TrkFramesArgs b, f
         xo = u(xo * a.ss);
         yo = u(yo * a.ss);
         const Lev LA = lev_prev(a, b, r, j);
-        const Lev LB = lev_of(a.B[r], (long)j * b.lfs[r]);
+        const Lev LB = lev_of(a.B[r], (long)j * b.lfs[r], a.oobx[r], a.ooby[r]);
         const bool lj = job && r == nlev - 1;
         T7_T(t_l0);
         val = level7<BAND, AOS, FAST>(a, LA, LB, xl, yl, xo, yo, lane, fi, fj, on, red, r == 0,
@@ -568,8 +577,38 @@ __global__ __launch_bounds__(kBlock) void k_track7(TrkArgs a, TrkFramesArgs b, f
 
 }  // namespace
 
-hipError_t launch_track7(hipStream_t st, bool band, const TrkArgs &a, const TrkFramesArgs &b, float *x, float *y,
+// out7's threshold for a level dimension n: the bit pattern of the smallest
+// float x >= 3 with (float)n - (x + 3) < 1.001f, by bisection over the
+// patterns of [3, n] (the test is false at 3 unless n < 7.001, true at n)
+static int oob_threshold(int n) {
+  auto out = [n](int xb) {
+    float x;
+    memcpy(&x, &xb, sizeof x);
+    volatile float t = x + 3.0f;  // the device's float operations, one rounding each
+    volatile float g = (float)n - t;
+    return g < 1.001f;
+  };
+  const float c = (float)(n > 3 ? n : 3);
+  int lo, hi;
+  const float three = 3.0f;
+  memcpy(&lo, &three, sizeof lo);
+  memcpy(&hi, &c, sizeof hi);
+  if (out(lo)) return lo;
+  while (hi - lo > 1) {  // out(lo) false, out(hi) true
+    const int mid = lo + (hi - lo) / 2;
+    if (out(mid)) hi = mid;
+    else lo = mid;
+  }
+  return hi;
+}
+
+hipError_t launch_track7(hipStream_t st, bool band, const TrkArgs &a_in, const TrkFramesArgs &b, float *x, float *y,
                          int *v, int n) {
+  TrkArgs a = a_in;
+  for (int l = 0; l < KLT_HIP_MAX_LEVELS; ++l) {
+    a.oobx[l] = oob_threshold(a.B[l].w);
+    a.ooby[l] = oob_threshold(a.B[l].h);
+  }
   const int nb = (n + kWaves - 1) / kWaves;
   const int grid = b.xcd_per > 0 ? 8 * b.xcd_per : nb;
   // band: escape checks (klt_hip_track_frames_band); aos: interleaved levels
