@@ -76,11 +76,13 @@ struct Pix {
   float w0, w1, w2, w3;
 };
 
+// Every caller gathers at a position that passed out7 (this pass's, the
+// level's x1, the previous frame's final one for the deferred residue), so
+// x + i lies in [0, w - 2.001) for every window column i and (int) needs no
+// clamp: the four corners are inside the level.
 __device__ __forceinline__ Pix pix_at(int w, int h, float x, float y) {
-  int xt = (int)x, yt = (int)y;
+  const int xt = (int)x, yt = (int)y;
   const float ax = x - xt, ay = y - yt;
-  xt = clampi(xt, 0, w - 2);  // only guards lanes / positions the bounds test excludes
-  yt = clampi(yt, 0, h - 2);
   Pix p;
   p.px = (unsigned)(yt * w + xt);
   p.off = p.px * 4u;
@@ -113,9 +115,11 @@ struct Tri {
   Quad i, x, y;
 };
 __device__ __forceinline__ Tri tri(const float *P, const Pix &p, unsigned rowb) {
-  const char *b = reinterpret_cast<const char *>(P) + p.px * 12u;
-  const f4u a0 = *reinterpret_cast<const f4u *>(b), b0 = *reinterpret_cast<const f4u *>(b + rowb);
-  const f2u a1 = *reinterpret_cast<const f2u *>(b + 16), b1 = *reinterpret_cast<const f2u *>(b + rowb + 16);
+  // uniform base + 32-bit lane offsets for both rows (scalar-base addressing)
+  const char *base = reinterpret_cast<const char *>(P);
+  const unsigned o0 = p.px * 12u, o1 = o0 + rowb;
+  const f4u a0 = *reinterpret_cast<const f4u *>(base + o0), b0 = *reinterpret_cast<const f4u *>(base + o1);
+  const f2u a1 = *reinterpret_cast<const f2u *>(base + o0 + 16), b1 = *reinterpret_cast<const f2u *>(base + o1 + 16);
   Tri t;
   t.i.r0 = make_float2(a0.x, a0.w);
   t.i.r1 = make_float2(b0.x, b0.w);
@@ -127,8 +131,9 @@ __device__ __forceinline__ Tri tri(const float *P, const Pix &p, unsigned rowb) 
 }
 // img alone from an interleaved level
 __device__ __forceinline__ Quad quad_i(const float *P, const Pix &p, unsigned rowb) {
-  const float *b = reinterpret_cast<const float *>(reinterpret_cast<const char *>(P) + p.px * 12u);
-  const float *c = reinterpret_cast<const float *>(reinterpret_cast<const char *>(P) + p.px * 12u + rowb);
+  const unsigned o0 = p.px * 12u, o1 = o0 + rowb;
+  const float *b = reinterpret_cast<const float *>(reinterpret_cast<const char *>(P) + o0);
+  const float *c = reinterpret_cast<const float *>(reinterpret_cast<const char *>(P) + o1);
   Quad q;
   q.r0 = make_float2(b[0], b[3]);
   q.r1 = make_float2(c[0], c[3]);
