@@ -44,6 +44,7 @@
 #include <thread>
 #include <vector>
 
+#include "host_sort.h"
 #include "klt_dev.h"
 
 namespace kltdev {
@@ -348,52 +349,6 @@ struct Seg {
   bool sorted = false;  // host segment already in its final order
 };
 
-// the exact partition step of klt_select.c (the reference's _quicksort body)
-// on host pairs {val, idx}
-unsigned host_partition(int2 *a, unsigned n) {
-  unsigned i = 0, j = n;
-  std::swap(a[0], a[n / 2]);
-  const int pv = a[0].x;
-  for (;;) {
-    do --j;
-    while (a[j].x < pv);
-    do ++i;
-    while (i < j && a[i].x > pv);
-    if (i >= j) break;
-    std::swap(a[i], a[j]);
-  }
-  std::swap(a[j], a[0]);
-  return j;
-}
-
-// the whole quicksort of a[0..n) below one partition step: the left part, then
-// the right part, each sorted the same way.  The two parts are disjoint, so
-// sorting them in any order -- or at once, on two threads -- leaves every
-// element where the sequential recursion (and the lazy walk over it) puts it.
-// The smaller part recurses and the larger one loops, which bounds the
-// recursion depth by log2(n) whatever the pivots.
-void host_sort(int2 *a, unsigned n, int par) {
-  while (n > 1) {
-    const unsigned j = host_partition(a, n);
-    int2 *lo = a, *hi = a + j + 1;
-    unsigned nlo = j, nhi = n - j - 1;
-    if (par > 0 && nlo >= kSelParMin && nhi >= kSelParMin) {
-      std::thread t([=] { host_sort(hi, nhi, par - 1); });
-      host_sort(lo, nlo, par - 1);
-      t.join();
-      return;
-    }
-    if (nlo < nhi) {
-      host_sort(lo, nlo, par);
-      a = hi;
-      n = nhi;
-    } else {
-      host_sort(hi, nhi, par);
-      n = nlo;
-    }
-  }
-}
-
 // split device segment g on the device until its leftmost part is at most the
 // threshold; the resulting segments are pushed onto stk (device-resident)
 int dev_refine(SelEngine *e, hipStream_t st, Seg g, std::vector<Seg> &stk, std::string *err) {
@@ -483,7 +438,7 @@ struct LazySort {
         // a segment the walk has reached is consumed almost whole: sort it
         // outright (in parallel) and hand its positions out in order
         const double t0 = now_us();
-        host_sort(e->h_kv + g.start, (unsigned)g.len, kSelParDepth);
+        kltsort::Pool<int2>::get((1 << kSelParDepth) - 1).sort(e->h_kv + g.start, (unsigned)g.len, kSelParDepth, kSelParMin);
         e->us[2] += now_us() - t0;
         g.sorted = true;
       }

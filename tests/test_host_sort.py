@@ -1,0 +1,84 @@
+"""The pooled host quicksort (csrc/host_sort.h) on the CPU.
+
+select.hip sorts the map segments the minimum-distance walk reaches
+(selectGoodFeatures.c:62-96 quicksort order) on a persistent worker pool.
+The reference's quicksort is unstable, so the permutation -- not just the
+sorted keys -- must equal the sequential recursion's.  This builds the header
+with g++ into a small driver and compares the pooled sort (up to 2^3 tasks,
+small par_min so every size splits) with the one-thread sort, element for
+element, on random, tie-heavy, constant and presorted inputs, including
+several callers sorting at once on the shared pool.
+"""
+from __future__ import annotations
+
+import shutil
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+CSRC = ROOT / "klt-feature-tracker-acceleration-gpus_amd" / "csrc"
+
+DRIVER = r"""
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <thread>
+#include <vector>
+#include "host_sort.h"
+struct P { int x, y; };
+static std::vector<P> make(int kind, unsigned n, unsigned seed) {
+  std::mt19937 r(seed);
+  std::vector<P> v(n);
+  for (unsigned i = 0; i < n; ++i) {
+    int x = kind == 0 ? (int)(r() >> 1) : kind == 1 ? (int)(r() % 7) : kind == 2 ? 5 : (int)(n - i);
+    v[i] = P{x, (int)i};
+  }
+  return v;
+}
+int main() {
+  auto &pool = kltsort::Pool<P>::get(7);
+  int bad = 0, cases = 0;
+  const unsigned sizes[] = {0, 1, 2, 3, 17, 255, 4096, 40000, 100003};
+  for (int kind = 0; kind < 4; ++kind)
+    for (unsigned n : sizes)
+      for (unsigned par_min : {2u, 64u, 2048u}) {
+        std::vector<P> a = make(kind, n, n * 31 + kind), b = a;
+        pool.sort(a.data(), n, 0, par_min);   // sequential: no task is queued
+        pool.sort(b.data(), n, 3, par_min);
+        ++cases;
+        for (unsigned i = 0; i < n; ++i)
+          if (a[i].x != b[i].x || a[i].y != b[i].y) { ++bad; std::printf("mismatch kind %d n %u pm %u at %u\n", kind, n, par_min, i); break; }
+        for (unsigned i = 1; i < n; ++i)
+          if (a[i - 1].x < a[i].x) { ++bad; std::printf("unsorted kind %d n %u\n", kind, n); break; }
+      }
+  // four callers at once on the shared pool
+  std::vector<std::vector<P>> seq(4), par(4);
+  for (int c = 0; c < 4; ++c) {
+    seq[c] = make(c % 2, 60000, 100 + c);
+    par[c] = seq[c];
+    pool.sort(seq[c].data(), 60000, 0, 64);
+  }
+  std::vector<std::thread> th;
+  for (int c = 0; c < 4; ++c) th.emplace_back([&, c] { pool.sort(par[c].data(), 60000, 3, 64); });
+  for (auto &t : th) t.join();
+  for (int c = 0; c < 4; ++c, ++cases)
+    for (unsigned i = 0; i < 60000; ++i)
+      if (seq[c][i].x != par[c][i].x || seq[c][i].y != par[c][i].y) { ++bad; std::printf("concurrent mismatch %d\n", c); break; }
+  std::printf("cases %d bad %d\n", cases, bad);
+  return bad != 0;
+}
+"""
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
+def test_pooled_sort_equals_sequential(tmp_path):
+    src = tmp_path / "drv.cpp"
+    src.write_text(DRIVER)
+    exe = tmp_path / "drv"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", f"-I{CSRC}", str(src), "-o", str(exe)],
+                   check=True, capture_output=True, text=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "bad 0" in out.stdout
