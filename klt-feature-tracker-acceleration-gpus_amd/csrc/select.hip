@@ -36,6 +36,7 @@
 #pragma clang fp contract(off)
 
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -57,7 +58,7 @@ constexpr int kSelStack = 512;                      // segments a device refinem
 constexpr int kSelScanThreads = 1024;
 constexpr unsigned kBlockedBit = 0x80000000u;
 constexpr unsigned kSelParMin = 2048;               // host sort: parts at least this long go to a second thread
-constexpr int kSelParDepth = 3;                     // host sort: up to 2^3 threads
+constexpr int kSelParDepth = 4;                     // host sort: up to 2^4 tasks (tools/sort_depth_ab.sh: 4 beat 3, 5)
 
 struct SelState {
   int start, len;  // the leftmost segment still to split
@@ -349,6 +350,17 @@ struct Seg {
   bool sorted = false;  // host segment already in its final order
 };
 
+// levels of two-way task splits in the host sort (2^depth tasks on the pool);
+// KLT_AMD_SORT_DEPTH (0..5) overrides the default for A/B runs, read once
+int sort_depth() {
+  static const int d = [] {
+    const char *v = getenv("KLT_AMD_SORT_DEPTH");
+    const int x = v && *v ? atoi(v) : kSelParDepth;
+    return x < 0 ? 0 : x > 5 ? 5 : x;
+  }();
+  return d;
+}
+
 // split device segment g on the device until its leftmost part is at most the
 // threshold; the resulting segments are pushed onto stk (device-resident)
 int dev_refine(SelEngine *e, hipStream_t st, Seg g, std::vector<Seg> &stk, std::string *err) {
@@ -438,7 +450,9 @@ struct LazySort {
         // a segment the walk has reached is consumed almost whole: sort it
         // outright (in parallel) and hand its positions out in order
         const double t0 = now_us();
-        kltsort::Pool<int2>::get((1 << kSelParDepth) - 1).sort(e->h_kv + g.start, (unsigned)g.len, kSelParDepth, kSelParMin);
+        const int depth = sort_depth();
+        static const int workers = std::max(0, std::min((1 << depth) - 1, (int)std::thread::hardware_concurrency() - 1));
+        kltsort::Pool<int2>::get(workers).sort(e->h_kv + g.start, (unsigned)g.len, depth, kSelParMin);
         e->us[2] += now_us() - t0;
         g.sorted = true;
       }
