@@ -41,6 +41,7 @@ sys.path.insert(0, str(ROOT / "tests"))
 
 METRIC = "frames/sec + pyramid Gpix/s @1080p 5000 feats, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+REPLAY_WARMUP_S = 0.030  # untimed replays before the event-timed one (same clock state in every run shape)
 
 
 def parse():
@@ -65,8 +66,8 @@ def parse():
     p.add_argument("--chunk", type=int, default=None,
                    help="frames per batched pyramid/track launch (klt_hip_track_frames; default 64; sharded: frames "
                         "per exchange, 64; "
-                        "capped at ceil(steps/2) so that the timed region always holds >= 2 chunks and the "
-                        "overlapped schedule really runs); 0 = the per-frame pipelined path (klt_hip_track_sequence)")
+                        "capped at ceil(steps / --min-chunks)); 0 = the per-frame pipelined path "
+                        "(klt_hip_track_sequence)")
     p.add_argument("--replay-frames", type=int, default=489,
                    help="frames of the per-kernel event replay and the tracker-count replay (at least --steps); "
                         "they run at the production chunk (--chunk, default 64) whatever --steps caps the timed "
@@ -80,9 +81,11 @@ def parse():
     p.add_argument("--serial", action="store_true",
                    help="build and track on one stream; default: chunk c+1's pyramids are built on a second "
                         "stream while chunk c is tracked (they fill the CUs the tracker's last waves leave idle)")
-    p.add_argument("--min-chunks", type=int, default=2,
+    p.add_argument("--min-chunks", type=int, default=1,
                    help="the timed region holds at least this many chunks (the chunk is capped at "
-                        "ceil(steps / min-chunks)); 1 with --serial: one launch pair over the whole region")
+                        "ceil(steps / min-chunks)); default 1: a region of at most --chunk frames is one launch "
+                        "pair on one stream (nothing to overlap), a longer one overlaps chunk c+1's pyramids with "
+                        "chunk c's tracking")
     p.add_argument("--event-timing", choices=["timed", "replay"], default="replay",
                    help="record per-kernel HIP events inside the timed region or in a replay")
     a = p.parse_args()
@@ -177,14 +180,19 @@ def main() -> None:
               "build")
         slot.value = 0
 
+    def frames_args(t0, n, chunk):
+        """klt_hip_track_frames' arguments for frames t0 .. t0+n-1 (built
+        outside the timed region: the marshalling is the harness's, not the
+        library's)"""
+        tp = [C.c_void_p(a.data_ptr() + a.element_size() * t0 * NF) for a in tab]
+        return (ctx, C.byref(pd), C.byref(td), C.c_void_p(fptr + t0 * W * H), W, W * H, n, chunk,
+                C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()), NF, tp[0], tp[1],
+                tp[2], NF)
+
     def run(t0, n, chunk=None):
         chunk = args.chunk if chunk is None else chunk
         if chunk > 0:
-            tp = [C.c_void_p(a.data_ptr() + a.element_size() * t0 * NF) for a in tab]
-            check(lib, ctx, lib.klt_hip_track_frames(ctx, C.byref(pd), C.byref(td), C.c_void_p(fptr + t0 * W * H),
-                                                     W, W * H, n, chunk, C.c_void_p(x.data_ptr()),
-                                                     C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()), NF,
-                                                     tp[0], tp[1], tp[2], NF), "track_frames")
+            check(lib, ctx, lib.klt_hip_track_frames(*frames_args(t0, n, chunk)), "track_frames")
             return
         check(lib, ctx, lib.klt_hip_track_sequence(ctx, C.byref(pd), C.byref(td), C.c_void_p(fptr), W, W * H,
                                                    t0, n, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()),
@@ -200,11 +208,20 @@ def main() -> None:
     lib.klt_hip_set_timing(ctx, 1 if timed_events else 0)
     if world > 1:
         dist.barrier()
+    if args.chunk > 0:
+        fa = frames_args(t_start, args.steps, args.chunk)
+        timed = lambda: lib.klt_hip_track_frames(*fa)  # noqa: E731
+    else:
+        timed = lambda: run(t_start, args.steps) or 0  # noqa: E731
     torch.cuda.synchronize()
+    m0 = time.monotonic_ns()
     t0 = time.perf_counter()
-    run(t_start, args.steps)
+    rc = timed()
+    t_enq = time.perf_counter() - t0
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    m1 = time.monotonic_ns()
+    check(lib, ctx, rc, "track_frames (timed region)")
     if world > 1:
         dist.barrier()
     live_after = int((v >= 0).sum().item())
@@ -216,8 +233,24 @@ def main() -> None:
         # production chunk over `replay` frames: each kernel's duration is then
         # its own (the roofline), not time shared with a kernel overlapping it
         # on the other stream, and the launches are 64-frame launches
-        x.copy_(xs); y.copy_(ys); v.copy_(vs)
         check(lib, ctx, lib.klt_hip_set_frames_overlap(ctx, 0), "overlap")
+        # a fixed warm-up first: the same replay, untimed, repeated for at least
+        # REPLAY_WARMUP_S of device time, so that the timed replay follows the
+        # same sustained load whatever the timed region's length (the kernels'
+        # durations follow the shader clock, which the chip lowers and then
+        # partly restores over the first milliseconds of pyramid load:
+        # tools/clock_of.py)
+        w0, warm_runs = time.perf_counter(), 0
+        while True:
+            x.copy_(xs); y.copy_(ys); v.copy_(vs)
+            build0(t_start - 1)
+            run(t_start, replay, rchunk)
+            torch.cuda.synchronize()
+            warm_runs += 1
+            if time.perf_counter() - w0 >= REPLAY_WARMUP_S:
+                break
+        warm_ms = 1e3 * (time.perf_counter() - w0)
+        x.copy_(xs); y.copy_(ys); v.copy_(vs)
         build0(t_start - 1)
         lib.klt_hip_set_timing(ctx, 1)
         run(t_start, replay, rchunk)
@@ -238,8 +271,9 @@ def main() -> None:
         lib.klt_hip_set_track_count(ctx, 0)
         # feature-frames: features live when frame j starts (table row j-1 holds the list after j-1)
         ff = int((tab[2][t_start - 1:t_start - 1 + nrep] >= 0).sum().item())
-        tracker = tracker_line(solves.value, passes.value, ff, tm,
-                               "kltdev::k_track7<false>" if args.reduction == "exact" else "kltdev::k_track_frames_g")
+        # the instance the runtime actually launched (rocprofv3's name for it), so
+        # that the PMC summary below is matched to the same kernel
+        tracker = tracker_line(solves.value, passes.value, ff, tm, lib.klt_hip_track_kernel(ctx).decode())
         pmc = ROOT / "profiles" / "pmc_tracker.json"
         if pmc.exists():
             try:
@@ -314,9 +348,17 @@ def main() -> None:
         "kernels_us_per_frame": {"k_pyr_l0": l0f, "k_pyr_l1": l1f, "k_track": trkf},
         "replay": {"frames": replay if not timed_events else args.steps,
                    "chunk": rchunk if not timed_events else args.chunk,
+                   "warmup": ({"runs": warm_runs, "ms": warm_ms,
+                               "what": f"the same {replay}-frame replay, untimed, repeated for >= "
+                                       f"{1e3 * REPLAY_WARMUP_S:.0f} ms right before the timed one"}
+                              if not timed_events else None),
                    "what": "per-kernel HIP events and tracker counters come from replays of this length and chunk"},
         "frames_per_launch": fpl,
         "live_features": {"after_warmup": live_before, "at_end": live_after},
+        # host side of the timed region: the time the call took to queue its
+        # launches, and CLOCK_MONOTONIC marks around the region (rocprofv3
+        # kernel traces use the same clock, so launch latency can be read off)
+        "timed_region_host": {"enqueue_us": 1e6 * t_enq, "monotonic_ns": [m0, m1]},
     }
     result["value_kind"] = "device_only"
     if tracker:

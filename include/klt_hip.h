@@ -109,6 +109,9 @@ int klt_hip_ctx_device(klt_hip_ctx *ctx);
 /* the calling thread's current HIP device, -1 on error */
 int klt_hip_current_device(void);
 const char *klt_hip_last_error(klt_hip_ctx *ctx);
+/* the tracker kernel instance the context launched last, as rocprofv3 names it
+   (e.g. "kltdev::k_track7<false, true, 2, false>"); "" before any launch */
+const char *klt_hip_track_kernel(klt_hip_ctx *ctx);
 /* stream: a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL
    restores the context's own non-blocking stream */
 int klt_hip_set_stream(klt_hip_ctx *ctx, void *stream);
@@ -172,7 +175,14 @@ int klt_hip_get_host_threads(klt_hip_ctx *ctx);
    staging; for callers that reuse fixed frame buffers (the reference harness:
    img1/img2, example3.c:45-46,56,75).  Registered buffers must not overlap;
    they are released by klt_hip_unregister_host (after the context's streams
-   drain), when the context is reset (parked) or destroyed. */
+   drain), when the context is reset (parked) or destroyed.
+   Lifetime: klt_hip_upload_frame from a registered buffer only QUEUES that
+   DMA (the pageable path has finished reading the caller's bytes when it
+   returns), so a direct klt_hip_* caller must not modify the frame's bytes
+   until the context's stream has drained past the upload (klt_hip_sync, or
+   any synchronous call after it).  The klt.h entry points (KLTTrackFeatures,
+   KLTSelectGoodFeatures, KLTReplaceLostFeatures) synchronize before they
+   return, so their callers may reuse the buffer at once. */
 int klt_hip_register_host(klt_hip_ctx *ctx, const void *ptr, size_t bytes);
 int klt_hip_unregister_host(klt_hip_ctx *ctx, const void *ptr);
 /* Byte budget of the three pyramid banks of klt_hip_track_frames* (one device

@@ -185,7 +185,7 @@ hipError_t launch_track_frames(hipStream_t st, bool exact, bool li, bool patch, 
 // track7.hip: the default configuration (7x7 window, exact sums, no gain/bias,
 // one wave per feature) with the latency-lean pass; band: escape checks
 hipError_t launch_track7(hipStream_t st, bool band, const TrkArgs &a, const TrkFramesArgs &b, float *x, float *y,
-                         int *v, int n);
+                         int *v, int n, const char **name = nullptr);
 // band-sorted processing order (one workgroup); count != nullptr: keep only
 // live features with own_lo <= y < own_hi and store how many
 hipError_t launch_band_order(hipStream_t st, const float *fy, const int *fv, int n, int nrows, int *perm,

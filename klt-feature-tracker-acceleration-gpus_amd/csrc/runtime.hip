@@ -194,11 +194,12 @@ struct klt_hip_ctx {
   float *pl_scr[2][KLT_HIP_MAX_LEVELS] = {};
   size_t pl_cap[2][KLT_HIP_MAX_LEVELS] = {};
   int track_impl = 0;    // 0: track7.hip for the default configuration, 1: the generic k_track_frames_g
+  const char *track_kernel = nullptr;  // instance name of the last tracker launch (klt_hip_track_kernel)
   int serial_frames = 1;  // klt_hip_track_frames: 1 builds and tracks on one stream (default: the
                           // tracker and the pyramid kernels compete for the same CUs; overlap buys ~3 %)
   int *d_perm = nullptr;
   size_t perm_cap = 0;
-  int perm_n = -1, perm_age = 0;  // features of the order in d_perm (-1: none), calls since it was sorted
+  int perm_n = -1, perm_age = 0;  // features of the order in d_perm (-1: none), frames tracked with it
   int *d_count = nullptr;  // band mode: features owned in this chunk
   unsigned long long *d_trk_count = nullptr;  // klt_hip_set_track_count: {solves, passes}, null when off
   // klt_hip_track_frames_host: frames uploaded chunk by chunk.  Two slots per
@@ -548,8 +549,10 @@ void fill_trk_args(const klt_hip_track_desc *d, int nlev, int ss, int ncols, int
 
 // fewer features than this: input order (the sort launch would not pay)
 constexpr int kOrderMin = 2048;
-// one-frame launches re-sort the processing order every this many calls
-constexpr int kOrderReuse = 8;
+// the processing order (a locality hint: any permutation gives the same
+// results) is re-sorted once it covers this many tracked frames; features
+// move about a pixel per frame, the XCDs' row bands are ~H/8 rows tall
+constexpr int kOrderMaxAge = 32;
 
 // the default configuration's latency-lean tracker (track7.hip) serves this
 // launch: 7x7 window, exact sums, no gain/bias, the lane-patch path on, and
@@ -573,20 +576,31 @@ bool t7_tracks(const klt_hip_ctx *c, const klt_hip_track_desc *d) {
 int order_features(klt_hip_ctx *c, hipStream_t st, int nrows, const float *y, const int *v, int n, int nframes,
                    const float *own, TrkFramesArgs &bb) {
   if (own || (c->track_order == 0 && n >= kOrderMin)) {
-    // one-frame launches (KLTTrackFeatures) reuse the order of a recent call
-    // with the same feature count: any permutation gives the same results,
-    // and features move little from one frame to the next
-    const bool reuse = !own && nframes == 1 && c->perm_n == n && c->perm_age < kOrderReuse;
+    // a launch reuses the order of a recent one with the same feature count
+    // while that order covers at most kOrderMaxAge frames in all: any
+    // permutation gives the same results, and features move little from one
+    // frame to the next (per-call KLTTrackFeatures and short batched calls
+    // then skip the sort; 64-frame chunks re-sort every launch)
+    const bool reuse = !own && c->perm_n == n && c->perm_age + nframes <= kOrderMaxAge;
     if (reuse) {
-      ++c->perm_age;
+      c->perm_age += nframes;
     } else {
       if (grow(c, &c->d_perm, &c->perm_cap, (size_t)n)) return -1;
       if (own && !c->d_count) HIPCHK(c, hipMalloc((void **)&c->d_count, sizeof(int)));
+#ifdef KLT_HOST_PROF
+      timespec t0_, t1_;
+      clock_gettime(CLOCK_MONOTONIC, &t0_);
+#endif
       if (launched(c, "k_band_order", launch_band_order(st, y, v, n, nrows, c->d_perm, own ? own[0] : 0.0f,
                                                         own ? own[1] : 0.0f, own ? c->d_count : (int *)nullptr)))
         return -1;
+#ifdef KLT_HOST_PROF
+      clock_gettime(CLOCK_MONOTONIC, &t1_);
+      fprintf(stderr, "hostmark band_order_launch %.2f us\n",
+              (t1_.tv_sec - t0_.tv_sec) * 1e6 + (t1_.tv_nsec - t0_.tv_nsec) * 1e-3);
+#endif
       c->perm_n = own ? -1 : n;  // a band's order lists only the band's features
-      c->perm_age = 0;
+      c->perm_age = nframes;
     }
     if (own) bb.n_dev = c->d_count;
     const int per = kBlock / kWave, nb = (n + per - 1) / per;
@@ -639,7 +653,8 @@ int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc
       }
     }
   }
-  if (t7) return launched(c, "k_track7", launch_track7(st, aa.escape != nullptr, aa, b2, x, y, v, n));
+  if (t7) return launched(c, "k_track7", launch_track7(st, aa.escape != nullptr, aa, b2, x, y, v, n, &c->track_kernel));
+  c->track_kernel = "kltdev::k_track_frames_g";
   return launched(c, "k_track_frames", launch_track_frames(st, exact, li, patch, win7, npx, aa, b2, x, y, v, n));
 }
 
@@ -959,8 +974,9 @@ KLT_API int klt_hip_ctx_reset(klt_hip_ctx *c) {
   if (!c) return -1;
   if (use_device(c)) return -1;
   // nothing of the previous owner is still running: the context's own streams
-  // (a caller's stream set with klt_hip_set_stream is the caller's to drain)
-  for (hipStream_t st : {c->stream, c->own, c->pstream, c->cstream, c->dstream})
+  // (a caller's stream set with klt_hip_set_stream is the caller's to drain:
+  // it may already be destroyed, so c->stream is not touched unless it is ours)
+  for (hipStream_t st : {c->own, c->pstream, c->cstream, c->dstream})
     if (st) HIPCHK(c, hipStreamSynchronize(st));
   if (klt_hip_ctx_footprint(c) > kKeepBytes) {
     free_banks(c);
@@ -1018,6 +1034,8 @@ KLT_API int klt_hip_ctx_reset(klt_hip_ctx *c) {
 }
 
 KLT_API const char *klt_hip_last_error(klt_hip_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+KLT_API const char *klt_hip_track_kernel(klt_hip_ctx *c) { return c && c->track_kernel ? c->track_kernel : ""; }
 
 KLT_API int klt_hip_set_stream(klt_hip_ctx *c, void *stream) {
   if (!c) return -1;
@@ -1703,10 +1721,37 @@ void band_planes(const BandSpec &b, int &p0, int &p1) {
   if (p1 < p0) p1 = p0;
 }
 
+#ifdef KLT_HOST_PROF  // experiment builds: CLOCK_MONOTONIC marks through one call, printed to stderr
+struct HostMarks {
+  long t[16];
+  const char *what[16];
+  int n = 0;
+  void mark(const char *w) {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    if (n < 16) {
+      t[n] = ts.tv_sec * 1000000000L + ts.tv_nsec;
+      what[n++] = w;
+    }
+  }
+  ~HostMarks() {
+    for (int i = 1; i < n; ++i) fprintf(stderr, "hostmark %s %.2f us\n", what[i], (t[i] - t[i - 1]) * 1e-3);
+    if (n) fprintf(stderr, "hostmark enter_ns %ld\n", t[0]);
+  }
+};
+#define HMARK(w) hm_.mark(w)
+#else
+#define HMARK(w) (void)0
+#endif
+
 int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
                       const unsigned char *frames, long pitch, long stride, int nframes, int chunk, float *x,
                       float *y, int *val, int n, float *tab_x, float *tab_y, int *tab_val, long tab_stride,
                       const BandSpec *band) {
+#ifdef KLT_HOST_PROF
+  HostMarks hm_;
+#endif
+  HMARK("enter");
   if (!c || !pd || !td) return fail(c, "track_frames: null argument");
   if (!c->frames_ready) return fail(c, "track_frames: no previous pyramid (call klt_hip_frames_begin)");
   if (nframes < 0 || chunk < 1 || n < 0) return fail(c, "track_frames: bad nframes/chunk/n");
@@ -1725,7 +1770,9 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
                   pd->nrows, pd->nlevels, p0.w, p0.h, nl);
   }
   if (nframes == 0) return 0;
+  HMARK("checks");
   if (use_device(c)) return -1;
+  HMARK("set_device");
   if (!c->pstream) {
     HIPCHK(c, hipStreamCreateWithFlags(&c->pstream, hipStreamNonBlocking));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
@@ -1755,6 +1802,7 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
       chunk = fit;
     }
   }
+  HMARK("budget");
   c->chunk_used = chunk;
   const int F = chunk < nframes ? chunk : nframes;
   // banks hold `chunk` frames whatever this call's length, so a short first
@@ -1777,7 +1825,12 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
   }
   // band calls always use both streams: the next chunk's band pyramids are
   // built on the pyramid stream while this chunk is tracked and exchanged
-  const bool serial = band ? false : c->serial_frames != 0;
+  // A call that fits one chunk has nothing to overlap (its one pyramid build
+  // must finish before its tracker starts), so it stays on the tracking
+  // stream: the cross-queue event hand-off would only add its latency
+  // (~12 us measured between k_pyr_l1's end and k_track7's start).  The next
+  // call's pyramid stream still starts behind it (ev_start below).
+  const bool serial = band ? false : (c->serial_frames != 0 || nframes <= chunk);
   // the pyramid stream starts behind everything already queued on the tracking stream
   if (!serial) {
     HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
@@ -1805,7 +1858,9 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     // serial, ahead of the build), so the sort is off the chain
     TrkFramesArgs b;
     memset(&b, 0, sizeof b);
+    HMARK("chunk_top");
     if (n > 0 && order_features(c, c->stream, pd->nrows, y, val, n, Fc, band ? band->own : nullptr, b)) return -1;
+    HMARK("order");
     const bool prebuilt = band && c->pre.bank == bi && c->pre.src == src && c->pre.F == Fc &&
                           c->pre.stride == stride && c->pre.row_lo == band->row_lo && c->pre.row_hi == band->row_hi &&
                           c->pre.il == bil;
@@ -1827,6 +1882,7 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
           if (copy_level(c, level_view(c->slot[kScratchSlot].lv[l]), K.lv[l], f, ps)) return -1;
       }
     }
+    HMARK("pyramids");
     if (!serial) {
       if (!prebuilt) HIPCHK(c, hipEventRecord(c->ev_bbuilt[bi], ps));
       HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_bbuilt[bi], 0));
@@ -1845,6 +1901,7 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     }
     if (n > 0 && track_frames_launch(c, c->stream, td, a, b, x, y, val, n, band ? band->own : nullptr, true))
       return -1;
+    HMARK("track");
     if (!serial && c->prev.bank >= 0) HIPCHK(c, hipEventRecord(c->ev_bfree[c->prev.bank], c->stream));
     c->prev = PrevRef{bi, Fc - 1};
   }

@@ -608,7 +608,7 @@ static int oob_threshold(int n) {
 }
 
 hipError_t launch_track7(hipStream_t st, bool band, const TrkArgs &a_in, const TrkFramesArgs &b, float *x, float *y,
-                         int *v, int n) {
+                         int *v, int n, const char **name) {
   TrkArgs a = a_in;
   for (int l = 0; l < KLT_HIP_MAX_LEVELS; ++l) {
     a.oobx[l] = oob_threshold(a.B[l].w);
@@ -619,6 +619,15 @@ hipError_t launch_track7(hipStream_t st, bool band, const TrkArgs &a_in, const T
   // band: escape checks (klt_hip_track_frames_band); aos: interleaved levels
   // (interleaved levels are the fused path's, always two levels deep)
   const bool two = KLT_T7_NL2 && a.nlev == 2;
+  // the instance's name as rocprofv3 reports it (bench.py matches PMC summaries on it)
+  if (name)
+    *name = a.fast ? (band ? "kltdev::k_track7<true, true, 2, true>" : "kltdev::k_track7<false, true, 2, true>")
+            : band && a.aos && two ? "kltdev::k_track7<true, true, 2, false>"
+            : a.aos && two         ? "kltdev::k_track7<false, true, 2, false>"
+            : band && a.aos        ? "kltdev::k_track7<true, true, 0, false>"
+            : band                 ? "kltdev::k_track7<true, false, 0, false>"
+            : a.aos                ? "kltdev::k_track7<false, true, 0, false>"
+                                   : "kltdev::k_track7<false, false, 0, false>";
   if (a.fast) {  // KLT_HIP_FAST: the runtime sends only interleaved two-level pyramids here
     if (band)
       hipLaunchKernelGGL((k_track7<true, true, 2, true>), dim3(grid), dim3(kBlock), 0, st, a, b, x, y, v, n);

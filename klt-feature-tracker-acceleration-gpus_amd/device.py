@@ -54,6 +54,7 @@ DEVICE_PROTOS = {
     "klt_hip_ctx_create": (V, [C.c_int]),
     "klt_hip_ctx_destroy": (None, [V]),
     "klt_hip_last_error": (C.c_char_p, [V]),
+    "klt_hip_track_kernel": (C.c_char_p, [V]),
     "klt_hip_set_stream": (C.c_int, [V, V]),
     "klt_hip_get_stream": (V, [V]),
     "klt_hip_sync": (C.c_int, [V]),
