@@ -208,7 +208,7 @@ int klt_hip_pyramid_path(klt_hip_ctx *ctx, int slot);
 int klt_hip_level_dims(klt_hip_ctx *ctx, int slot, int level, int *ncols, int *nrows);
 /* synchronous copy of one level plane (which: 0 img, 1 gradx, 2 grady) */
 int klt_hip_download_level(klt_hip_ctx *ctx, int slot, int level, int which, float *host);
-/* 1 if the level is stored interleaved ({img, gradx, grady} per pixel: the
+/* 1 if the level is stored interleaved ({gradx, grady, img} per pixel: the
    fused default-parameter pyramid, the layout k_track7 reads), 0 if as three
    planes (the generic path), -1 for a bad slot/level */
 int klt_hip_level_interleaved(klt_hip_ctx *ctx, int slot, int level);

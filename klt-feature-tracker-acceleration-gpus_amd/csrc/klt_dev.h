@@ -69,6 +69,13 @@ __host__ __device__ __forceinline__ long hs_size(int W1, int H) {
   return (long)((W1 + kHsSlab - 1) / kHsSlab) * kHsSlab * H;
 }
 
+// An interleaved level stores one 12-byte record per pixel, {gx, gy, img}:
+// the gradient pair first, so that a kernel computing (gx, gy) as one packed
+// f32 pair writes it and the image value with one 12-byte store from three
+// consecutive registers (the pair is even-aligned), and a wave writes 64
+// consecutive records as one contiguous 768-byte run.
+constexpr int kRecGx = 0, kRecGy = 1, kRecImg = 2, kRec = 3;
+
 // tile geometry the runtime needs for grids and band bookkeeping
 namespace geom {
 constexpr int L0_TW = 64, L0_TH = 32;  // k_pyr_l0 tile (level-0 pixels)
@@ -84,7 +91,7 @@ inline unsigned blocks_for(long n) { return (unsigned)((n + kBlock - 1) / kBlock
 // tracker arguments (track.hip)
 // ---------------------------------------------------------------------------
 struct TrkLevel {
-  const float *img, *gx, *gy;  // il: img is the interleaved base ({img, gx, gy} per pixel), gx/gy null
+  const float *img, *gx, *gy;  // il: img is the interleaved base ({gx, gy, img} per pixel), gx/gy null
   int w, h;
   int vlo = 0, vhi = 1 << 30;  // rows that hold valid data (a band-built pyramid: fewer)
   int il = 0;
@@ -104,7 +111,7 @@ struct TrkArgs {
   int merge_res;     // 1: defer the finest level's residue into the next frame's first pass
   int *escape;       // band mode: set when a window needs rows outside [vlo, vhi)
   int prio;          // 1: tracker waves raise their issue priority (s_setprio 3) over concurrent pyramid waves
-  int aos;           // 1 (k_track7): a level's img is {img, gx, gy} interleaved per pixel (gx/gy unused)
+  int aos;           // 1 (k_track7): a level's img is {gx, gy, img} interleaved per pixel (gx/gy unused)
   int fast;          // 1 (k_track7): KLT_HIP_FAST window sums (DPP tree), interleaved two-level pyramids only
   // k_track7 (set by launch_track7): per level, the bit pattern of the smallest
   // float x >= 3 with (float)w - (x + 3) < 1.001f (ooby: the same for h), so the
@@ -157,7 +164,7 @@ hipError_t launch_pyr_l0(hipStream_t st, const uint8_t *src, int pitch, long str
                          int vec_u8, int vec_out, float *img, float *gx, float *gy, float *hs, int W1, int do_hs,
                          long fs0, long fsh, int F, int ty0, int ty1, int py0 = 0, int py1 = 1 << 30, int il = 0);
 // k_pyr_l1 over F frames, level-1 tile rows [ty0, ty1)
-// il != 0 (both): the planes interleaved per pixel, {img, gx, gy} at img + 3*(y*w + x); gx/gy unused
+// il != 0 (both): the planes interleaved per pixel, {gx, gy, img} at img + 3*(y*w + x); gx/gy unused
 hipError_t launch_pyr_l1(hipStream_t st, const float *hs, int W1, int H, int H1, const DefTaps &T, int vec,
                          float *img1, float *gx1, float *gy1, long fsh, long fs1, int F, int ty0, int ty1, int il = 0);
 // generic one-pass kernels (any sigma / levels / subsampling)

@@ -133,8 +133,8 @@ __device__ unsigned long long *g_pyr_prof;
 
 // Edge tiles (INT false) clamp their loads and apply the zero-border rules per
 // element; interior tiles (~90 % at 1080p, 94 % at 4K) need neither.
-// IL: the level's planes interleaved per pixel, {img, gx, gy} (12 bytes) at
-// img0 + 3*(y*W + x) -- written in E, where img0 is still in LDS; gx0/gy0 unused
+// IL: the level's planes interleaved per pixel, {gx, gy, img} (12 bytes, klt_dev.h)
+// at img0 + 3*(y*W + x) -- written in E, where img0 is still in LDS; gx0/gy0 unused
 template <bool INT, bool IL>
 __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8_t *__restrict__ src, int spitch,
                                             int W, int H, const DefTaps &T, int vec_u8,
@@ -360,11 +360,12 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
       const int y = R0 + 4 * b + rr, x = C0 + 2 * g;
       if (IL) {
         const f2 iv = *reinterpret_cast<const f2 *>(im + (4 * b + rr + RG) * PI + 8 + 2 * g);
+        static_assert(kRecGx == 0 && kRecGy == 1 && kRecImg == 2, "record layout");
         if (INT) {
           float *o = img0 + 3u * (unsigned)(y * W + x);
-          st2_out(o, f2{iv.x, ax.x});
-          st2_out(o + 2, f2{ay.x, iv.y});
-          st2_out(o + 4, f2{ax.y, ay.y});
+          st2_out(o, f2{ax.x, ay.x});
+          st2_out(o + 2, f2{iv.x, ax.y});
+          st2_out(o + 4, f2{ay.y, iv.y});
         } else {
           if (y >= H || x >= W) continue;
           if (!(y >= RG && y < H - RG)) {
@@ -372,13 +373,13 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
             ay = ax;
           }
           float *o = img0 + 3u * (unsigned)(y * W + x);
-          o[0] = iv.x;
-          o[1] = ax.x;
-          o[2] = ay.x;
+          o[kRecImg] = iv.x;
+          o[kRecGx] = ax.x;
+          o[kRecGy] = ay.x;
           if (x + 1 < W) {
-            o[3] = iv.y;
-            o[4] = ax.y;
-            o[5] = ay.y;
+            o[3 + kRecImg] = iv.y;
+            o[3 + kRecGx] = ax.y;
+            o[3 + kRecGy] = ay.y;
           }
         }
       } else if (INT) {
@@ -590,9 +591,10 @@ __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs,
       // 16-byte pieces (a per-pixel triple stride would split them 3 ways)
       const f4 iv = ld4(im + (r + RG) * JW + 4 + 4 * g);
       float *o = stg + r * (3 * TW) + 12 * g;
-      st4(o, f4{iv.x, ax.x, ay.x, iv.y});
-      st4(o + 4, f4{ax.y, ay.y, iv.z, ax.z});
-      st4(o + 8, f4{ay.z, iv.w, ax.w, ay.w});
+      static_assert(kRecGx == 0 && kRecGy == 1 && kRecImg == 2, "record layout");
+      st4(o, f4{ax.x, ay.x, iv.x, ax.y});
+      st4(o + 4, f4{ay.y, iv.y, ax.z, ay.z});
+      st4(o + 8, f4{iv.z, ax.w, ay.w, iv.w});
       continue;
     }
     float *px = gx1 + (unsigned)(Y * W1 + X);
@@ -684,7 +686,7 @@ __device__ __forceinline__ int x86_ftoi(float v) {
   return (int)v;
 }
 
-// gx/gy: the gradient planes, or an interleaved level's gx/gy (base + 1, +2) with ps = 3
+// gx/gy: the gradient planes, or an interleaved level's gx/gy (base + kRecGx, + kRecGy) with ps = 3
 __global__ __launch_bounds__(kBlock) void k_min_eigen(const float *__restrict__ gx,
                                                       const float *__restrict__ gy, int W, int ps, int bx,
                                                       int by, int step, int nx, int ny, int hw, int hh,
@@ -722,15 +724,15 @@ __global__ __launch_bounds__(kBlock) void k_synth(unsigned long long seed, int t
   out[(long)blockIdx.y * fstride + (long)y * pitch + x] = klt_synth_pixel(seed, t, x, row0 + y);
 }
 
-// an interleaved level ({img, gx, gy} per pixel) as three planes, for the
-// kernels that read planes (the generic tracker, the affine check)
+// an interleaved level ({gx, gy, img} per pixel, klt_dev.h) as three planes,
+// for the kernels that read planes (the generic tracker, the affine check)
 __global__ __launch_bounds__(kBlock) void k_from_il(const float *__restrict__ il, float *__restrict__ img,
                                                     float *__restrict__ gx, float *__restrict__ gy, long n) {
   const long i = (long)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
-  img[i] = il[3 * i];
-  gx[i] = il[3 * i + 1];
-  gy[i] = il[3 * i + 2];
+  img[i] = il[kRec * i + kRecImg];
+  gx[i] = il[kRec * i + kRecGx];
+  gy[i] = il[kRec * i + kRecGy];
 }
 
 // n 32-bit words from src to dst (16-byte aligned), 16 bytes per thread; one

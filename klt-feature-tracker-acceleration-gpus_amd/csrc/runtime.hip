@@ -30,7 +30,7 @@ using namespace kltdev;
 // host side
 // ===========================================================================
 // A level's storage is one block of 3 * cap floats, img | gx | gy.  Built by
-// the fused kernels it holds the level interleaved (il: {img, gx, gy} per
+// the fused kernels it holds the level interleaved (il: {gx, gy, img} per
 // pixel from img on, the form the default tracker reads); built by the
 // generic one-pass kernels it holds the three planes at img, gx and gy.
 struct Level {
@@ -2126,7 +2126,7 @@ KLT_API int klt_hip_min_eigen(klt_hip_ctx *c, int s, const klt_hip_select_desc *
   if (grow(c, &c->d_eig, &c->eig_cap, (size_t)np)) return -1;
   {
     TimedScope ts(c, T_EIG, c->stream);
-    if (launched(c, "k_min_eigen", launch_min_eigen(c->stream, L.il ? L.img + 1 : L.gx, L.il ? L.img + 2 : L.gy,
+    if (launched(c, "k_min_eigen", launch_min_eigen(c->stream, L.il ? L.img + kRecGx : L.gx, L.il ? L.img + kRecGy : L.gy,
                                                     L.w, L.il ? 3 : 1, bx, by, step, gx, gy, hw, hh, c->d_eig)))
       return -1;
   }
@@ -2143,7 +2143,7 @@ static int eigen_to_dev(klt_hip_ctx *c, int s, const klt_hip_select_desc *d, int
   const Level &L = c->slot[s].lv[0];
   if (grow(c, &c->d_eig, &c->eig_cap, (size_t)np)) return -1;
   TimedScope ts(c, T_EIG, c->stream);
-  return launched(c, "k_min_eigen", launch_min_eigen(c->stream, L.il ? L.img + 1 : L.gx, L.il ? L.img + 2 : L.gy,
+  return launched(c, "k_min_eigen", launch_min_eigen(c->stream, L.il ? L.img + kRecGx : L.gx, L.il ? L.img + kRecGy : L.gy,
                                                      L.w, L.il ? 3 : 1, d->borderx, d->bordery,
                                                      d->nSkippedPixels + 1, *nx, *ny, d->window_width / 2,
                                                      d->window_height / 2, c->d_eig));
@@ -2236,7 +2236,7 @@ KLT_API int klt_hip_min_eigen_rows(klt_hip_ctx *c, const klt_hip_select_desc *d,
   if (ylo < L.vlo || (yhi > L.vhi && L.vhi < L.h)) return 1;
   if (use_device(c)) return -1;
   TimedScope ts(c, T_EIG, c->stream);
-  return launched(c, "k_min_eigen", launch_min_eigen(c->stream, L.il ? L.img + 1 : L.gx, L.il ? L.img + 2 : L.gy,
+  return launched(c, "k_min_eigen", launch_min_eigen(c->stream, L.il ? L.img + kRecGx : L.gx, L.il ? L.img + kRecGy : L.gy,
                                                      L.w, L.il ? 3 : 1, bx, by + j0 * step, step, gx, j1 - j0, hw,
                                                      hh, dev_map + (long)j0 * gx));
 }

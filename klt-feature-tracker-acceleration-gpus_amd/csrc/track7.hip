@@ -10,7 +10,7 @@
 // the code on the chain that one wave walks for each Newton pass:
 //   * lane p < 49 owns window pixel p (row-major, the reference's order) and
 //     gathers its four bilinear corners itself: from a level stored
-//     interleaved ({img, gx, gy} per pixel, as the fused pyramid kernels
+//     interleaved ({gx, gy, img} per pixel, as the fused pyramid kernels
 //     write it) one 24-byte run per row for all three planes, from planes
 //     two 8-byte loads per plane:
 //     no lane shuffles and no patch-fit test, so there is no fallback path;
@@ -107,7 +107,7 @@ __device__ __forceinline__ Quad quad(const float *P, const Pix &p, unsigned rowb
   return q;
 }
 
-// interleaved levels ({img, gx, gy} per pixel, 12 bytes): one 24-byte run per
+// interleaved levels ({gx, gy, img} per pixel, 12 bytes): one 24-byte run per
 // row holds both corners of all three planes
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
 typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
@@ -120,13 +120,15 @@ __device__ __forceinline__ Tri tri(const float *P, const Pix &p, unsigned rowb) 
   const unsigned o0 = p.px * 12u, o1 = o0 + rowb;
   const f4u a0 = *reinterpret_cast<const f4u *>(base + o0), b0 = *reinterpret_cast<const f4u *>(base + o1);
   const f2u a1 = *reinterpret_cast<const f2u *>(base + o0 + 16), b1 = *reinterpret_cast<const f2u *>(base + o1 + 16);
+  // records {gx, gy, img} (klt_dev.h): a0 = gx0 gy0 img0 gx1, a1 = gy1 img1
+  static_assert(kRecGx == 0 && kRecGy == 1 && kRecImg == 2, "record layout");
   Tri t;
-  t.i.r0 = make_float2(a0.x, a0.w);
-  t.i.r1 = make_float2(b0.x, b0.w);
-  t.x.r0 = make_float2(a0.y, a1.x);
-  t.x.r1 = make_float2(b0.y, b1.x);
-  t.y.r0 = make_float2(a0.z, a1.y);
-  t.y.r1 = make_float2(b0.z, b1.y);
+  t.i.r0 = make_float2(a0.z, a1.y);
+  t.i.r1 = make_float2(b0.z, b1.y);
+  t.x.r0 = make_float2(a0.x, a0.w);
+  t.x.r1 = make_float2(b0.x, b0.w);
+  t.y.r0 = make_float2(a0.y, a1.x);
+  t.y.r1 = make_float2(b0.y, b1.x);
   return t;
 }
 // img alone from an interleaved level
@@ -135,8 +137,8 @@ __device__ __forceinline__ Quad quad_i(const float *P, const Pix &p, unsigned ro
   const float *b = reinterpret_cast<const float *>(reinterpret_cast<const char *>(P) + o0);
   const float *c = reinterpret_cast<const float *>(reinterpret_cast<const char *>(P) + o1);
   Quad q;
-  q.r0 = make_float2(b[0], b[3]);
-  q.r1 = make_float2(c[0], c[3]);
+  q.r0 = make_float2(b[kRecImg], b[kRec + kRecImg]);
+  q.r1 = make_float2(c[kRecImg], c[kRec + kRecImg]);
   return q;
 }
 

@@ -122,7 +122,7 @@ def test_selection_images_no_presmoothing(gpu, oracle):
 
 def test_level_layout_api(gpu):
     """klt_hip_level_interleaved / klt_hip_level_ptr: fused levels are one
-    {img, gx, gy} record per pixel at the base (gx/gy queries return NULL),
+    {gx, gy, img} record per pixel at the base (gx/gy queries return NULL),
     generic levels are three planes; both de-interleave to the same planes."""
     import ctypes as C
     h, w = 67, 129
@@ -142,6 +142,6 @@ def test_level_layout_api(gpu):
         rec = np.empty((lh, lw, 3), np.float32)
         check(lib, ctx, lib.klt_hip_sync(ctx), "sync")
         check(lib, ctx, lib.klt_hip_memcpy(ctx, rec.ctypes.data, C.c_void_p(base), rec.nbytes, 2), "d2h")
-        for k in range(3):
-            assert np.array_equal(bits(rec[:, :, k]), bits(want[lv][k])), (lv, k)
+        for k, plane in enumerate((1, 2, 0)):  # record {gx, gy, img} (klt_dev.h kRec*)
+            assert np.array_equal(bits(rec[:, :, k]), bits(want[lv][plane])), (lv, k)
     assert lib.klt_hip_level_interleaved(ctx, 0, 5) == -1
