@@ -23,6 +23,7 @@
 #pragma clang fp contract(off)
 
 #include <math.h>
+#include <stdlib.h>
 
 #include "klt_dev.h"
 #include "klt_synth.h"
@@ -44,6 +45,8 @@ __device__ __forceinline__ void st4(float *p, f4 v) { *reinterpret_cast<f4 *>(p)
 // level-0 HBM stores are nontemporal (measured 1-2 % faster than plain stores)
 __device__ __forceinline__ void st4_out(float *p, f4 v) { __builtin_nontemporal_store(v, reinterpret_cast<f4 *>(p)); }
 __device__ __forceinline__ void st2_out(float *p, f2 v) { __builtin_nontemporal_store(v, reinterpret_cast<f2 *>(p)); }
+typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
+__device__ __forceinline__ void st3_out(float *p, f3u v) { __builtin_nontemporal_store(v, reinterpret_cast<f3u *>(p)); }
 
 // acc[i] += v[i + off] * k for 4 lanes, as two packed-f32 pairs
 __device__ __forceinline__ void mac4(f4 &acc, const float *v, float k) {
@@ -94,7 +97,7 @@ constexpr int IHB = (IH + 3) / 4;             // 4-row blocks of img0 computed
 // LDS pitches (floats) chosen with tools/lds_banks.py so that the 16-lane
 // groups of each ds_read_b128 hit (nearly) distinct bank slots; a few bank
 // conflicts were traded for a 4th workgroup per CU
-constexpr int PT = 88, PI = 92, PX = TW;
+constexpr int PT = 88, PI = 92, PX = TW, PXY = 2 * TW;
 constexpr int PUB = 24;                   // staged u8 row pitch in dwords (96 bytes)
 constexpr int U_WORDS = UH * PUB;
 constexpr int REG_A = U_WORDS > IH * PI ? U_WORDS : IH * PI;  // u during A-B, then img0 during C-D
@@ -147,6 +150,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
   float *t1 = lds + REG_A;   // [UH][PT]
   float *tx = lds + REG_A;   // [IH][PX]      (after t1 is dead)
   float *ty = tx + IH * PX;
+  float *txy = lds + REG_A;  // IL: [IH][PXY], {tx, ty} per pixel (after t1 is dead)
 
   // A. u8 tile + halo -> LDS; every load issued before the first is used
   if constexpr (INT) {
@@ -284,6 +288,36 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     *reinterpret_cast<f4 *>(v) = ld4(row);
     *reinterpret_cast<f4 *>(v + 4) = ld4(row + 4);
     *reinterpret_cast<f4 *>(v + 8) = ld4(row + 8);
+    if constexpr (IL) {
+      // one (tx, ty) pair per pixel: every tap multiplies a BROADCAST input
+      // (op_sel picks either half of its register pair), so a sliding window
+      // needs no odd-offset pairs assembled by moves.  Reference order with
+      // every tap (the zero centre tap included) from the first product:
+      // 0 + t0 and t0 differ only for t0 = -0, and then only while every
+      // later term is -0 too -- but img0 >= +0 meets a positive derivative
+      // tap (m > kDC) and positive gauss taps, whose products are >= +0
+      f2 p[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) p[e] = f2{v[1 + e], v[1 + e]} * f2{T.d[0], T.g[0]};
+#pragma unroll
+      for (int m = 1; m < 7; ++m)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) p[e] += f2{v[1 + e + m], v[1 + e + m]} * f2{T.d[m], T.g[m]};
+      if (!INT) {
+        const int x = C0 + 4 * g;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (!(x + e >= RG && x + e < W - RG)) p[e] = f2{0.0f, 0.0f};
+      }
+      // {tx, ty} of pixel c in 16-byte chunk txy_chunk(c >> 1) of row r: the
+      // chunks of pixels 4g.. and 4g+2.. swap places for g % 8 >= 4, so that
+      // each 8-lane group of a ds_write_b128 fills 8 distinct bank quads
+      const int sw = (g >> 2) & 1;
+      float *o = txy + r * PXY + 8 * g;
+      st4(o + 4 * sw, f4{p[0].x, p[0].y, p[1].x, p[1].y});
+      st4(o + 4 - 4 * sw, f4{p[2].x, p[2].y, p[3].x, p[3].y});
+      continue;
+    }
     // ay: img0 >= +0 and gauss taps > 0, so every term is >= +0 and the +0
     // start can be left out (mul4); ax has signed taps and keeps it
     f4 ax = {0.0f, 0.0f, 0.0f, 0.0f}, ay = mul4(v + 1, T.g[0]);
@@ -339,6 +373,49 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
   __syncthreads();
   PYR_STAMP(4)
 
+  // E (IL). columns passes of both gradients as one (gx, gy) pair per pixel,
+  //    from the {tx, ty} pairs: column c = lane, tile rows 8w..8w+7 per thread
+  //    (14 pair rows read for 8 outputs); zero unless RG <= y < H-RG.  Each
+  //    output is one 12-byte {gx, gy, img} record from three consecutive
+  //    registers, and a wave's 64 lanes write 64 consecutive records of a row:
+  //    one contiguous 768-byte run per store instruction, whole lines
+  if constexpr (IL) {
+    if (!planes) return;
+    static_assert(kRecGx == 0 && kRecGy == 1 && kRecImg == 2, "record layout");
+    static_assert(TW == kWave && TH == 8 * (kBlock / kWave), "E: a wave per 8 rows x 64 columns");
+    const int c = tid & (kWave - 1), w8 = __builtin_amdgcn_readfirstlane(8 * (tid / kWave));  // wave-uniform
+    const int cq = 4 * ((c >> 1) ^ ((c >> 4) & 1)) + 2 * (c & 1);  // D2's chunk order (conflict-free here too)
+    f2 q[14];
+#pragma unroll
+    for (int k = 0; k < 14; ++k) q[k] = *reinterpret_cast<const f2 *>(txy + (w8 + k) * PXY + cq);
+    f2 gg[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) gg[k] = f2{0.0f, 0.0f};
+#pragma unroll
+    for (int m = 0; m < 7; ++m)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) gg[k] += q[k + m] * f2{T.g[m], T.d[m]};  // gy's zero centre tap adds +-0: exact
+    const int x = C0 + c;
+    // a wave-uniform row base and 32-bit lane offsets (scalar-base addressing)
+    char *rb = reinterpret_cast<char *>(img0 + 3 * ((size_t)(R0 + w8) * W + C0));
+    const unsigned lo = 12u * (unsigned)c, rs = 12u * (unsigned)W;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int y = R0 + w8 + k;
+      const float iv = im[(w8 + k + RG) * PI + 8 + c];
+      float *o = img0 + 3u * (unsigned)(y * W + x);
+      if (INT) {
+        st3_out(reinterpret_cast<float *>(rb + (lo + k * rs)), f3u{gg[k].x, gg[k].y, iv});
+      } else {
+        if (y >= H || x >= W) continue;
+        const bool zr = !(y >= RG && y < H - RG);
+        o[kRecGx] = zr ? 0.0f : gg[k].x;
+        o[kRecGy] = zr ? 0.0f : gg[k].y;
+        o[kRecImg] = iv;
+      }
+    }
+    return;
+  }
   // E. columns passes of both gradients; zero unless RG <= y < H-RG.  4 rows x
   //    2 columns per thread from 8-byte LDS reads (10 rows read for 4 outputs)
   for (int i = planes ? tid : kBlock; i < (TH / 4) * (TW / 2); i += kBlock) {
