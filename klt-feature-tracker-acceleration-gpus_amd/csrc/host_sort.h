@@ -18,9 +18,9 @@
 namespace kltsort {
 
 // the exact partition step on a[0..n) with pivot a[n/2] swapped to the front
-// (descending order of .x)
+// (descending order of .x): the reference's _quicksort body as written
 template <class P>
-unsigned partition(P *a, unsigned n) {
+unsigned partition_hoare(P *a, unsigned n) {
   unsigned i = 0, j = n;
   std::swap(a[0], a[n / 2]);
   const auto pv = a[0].x;
@@ -36,12 +36,81 @@ unsigned partition(P *a, unsigned n) {
   return j;
 }
 
+// The same step, element for element, without its data-dependent branches.
+// partition_hoare's k-th swap exchanges the k-th left stop l_k (ascending
+// positions >= 1 with .x <= pv) with the k-th right stop r_k (descending
+// positions with .x >= pv), for as long as l_k < r_k, reading each position
+// before any swap has touched it (swaps only touch positions behind both
+// scans).  So the stops are collected here in blocks of positions, branch-free
+// (a position is written to the stop buffer and the count advances by the
+// comparison), and paired in order until a pair crosses; a block that reads
+// past the crossing point only yields stops that fail the pairing, as the
+// reference's capped scans would stop there.  The pivot's slot is then the
+// reference's last j: scanning down from the last swapped right stop, the
+// first position whose CURRENT value is >= pv (a[0], the pivot, at worst).
+// Random keys make the reference's branches mispredict about every other
+// element; this runs ~3x faster on them (tools/hostcheck/sortbench.cpp).
+template <class P>
+unsigned partition(P *a, unsigned n) {
+  if (n < 16) return partition_hoare(a, n);
+  std::swap(a[0], a[n / 2]);
+  const auto pv = a[0].x;
+  constexpr unsigned B = 64;
+  unsigned L[B], R[B];
+  unsigned nl = 0, sl = 0, nr = 0, sr = 0;
+  unsigned lp = 1, rp = n - 1;  // next positions to scan: up from lp, down from rp
+  unsigned last_r = n;          // the last swapped right stop (n: none)
+  for (;;) {
+    if (sl == nl) {
+      if (lp > n - 1) break;  // no further left stop: the reference's i runs into j
+      nl = sl = 0;
+      const unsigned e = lp + B - 1 < n - 1 ? lp + B - 1 : n - 1;
+      for (unsigned p = lp; p <= e; ++p) {
+        L[nl] = p;
+        nl += a[p].x <= pv;
+      }
+      lp = e + 1;
+      continue;
+    }
+    if (sr == nr) {
+      if (rp < 1) break;  // no further right stop above the pivot
+      nr = sr = 0;
+      const unsigned e = rp >= B ? rp - B + 1 : 1;
+      for (unsigned p = rp + 1; p-- > e;) {
+        R[nr] = p;
+        nr += a[p].x >= pv;
+      }
+      rp = e - 1;
+      continue;
+    }
+    const unsigned l = L[sl], r = R[sr];
+    if (l >= r) break;
+    std::swap(a[l], a[r]);
+    ++sl;
+    ++sr;
+    last_r = r;
+  }
+  unsigned j = last_r;
+  do --j;
+  while (a[j].x < pv);
+  std::swap(a[j], a[0]);
+  return j;
+}
+
 // Persistent workers, shared by every caller in the process (a REPLACE sorts a
 // dozen segments; creating a thread per split cost more than many of the
 // splits).  Tasks never wait on other tasks: a task hands its right part to
-// the queue and goes on with its left part, and the caller of sort() drains
-// the queue beside the workers until its own count of unfinished tasks is
-// zero, so no wait can deadlock.
+// the queue and goes on with its left part, and the caller of sort() works
+// through its OWN queued tasks beside the workers until its count of
+// unfinished tasks is zero, so no wait can deadlock and one caller's sort never
+// runs another's tasks on its thread.  While any sort is in progress the idle
+// workers spin on the queue instead of sleeping, so a queued half starts
+// within a microsecond or so rather than after a futex wake-up (the wake-ups
+// cost more than the splits they were waking for); between sorts they sleep.
+// The pool grows to the largest worker count asked for and lives until the
+// process exits: its detached workers are never joined, so the library that
+// holds it must not be unloaded (dlclose) while the process goes on
+// (INTEGRATION.md).
 template <class P>
 struct Pool {
   struct Task {
@@ -54,32 +123,44 @@ struct Pool {
   std::mutex m;
   std::condition_variable cv, done;
   std::deque<Task> q;
+  std::atomic<int> qn{0};    // tasks queued (read without the lock by spinning workers)
+  std::atomic<int> hot{0};   // sorts in progress
+  int nworkers = 0;
 
-  // never destroyed: the workers stay blocked on cv until the process ends
   static Pool &get(int workers) {
-    static Pool *p = new Pool(workers);
+    static Pool *p = new Pool();  // never destroyed (above)
+    p->grow(workers);
     return *p;
   }
-  explicit Pool(int workers) {
-    for (int i = 0; i < workers; ++i)
-      std::thread([this] {
-        for (;;) {
-          Task t;
-          {
-            std::unique_lock<std::mutex> lk(m);
-            cv.wait(lk, [this] { return !q.empty(); });
-            t = q.front();
-            q.pop_front();
-          }
-          run(t);
-        }
-      }).detach();
+  void grow(int workers) {
+    std::lock_guard<std::mutex> lk(m);
+    for (; nworkers < workers; ++nworkers) std::thread([this] { work(); }).detach();
+  }
+  void work() {
+    for (;;) {
+      while (hot.load(std::memory_order_acquire) > 0 && qn.load(std::memory_order_relaxed) == 0) {
+#if defined(__x86_64__) || defined(__i386__)
+        __builtin_ia32_pause();
+#endif
+      }
+      Task t;
+      {
+        std::unique_lock<std::mutex> lk(m);
+        cv.wait(lk, [this] { return !q.empty() || hot.load(std::memory_order_relaxed) > 0; });
+        if (q.empty()) continue;
+        t = q.front();
+        q.pop_front();
+        qn.fetch_sub(1, std::memory_order_relaxed);
+      }
+      run(t);
+    }
   }
   void submit(const Task &t) {
     t.pending->fetch_add(1, std::memory_order_relaxed);
     {
       std::lock_guard<std::mutex> lk(m);
       q.push_back(t);
+      qn.fetch_add(1, std::memory_order_release);
     }
     cv.notify_one();
   }
@@ -124,13 +205,21 @@ struct Pool {
   // sort a[0..n) with up to 2^par tasks; returns when all of them are done
   void sort(P *a, unsigned n, int par, unsigned par_min) {
     std::atomic<int> pending{1};
+    const bool spin = par > 0 && n >= 2 * par_min;  // tasks will be queued: keep the workers awake meanwhile
+    if (spin) {
+      hot.fetch_add(1, std::memory_order_release);
+      { std::lock_guard<std::mutex> lk(m); }
+      cv.notify_all();
+    }
     run(Task{a, n, par, par_min, &pending});
     std::unique_lock<std::mutex> lk(m);
     for (;;) {
-      if (pending.load(std::memory_order_acquire) == 0) return;
-      if (!q.empty()) {  // help with a queued task (of any caller) rather than sleep
-        Task t = q.front();
-        q.pop_front();
+      if (pending.load(std::memory_order_acquire) == 0) break;
+      auto it = std::find_if(q.begin(), q.end(), [&](const Task &t) { return t.pending == &pending; });
+      if (it != q.end()) {  // help with one of this sort's own queued tasks rather than sleep
+        Task t = *it;
+        q.erase(it);
+        qn.fetch_sub(1, std::memory_order_relaxed);
         lk.unlock();
         run(t);
         lk.lock();
@@ -138,6 +227,8 @@ struct Pool {
       }
       done.wait(lk);
     }
+    lk.unlock();
+    if (spin) hot.fetch_sub(1, std::memory_order_release);
   }
 };
 

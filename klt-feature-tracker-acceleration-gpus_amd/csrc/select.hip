@@ -68,6 +68,7 @@ struct SelState {
   int totL, totR;  // left / right stops of the current step
   int nstack;      // segments pushed (start, len), in push order
   int stack[2 * kSelStack];
+  int2 pivot[kSelStack];  // stack entries of length -1 are a split's pivot, this element: no download
 };
 
 __device__ __forceinline__ void swap2(int2 *a, int i, int j) {
@@ -286,7 +287,8 @@ __global__ __launch_bounds__(kSelThreads) void k_sel_swap(SelState *s, int2 *__r
     }
     if (ns < kSelStack) {
       s->stack[2 * ns] = st + jf;
-      s->stack[2 * ns + 1] = 1;
+      s->stack[2 * ns + 1] = -1;  // one element, the pivot: its value rides along in pivot[]
+      s->pivot[ns] = kv[st + jf];
       ++ns;
     }
     s->nstack = ns;
@@ -312,6 +314,7 @@ struct SelEngine {
   float *d_fx = nullptr, *d_fy = nullptr;
   int *d_fv = nullptr;
   size_t fx_cap = 0, fy_cap = 0, fv_cap = 0;
+  hipEvent_t ev_dl = nullptr, ev_ref = nullptr;  // a segment download done / a look-ahead refinement done
   int threshold = kSelDefaultThreshold;  // segments at most this long go to the host
   // statistics of the last run
   long downloaded = 0, device_steps = 0, visited = 0;
@@ -320,6 +323,14 @@ struct SelEngine {
 
 double now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// KLT_SEL_TRACE=1: one stderr line per device refinement, segment download and
+// host sort of every selection (what, size, microseconds) -- a timeline of the
+// engine for tuning; read once
+bool sel_trace() {
+  static const bool t = getenv("KLT_SEL_TRACE") && atoi(getenv("KLT_SEL_TRACE")) != 0;
+  return t;
 }
 
 namespace {
@@ -361,55 +372,72 @@ int sort_depth() {
   return d;
 }
 
-// split device segment g on the device until its leftmost part is at most the
-// threshold; the resulting segments are pushed onto stk (device-resident)
-int dev_refine(SelEngine *e, hipStream_t st, Seg g, std::vector<Seg> &stk, std::string *err) {
-  const double t0 = now_us();
-  struct Acc {
-    SelEngine *e;
-    double t0;
-    ~Acc() { e->us[1] += now_us() - t0; }
-  } acc{e, t0};
+// Split device segment g on the device until its leftmost part is at most the
+// threshold; the resulting segments are pushed onto stk (device-resident).
+// In two halves: refine_launch queues the partition steps and the state's
+// copy back (asynchronous: a look-ahead refinement runs while the host sorts
+// the segment before it), refine_finish waits for them and pushes the parts.
+int refine_launch(SelEngine *e, hipStream_t st, Seg g, std::string *err) {
   const int T = e->threshold;
   const int nb = (g.len + kSelBS - 1) / kSelBS;
   if (sel_grow(&e->d_cnt, &e->cnt_cap, 2 * (size_t)nb, err) || sel_grow(&e->d_off, &e->off_cap, 2 * (size_t)nb, err) ||
       sel_grow(&e->d_posL, &e->posL_cap, (size_t)g.len + 1, err) ||
       sel_grow(&e->d_posR, &e->posR_cap, (size_t)g.len + 1, err))
     return -1;
+  memset(e->h_state, 0, offsetof(SelState, stack));
+  e->h_state->start = g.start;
+  e->h_state->len = g.len;
+  SELCHK(hipMemcpyAsync(e->d_state, e->h_state, offsetof(SelState, stack), hipMemcpyHostToDevice, st));
+  // splits expected to reach the threshold, plus slack; refine_finish
+  // continues if the pivots were unlucky
+  int levels = 2;
+  for (long l = g.len; l > T; l /= 2) ++levels;
+  const int sw = (g.len / 2 + kSelThreads) / kSelThreads;
+  for (int l = 0; l < levels; ++l) {
+    hipLaunchKernelGGL(k_sel_pivot, dim3(1), dim3(1), 0, st, e->d_state, e->d_kv, T);
+    hipLaunchKernelGGL(k_sel_count, dim3(nb), dim3(kSelThreads), 0, st, e->d_state, e->d_kv, e->d_cnt);
+    hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(kSelScanThreads), 0, st, e->d_state, e->d_cnt, e->d_off);
+    hipLaunchKernelGGL(k_sel_rank, dim3(nb), dim3(kSelThreads), 0, st, e->d_state, e->d_kv, e->d_off, e->d_posL,
+                       e->d_posR);
+    hipLaunchKernelGGL(k_sel_swap, dim3(sw), dim3(kSelThreads), 0, st, e->d_state, e->d_kv, e->d_posL, e->d_posR);
+    e->device_steps++;
+  }
+  SELCHK(hipGetLastError());
+  SELCHK(hipMemcpyAsync(e->h_state, e->d_state, sizeof(SelState), hipMemcpyDeviceToHost, st));
+  SELCHK(hipEventRecord(e->ev_ref, st));
+  return 0;
+}
+
+int refine_finish(SelEngine *e, hipStream_t st, Seg g, std::vector<Seg> &stk, double t0, std::string *err) {
+  const int T = e->threshold;
   for (;;) {
-    memset(e->h_state, 0, sizeof(SelState));
-    e->h_state->start = g.start;
-    e->h_state->len = g.len;
-    SELCHK(hipMemcpyAsync(e->d_state, e->h_state, offsetof(SelState, stack), hipMemcpyHostToDevice, st));
-    // splits expected to reach the threshold, plus slack; the loop below
-    // continues if the pivots were unlucky
-    int levels = 2;
-    for (long l = g.len; l > T; l /= 2) ++levels;
-    const int sw = (g.len / 2 + kSelThreads) / kSelThreads;
-    for (int l = 0; l < levels; ++l) {
-      hipLaunchKernelGGL(k_sel_pivot, dim3(1), dim3(1), 0, st, e->d_state, e->d_kv, T);
-      hipLaunchKernelGGL(k_sel_count, dim3(nb), dim3(kSelThreads), 0, st, e->d_state, e->d_kv, e->d_cnt);
-      hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(kSelScanThreads), 0, st, e->d_state, e->d_cnt, e->d_off);
-      hipLaunchKernelGGL(k_sel_rank, dim3(nb), dim3(kSelThreads), 0, st, e->d_state, e->d_kv, e->d_off, e->d_posL,
-                         e->d_posR);
-      hipLaunchKernelGGL(k_sel_swap, dim3(sw), dim3(kSelThreads), 0, st, e->d_state, e->d_kv, e->d_posL, e->d_posR);
-      e->device_steps++;
-    }
-    SELCHK(hipGetLastError());
-    SELCHK(hipMemcpyAsync(e->h_state, e->d_state, sizeof(SelState), hipMemcpyDeviceToHost, st));
-    SELCHK(hipStreamSynchronize(st));
+    SELCHK(hipEventSynchronize(e->ev_ref));
+    if (sel_trace()) fprintf(stderr, "seltrace refine len=%d us=%.1f\n", g.len, now_us() - t0);
     const SelState &S = *e->h_state;
     if (S.nstack >= kSelStack) {
       if (err) *err = "select: device partition stack overflow";
       return -1;
     }
-    for (int k = 0; k < S.nstack; ++k) stk.push_back(Seg{S.stack[2 * k], S.stack[2 * k + 1], false});
+    for (int k = 0; k < S.nstack; ++k) {
+      const int st0 = S.stack[2 * k], len = S.stack[2 * k + 1];
+      if (len == -1) {  // a split's pivot: its element came back with the state
+        e->h_kv[st0] = S.pivot[k];
+        stk.push_back(Seg{st0, 1, true, true});
+      } else {
+        stk.push_back(Seg{st0, len, false});
+      }
+    }
     if (S.done || S.len <= T) {
       stk.push_back(Seg{S.start, S.len, false});
       return 0;
     }
     g = Seg{S.start, S.len, false};  // unlucky pivots: more steps on what is left
+    if (refine_launch(e, st, g, err)) return -1;
   }
+}
+
+int dev_refine(SelEngine *e, hipStream_t st, Seg g, std::vector<Seg> &stk, std::string *err) {
+  return refine_launch(e, st, g, err) ? -1 : refine_finish(e, st, g, stk, now_us(), err);
 }
 
 // the lazy sort: next position in sorted order, or -1 when exhausted
@@ -419,6 +447,17 @@ struct LazySort {
   std::vector<Seg> stk;
   std::string *err;
   int failed = 0;
+  // a refinement queued ahead (while the host sorts the segment before it):
+  // the segment it splits, which sits on stk (marked by its start) until popped
+  bool ahead = false;
+  int ahead_start = -1;
+  double ahead_t0 = 0.0;
+
+  // a walk that stops early may leave a look-ahead refinement in flight: its
+  // state copy into pinned memory must land before the engine is used again
+  ~LazySort() {
+    if (ahead) (void)hipEventSynchronize(e->ev_ref);
+  }
 
   long next() {
     while (!stk.empty()) {
@@ -427,7 +466,16 @@ struct LazySort {
       if (g.len <= 0) continue;
       if (!g.host) {
         if (g.len > e->threshold) {
-          if (dev_refine(e, st, g, stk, err)) {
+          const double t0 = now_us();
+          int rc;
+          if (ahead && ahead_start == g.start) {  // queued while the previous segment was sorted
+            ahead = false;
+            rc = refine_finish(e, st, g, stk, ahead_t0, err);
+          } else {
+            rc = dev_refine(e, st, g, stk, err);
+          }
+          e->us[1] += now_us() - t0;
+          if (rc) {
             failed = 1;
             return -1;
           }
@@ -436,13 +484,37 @@ struct LazySort {
         const double t0 = now_us();
         if (hipMemcpyAsync(e->h_kv + g.start, e->d_kv + g.start, sizeof(int2) * (size_t)g.len,
                            hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess) {
+            hipEventRecord(e->ev_dl, st) != hipSuccess) {
+          if (err) *err = "select: segment download failed";
+          failed = 1;
+          return -1;
+        }
+        // look ahead: the next device segment the walk will reach, if it needs
+        // splitting, is split on the device while this one is sorted here
+        if (!ahead) {
+          for (size_t k = stk.size(); k-- > 0;) {
+            const Seg &h = stk[k];
+            if (h.host || h.len <= 0) continue;
+            if (h.len > e->threshold) {
+              if (refine_launch(e, st, h, err)) {
+                failed = 1;
+                return -1;
+              }
+              ahead = true;
+              ahead_start = h.start;
+              ahead_t0 = now_us();
+            }
+            break;
+          }
+        }
+        if (hipEventSynchronize(e->ev_dl) != hipSuccess) {
           if (err) *err = "select: segment download failed";
           failed = 1;
           return -1;
         }
         e->downloaded += g.len;
         e->us[2] += now_us() - t0;
+        if (sel_trace()) fprintf(stderr, "seltrace download len=%d us=%.1f\n", g.len, now_us() - t0);
         g.host = true;
       }
       if (g.len == 1) return g.start;
@@ -454,6 +526,7 @@ struct LazySort {
         static const int workers = std::max(0, std::min((1 << depth) - 1, (int)std::thread::hardware_concurrency() - 1));
         kltsort::Pool<int2>::get(workers).sort(e->h_kv + g.start, (unsigned)g.len, depth, kSelParMin);
         e->us[2] += now_us() - t0;
+        if (sel_trace()) fprintf(stderr, "seltrace sort len=%d us=%.1f\n", g.len, now_us() - t0);
         g.sorted = true;
       }
       stk.push_back(Seg{g.start + 1, g.len - 1, true, true});
@@ -495,6 +568,8 @@ void sel_engine_destroy(SelEngine *e) {
                   (void *)e->d_state, (void *)e->d_map, (void *)e->d_fx, (void *)e->d_fy, (void *)e->d_fv})
     hipFree(p);
   if (e->h_state) hipHostFree(e->h_state);
+  if (e->ev_dl) hipEventDestroy(e->ev_dl);
+  if (e->ev_ref) hipEventDestroy(e->ev_ref);
   if (e->h_kv) hipHostFree(e->h_kv);
   delete e;
 }
@@ -515,6 +590,8 @@ static int sel_prepare(SelEngine *e, hipStream_t st, const int *dev_vals, int nx
   if (sel_grow(&e->d_kv, &e->kv_cap, n, err)) return -1;
   if (!e->d_state) SELCHK(hipMalloc((void **)&e->d_state, sizeof(SelState)));
   if (!e->h_state) SELCHK(hipHostMalloc((void **)&e->h_state, sizeof(SelState), hipHostMallocDefault));
+  if (!e->ev_dl) SELCHK(hipEventCreateWithFlags(&e->ev_dl, hipEventDisableTiming));
+  if (!e->ev_ref) SELCHK(hipEventCreateWithFlags(&e->ev_ref, hipEventDisableTiming));
   if (e->hkv_cap < n) {
     if (e->h_kv) hipHostFree(e->h_kv);
     e->h_kv = nullptr;
@@ -590,6 +667,9 @@ int sel_engine_run(SelEngine *e, hipStream_t st, const int *dev_vals, int nx, in
   }
   if (ls.failed) return -1;
   e->us[3] = now_us() - t_start;
+  if (sel_trace())
+    fprintf(stderr, "seltrace done init_us=%.1f visited=%ld downloaded=%ld total_us=%.1f\n", e->us[0], e->visited,
+            e->downloaded, e->us[3]);
   if (!filled)  // list exhausted: remaining slots become NOT_FOUND (:175-195)
     for (; k < n; ++k)
       if (overwrite_all || val[k] < 0) {

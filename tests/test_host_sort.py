@@ -7,7 +7,9 @@ sorted keys -- must equal the sequential recursion's.  This builds the header
 with g++ into a small driver and compares the pooled sort (up to 2^3 tasks,
 small par_min so every size splits) with the one-thread sort, element for
 element, on random, tie-heavy, constant and presorted inputs, including
-several callers sorting at once on the shared pool.
+several callers sorting at once on the shared pool; and the branch-free
+partition step (host_sort.h partition) with the reference's own
+(partition_hoare), array and pivot slot, on every size up to 139 and more.
 """
 from __future__ import annotations
 
@@ -37,9 +39,41 @@ static std::vector<P> make(int kind, unsigned n, unsigned seed) {
   }
   return v;
 }
+// the reference's recursion with its own partition step (partition_hoare)
+static void ref_sort(P *a, unsigned n) {
+  while (n > 1) {
+    const unsigned j = kltsort::partition_hoare(a, n);
+    ref_sort(a, j);
+    a += j + 1;
+    n -= j + 1;
+  }
+}
 int main() {
   auto &pool = kltsort::Pool<P>::get(7);
   int bad = 0, cases = 0;
+  // the branch-free partition step equals the reference's, element for element
+  for (int kind = 0; kind < 6; ++kind)
+    for (unsigned n = 1; n < 400; n += (n < 140 ? 1 : 37))
+      for (unsigned seed = 0; seed < 6; ++seed) {
+        std::vector<P> a = make(kind % 4, n, seed * 977 + n), b;
+        if (kind == 4) for (unsigned i = 0; i < n; ++i) a[i].x = (int)(i % 3);           // few distinct, periodic
+        if (kind == 5) for (unsigned i = 0; i < n; ++i) a[i].x = (int)((n - i) / 5);     // runs of ties, descending
+        b = a;
+        const unsigned ja = kltsort::partition(a.data(), n), jb = kltsort::partition_hoare(b.data(), n);
+        ++cases;
+        bool same = ja == jb;
+        for (unsigned i = 0; same && i < n; ++i) same = a[i].x == b[i].x && a[i].y == b[i].y;
+        if (!same) { ++bad; std::printf("partition mismatch kind %d n %u seed %u\n", kind, n, seed); }
+      }
+  for (int kind = 0; kind < 4; ++kind)
+    for (unsigned n : {1000u, 40000u, 100003u}) {
+      std::vector<P> a = make(kind, n, n + kind), b = a;
+      pool.sort(a.data(), n, 3, 2048);
+      ref_sort(b.data(), n);
+      ++cases;
+      for (unsigned i = 0; i < n; ++i)
+        if (a[i].x != b[i].x || a[i].y != b[i].y) { ++bad; std::printf("sort vs reference mismatch kind %d n %u\n", kind, n); break; }
+    }
   const unsigned sizes[] = {0, 1, 2, 3, 17, 255, 4096, 40000, 100003};
   for (int kind = 0; kind < 4; ++kind)
     for (unsigned n : sizes)
