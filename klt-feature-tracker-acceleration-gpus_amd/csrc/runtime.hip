@@ -173,8 +173,6 @@ struct klt_hip_ctx {
   // caller buffers registered with klt_hip_register_host (page-locked): frame
   // uploads from inside one are one DMA from the caller's pages, no staging
   std::vector<std::pair<const unsigned char *, size_t>> registered;
-  std::vector<const unsigned char *> registered_dev;  // their device-side addresses (mapped)
-  const unsigned char *u8_mapped[2] = {nullptr, nullptr};  // upload slot b reads the caller's pages directly
   // affine consistency check: stored windows (3*aff_S floats per feature) and per-call arrays
   float *d_aff_store = nullptr;
   size_t aff_store_cap = 0;
@@ -1000,8 +998,6 @@ KLT_API int klt_hip_ctx_reset(klt_hip_ctx *c) {
   c->feat_mode = 2;
   for (auto &r : c->registered) (void)hipHostUnregister(const_cast<unsigned char *>(r.first));
   c->registered.clear();
-  c->registered_dev.clear();
-  c->u8_mapped[0] = c->u8_mapped[1] = nullptr;
   if (c->sel) sel_engine_set_threshold(c->sel, kSelDefaultThreshold);
   c->bank_budget = 0;
   c->chunk_used = 0;
@@ -1068,18 +1064,14 @@ KLT_API int klt_hip_upload_frame(klt_hip_ctx *c, int buf, const unsigned char *h
     }
     c->u8_cap = n;
   }
-  c->u8_mapped[buf] = nullptr;
-  // a frame inside a registered caller buffer: one DMA straight from it, or
-  // (KLT_MAPPED_FRAMES=1, experiment) no copy at all: the level-0 kernel reads
-  // the caller's pages over the bus
+  // a frame inside a registered caller buffer: one DMA straight from it.
+  // (Letting k_pyr_l0 read the caller's mapped pages over the bus instead, no
+  // copy at all, measured slower: 120-122 against 107-108 us per registered
+  // call, tools/exp/r04q.sh.)
   for (size_t i = 0; i < c->registered.size(); ++i) {
     const auto &r = c->registered[i];
     if (host >= r.first && n <= r.second && (size_t)(host - r.first) <= r.second - n) {
-      if (c->registered_dev[i] && getenv("KLT_MAPPED_FRAMES") && atoi(getenv("KLT_MAPPED_FRAMES")) == 1) {
-        c->u8_mapped[buf] = c->registered_dev[i] + (host - r.first);
-      } else {
-        HIPCHK(c, hipMemcpyAsync(c->d_u8[buf], host, n, hipMemcpyHostToDevice, c->stream));
-      }
+      HIPCHK(c, hipMemcpyAsync(c->d_u8[buf], host, n, hipMemcpyHostToDevice, c->stream));
       HIPCHK(c, hipEventRecord(c->u8_done[buf], c->stream));
       c->u8_w[buf] = ncols;
       c->u8_h[buf] = nrows;
@@ -1136,7 +1128,7 @@ static int build_pyramid_on(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, co
     if (c->u8_w[buf] != d->ncols || c->u8_h[buf] != d->nrows)
       return fail(c, "build_pyramid: uploaded frame is %dx%d, desc %dx%d", c->u8_w[buf], c->u8_h[buf],
                   d->ncols, d->nrows);
-    src = c->u8_mapped[buf] ? c->u8_mapped[buf] : c->d_u8[buf];
+    src = c->d_u8[buf];
     pitch = d->ncols;
   }
   if (pitch < d->ncols) return fail(c, "build_pyramid: pitch %ld < ncols %d", pitch, d->ncols);
@@ -1180,10 +1172,7 @@ KLT_API int klt_hip_register_host(klt_hip_ctx *c, const void *ptr, size_t bytes)
       return fail(c, "register_host: [%p, +%zu) overlaps a registered buffer", ptr, bytes);
   if (use_device(c)) return -1;
   HIPCHK(c, hipHostRegister(const_cast<void *>(ptr), bytes, hipHostRegisterMapped));
-  void *dp = nullptr;
-  if (hipHostGetDevicePointer(&dp, const_cast<void *>(ptr), 0) != hipSuccess) dp = nullptr;
   c->registered.push_back({p, bytes});
-  c->registered_dev.push_back(static_cast<const unsigned char *>(dp));
   return 0;
 }
 
@@ -1197,8 +1186,6 @@ KLT_API int klt_hip_unregister_host(klt_hip_ctx *c, const void *ptr) {
         if (st) HIPCHK(c, hipStreamSynchronize(st));
       HIPCHK(c, hipHostUnregister(const_cast<void *>(ptr)));
       c->registered.erase(c->registered.begin() + (long)i);
-      c->registered_dev.erase(c->registered_dev.begin() + (long)i);
-      c->u8_mapped[0] = c->u8_mapped[1] = nullptr;
       return 0;
     }
   return fail(c, "unregister_host: %p is not registered", ptr);

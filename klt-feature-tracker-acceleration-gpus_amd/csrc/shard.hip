@@ -39,6 +39,7 @@ struct klt_shard {
   bool dead = false;                    // the communicator was aborted (a rank could not take part)
   int *d_map = nullptr;                 // the trackability map (replacement)
   size_t map_cap = 0;
+  int faults = 0;                       // KLT_SHARD_FAULT_* (klt_shard_inject_fault; tests)
   std::string err;
 };
 
@@ -90,7 +91,8 @@ int abort_comm(klt_shard *s, const char *what) {
 // features, which nobody tracks); the escape flag as the last element
 __global__ void k_shard_pack(const float *__restrict__ x, const float *__restrict__ y, const int *__restrict__ v,
                              const float *__restrict__ y0, const int *__restrict__ v0, float own_lo, float own_hi,
-                             int rank0, const int *__restrict__ escape, int failed, int *__restrict__ buf, int n) {
+                             int rank0, const int *__restrict__ escape, int failed, int nfail,
+                             int *__restrict__ buf, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
     const bool owned = !failed && v0[i] >= 0 && y0[i] >= own_lo && y0[i] < own_hi;  // k_band_order's test
@@ -101,7 +103,7 @@ __global__ void k_shard_pack(const float *__restrict__ x, const float *__restric
   }
   if (i == 0) {
     buf[3 * n] = escape && !failed ? *escape : 0;
-    buf[3 * n + 1] = failed;
+    buf[3 * n + 1] = nfail;
   }
 }
 
@@ -130,6 +132,7 @@ __global__ void k_shard_save(const float *__restrict__ x, const float *__restric
 }
 
 int grow_buffers(klt_shard *s, int n) {
+  if (s->faults & KLT_SHARD_FAULT_ALLOC) return sfail(s, "exchange buffers: injected allocation failure");
   if ((size_t)n <= s->cap && s->d_buf) return 0;
   hipFree(s->d_buf);
   hipFree(s->d_x0);
@@ -148,6 +151,12 @@ int grow_buffers(klt_shard *s, int n) {
   return 0;
 }
 
+// this rank's contribution to a failure count: 1 when it failed, plus one
+// phantom failed peer under KLT_SHARD_FAULT_PEER
+int fail_count(const klt_shard *s, int failed) {
+  return (failed ? 1 : 0) + ((s->faults & KLT_SHARD_FAULT_PEER) ? 1 : 0);
+}
+
 // pack this rank's results, all-reduce them with every rank's, unpack; the
 // summed escape flag lands in h_flag[0], the number of ranks that failed this
 // step (failed != 0: this one, which contributes nothing else) in h_flag[1].
@@ -157,7 +166,7 @@ int grow_buffers(klt_shard *s, int n) {
 int exchange(klt_shard *s, hipStream_t st, float *x, float *y, int *v, int n, const int *escape, int failed) {
   const int nb = (n + 255) / 256 > 0 ? (n + 255) / 256 : 1;
   hipLaunchKernelGGL(k_shard_pack, dim3(nb), dim3(256), 0, st, x, y, v, s->d_y0, s->d_v0, s->own_lo, s->own_hi,
-                     s->rank == 0 ? 1 : 0, escape, failed ? 1 : 0, s->d_buf, n);
+                     s->rank == 0 ? 1 : 0, escape, failed ? 1 : 0, fail_count(s, failed), s->d_buf, n);
   SHIP(s, hipGetLastError());
   SNCCL(s, ncclAllReduce(s->d_buf, s->d_buf, (size_t)3 * n + 2, ncclInt32, ncclSum, s->comm, st));
   SHIP(s, hipMemcpyAsync(s->h_flag, s->d_buf + (size_t)3 * n, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
@@ -172,7 +181,8 @@ int exchange(klt_shard *s, hipStream_t st, float *x, float *y, int *v, int n, co
 // one int32 all-reduce of this rank's failure flag: how many ranks failed
 int agree(klt_shard *s, hipStream_t st, int failed, int *failed_ranks) {
   int *w = s->d_buf + (size_t)3 * s->cap + 1;
-  SHIP(s, hipMemcpyAsync(w, &failed, sizeof(int), hipMemcpyHostToDevice, st));
+  const int mine = fail_count(s, failed);
+  SHIP(s, hipMemcpyAsync(w, &mine, sizeof(int), hipMemcpyHostToDevice, st));
   SNCCL(s, ncclAllReduce(w, w, 1, ncclInt32, ncclSum, s->comm, st));
   SHIP(s, hipMemcpyAsync(s->h_flag + 1, w, sizeof(int), hipMemcpyDeviceToHost, st));
   SHIP(s, hipStreamSynchronize(st));
@@ -250,6 +260,12 @@ KLT_API void klt_shard_destroy(klt_shard *s) {
   delete s;
 }
 
+KLT_API int klt_shard_inject_fault(klt_shard *s, int faults) {
+  if (!s || (faults & ~(KLT_SHARD_FAULT_LOCAL | KLT_SHARD_FAULT_PEER | KLT_SHARD_FAULT_ALLOC))) return -1;
+  s->faults = faults;
+  return 0;
+}
+
 KLT_API const char *klt_shard_last_error(klt_shard *s) { return s ? s->err.c_str() : "null shard"; }
 
 KLT_API int klt_shard_rows(const klt_shard *s, int *lo, int *hi) {
@@ -281,6 +297,7 @@ KLT_API int klt_shard_track(klt_shard *s, const klt_hip_pyr_desc *pd, const klt_
   hipLaunchKernelGGL(k_shard_save, dim3(n > 0 ? (n + 255) / 256 : 1), dim3(256), 0, st, x, y, val, s->d_x0, s->d_y0,
                      s->d_v0, escape, n);
   if (hipGetLastError() != hipSuccess) local = "chunk-start save failed";
+  if (local.empty() && (s->faults & KLT_SHARD_FAULT_LOCAL)) local = "injected local fault";
   if (local.empty() &&
       klt_hip_track_frames_band(s->ctx, pd, td, frames, pitch, stride, nframes, x, y, val, n, s->own_lo, s->own_hi,
                                 s->row_lo, s->row_hi, escape, next_frames, next_nframes))
@@ -406,6 +423,7 @@ KLT_API int klt_shard_replace(klt_shard *s, const klt_hip_pyr_desc *pd, const kl
   int nx, ny, j0, j1;
   std::string local;  // this rank's failure: it still joins the agreement below
   if (klt_hip_min_eigen_rows(s->ctx, sd, 0, 0, nullptr, &nx, &ny, &j0, &j1) < 0) local = klt_hip_last_error(s->ctx);
+  if (local.empty() && (s->faults & KLT_SHARD_FAULT_LOCAL)) local = "injected local fault";
   const size_t np = local.empty() ? (size_t)nx * ny : 0;
   if (local.empty() && np > s->map_cap) {
     hipFree(s->d_map);

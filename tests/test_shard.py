@@ -519,6 +519,74 @@ def test_c_shard_errors(gpu):
     gpu.KLTFreeTrackingContext(rk.tc)
 
 
+@pytest.mark.gpu
+def test_c_shard_failure_agreement(gpu):
+    """The failure agreement of klt_shard_track / klt_shard_replace over a real
+    one-rank RCCL communicator, driven by klt_shard_inject_fault: a local
+    failure still runs the exchange (agreement) and reports its own message;
+    a failure count from a peer (phantom) makes the call fail with "1 peer
+    rank(s) failed"; clearing the faults makes the shard work again; an
+    exchange-buffer allocation failure aborts the communicator and the shard
+    refuses every later call."""
+    from kltamd.device import SelectDesc
+    frames = synth(gpu, 91, 640, 480, 3)
+    H, W = frames[0].shape
+    dev = torch.device("cuda", 0)
+    dfr = torch.from_numpy(np.ascontiguousarray(np.stack(frames))).to(dev)
+    rk = _Rank(gpu, dfr, H, W, 1, 0, 64)
+    uid = (C.c_ubyte * 128)()
+    assert gpu.klt_shard_unique_id(uid) == 0
+    s = gpu.klt_shard_create(rk.ctx, 0, 1, uid, H, 64)
+    assert s
+    assert gpu.klt_shard_inject_fault(s, 8) == -1  # unknown fault bit
+    x, y, v = (torch.from_numpy(a).to(dev) for a in _select(gpu, frames[0], 600))
+    x0, y0, v0 = x.clone(), y.clone(), v.clone()
+    ptrs = (C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()), x.numel())
+    tc = rk.tc.contents
+    sd = SelectDesc(tc.window_width, tc.window_height, max(tc.borderx, tc.window_width // 2),
+                    max(tc.bordery, tc.window_height // 2), tc.nSkippedPixels)
+    f1 = C.c_void_p(dfr.data_ptr() + H * W)
+
+    def track():
+        x.copy_(x0), y.copy_(y0), v.copy_(v0)
+        assert gpu.klt_hip_frames_begin(rk.ctx, C.byref(rk.pd), C.c_void_p(dfr.data_ptr()), W) == 0
+        return gpu.klt_shard_track(s, C.byref(rk.pd), C.byref(rk.td), f1, W, H * W, 1, None, 0, *ptrs, None, None)
+
+    def replace():
+        return gpu.klt_shard_replace(s, C.byref(rk.pd), C.byref(sd), W, tc.mindist, tc.min_eigenvalue, *ptrs,
+                                     None, None)
+
+    def err():
+        return gpu.klt_shard_last_error(s).decode()
+
+    assert track() == 0
+    good = [t.clone() for t in (x, y, v)]
+    assert gpu.klt_shard_inject_fault(s, 1) == 0  # LOCAL
+    assert track() < 0 and err() == "shard_track: injected local fault"
+    x.copy_(good[0]), y.copy_(good[1]), v.copy_(good[2])
+    assert replace() < 0 and err() == "shard_replace: injected local fault"
+    assert torch.equal(x, good[0]) and torch.equal(v, good[2])  # no selection ran
+    assert gpu.klt_shard_inject_fault(s, 2) == 0  # PEER
+    assert track() < 0 and err() == "shard_track: 1 peer rank(s) failed this chunk"
+    x.copy_(good[0]), y.copy_(good[1]), v.copy_(good[2])
+    assert replace() < 0 and err() == "shard_replace: 1 peer rank(s) failed the trackability map"
+    assert torch.equal(x, good[0]) and torch.equal(v, good[2])
+    assert gpu.klt_shard_inject_fault(s, 3) == 0  # both: this rank's own message wins
+    assert track() < 0 and err() == "shard_track: injected local fault"
+    assert gpu.klt_shard_inject_fault(s, 0) == 0  # cleared: the communicator still works
+    assert track() == 0
+    assert all(torch.equal(a.view(torch.int32), b.view(torch.int32)) for a, b in zip((x, y, v), good))
+    assert replace() == 0
+    assert gpu.klt_shard_inject_fault(s, 4) == 0  # ALLOC: abort
+    assert track() < 0 and "communicator aborted" in err() and "injected allocation failure" in err()
+    assert gpu.klt_shard_inject_fault(s, 0) == 0
+    assert track() < 0 and err() == "shard_track: the communicator was aborted"
+    assert replace() < 0 and err() == "shard_replace: the communicator was aborted"
+    assert gpu.klt_hip_current_device() == 0
+    gpu.klt_shard_destroy(s)
+    gpu.KLTFreeTrackingContext(rk.tc)
+
+
 # ---------------------------------------------------------------------------
 # GPU: kltamd.shard.ShardedSequence itself, one thread per rank on one GPU,
 # the collectives done by a thread group (sum / copy between the ranks' tensors)
