@@ -120,10 +120,24 @@ struct Pool {
     unsigned par_min;
     std::atomic<int> *pending;
   };
+
+  static void pause() {
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_pause();
+#endif
+  }
   std::mutex m;
   std::condition_variable cv, done;
   std::deque<Task> q;
-  std::atomic<int> qn{0};    // tasks queued (read without the lock by spinning workers)
+  // Queued tasks not yet claimed.  A worker claims one by decrementing qn
+  // (compare-and-swap, no lock), then pops the queue's front under m; so only
+  // as many threads take the lock as there are tasks, not every spinning
+  // worker at once.  A thread that removes a particular task (a sort's caller
+  // helping with its own) decrements qn
+  // only if it is positive: when every queued task is already claimed, one
+  // claimant finds one task fewer, or the queue empty, and goes back to
+  // spinning.  qn never exceeds the queue's length, and no task is stranded.
+  std::atomic<int> qn{0};
   std::atomic<int> hot{0};   // sorts in progress
   int nworkers = 0;
 
@@ -136,21 +150,32 @@ struct Pool {
     std::lock_guard<std::mutex> lk(m);
     for (; nworkers < workers; ++nworkers) std::thread([this] { work(); }).detach();
   }
+  bool claim() {
+    int k = qn.load(std::memory_order_relaxed);
+    while (k > 0)
+      if (qn.compare_exchange_weak(k, k - 1, std::memory_order_acq_rel, std::memory_order_relaxed)) return true;
+    return false;
+  }
+  void unreserve_one() { claim(); }
   void work() {
     for (;;) {
-      while (hot.load(std::memory_order_acquire) > 0 && qn.load(std::memory_order_relaxed) == 0) {
-#if defined(__x86_64__) || defined(__i386__)
-        __builtin_ia32_pause();
-#endif
+      if (!claim()) {
+        if (hot.load(std::memory_order_acquire) > 0) {
+          pause();
+        } else {  // no sort in progress: sleep until a task or a sort comes
+          std::unique_lock<std::mutex> lk(m);
+          cv.wait(lk, [this] {
+            return qn.load(std::memory_order_relaxed) > 0 || hot.load(std::memory_order_relaxed) > 0;
+          });
+        }
+        continue;
       }
       Task t;
       {
-        std::unique_lock<std::mutex> lk(m);
-        cv.wait(lk, [this] { return !q.empty() || hot.load(std::memory_order_relaxed) > 0; });
-        if (q.empty()) continue;
+        std::lock_guard<std::mutex> lk(m);
+        if (q.empty()) continue;  // its task was taken by the sort it belonged to
         t = q.front();
         q.pop_front();
-        qn.fetch_sub(1, std::memory_order_relaxed);
       }
       run(t);
     }
@@ -216,16 +241,24 @@ struct Pool {
     for (;;) {
       if (pending.load(std::memory_order_acquire) == 0) break;
       auto it = std::find_if(q.begin(), q.end(), [&](const Task &t) { return t.pending == &pending; });
-      if (it != q.end()) {  // help with one of this sort's own queued tasks rather than sleep
+      if (it != q.end()) {  // help with one of this sort's own queued tasks rather than wait
         Task t = *it;
         q.erase(it);
-        qn.fetch_sub(1, std::memory_order_relaxed);
+        unreserve_one();
         lk.unlock();
         run(t);
         lk.lock();
         continue;
       }
-      done.wait(lk);
+      if (!spin) {
+        done.wait(lk);
+        continue;
+      }
+      // the workers are spinning: so does the caller, rather than pay a
+      // wake-up when its last task ends
+      lk.unlock();
+      while (pending.load(std::memory_order_acquire) != 0 && qn.load(std::memory_order_relaxed) == 0) pause();
+      lk.lock();
     }
     lk.unlock();
     if (spin) hot.fetch_sub(1, std::memory_order_release);

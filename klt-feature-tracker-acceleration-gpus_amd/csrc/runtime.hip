@@ -1065,9 +1065,11 @@ KLT_API int klt_hip_upload_frame(klt_hip_ctx *c, int buf, const unsigned char *h
     c->u8_cap = n;
   }
   // a frame inside a registered caller buffer: one DMA straight from it.
-  // (Letting k_pyr_l0 read the caller's mapped pages over the bus instead, no
-  // copy at all, measured slower: 120-122 against 107-108 us per registered
-  // call, tools/exp/r04q.sh.)
+  // Measured slower (round 4, per registered call): k_pyr_l0 reading the
+  // caller's mapped pages over the bus, no copy at all, 120-122 against
+  // 107-108 us (tools/exp/r04q.sh); a copy kernel on the tracking stream
+  // reading them (no copy-engine hand-off), 116-117 against 106 us
+  // (tools/exp/r04t.sh).
   for (size_t i = 0; i < c->registered.size(); ++i) {
     const auto &r = c->registered[i];
     if (host >= r.first && n <= r.second && (size_t)(host - r.first) <= r.second - n) {

@@ -311,9 +311,8 @@ struct SelEngine {
   size_t hkv_cap = 0;
   uint8_t *d_map = nullptr;
   size_t map_cap = 0;
-  float *d_fx = nullptr, *d_fy = nullptr;
-  int *d_fv = nullptr;
-  size_t fx_cap = 0, fy_cap = 0, fv_cap = 0;
+  int *d_f = nullptr, *h_f = nullptr;  // the live features for the paint: x | y | val, n each
+  size_t f_cap = 0, hf_cap = 0;
   hipEvent_t ev_dl = nullptr, ev_ref = nullptr;  // a segment download done / a look-ahead refinement done
   int threshold = kSelDefaultThreshold;  // segments at most this long go to the host
   // statistics of the last run
@@ -565,9 +564,10 @@ SelEngine *sel_engine_create() { return new SelEngine(); }
 void sel_engine_destroy(SelEngine *e) {
   if (!e) return;
   for (void *p : {(void *)e->d_kv, (void *)e->d_cnt, (void *)e->d_off, (void *)e->d_posL, (void *)e->d_posR,
-                  (void *)e->d_state, (void *)e->d_map, (void *)e->d_fx, (void *)e->d_fy, (void *)e->d_fv})
+                  (void *)e->d_state, (void *)e->d_map, (void *)e->d_f})
     hipFree(p);
   if (e->h_state) hipHostFree(e->h_state);
+  if (e->h_f) hipHostFree(e->h_f);
   if (e->ev_dl) hipEventDestroy(e->ev_dl);
   if (e->ev_ref) hipEventDestroy(e->ev_ref);
   if (e->h_kv) hipHostFree(e->h_kv);
@@ -621,16 +621,27 @@ int sel_engine_run(SelEngine *e, hipStream_t st, const int *dev_vals, int nx, in
   const uint8_t *map = nullptr;
   if (!overwrite_all && n > 0 && r >= 0) {
     // the squares of the live features, painted on the device (:160-166)
-    if (sel_grow(&e->d_map, &e->map_cap, (size_t)W * H, err) || sel_grow(&e->d_fx, &e->fx_cap, (size_t)n, err) ||
-        sel_grow(&e->d_fy, &e->fy_cap, (size_t)n, err) || sel_grow(&e->d_fv, &e->fv_cap, (size_t)n, err))
+    if (sel_grow(&e->d_map, &e->map_cap, (size_t)W * H, err) || sel_grow(&e->d_f, &e->f_cap, 3 * (size_t)n, err))
       return -1;
+    // one DMA from pinned staging: the caller's arrays may be pageable, and
+    // each pageable copy is a blocking staged transfer of its own (the last
+    // run's copy out of h_f ended at its synchronize below)
+    if (e->hf_cap < 3 * (size_t)n) {
+      if (e->h_f) hipHostFree(e->h_f);
+      e->h_f = nullptr;
+      e->hf_cap = 0;
+      SELCHK(hipHostMalloc((void **)&e->h_f, sizeof(int) * 3 * (size_t)n, hipHostMallocDefault));
+      e->hf_cap = 3 * (size_t)n;
+    }
+    memcpy(e->h_f, x, sizeof(float) * n);
+    memcpy(e->h_f + n, y, sizeof(float) * n);
+    memcpy(e->h_f + 2 * (size_t)n, val, sizeof(int) * n);
     SELCHK(hipMemsetAsync(e->d_map, 0, (size_t)W * H, st));
-    SELCHK(hipMemcpyAsync(e->d_fx, x, sizeof(float) * n, hipMemcpyHostToDevice, st));
-    SELCHK(hipMemcpyAsync(e->d_fy, y, sizeof(float) * n, hipMemcpyHostToDevice, st));
-    SELCHK(hipMemcpyAsync(e->d_fv, val, sizeof(int) * n, hipMemcpyHostToDevice, st));
+    SELCHK(hipMemcpyAsync(e->d_f, e->h_f, sizeof(int) * 3 * (size_t)n, hipMemcpyHostToDevice, st));
     const long cells = (long)n * (2 * r + 1) * (2 * r + 1);
     hipLaunchKernelGGL(k_sel_paint, dim3((unsigned)((cells + kSelThreads - 1) / kSelThreads)), dim3(kSelThreads), 0,
-                       st, e->d_fx, e->d_fy, e->d_fv, n, r, W, H, e->d_map);
+                       st, (const float *)e->d_f, (const float *)(e->d_f + n), e->d_f + 2 * (size_t)n, n, r, W, H,
+                       e->d_map);
     SELCHK(hipGetLastError());
     map = e->d_map;
   }

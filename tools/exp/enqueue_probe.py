@@ -91,6 +91,19 @@ def main():
             check(lib, ctx, lib.klt_hip_frames_begin(ctx, C.byref(pd), C.c_void_p(fptr), W), "begin")
         spin()
 
+    def sync_then_cpu_busy():
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        while time.perf_counter() - t < 300e-6:
+            pass
+
+    def heavy_sync_then_cpu_busy():
+        for _ in range(41):
+            check(lib, ctx, lib.klt_hip_frames_begin(ctx, C.byref(pd), C.c_void_p(fptr), W), "begin")
+        sync_then_cpu_busy()
+
+    case("sync, then 300 us of host busy loop", sync_then_cpu_busy)
+    case("1 ms of GPU work, sync, 300 us busy loop", heavy_sync_then_cpu_busy)
     case("1 ms of GPU work, then spin-poll + sync", heavy_then_spin)
     case("torch.cuda.synchronize", torch.cuda.synchronize)
     case("spin-poll, then torch.cuda.synchronize", spin)

@@ -32,18 +32,18 @@ int main() {
     std::vector<P> base(n);
     for (unsigned i = 0; i < n; ++i) base[i] = P{(int)(r() % 50000), (int)i};
     for (int depth = 0; depth <= 4; ++depth) {
-      auto &pool = kltsort::Pool<P>::get(15);
-      std::vector<double> t;
-      for (int rep = 0; rep < 60; ++rep) {
-        std::vector<P> a = base;
-        const double t0 = now_us();
-        pool.sort(a.data(), n, depth, 2048);
-        t.push_back(now_us() - t0);
+        auto &pool = kltsort::Pool<P>::get(15);
+        std::vector<double> t;
+        for (int rep = 0; rep < 60; ++rep) {
+          std::vector<P> a = base;
+          const double t0 = now_us();
+          pool.sort(a.data(), n, depth, 2048);
+          t.push_back(now_us() - t0);
+        }
+        std::sort(t.begin(), t.end());
+        std::printf("{\"n\": %u, \"depth\": %d, \"workers\": %d, \"us_median\": %.1f, \"us_min\": %.1f}\n", n, depth,
+                    pool.nworkers, t[t.size() / 2], t[0]);
       }
-      std::sort(t.begin(), t.end());
-      std::printf("{\"n\": %u, \"depth\": %d, \"us_median\": %.1f, \"us_min\": %.1f}\n", n, depth, t[t.size() / 2],
-                  t[0]);
-    }
   }
   return 0;
 }
