@@ -210,6 +210,7 @@ constexpr int kSelDefaultThreshold = 32768;  // map points: longer segments are 
 SelEngine *sel_engine_create();
 void sel_engine_destroy(SelEngine *e);
 void sel_engine_set_threshold(SelEngine *e, int threshold);
+int sel_default_threshold();
 void sel_engine_stats(const SelEngine *e, long *downloaded, long *steps, long *visited, double *us);
 int sel_engine_run(SelEngine *e, hipStream_t st, const int *dev_vals, int nx, int ny, int bx, int by, int step,
                    int W, int H, int mindist, int min_eigenvalue, int overwrite_all, float *x, float *y, int *val,

@@ -87,27 +87,41 @@ __device__ __forceinline__ f4 mul4(const float *v, float k) {
 //   D  img0 -> HBM; gradient rows passes -> tx, ty; pyramid rows pass -> hs
 //   E  gradient columns passes -> gx0, gy0 (4 rows x 2 columns per thread)
 // ---------------------------------------------------------------------------
+// k_pyr_l0's geometry for tiles of 64 x TH_ pixels on TH_ * 8 threads (a
+// wave per 8 tile rows in E): TH_ = 32 (256 threads; band builds, whose rows
+// are whole 32-row tiles) or 64 (512 threads; whole frames: fewer halo rows
+// recomputed per output row, LDS 61.6 KB, two workgroups per CU)
+template <int TH_>
+struct L0G {
+  static constexpr int RS = kRS, RG = kRG, RP = kRP, SS = kSS, TW = geom::L0_TW, TH = TH_;
+  static constexpr int NT = 8 * TH;                // threads
+  static constexpr int UQ = 24;                    // staged u8 dwords per row: global [C0-12, C0+84)
+  static constexpr int UH = TH + 2 * RG + 2 * RS + 2;  // staged rows: global R0-5 ..  (2 spare for 4-row blocks)
+  static constexpr int NG = 21;                    // 4-column groups of t1 / img0: global [C0-8, C0+76)
+  static constexpr int IH = TH + 2 * RG;           // img0 rows used (global R0-3 ..)
+  static constexpr int IHB = (IH + 3) / 4;         // 4-row blocks of img0 computed
+  // LDS pitches (floats) chosen with tools/lds_banks.py so that the 16-lane
+  // groups of each ds_read_b128 hit (nearly) distinct bank slots; a few bank
+  // conflicts were traded for a 4th workgroup per CU (32-row tiles)
+  static constexpr int PT = 88, PI = 92, PX = TW, PXY = 2 * TW;
+  static constexpr int PUB = 24;                   // staged u8 row pitch in dwords (96 bytes)
+  static constexpr int U_WORDS = UH * PUB;
+  static constexpr int REG_A = U_WORDS > IH * PI ? U_WORDS : IH * PI;  // u during A-B, then img0 during C-D
+  static constexpr int REG_B = 2 * IH * PX;                            // t1 during B-C, then tx|ty during D-E
+  static constexpr int LDS = REG_A + REG_B;
+  static constexpr int RB = NT / 11;               // B: rows per pass (11 eight-column groups a row)
+  static constexpr int R16 = NT / 16;              // D: rows per pass (16 four-column groups a row)
+  // interior tiles: one 16-byte chunk per thread covers the staged rows
+  static constexpr int NQ = UQ / 4, NR = TH + 2 * RG + 2 * RS;
+  static_assert(IH * PI <= REG_A && UH * PT <= REG_B, "LDS aliasing");
+  static_assert(TH % 16 == 0 && TW % 16 == 0 && TH * TW / 16 <= NT, "tile shape");
+  static_assert(NR * NQ <= NT && NR <= UH, "one 16-byte load per thread");
+  static_assert(IHB * NG <= NT, "C: one item per thread");
+  static_assert(TH % R16 == 0, "D1: whole passes");
+};
 namespace l0 {
-constexpr int RS = kRS, RG = kRG, RP = kRP, SS = kSS, TW = geom::L0_TW, TH = geom::L0_TH;
-constexpr int UQ = 24;                        // staged u8 dwords per row: global [C0-12, C0+84)
-constexpr int UH = TH + 2 * RG + 2 * RS + 2;  // 44 rows: global R0-5 ..  (2 spare for 4-row blocks)
-constexpr int NG = 21;                        // 4-column groups of t1 / img0: global [C0-8, C0+76)
-constexpr int IH = TH + 2 * RG;               // 38 img0 rows used (global R0-3 ..)
-constexpr int IHB = (IH + 3) / 4;             // 4-row blocks of img0 computed
-// LDS pitches (floats) chosen with tools/lds_banks.py so that the 16-lane
-// groups of each ds_read_b128 hit (nearly) distinct bank slots; a few bank
-// conflicts were traded for a 4th workgroup per CU
-constexpr int PT = 88, PI = 92, PX = TW, PXY = 2 * TW;
-constexpr int PUB = 24;                   // staged u8 row pitch in dwords (96 bytes)
-constexpr int U_WORDS = UH * PUB;
-constexpr int REG_A = U_WORDS > IH * PI ? U_WORDS : IH * PI;  // u during A-B, then img0 during C-D
-constexpr int REG_B = 2 * IH * PX;                            // t1 during B-C, then tx|ty during D-E
-constexpr int LDS = REG_A + REG_B;
-static_assert(IH * PI <= REG_A && UH * PT <= REG_B, "LDS aliasing");
-static_assert(TH % 4 == 0 && TH * TW / 16 <= kBlock && TW % 16 == 0, "tile shape");
-// interior tiles: one 16-byte chunk per thread covers the staged rows
-constexpr int NQ = UQ / 4, NR = TH + 2 * RG + 2 * RS;
-static_assert(NR * NQ <= kBlock && NR <= UH, "one 16-byte load per thread");
+using G32 = L0G<32>;
+constexpr int TW = G32::TW, SS = G32::SS;
 }  // namespace l0
 
 // XCD-aware tile order: consecutive workgroups are dealt to the 8 XCDs in
@@ -138,13 +152,16 @@ __device__ unsigned long long *g_pyr_prof;
 // element; interior tiles (~90 % at 1080p, 94 % at 4K) need neither.
 // IL: the level's planes interleaved per pixel, {gx, gy, img} (12 bytes, klt_dev.h)
 // at img0 + 3*(y*W + x) -- written in E, where img0 is still in LDS; gx0/gy0 unused
-template <bool INT, bool IL>
+template <bool INT, bool IL, int TH_>
 __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8_t *__restrict__ src, int spitch,
                                             int W, int H, const DefTaps &T, int vec_u8,
                                             float *__restrict__ img0, float *__restrict__ gx0,
                                             float *__restrict__ gy0, float *__restrict__ hs, int hsW,
                                             int do_hs, int vec_out, int C0, int R0, int tid, bool planes) {
-  using namespace l0;
+  using G = L0G<TH_>;
+  constexpr int RS = G::RS, RG = G::RG, RP = G::RP, SS = G::SS, TW = G::TW, TH = G::TH, NT = G::NT;
+  constexpr int UQ = G::UQ, UH = G::UH, NG = G::NG, IH = G::IH, IHB = G::IHB, PT = G::PT, PI = G::PI, PX = G::PX,
+                PXY = G::PXY, PUB = G::PUB, REG_A = G::REG_A, NQ = G::NQ, NR = G::NR, RB = G::RB, R16 = G::R16;
   float *u = lds;            // [UH][PUB] staged bytes
   float *im = lds;           // [IHB*4][PI]   (after u is dead)
   float *t1 = lds + REG_A;   // [UH][PT]
@@ -166,14 +183,14 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     const uint4 c = *reinterpret_cast<const uint4 *>(src + (unsigned)((R0 - RG - RS + r) * spitch + C0 - 12 + 16 * q));
     *reinterpret_cast<uint4 *>(reinterpret_cast<uint32_t *>(u) + r * PUB + 4 * q) = c;
   } else {
-    constexpr int NA = UH * UQ, PER = (NA + kBlock - 1) / kBlock;
+    constexpr int NA = UH * UQ, PER = (NA + NT - 1) / NT;
     uint32_t w[PER];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       // unconditional: items past NA reload the last dword and land in LDS
       // past the staged rows (unused), so no load sits under a branch -- the
       // compiler's wait counting then stays exact
-      const int i = min(tid + k * kBlock, NA - 1);
+      const int i = min(tid + k * NT, NA - 1);
       const int r = i / UQ, q = i - r * UQ;
       const int x = C0 - 12 + 4 * q;
       const unsigned rowp = (unsigned)(clampi(R0 - RG - RS + r, 0, H - 1) * spitch);
@@ -185,10 +202,10 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
                ((uint32_t)src[rowp + clampi(x + 3, 0, W - 1)] << 24);
       }
     }
-    static_assert(PER * kBlock <= REG_A, "phase A spill-over stays inside region A");
+    static_assert(PER * NT <= REG_A, "phase A spill-over stays inside region A");
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      const int i = tid + k * kBlock;
+      const int i = tid + k * NT;
       const int r = i / UQ, q = i - r * UQ;
       reinterpret_cast<uint32_t *>(u)[r * PUB + q] = w[k];
     }
@@ -197,13 +214,13 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
   PYR_STAMP(1)
 
   // B. rows pass of the smoothing: t1 idx k <-> global C0-8+k; zero unless RS <= x < W-RS.
-  //    23 rows of 11 eight-column groups per pass (t1 idx 0..87): bytes [8j, 8j+16) of a staged row
+  //    RB rows of 11 eight-column groups per pass (t1 idx 0..87): bytes [8j, 8j+16) of a staged row
   {
     const int j = tid % 11, r0 = tid / 11;
 #pragma unroll
-    for (int k = 0; k < (UH + 22) / 23; ++k) {
-      const int r = r0 + 23 * k;
-      if (r0 >= 23 || r >= UH) break;
+    for (int k = 0; k < (UH + RB - 1) / RB; ++k) {
+      const int r = r0 + RB * k;
+      if (r0 >= RB || r >= UH) break;
       const uint32_t *row = reinterpret_cast<const uint32_t *>(u) + r * PUB + 2 * j;
       const uint2 d01 = *reinterpret_cast<const uint2 *>(row), d23 = *reinterpret_cast<const uint2 *>(row + 2);
       const uint32_t d[4] = {d01.x, d01.y, d23.x, d23.y};
@@ -263,9 +280,9 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
   // where only the sigma-3.6 rows pass is needed -- skips D1, D2 and E)
   const int g16 = tid & 15, r16 = tid >> 4;
 #pragma unroll
-  for (int k = 0; k < TH / 16; ++k) {
+  for (int k = 0; k < TH / R16; ++k) {
     if (!planes || IL) break;
-    const int r = r16 + 16 * k, g = g16;
+    const int r = r16 + R16 * k, g = g16;
     const int y = R0 + r, x = C0 + 4 * g;
     const f4 val = ld4(im + (r + RG) * PI + 8 + 4 * g);
     if (INT) {
@@ -280,8 +297,8 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
   }
   // D2. rows passes of both gradients; zero unless RG <= x < W-RG
 #pragma unroll
-  for (int k = 0; k < (IH + 15) / 16; ++k) {
-    const int r = r16 + 16 * k, g = g16;
+  for (int k = 0; k < (IH + R16 - 1) / R16; ++k) {
+    const int r = r16 + R16 * k, g = g16;
     if (r >= IH || !planes) break;
     const float *row = im + r * PI + 4 * g + 4;  // img0 idx c0+4 <-> global C0+c0-4
     float v[12];
@@ -342,8 +359,8 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
   // D3. pyramid rows pass at columns 4X+2; zero unless RP <= c < W-RP.  Four
   // outputs per item (36 values read for 4 outputs), TH*TW/16 items on the
   // upper threads, which take one gradient row group fewer in D2
-  if (do_hs && tid >= kBlock - TH * (TW / 16)) {
-    const int i = tid - (kBlock - TH * (TW / 16));
+  if (do_hs && tid >= NT - TH * (TW / 16)) {
+    const int i = tid - (NT - TH * (TW / 16));
     const int r = i / (TW / 16), q = i - r * (TW / 16);
     const float *row = im + (r + RG) * PI + 16 * q;  // idx 16q <-> global C0+16q-8
     float v[36];
@@ -382,7 +399,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
   if constexpr (IL) {
     if (!planes) return;
     static_assert(kRecGx == 0 && kRecGy == 1 && kRecImg == 2, "record layout");
-    static_assert(TW == kWave && TH == 8 * (kBlock / kWave), "E: a wave per 8 rows x 64 columns");
+    static_assert(TW == kWave && TH == 8 * (NT / kWave), "E: a wave per 8 rows x 64 columns");
     const int c = tid & (kWave - 1), w8 = __builtin_amdgcn_readfirstlane(8 * (tid / kWave));  // wave-uniform
     const int cq = 4 * ((c >> 1) ^ ((c >> 4) & 1)) + 2 * (c & 1);  // D2's chunk order (conflict-free here too)
     f2 q[14];
@@ -418,7 +435,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
   }
   // E. columns passes of both gradients; zero unless RG <= y < H-RG.  4 rows x
   //    2 columns per thread from 8-byte LDS reads (10 rows read for 4 outputs)
-  for (int i = planes ? tid : kBlock; i < (TH / 4) * (TW / 2); i += kBlock) {
+  for (int i = planes ? tid : NT; i < (TH / 4) * (TW / 2); i += NT) {
     const int b = i / (TW / 2), g = i - b * (TW / 2);
     f2 vx[10], vy[10];
 #pragma unroll
@@ -496,21 +513,22 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
 #endif
 }
 
-template <bool IL>
-__global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ src, int spitch, int W, int H,
+template <bool IL, int TH_>
+__global__ __launch_bounds__(L0G<TH_>::NT) void k_pyr_l0(const uint8_t *__restrict__ src, int spitch, int W, int H,
                                                    DefTaps T, int vec_u8, float *__restrict__ img0,
                                                    float *__restrict__ gx0, float *__restrict__ gy0,
                                                    float *__restrict__ hs, int hsW, int do_hs, int vec_out,
                                                    long fs_src, long fs0, long fs_hs, int ty0, int tiles_x,
                                                    int tiles_y, int py0, int py1) {
-  __shared__ __attribute__((aligned(16))) float lds[l0::LDS];
+  using G = L0G<TH_>;
+  __shared__ __attribute__((aligned(16))) float lds[G::LDS];
   int bx, by;
   if (!xcd_tile(tiles_x, tiles_y, bx, by)) return;  // whole workgroup: no barrier is skipped
 #ifdef KLT_PYR_PROF
   const int tid = threadIdx.x;
   PYR_STAMP(0)
 #endif
-  const int C0 = bx * l0::TW, R0 = (by + ty0) * l0::TH;
+  const int C0 = bx * G::TW, R0 = (by + ty0) * G::TH;
   // blockIdx.z: frame of a batch (frame strides in elements; 0 for one frame)
   src += blockIdx.z * fs_src;
   img0 += blockIdx.z * fs0;
@@ -518,15 +536,15 @@ __global__ __launch_bounds__(kBlock) void k_pyr_l0(const uint8_t *__restrict__ s
   gy0 += blockIdx.z * fs0;
   hs += blockIdx.z * fs_hs;
   // interior: unclamped aligned loads, no zero-border rule applies, all stores in bounds
-  const bool interior = vec_u8 && vec_out && (hsW * l0::SS == W) && (hsW % 2 == 0) && C0 >= 12 && C0 + 84 <= W &&
-                        R0 >= 5 && R0 + l0::TH + 7 <= H;
+  const bool interior = vec_u8 && vec_out && (hsW * G::SS == W) && (hsW % 2 == 0) && C0 >= 12 && C0 + 84 <= W &&
+                        R0 >= 5 && R0 + G::TH + 7 <= H;
   const bool planes = by + ty0 >= py0 && by + ty0 < py1;  // tile rows [py0, py1) store img0, gx0, gy0
   if (interior)
-    pyr_l0_tile<true, IL>(lds, src, spitch, W, H, T, vec_u8, img0, gx0, gy0, hs, hsW, do_hs, vec_out, C0, R0,
-                      threadIdx.x, planes);
+    pyr_l0_tile<true, IL, TH_>(lds, src, spitch, W, H, T, vec_u8, img0, gx0, gy0, hs, hsW, do_hs, vec_out, C0, R0,
+                               threadIdx.x, planes);
   else
-    pyr_l0_tile<false, IL>(lds, src, spitch, W, H, T, vec_u8, img0, gx0, gy0, hs, hsW, do_hs, vec_out, C0, R0,
-                       threadIdx.x, planes);
+    pyr_l0_tile<false, IL, TH_>(lds, src, spitch, W, H, T, vec_u8, img0, gx0, gy0, hs, hsW, do_hs, vec_out, C0, R0,
+                                threadIdx.x, planes);
 }
 
 // ---------------------------------------------------------------------------
@@ -790,6 +808,64 @@ __global__ __launch_bounds__(kBlock) void k_min_eigen(const float *__restrict__ 
   out[i] = x86_ftoi(val);
 }
 
+// The same map for the default 7x7 window, tiled: a workgroup covers 64 x 16
+// grid points (a lane per column, each wave four grid rows), stages the
+// gradients its windows read in LDS once (global reads drop from 49 per
+// point to ~1.4), and sums each window from LDS in the reference's order:
+// rows, then columns, from +0, one rounding per operation (sxx and syy as one
+// packed pair: two independent IEEE sums, the same bits).  step <= kEigMaxStep.
+namespace eig {
+constexpr int TX = 64, TY = 16, RPW = TY / 4, HW = 3;
+constexpr int kMaxStep = 2;
+constexpr int C_MAX = (TX - 1) * kMaxStep + 2 * HW + 1, R_MAX = (TY - 1) * kMaxStep + 2 * HW + 1;
+}  // namespace eig
+
+__global__ __launch_bounds__(256) void k_min_eigen7(const float *__restrict__ gx, const float *__restrict__ gy, int W,
+                                                   int ps, int bx, int by, int step, int nx, int ny,
+                                                   int *__restrict__ out) {
+  using namespace eig;
+  __shared__ f2 g[R_MAX * C_MAX];
+  const int tiles_x = (nx + TX - 1) / TX;
+  const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+  const int ix0 = tx * TX, iy0 = ty * TY;
+  const int C = (TX - 1) * step + 2 * HW + 1, R = (TY - 1) * step + 2 * HW + 1;
+  // pixel (x0 + c, y0 + r) for LDS cell (r, c); clamped to the last grid
+  // point's window (tiles past nx / ny read valid pixels they never use)
+  const int x0 = bx + ix0 * step - HW, y0 = by + iy0 * step - HW;
+  const int xmax = bx + (nx - 1) * step + HW, ymax = by + (ny - 1) * step + HW;
+  for (int p = threadIdx.x; p < R * C; p += 256) {
+    const int r = p / C, c = p - r * C;
+    const int yy = min(y0 + r, ymax), xx = min(x0 + c, xmax);
+    const long o = ((long)yy * W + xx) * ps;
+    g[r * C_MAX + c] = f2{gx[o], gy[o]};
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ix = ix0 + lane;
+  if (ix >= nx) return;
+#pragma unroll 1
+  for (int k = 0; k < RPW; ++k) {
+    const int iy = iy0 + w * RPW + k;
+    if (iy >= ny) return;
+    const f2 *base = g + ((w * RPW + k) * step) * C_MAX + lane * step;
+    f2 sq = {0.0f, 0.0f};  // (sxx, syy)
+    float sxy = 0.0f;
+#pragma unroll
+    for (int v = 0; v < 2 * HW + 1; ++v)
+#pragma unroll
+      for (int u = 0; u < 2 * HW + 1; ++u) {
+        const f2 ab = base[v * C_MAX + u];
+        sq += ab * ab;
+        sxy += ab.x * ab.y;
+      }
+    const float sxx = sq.x, syy = sq.y;
+    const float disc = (sxx - syy) * (sxx - syy) + 4.0f * sxy * sxy;
+    float val = (float)(((double)(sxx + syy) - sqrt((double)disc)) / 2.0);
+    if (val > 2147483648.0f) val = 2147483648.0f;
+    out[(long)iy * nx + ix] = x86_ftoi(val);
+  }
+}
+
 // synthetic frames (include/klt_synth.h), one thread per pixel
 // rows row0 .. row0+H-1 of the frames (row row0 lands in row 0 of `out`)
 __global__ __launch_bounds__(kBlock) void k_synth(unsigned long long seed, int t0, int W, int H, int row0,
@@ -839,6 +915,17 @@ __global__ void k_selftest_div(const float *a, const float *b, float *out, int n
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
+// 64-row level-0 tiles for whole frames of at least kL0WideMinRows rows
+// (default), or 32-row tiles everywhere (KLT_L0_WIDE=0; A/B)
+constexpr int kL0WideMinRows = 2000;
+bool l0_wide() {
+  static const bool on = [] {
+    const char *v = getenv("KLT_L0_WIDE");
+    return !(v && *v && atoi(v) == 0);
+  }();
+  return on;
+}
+
 hipError_t launch_pyr_l0(hipStream_t st, const uint8_t *src, int pitch, long stride, int W, int H, const DefTaps &T,
                          int vec_u8, int vec_out, float *img, float *gx, float *gy, float *hs, int W1, int do_hs,
                          long fs0, long fsh, int F, int ty0, int ty1, int py0, int py1, int il) {
@@ -847,12 +934,31 @@ hipError_t launch_pyr_l0(hipStream_t st, const uint8_t *src, int pitch, long str
 #ifdef KLT_EXP_NOHS  // timing experiment only: level 0 without the sigma-3.6 rows pass
   do_hs = 0;
 #endif
+  // a whole 4K-class frame with every tile's planes (ty, py in 32-row tiles)
+  // runs the 64-row tiles; a band, planes for some rows only, or a shorter
+  // frame the 32-row ones.  Same-box A/B (tools/exp/r04x.sh): 4K 29.4
+  // against 29.8-29.9 us per frame; 1080p 7.54-7.60 against 7.25 (more edge
+  // tiles, and ~one workgroup per slot: the launch's tail)
+  const int nty = (H + l0::G32::TH - 1) / l0::G32::TH;
+  if (l0_wide() && H >= kL0WideMinRows && ty0 == 0 && ty1 == nty && py0 == 0 && py1 >= nty) {
+    using G = L0G<64>;
+    const int ty = (H + G::TH - 1) / G::TH;
+    if (il)
+      hipLaunchKernelGGL((k_pyr_l0<true, 64>), dim3(xcd_grid(tx * ty), 1, F), dim3(G::NT), 0, st, src, pitch, W, H, T,
+                         vec_u8, img, gx, gy, hs, W1, do_hs, vec_out, stride, fs0, fsh, 0, tx, ty, 0, ty);
+    else
+      hipLaunchKernelGGL((k_pyr_l0<false, 64>), dim3(xcd_grid(tx * ty), 1, F), dim3(G::NT), 0, st, src, pitch, W, H,
+                         T, vec_u8, img, gx, gy, hs, W1, do_hs, vec_out, stride, fs0, fsh, 0, tx, ty, 0, ty);
+    return hipGetLastError();
+  }
+  using G = l0::G32;
   if (il)
-    hipLaunchKernelGGL(k_pyr_l0<true>, dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(kBlock), 0, st, src, pitch, W, H,
-                       T, vec_u8, img, gx, gy, hs, W1, do_hs, vec_out, stride, fs0, fsh, ty0, tx, ty1 - ty0, py0, py1);
+    hipLaunchKernelGGL((k_pyr_l0<true, 32>), dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(G::NT), 0, st, src, pitch, W,
+                       H, T, vec_u8, img, gx, gy, hs, W1, do_hs, vec_out, stride, fs0, fsh, ty0, tx, ty1 - ty0, py0, py1);
   else
-    hipLaunchKernelGGL(k_pyr_l0<false>, dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(kBlock), 0, st, src, pitch, W, H,
-                       T, vec_u8, img, gx, gy, hs, W1, do_hs, vec_out, stride, fs0, fsh, ty0, tx, ty1 - ty0, py0, py1);
+    hipLaunchKernelGGL((k_pyr_l0<false, 32>), dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(G::NT), 0, st, src, pitch,
+                       W, H, T, vec_u8, img, gx, gy, hs, W1, do_hs, vec_out, stride, fs0, fsh, ty0, tx, ty1 - ty0, py0,
+                       py1);
   return hipGetLastError();
 }
 
@@ -901,6 +1007,11 @@ hipError_t launch_min_eigen(hipStream_t st, const float *gx, const float *gy, in
                             int nx, int ny, int hw, int hh, int *out) {
   const long np = (long)nx * ny;
   if (np == 0) return hipSuccess;
+  if (hw == eig::HW && hh == eig::HW && step >= 1 && step <= eig::kMaxStep) {
+    const long tiles = (long)((nx + eig::TX - 1) / eig::TX) * ((ny + eig::TY - 1) / eig::TY);
+    hipLaunchKernelGGL(k_min_eigen7, dim3((unsigned)tiles), dim3(256), 0, st, gx, gy, W, ps, bx, by, step, nx, ny, out);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_min_eigen, dim3(blocks_for(np)), dim3(kBlock), 0, st, gx, gy, W, ps, bx, by, step, nx, ny, hw,
                      hh, out);
   return hipGetLastError();

@@ -998,7 +998,7 @@ KLT_API int klt_hip_ctx_reset(klt_hip_ctx *c) {
   c->feat_mode = 2;
   for (auto &r : c->registered) (void)hipHostUnregister(const_cast<unsigned char *>(r.first));
   c->registered.clear();
-  if (c->sel) sel_engine_set_threshold(c->sel, kSelDefaultThreshold);
+  if (c->sel) sel_engine_set_threshold(c->sel, sel_default_threshold());
   c->bank_budget = 0;
   c->chunk_used = 0;
   c->stream = c->own;

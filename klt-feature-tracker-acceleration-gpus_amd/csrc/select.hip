@@ -131,7 +131,7 @@ __global__ __launch_bounds__(kSelThreads) void k_sel_paint(const float *__restri
 }
 
 // step 0: pivot a[n/2] to the front (or stop: the segment is small enough)
-__global__ void k_sel_pivot(SelState *s, int2 *kv, int threshold) {
+__device__ __forceinline__ void sel_pivot(SelState *s, int2 *kv, int threshold) {
   if (s->done) return;
   if (s->len <= threshold) {
     s->done = 1;
@@ -143,12 +143,13 @@ __global__ void k_sel_pivot(SelState *s, int2 *kv, int threshold) {
   s->m = 0;
 }
 
+__global__ void k_sel_pivot(SelState *s, int2 *kv, int threshold) { sel_pivot(s, kv, threshold); }
+
 // step 1: left / right stop counts per block (positions 1 .. len-1)
-__global__ __launch_bounds__(kSelThreads) void k_sel_count(const SelState *s, const int2 *__restrict__ kv,
-                                                          int *__restrict__ cnt) {
-  __shared__ int tmp[kSelThreads / kWave];
+__device__ __forceinline__ void sel_count(const SelState *s, const int2 *__restrict__ kv, int *__restrict__ cnt,
+                                          int *tmp, int b) {
   if (s->done) return;
-  const int len = s->len, b = blockIdx.x;
+  const int len = s->len;
   if (b * kSelBS >= len) return;
   const int2 *a = kv + s->start;
   const int pv = s->pv;
@@ -171,14 +172,20 @@ __global__ __launch_bounds__(kSelThreads) void k_sel_count(const SelState *s, co
   }
 }
 
+__global__ __launch_bounds__(kSelThreads) void k_sel_count(const SelState *s, const int2 *__restrict__ kv,
+                                                          int *__restrict__ cnt) {
+  __shared__ int tmp[kSelThreads / kWave];
+  sel_count(s, kv, cnt, tmp, blockIdx.x);
+}
+
 // step 2 (one block): exclusive prefix of the left counts, exclusive suffix
 // (blocks after b) of the right counts, totals
-__global__ __launch_bounds__(kSelScanThreads) void k_sel_scan(SelState *s, const int *__restrict__ cnt,
-                                                             int *__restrict__ off) {
-  __shared__ int sl[kSelScanThreads], sr[kSelScanThreads];
+template <int NT>
+__device__ __forceinline__ void sel_scan(SelState *s, const int *__restrict__ cnt, int *__restrict__ off, int *sl,
+                                         int *sr) {
   if (s->done) return;
   const int nb = (s->len + kSelBS - 1) / kSelBS;
-  const int per = (nb + kSelScanThreads - 1) / kSelScanThreads;
+  const int per = (nb + NT - 1) / NT;
   const int t = threadIdx.x, b0 = t * per;
   int l = 0, r = 0;
   for (int k = 0; k < per; ++k)
@@ -189,14 +196,14 @@ __global__ __launch_bounds__(kSelScanThreads) void k_sel_scan(SelState *s, const
   sl[t] = l;
   sr[t] = r;
   __syncthreads();
-  for (int o = 1; o < kSelScanThreads; o <<= 1) {  // inclusive Hillis-Steele scans
+  for (int o = 1; o < NT; o <<= 1) {  // inclusive Hillis-Steele scans
     const int a = t >= o ? sl[t - o] : 0, c = t >= o ? sr[t - o] : 0;
     __syncthreads();
     sl[t] += a;
     sr[t] += c;
     __syncthreads();
   }
-  const int totL = sl[kSelScanThreads - 1], totR = sr[kSelScanThreads - 1];
+  const int totL = sl[NT - 1], totR = sr[NT - 1];
   int pl = sl[t] - l, pr = sr[t] - r;  // exclusive: blocks before b0
   for (int k = 0; k < per; ++k) {
     const int b = b0 + k;
@@ -212,16 +219,20 @@ __global__ __launch_bounds__(kSelScanThreads) void k_sel_scan(SelState *s, const
   }
 }
 
+__global__ __launch_bounds__(kSelScanThreads) void k_sel_scan(SelState *s, const int *__restrict__ cnt,
+                                                             int *__restrict__ off) {
+  __shared__ int sl[kSelScanThreads], sr[kSelScanThreads];
+  sel_scan<kSelScanThreads>(s, cnt, off, sl, sr);
+}
+
 // step 3: per position, its rank among the left stops (ascending) and the right
 // stops (descending); left stop k pairs with right stop k when the latter lies
 // further right.  posL[k-1] / posR[k-1] collect the pairs' positions; m counts
 // them.
-__global__ __launch_bounds__(kSelThreads) void k_sel_rank(SelState *s, const int2 *__restrict__ kv,
-                                                         const int *__restrict__ off, int *__restrict__ posL,
-                                                         int *__restrict__ posR) {
-  __shared__ int tmp[kSelThreads / kWave];
+__device__ __forceinline__ void sel_rank(SelState *s, const int2 *__restrict__ kv, const int *__restrict__ off,
+                                         int *__restrict__ posL, int *__restrict__ posR, int *tmp, int b) {
   if (s->done) return;
-  const int len = s->len, b = blockIdx.x;
+  const int len = s->len;
   if (b * kSelBS >= len) return;
   const int2 *a = kv + s->start;
   const int pv = s->pv, totL = s->totL;
@@ -264,15 +275,21 @@ __global__ __launch_bounds__(kSelThreads) void k_sel_rank(SelState *s, const int
   if (threadIdx.x == 0 && tot) atomicAdd(&s->m, tot);
 }
 
+__global__ __launch_bounds__(kSelThreads) void k_sel_rank(SelState *s, const int2 *__restrict__ kv,
+                                                         const int *__restrict__ off, int *__restrict__ posL,
+                                                         int *__restrict__ posR) {
+  __shared__ int tmp[kSelThreads / kWave];
+  sel_rank(s, kv, off, posL, posR, tmp, blockIdx.x);
+}
+
 // step 4: the m swaps, the pivot into its slot, and the split: right part and
 // pivot pushed (the order in which klt_select.c's lazy sort pushes them), the
 // left part becomes the current segment.  The thread of the last swap also
 // moves the pivot (its slot may be that swap's left position).
-__global__ __launch_bounds__(kSelThreads) void k_sel_swap(SelState *s, int2 *__restrict__ kv,
-                                                         const int *__restrict__ posL, const int *__restrict__ posR) {
+__device__ __forceinline__ void sel_swap(SelState *s, int2 *__restrict__ kv, const int *__restrict__ posL,
+                                         const int *__restrict__ posR, int k) {
   if (s->done) return;
   const int m = s->m, st = s->start;
-  const int k = blockIdx.x * kSelThreads + threadIdx.x;
   if (k < m) swap2(kv, st + posL[k], st + posR[k]);
   if (k == (m > 0 ? m - 1 : 0)) {
     const int len = s->len;
@@ -296,12 +313,28 @@ __global__ __launch_bounds__(kSelThreads) void k_sel_swap(SelState *s, int2 *__r
   }
 }
 
+__global__ __launch_bounds__(kSelThreads) void k_sel_swap(SelState *s, int2 *__restrict__ kv,
+                                                         const int *__restrict__ posL, const int *__restrict__ posR) {
+  sel_swap(s, kv, posL, posR, blockIdx.x * kSelThreads + threadIdx.x);
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
 // host driver
 // ---------------------------------------------------------------------------
+bool sel_graphs();
+
+// a captured refinement: `levels` partition steps over grids of nb / sw blocks
+struct SelGraph {
+  int levels, nb, sw, T;
+  const void *kv, *cnt, *off, *posL, *posR;  // the buffers it was captured with
+  hipGraphExec_t exec;
+};
+
 struct SelEngine {
+  std::vector<SelGraph> graphs;
+  hipStream_t cap = nullptr;  // capture only
   int2 *d_kv = nullptr;
   size_t kv_cap = 0;
   int *d_cnt = nullptr, *d_off = nullptr, *d_posL = nullptr, *d_posR = nullptr;
@@ -314,7 +347,13 @@ struct SelEngine {
   int *d_f = nullptr, *h_f = nullptr;  // the live features for the paint: x | y | val, n each
   size_t f_cap = 0, hf_cap = 0;
   hipEvent_t ev_dl = nullptr, ev_ref = nullptr;  // a segment download done / a look-ahead refinement done
-  int threshold = kSelDefaultThreshold;  // segments at most this long go to the host
+  // segment downloads run on a stream of their own: a look-ahead refinement
+  // queued on the selection stream (other positions of d_kv) does not delay
+  // them; ev_prep orders them after the map's preparation once per run
+  hipStream_t dl = nullptr;
+  hipEvent_t ev_prep = nullptr;
+  bool dl_ordered = false;
+  int threshold = sel_default_threshold();  // segments at most this long go to the host
   // statistics of the last run
   long downloaded = 0, device_steps = 0, visited = 0;
   double us[4] = {};  // host wall clock: map + paint + init queued and drained, device splits, segment downloads + host sorts, total
@@ -392,6 +431,48 @@ int refine_launch(SelEngine *e, hipStream_t st, Seg g, std::string *err) {
   int levels = 2;
   for (long l = g.len; l > T; l /= 2) ++levels;
   const int sw = (g.len / 2 + kSelThreads) / kSelThreads;
+  if (sel_graphs()) {
+    // the steps as one graph launch: 5 * levels kernel launches cost more
+    // host time than the steps take on the device.  The kernels read the
+    // segment from the device state and skip blocks past it, so one graph
+    // (grids rounded up to a power of two) serves every segment of that size
+    int nbp = 1, swp = 1;
+    while (nbp < nb) nbp *= 2;
+    while (swp < sw) swp *= 2;
+    hipGraphExec_t ex = nullptr;
+    for (const SelGraph &k : e->graphs)
+      if (k.levels == levels && k.nb == nbp && k.sw == swp && k.T == T && k.kv == e->d_kv && k.cnt == e->d_cnt &&
+          k.off == e->d_off && k.posL == e->d_posL && k.posR == e->d_posR)
+        ex = k.exec;
+    if (!ex) {
+      if (!e->cap) SELCHK(hipStreamCreateWithFlags(&e->cap, hipStreamNonBlocking));
+      SELCHK(hipStreamBeginCapture(e->cap, hipStreamCaptureModeThreadLocal));
+      for (int l = 0; l < levels; ++l) {
+        hipLaunchKernelGGL(k_sel_pivot, dim3(1), dim3(1), 0, e->cap, e->d_state, e->d_kv, T);
+        hipLaunchKernelGGL(k_sel_count, dim3(nbp), dim3(kSelThreads), 0, e->cap, e->d_state, e->d_kv, e->d_cnt);
+        hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(kSelScanThreads), 0, e->cap, e->d_state, e->d_cnt, e->d_off);
+        hipLaunchKernelGGL(k_sel_rank, dim3(nbp), dim3(kSelThreads), 0, e->cap, e->d_state, e->d_kv, e->d_off,
+                           e->d_posL, e->d_posR);
+        hipLaunchKernelGGL(k_sel_swap, dim3(swp), dim3(kSelThreads), 0, e->cap, e->d_state, e->d_kv, e->d_posL,
+                           e->d_posR);
+      }
+      hipGraph_t gr = nullptr;
+      SELCHK(hipStreamEndCapture(e->cap, &gr));
+      const hipError_t ie = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
+      hipGraphDestroy(gr);
+      SELCHK(ie);
+      if (e->graphs.size() >= 24) {  // bounded: drop the oldest
+        hipGraphExecDestroy(e->graphs.front().exec);
+        e->graphs.erase(e->graphs.begin());
+      }
+      e->graphs.push_back(SelGraph{levels, nbp, swp, T, e->d_kv, e->d_cnt, e->d_off, e->d_posL, e->d_posR, ex});
+    }
+    SELCHK(hipGraphLaunch(ex, st));
+    e->device_steps += levels;
+    SELCHK(hipMemcpyAsync(e->h_state, e->d_state, sizeof(SelState), hipMemcpyDeviceToHost, st));
+    SELCHK(hipEventRecord(e->ev_ref, st));
+    return 0;
+  }
   for (int l = 0; l < levels; ++l) {
     hipLaunchKernelGGL(k_sel_pivot, dim3(1), dim3(1), 0, st, e->d_state, e->d_kv, T);
     hipLaunchKernelGGL(k_sel_count, dim3(nb), dim3(kSelThreads), 0, st, e->d_state, e->d_kv, e->d_cnt);
@@ -481,9 +562,18 @@ struct LazySort {
           continue;
         }
         const double t0 = now_us();
+        // g's positions are final: it comes from the preparation (ordered
+        // below) or from a refinement whose state the host has already read
+        if (!e->dl_ordered && (hipEventRecord(e->ev_prep, st) != hipSuccess ||
+                               hipStreamWaitEvent(e->dl, e->ev_prep, 0) != hipSuccess)) {
+          if (err) *err = "select: download ordering failed";
+          failed = 1;
+          return -1;
+        }
+        e->dl_ordered = true;
         if (hipMemcpyAsync(e->h_kv + g.start, e->d_kv + g.start, sizeof(int2) * (size_t)g.len,
-                           hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipEventRecord(e->ev_dl, st) != hipSuccess) {
+                           hipMemcpyDeviceToHost, e->dl) != hipSuccess ||
+            hipEventRecord(e->ev_dl, e->dl) != hipSuccess) {
           if (err) *err = "select: segment download failed";
           failed = 1;
           return -1;
@@ -559,6 +649,27 @@ struct NearGrid {
 
 }  // namespace
 
+// a refinement's partition steps as one graph launch (default), or one launch
+// per kernel (KLT_SEL_GRAPH=0; A/B)
+bool sel_graphs() {
+  static const bool on = [] {
+    const char *v = getenv("KLT_SEL_GRAPH");
+    return !(v && *v && atoi(v) == 0);
+  }();
+  return on;
+}
+
+// kSelDefaultThreshold, or KLT_AMD_SELECT_THRESHOLD (tuning; any value gives
+// the same selection)
+int sel_default_threshold() {
+  static const int t = [] {
+    const char *v = getenv("KLT_AMD_SELECT_THRESHOLD");
+    const int x = v && *v ? atoi(v) : kSelDefaultThreshold;
+    return x < 1 ? kSelDefaultThreshold : x;
+  }();
+  return t;
+}
+
 SelEngine *sel_engine_create() { return new SelEngine(); }
 
 void sel_engine_destroy(SelEngine *e) {
@@ -570,6 +681,13 @@ void sel_engine_destroy(SelEngine *e) {
   if (e->h_f) hipHostFree(e->h_f);
   if (e->ev_dl) hipEventDestroy(e->ev_dl);
   if (e->ev_ref) hipEventDestroy(e->ev_ref);
+  if (e->ev_prep) hipEventDestroy(e->ev_prep);
+  for (const SelGraph &k : e->graphs) hipGraphExecDestroy(k.exec);
+  if (e->cap) hipStreamDestroy(e->cap);
+  if (e->dl) {
+    (void)hipStreamSynchronize(e->dl);
+    hipStreamDestroy(e->dl);
+  }
   if (e->h_kv) hipHostFree(e->h_kv);
   delete e;
 }
@@ -592,6 +710,9 @@ static int sel_prepare(SelEngine *e, hipStream_t st, const int *dev_vals, int nx
   if (!e->h_state) SELCHK(hipHostMalloc((void **)&e->h_state, sizeof(SelState), hipHostMallocDefault));
   if (!e->ev_dl) SELCHK(hipEventCreateWithFlags(&e->ev_dl, hipEventDisableTiming));
   if (!e->ev_ref) SELCHK(hipEventCreateWithFlags(&e->ev_ref, hipEventDisableTiming));
+  if (!e->ev_prep) SELCHK(hipEventCreateWithFlags(&e->ev_prep, hipEventDisableTiming));
+  if (!e->dl) SELCHK(hipStreamCreateWithFlags(&e->dl, hipStreamNonBlocking));
+  e->dl_ordered = false;
   if (e->hkv_cap < n) {
     if (e->h_kv) hipHostFree(e->h_kv);
     e->h_kv = nullptr;
@@ -647,7 +768,8 @@ int sel_engine_run(SelEngine *e, hipStream_t st, const int *dev_vals, int nx, in
   }
   const double t_start = now_us();
   if (sel_prepare(e, st, dev_vals, nx, ny, bx, by, step, W, map, err)) return -1;
-  SELCHK(hipStreamSynchronize(st));
+  // no wait here: the whole map's first refinement queues behind the map's
+  // preparation, and the walk's first wait covers both (us[0] is host time)
   e->us[0] = now_us() - t_start;
   const int np = nx * ny;
   LazySort ls{e, st, {}, err};

@@ -29,11 +29,16 @@ def test_eigen_map_bit_exact(gpu, oracle, shape):
     assert pts[0, 0] == b and pts[0, 1] == b and pts[nx, 1] == b + 1
 
 
-def test_eigen_map_skipped_pixels(gpu, oracle):
-    img = synth(gpu, 3, 320, 240, 1)[0]
+@pytest.mark.parametrize("skip,window", [(1, 7), (2, 7), (0, 9), (1, 5)])
+def test_eigen_map_skipped_pixels(gpu, oracle, skip, window):
+    """Grid steps and windows: the tiled 7x7 kernel serves steps 1-2
+    (k_min_eigen7), the per-point kernel every other case; both equal the
+    oracle value for value."""
+    img = synth(gpu, 3 + skip, 333, 251, 1)[0]
 
     def setup(t):
-        t.nSkippedPixels = 2
+        t.nSkippedPixels = skip
+        t.window_width = t.window_height = window
 
     dev = Dev(gpu, setup)
     dev.build(img, nlevels=1)
