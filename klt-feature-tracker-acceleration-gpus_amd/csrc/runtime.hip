@@ -294,6 +294,39 @@ hipEvent_t take_event(klt_hip_ctx *c) {
 }
 
 // HIP events around one launch, recorded on the stream the kernel runs on
+#ifdef KLT_HOST_PROF  // experiment builds: CLOCK_MONOTONIC marks through one call, printed to stderr
+struct HostMarks {
+  long t[32];
+  const char *what[32];
+  int n = 0;
+  void mark(const char *w) {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    if (n < 32) {
+      t[n] = ts.tv_sec * 1000000000L + ts.tv_nsec;
+      what[n++] = w;
+    }
+  }
+  HostMarks();
+  ~HostMarks() {
+    cur() = nullptr;
+    for (int i = 1; i < n; ++i) fprintf(stderr, "hostmark %s %.2f us\n", what[i], (t[i] - t[i - 1]) * 1e-3);
+    if (n) fprintf(stderr, "hostmark enter_ns %ld\n", t[0]);
+  }
+  static HostMarks *&cur() {
+    static thread_local HostMarks *p = nullptr;
+    return p;
+  }
+};
+inline HostMarks::HostMarks() { cur() = this; }
+#define HMARK(w) hm_.mark(w)
+#define HMARK_IN(w) \
+  if (HostMarks::cur()) HostMarks::cur()->mark(w)
+#else
+#define HMARK(w) (void)0
+#define HMARK_IN(w) (void)0
+#endif
+
 struct TimedScope {
   klt_hip_ctx *c;
   int cls;
@@ -651,6 +684,7 @@ int track_frames_launch(klt_hip_ctx *c, hipStream_t st, const klt_hip_track_desc
       }
     }
   }
+  HMARK_IN("track_args");
   if (t7) return launched(c, "k_track7", launch_track7(st, aa.escape != nullptr, aa, b2, x, y, v, n, &c->track_kernel));
   c->track_kernel = "kltdev::k_track_frames_g";
   return launched(c, "k_track_frames", launch_track_frames(st, exact, li, patch, win7, npx, aa, b2, x, y, v, n));
@@ -843,11 +877,13 @@ int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const u
     K.vhi[1] = yhi >= H1 ? (1 << 30) : yhi;
     if (yhi > ylo) {
       const int t1lo = ylo / TH1, t1hi = clampi((yhi + TH1 - 1) / TH1, t1lo, nt1);
+      HMARK_IN("l0_launched");
       TimedScope ts(c, T_L1, st, F);
       const int vec = (W1 % 4 == 0 && W1 >= 8) ? 1 : 0;
       if (launched(c, "k_pyr_l1", launch_pyr_l1(st, K.hs, W1, H, H1, T, vec, K.lv[1].img, K.lv[1].gx, K.lv[1].gy,
                                                 fsh, np * fs1, F, t1lo, t1hi, il)))
         return -1;
+      HMARK_IN("l1_launched");
     }
   }
   return 0;
@@ -1710,28 +1746,6 @@ void band_planes(const BandSpec &b, int &p0, int &p1) {
   if (p1 < p0) p1 = p0;
 }
 
-#ifdef KLT_HOST_PROF  // experiment builds: CLOCK_MONOTONIC marks through one call, printed to stderr
-struct HostMarks {
-  long t[16];
-  const char *what[16];
-  int n = 0;
-  void mark(const char *w) {
-    timespec ts;
-    clock_gettime(CLOCK_MONOTONIC, &ts);
-    if (n < 16) {
-      t[n] = ts.tv_sec * 1000000000L + ts.tv_nsec;
-      what[n++] = w;
-    }
-  }
-  ~HostMarks() {
-    for (int i = 1; i < n; ++i) fprintf(stderr, "hostmark %s %.2f us\n", what[i], (t[i] - t[i - 1]) * 1e-3);
-    if (n) fprintf(stderr, "hostmark enter_ns %ld\n", t[0]);
-  }
-};
-#define HMARK(w) hm_.mark(w)
-#else
-#define HMARK(w) (void)0
-#endif
 
 int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_track_desc *td,
                       const unsigned char *frames, long pitch, long stride, int nframes, int chunk, float *x,
