@@ -1948,10 +1948,16 @@ KLT_API int klt_hip_track_frames(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, con
 // host slot (a third stream), and the pool hands them to the caller's
 // callback.  Two slots of each: the upload of chunk c+1 and the delivery of
 // chunk c-1 run on the host while chunk c is on the device.
-namespace {
-int host_pipeline_prepare(klt_hip_ctx *c, size_t stage_bytes, size_t rows_bytes) {
+// the copy streams of the host pipeline (KLTTrackSequence)
+static int copy_streams(klt_hip_ctx *c) {
   for (hipStream_t *st : {&c->cstream, &c->dstream})
     if (!*st) HIPCHK(c, hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+  return 0;
+}
+
+namespace {
+int host_pipeline_prepare(klt_hip_ctx *c, size_t stage_bytes, size_t rows_bytes) {
+  if (copy_streams(c)) return -1;
   for (int k = 0; k < 2; ++k)
     for (hipEvent_t *e : {&c->ev_ring_free[k], &c->ev_dma[k], &c->ev_tracked[k], &c->ev_rows[k]})
       if (!*e) HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
@@ -2156,6 +2162,7 @@ static SelEngine *sel_of(klt_hip_ctx *c) {
   if (!c->sel) c->sel = sel_engine_create();
   return c->sel;
 }
+
 
 KLT_API int klt_hip_select(klt_hip_ctx *c, int s, const klt_hip_select_desc *d, int ncols, int nrows, int mindist,
                            int min_eigenvalue, int overwrite_all, float *x, float *y, int *val,

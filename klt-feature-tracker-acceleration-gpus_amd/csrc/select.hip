@@ -334,7 +334,6 @@ struct SelGraph {
 
 struct SelEngine {
   std::vector<SelGraph> graphs;
-  hipStream_t cap = nullptr;  // capture only
   int2 *d_kv = nullptr;
   size_t kv_cap = 0;
   int *d_cnt = nullptr, *d_off = nullptr, *d_posL = nullptr, *d_posR = nullptr;
@@ -347,12 +346,7 @@ struct SelEngine {
   int *d_f = nullptr, *h_f = nullptr;  // the live features for the paint: x | y | val, n each
   size_t f_cap = 0, hf_cap = 0;
   hipEvent_t ev_dl = nullptr, ev_ref = nullptr;  // a segment download done / a look-ahead refinement done
-  // segment downloads run on a stream of their own: a look-ahead refinement
-  // queued on the selection stream (other positions of d_kv) does not delay
-  // them; ev_prep orders them after the map's preparation once per run
-  hipStream_t dl = nullptr;
-  hipEvent_t ev_prep = nullptr;
-  bool dl_ordered = false;
+
   int threshold = sel_default_threshold();  // segments at most this long go to the host
   // statistics of the last run
   long downloaded = 0, device_steps = 0, visited = 0;
@@ -445,22 +439,44 @@ int refine_launch(SelEngine *e, hipStream_t st, Seg g, std::string *err) {
           k.off == e->d_off && k.posL == e->d_posL && k.posR == e->d_posR)
         ex = k.exec;
     if (!ex) {
-      if (!e->cap) SELCHK(hipStreamCreateWithFlags(&e->cap, hipStreamNonBlocking));
-      SELCHK(hipStreamBeginCapture(e->cap, hipStreamCaptureModeThreadLocal));
-      for (int l = 0; l < levels; ++l) {
-        hipLaunchKernelGGL(k_sel_pivot, dim3(1), dim3(1), 0, e->cap, e->d_state, e->d_kv, T);
-        hipLaunchKernelGGL(k_sel_count, dim3(nbp), dim3(kSelThreads), 0, e->cap, e->d_state, e->d_kv, e->d_cnt);
-        hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(kSelScanThreads), 0, e->cap, e->d_state, e->d_cnt, e->d_off);
-        hipLaunchKernelGGL(k_sel_rank, dim3(nbp), dim3(kSelThreads), 0, e->cap, e->d_state, e->d_kv, e->d_off,
-                           e->d_posL, e->d_posR);
-        hipLaunchKernelGGL(k_sel_swap, dim3(swp), dim3(kSelThreads), 0, e->cap, e->d_state, e->d_kv, e->d_posL,
-                           e->d_posR);
-      }
+      // built node by node (no capture stream: a stream of its own would take
+      // a hardware queue the context's other streams may need)
       hipGraph_t gr = nullptr;
-      SELCHK(hipStreamEndCapture(e->cap, &gr));
-      const hipError_t ie = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
+      SELCHK(hipGraphCreate(&gr, 0));
+      hipGraphNode_t prev = nullptr;
+      hipError_t ge = hipSuccess;
+      auto add = [&](const void *fn, unsigned grid, unsigned block, void **args) {
+        if (ge != hipSuccess) return;
+        hipKernelNodeParams kp{};
+        kp.func = const_cast<void *>(fn);
+        kp.gridDim = dim3(grid);
+        kp.blockDim = dim3(block);
+        kp.sharedMemBytes = 0;
+        kp.kernelParams = args;
+        kp.extra = nullptr;
+        hipGraphNode_t node = nullptr;
+        ge = hipGraphAddKernelNode(&node, gr, prev ? &prev : nullptr, prev ? 1 : 0, &kp);
+        prev = node;
+      };
+      SelState *ds = e->d_state;
+      int2 *kv = e->d_kv;
+      int *cnt = e->d_cnt, *off = e->d_off, *pl = e->d_posL, *pr = e->d_posR;
+      int thr = T;
+      void *a_pivot[] = {&ds, &kv, &thr};
+      void *a_count[] = {&ds, &kv, &cnt};
+      void *a_scan[] = {&ds, &cnt, &off};
+      void *a_rank[] = {&ds, &kv, &off, &pl, &pr};
+      void *a_swap[] = {&ds, &kv, &pl, &pr};
+      for (int l = 0; l < levels; ++l) {
+        add(reinterpret_cast<const void *>(k_sel_pivot), 1, 1, a_pivot);
+        add(reinterpret_cast<const void *>(k_sel_count), nbp, kSelThreads, a_count);
+        add(reinterpret_cast<const void *>(k_sel_scan), 1, kSelScanThreads, a_scan);
+        add(reinterpret_cast<const void *>(k_sel_rank), nbp, kSelThreads, a_rank);
+        add(reinterpret_cast<const void *>(k_sel_swap), swp, kSelThreads, a_swap);
+      }
+      if (ge == hipSuccess) ge = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
       hipGraphDestroy(gr);
-      SELCHK(ie);
+      SELCHK(ge);
       if (e->graphs.size() >= 24) {  // bounded: drop the oldest
         hipGraphExecDestroy(e->graphs.front().exec);
         e->graphs.erase(e->graphs.begin());
@@ -562,18 +578,9 @@ struct LazySort {
           continue;
         }
         const double t0 = now_us();
-        // g's positions are final: it comes from the preparation (ordered
-        // below) or from a refinement whose state the host has already read
-        if (!e->dl_ordered && (hipEventRecord(e->ev_prep, st) != hipSuccess ||
-                               hipStreamWaitEvent(e->dl, e->ev_prep, 0) != hipSuccess)) {
-          if (err) *err = "select: download ordering failed";
-          failed = 1;
-          return -1;
-        }
-        e->dl_ordered = true;
         if (hipMemcpyAsync(e->h_kv + g.start, e->d_kv + g.start, sizeof(int2) * (size_t)g.len,
-                           hipMemcpyDeviceToHost, e->dl) != hipSuccess ||
-            hipEventRecord(e->ev_dl, e->dl) != hipSuccess) {
+                           hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipEventRecord(e->ev_dl, st) != hipSuccess) {
           if (err) *err = "select: segment download failed";
           failed = 1;
           return -1;
@@ -681,13 +688,7 @@ void sel_engine_destroy(SelEngine *e) {
   if (e->h_f) hipHostFree(e->h_f);
   if (e->ev_dl) hipEventDestroy(e->ev_dl);
   if (e->ev_ref) hipEventDestroy(e->ev_ref);
-  if (e->ev_prep) hipEventDestroy(e->ev_prep);
   for (const SelGraph &k : e->graphs) hipGraphExecDestroy(k.exec);
-  if (e->cap) hipStreamDestroy(e->cap);
-  if (e->dl) {
-    (void)hipStreamSynchronize(e->dl);
-    hipStreamDestroy(e->dl);
-  }
   if (e->h_kv) hipHostFree(e->h_kv);
   delete e;
 }
@@ -710,9 +711,6 @@ static int sel_prepare(SelEngine *e, hipStream_t st, const int *dev_vals, int nx
   if (!e->h_state) SELCHK(hipHostMalloc((void **)&e->h_state, sizeof(SelState), hipHostMallocDefault));
   if (!e->ev_dl) SELCHK(hipEventCreateWithFlags(&e->ev_dl, hipEventDisableTiming));
   if (!e->ev_ref) SELCHK(hipEventCreateWithFlags(&e->ev_ref, hipEventDisableTiming));
-  if (!e->ev_prep) SELCHK(hipEventCreateWithFlags(&e->ev_prep, hipEventDisableTiming));
-  if (!e->dl) SELCHK(hipStreamCreateWithFlags(&e->dl, hipStreamNonBlocking));
-  e->dl_ordered = false;
   if (e->hkv_cap < n) {
     if (e->h_kv) hipHostFree(e->h_kv);
     e->h_kv = nullptr;
