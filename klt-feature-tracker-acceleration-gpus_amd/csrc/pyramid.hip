@@ -33,9 +33,6 @@ namespace {
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-#ifndef KLT_L0_D3_READ2  // k_pyr_l0's sigma-3.6 rows pass reads its tap pairs with ds_read2_b32 (A/B: -D...=0)
-#define KLT_L0_D3_READ2 0
-#endif
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f4 ld4(const float *p) { return *reinterpret_cast<const f4 *>(p); }
@@ -367,25 +364,6 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     const int i = tid - (NT - TH * (TW / 16));
     const int r = i / (TW / 16), q = i - r * (TW / 16);
     const float *row = im + (r + RG) * PI + 16 * q;  // idx 16q <-> global C0+16q-8
-#if KLT_L0_D3_READ2
-    // outputs e and e+1 are 4 columns apart: the pair (row[j], row[j+4]) of
-    // every tap comes straight from LDS into an aligned register pair (one
-    // ds_read2_b32 each), where 16-byte reads needed two moves per pair
-    f2 pr[29];
-    const unsigned lb = (unsigned)(size_t)(__attribute__((address_space(3))) const float *)row;
-#pragma unroll
-    for (int j = 0; j < 29; ++j)
-      asm volatile("ds_read2_b32 %0, %1 offset0:%2 offset1:%3" : "=v"(pr[j]) : "v"(lb), "i"(j), "i"(j + 4) : "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm reads are invisible to the compiler's wait counts
-    f2 a01 = pr[0] * f2{T.p[0], T.p[0]};  // terms >= +0
-    f2 a23 = pr[8] * f2{T.p[0], T.p[0]};
-#pragma unroll
-    for (int m = 1; m < 21; ++m) {
-      const f2 kk = {T.p[m], T.p[m]};
-      a01 += pr[m] * kk;
-      a23 += pr[m + 8] * kk;
-    }
-#else
     float v[36];
 #pragma unroll
     for (int k = 0; k < 9; ++k) *reinterpret_cast<f4 *>(v + 4 * k) = ld4(row + 4 * k);
@@ -397,7 +375,6 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
       a01 += f2{v[m], v[m + 4]} * kk;
       a23 += f2{v[m + 8], v[m + 12]} * kk;
     }
-#endif
     const int y = R0 + r;
     const int X = C0 / SS + 4 * q;
     if (INT) {
