@@ -461,7 +461,7 @@ def run_sharded(args, world, rank, dev) -> None:
                           margin=args.margin)
     seq.begin(0)
     seq.run(1, args.warmup)
-    live_before = int((v >= 0).sum().item())
+    v_warm = v.clone()  # the live count after the warm-up, read after the timed region (as in the default mode)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -469,6 +469,7 @@ def run_sharded(args, world, rank, dev) -> None:
     seq.run(1 + args.warmup, args.steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    live_before = int((v_warm >= 0).sum().item())
     if world > 1:
         dist.barrier()
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
