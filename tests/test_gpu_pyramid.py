@@ -49,7 +49,11 @@ def test_fused_pyramid_real_frames(gpu, oracle, frames):
         assert_planes_equal(dev.levels(0, 2), ot.frame_pyramid(img), "images_provided")
 
 
-STRIP_SHAPES = [(480, 640), (1080, 1920), (67, 136), (31, 40), (9, 64), (200, 72), (2160, 3840)]
+# (2001, 2100), (2003, 2050), (2160, 3840): whole frames of >= 2000 rows run
+# the 64-row level-0 tiles (pyramid.hip kL0WideMinRows), with a partial last
+# tile row, a partial last tile column and (2050) no 4-byte row alignment
+STRIP_SHAPES = [(480, 640), (1080, 1920), (67, 136), (31, 40), (9, 64), (200, 72), (2160, 3840), (2001, 2100),
+                (2003, 2050)]
 
 
 @pytest.mark.parametrize("shape", STRIP_SHAPES)
