@@ -206,7 +206,7 @@ int ctx_fail(klt_hip_ctx *c, const char *fmt, ...);
 // select.hip: exact lazy selection (the reference's quicksort order) with the
 // top-level partition steps on the device
 struct SelEngine;
-constexpr int kSelDefaultThreshold = 32768;  // map points: longer segments are split on the device
+constexpr int kSelDefaultThreshold = 49152;  // map points: longer segments are split on the device (tools/exp/r04ah.sh)
 SelEngine *sel_engine_create();
 void sel_engine_destroy(SelEngine *e);
 void sel_engine_set_threshold(SelEngine *e, int threshold);

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 4: selection threshold 49152 by default: selection/REPLACE parity and the API legs
+set -o pipefail
+OUT=gpurun_out/r04ai; mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_select.py tests/test_gpu_select_engine.py "tests/test_gpu_long.py::test_replace_harness_config3r" "tests/test_shard.py::test_c_shard_replace_equals_single_gpu" "tests/test_shard.py::test_sharded_sequence_replace_equals_oracle" tests/test_abi.py -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
+tail -1 $OUT/tests.log
+Q="--steps 20 --warmup 5 --no-cpu --no-4k --no-fast"
+for i in 1 2; do
+  timeout -k 10 300 python3 bench.py $Q > $OUT/b.json 2> $OUT/b.err || { tail -5 $OUT/b.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$OUT/b.json'))['api']; print({k: round(v['value']) for k,v in d.items() if isinstance(v, dict) and 'value' in v}, round(d['replace']['us_per_replace_median']), d['replace']['parity']['columns_mismatched'])"
+done
