@@ -143,7 +143,7 @@ def main():
         fl = lib.KLTCreateFeatureList(a.features)
         lib.KLTSelectGoodFeatures(tc, u8(host[0]), W, H, fl)
         ft = lib.KLTCreateFeatureTable(nh - 1, a.features)
-        for rep in range(3):
+        for rep in range(a.reps if a.reps < 50 else 3):  # apiseq: --reps below 50 sets the call count
             fl = lib.KLTCreateFeatureList(a.features)
             lib.KLTSelectGoodFeatures(tc, u8(host[0]), W, H, fl)
             t0 = time.perf_counter()
