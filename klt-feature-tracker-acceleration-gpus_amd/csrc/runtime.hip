@@ -137,6 +137,26 @@ struct HostPool {
 
 constexpr int kMaxCopyThreads = 16;  // copy-pool workers per device context, at most
 
+// host copy workers of a new context (KLT_AMD_HOST_THREADS; default 7) and
+// the piece a worker copies at a time (KLT_AMD_COPY_PIECE bytes; default 64 KiB):
+// tuning hooks, any value gives the same results
+static int default_host_threads() {
+  static const int n = [] {
+    const char *v = getenv("KLT_AMD_HOST_THREADS");
+    const int x = v && *v ? atoi(v) : 7;
+    return x < 0 ? 0 : x > 63 ? 63 : x;
+  }();
+  return n;
+}
+static size_t copy_piece() {
+  static const size_t n = [] {
+    const char *v = getenv("KLT_AMD_COPY_PIECE");
+    const long x = v && *v ? atol(v) : 64L << 10;
+    return (size_t)(x < 4096 ? 4096 : x);
+  }();
+  return n;
+}
+
 struct klt_hip_ctx {
   int device = 0;
   hipStream_t own = nullptr;
@@ -210,7 +230,7 @@ struct klt_hip_ctx {
   hipStream_t cstream = nullptr, dstream = nullptr;
   hipEvent_t ev_ring_free[2] = {}, ev_dma[2] = {}, ev_tracked[2] = {}, ev_rows[2] = {};
   HostPool *pool = nullptr;
-  int copy_threads = 7;  // pool workers besides the caller (0: the caller alone)
+  int copy_threads = default_host_threads();  // pool workers besides the caller (0: the caller alone)
   unsigned long long *prof = nullptr;  // instrumented build: per-wave tracker phase counters
   Bank bank[3];  // views into bank_arena
   void *bank_arena = nullptr;
@@ -1026,10 +1046,10 @@ KLT_API int klt_hip_ctx_reset(klt_hip_ctx *c) {
     c->stage_cap = c->hrows_cap = 0;
     c->prev = PrevRef{};
   }
-  if (c->copy_threads != 7) {
+  if (c->copy_threads != default_host_threads()) {
     delete c->pool;  // idle between calls; joined here
     c->pool = nullptr;
-    c->copy_threads = 7;
+    c->copy_threads = default_host_threads();
   }
   c->feat_mode = 2;
   for (auto &r : c->registered) (void)hipHostUnregister(const_cast<unsigned char *>(r.first));
@@ -1121,7 +1141,7 @@ KLT_API int klt_hip_upload_frame(klt_hip_ctx *c, int buf, const unsigned char *h
   // in groups: the host pool copies group g+1 into pinned memory while group
   // g's DMA runs
   ensure_pool(c);
-  const size_t group = n >= (1u << 20) ? (n + 3) / 4 : n, piece = 64 << 10;
+  const size_t group = n >= (1u << 20) ? (n + 3) / 4 : n, piece = copy_piece();
   for (size_t o = 0; o < n; o += group) {
     const size_t m = n - o < group ? n - o : group;
     unsigned char *dst = c->h_u8[buf] + o;
