@@ -144,7 +144,7 @@ static int default_host_threads() {
   static const int n = [] {
     const char *v = getenv("KLT_AMD_HOST_THREADS");
     const int x = v && *v ? atoi(v) : 7;
-    return x < 0 ? 0 : x > 63 ? 63 : x;
+    return x < 0 ? 0 : x > kMaxCopyThreads ? kMaxCopyThreads : x;  // klt_hip_set_host_threads' range
   }();
   return n;
 }
