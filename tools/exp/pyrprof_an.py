@@ -23,6 +23,11 @@ for k, n in enumerate(names):
     print(f"  {n:24s} median {np.median(d[inter, k]):8.0f}  mean {d[inter, k].mean():8.0f} cycles")
 life = t[:, 5] - t[:, 0]
 print(f"  {'entry -> last stamp':24s} median {np.median(life[inter]):8.0f}  mean {life[inter].mean():8.0f}")
+if (~inter).any():  # edge tiles: clamped loads and per-element zero-border rules
+    print(f"  edge tiles ({(~inter).sum()}):")
+    for k, n in enumerate(names):
+        print(f"  {n:24s} median {np.median(d[~inter, k]):8.0f}  mean {d[~inter, k].mean():8.0f} cycles")
+    print(f"  {'entry -> last stamp':24s} median {np.median(life[~inter]):8.0f}  mean {life[~inter].mean():8.0f}")
 gaps, conc = [], []
 for k in np.unique(key):
     m = key == k
