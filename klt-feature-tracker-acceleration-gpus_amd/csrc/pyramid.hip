@@ -145,8 +145,19 @@ __device__ unsigned long long *g_pyr_prof;
 #define PYR_STAMP(k)                                                                                  \
   if (g_pyr_prof && tid == 0)                                                                         \
     g_pyr_prof[((long)blockIdx.z * gridDim.x + blockIdx.x) * 8 + (k)] = clock64();
+// the last stamp, where the workgroup ran, and whether the tile was interior
+#define PYR_END()                                                                                    \
+  __syncthreads();                                                                                    \
+  PYR_STAMP(5)                                                                                        \
+  if (g_pyr_prof && tid == 0) {                                                                       \
+    const long o_ = ((long)blockIdx.z * gridDim.x + blockIdx.x) * 8;                                  \
+    g_pyr_prof[o_ + 6] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |    \
+                         (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4); /* XCC_ID : HW_ID */    \
+    g_pyr_prof[o_ + 7] = INT ? 1 : 0;                                                                 \
+  }
 #else
 #define PYR_STAMP(k)
+#define PYR_END()
 #endif
 
 // Edge tiles (INT false) clamp their loads and apply the zero-border rules per
@@ -182,6 +193,28 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     const int i = min(tid, NR * NQ - 1);
     const int r = i / NQ, q = i - r * NQ;
     const uint4 c = *reinterpret_cast<const uint4 *>(src + (unsigned)((R0 - RG - RS + r) * spitch + C0 - 12 + 16 * q));
+    *reinterpret_cast<uint4 *>(reinterpret_cast<uint32_t *>(u) + r * PUB + 4 * q) = c;
+  } else if (vec_u8) {
+    // edge tile: the interior's one 16-byte chunk per thread (the same rows),
+    // rows clamped into the frame; a chunk that crosses the frame's left or
+    // right edge is loaded as four dwords, each clamped into the frame.  Bytes
+    // outside the frame feed only t1 columns x < RS or >= W-RS and rows
+    // y < RS or >= H-RS, which the zero-border rules overwrite before any
+    // later pass reads them, so the clamps only keep the addresses inside the
+    // frame; every in-frame dword (W % 4 == 0 under vec_u8) is exact
+    const int i = min(tid, NR * NQ - 1);
+    const int r = i / NQ, q = i - r * NQ;
+    const uint8_t *row = src + (unsigned)(clampi(R0 - RG - RS + r, 0, H - 1) * spitch);
+    const int x = C0 - 12 + 16 * q;
+    uint4 c;
+    if (x >= 0 && x + 16 <= W) {
+      c = *reinterpret_cast<const uint4 *>(row + x);
+    } else {
+      c.x = *reinterpret_cast<const uint32_t *>(row + clampi(x, 0, W - 4));
+      c.y = *reinterpret_cast<const uint32_t *>(row + clampi(x + 4, 0, W - 4));
+      c.z = *reinterpret_cast<const uint32_t *>(row + clampi(x + 8, 0, W - 4));
+      c.w = *reinterpret_cast<const uint32_t *>(row + clampi(x + 12, 0, W - 4));
+    }
     *reinterpret_cast<uint4 *>(reinterpret_cast<uint32_t *>(u) + r * PUB + 4 * q) = c;
   } else {
     constexpr int NA = UH * UQ, PER = (NA + NT - 1) / NT;
@@ -380,11 +413,18 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     if (INT) {
       *reinterpret_cast<f4 *>(hs + hs_at32(y, X, H)) = f4{a01.x, a01.y, a23.x, a23.y};
     } else if (y < H) {
-      const float o[4] = {a01.x, a01.y, a23.x, a23.y};
+      float o[4] = {a01.x, a01.y, a23.x, a23.y};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int c = C0 + 16 * q + 4 * e + 2;
-        if (X + e < hsW) hs[hs_at32(y, X + e, H)] = (c >= RP && c < W - RP) ? o[e] : 0.0f;
+        if (!(c >= RP && c < W - RP)) o[e] = 0.0f;
+      }
+      if (X + 3 < hsW) {  // X % 4 == 0: four columns of one slab
+        *reinterpret_cast<f4 *>(hs + hs_at32(y, X, H)) = f4{o[0], o[1], o[2], o[3]};
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (X + e < hsW) hs[hs_at32(y, X + e, H)] = o[e];
       }
     }
   }
@@ -427,11 +467,10 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
       } else {
         if (y >= H || x >= W) continue;
         const bool zr = !(y >= RG && y < H - RG);
-        o[kRecGx] = zr ? 0.0f : gg[k].x;
-        o[kRecGy] = zr ? 0.0f : gg[k].y;
-        o[kRecImg] = iv;
+        st3_out(o, f3u{zr ? 0.0f : gg[k].x, zr ? 0.0f : gg[k].y, iv});  // the whole record, as interior tiles
       }
     }
+    PYR_END()
     return;
   }
   // E. columns passes of both gradients; zero unless RG <= y < H-RG.  4 rows x
@@ -502,16 +541,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
       }
     }
   }
-#ifdef KLT_PYR_PROF
-  __syncthreads();
-  PYR_STAMP(5)
-  if (g_pyr_prof && tid == 0) {
-    const long o = ((long)blockIdx.z * gridDim.x + blockIdx.x) * 8;
-    g_pyr_prof[o + 6] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
-                        (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);  // XCC_ID : HW_ID
-    g_pyr_prof[o + 7] = INT ? 1 : 0;
-  }
-#endif
+  PYR_END()
 }
 
 template <bool IL, int TH_>
