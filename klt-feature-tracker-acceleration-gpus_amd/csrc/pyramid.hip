@@ -169,7 +169,8 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
                                             int W, int H, const DefTaps &T, int vec_u8,
                                             float *__restrict__ img0, float *__restrict__ gx0,
                                             float *__restrict__ gy0, float *__restrict__ hs, int hsW,
-                                            int do_hs, int vec_out, int C0, int R0, int tid, bool planes) {
+                                            int do_hs, int vec_out, int C0, int R0, int tid, bool planes,
+                                            bool cols_in, bool rows_in) {
   using G = L0G<TH_>;
   constexpr int RS = G::RS, RG = G::RG, RP = G::RP, SS = G::SS, TW = G::TW, TH = G::TH, NT = G::NT;
   constexpr int UQ = G::UQ, UH = G::UH, NG = G::NG, IH = G::IH, IHB = G::IHB, PT = G::PT, PI = G::PI, PX = G::PX,
@@ -272,7 +273,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
         mac4(a0, v + 2 + m, T.s[m]);
         mac4(a1, v + 6 + m, T.s[m]);
       }
-      if (!INT) {
+      if (!INT && !cols_in) {
         const int x = C0 - 8 + 8 * j;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -300,7 +301,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
       f4 acc = mul4(reinterpret_cast<const float *>(&v[rr]), T.s[0]);
 #pragma unroll
       for (int m = 1; m < 5; ++m) mac4(acc, reinterpret_cast<const float *>(&v[rr + m]), T.s[m]);
-      if (!INT) {
+      if (!INT && !rows_in) {
         const int y = R0 - RG + 4 * b + rr;
         if (!(y >= RS && y < H - RS)) acc = f4{0.0f, 0.0f, 0.0f, 0.0f};
       }
@@ -354,7 +355,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
       for (int m = 1; m < 7; ++m)
 #pragma unroll
         for (int e = 0; e < 4; ++e) p[e] += f2{v[1 + e + m], v[1 + e + m]} * f2{T.d[m], T.g[m]};
-      if (!INT) {
+      if (!INT && !cols_in) {
         const int x = C0 + 4 * g;
 #pragma unroll
         for (int e = 0; e < 4; ++e)
@@ -377,7 +378,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
       if (m != kDC) mac4(ax, v + 1 + m, T.d[m]);  // zero centre tap: exact to skip (see kDC)
       if (m > 0) mac4(ay, v + 1 + m, T.g[m]);
     }
-    if (!INT) {
+    if (!INT && !cols_in) {
       const int x = C0 + 4 * g;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -414,10 +415,12 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
       *reinterpret_cast<f4 *>(hs + hs_at32(y, X, H)) = f4{a01.x, a01.y, a23.x, a23.y};
     } else if (y < H) {
       float o[4] = {a01.x, a01.y, a23.x, a23.y};
+      if (!cols_in) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int c = C0 + 16 * q + 4 * e + 2;
-        if (!(c >= RP && c < W - RP)) o[e] = 0.0f;
+        for (int e = 0; e < 4; ++e) {
+          const int c = C0 + 16 * q + 4 * e + 2;
+          if (!(c >= RP && c < W - RP)) o[e] = 0.0f;
+        }
       }
       if (X + 3 < hsW) {  // X % 4 == 0: four columns of one slab
         *reinterpret_cast<f4 *>(hs + hs_at32(y, X, H)) = f4{o[0], o[1], o[2], o[3]};
@@ -459,15 +462,15 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     const unsigned lo = 12u * (unsigned)c, rs = 12u * (unsigned)W;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int y = R0 + w8 + k;
+      const int y = R0 + w8 + k;  // wave-uniform
       const float iv = im[(w8 + k + RG) * PI + 8 + c];
-      float *o = img0 + 3u * (unsigned)(y * W + x);
+      float *o = reinterpret_cast<float *>(rb + (lo + k * rs));
       if (INT) {
-        st3_out(reinterpret_cast<float *>(rb + (lo + k * rs)), f3u{gg[k].x, gg[k].y, iv});
+        st3_out(o, f3u{gg[k].x, gg[k].y, iv});
       } else {
-        if (y >= H || x >= W) continue;
-        const bool zr = !(y >= RG && y < H - RG);
-        st3_out(o, f3u{zr ? 0.0f : gg[k].x, zr ? 0.0f : gg[k].y, iv});  // the whole record, as interior tiles
+        if (y >= H) break;
+        const bool zr = !rows_in && !(y >= RG && y < H - RG);
+        if (x < W) st3_out(o, f3u{zr ? 0.0f : gg[k].x, zr ? 0.0f : gg[k].y, iv});  // the whole record
       }
     }
     PYR_END()
@@ -567,15 +570,17 @@ __global__ __launch_bounds__(L0G<TH_>::NT) void k_pyr_l0(const uint8_t *__restri
   gy0 += blockIdx.z * fs0;
   hs += blockIdx.z * fs_hs;
   // interior: unclamped aligned loads, no zero-border rule applies, all stores in bounds
-  const bool interior = vec_u8 && vec_out && (hsW * G::SS == W) && (hsW % 2 == 0) && C0 >= 12 && C0 + 84 <= W &&
-                        R0 >= 5 && R0 + G::TH + 7 <= H;
+  // the frame edge only left / right (rows_in) or only above / below (cols_in):
+  // an edge tile then skips the other direction's zero-border tests
+  const bool cols_in = C0 >= 12 && C0 + 84 <= W, rows_in = R0 >= 5 && R0 + G::TH + 7 <= H;
+  const bool interior = vec_u8 && vec_out && (hsW * G::SS == W) && (hsW % 2 == 0) && cols_in && rows_in;
   const bool planes = by + ty0 >= py0 && by + ty0 < py1;  // tile rows [py0, py1) store img0, gx0, gy0
   if (interior)
     pyr_l0_tile<true, IL, TH_>(lds, src, spitch, W, H, T, vec_u8, img0, gx0, gy0, hs, hsW, do_hs, vec_out, C0, R0,
-                               threadIdx.x, planes);
+                               threadIdx.x, planes, true, true);
   else
     pyr_l0_tile<false, IL, TH_>(lds, src, spitch, W, H, T, vec_u8, img0, gx0, gy0, hs, hsW, do_hs, vec_out, C0, R0,
-                                threadIdx.x, planes);
+                                threadIdx.x, planes, cols_in, rows_in);
 }
 
 // ---------------------------------------------------------------------------
