@@ -619,6 +619,10 @@ __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs,
   if (!xcd_tile(tiles_x, tiles_y, bx, by)) return;
   const int x0 = bx * TW, y0 = (by + ty0) * TH;
   const int tid = threadIdx.x;
+  // every img1 row and column the tile computes passes the zero-border rules
+  // (rows: 0 <= Y < H1 and RP <= 4Y+2 < H-RP; columns: 0 <= X < W1 and the
+  // gradient rows' RG <= X < W1-RG): the per-element tests are skipped
+  const bool in1 = y0 >= 5 && SS * (y0 + TH + 2) + SS / 2 < H - RP && y0 + TH + 2 < H1 && x0 >= 4 && x0 + 36 <= W1;
 
   {
     constexpr int NQ = JW / 4, NA = HR * NQ, PER = (NA + NT - 1) / NT;
@@ -656,11 +660,13 @@ __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs,
       const f4 v = ld4(col + m * JW);
       mac4(acc, reinterpret_cast<const float *>(&v), T.p[m]);
     }
-    const int Y = y0 - RG + r, X = x0 - 4 + 4 * g, rr = SS * Y + SS / 2;
-    const bool rowok = Y >= 0 && Y < H1 && rr >= RP && rr < H - RP;
+    if (!in1) {
+      const int Y = y0 - RG + r, X = x0 - 4 + 4 * g, rr = SS * Y + SS / 2;
+      const bool rowok = Y >= 0 && Y < H1 && rr >= RP && rr < H - RP;
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (!(rowok && X + e >= 0 && X + e < W1)) acc[e] = 0.0f;
+      for (int e = 0; e < 4; ++e)
+        if (!(rowok && X + e >= 0 && X + e < W1)) acc[e] = 0.0f;
+    }
     st4(im + r * JW + 4 * g, acc);
   }
   __syncthreads();
@@ -688,12 +694,14 @@ __global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs,
       if (m != kDC) mac4(ax, v + 1 + m, T.d[m]);
       if (m > 0) mac4(ay, v + 1 + m, T.g[m]);
     }
-    const int X = x0 + 4 * g;
+    if (!in1) {
+      const int X = x0 + 4 * g;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      if (!(X + e >= RG && X + e < W1 - RG)) {
-        ax[e] = 0.0f;
-        ay[e] = 0.0f;
+      for (int e = 0; e < 4; ++e) {
+        if (!(X + e >= RG && X + e < W1 - RG)) {
+          ax[e] = 0.0f;
+          ay[e] = 0.0f;
+        }
       }
     }
     st4(tx + r * TW + 4 * g, ax);
