@@ -68,19 +68,24 @@ const char *klt_shard_last_error(klt_shard *s);
    cannot take part at all (its exchange buffers cannot be allocated) aborts
    the communicator (ncclCommAbort) so that its peers' collectives fail; the
    shard is then unusable.  Entry points restore the caller's current device. */
-/* Fault injection (tests of the failure agreement above on one rank; 0
-   clears, the faults persist until then).  LOCAL: this rank's band tracking
+#ifdef KLT_SHARD_TESTING
+/* TEST-ONLY fault injection (tests of the failure agreement above on one
+   rank; 0 clears, the faults persist until then).  Declared only with
+   KLT_SHARD_TESTING defined, and inert unless the process runs with the
+   environment variable KLT_SHARD_TESTING=1 (it then returns -2 and changes
+   nothing), so no production caller can abort a communicator through it.  LOCAL: this rank's band tracking
    (klt_shard_track) or trackability map (klt_shard_replace) fails after its
    argument checks, so it still joins the exchange/agreement and reports its
    own message.  PEER: this rank adds one phantom failed peer to every failure
    count it contributes, as a failing peer's contribution would, so the call
    returns "1 peer rank(s) failed".  ALLOC: the exchange buffers cannot be
    allocated, so the communicator is aborted and the shard refuses every later
-   call.  Returns 0, -1 on an unknown bit. */
+   call.  Returns 0, -1 on an unknown bit, -2 when testing is off. */
 #define KLT_SHARD_FAULT_LOCAL 1
 #define KLT_SHARD_FAULT_PEER 2
 #define KLT_SHARD_FAULT_ALLOC 4
 int klt_shard_inject_fault(klt_shard *s, int faults);
+#endif
 /* rows [*lo, *hi) of every frame this rank's band build reads: the only rows
    klt_shard_track's frames must hold (its band, margin and tile halo) */
 int klt_shard_rows(const klt_shard *s, int *lo, int *hi);

@@ -7,7 +7,13 @@
 // check the pooled sort against the sequential one on the CPU.
 #pragma once
 
+#include <sched.h>
+
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <atomic>
 #include <condition_variable>
 #include <deque>
@@ -97,20 +103,41 @@ unsigned partition(P *a, unsigned n) {
   return j;
 }
 
+// CPUs this process may run on: the affinity mask, capped by a cgroup-v2 CPU
+// quota (cpu.max) when one is set -- std::thread::hardware_concurrency counts
+// every CPU of the machine, which on a shared box is many times its share.
+inline int usable_cpus() {
+  int n = (int)std::thread::hardware_concurrency();
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  if (sched_getaffinity(0, sizeof set, &set) == 0 && CPU_COUNT(&set) > 0) n = CPU_COUNT(&set);
+  if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {};
+    long period = 0;
+    if (std::fscanf(f, "%31s %ld", q, &period) == 2 && period > 0 && std::strcmp(q, "max") != 0) {
+      const long quota = std::atol(q);
+      const int c = (int)((quota + period - 1) / period);
+      if (c > 0 && c < n) n = c;
+    }
+    std::fclose(f);
+  }
+  return n > 0 ? n : 1;
+}
+
 // Persistent workers, shared by every caller in the process (a REPLACE sorts a
 // dozen segments; creating a thread per split cost more than many of the
 // splits).  Tasks never wait on other tasks: a task hands its right part to
 // the queue and goes on with its left part, and the caller of sort() works
 // through its OWN queued tasks beside the workers until its count of
 // unfinished tasks is zero, so no wait can deadlock and one caller's sort never
-// runs another's tasks on its thread.  While any sort is in progress the idle
-// workers spin on the queue instead of sleeping, so a queued half starts
-// within a microsecond or so rather than after a futex wake-up (the wake-ups
-// cost more than the splits they were waking for); between sorts they sleep.
-// The pool grows to the largest worker count asked for and lives until the
-// process exits: its detached workers are never joined, so the library that
-// holds it must not be unloaded (dlclose) while the process goes on
-// (INTEGRATION.md).
+// runs another's tasks on its thread.  While any sort is in progress an idle
+// worker spins on the queue for up to kSpinUs after its last task instead of
+// sleeping, so a queued half starts within a microsecond or so rather than
+// after a futex wake-up (the wake-ups cost more than the splits they were
+// waking for); past that, and between sorts, it sleeps until a task is
+// queued.  The pool grows to the largest worker count asked for and lives
+// until shutdown(), which the library's exit hook calls (runtime.hip): its
+// workers are joined there, before the library's own exit-time teardown runs.
 template <class P>
 struct Pool {
   struct Task {
@@ -121,10 +148,14 @@ struct Pool {
     std::atomic<int> *pending;
   };
 
+  static constexpr double kSpinUs = 50.0;
   static void pause() {
 #if defined(__x86_64__) || defined(__i386__)
     __builtin_ia32_pause();
 #endif
+  }
+  static double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
   }
   std::mutex m;
   std::condition_variable cv, done;
@@ -139,16 +170,34 @@ struct Pool {
   // spinning.  qn never exceeds the queue's length, and no task is stranded.
   std::atomic<int> qn{0};
   std::atomic<int> hot{0};   // sorts in progress
-  int nworkers = 0;
+  std::atomic<bool> quit{false};
+  std::atomic<unsigned> gen{0};  // sorts started that queue tasks: wakes the sleepers ahead of the first task
+  std::vector<std::thread> threads;
 
+  // workers: clamped to usable_cpus() - 1 (the caller sorts too)
   static Pool &get(int workers) {
-    static Pool *p = new Pool();  // never destroyed (above)
+    static Pool *p = new Pool();  // outlives every caller; shutdown() stops its threads
     p->grow(workers);
     return *p;
   }
   void grow(int workers) {
+    static const int cap = usable_cpus() - 1;
+    if (workers > cap) workers = cap;
     std::lock_guard<std::mutex> lk(m);
-    for (; nworkers < workers; ++nworkers) std::thread([this] { work(); }).detach();
+    if (quit.load(std::memory_order_relaxed)) return;
+    while ((int)threads.size() < workers) threads.emplace_back([this] { work(); });
+  }
+  // stop and join every worker (no sort may be in progress); later sorts run
+  // on their callers' threads alone
+  void shutdown() {
+    {
+      std::lock_guard<std::mutex> lk(m);
+      quit.store(true, std::memory_order_relaxed);
+    }
+    cv.notify_all();
+    for (std::thread &t : threads)
+      if (t.joinable()) t.join();
+    threads.clear();
   }
   bool claim() {
     int k = qn.load(std::memory_order_relaxed);
@@ -158,15 +207,21 @@ struct Pool {
   }
   void unreserve_one() { claim(); }
   void work() {
+    double last = now_us();
+    unsigned seen = gen.load(std::memory_order_relaxed);
     for (;;) {
+      if (quit.load(std::memory_order_relaxed)) return;
       if (!claim()) {
-        if (hot.load(std::memory_order_acquire) > 0) {
-          pause();
-        } else {  // no sort in progress: sleep until a task or a sort comes
+        if (hot.load(std::memory_order_acquire) > 0 && now_us() - last < kSpinUs) {
+          for (int k = 0; k < 32; ++k) pause();
+        } else {  // no sort in progress, or none of its tasks for a while: sleep until a task comes
           std::unique_lock<std::mutex> lk(m);
-          cv.wait(lk, [this] {
-            return qn.load(std::memory_order_relaxed) > 0 || hot.load(std::memory_order_relaxed) > 0;
+          cv.wait(lk, [this, seen] {
+            return qn.load(std::memory_order_relaxed) > 0 || quit.load(std::memory_order_relaxed) ||
+                   gen.load(std::memory_order_relaxed) != seen;
           });
+          seen = gen.load(std::memory_order_relaxed);
+          last = now_us();
         }
         continue;
       }
@@ -178,6 +233,7 @@ struct Pool {
         q.pop_front();
       }
       run(t);
+      last = now_us();
     }
   }
   void submit(const Task &t) {
@@ -230,10 +286,14 @@ struct Pool {
   // sort a[0..n) with up to 2^par tasks; returns when all of them are done
   void sort(P *a, unsigned n, int par, unsigned par_min) {
     std::atomic<int> pending{1};
+    if (threads.empty()) par = 0;  // no workers (shut down, or one CPU): the sequential recursion
     const bool spin = par > 0 && n >= 2 * par_min;  // tasks will be queued: keep the workers awake meanwhile
     if (spin) {
       hot.fetch_add(1, std::memory_order_release);
-      { std::lock_guard<std::mutex> lk(m); }
+      {
+        std::lock_guard<std::mutex> lk(m);
+        gen.fetch_add(1, std::memory_order_relaxed);
+      }
       cv.notify_all();
     }
     run(Task{a, n, par, par_min, &pending});
@@ -250,12 +310,15 @@ struct Pool {
         lk.lock();
         continue;
       }
-      if (!spin) {
+      if (!spin || !q.empty()) {
+        // none of the queued tasks is this sort's (or it queues none): wait
+        // for its last task to end (run() notifies under m) instead of
+        // rescanning another sort's queue
         done.wait(lk);
         continue;
       }
-      // the workers are spinning: so does the caller, rather than pay a
-      // wake-up when its last task ends
+      // the workers are spinning on this sort's halves: so does the caller,
+      // rather than pay a wake-up when its last task ends
       lk.unlock();
       while (pending.load(std::memory_order_acquire) != 0 && qn.load(std::memory_order_relaxed) == 0) pause();
       lk.lock();

@@ -173,7 +173,8 @@ hipError_t launch_rows(hipStream_t st, const float *in, int W, int H, const RTap
 hipError_t launch_cols(hipStream_t st, const float *in, int W, int H, const RTaps &t, float *out);
 hipError_t launch_subsample(hipStream_t st, const float *in, int W, int ss, float *out, int W1, int H1);
 // trackability map over the nx x ny grid from (bx, by), step apart; ps: the
-// gradients' pixel stride (1 planes, 3 an interleaved level's gx = base+1, gy = base+2)
+// gradients' pixel stride (1 planes; 3 an interleaved level's {gx, gy, img}
+// records, gx = base + kRecGx, gy = base + kRecGy)
 hipError_t launch_min_eigen(hipStream_t st, const float *gx, const float *gy, int W, int ps, int bx, int by, int step,
                             int nx, int ny, int hw, int hh, int *out);
 hipError_t launch_synth(hipStream_t st, unsigned long long seed, int t0, int n, int W, int H, int row0, uint8_t *out,
@@ -209,6 +210,8 @@ struct SelEngine;
 constexpr int kSelDefaultThreshold = 49152;  // map points: longer segments are split on the device (tools/exp/r04ah.sh)
 SelEngine *sel_engine_create();
 void sel_engine_destroy(SelEngine *e);
+void sel_engine_release_graphs(SelEngine *e);  // exit hook: the captured graphs before the code object goes
+void sel_pool_shutdown();                       // exit hook: join the host sort pool's workers
 void sel_engine_set_threshold(SelEngine *e, int threshold);
 int sel_default_threshold();
 void sel_engine_stats(const SelEngine *e, long *downloaded, long *steps, long *visited, double *us);

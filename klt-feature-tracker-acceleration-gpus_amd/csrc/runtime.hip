@@ -15,6 +15,7 @@
 #include <condition_variable>
 #include <functional>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -165,6 +166,11 @@ struct klt_hip_ctx {
   hipEvent_t ev_built[KLT_HIP_MAX_SLOTS] = {};
   hipEvent_t ev_free[KLT_HIP_MAX_SLOTS] = {};
   hipEvent_t ev_start = nullptr;
+  // a caller's stream (klt_hip_set_stream): ev_caller is recorded on it when
+  // the context switches away from it, so a reset or destroy can wait for the
+  // work queued there even after the caller has destroyed the stream
+  hipEvent_t ev_caller = nullptr;
+  bool caller_pending = false;
   Slot slot[KLT_HIP_MAX_SLOTS + 2];  // + the batch seed and scratch slots
   uint8_t *d_u8[2] = {nullptr, nullptr};
   uint8_t *h_u8[2] = {nullptr, nullptr};
@@ -910,6 +916,61 @@ int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const u
 }
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// Process exit.  hipcc's module constructor of each translation unit registers
+// the code object at load time and an atexit handler that unregisters it; the
+// HIP runtime (and a profiler's tool library, e.g. rocprofv3) tear down in
+// their own exit handlers.  Anything of ours still holding the code object's
+// kernels or HIP state at that point -- the selection engine's instantiated
+// graphs of every live or parked context, the host sort pool's threads --
+// is released by exit_hook, which atexit() runs BEFORE those handlers because
+// it is registered after them (at the first context's creation).
+// ---------------------------------------------------------------------------
+namespace {
+std::mutex g_live_m;
+std::set<klt_hip_ctx *> *g_live = new std::set<klt_hip_ctx *>();  // never destroyed: exit_hook reads it
+std::atomic<bool> g_exiting{false};
+
+void exit_hook() {
+  g_exiting.store(true);
+  std::lock_guard<std::mutex> lk(g_live_m);
+  std::set<int> devs;
+  for (klt_hip_ctx *c : *g_live) devs.insert(c->device);
+  for (int d : devs)  // a look-ahead refinement's graph may still be in flight
+    if (hipSetDevice(d) == hipSuccess) (void)hipDeviceSynchronize();
+  for (klt_hip_ctx *c : *g_live) sel_engine_release_graphs(c->sel);
+  sel_pool_shutdown();
+}
+
+void live_add(klt_hip_ctx *c) {
+  static std::once_flag once;
+  std::call_once(once, [] { atexit(exit_hook); });
+  std::lock_guard<std::mutex> lk(g_live_m);
+  g_live->insert(c);
+}
+
+void live_remove(klt_hip_ctx *c) {
+  std::lock_guard<std::mutex> lk(g_live_m);
+  g_live->erase(c);
+}
+
+// wait for what a caller's stream holds of this context's work: the event
+// recorded when the context left it, and the stream still set (which must be
+// valid until klt_hip_set_stream(c, NULL), the reset or the destroy)
+int drain_caller(klt_hip_ctx *c) {
+  if (c->stream && c->stream != c->own) {
+    if (!c->ev_caller) HIPCHK(c, hipEventCreateWithFlags(&c->ev_caller, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(c->ev_caller, c->stream));
+    c->caller_pending = true;
+  }
+  if (c->caller_pending) {
+    HIPCHK(c, hipEventSynchronize(c->ev_caller));
+    c->caller_pending = false;
+  }
+  return 0;
+}
+}  // namespace
+
 // ===========================================================================
 // C ABI
 // ===========================================================================
@@ -932,13 +993,15 @@ KLT_API klt_hip_ctx *klt_hip_ctx_create(int device) {
   }
   c->stream = c->own;
   for (int i = 0; i < 2; ++i) hipEventCreateWithFlags(&c->u8_done[i], hipEventDisableTiming);
+  live_add(c);
   return c;
 }
 
 KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
   if (!c) return;
+  live_remove(c);
   hipSetDevice(c->device);
-  hipStreamSynchronize(c->stream);
+  (void)drain_caller(c);
   if (c->own) hipStreamSynchronize(c->own);
   if (c->pstream) hipStreamSynchronize(c->pstream);
   for (auto &S : c->slot)
@@ -994,6 +1057,7 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
     if (c->ev_free[k]) hipEventDestroy(c->ev_free[k]);
   }
   if (c->ev_start) hipEventDestroy(c->ev_start);
+  if (c->ev_caller) hipEventDestroy(c->ev_caller);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
 }
@@ -1027,9 +1091,10 @@ KLT_API size_t klt_hip_ctx_footprint(klt_hip_ctx *c) {
 KLT_API int klt_hip_ctx_reset(klt_hip_ctx *c) {
   if (!c) return -1;
   if (use_device(c)) return -1;
-  // nothing of the previous owner is still running: the context's own streams
-  // (a caller's stream set with klt_hip_set_stream is the caller's to drain:
-  // it may already be destroyed, so c->stream is not touched unless it is ours)
+  // nothing of the previous owner is still running: the context's own streams,
+  // and a caller's stream through drain_caller (an event recorded on it, so a
+  // stream the caller has switched away from and destroyed is never touched)
+  if (drain_caller(c)) return -1;
   for (hipStream_t st : {c->own, c->pstream, c->cstream, c->dstream})
     if (st) HIPCHK(c, hipStreamSynchronize(st));
   if (klt_hip_ctx_footprint(c) > kKeepBytes) {
@@ -1091,7 +1156,16 @@ KLT_API const char *klt_hip_track_kernel(klt_hip_ctx *c) { return c && c->track_
 
 KLT_API int klt_hip_set_stream(klt_hip_ctx *c, void *stream) {
   if (!c) return -1;
-  c->stream = stream ? (hipStream_t)stream : c->own;
+  const hipStream_t next = stream ? (hipStream_t)stream : c->own;
+  if (next != c->stream && c->stream != c->own) {
+    // leaving a caller's stream: remember its last work (drain_caller)
+    if (use_device(c)) return -1;
+    if (c->caller_pending) HIPCHK(c, hipEventSynchronize(c->ev_caller));
+    if (!c->ev_caller) HIPCHK(c, hipEventCreateWithFlags(&c->ev_caller, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(c->ev_caller, c->stream));
+    c->caller_pending = true;
+  }
+  c->stream = next;
   return 0;
 }
 

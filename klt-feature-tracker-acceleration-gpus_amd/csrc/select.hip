@@ -346,6 +346,8 @@ struct SelEngine {
   int *d_f = nullptr, *h_f = nullptr;  // the live features for the paint: x | y | val, n each
   size_t f_cap = 0, hf_cap = 0;
   hipEvent_t ev_dl = nullptr, ev_ref = nullptr;  // a segment download done / a look-ahead refinement done
+  hipEvent_t ev_hf = nullptr;  // the last upload out of h_f done (recorded when hf_busy)
+  bool hf_busy = false;
 
   int threshold = sel_default_threshold();  // segments at most this long go to the host
   // statistics of the last run
@@ -619,8 +621,9 @@ struct LazySort {
         // outright (in parallel) and hand its positions out in order
         const double t0 = now_us();
         const int depth = sort_depth();
-        static const int workers = std::max(0, std::min((1 << depth) - 1, (int)std::thread::hardware_concurrency() - 1));
-        kltsort::Pool<int2>::get(workers).sort(e->h_kv + g.start, (unsigned)g.len, depth, kSelParMin);
+        // 2^depth tasks: up to 2^depth - 1 workers beside the caller (Pool::grow
+        // caps them at the process's usable CPUs)
+        kltsort::Pool<int2>::get((1 << depth) - 1).sort(e->h_kv + g.start, (unsigned)g.len, depth, kSelParMin);
         e->us[2] += now_us() - t0;
         if (sel_trace()) fprintf(stderr, "seltrace sort len=%d us=%.1f\n", g.len, now_us() - t0);
         g.sorted = true;
@@ -679,8 +682,19 @@ int sel_default_threshold() {
 
 SelEngine *sel_engine_create() { return new SelEngine(); }
 
+// The captured refinements hold kernel nodes of this library's code object:
+// they must be gone before the module's own exit-time unregistration runs
+// (runtime.hip's exit hook calls this for every live context).
+void sel_engine_release_graphs(SelEngine *e) {
+  if (!e) return;
+  for (const SelGraph &k : e->graphs) hipGraphExecDestroy(k.exec);
+  e->graphs.clear();
+}
+
 void sel_engine_destroy(SelEngine *e) {
   if (!e) return;
+  if (e->hf_busy) hipEventSynchronize(e->ev_hf);
+  if (e->ev_hf) hipEventDestroy(e->ev_hf);
   for (void *p : {(void *)e->d_kv, (void *)e->d_cnt, (void *)e->d_off, (void *)e->d_posL, (void *)e->d_posR,
                   (void *)e->d_state, (void *)e->d_map, (void *)e->d_f})
     hipFree(p);
@@ -688,10 +702,13 @@ void sel_engine_destroy(SelEngine *e) {
   if (e->h_f) hipHostFree(e->h_f);
   if (e->ev_dl) hipEventDestroy(e->ev_dl);
   if (e->ev_ref) hipEventDestroy(e->ev_ref);
-  for (const SelGraph &k : e->graphs) hipGraphExecDestroy(k.exec);
+  sel_engine_release_graphs(e);
   if (e->h_kv) hipHostFree(e->h_kv);
   delete e;
 }
+
+// exit hook (runtime.hip): join the sort pool's workers
+void sel_pool_shutdown() { kltsort::Pool<int2>::get(0).shutdown(); }
 
 void sel_engine_set_threshold(SelEngine *e, int t) { e->threshold = t < 1 ? 1 : t; }
 
@@ -743,8 +760,15 @@ int sel_engine_run(SelEngine *e, hipStream_t st, const int *dev_vals, int nx, in
     if (sel_grow(&e->d_map, &e->map_cap, (size_t)W * H, err) || sel_grow(&e->d_f, &e->f_cap, 3 * (size_t)n, err))
       return -1;
     // one DMA from pinned staging: the caller's arrays may be pageable, and
-    // each pageable copy is a blocking staged transfer of its own (the last
-    // run's copy out of h_f ended at its synchronize below)
+    // each pageable copy is a blocking staged transfer of its own.  Nothing in
+    // a run waits for that DMA on the host (a run with nothing to walk, or one
+    // that fails, returns with it queued), so the next write into h_f -- or
+    // its free -- first waits for the event recorded after it
+    if (e->hf_busy) {
+      SELCHK(hipEventSynchronize(e->ev_hf));
+      e->hf_busy = false;
+    }
+    if (!e->ev_hf) SELCHK(hipEventCreateWithFlags(&e->ev_hf, hipEventDisableTiming));
     if (e->hf_cap < 3 * (size_t)n) {
       if (e->h_f) hipHostFree(e->h_f);
       e->h_f = nullptr;
@@ -757,6 +781,8 @@ int sel_engine_run(SelEngine *e, hipStream_t st, const int *dev_vals, int nx, in
     memcpy(e->h_f + 2 * (size_t)n, val, sizeof(int) * n);
     SELCHK(hipMemsetAsync(e->d_map, 0, (size_t)W * H, st));
     SELCHK(hipMemcpyAsync(e->d_f, e->h_f, sizeof(int) * 3 * (size_t)n, hipMemcpyHostToDevice, st));
+    SELCHK(hipEventRecord(e->ev_hf, st));
+    e->hf_busy = true;
     const long cells = (long)n * (2 * r + 1) * (2 * r + 1);
     hipLaunchKernelGGL(k_sel_paint, dim3((unsigned)((cells + kSelThreads - 1) / kSelThreads)), dim3(kSelThreads), 0,
                        st, (const float *)e->d_f, (const float *)(e->d_f + n), e->d_f + 2 * (size_t)n, n, r, W, H,

@@ -9,12 +9,14 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
 #include <vector>
 
 #include "klt_dev.h"
+#define KLT_SHARD_TESTING 1  // this file defines the test-only hook
 #include "klt_shard.h"
 
 extern "C" {
@@ -260,7 +262,10 @@ KLT_API void klt_shard_destroy(klt_shard *s) {
   delete s;
 }
 
+// test-only (include/klt_shard.h): inert unless KLT_SHARD_TESTING=1 is set
 KLT_API int klt_shard_inject_fault(klt_shard *s, int faults) {
+  const char *on = getenv("KLT_SHARD_TESTING");
+  if (!on || atoi(on) != 1) return -2;
   if (!s || (faults & ~(KLT_SHARD_FAULT_LOCAL | KLT_SHARD_FAULT_PEER | KLT_SHARD_FAULT_ALLOC))) return -1;
   s->faults = faults;
   return 0;

@@ -148,3 +148,28 @@ def test_registered_buffers_bit_identical(gpu):
     for ca, cb in zip(a, b):
         for p, q in zip(ca, cb):
             assert np.array_equal(p.view(np.int32), q.view(np.int32))
+
+
+def test_reset_drains_the_callers_stream(gpu):
+    """a context parked (klt_hip_ctx_reset) while the caller's
+    stream (klt_hip_set_stream) still runs its work waits for that work before
+    its buffers are freed and the context is handed on -- both for the stream
+    still set and for one the context switched away from."""
+    import torch
+    from kltamd.device import check
+    W, H, n = 1920, 1080, 96
+    dev = torch.device("cuda", 0)
+    for switch_away in (False, True):
+        tc = gpu.KLTCreateTrackingContext()
+        ctx = gpu.klt_amd_device_context(tc)
+        s = torch.cuda.Stream(dev)
+        check(gpu, ctx, gpu.klt_hip_set_stream(ctx, C.c_void_p(s.cuda_stream)), "set_stream")
+        fr = torch.empty((n, H, W), dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        check(gpu, ctx, gpu.klt_hip_synth_frames(ctx, 9, 0, n, W, H, C.c_void_p(fr.data_ptr()), W, W * H), "synth")
+        if switch_away:
+            check(gpu, ctx, gpu.klt_hip_set_stream(ctx, None), "own stream")
+        gpu.KLTFreeTrackingContext(tc)  # parks the device context: klt_hip_ctx_reset
+        assert s.query(), "the reset returned while the caller's stream still ran the context's work"
+        del fr
+    assert gpu.klt_amd_release_cached_devices() >= 1

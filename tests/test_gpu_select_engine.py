@@ -83,3 +83,51 @@ def test_selection_with_device_steps_vs_oracle(gpu, oracle, threshold):
     assert np.array_equal(V[:, :T], OV[:, :T])
     assert np.array_equal(X[:, :T].view(np.int32), OX[:, :T].view(np.int32))
     assert np.array_equal(Y[:, :T].view(np.int32), OY[:, :T].view(np.int32))
+
+
+EXIT_CHILD = r"""
+import ctypes as C, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import kltamd
+lib = kltamd.load()
+lib.KLTSetVerbosity(0)
+W, H, NF = 1280, 720, 3000
+u8 = lambda a: a.ctypes.data_as(C.POINTER(C.c_ubyte))
+fr = []
+for t in range(5):
+    a = np.empty((H, W), np.uint8)
+    lib.klt_synth_frame(720, t, W, H, a.ctypes.data)
+    fr.append(a)
+parked = lib.KLTCreateTrackingContext()  # freed below: its device context is parked, graphs and all
+tc = lib.KLTCreateTrackingContext()      # never freed: live at exit
+for c in (parked, tc):
+    c.contents.sequentialMode = 1
+fl = lib.KLTCreateFeatureList(NF)
+for c in (parked, tc):
+    lib.KLTSelectGoodFeatures(c, u8(fr[0]), W, H, fl)
+    for t in range(1, 5):
+        lib.KLTTrackFeatures(c, u8(fr[t - 1]), u8(fr[t]), W, H, fl)
+        lib.KLTReplaceLostFeatures(c, u8(fr[t]), W, H, fl)
+lib.KLTFreeTrackingContext(parked)
+print("child done", flush=True)
+"""
+
+
+def test_exit_after_replace_is_clean(tmp_path):
+    """The process exits cleanly after REPLACE calls whose partition steps were
+    graph launches, with one tracking context freed (its device context
+    parked) and one never freed: the library's exit hook (runtime.hip
+    exit_hook) drains the device, releases the instantiated graphs and joins
+    the host sort pool before the code object's own exit-time
+    unregistration.  A crash inside exit() after such a run was seen once
+    under rocprofv3 in round 4."""
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    script = tmp_path / "exit_child.py"
+    script.write_text(EXIT_CHILD)
+    r = subprocess.run([sys.executable, str(script), str(root)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    assert "child done" in r.stdout

@@ -529,6 +529,7 @@ def test_c_shard_failure_agreement(gpu):
     exchange-buffer allocation failure aborts the communicator and the shard
     refuses every later call."""
     from kltamd.device import SelectDesc
+    os.environ.pop("KLT_SHARD_TESTING", None)
     frames = synth(gpu, 91, 640, 480, 3)
     H, W = frames[0].shape
     dev = torch.device("cuda", 0)
@@ -538,6 +539,8 @@ def test_c_shard_failure_agreement(gpu):
     assert gpu.klt_shard_unique_id(uid) == 0
     s = gpu.klt_shard_create(rk.ctx, 0, 1, uid, H, 64)
     assert s
+    assert gpu.klt_shard_inject_fault(s, 1) == -2  # test-only: inert without KLT_SHARD_TESTING=1
+    os.environ["KLT_SHARD_TESTING"] = "1"
     assert gpu.klt_shard_inject_fault(s, 8) == -1  # unknown fault bit
     x, y, v = (torch.from_numpy(a).to(dev) for a in _select(gpu, frames[0], 600))
     x0, y0, v0 = x.clone(), y.clone(), v.clone()

@@ -1,0 +1,47 @@
+#!/bin/bash
+# Round-5 GPU steps.  usage (via gpurun): bash tools/r05.sh <tag> <step>...
+# Steps (each GPU step under its own time limit; the script stops at the
+# first failure and starts nothing more on the GPU):
+#   tests      pytest -m gpu (whole suite)
+#   t:<expr>   pytest -m gpu -k <expr>
+#   exitprof   tools/exp/replace_probe.py 6 under rocprofv3 --kernel-trace (clean exit after REPLACE)
+#   bench      bench.py (default shape); s20: bench.py --steps 20 --warmup 5
+#   shard8     tools/shard_sim.py, 1 and 8 ranks over config 4's 1001 frames
+#   py:<file>  python3 <file> (an experiment script), output in <tag>/
+set -o pipefail
+TAG=${1:-r05}; shift; OUT=gpurun_out/$TAG; mkdir -p $OUT
+export TMPDIR=/tmp
+C=${COMMIT:-unknown}
+echo "# commit $C" > $OUT/commit.txt
+for step in "$@"; do
+  echo "== $step $(date +%T)"
+  case $step in
+    tests)
+      timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+        > $OUT/gpu_tests.log 2>&1 || { tail -40 $OUT/gpu_tests.log; exit 1; }
+      tail -2 $OUT/gpu_tests.log ;;
+    t:*)
+      timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+        -k "${step#t:}" > $OUT/gpu_tests_k.log 2>&1 || { tail -40 $OUT/gpu_tests_k.log; exit 1; }
+      tail -2 $OUT/gpu_tests_k.log ;;
+    exitprof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/exitprof -o rp --output-format csv -- \
+        python3 tools/exp/replace_probe.py 6 > $OUT/exitprof.log 2>&1
+      rc=$?; echo "exitprof rc=$rc" | tee -a $OUT/exitprof.log; [ $rc -eq 0 ] || exit 1 ;;
+    bench)
+      timeout -k 10 600 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
+      head -c 600 $OUT/bench.json; echo ;;
+    s20)
+      timeout -k 10 600 python3 bench.py --steps 20 --warmup 5 > $OUT/bench_s20.json 2> $OUT/bench_s20.err || { tail -20 $OUT/bench_s20.err; exit 1; }
+      head -c 400 $OUT/bench_s20.json; echo ;;
+    shard8)
+      timeout -k 10 1100 python3 -u tools/shard_sim.py --frames 1001 --chunk 64 --worlds 1 8 --margins 64 --pass1-shared \
+        > $OUT/shard8.log 2>&1 || { tail -20 $OUT/shard8.log; exit 1; }
+      head -3 $OUT/shard8.log ;;
+    py:*)
+      f=${step#py:}; b=$(basename $f .py)
+      timeout -k 10 900 python3 -u $f $OUT > $OUT/$b.log 2>&1 || { tail -30 $OUT/$b.log; exit 1; }
+      tail -15 $OUT/$b.log ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
