@@ -22,6 +22,9 @@ Output: tests/golden/long_<name>.json
            single-GPU result the sharded run must equal)
   config3r: config 3's sequence (60 frames) through the REPLACE harness:
            KLTReplaceLostFeatures after every KLTTrackFeatures
+  config5: configs[4]'s other per-GPU sequences -- 1920x1080, 5000 features,
+           100 frames each at seeds 1081 .. 1087 (bench.py's rank r runs seed
+           1080 + r; seed 1080 is config3's) -- one entry per seed
 """
 from __future__ import annotations
 
@@ -45,6 +48,7 @@ CONFIGS = {
     # the REPLACE harness (example3.c:67-69: KLTReplaceLostFeatures after every
     # KLTTrackFeatures, before KLTStoreFeatureList) at the config-3 size
     "config3r": dict(w=1920, h=1080, features=5000, frames=60, seed=1080, replace=True),
+    "config5": dict(w=1920, h=1080, features=5000, frames=100, seeds=list(range(1081, 1088))),
 }
 
 
@@ -67,12 +71,16 @@ def list_view(fl):
     return raw[:, 0].view(np.float32), raw[:, 1].view(np.float32), raw[:, 2]
 
 
-def run(name: str) -> dict:
+def run(name: str, p: dict | None = None) -> dict:
     import kltamd
     amd = kltamd.load()  # host-side synthetic generator only (klt_synth_frame)
-    p = CONFIGS[name]
+    p = dict(p or CONFIGS[name])
+    if "seeds" in p:  # one sequence per seed, each a fixture of its own
+        seeds = p.pop("seeds")
+        per = {str(sd): run(f"{name} seed {sd}", dict(p, seed=sd)) for sd in seeds}
+        return {"config": name, **p, "seeds": per,
+                "produced_by": "oracle/_ref/libklt_ref.so (reference src/V3 compiled from its own sources)"}
     w, h, nf, nframes, seed = p["w"], p["h"], p["features"], p["frames"], p["seed"]
-    p = dict(p)
     ref = bind_klt(REF_LIB)
     ref.KLTSetVerbosity(0)
 
@@ -116,7 +124,7 @@ def main() -> None:
     for name in sys.argv[1:] or list(CONFIGS):
         out = run(name)
         (HERE / f"long_{name}.json").write_text(json.dumps(out, indent=0) + "\n")
-        print(f"wrote long_{name}.json ({len(out['columns'])} columns, {out['cpu_seconds']}s)")
+        print(f"wrote long_{name}.json")
 
 
 if __name__ == "__main__":

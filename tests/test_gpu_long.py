@@ -17,7 +17,9 @@ Paths covered, each over the whole sequence:
     every KLTTrackFeatures, 60 frames, long_config3r.json);
   * the feature-sharded schedule (config 4, 2/4/8 simulated ranks);
   * the fast (wave-shuffle) reduction, against the exact path, with the
-    tolerance it is held to.
+    tolerance it is held to (SURVEY 8c);
+  * config 5's other per-GPU sequences (seeds 1081 .. 1087, 100 frames each,
+    long_config5.json) on the batched path.
 """
 from __future__ import annotations
 
@@ -130,6 +132,22 @@ def test_batched_full_sequence_vs_reference(gpu, name):
     j = first_mismatch(X, Y, V, cfg["columns"])
     assert j is None, f"{name}: table differs from the reference from frame {j + 1}"
     assert [int((V[k] >= 0).sum()) for k in range(0, X.shape[0], 50)] == cfg["live"][::50]
+
+
+def test_config5_seeds_vs_reference(gpu):
+    """BASELINE config 5 (one independent 1080p/5000 sequence per GPU): bench.py's
+    rank r tracks seed 1080 + r.  Seed 1080 is config 3 (above); seeds 1081 ..
+    1087, 100 frames each, on the bench's batched path against the reference's
+    per-column digests (long_config5.json), so every rank's workload of the
+    8-GPU run is reference-pinned."""
+    cfg5 = fixture("config5")
+    assert sorted(int(k) for k in cfg5["seeds"]) == list(range(1081, 1088))
+    for sd, cfg in sorted(cfg5["seeds"].items()):
+        X, Y, V = device_run(gpu, cfg)
+        assert len(cfg["columns"]) == X.shape[0] == cfg["frames"] - 1
+        j = first_mismatch(X, Y, V, cfg["columns"])
+        assert j is None, f"config5 seed {sd}: table differs from the reference from frame {j + 1}"
+        assert [int((V[k] >= 0).sum()) for k in range(X.shape[0])] == cfg["live"]
 
 
 @pytest.mark.parametrize("name,chunk,overlap", [("config2", 1, 0), ("config2", 7, 1), ("config4", 32, 0)])

@@ -153,3 +153,24 @@ def test_live_vs_reference_nondefault(oracle, ref, syn333):
 
     r, o = both(li)
     assert table_eq(r, o)
+
+
+@pytest.mark.parametrize("seed", ["1081", "1087"])
+def test_oracle_config5_prefix(oracle, amd, seed):
+    """The oracle against the reference's config-5 fixtures (long_config5.json,
+    1080p/5000, seeds 1081 .. 1087): the first three columns of two seeds --
+    the CPU half of the pinning whose GPU half is
+    test_gpu_long.py::test_config5_seeds_vs_reference."""
+    cfg = json.loads((GOLDEN / "long_config5.json").read_text())["seeds"][seed]
+    w, h, n = cfg["w"], cfg["h"], cfg["features"]
+    frames = []
+    for t in range(4):
+        a = np.empty((h, w), np.uint8)
+        amd.klt_synth_frame(int(seed), t, w, h, a.ctypes.data)
+        frames.append(a)
+    X, Y, V = OracleTracker(oracle).harness(frames, n, 4, first=frames[0])
+    for c in range(3):
+        hh = hashlib.sha256()
+        for a, dt in ((X[:, c], "<f4"), (Y[:, c], "<f4"), (V[:, c], "<i4")):
+            hh.update(np.ascontiguousarray(a, dt).tobytes())
+        assert hh.hexdigest() == cfg["columns"][c], f"seed {seed} column {c}"
