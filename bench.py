@@ -61,7 +61,9 @@ def parse():
     p.add_argument("--cpu-frames", type=int, default=160,
                    help="frames of the bounded CPU-baseline sample (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--no-4k", action="store_true", help="skip the 4K pyramid-pass roofline line (rank 0, N=1)")
+    p.add_argument("--no-4k", action="store_true", help="skip the 4K legs (pass roofline, frames_4k; rank 0, N=1)")
+    p.add_argument("--no-frames-4k", action="store_true",
+                   help="skip the frames_4k leg (config 4 on one GPU: 1000 4K frames, device and KLTTrackSequence)")
     p.add_argument("--reduction", choices=["exact", "fast"], default="exact")
     p.add_argument("--chunk", type=int, default=None,
                    help="frames per batched pyramid/track launch (klt_hip_track_frames; default 64; sharded: frames "
@@ -398,6 +400,8 @@ def main() -> None:
         result["roofline_4k"] = pass_4k(lib, dev)
         attach_traffic(result["roofline_4k"], ROOT / "profiles" / "pmc_4k_latest.json", "3840x2160",
                        result["roofline_4k"]["frames_per_launch"])
+    if rank == 0 and world == 1 and not args.no_4k and not args.no_frames_4k:
+        result["frames_4k"] = frames_4k_leg(lib, dev)
     if rank == 0 and world == 1:
         # the fraction also against a measured copy peak
         mp = measured_peaks(dev)
@@ -596,6 +600,122 @@ def pass_4k(lib, dev, chunk=64, reps=2, nf=20000):
                               "achieved": pach, "frac": pach / HBM_PEAK_GBS, "us_per_frame": p0 + p1,
                               "kernels_us_per_frame": {"k_pyr_l0": p0, "k_pyr_l1": p1},
                               "frames_timed": int(ptm.frames_pyr_l0)}}
+
+
+def frames_4k_leg(lib, dev, chunk=64):
+    """North_star's frames/s at 4K: BASELINE config 4 on one GPU -- 3840x2160,
+    20 000 features selected on frame 0, all 1000 tracked frames (seed 2160,
+    the sequence tests/golden/long_config4.json pins), KLTStoreFeatureList per
+    frame.  Two regions, each timed by the wall clock after an untimed warm-up
+    run of its own:
+      device: frames synthesised into HBM, klt_hip_track_frames with the
+              feature table on the device (the 1080p headline's path, 64-frame
+              chunks, the next chunk's pyramids on a second stream);
+      sequence: KLTTrackSequence over host frames (pageable numpy) writing a
+              host KLT_FeatureTable -- frame uploads over PCIe, pyramids,
+              tracking and the table rows coming back, all inside the region.
+    Parity: every column of both tables against the reference's per-frame
+    digests (long_config4.json, made by the reference compiled from its own
+    sources), bit for bit."""
+    import hashlib
+    import torch
+    from kltabi import GOLDEN, fl_to_arrays
+    from kltamd.device import PyrDesc, TrackDesc, check, use_torch_stream
+    cfg = json.loads((GOLDEN / "long_config4.json").read_text())
+    W, H, NF, NFR, seed = cfg["w"], cfg["h"], cfg["features"], cfg["frames"], cfg["seed"]
+    T = NFR - 1
+    U8P = C.POINTER(C.c_ubyte)
+    lib.klt_amd_release_cached_devices()
+    torch.cuda.empty_cache()
+
+    def digest_cols(X, Y, V):
+        out = []
+        for j in range(X.shape[0]):
+            h = hashlib.sha256()
+            h.update(np.ascontiguousarray(X[j], "<f4").tobytes())
+            h.update(np.ascontiguousarray(Y[j], "<f4").tobytes())
+            h.update(np.ascontiguousarray(V[j], "<i4").tobytes())
+            out.append(h.hexdigest())
+        return out
+
+    def mismatched(cols):
+        return sum(1 for a, b in zip(cols, cfg["columns"]) if a != b) + abs(len(cols) - len(cfg["columns"]))
+
+    tc = lib.KLTCreateTrackingContext()
+    tc.contents.sequentialMode = 1
+    ctx = lib.klt_amd_device_context(tc)
+    check(lib, ctx, lib.klt_hip_set_frames_overlap(ctx, 1), "overlap")
+    use_torch_stream(lib, ctx, dev)
+    fr = torch.empty((NFR, H, W), dtype=torch.uint8, device=dev)
+    check(lib, ctx, lib.klt_hip_synth_frames(ctx, seed, 0, NFR, W, H, C.c_void_p(fr.data_ptr()), W, W * H), "synth")
+    host = fr.cpu().numpy()  # the sequence leg's pageable host frames (the same bytes)
+    fl = lib.KLTCreateFeatureList(NF)
+    lib.KLTSelectGoodFeatures(tc, host[0].ctypes.data_as(U8P), W, H, fl)
+    sel = fl_to_arrays(fl)
+    lib.KLTFreeFeatureList(fl)
+    pd, td = PyrDesc(), TrackDesc()
+    lib.klt_amd_pyr_desc(tc, W, H, tc.contents.nPyramidLevels, 1, C.byref(pd))
+    lib.klt_amd_track_desc(tc, C.byref(td))
+    tab = [torch.empty((T, NF), dtype=dt, device=dev) for dt in (torch.float32, torch.float32, torch.int32)]
+    xyz = [torch.from_numpy(np.asarray(a).copy()).to(dev) for a in sel]
+
+    def device_run():
+        for t, a in zip(xyz, sel):
+            t.copy_(torch.from_numpy(np.asarray(a)))
+        check(lib, ctx, lib.klt_hip_frames_begin(ctx, C.byref(pd), C.c_void_p(fr.data_ptr()), W), "4k begin")
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        check(lib, ctx, lib.klt_hip_track_frames(
+            ctx, C.byref(pd), C.byref(td), C.c_void_p(fr.data_ptr() + W * H), W, W * H, T, chunk,
+            *[C.c_void_p(t.data_ptr()) for t in xyz], NF, *[C.c_void_p(t.data_ptr()) for t in tab], NF), "4k frames")
+        torch.cuda.synchronize()
+        return time.perf_counter() - a
+
+    device_run()  # warm-up: allocations, banks written once
+    dt_dev = device_run()
+    dev_cols = digest_cols(*(t.cpu().numpy() for t in tab))
+    live_dev = int((xyz[2] >= 0).sum().item())
+    lib.KLTFreeTrackingContext(tc)
+    del fr, tab, xyz
+    torch.cuda.empty_cache()
+
+    arr = (U8P * NFR)(*[host[t].ctypes.data_as(U8P) for t in range(NFR)])
+    ft = lib.KLTCreateFeatureTable(T, NF)
+
+    def sequence():
+        tc = lib.KLTCreateTrackingContext()
+        tc.contents.sequentialMode = 1
+        fl = lib.KLTCreateFeatureList(NF)
+        lib.KLTSelectGoodFeatures(tc, host[0].ctypes.data_as(U8P), W, H, fl)
+        a = time.perf_counter()
+        lib.KLTTrackSequence(tc, arr, NFR, W, H, fl, ft, 0)
+        d = time.perf_counter() - a
+        lib.KLTFreeFeatureList(fl)
+        lib.KLTFreeTrackingContext(tc)
+        return d
+
+    sequence()  # warm-up call: the device context, staging and host threads; the table's first touch
+    dt_seq = sequence()
+    nfr = ft.contents.nFrames
+    base = C.addressof(ft.contents.feature[0][0].contents)
+    raw = np.ctypeslib.as_array((C.c_uint8 * (64 * NF * nfr)).from_address(base)).view(np.int32)
+    raw = raw.reshape(NF, nfr, 16)[:, :T]
+    seq_cols = digest_cols(raw[:, :, 0].view(np.float32).T, raw[:, :, 1].view(np.float32).T, raw[:, :, 2].T)
+    lib.KLTFreeFeatureTable(ft)
+    del host
+    lib.klt_amd_release_cached_devices()
+    return {"workload": f"{W}x{H}, {NF} features selected on frame 0, {T} tracked frames (BASELINE config 4 on one "
+                        f"GPU, seed {seed}), KLTStoreFeatureList per frame",
+            "device": {"value": T / dt_dev, "unit": "frames/s", "frames": T, "ms": 1e3 * dt_dev,
+                       "region": "klt_hip_track_frames over frames resident in HBM, feature table on the device, "
+                                 f"{chunk}-frame chunks, next chunk's pyramids on a second stream",
+                       "live_features_at_end": live_dev, "columns_mismatched": mismatched(dev_cols)},
+            "sequence": {"value": T / dt_seq, "unit": "frames/s", "frames": T, "ms": 1e3 * dt_seq,
+                         "region": "one KLTTrackSequence call over pageable host frames writing a host "
+                                   "KLT_FeatureTable (PCIe uploads and table rows inside the region)",
+                         "columns_mismatched": mismatched(seq_cols)},
+            "parity": f"every column of both tables against tests/golden/long_config4.json ({len(cfg['columns'])} "
+                      "reference digests)"}
 
 
 def attach_traffic(line, pmc, resolution, fpl) -> None:

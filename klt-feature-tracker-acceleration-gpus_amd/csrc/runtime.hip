@@ -293,6 +293,17 @@ namespace {
     if (e_ != hipSuccess) return fail((c), "%s: %s", #expr, hipGetErrorString(e_));    \
   } while (0)
 
+bool seq_trace() {
+  static const bool t = getenv("KLT_SEQ_TRACE") && atoi(getenv("KLT_SEQ_TRACE")) != 0;
+  return t;
+}
+
+double wall_us() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+
 int use_device(klt_hip_ctx *c) {
   HIPCHK(c, hipSetDevice(c->device));
   return 0;
@@ -2116,16 +2127,28 @@ KLT_API int klt_hip_track_frames_host(klt_hip_ctx *c, const klt_hip_pyr_desc *pd
     HIPCHK(c, hipEventRecord(c->ev_rows[k], c->stream));
   }
   const int nchunks = (nframes + F - 1) / F;
+  // KLT_SEQ_TRACE=1: one stderr line per call -- host time waiting for the
+  // staging slot's previous DMA, copying frames into staging, waiting for the
+  // table rows and handing them out, and the whole call (tools/seq_variance.py)
+  const bool trace = seq_trace();
+  double tr_dma = 0, tr_copy = 0, tr_rows = 0, tr_deliver = 0;
+  const double tr0 = trace ? wall_us() : 0.0;
   auto upload = [&](int ci) -> int {
     const int k = ci & 1, f0 = ci * F, nf = F < nframes - f0 ? F : nframes - f0;
     unsigned char *stage = c->h_stage + (size_t)k * F * fb;
+    const double a = trace ? wall_us() : 0.0;
     HIPCHK(c, hipEventSynchronize(c->ev_dma[k]));  // the slot's previous DMA is done
+    const double b = trace ? wall_us() : 0.0;
     const size_t piece = 512 << 10, per = (fb + piece - 1) / piece;
     if (host_parallel(c, (size_t)nf * per, [&](size_t t) {
           const size_t f = t / per, o = (t - f * per) * piece;
           copy_stream(stage + f * fb + o, frames[f0 + f] + o, fb - o < piece ? fb - o : piece);
         }))
       return -1;
+    if (trace) {
+      tr_dma += b - a;
+      tr_copy += wall_us() - b;
+    }
     HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_ring_free[k], 0));
     HIPCHK(c, hipMemcpyAsync(c->d_ring + (size_t)k * F * fb, stage, (size_t)nf * fb, hipMemcpyHostToDevice,
                              c->cstream));
@@ -2148,14 +2171,21 @@ KLT_API int klt_hip_track_frames_host(klt_hip_ctx *c, const klt_hip_pyr_desc *pd
     span(ci, t0, nt, skip);
     if (!rows || nt <= 0 || n <= 0) return 0;
     const int k = ci & 1;
+    const double a0 = trace ? wall_us() : 0.0;
     HIPCHK(c, hipEventSynchronize(c->ev_rows[k]));
+    const double a1 = trace ? wall_us() : 0.0;
     const float *hx = c->h_rows + k * rows_slot, *hy = hx + (size_t)F * n;
     const int *hv = reinterpret_cast<const int *>(hy + (size_t)F * n);
     const int per = 256;
-    return host_parallel(c, (size_t)(n + per - 1) / per, [&](size_t t) {
+    const int rc = host_parallel(c, (size_t)(n + per - 1) / per, [&](size_t t) {
       const int a = (int)t * per, b = a + per < n ? a + per : n;
       rows(user, t0, nt, a, b, hx, hy, hv, n);
     });
+    if (trace) {
+      tr_rows += a1 - a0;
+      tr_deliver += wall_us() - a1;
+    }
+    return rc;
   };
   if (upload(0)) return -1;
   if (seed_first) {  // frames[0]'s pyramid, built from its uploaded copy
@@ -2193,6 +2223,10 @@ KLT_API int klt_hip_track_frames_host(klt_hip_ctx *c, const klt_hip_pyr_desc *pd
     HIPCHK(c, hipMemcpyAsync(c->h_feat, c->d_feat, 3 * sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
     if (feat_unpack(c, x, y, val, n)) return -1;
   }
+  if (trace)
+    fprintf(stderr, "seqtrace frames=%d chunks=%d total_us=%.0f wait_dma_us=%.0f stage_copy_us=%.0f "
+            "wait_rows_us=%.0f deliver_us=%.0f threads=%d\n", nframes, nchunks, wall_us() - tr0, tr_dma, tr_copy,
+            tr_rows, tr_deliver, c->copy_threads);
   return 0;
 }
 

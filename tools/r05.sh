@@ -38,6 +38,18 @@ for step in "$@"; do
       timeout -k 10 1100 python3 -u tools/shard_sim.py --frames 1001 --chunk 64 --worlds 1 8 --margins 64 --pass1-shared \
         > $OUT/shard8.log 2>&1 || { tail -20 $OUT/shard8.log; exit 1; }
       head -3 $OUT/shard8.log ;;
+    apitl)  # per-call KLTTrackFeatures timeline, registered buffers (tools/api_timeline.py)
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d $OUT/apitl -o run --output-format csv -- \
+        python3 tools/api_timeline.py run --register --frames 60 > $OUT/apitl.log 2>&1 || { tail -20 $OUT/apitl.log; exit 1; }
+      python3 tools/api_timeline.py summary $OUT/apitl > $OUT/apitl_summary.txt 2>&1 || { tail -20 $OUT/apitl_summary.txt; exit 1; }
+      tail -25 $OUT/apitl_summary.txt ;;
+    seqvar)  # KLTTrackSequence call-to-call variance, plain and under a kernel + copy trace
+      timeout -k 10 300 python3 -u tools/seq_variance.py $OUT > $OUT/seqvar.log 2>&1 || { tail -20 $OUT/seqvar.log; exit 1; }
+      grep -E "fps|seqtrace" $OUT/seqvar.log | cut -c1-220
+      mkdir -p $OUT/seqprof
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d $OUT/seqprof -o run --output-format csv -- \
+        python3 -u tools/seq_variance.py $OUT/seqprof > $OUT/seqprof.log 2>&1 || { tail -20 $OUT/seqprof.log; exit 1; }
+      grep -E "fps|seqtrace" $OUT/seqprof.log | cut -c1-220 ;;
     py:*)
       f=${step#py:}; b=$(basename $f .py)
       timeout -k 10 900 python3 -u $f $OUT > $OUT/$b.log 2>&1 || { tail -30 $OUT/$b.log; exit 1; }

@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""KLTTrackSequence call-to-call variance (calls 2-3x slower now
+and then).  One process makes --calls calls over the same 1080p/5000 host
+frames and feature table (each with a fresh tracking context and selection,
+as bench.py's api.sequence leg does), with KLT_SEQ_TRACE=1 so the library
+prints, per call, the host time spent waiting for a staging slot's DMA,
+copying frames into pinned staging, waiting for and handing out table rows.
+Between calls it measures the host's memcpy bandwidth (pageable -> pageable,
+400 MB) and the H2D DMA bandwidth (pinned, 256 MB), to tell a slow host or
+bus from a slow library.  usage: tools/seq_variance.py OUTDIR [--calls 12]"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("out")
+    ap.add_argument("--calls", type=int, default=12)
+    ap.add_argument("--frames", type=int, default=201)
+    a = ap.parse_args()
+    os.environ["KLT_SEQ_TRACE"] = "1"
+    import torch
+    import kltamd
+    lib = kltamd.load()
+    lib.KLTSetVerbosity(0)
+    W, H, NF, n = 1920, 1080, 5000, a.frames
+    U8P = C.POINTER(C.c_ubyte)
+    dev = torch.device("cuda", 0)
+    fr = torch.empty((n, H, W), dtype=torch.uint8, device=dev)
+    tc = lib.KLTCreateTrackingContext()
+    ctx = lib.klt_amd_device_context(tc)
+    lib.klt_hip_synth_frames(ctx, 1080, 0, n, W, H, C.c_void_p(fr.data_ptr()), W, W * H)
+    torch.cuda.synchronize()
+    host = fr.cpu().numpy()
+    lib.KLTFreeTrackingContext(tc)
+    del fr
+    arr = (U8P * n)(*[host[t].ctypes.data_as(U8P) for t in range(n)])
+    ft = lib.KLTCreateFeatureTable(n - 1, NF)
+    src = np.ones(400 << 20, np.uint8)
+    dst = np.empty_like(src)
+    pin = torch.empty(256 << 20, dtype=torch.uint8).pin_memory()
+    gdst = torch.empty(256 << 20, dtype=torch.uint8, device=dev)
+    rows = []
+    for k in range(a.calls):
+        t0 = time.perf_counter()
+        np.copyto(dst, src)
+        memcpy_gbs = src.nbytes / (time.perf_counter() - t0) / 1e9
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        gdst.copy_(pin, non_blocking=True)
+        torch.cuda.synchronize()
+        h2d_gbs = pin.numel() / (time.perf_counter() - t0) / 1e9
+        tc = lib.KLTCreateTrackingContext()
+        tc.contents.sequentialMode = 1
+        fl = lib.KLTCreateFeatureList(NF)
+        lib.KLTSelectGoodFeatures(tc, host[0].ctypes.data_as(U8P), W, H, fl)
+        sys.stderr.flush()
+        t0 = time.perf_counter()
+        lib.KLTTrackSequence(tc, arr, n, W, H, fl, ft, 0)
+        dt = time.perf_counter() - t0
+        lib.KLTFreeFeatureList(fl)
+        lib.KLTFreeTrackingContext(tc)
+        row = {"call": k, "fps": (n - 1) / dt, "ms": 1e3 * dt, "host_memcpy_gbs_before": memcpy_gbs,
+               "h2d_pinned_gbs_before": h2d_gbs}
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+    lib.KLTFreeFeatureTable(ft)
+    Path(a.out, "seq_variance.json").write_text(json.dumps(rows, indent=1) + "\n")
+
+
+if __name__ == "__main__":
+    main()
