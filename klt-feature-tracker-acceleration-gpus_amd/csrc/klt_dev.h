@@ -165,8 +165,11 @@ hipError_t launch_pyr_l0(hipStream_t st, const uint8_t *src, int pitch, long str
                          long fs0, long fsh, int F, int ty0, int ty1, int py0 = 0, int py1 = 1 << 30, int il = 0);
 // k_pyr_l1 over F frames, level-1 tile rows [ty0, ty1)
 // il != 0 (both): the planes interleaved per pixel, {gx, gy, img} at img + 3*(y*w + x); gx/gy unused
+// thin: 8-row tiles (ty0/ty1 in those), for a single frame; else geom::L1_TH rows
 hipError_t launch_pyr_l1(hipStream_t st, const float *hs, int W1, int H, int H1, const DefTaps &T, int vec,
-                         float *img1, float *gx1, float *gy1, long fsh, long fs1, int F, int ty0, int ty1, int il = 0);
+                         float *img1, float *gx1, float *gy1, long fsh, long fs1, int F, int ty0, int ty1, int il = 0,
+                         int thin = 0);
+constexpr int kL1ThinRows = 8;  // launch_pyr_l1's thin tiles
 // generic one-pass kernels (any sigma / levels / subsampling)
 hipError_t launch_u8_to_f32(hipStream_t st, const uint8_t *src, long pitch, int W, int H, float *out);
 hipError_t launch_rows(hipStream_t st, const float *in, int W, int H, const RTaps &t, float *out);

@@ -585,25 +585,32 @@ __global__ __launch_bounds__(L0G<TH_>::NT) void k_pyr_l0(const uint8_t *__restri
 
 // ---------------------------------------------------------------------------
 // k_pyr_l1: img1 = cols_p(hs) sampled at rows 4Y+2 (rest of pyramid.c:114-124)
-// and its gradients.  One 256-thread workgroup per 32x32 tile of level 1.
+// and its gradients.  One 256-thread workgroup per 32 x TH tile of level 1:
+// TH = 32 for batches (geom::L1_TH: the band bookkeeping's unit), TH = 8 for
+// a single frame (a klt.h call's slot), where 32-row tiles leave 135 of 256
+// CUs a workgroup each (1080p) and the launch is one tile's latency.
 // ---------------------------------------------------------------------------
-namespace l1 {
-constexpr int RG = kRG, RP = kRP, SS = kSS, TW = geom::L1_TW, TH = geom::L1_TH, NT = 256;
-constexpr int JW = 40;                          // img1 / hs columns: X in [x0-4, x0+36)
-constexpr int JH = TH + 2 * RG;                 // img1 rows: Y in [y0-3, y0+TH+3)
-constexpr int HR = SS * (JH - 1) + 2 * RP + 1;  // hs rows: [4y0-20, 4y0-20+HR)
-constexpr int LDS_H = HR * JW, LDS_J = JH * JW, LDS_X = JH * TW;
-constexpr int LDS = LDS_H + LDS_J;
-static_assert(2 * LDS_X + TH * 3 * TW <= LDS_H, "tx/ty and the interleaved output tile reuse the hs region");
-static_assert(HR == geom::L1_HR, "geometry");
-}  // namespace l1
+template <int TH_>
+struct L1G {
+  static constexpr int RG = kRG, RP = kRP, SS = kSS, TW = geom::L1_TW, TH = TH_, NT = 256;
+  static constexpr int JW = 40;                          // img1 / hs columns: X in [x0-4, x0+36)
+  static constexpr int JH = TH + 2 * RG;                 // img1 rows: Y in [y0-3, y0+TH+3)
+  static constexpr int HR = SS * (JH - 1) + 2 * RP + 1;  // hs rows: [4y0-20, 4y0-20+HR)
+  static constexpr int LDS_H = HR * JW, LDS_J = JH * JW, LDS_X = JH * TW;
+  static constexpr int LDS = LDS_H + LDS_J;
+  static_assert(2 * LDS_X + TH * 3 * TW <= LDS_H, "tx/ty and the interleaved output tile reuse the hs region");
+};
+static_assert(L1G<geom::L1_TH>::HR == geom::L1_HR, "geometry");
+constexpr int kL1ThinTH = 8;  // single-frame level-1 tiles
 
-template <bool IL>
-__global__ __launch_bounds__(l1::NT) void k_pyr_l1(const float *__restrict__ hs, int W1, int H, int H1,
-                                                   DefTaps T, int vec, float *__restrict__ img1,
-                                                   float *__restrict__ gx1, float *__restrict__ gy1,
-                                                   long fs_hs, long fs1, int ty0, int tiles_x, int tiles_y) {
-  using namespace l1;
+template <bool IL, int TH_>
+__global__ __launch_bounds__(256) void k_pyr_l1(const float *__restrict__ hs, int W1, int H, int H1,
+                                                DefTaps T, int vec, float *__restrict__ img1,
+                                                float *__restrict__ gx1, float *__restrict__ gy1,
+                                                long fs_hs, long fs1, int ty0, int tiles_x, int tiles_y) {
+  using G = L1G<TH_>;
+  constexpr int RG = G::RG, RP = G::RP, SS = G::SS, TW = G::TW, TH = G::TH, NT = G::NT, JW = G::JW, JH = G::JH,
+                HR = G::HR, LDS_H = G::LDS_H, LDS_X = G::LDS_X, LDS = G::LDS;
   hs += blockIdx.z * fs_hs;
   img1 += blockIdx.z * fs1;
   gx1 += blockIdx.z * fs1;
@@ -1007,15 +1014,25 @@ hipError_t launch_pyr_l0(hipStream_t st, const uint8_t *src, int pitch, long str
 }
 
 hipError_t launch_pyr_l1(hipStream_t st, const float *hs, int W1, int H, int H1, const DefTaps &T, int vec,
-                         float *img1, float *gx1, float *gy1, long fsh, long fs1, int F, int ty0, int ty1, int il) {
-  const int tx = (W1 + l1::TW - 1) / l1::TW;
+                         float *img1, float *gx1, float *gy1, long fsh, long fs1, int F, int ty0, int ty1, int il,
+                         int thin) {
+  const int tx = (W1 + geom::L1_TW - 1) / geom::L1_TW;
   if (F <= 0 || ty1 <= ty0) return hipSuccess;
+  if (thin) {  // single frame: ty0/ty1 in 8-row tiles
+    if (il)
+      hipLaunchKernelGGL((k_pyr_l1<true, kL1ThinTH>), dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(256), 0, st, hs,
+                         W1, H, H1, T, vec, img1, gx1, gy1, fsh, fs1, ty0, tx, ty1 - ty0);
+    else
+      hipLaunchKernelGGL((k_pyr_l1<false, kL1ThinTH>), dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(256), 0, st, hs,
+                         W1, H, H1, T, vec, img1, gx1, gy1, fsh, fs1, ty0, tx, ty1 - ty0);
+    return hipGetLastError();
+  }
   if (il)
-    hipLaunchKernelGGL(k_pyr_l1<true>, dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(l1::NT), 0, st, hs, W1, H, H1, T,
-                       vec, img1, gx1, gy1, fsh, fs1, ty0, tx, ty1 - ty0);
+    hipLaunchKernelGGL((k_pyr_l1<true, geom::L1_TH>), dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(256), 0, st, hs,
+                       W1, H, H1, T, vec, img1, gx1, gy1, fsh, fs1, ty0, tx, ty1 - ty0);
   else
-    hipLaunchKernelGGL(k_pyr_l1<false>, dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(l1::NT), 0, st, hs, W1, H, H1, T,
-                       vec, img1, gx1, gy1, fsh, fs1, ty0, tx, ty1 - ty0);
+    hipLaunchKernelGGL((k_pyr_l1<false, geom::L1_TH>), dim3(xcd_grid(tx * (ty1 - ty0)), 1, F), dim3(256), 0, st, hs,
+                       W1, H, H1, T, vec, img1, gx1, gy1, fsh, fs1, ty0, tx, ty1 - ty0);
   return hipGetLastError();
 }
 

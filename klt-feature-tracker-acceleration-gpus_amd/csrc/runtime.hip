@@ -554,6 +554,15 @@ int launch_l0(klt_hip_ctx *c, hipStream_t st, const uint8_t *src, long pitch, lo
                                                hs, W1, do_hs, fs0, fsh, F, ty0, ty1, py0, py1, il));
 }
 
+// KLT_L1_THIN=0: a single frame's level 1 in 32-row tiles too (A/B)
+bool l1_thin() {
+  static const bool on = [] {
+    const char *v = getenv("KLT_L1_THIN");
+    return !(v && *v && atoi(v) == 0);
+  }();
+  return on;
+}
+
 int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
                 hipStream_t st) {
   Slot &S = c->slot[s];
@@ -576,9 +585,11 @@ int build_fused(klt_hip_ctx *c, int s, const klt_hip_pyr_desc *d, const uint8_t 
   if (two && (long)W1 * H1 > 0) {
     TimedScope ts(c, T_L1, st);
     const int vec = (W1 % 4 == 0 && W1 >= 8) ? 1 : 0;
-    const int ty = (H1 + geom::L1_TH - 1) / geom::L1_TH;
+    // one frame: thin tiles (a 32-row tile per workgroup leaves most CUs idle)
+    const int thin = l1_thin() ? 1 : 0, th = thin ? kL1ThinRows : geom::L1_TH;
+    const int ty = (H1 + th - 1) / th;
     if (launched(c, "k_pyr_l1", launch_pyr_l1(st, c->d_hs, W1, H, H1, T, vec, S.lv[1].img, S.lv[1].gx, S.lv[1].gy,
-                                              0L, 0L, 1, 0, ty, 1)))
+                                              0L, 0L, 1, 0, ty, 1, thin)))
       return -1;
   }
   return 0;
