@@ -420,7 +420,8 @@ def run_sharded(args, world, rank, dev) -> None:
     holds only the rows of each frame its band build reads (its band, margin
     and tile halo: kltamd.shard.BandFrames, synthesized in place of its
     ingest), builds pyramids for its row band (+margin) and tracks the features
-    it owns; one all-reduce of the owners' (x, y, val) per chunk (kltamd.shard)."""
+    it owns; one all-gather of the owners' (x, y, val) slots per chunk
+    (kltamd.shard)."""
     import torch
     import torch.distributed as dist
 
@@ -457,11 +458,17 @@ def run_sharded(args, world, rank, dev) -> None:
     lib.klt_amd_pyr_desc(tc, W, H, tc.contents.nPyramidLevels, 1, C.byref(pd))
     lib.klt_amd_track_desc(tc, C.byref(td))
 
-    def all_reduce(t):
-        if world > 1:
-            dist.all_reduce(t)
+    def all_gather(out, inp):  # the per-chunk exchange: every rank's slot, in rank order
+        if world == 1:
+            out.copy_(inp)
+        elif dist.get_backend() == "gloo":  # the shared-GPU rehearsal (KLT_BENCH_SHARE_GPU=1)
+            parts = [torch.empty_like(inp) for _ in range(world)]
+            dist.all_gather(parts, inp)
+            out.copy_(torch.cat(parts))
+        else:
+            dist.all_gather_into_tensor(out, inp)
 
-    seq = ShardedSequence(lib, ctx, pd, td, frames, x, y, v, rank, world, all_reduce, chunk=args.chunk,
+    seq = ShardedSequence(lib, ctx, pd, td, frames, x, y, v, rank, world, all_gather, chunk=args.chunk,
                           margin=args.margin)
     seq.begin(0)
     seq.run(1, args.warmup)

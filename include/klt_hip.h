@@ -371,6 +371,30 @@ int klt_hip_min_eigen_rows(klt_hip_ctx *ctx, const klt_hip_select_desc *desc, in
 int klt_hip_select_map(klt_hip_ctx *ctx, int ncols, int nrows, const klt_hip_select_desc *desc, int mindist,
                        int min_eigenvalue, const int *dev_map, float *x, float *y, int *val, int n);
 
+/* The sharded schedule's exchange as an all-gather of per-rank slots (SURVEY
+   8e; kltamd/shard.py and klt_shard_track use it).  Rank r owns the live
+   features (val >= 0) whose chunk-start y0 lies in [edges[r], edges[r+1])
+   (edges: world+1 floats, edges[0] = -inf, edges[world] = +inf; the band
+   test of klt_hip_track_frames_band).  gather_order fills the device int
+   array work[n + world]: per feature its owner and place among the owner's
+   features in index order, then every rank's count (work + n).  gather_pack
+   writes rank `rank`'s owned (x, y, val) bit patterns into its slot of
+   KLT_HIP_GATHER_SLOT_WORDS(S) int32 (S >= the largest count) with the escape
+   flag (device int, may be NULL) and a failure count; the caller all-gathers
+   the slots; gather_unpack takes every feature from its owner's slot
+   (slots[k] is rank first_rank + k's, k < nslots; features of ranks outside
+   them are left as they are) and writes flags[0] = the escape flags summed,
+   flags[1] = the failures summed (a slot shorter than its count counts as
+   one; nothing is unpacked then).  All three queue on the context's stream. */
+#define KLT_HIP_GATHER_MAX_RANKS 64
+#define KLT_HIP_GATHER_SLOT_WORDS(S) (4 + 3 * (long)(S))
+int klt_hip_gather_order(klt_hip_ctx *ctx, const float *y0, const int *v0, int n, const float *edges, int world,
+                         int *work);
+int klt_hip_gather_pack(klt_hip_ctx *ctx, const float *x, const float *y, const int *val, const int *work, int n,
+                        int world, int rank, const int *escape, int nfail, int *slot, int S);
+int klt_hip_gather_unpack(klt_hip_ctx *ctx, const int *slots, int nslots, int first_rank, const int *work, int n,
+                          int S, float *x, float *y, int *val, int *flags);
+
 /* synthetic frames t0..t0+n-1 (include/klt_synth.h) into device memory */
 int klt_hip_synth_frames(klt_hip_ctx *ctx, unsigned long long seed, int t0, int n, int ncols,
                          int nrows, unsigned char *dev, long pitch, long frame_stride);

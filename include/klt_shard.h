@@ -8,12 +8,14 @@
  * Rank r of N owns the features whose y lies in its row band
  * [r*H/N, (r+1)*H/N) at the start of a chunk, builds band-limited pyramids
  * (its band +/- margin rows; klt_hip_track_frames_band) and tracks them;
- * after each chunk one RCCL all-reduce of the int32 bit patterns of
- * (x, y, val) -- every feature has exactly one contributor: its owner, rank 0
- * for lost features -- leaves every rank with the same list, bit-identical
- * to one GPU's.  A window that needs rows a rank did not build raises an
- * escape flag that rides in the same all-reduce; every rank then redoes the
- * chunk from whole frames (obtained through the caller's callback).
+ * after each chunk one RCCL all-gather of fixed per-rank slots -- each rank's
+ * owned features' (x, y, val) bit patterns in index order
+ * (klt_hip_gather_order/pack/unpack; every rank knows every feature's owner
+ * from the common chunk-start state, lost features are nobody's and stay as
+ * they are) -- leaves every rank with the same list, bit-identical to one
+ * GPU's.  A window that needs rows a rank did not build raises an escape
+ * flag that rides in the slot's header; every rank then redoes the chunk from
+ * whole frames (obtained through the caller's callback).
  *
  * Usage, per rank:
  *   rank 0: klt_shard_unique_id(id); distribute id (MPI, a file, a socket);
@@ -49,10 +51,10 @@ int klt_shard_unique_id(unsigned char id[KLT_SHARD_ID_BYTES]);
 klt_shard *klt_shard_create(klt_hip_ctx *ctx, int rank, int world, const unsigned char id[KLT_SHARD_ID_BYTES],
                             int nrows, int margin);
 /* single-process rehearsal (tests): the band of rank/world, but the exchange
-   runs over a communicator of this rank alone, so klt_shard_track leaves only
-   this rank's contribution (its owned features, rank 0 also the lost ones;
-   0 elsewhere) and redoes a chunk only when this rank escaped.  The caller
-   sums the ranks' int32 bit patterns to get the merged list. */
+   runs over a communicator of this rank alone, so klt_shard_track updates
+   only this rank's owned features (the others keep their chunk-start values)
+   and redoes a chunk only when this rank escaped.  The caller takes each
+   feature from its owner's result to get the merged list. */
 klt_shard *klt_shard_create_local(klt_hip_ctx *ctx, int rank, int world, int nrows, int margin);
 /* before the tracking context that owns ctx is freed (it synchronizes ctx) */
 void klt_shard_destroy(klt_shard *s);
@@ -62,7 +64,7 @@ const char *klt_shard_last_error(klt_shard *s);
    caller passes every rank the same geometry, so every rank returns there.
    A failure after that point (a device call, the whole-frame callback, the
    band build) does not skip the rank's collectives: klt_shard_track sends a
-   failure count with its all-reduce and klt_shard_replace agrees on one
+   failure count in its slot of the all-gather and klt_shard_replace agrees on one
    before its broadcasts, so every rank returns < 0 together ("peer rank(s)
    failed" on the others) and none waits for a rank that left.  A rank that
    cannot take part at all (its exchange buffers cannot be allocated) aborts

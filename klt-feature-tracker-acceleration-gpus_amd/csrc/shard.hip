@@ -1,8 +1,8 @@
 // shard.hip -- feature-sharded tracking over N GPUs for C callers
 // (include/klt_shard.h): the row-band decomposition of BASELINE config 4 on
 // top of klt_hip_track_frames_band, with the per-chunk exchange as one RCCL
-// all-reduce on the context's stream.  kltamd/shard.py is the same schedule
-// for torch.distributed callers; both merge bit for bit.
+// all-gather of per-rank slots on the context's stream.  kltamd/shard.py is
+// the same schedule for torch.distributed callers; both merge bit for bit.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -33,11 +33,16 @@ struct klt_shard {
   int row_lo = 0, row_hi = 0;           // level-0 rows built
   int load_lo = 0, load_hi = 0;         // u8 rows the band build reads
   ncclComm_t comm = nullptr;
-  int *d_buf = nullptr;                 // 3n+2 int32: x | y | val bit patterns, escape flag, error count
+  std::vector<float> edges;             // world+1 band edges (ownership of every rank's features)
+  int *d_send = nullptr;                // this rank's slot: KLT_HIP_GATHER_SLOT_WORDS(S) int32, S <= cap
+  int *d_recv = nullptr;                // cranks slots, all-gathered
+  int *d_work = nullptr;                // gather order: n codes + world counts
+  int *d_esc = nullptr;                 // device escape flag | exchange flags (escapes, failures) | agreement word
   float *d_x0 = nullptr, *d_y0 = nullptr;
   int *d_v0 = nullptr;                  // chunk-start state (ownership, redo)
   size_t cap = 0;
-  int *h_flag = nullptr;                // pinned: the summed escape flag and error count
+  int *h_flag = nullptr;                // pinned: the summed escape flag and error count, then world counts
+  hipEvent_t ev_counts = nullptr;       // the counts' download
   bool dead = false;                    // the communicator was aborted (a rank could not take part)
   int *d_map = nullptr;                 // the trackability map (replacement)
   size_t map_cap = 0;
@@ -89,35 +94,6 @@ int abort_comm(klt_shard *s, const char *what) {
   return sfail(s, "%s (communicator aborted)", what);
 }
 
-// the owners' bit patterns, zero elsewhere (rank 0 also contributes the lost
-// features, which nobody tracks); the escape flag as the last element
-__global__ void k_shard_pack(const float *__restrict__ x, const float *__restrict__ y, const int *__restrict__ v,
-                             const float *__restrict__ y0, const int *__restrict__ v0, float own_lo, float own_hi,
-                             int rank0, const int *__restrict__ escape, int failed, int nfail,
-                             int *__restrict__ buf, int n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) {
-    const bool owned = !failed && v0[i] >= 0 && y0[i] >= own_lo && y0[i] < own_hi;  // k_band_order's test
-    const bool keep = owned || (!failed && rank0 && v0[i] < 0);
-    buf[i] = keep ? __float_as_int(x[i]) : 0;
-    buf[n + i] = keep ? __float_as_int(y[i]) : 0;
-    buf[2 * n + i] = keep ? v[i] : 0;
-  }
-  if (i == 0) {
-    buf[3 * n] = escape && !failed ? *escape : 0;
-    buf[3 * n + 1] = nfail;
-  }
-}
-
-__global__ void k_shard_unpack(const int *__restrict__ buf, float *__restrict__ x, float *__restrict__ y,
-                               int *__restrict__ v, int n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  x[i] = __int_as_float(buf[i]);
-  y[i] = __int_as_float(buf[n + i]);
-  v[i] = buf[2 * n + i];
-}
-
 // the chunk-start state (ownership and the redo's starting point) and the
 // escape flag's reset in one launch: no copy-engine hand-offs between two
 // tracker launches
@@ -133,19 +109,138 @@ __global__ void k_shard_save(const float *__restrict__ x, const float *__restric
   if (i == 0) *escape = 0;
 }
 
+// ---------------------------------------------------------------------------
+// The exchange as an all-gather of per-rank slots.  Every rank
+// holds the same chunk-start state and the same band edges, so every rank
+// knows, for every live feature, its owner q (edges[q] <= y0 < edges[q+1],
+// k_band_order's test) and its place p among q's features in index order
+// (k_gather_order: code = q << 24 | p, counts[q]).  Rank q packs its owned
+// features' (x, y, val) bit patterns at places 0 .. counts[q]-1 of its slot
+// (k_gather_pack), the slots are all-gathered, and every rank takes each
+// feature from its owner's slot (k_gather_unpack).  Lost features are nobody's
+// and stay as they are on every rank.  A slot: {escape, failures, count, S,
+// x[S], y[S], val[S]} int32, S >= max counts (the drivers read counts first).
+// ---------------------------------------------------------------------------
+constexpr int kGatherHdr = 4;
+constexpr int kGatherThreads = 1024;
+
+struct GatherEdges {
+  float e[KLT_HIP_GATHER_MAX_RANKS + 1];
+  int world;
+};
+
+__global__ __launch_bounds__(kGatherThreads) void k_gather_order(const float *__restrict__ y0,
+                                                                 const int *__restrict__ v0, int n, GatherEdges E,
+                                                                 int *__restrict__ code, int *__restrict__ counts) {
+  constexpr int NW = kGatherThreads / 64;
+  __shared__ int wc[NW][KLT_HIP_GATHER_MAX_RANKS];
+  __shared__ int base[KLT_HIP_GATHER_MAX_RANKS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < E.world) base[tid] = 0;
+  __syncthreads();
+  for (int r0 = 0; r0 < n; r0 += kGatherThreads) {  // rounds of 1024 features, in index order
+    const int i = r0 + tid;
+    int q = -1;
+    if (i < n && v0[i] >= 0) {
+      const float y = y0[i];
+      for (int r = 0; r < E.world; ++r)
+        if (y >= E.e[r] && y < E.e[r + 1]) {
+          q = r;
+          break;
+        }
+    }
+    int mine = 0;
+    for (int r = 0; r < E.world; ++r) {
+      const unsigned long long b = __ballot(q == r);
+      if (lane == 0) wc[wave][r] = __popcll(b);
+      if (q == r) mine = __popcll(b & ((1ull << lane) - 1ull));
+    }
+    __syncthreads();
+    if (q >= 0) {
+      int p = base[q] + mine;
+      for (int w = 0; w < wave; ++w) p += wc[w][q];
+      code[i] = (q << 24) | p;
+    } else if (i < n) {
+      code[i] = -1;
+    }
+    __syncthreads();
+    if (tid < E.world) {
+      int t = 0;
+      for (int w = 0; w < NW; ++w) t += wc[w][tid];
+      base[tid] += t;
+    }
+    __syncthreads();
+  }
+  if (tid < E.world) counts[tid] = base[tid];
+}
+
+__global__ void k_gather_pack(const float *__restrict__ x, const float *__restrict__ y, const int *__restrict__ v,
+                              const int *__restrict__ code, const int *__restrict__ counts, int n, int rank,
+                              const int *__restrict__ escape, int nfail, int *__restrict__ slot, int S) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const int c = code[i];
+    if (c >= 0 && (c >> 24) == rank) {
+      const int p = c & 0xFFFFFF;
+      if (p < S) {
+        slot[kGatherHdr + p] = __float_as_int(x[i]);
+        slot[kGatherHdr + S + p] = __float_as_int(y[i]);
+        slot[kGatherHdr + 2 * S + p] = v[i];
+      }
+    }
+  }
+  if (i == 0) {
+    slot[0] = escape ? *escape : 0;
+    slot[1] = nfail;
+    slot[2] = counts[rank];
+    slot[3] = S;
+  }
+}
+
+// slots[k] is rank r0 + k's (k < nslots); features of other owners stay as
+// they are.  flags[0]: the escape flags summed, flags[1]: failures (a slot too
+// short for its count is one); nothing is unpacked when flags[1] != 0.
+__global__ void k_gather_unpack(const int *__restrict__ slots, int nslots, int r0, const int *__restrict__ code,
+                                int n, int S, float *__restrict__ x, float *__restrict__ y, int *__restrict__ v,
+                                int *__restrict__ flags) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const long words = kGatherHdr + 3L * S;
+  int esc = 0, bad = 0;
+  for (int k = 0; k < nslots; ++k) {
+    const int *h = slots + k * words;
+    esc += h[0];
+    bad += h[1] + (h[2] > S || h[3] != S ? 1 : 0);
+  }
+  if (i == 0) {
+    flags[0] = esc;
+    flags[1] = bad;
+  }
+  if (i >= n || bad) return;
+  const int c = code[i];
+  if (c < 0) return;
+  const int k = (c >> 24) - r0;
+  if (k < 0 || k >= nslots) return;
+  const int *sl = slots + k * words + kGatherHdr, p = c & 0xFFFFFF;
+  x[i] = __int_as_float(sl[p]);
+  y[i] = __int_as_float(sl[S + p]);
+  v[i] = sl[2 * S + p];
+}
+
 int grow_buffers(klt_shard *s, int n) {
   if (s->faults & KLT_SHARD_FAULT_ALLOC) return sfail(s, "exchange buffers: injected allocation failure");
-  if ((size_t)n <= s->cap && s->d_buf) return 0;
-  hipFree(s->d_buf);
-  hipFree(s->d_x0);
-  hipFree(s->d_y0);
-  hipFree(s->d_v0);
-  s->d_buf = nullptr;
+  if ((size_t)n <= s->cap && s->d_send) return 0;
+  for (void *p : {(void *)s->d_send, (void *)s->d_recv, (void *)s->d_work, (void *)s->d_esc, (void *)s->d_x0,
+                  (void *)s->d_y0, (void *)s->d_v0})
+    hipFree(p);
+  s->d_send = s->d_recv = s->d_work = s->d_esc = nullptr;
   s->d_x0 = s->d_y0 = nullptr;
   s->d_v0 = nullptr;
   s->cap = 0;
-  const size_t m = n > 0 ? (size_t)n : 1;
-  SHIP(s, hipMalloc((void **)&s->d_buf, (3 * m + 2) * sizeof(int)));
+  const size_t m = n > 0 ? (size_t)n : 1, words = (size_t)KLT_HIP_GATHER_SLOT_WORDS(m);
+  SHIP(s, hipMalloc((void **)&s->d_send, words * sizeof(int)));
+  SHIP(s, hipMalloc((void **)&s->d_recv, (size_t)s->cranks * words * sizeof(int)));
+  SHIP(s, hipMalloc((void **)&s->d_work, (m + s->world) * sizeof(int)));
+  SHIP(s, hipMalloc((void **)&s->d_esc, 4 * sizeof(int)));
   SHIP(s, hipMalloc((void **)&s->d_x0, m * sizeof(float)));
   SHIP(s, hipMalloc((void **)&s->d_y0, m * sizeof(float)));
   SHIP(s, hipMalloc((void **)&s->d_v0, m * sizeof(int)));
@@ -159,30 +254,53 @@ int fail_count(const klt_shard *s, int failed) {
   return (failed ? 1 : 0) + ((s->faults & KLT_SHARD_FAULT_PEER) ? 1 : 0);
 }
 
-// pack this rank's results, all-reduce them with every rank's, unpack; the
-// summed escape flag lands in h_flag[0], the number of ranks that failed this
-// step (failed != 0: this one, which contributes nothing else) in h_flag[1].
-// Every rank calls it at the same point whatever went wrong locally, so no
-// peer waits in the collective for a rank that returned early; a nonzero
-// error count makes every rank return an error.  Synchronous.
-int exchange(klt_shard *s, hipStream_t st, float *x, float *y, int *v, int n, const int *escape, int failed) {
-  const int nb = (n + 255) / 256 > 0 ? (n + 255) / 256 : 1;
-  hipLaunchKernelGGL(k_shard_pack, dim3(nb), dim3(256), 0, st, x, y, v, s->d_y0, s->d_v0, s->own_lo, s->own_hi,
-                     s->rank == 0 ? 1 : 0, escape, failed ? 1 : 0, fail_count(s, failed), s->d_buf, n);
-  SHIP(s, hipGetLastError());
-  SNCCL(s, ncclAllReduce(s->d_buf, s->d_buf, (size_t)3 * n + 2, ncclInt32, ncclSum, s->comm, st));
-  SHIP(s, hipMemcpyAsync(s->h_flag, s->d_buf + (size_t)3 * n, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+// the ownership of the chunk-start state (d_y0, d_v0) and every rank's count,
+// downloaded behind an event (read after the band call is queued)
+int order_counts(klt_shard *s, hipStream_t st, int n) {
+  if (klt_hip_gather_order(s->ctx, s->d_y0, s->d_v0, n, s->edges.data(), s->world, s->d_work))
+    return sfail(s, "%s", klt_hip_last_error(s->ctx));
+  SHIP(s, hipMemcpyAsync(s->h_flag + 2, s->d_work + n, s->world * sizeof(int), hipMemcpyDeviceToHost, st));
+  SHIP(s, hipEventRecord(s->ev_counts, st));
+  return 0;
+}
+
+// the slot size every rank uses: the largest count (the same on every rank,
+// which holds the same chunk-start state)
+int slot_size(klt_shard *s, int *S) {
+  SHIP(s, hipEventSynchronize(s->ev_counts));
+  int m = 1;
+  for (int r = 0; r < s->world; ++r) m = s->h_flag[2 + r] > m ? s->h_flag[2 + r] : m;
+  *S = m;
+  return 0;
+}
+
+// pack this rank's results into its slot, all-gather the slots, take every
+// feature from its owner's; the summed escape flag lands in h_flag[0], the
+// number of ranks that failed this step (failed != 0: this one, whose slot
+// carries nothing else) in h_flag[1].  Every rank calls it at the same point
+// whatever went wrong locally, so no peer waits in the collective for a rank
+// that returned early; a nonzero failure count makes every rank return an
+// error (nothing is unpacked).  A local shard gathers its own slot alone and
+// leaves the other ranks' features as they are.  Synchronous.
+int exchange(klt_shard *s, hipStream_t st, float *x, float *y, int *v, int n, int S, const int *escape, int failed) {
+  const long words = KLT_HIP_GATHER_SLOT_WORDS(S);
+  // a failed rank's slot carries its failure count (its features are never unpacked)
+  if (klt_hip_gather_pack(s->ctx, x, y, v, s->d_work, n, s->world, s->rank, failed ? nullptr : escape,
+                          fail_count(s, failed), s->d_send, S))
+    return sfail(s, "%s", klt_hip_last_error(s->ctx));
+  SNCCL(s, ncclAllGather(s->d_send, s->d_recv, (size_t)words, ncclInt32, s->comm, st));
+  int *flags = s->d_esc + 1;
+  if (klt_hip_gather_unpack(s->ctx, s->d_recv, s->cranks, s->cranks == 1 ? s->rank : 0, s->d_work, n, S, x, y, v,
+                            flags))
+    return sfail(s, "%s", klt_hip_last_error(s->ctx));
+  SHIP(s, hipMemcpyAsync(s->h_flag, flags, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
   SHIP(s, hipStreamSynchronize(st));
-  if (s->h_flag[1] == 0 && n > 0) {
-    hipLaunchKernelGGL(k_shard_unpack, dim3(nb), dim3(256), 0, st, s->d_buf, x, y, v, n);
-    SHIP(s, hipGetLastError());
-  }
   return 0;
 }
 
 // one int32 all-reduce of this rank's failure flag: how many ranks failed
 int agree(klt_shard *s, hipStream_t st, int failed, int *failed_ranks) {
-  int *w = s->d_buf + (size_t)3 * s->cap + 1;
+  int *w = s->d_esc + 3;
   const int mine = fail_count(s, failed);
   SHIP(s, hipMemcpyAsync(w, &mine, sizeof(int), hipMemcpyHostToDevice, st));
   SNCCL(s, ncclAllReduce(w, w, 1, ncclInt32, ncclSum, s->comm, st));
@@ -193,6 +311,50 @@ int agree(klt_shard *s, hipStream_t st, int failed, int *failed_ranks) {
 }
 
 }  // namespace
+
+KLT_API int klt_hip_gather_order(klt_hip_ctx *ctx, const float *y0, const int *v0, int n, const float *edges,
+                                 int world, int *work) {
+  if (!ctx || world < 1 || world > KLT_HIP_GATHER_MAX_RANKS || n < 0 || n >= (1 << 24) || !edges || !work ||
+      (n > 0 && (!y0 || !v0)))
+    return ctx ? kltdev::ctx_fail(ctx, "gather_order: bad argument") : -1;
+  DeviceGuard guard;
+  if (hipSetDevice(klt_hip_ctx_device(ctx)) != hipSuccess) return kltdev::ctx_fail(ctx, "gather_order: device");
+  GatherEdges E{};
+  for (int r = 0; r <= world; ++r) E.e[r] = edges[r];
+  E.world = world;
+  hipLaunchKernelGGL(k_gather_order, dim3(1), dim3(kGatherThreads), 0, (hipStream_t)klt_hip_get_stream(ctx), y0, v0,
+                     n, E, work, work + n);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : kltdev::ctx_fail(ctx, "gather_order: %s", hipGetErrorString(e));
+}
+
+KLT_API int klt_hip_gather_pack(klt_hip_ctx *ctx, const float *x, const float *y, const int *val, const int *work,
+                                int n, int world, int rank, const int *escape, int nfail, int *slot, int S) {
+  if (!ctx || rank < 0 || rank >= world || world > KLT_HIP_GATHER_MAX_RANKS || n < 0 || S < 0 || !work || !slot ||
+      (n > 0 && (!x || !y || !val)))
+    return ctx ? kltdev::ctx_fail(ctx, "gather_pack: bad argument") : -1;
+  DeviceGuard guard;
+  if (hipSetDevice(klt_hip_ctx_device(ctx)) != hipSuccess) return kltdev::ctx_fail(ctx, "gather_pack: device");
+  const int nb = n > 0 ? (n + 255) / 256 : 1;
+  hipLaunchKernelGGL(k_gather_pack, dim3(nb), dim3(256), 0, (hipStream_t)klt_hip_get_stream(ctx), x, y, val, work,
+                     work + n, n, rank, escape, nfail, slot, S);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : kltdev::ctx_fail(ctx, "gather_pack: %s", hipGetErrorString(e));
+}
+
+KLT_API int klt_hip_gather_unpack(klt_hip_ctx *ctx, const int *slots, int nslots, int first_rank, const int *work,
+                                  int n, int S, float *x, float *y, int *val, int *flags) {
+  if (!ctx || nslots < 1 || first_rank < 0 || n < 0 || S < 0 || !slots || !work || !flags ||
+      (n > 0 && (!x || !y || !val)))
+    return ctx ? kltdev::ctx_fail(ctx, "gather_unpack: bad argument") : -1;
+  DeviceGuard guard;
+  if (hipSetDevice(klt_hip_ctx_device(ctx)) != hipSuccess) return kltdev::ctx_fail(ctx, "gather_unpack: device");
+  const int nb = n > 0 ? (n + 255) / 256 : 1;
+  hipLaunchKernelGGL(k_gather_unpack, dim3(nb), dim3(256), 0, (hipStream_t)klt_hip_get_stream(ctx), slots, nslots,
+                     first_rank, work, n, S, x, y, val, flags);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : kltdev::ctx_fail(ctx, "gather_unpack: %s", hipGetErrorString(e));
+}
 
 KLT_API int klt_shard_unique_id(unsigned char id[KLT_SHARD_ID_BYTES]) {
   if (!id) return -1;
@@ -227,9 +389,16 @@ klt_shard *make_shard(klt_hip_ctx *ctx, int rank, int world, const unsigned char
   s->load_hi = t_hi + halo < nrows ? t_hi + halo : nrows;
   ncclUniqueId u;
   memcpy(&u, id, sizeof u);
-  if (hipSetDevice(klt_hip_ctx_device(ctx)) != hipSuccess || ncclCommInitRank(&s->comm, cranks, u, crank) != ncclSuccess ||
-      hipHostMalloc((void **)&s->h_flag, 2 * sizeof(int), hipHostMallocDefault) != hipSuccess) {
+  s->edges.resize(world + 1);
+  for (int r = 0; r <= world; ++r) s->edges[r] = (float)((long)r * nrows / world);
+  s->edges[0] = -INFINITY;
+  s->edges[world] = INFINITY;
+  if (world > KLT_HIP_GATHER_MAX_RANKS || hipSetDevice(klt_hip_ctx_device(ctx)) != hipSuccess ||
+      ncclCommInitRank(&s->comm, cranks, u, crank) != ncclSuccess ||
+      hipHostMalloc((void **)&s->h_flag, (2 + world) * sizeof(int), hipHostMallocDefault) != hipSuccess ||
+      hipEventCreateWithFlags(&s->ev_counts, hipEventDisableTiming) != hipSuccess) {
     if (s->comm) ncclCommDestroy(s->comm);
+    if (s->h_flag) hipHostFree(s->h_flag);
     delete s;
     return nullptr;
   }
@@ -253,7 +422,8 @@ KLT_API void klt_shard_destroy(klt_shard *s) {
   if (!s) return;
   if (s->ctx) klt_hip_sync(s->ctx);
   if (s->comm) ncclCommDestroy(s->comm);
-  hipFree(s->d_buf);
+  for (void *p : {(void *)s->d_send, (void *)s->d_recv, (void *)s->d_work, (void *)s->d_esc}) hipFree(p);
+  if (s->ev_counts) hipEventDestroy(s->ev_counts);
   hipFree(s->d_x0);
   hipFree(s->d_y0);
   hipFree(s->d_v0);
@@ -295,19 +465,25 @@ KLT_API int klt_shard_track(klt_shard *s, const klt_hip_pyr_desc *pd, const klt_
   if (hipSetDevice(klt_hip_ctx_device(s->ctx)) != hipSuccess) return abort_comm(s, "shard_track: device");
   hipStream_t st = (hipStream_t)klt_hip_get_stream(s->ctx);
   if (grow_buffers(s, n)) return abort_comm(s, ("shard_track: " + s->err).c_str());
-  // the chunk-start state: ownership (y0, v0) and the redo's starting point
+  // the chunk-start state: ownership (y0, v0) and the redo's starting point;
+  // its gather order and every rank's count go down behind an event
   const size_t fb = sizeof(float) * (size_t)n;
   std::string local;  // this rank's failure, if any: it still takes part in every exchange
-  int *escape = s->d_buf + (size_t)3 * s->cap;  // the buffer's slot after the features doubles as the device flag
+  int *escape = s->d_esc;
   hipLaunchKernelGGL(k_shard_save, dim3(n > 0 ? (n + 255) / 256 : 1), dim3(256), 0, st, x, y, val, s->d_x0, s->d_y0,
                      s->d_v0, escape, n);
-  if (hipGetLastError() != hipSuccess) local = "chunk-start save failed";
-  if (local.empty() && (s->faults & KLT_SHARD_FAULT_LOCAL)) local = "injected local fault";
+  if (hipGetLastError() != hipSuccess) return abort_comm(s, "shard_track: chunk-start save failed");
+  if (order_counts(s, st, n)) return abort_comm(s, ("shard_track: " + s->err).c_str());
+  if (s->faults & KLT_SHARD_FAULT_LOCAL) local = "injected local fault";
   if (local.empty() &&
       klt_hip_track_frames_band(s->ctx, pd, td, frames, pitch, stride, nframes, x, y, val, n, s->own_lo, s->own_hi,
                                 s->row_lo, s->row_hi, escape, next_frames, next_nframes))
     local = klt_hip_last_error(s->ctx);
-  if (exchange(s, st, x, y, val, n, escape, !local.empty())) return abort_comm(s, ("shard_track: " + s->err).c_str());
+  // the slot size, read while the band call runs: every rank reads the same
+  int S = 1;
+  if (slot_size(s, &S)) return abort_comm(s, ("shard_track: " + s->err).c_str());
+  if (exchange(s, st, x, y, val, n, S, escape, !local.empty()))
+    return abort_comm(s, ("shard_track: " + s->err).c_str());
   if (s->h_flag[1]) {
     return local.empty() ? sfail(s, "shard_track: %d peer rank(s) failed this chunk", s->h_flag[1])
                          : sfail(s, "shard_track: %s", local.c_str());
@@ -331,7 +507,8 @@ KLT_API int klt_shard_track(klt_shard *s, const klt_hip_pyr_desc *pd, const klt_
       klt_hip_track_frames_band(s->ctx, pd, td, whole + wstride, pitch, wstride, nframes, x, y, val, n, s->own_lo,
                                 s->own_hi, 0, s->nrows, escape, nullptr, 0))
     local = std::string("redo: ") + klt_hip_last_error(s->ctx);
-  if (exchange(s, st, x, y, val, n, nullptr, !local.empty())) return abort_comm(s, ("shard_track: " + s->err).c_str());
+  if (exchange(s, st, x, y, val, n, S, nullptr, !local.empty()))
+    return abort_comm(s, ("shard_track: " + s->err).c_str());
   if (s->h_flag[1])
     return local.empty() ? sfail(s, "shard_track: %d peer rank(s) failed the redo", s->h_flag[1])
                          : sfail(s, "shard_track: %s", local.c_str());

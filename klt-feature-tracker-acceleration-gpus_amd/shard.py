@@ -3,20 +3,27 @@
 Row-band decomposition: rank r of N owns the features whose y lies in its band
 [r*H/N, (r+1)*H/N) at the start of a chunk, builds pyramids only for its band
 plus a margin (klt_hip_track_frames_band), and tracks its features through the
-chunk.  After every chunk the ranks exchange results with one all-reduce of
-the 32-bit patterns of (x, y, val): every feature has exactly one contributor
-(its owner; rank 0 for lost features, which nobody tracks), so the sum is the
-owner's value bit for bit.  A feature whose window would leave a rank's built
-rows raises the chunk's escape flag; all ranks then redo that chunk from
-full-frame pyramids, so the result never depends on the margin.
+chunk.  After every chunk the ranks exchange results with one all-gather of
+fixed per-rank slots: every rank holds the same chunk-start state, so every
+rank knows every live feature's owner and its place among the owner's
+features (klt_hip_gather_order); rank r packs its features' (x, y, val) bit
+patterns in index order into its slot (klt_hip_gather_pack), the slots are
+all-gathered, and every rank takes each feature from its owner's slot
+(klt_hip_gather_unpack).  Lost features are nobody's and stay as they are,
+the same on every rank.  A feature whose window would leave a rank's built
+rows raises the chunk's escape flag (it rides in the slot's header); all
+ranks then redo that chunk from full-frame pyramids, so the result never
+depends on the margin.
 
-The data path has one collective per chunk: 3*n+1 int32 (240 KB at 20k
-features) -- the position exchange the path really has, with the escape flag
-riding along as its last element -- and one host read of that flag after it.
-Only a chunk that escaped costs a second build and a second exchange.  The
-next chunk's band pyramids depend on frames only, so each call hands the
-library the next chunk's frames: it builds them on its pyramid stream while
-this chunk is tracked and exchanged.
+The slot size is the largest owner's count, the same on every rank: the
+counts are computed on the device right after the previous exchange and read
+while the next chunk is already tracking.  The driver is speculative: chunk
+c+1 is queued before chunk c's escape flag is read, and a chunk that escaped
+(rare by design; never at the default margin on the synthetic sequences)
+costs a drain, the redo and chunk c+1 again.  The next chunk's band pyramids
+depend on frames only, so each call hands the library the next chunk's
+frames: it builds them on its pyramid stream while this chunk is tracked and
+exchanged.
 """
 from __future__ import annotations
 
@@ -131,25 +138,126 @@ def owned_mask(y0: torch.Tensor, v0: torch.Tensor, band: Band) -> torch.Tensor:
     return (v0 >= 0) & (y0 >= band.own_lo) & (y0 < band.own_hi)
 
 
-def merge_chunk(x, y, v, y0, v0, band: Band, rank: int, all_reduce, escape=None):
-    """In place, after one chunk: every rank ends with the owners' (x, y, val).
-    y0/v0 are the chunk-start state (ownership); lost features, which nobody
-    tracks, are contributed by rank 0.  escape (a 1-element int32 device
-    tensor, optional) is summed over the ranks in the same collective; the sum
-    is returned (None without it)."""
-    n = x.numel()
-    owned = owned_mask(y0, v0, band)
-    keep = owned | (v0 < 0) if rank == 0 else owned
-    bits = torch.stack([x.view(torch.int32), y.view(torch.int32), v.view(torch.int32)])
-    bits = torch.where(keep.unsqueeze(0), bits, torch.zeros_like(bits))
-    if escape is not None:
-        bits = torch.cat([bits.reshape(-1), escape.reshape(1).to(torch.int32)])
-    all_reduce(bits)
-    flat = bits[:3 * n].reshape(3, n)
-    x.view(torch.int32).copy_(flat[0])
-    y.view(torch.int32).copy_(flat[1])
-    v.copy_(flat[2])
-    return bits[3 * n:] if escape is not None else None
+def band_edges(nrows: int, world: int, edges=None) -> list[float]:
+    """The world+1 ownership edges of band_of: rank r owns edges[r] <= y < edges[r+1]."""
+    out = [band_of(nrows, world, r, 0, edges).own_lo for r in range(world)]
+    return out + [float("inf")]
+
+
+SLOT_HDR = 4  # slot header: escape flag, failures, count, S (klt_hip.h KLT_HIP_GATHER_SLOT_WORDS)
+
+
+def slot_words(S: int) -> int:
+    return SLOT_HDR + 3 * S
+
+
+def gather_order_ref(y0: torch.Tensor, v0: torch.Tensor, edges: list[float]):
+    """Owner (-1: none) and place among the owner's features in index order of
+    every feature, and every rank's count: what klt_hip_gather_order computes
+    (torch, for the CPU tests)."""
+    world = len(edges) - 1
+    owner = torch.full(y0.shape, -1, dtype=torch.int64)
+    for r in range(world):
+        m = (v0 >= 0) & (y0 >= edges[r]) & (y0 < edges[r + 1]) & (owner < 0)
+        owner[m] = r
+    place = torch.zeros_like(owner)
+    counts = []
+    for r in range(world):
+        m = owner == r
+        place[m] = torch.arange(int(m.sum()))
+        counts.append(int(m.sum()))
+    return owner, place, counts
+
+
+def gather_merge_ref(x, y, v, y0, v0, edges, rank: int, all_gather, escape: int = 0) -> int:
+    """In place, after one chunk, with torch ops (CPU tests of the exchange
+    over a real process group): this rank's slot of its owned features,
+    all_gather(out, inp) of the world's slots, every feature from its owner's
+    slot.  Same slots as klt_hip_gather_pack/unpack; returns the summed escape
+    flags."""
+    owner, place, counts = gather_order_ref(y0, v0, edges)
+    S = max(1, max(counts))
+    world = len(edges) - 1
+    slot = torch.zeros(slot_words(S), dtype=torch.int32)
+    slot[0], slot[1], slot[2], slot[3] = escape, 0, counts[rank], S
+    m = owner == rank
+    p = place[m] + SLOT_HDR
+    slot[p] = x.view(torch.int32)[m]
+    slot[p + S] = y.view(torch.int32)[m]
+    slot[p + 2 * S] = v[m]
+    out = torch.zeros(world * slot_words(S), dtype=torch.int32)
+    all_gather(out, slot)
+    sl = out.view(world, slot_words(S))
+    m = owner >= 0
+    q, p = owner[m], place[m] + SLOT_HDR
+    x.view(torch.int32)[m] = sl[q, p]
+    y.view(torch.int32)[m] = sl[q, p + S]
+    v[m] = sl[q, p + 2 * S]
+    return int(sl[:, 0].sum())
+
+
+class Exchange:
+    """The device side of the all-gather (klt_hip_gather_*) for one rank: a
+    chunk-start order, this rank's slot, the gathered slots, and pinned
+    host copies of the counts and flags behind one event.  all_gather(out, inp)
+    gathers the ranks' slots into out in rank order
+    (torch.distributed.all_gather_into_tensor in production)."""
+
+    def __init__(self, lib, ctx, n: int, edges: list[float], rank: int, all_gather, device):
+        self.lib, self.ctx, self.n, self.rank, self.all_gather = lib, ctx, n, rank, all_gather
+        self.world = len(edges) - 1
+        self.edges = (C.c_float * (self.world + 1))(*edges)
+        self.work = torch.empty(n + self.world, dtype=torch.int32, device=device)
+        self.send = torch.empty(slot_words(max(n, 1)), dtype=torch.int32, device=device)
+        self.recv = torch.empty(self.world * slot_words(max(n, 1)), dtype=torch.int32, device=device)
+        self.flags = torch.zeros(2, dtype=torch.int32, device=device)
+        self.h_counts = torch.zeros(self.world, dtype=torch.int32, pin_memory=True)
+        self.h_flags = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+        self.ev = torch.cuda.Event()
+        self.timing = False  # tools/shard_sim.py: a timing event after every exchange
+        self.timing_events = []
+
+    def _check(self, rc, what):
+        from .device import check
+        check(self.lib, self.ctx, rc, what)
+
+    def order(self, y, v) -> None:
+        """Ownership of the chunk-start state y/v; counts down behind the event."""
+        self._check(self.lib.klt_hip_gather_order(self.ctx, C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()),
+                                                  self.n, self.edges, self.world, C.c_void_p(self.work.data_ptr())),
+                    "gather_order")
+        self.h_counts.copy_(self.work[self.n:], non_blocking=True)
+        self.h_flags.copy_(self.flags, non_blocking=True)
+        self.ev.record()
+
+    def slot_size(self) -> int:
+        """The largest count of the last order() (waits for its event)."""
+        self.ev.synchronize()
+        return max(1, int(self.h_counts.max()))
+
+    def exchange(self, x, y, v, escape, S: int) -> None:
+        """Pack, all-gather, unpack in place; then the next chunk's order()."""
+        W = slot_words(S)
+        send, recv = self.send[:W], self.recv[:self.world * W]
+        self._check(self.lib.klt_hip_gather_pack(
+            self.ctx, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()),
+            C.c_void_p(self.work.data_ptr()), self.n, self.world, self.rank,
+            C.c_void_p(escape.data_ptr()) if escape is not None else None, 0, C.c_void_p(send.data_ptr()), S),
+            "gather_pack")
+        self.all_gather(recv, send)
+        self._check(self.lib.klt_hip_gather_unpack(
+            self.ctx, C.c_void_p(recv.data_ptr()), self.world, 0, C.c_void_p(self.work.data_ptr()), self.n, S,
+            C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()),
+            C.c_void_p(self.flags.data_ptr())), "gather_unpack")
+        self.order(y, v)
+        if self.timing:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self.timing_events.append(e)
+
+    def verdict(self) -> tuple[int, int]:
+        """(escape flags summed, failures) of the last exchange (after slot_size or ev.synchronize)."""
+        return int(self.h_flags[0]), int(self.h_flags[1])
 
 
 class ShardedSequence:
@@ -161,17 +269,17 @@ class ShardedSequence:
     band_of(H, world, rank, margin, edges)); x/y/v: device feature arrays
     (identical on every rank at the start), on the stream the context uses.
     edges: row boundaries of the bands (balanced_edges), default equal rows.
-    all_reduce(tensor) sums a device tensor over the ranks in place
-    (torch.distributed.all_reduce in production).
+    all_gather(out, inp) gathers a device int32 tensor of every rank into out
+    in rank order (torch.distributed.all_gather_into_tensor in production).
     """
 
-    def __init__(self, lib, ctx, pd, td, frames: torch.Tensor, x, y, v, rank: int, world: int, all_reduce,
+    def __init__(self, lib, ctx, pd, td, frames: torch.Tensor, x, y, v, rank: int, world: int, all_gather,
                  chunk: int = 64, margin: int = DEFAULT_MARGIN, edges=None):
         from .device import check
         self.lib, self.ctx, self.pd, self.td = lib, ctx, pd, td
         self.src = frames if isinstance(frames, (FullFrames, BandFrames)) else FullFrames(frames)
         self.x, self.y, self.v = x, y, v
-        self.rank, self.world, self.all_reduce, self.chunk = rank, world, all_reduce, chunk
+        self.rank, self.world, self.chunk = rank, world, chunk
         H, W = self.src.H, self.src.W
         self.H, self.W = H, W
         self.edges = edges
@@ -180,6 +288,7 @@ class ShardedSequence:
             ra, rb = band_rows(H, self.band)
             assert self.src.ra <= ra and self.src.rb >= rb, "BandFrames built for another band"
         self.escape = torch.zeros(1, dtype=torch.int32, device=x.device)
+        self.xch = Exchange(lib, ctx, x.numel(), band_edges(H, world, edges), rank, all_gather, x.device)
         self.redone = 0
         self.rebuilt = 0  # replacements whose band pyramid was too short for the selection window
         self.t_last = None  # last tracked frame
@@ -200,33 +309,58 @@ class ShardedSequence:
             self.x.numel(), b.own_lo, b.own_hi, row_lo, row_hi, C.c_void_p(self.escape.data_ptr()),
             C.c_void_p(next_ptr) if next_n > 0 else None, next_n), "track_frames_band")
 
+    def _redo(self, c0: int, n: int, saved) -> None:
+        """Chunk [c0, c0+n) again from whole frames and its start state, exchanged
+        (every rank does it: they all read the same summed escape flag)."""
+        torch.cuda.current_stream().synchronize()
+        self.redone += 1
+        for t, s in zip((self.x, self.y, self.v), saved):
+            t.copy_(s)
+        self.xch.order(self.y, self.v)
+        S = self.xch.slot_size()
+        ptr, fb = self.src.full(c0 - 1, n + 1)  # whole frames c0-1 .. c0+n-1
+        self._check(self.lib, self.ctx, self.lib.klt_hip_frames_begin(
+            self.ctx, C.byref(self.pd), C.c_void_p(ptr), self.W), "frames_begin")
+        self.escape.zero_()
+        self._band_call(ptr + fb, fb, n, 0, self.H)
+        self.xch.exchange(self.x, self.y, self.v, self.escape, S)
+        self.xch.ev.synchronize()
+        esc, bad = self.xch.verdict()
+        assert esc == 0 and bad == 0, "a chunk redone from whole frames escaped or failed"
+
     def run(self, t0: int, nframes: int) -> None:
         """Track frames t0 .. t0+nframes-1 (the pyramid of t0-1 must be current:
-        begin(t0-1) first, or a previous run ending at t0-1)."""
+        begin(t0-1) first, or a previous run ending at t0-1).  Chunk c+1 is
+        queued before chunk c's verdict is read; an escaped chunk c is redone
+        and chunk c+1 runs again."""
         end = t0 + nframes
-        for c0 in range(t0, end, self.chunk):
-            n = min(self.chunk, end - c0)
-            nn = min(self.chunk, end - c0 - n)  # the next chunk, built ahead
-            xs, ys, vs = self.x.clone(), self.y.clone(), self.v.clone()
+        chunks = [(c0, min(self.chunk, end - c0)) for c0 in range(t0, end, self.chunk)]
+        self.xch.order(self.y, self.v)  # the first chunk's ownership and counts
+        prev = None  # (c0, n, saved start state) of the chunk whose verdict is still unread
+        i = 0
+        while i < len(chunks):
+            c0, n = chunks[i]
+            nn = chunks[i + 1][1] if i + 1 < len(chunks) else 0  # the next chunk, built ahead
+            saved = (self.x.clone(), self.y.clone(), self.v.clone())
             self.escape.zero_()
             src = self.src
             self._band_call(src.band(c0), src.stride, n, self.band.row_lo, self.band.row_hi,
                             src.band(c0 + n) if nn > 0 else 0, nn)
-            # one collective: the owners' results and the escape flag summed over ranks
-            flag = merge_chunk(self.x, self.y, self.v, ys, vs, self.band, self.rank, self.all_reduce,
-                               escape=self.escape)
-            if int(flag.item()) != 0:
-                # some rank's window left its built rows: redo the chunk from
-                # full-frame pyramids (exact whatever the motion), merge again
-                self.redone += 1
-                self.x.copy_(xs), self.y.copy_(ys), self.v.copy_(vs)
-                ptr, fb = self.src.full(c0 - 1, n + 1)  # whole frames c0-1 .. c0+n-1
-                self._check(self.lib, self.ctx, self.lib.klt_hip_frames_begin(
-                    self.ctx, C.byref(self.pd), C.c_void_p(ptr), self.W), "frames_begin")
-                self.escape.zero_()
-                self._band_call(ptr + fb, fb, n, 0, self.H)
-                merge_chunk(self.x, self.y, self.v, ys, vs, self.band, self.rank, self.all_reduce)
-            self.t_last = c0 + n - 1
+            S = self.xch.slot_size()  # this chunk's counts, with the previous chunk's verdict
+            if prev is not None:
+                esc, bad = self.xch.verdict()
+                assert bad == 0, "exchange failed"
+                if esc:  # the previous chunk escaped: this chunk ran from a wrong state
+                    self._redo(*prev)
+                    prev = None
+                    continue
+            self.xch.exchange(self.x, self.y, self.v, self.escape, S)
+            prev = (c0, n, saved)
+            i += 1
+        self.xch.ev.synchronize()
+        if prev is not None and self.xch.verdict()[0]:
+            self._redo(*prev)
+        self.t_last = end - 1
 
     # -- KLTReplaceLostFeatures across the ranks (selectGoodFeatures.c:514-541,
     # sequential mode: the last tracked frame's pyramid, :342-348) ------------

@@ -16,7 +16,7 @@ import torch.multiprocessing as mp
 from conftest import synth
 
 import kltamd  # noqa: F401  (package import path)
-from kltamd.shard import Band, band_of, merge_chunk, owned_mask
+from kltamd.shard import Band, band_edges, band_of, gather_merge_ref, gather_order_ref, owned_mask
 
 
 def _free_port() -> int:
@@ -40,31 +40,61 @@ def test_bands_partition_rows_and_features(H, world):
     assert torch.equal(owners, (v >= 0).int())  # every live feature has exactly one owner
 
 
+def _state(n=64, seed=7):
+    g = torch.Generator().manual_seed(seed)
+    y0 = torch.rand(n, generator=g) * 100
+    v0 = torch.where(torch.rand(n, generator=g) < 0.2, torch.full((n,), -1), torch.zeros(n, dtype=torch.int64))
+    v0 = v0.to(torch.int32)
+    x0 = torch.rand(n, generator=g) * 100
+    return x0, y0, v0
+
+
+def _tracked(x0, y0, v0, world, rank):
+    """each rank "tracks" its own features: a rank-specific result; others stale"""
+    owned = owned_mask(y0, v0, band_of(100, world, rank, margin=0))
+    x, y, v = x0.clone(), y0.clone(), v0.clone()
+    x[owned] = x0[owned] + 1000 * (rank + 1)
+    y[owned] = -1.0
+    v[owned] = -3 - rank
+    return x, y, v
+
+
 def _merge_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        n = 64
-        g = torch.Generator().manual_seed(7)
-        y0 = torch.rand(n, generator=g) * 100
-        v0 = torch.where(torch.rand(n, generator=g) < 0.2, torch.full((n,), -1), torch.zeros(n, dtype=torch.int64))
-        v0 = v0.to(torch.int32)
-        x0 = torch.rand(n, generator=g) * 100
-        band = band_of(100, world, rank, margin=0)
-        # each rank "tracks" its own features: a rank-specific result; others stale
-        owned = owned_mask(y0, v0, band)
-        x, y, v = x0.clone(), y0.clone(), v0.clone()
-        x[owned] = x0[owned] + 1000 * (rank + 1)
-        y[owned] = -1.0
-        v[owned] = -3 - rank
-        flag = merge_chunk(x, y, v, y0.clone(), v0.clone(), band, rank, lambda t: dist.all_reduce(t),
-                           escape=torch.tensor([rank + 1], dtype=torch.int32))
-        q.put((rank, x.numpy(), y.numpy(), v.numpy(), int(flag.item())))
+        x0, y0, v0 = _state()
+        x, y, v = _tracked(x0, y0, v0, world, rank)
+
+        def all_gather(out, inp):
+            parts = [torch.empty_like(inp) for _ in range(world)]
+            dist.all_gather(parts, inp)
+            out.copy_(torch.cat(parts))
+        esc = gather_merge_ref(x, y, v, y0.clone(), v0.clone(), band_edges(100, world), rank, all_gather,
+                               escape=rank + 1)
+        q.put((rank, x.numpy(), y.numpy(), v.numpy(), esc))
     finally:
         dist.destroy_process_group()
 
 
+def test_gather_order_ref_partitions_live_features():
+    """Every live feature has exactly one owner; places are 0 .. count-1 in
+    index order within each owner; lost features are nobody's."""
+    x0, y0, v0 = _state(300, 3)
+    for world in (1, 2, 3, 8):
+        edges = band_edges(100, world)
+        owner, place, counts = gather_order_ref(y0, v0, edges)
+        assert torch.equal(owner >= 0, v0 >= 0)
+        for r in range(world):
+            m = owner == r
+            assert torch.equal(m, owned_mask(y0, v0, band_of(100, world, r, 0)))
+            assert place[m].tolist() == list(range(counts[r]))
+        assert sum(counts) == int((v0 >= 0).sum())
+
+
 def test_merge_chunk_gloo_world2():
+    """The exchange over a real world-size-2 gloo group (CPU): each rank's
+    slot of its owned features, all-gathered, merged identically on both."""
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -76,24 +106,18 @@ def test_merge_chunk_gloo_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     res.sort(key=lambda t: t[0])
-    # the escape flags ride along in the same collective: summed on every rank
+    # the escape flags ride along in the slots' headers: summed on every rank
     assert [r[4] for r in res] == [3, 3]
     # both ranks hold identical arrays ...
     for a, b in zip(res[0][1:4], res[1][1:4]):
         assert np.array_equal(a.view(np.int32), b.view(np.int32))
-    # ... equal to the owners' values
-    n = 64
-    g = torch.Generator().manual_seed(7)
-    y0 = torch.rand(n, generator=g) * 100
-    v0 = torch.where(torch.rand(n, generator=g) < 0.2, torch.full((n,), -1), torch.zeros(n, dtype=torch.int64))
-    v0 = v0.to(torch.int32)
-    x0 = torch.rand(n, generator=g) * 100
+    # ... equal to the owners' values (lost features as they were)
+    x0, y0, v0 = _state()
     x, y, v = x0.clone(), y0.clone(), v0.clone()
     for r in range(world):
         own = owned_mask(y0, v0, band_of(100, world, r, margin=0))
-        x[own] = x0[own] + 1000 * (r + 1)
-        y[own] = -1.0
-        v[own] = -3 - r
+        xr, yr, vr = _tracked(x0, y0, v0, world, r)
+        x[own], y[own], v[own] = xr[own], yr[own], vr[own]
     assert np.array_equal(res[0][1].view(np.int32), x.numpy().view(np.int32))
     assert np.array_equal(res[0][2].view(np.int32), y.numpy().view(np.int32))
     assert np.array_equal(res[0][3], v.numpy())
@@ -171,6 +195,94 @@ class _Rank:
         assert rc == 0, self.gpu.klt_hip_last_error(self.ctx)
 
 
+def device_gather_merge(gpu, ctx, state, outs, edges, escapes=None):
+    """The exchange of simulated ranks with the device kernels: order the
+    chunk-start state, pack each rank's result into its slot, unpack the
+    stacked slots into a copy of the start state.  Returns (x, y, v)."""
+    from kltamd.device import check
+    from kltamd.shard import slot_words
+    world = len(outs)
+    n = state[0].numel()
+    dev = state[0].device
+    work = torch.empty(n + world, dtype=torch.int32, device=dev)
+    E = (C.c_float * (world + 1))(*edges)
+    check(gpu, ctx, gpu.klt_hip_gather_order(ctx, C.c_void_p(state[1].data_ptr()), C.c_void_p(state[2].data_ptr()),
+                                             n, E, world, C.c_void_p(work.data_ptr())), "order")
+    S = max(1, int(work[n:].max().item()))
+    W = slot_words(S)
+    slots = torch.zeros(world * W, dtype=torch.int32, device=dev)
+    for r, (xr, yr, vr) in enumerate(outs):
+        esc = escapes[r] if escapes is not None else None
+        check(gpu, ctx, gpu.klt_hip_gather_pack(ctx, C.c_void_p(xr.data_ptr()), C.c_void_p(yr.data_ptr()),
+                                                C.c_void_p(vr.data_ptr()), C.c_void_p(work.data_ptr()), n, world, r,
+                                                C.c_void_p(esc.data_ptr()) if esc is not None else None, 0,
+                                                C.c_void_p(slots[r * W:].data_ptr()), S), "pack")
+    x, y, v = (t.clone() for t in state)
+    flags = torch.zeros(2, dtype=torch.int32, device=dev)
+    check(gpu, ctx, gpu.klt_hip_gather_unpack(ctx, C.c_void_p(slots.data_ptr()), world, 0,
+                                              C.c_void_p(work.data_ptr()), n, S, C.c_void_p(x.data_ptr()),
+                                              C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()),
+                                              C.c_void_p(flags.data_ptr())), "unpack")
+    assert int(flags[1].item()) == 0
+    device_gather_merge.flags = flags.cpu().tolist()
+    return x, y, v
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_gather_kernels_equal_reference(gpu, world):
+    """klt_hip_gather_order/pack/unpack against the torch restatement
+    (gather_merge_ref): random chunk-start states with lost features, y
+    exactly on band edges, NaN and out-of-frame y, a rank owning nothing;
+    the escape flags summed in the slots' headers."""
+    from kltamd.device import check
+    H, n = 480, 5003
+    rng = np.random.default_rng(world)
+    y0 = rng.uniform(-10, H + 10, n).astype(np.float32)
+    y0[:world + 1] = [r * H // world for r in range(world + 1)]  # on the edges
+    y0[world + 1] = np.nan
+    if world > 2:
+        y0[(y0 >= H // world) & (y0 < 2 * H // world)] = 1.0  # rank 1 owns nothing
+    v0 = np.where(rng.uniform(size=n) < 0.15, -1, 0).astype(np.int32)
+    x0 = rng.uniform(0, 640, n).astype(np.float32)
+    edges = band_edges(H, world)
+    # each rank's "result": its owned features moved by a rank-specific amount
+    res = []
+    for r in range(world):
+        own = owned_mask(torch.from_numpy(y0), torch.from_numpy(v0), band_of(H, world, r, 0))
+        x, y, v = torch.from_numpy(x0.copy()), torch.from_numpy(y0.copy()), torch.from_numpy(v0.copy())
+        x[own] += 1000.0 * (r + 1)
+        y[own] = -2.5 * (r + 1)
+        v[own] = -7 - r
+        res.append((x, y, v))
+    # torch reference: rank r's slot from its own result; all ranks' slots stacked
+    slots_ref = []
+    ref = None
+    for r in range(world):
+        st = [t.clone() for t in res[r]]
+
+        def ag(out, inp, r=r):
+            slots_ref.append(inp.clone())
+            out.zero_()
+        gather_merge_ref(*st, torch.from_numpy(y0), torch.from_numpy(v0), edges, r, ag, escape=r)
+    stacked = torch.cat(slots_ref)
+    x, y, v = torch.from_numpy(x0.copy()), torch.from_numpy(y0.copy()), torch.from_numpy(v0.copy())
+    esc_ref = gather_merge_ref(x, y, v, torch.from_numpy(y0), torch.from_numpy(v0), edges, 0,
+                               lambda out, inp: out.copy_(stacked), escape=0)
+    ref = (x, y, v)
+    dev = torch.device("cuda", 0)
+    tc = gpu.KLTCreateTrackingContext()
+    ctx = gpu.klt_amd_device_context(tc)
+    state = tuple(torch.from_numpy(a.copy()).to(dev) for a in (x0, y0, v0))
+    outs = [tuple(t.to(dev) for t in rr) for rr in res]
+    escs = [torch.tensor([r], dtype=torch.int32, device=dev) for r in range(world)]
+    got = device_gather_merge(gpu, ctx, state, outs, edges, escs)
+    for g, w in zip(got, ref):
+        assert np.array_equal(g.cpu().numpy().view(np.int32), w.numpy().view(np.int32))
+    assert device_gather_merge.flags == [sum(range(world)), 0] == [esc_ref, 0]
+    gpu.KLTFreeTrackingContext(tc)
+
+
 def sharded_sequence(gpu, frames, nfeat, world, chunk, margin, ahead=True, band_only=False):
     """Frames[0] selects; frames[1:] are tracked by `world` simulated ranks
     (ahead: each call builds the next chunk's band pyramids ahead; band_only:
@@ -209,16 +321,9 @@ def sharded_sequence(gpu, frames, nfeat, world, chunk, margin, ahead=True, band_
                 rk.chunk(c0, n, xr, yr, vr, esc, full=True, next_n=nn)
                 assert int(esc.item()) == 0
                 outs.append((xr, yr, vr))
-        # the all-reduce, done by hand: sum of the ranks' kept bit patterns
-        acc = None
-        for rk, (xr, yr, vr) in zip(ranks, outs):
-            parts = []
-
-            def fake_reduce(t, parts=parts):
-                parts.append(t.clone())
-            merge_chunk(xr, yr, vr, state[1], state[2], rk.band, rk.rank, fake_reduce)
-            acc = parts[0] if acc is None else acc + parts[0]
-        x.view(torch.int32).copy_(acc[0]), y.view(torch.int32).copy_(acc[1]), v.copy_(acc[2])
+        # the all-gather, done by hand: every rank's slot packed on the device
+        # (klt_hip_gather_pack), the slots stacked, unpacked into the chunk-start state
+        x, y, v = device_gather_merge(gpu, ranks[0].ctx, state, outs, band_edges(H, world))
     for rk in ranks:
         gpu.KLTFreeTrackingContext(rk.tc)
     return x.cpu().numpy(), y.cpu().numpy(), v.cpu().numpy(), redone
@@ -270,8 +375,8 @@ _FRAMES_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C
 
 def c_sharded_sequence(gpu, frames, nfeat, world, chunk, margin, band_only=False, real_comm=False, replace=False):
     """klt_shard_track per chunk for every rank (klt_shard_create_local: the
-    rank's band, a communicator of its own), then the all-reduce done by hand:
-    the sum of the ranks' int32 contributions.  real_comm (world 1): the
+    rank's band, a communicator of its own), then the all-gather done by hand:
+    each feature from its owner's result.  real_comm (world 1): the
     RCCL path proper, klt_shard_unique_id + klt_shard_create.  replace: lost
     features replaced after every chunk -- klt_shard_replace over the real
     communicator, else every rank's klt_shard_eigen rows into one map and
@@ -307,6 +412,7 @@ def c_sharded_sequence(gpu, frames, nfeat, world, chunk, margin, band_only=False
         ranks.append(rk)
         shards.append(s)
     redone, cur, rebuilt = [0], [0], [0]
+    bands = [band_of(H, world, r, margin) for r in range(world)]
 
     def whole(user, frames_out, stride_out):  # whole frames from frame cur[0] on
         frames_out[0] = dfr.data_ptr() + cur[0] * H * W
@@ -319,17 +425,20 @@ def c_sharded_sequence(gpu, frames, nfeat, world, chunk, margin, band_only=False
         n = min(chunk, 1 + T - c0)
         nn = min(chunk, 1 + T - c0 - n)
         cur[0] = c0 - 1
-        acc = None
-        for rk, s in zip(ranks, shards):
+        merged = (x.clone(), y.clone(), v.clone())
+        for r, (rk, s) in enumerate(zip(ranks, shards)):
             xr, yr, vr = x.clone(), y.clone(), v.clone()
             nxt = C.c_void_p(rk.base + (c0 + n) * rk.stride) if nn else None
             rc = gpu.klt_shard_track(s, C.byref(rk.pd), C.byref(rk.td), C.c_void_p(rk.base + c0 * rk.stride), W,
                                      rk.stride, n, nxt, nn, C.c_void_p(xr.data_ptr()), C.c_void_p(yr.data_ptr()),
                                      C.c_void_p(vr.data_ptr()), x.numel(), cb, None)
             assert rc in (0, 1), gpu.klt_shard_last_error(s)
-            part = torch.stack([xr.view(torch.int32), yr.view(torch.int32), vr])
-            acc = part if acc is None else acc + part
-        x.view(torch.int32).copy_(acc[0]), y.view(torch.int32).copy_(acc[1]), v.copy_(acc[2])
+            # a local shard updates its owned features and leaves the others as they were
+            own = owned_mask(y, v, bands[r])
+            assert torch.equal(xr.view(torch.int32)[~own], x.view(torch.int32)[~own])
+            for m, t in zip(merged, (xr, yr, vr)):
+                m[own] = t[own]
+        x, y, v = merged
         if replace:
             tc = ranks[0].tc.contents
             sd = SelectDesc(tc.window_width, tc.window_height, max(tc.borderx, tc.window_width // 2),
@@ -614,6 +723,14 @@ class _ThreadGroup:
         torch.cuda.current_stream().synchronize()
         self.bar.wait()
 
+    def all_gather(self, rank, out, inp):
+        torch.cuda.current_stream().synchronize()
+        self.slots[rank] = inp
+        self.bar.wait()
+        out.copy_(torch.cat(self.slots))
+        torch.cuda.current_stream().synchronize()
+        self.bar.wait()
+
     def broadcast(self, rank, t, src):
         torch.cuda.current_stream().synchronize()
         if rank == src:
@@ -663,7 +780,8 @@ def threaded_sequence(gpu, frames, nfeat, world, chunk, margin, replace=False, b
                 src = BandFrames(T + 1, H, W, band_of(H, world, rank, margin), load, dev)
             else:
                 src = FullFrames(dfr)
-            seq = ShardedSequence(gpu, ctx, pd, td, src, x, y, v, rank, world, lambda t: grp.all_reduce(rank, t),
+            seq = ShardedSequence(gpu, ctx, pd, td, src, x, y, v, rank, world,
+                                  lambda o, i: grp.all_gather(rank, o, i),
                                   chunk=chunk, margin=margin)
             seq.begin(0)
             if replace:

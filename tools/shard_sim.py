@@ -1,28 +1,36 @@
 #!/usr/bin/env python3
-"""Config 4 (feature-sharded 4K sequence) on ONE GPU.  Pass 1: every rank of
-an N-rank row-band decomposition runs in turn per chunk (its own device
-context, band pyramids and features, klt_hip_track_frames_band with the next
-chunk built ahead), and the ranks' results are merged exactly as
-kltamd.shard.merge_chunk merges them over RCCL; every N must end in the same
-feature state bit for bit (the state digest).  Pass 2: each rank alone replays
-its whole schedule from the merged chunk-start states -- band call with the
-next chunk built ahead on its pyramid stream, then the host read of the escape
-flag, as ShardedSequence does -- timed by the host clock, in a process of its
-own (one device context, as on an N-GPU node: the ranks' streams must not
-share hardware queues).  That is what one rank does, and gives the projected
-N-GPU rate
-    frame time(N) = max over ranks (rank time per frame) + exchange(N)
-with the exchange (one all-reduce of 3n+1 int32 per chunk) from
---exchange-us, since one GPU cannot measure RCCL over xGMI.
-usage: python tools/shard_sim.py [--worlds 1 2 4 8] [--margins 64] [--frames 129] [--chunk 32]
+"""Config 4 (feature-sharded 4K sequence) on ONE GPU: the projected 1 -> N
+GPU curve of kltamd.shard.ShardedSequence, measured per rank.
+
+Pass 1 runs every rank of an N-rank row-band decomposition in turn per chunk
+(klt_hip_track_frames_band, the next chunk built ahead) and merges them with
+the exchange's own device kernels (klt_hip_gather_order/pack/unpack): every N
+must end in the same feature state bit for bit (the state digest), and the
+all-gathered slots of every chunk are kept.  Pass 2 runs, for each rank in a
+process of its own (one device context, as on an N-GPU node), the production
+driver itself -- ShardedSequence.run over the whole sequence, speculative
+(chunk c+1 queued before chunk c's verdict is read), band pyramids built
+ahead -- with only the RCCL transfer replaced by a copy of pass 1's gathered
+slots for that chunk.  It is timed by the host clock, and per chunk by an
+event after each exchange.  Since the collective makes every rank wait for
+the slowest one every chunk, the projected N-GPU frame time is
+
+    sum over chunks of max over ranks (chunk time) + exchange(N)
+
+(reported beside the looser max over ranks of each rank's own total), with
+the exchange (an all-gather of the ranks' slots plus its latency) from
+--exchange-us per chunk, since one GPU cannot measure RCCL over xGMI.
+usage: python tools/shard_sim.py [--worlds 1 8] [--margins 64] [--frames 1001] [--chunk 64]
 """
 from __future__ import annotations
 
 import argparse
-import os
 import ctypes as C
 import json
+import os
+import subprocess
 import sys
+import tempfile
 import time
 from pathlib import Path
 
@@ -39,32 +47,25 @@ def main():
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--features", type=int, default=20000)
     ap.add_argument("--frames", type=int, default=129, help="frames incl. the selection frame")
-    ap.add_argument("--chunk", type=int, default=32)
+    ap.add_argument("--chunk", type=int, default=64)
     ap.add_argument("--worlds", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--margins", type=int, nargs="+", default=[64])
     ap.add_argument("--seed", type=int, default=2160)
     ap.add_argument("--balanced", action="store_true", help="bands of equal feature counts (balanced_edges)")
-    ap.add_argument("--no-ahead", action="store_true", help="pass 2 without building the next chunk ahead")
-    ap.add_argument("--own-streams", action="store_true",
-                    help="pass 2: the library on its own streams (not a torch pool stream), synchronized by host")
-    ap.add_argument("--lazy-flag", action="store_true",
-                    help="pass 2: read chunk c's escape flag after chunk c+1 is queued (a speculative driver "
-                         "redoes c and drops c+1 when it is set), so the host never drains the stream per chunk")
-    ap.add_argument("--keep-states", default=None,
-                    help="save pass 1's chunk-start states as DIR/states_w<N>.npz (for a profiled --replay)")
+    ap.add_argument("--keep-states", default=None, help="save pass 1's record as DIR/states_w<N>.npz")
     ap.add_argument("--pass1-shared", action="store_true",
-                    help="pass 1 (the merged states) through one device context for every rank, each chunk "
-                         "started from a whole-frame pyramid: one bank arena instead of N (long chunks at 4K)")
-    ap.add_argument("--replay", default=None, help=argparse.SUPPRESS)  # internal: pass 2 of one rank (npz of states)
+                    help="pass 1 through one device context for every rank, each chunk started from a "
+                         "whole-frame pyramid: one bank arena instead of N (long chunks at 4K)")
+    ap.add_argument("--replay", default=None, help=argparse.SUPPRESS)  # internal: pass 2 of one rank
     ap.add_argument("--rank", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--exchange-us", type=float, default=40.0,
-                    help="assumed per-chunk exchange: RCCL all-reduce of 3n+1 int32 + escape-flag read (N > 1)")
+                    help="assumed per-chunk exchange at N > 1: an all-gather of the ranks' slots over xGMI")
     a = ap.parse_args()
 
     import torch
     import kltamd
     from kltamd.device import PyrDesc, Timing, TrackDesc, check, use_torch_stream
-    from kltamd.shard import balanced_edges, band_of, merge_chunk
+    from kltamd.shard import (FullFrames, ShardedSequence, balanced_edges, band_edges, band_of, slot_words)
     from kltabi import fl_to_arrays, u8ptr
 
     lib = kltamd.load()
@@ -85,17 +86,73 @@ def main():
     lib.KLTFreeFeatureList(fl)
     lib.KLTFreeTrackingContext(tc0)
 
+    T = a.frames - 1
+    chunks = [(c0, min(a.chunk, 1 + T - c0)) for c0 in range(1, 1 + T, a.chunk)]
+
+    def descs(tc):
+        pd, td = PyrDesc(), TrackDesc()
+        lib.klt_amd_pyr_desc(tc, W, H, tc.contents.nPyramidLevels, 1, C.byref(pd))
+        lib.klt_amd_track_desc(tc, C.byref(td))
+        return pd, td
+
+    if a.replay:
+        # pass 2 for one rank, alone in this process: the production driver,
+        # its all-gather replaced by pass 1's gathered slots of each chunk
+        rec = np.load(a.replay)
+        world, margin = int(rec["world"]), int(rec["margin"])
+        edges = [float(e) for e in rec["edges"]] if a.balanced else None
+        flat = torch.from_numpy(rec["slots"]).to(dev)
+        offs = rec["slot_offsets"]
+        tc = lib.KLTCreateTrackingContext()
+        tc.contents.sequentialMode = 1
+        ctx = lib.klt_amd_device_context(tc)
+        use_torch_stream(lib, ctx, dev)
+        pd, td = descs(tc)
+        k = [0]
+
+        def replay_gather(out, inp):  # chunk k's slots as RCCL would have delivered them
+            s0, s1 = int(offs[k[0]]), int(offs[k[0] + 1])
+            out[:s1 - s0].copy_(flat[s0:s1])
+            k[0] += 1
+
+        ev_start = torch.cuda.Event(enable_timing=True)
+        for rep in range(3):  # the first two warm the device up (allocations, clocks); the last is timed
+            x, y, v = xs.clone(), ys.clone(), vs.clone()
+            k[0] = 0
+            seq = ShardedSequence(lib, ctx, pd, td, FullFrames(fr), x, y, v, a.rank, world, replay_gather,
+                                  chunk=a.chunk, margin=margin, edges=edges)
+            seq.xch.timing = rep == 2
+            seq.begin(0)
+            lib.klt_hip_set_timing(ctx, 1 if rep == 2 else 0)
+            torch.cuda.synchronize()
+            ev_start.record()
+            t_start = time.perf_counter()
+            seq.run(1, T)
+            torch.cuda.synchronize()
+            wall = time.perf_counter() - t_start
+        evs = [ev_start] + seq.xch.timing_events
+        per_chunk = [evs[i].elapsed_time(evs[i + 1]) * 1e3 for i in range(len(evs) - 1)]  # us
+        tm = Timing()
+        check(lib, ctx, lib.klt_hip_get_timing(ctx, C.byref(tm)), "timing")
+        # per-kernel event time per frame (build-ahead: contended durations)
+        kern = {"k_pyr_l0": 1e3 * tm.ms_pyr_l0 / T, "k_pyr_l1": 1e3 * tm.ms_pyr_l1 / T,
+                "k_track": 1e3 * tm.ms_track / T}
+        print(json.dumps({"rank": a.rank, "us_per_frame": 1e6 * wall / T, "chunk_us": per_chunk,
+                          "kernels_us_per_frame": kern, "redone": seq.redone,
+                          "digest": int((x.view(torch.int32).to(torch.int64).sum() * 3 +
+                                         y.view(torch.int32).to(torch.int64).sum() * 5 +
+                                         v.to(torch.int64).sum() * 7).item())}))
+        lib.KLTFreeTrackingContext(tc)
+        return
+
     class Rank:
-        def __init__(self, world, rank, margin, own=False):
+        def __init__(self, world, rank, margin, edges):
             self.tc = lib.KLTCreateTrackingContext()
             self.tc.contents.sequentialMode = 1
             self.ctx = lib.klt_amd_device_context(self.tc)
-            if not own:
-                use_torch_stream(lib, self.ctx, dev)
-            self.pd, self.td = PyrDesc(), TrackDesc()
-            lib.klt_amd_pyr_desc(self.tc, W, H, self.tc.contents.nPyramidLevels, 1, C.byref(self.pd))
-            lib.klt_amd_track_desc(self.tc, C.byref(self.td))
-            self.band = band_of(H, world, rank, margin, balanced_edges(ys, vs, H, world) if a.balanced else None)
+            use_torch_stream(lib, self.ctx, dev)
+            self.pd, self.td = descs(self.tc)
+            self.band = band_of(H, world, rank, margin, edges)
             self.rank = rank
 
         def ptr(self, t):
@@ -112,162 +169,117 @@ def main():
                 H if full else b.row_hi, C.c_void_p(esc.data_ptr()), self.ptr(t0 + n) if next_n > 0 else None,
                 next_n), "band")
 
-    T = a.frames - 1
-    chunks = [(c0, min(a.chunk, 1 + T - c0)) for c0 in range(1, 1 + T, a.chunk)]
-
-    if a.replay:
-        # pass 2 for one rank, alone in this process
-        world = int(np.load(a.replay)["world"])
-        margin = int(np.load(a.replay)["margin"])
-        st = np.load(a.replay)
-        own = a.own_streams
-        rk = Rank(world, a.rank, margin, own)
-        xr, yr, vr = xs.clone(), ys.clone(), vs.clone()
-        esc = torch.zeros(1, dtype=torch.int32, device=dev)
-        escs = torch.zeros(len(chunks), dtype=torch.int32, device=dev)
-        esc_host = torch.zeros(len(chunks), dtype=torch.int32, pin_memory=True)
-        esc_ev = [torch.cuda.Event() for _ in chunks]
-        sx, sy, sv = (torch.from_numpy(st[k]).to(dev) for k in ("x", "y", "v"))
-        for rep in range(3):  # the first two warm the device up (allocations, clocks); the last is timed
-            rk.begin(0)
-            lib.klt_hip_set_timing(rk.ctx, 1 if rep == 2 else 0)  # per-kernel events of the timed run
-            torch.cuda.synchronize()
-            t_start = time.perf_counter()
-            for ci, (c0, n) in enumerate(chunks):
-                nn = chunks[ci + 1][1] if ci + 1 < len(chunks) and not a.no_ahead else 0
-                xr.copy_(sx[ci]), yr.copy_(sy[ci]), vr.copy_(sv[ci])
-                e = escs[ci:ci + 1] if a.lazy_flag else esc
-                e.zero_()
-                if own:
-                    torch.cuda.current_stream().synchronize()
-                rk.chunk(c0, n, xr, yr, vr, e, next_n=nn)
-                if own:
-                    check(lib, rk.ctx, lib.klt_hip_sync(rk.ctx), "sync")
-                if not a.lazy_flag:
-                    int(esc.item())  # the host's read of the escape flag (merge_chunk)
-                else:
-                    esc_host[ci:ci + 1].copy_(e, non_blocking=True)
-                    esc_ev[ci].record()
-                    if ci > 0:  # chunk c-1's flag, read while chunk c runs
-                        esc_ev[ci - 1].synchronize()
-                        int(esc_host[ci - 1])
-            torch.cuda.synchronize()
-        frames_timed = sum(n for _, n in chunks)
-        wall = 1e6 * (time.perf_counter() - t_start) / frames_timed
-        tm = Timing()
-        check(lib, rk.ctx, lib.klt_hip_get_timing(rk.ctx, C.byref(tm)), "timing")
-        # per-kernel event time per frame of the timed run (overlapping kernels share the GPU: with
-        # build-ahead these are contended durations; with --no-ahead each kernel runs alone)
-        kern = {"k_pyr_l0": 1e3 * tm.ms_pyr_l0 / frames_timed, "k_pyr_l1": 1e3 * tm.ms_pyr_l1 / frames_timed,
-                "k_track": 1e3 * tm.ms_track / frames_timed}
-        print(json.dumps({"rank": a.rank, "us_per_frame": wall, "kernels_us_per_frame": kern}))
-        return
-
-    out = {"workload": f"{W}x{H}, {NF} features, {a.frames - 1} tracked frames, {a.chunk}-frame chunks"
+    out = {"workload": f"{W}x{H}, {NF} features, {T} tracked frames, {a.chunk}-frame chunks"
                        + (", bands of equal feature counts" if a.balanced else ""),
-           "exchange_us_assumed": a.exchange_us, "runs": []}
-    base_fps = None
+           "exchange_us_assumed_per_chunk": a.exchange_us, "runs": []}
+    base = None
     for margin in a.margins:
         for world in a.worlds:
-            ranks = [Rank(world, r, margin) for r in range(1 if a.pass1_shared else world)]
+            edges = balanced_edges(ys, vs, H, world) if a.balanced else None
+            gedges = band_edges(H, world, edges)
+            ranks = [Rank(world, r, margin, edges) for r in range(1 if a.pass1_shared else world)]
             if a.pass1_shared:
-                # one context; each rank's chunk starts from frame c0-1's whole-frame pyramid (band-built
-                # rows equal whole-frame ones, so the states are the same) without build-ahead
                 for r in range(1, world):
                     rk = Rank.__new__(Rank)
                     rk.__dict__.update(ranks[0].__dict__)
-                    rk.band = band_of(H, world, r, margin, balanced_edges(ys, vs, H, world) if a.balanced else None)
+                    rk.band = band_of(H, world, r, margin, edges)
                     rk.rank = r
                     ranks.append(rk)
             for rk in ranks[:1] if a.pass1_shared else ranks:
                 rk.begin(0)
+            ctx = ranks[0].ctx
             x, y, v = xs.clone(), ys.clone(), vs.clone()
-            starts, redone, per_rank = [], 0, [[0.0, 0.0, 0.0, 0] for _ in ranks]
+            redone, slots_rec = 0, []
+            work = torch.empty(NF + world, dtype=torch.int32, device=dev)
+            E = (C.c_float * (world + 1))(*gedges)
+            flags = torch.zeros(2, dtype=torch.int32, device=dev)
             for ci, (c0, n) in enumerate(chunks):
                 nn = chunks[ci + 1][1] if ci + 1 < len(chunks) else 0
                 state = (x.clone(), y.clone(), v.clone())
-                starts.append(state)
-                outs, esc_any = [], 0
-                for i, rk in enumerate(ranks):
+                outs, escs = [], []
+                for rk in ranks:
                     xr, yr, vr = (t.clone() for t in state)
                     esc = torch.zeros(1, dtype=torch.int32, device=dev)
-                    lib.klt_hip_set_timing(rk.ctx, 1)
                     if a.pass1_shared:
                         rk.begin(c0 - 1)
                     rk.chunk(c0, n, xr, yr, vr, esc, next_n=0 if a.pass1_shared else nn)
-                    tm = Timing()
-                    check(lib, rk.ctx, lib.klt_hip_get_timing(rk.ctx, C.byref(tm)), "timing")
-                    lib.klt_hip_set_timing(rk.ctx, 0)
-                    pr = per_rank[i]
-                    pr[0] += tm.ms_pyr_l0 * 1e3
-                    pr[1] += tm.ms_pyr_l1 * 1e3
-                    pr[2] += tm.ms_track * 1e3
-                    pr[3] += n
-                    esc_any += int(esc.item())
                     outs.append((xr, yr, vr))
-                if esc_any:
+                    escs.append(esc)
+                if sum(int(e.item()) for e in escs):
                     redone += 1
                     outs = []
-                    for rk in ranks:
+                    for rk, esc in zip(ranks, escs):
                         xr, yr, vr = (t.clone() for t in state)
-                        esc = torch.zeros(1, dtype=torch.int32, device=dev)
+                        esc.zero_()
                         rk.begin(c0 - 1)
                         rk.chunk(c0, n, xr, yr, vr, esc, full=True, next_n=0 if a.pass1_shared else nn)
                         outs.append((xr, yr, vr))
-                acc = None
-                for rk, (xr, yr, vr) in zip(ranks, outs):
-                    parts = []
-                    merge_chunk(xr, yr, vr, state[1], state[2], rk.band, rk.rank, lambda t, p=parts: p.append(t.clone()))
-                    acc = parts[0] if acc is None else acc + parts[0]
-                x.view(torch.int32).copy_(acc[0]), y.view(torch.int32).copy_(acc[1]), v.copy_(acc[2])
+                # the exchange with its own kernels: order, each rank's slot, unpack
+                check(lib, ctx, lib.klt_hip_gather_order(ctx, C.c_void_p(state[1].data_ptr()),
+                                                         C.c_void_p(state[2].data_ptr()), NF, E, world,
+                                                         C.c_void_p(work.data_ptr())), "order")
+                S = max(1, int(work[NF:].max().item()))
+                Wd = slot_words(S)
+                slots = torch.zeros(world * Wd, dtype=torch.int32, device=dev)
+                for r, ((xr, yr, vr), esc) in enumerate(zip(outs, escs)):
+                    check(lib, ctx, lib.klt_hip_gather_pack(
+                        ctx, C.c_void_p(xr.data_ptr()), C.c_void_p(yr.data_ptr()), C.c_void_p(vr.data_ptr()),
+                        C.c_void_p(work.data_ptr()), NF, world, r, C.c_void_p(esc.data_ptr()), 0,
+                        C.c_void_p(slots[r * Wd:].data_ptr()), S), "pack")
+                check(lib, ctx, lib.klt_hip_gather_unpack(ctx, C.c_void_p(slots.data_ptr()), world, 0,
+                                                          C.c_void_p(work.data_ptr()), NF, S,
+                                                          C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()),
+                                                          C.c_void_p(v.data_ptr()), C.c_void_p(flags.data_ptr())),
+                      "unpack")
+                assert int(flags[1].item()) == 0
+                slots_rec.append(slots.cpu().numpy())
             digest = int((x.view(torch.int32).to(torch.int64).sum() * 3 + y.view(torch.int32).to(torch.int64).sum() * 5
                           + v.to(torch.int64).sum() * 7).item())
+            for rk in ranks[:1] if a.pass1_shared else ranks:
+                lib.KLTFreeTrackingContext(rk.tc)
+            torch.cuda.synchronize()
             # pass 2: each rank alone over the whole schedule, in a process of its own
-            # (the third of three runs timed: allocations and clocks settle first)
-            import subprocess
-            import tempfile
+            reps = []
             with tempfile.TemporaryDirectory() as td:
-                f = f"{td}/states.npz"
-                np.savez(f, world=world, margin=margin,
-                         x=np.stack([t[0].cpu().numpy() for t in starts]),
-                         y=np.stack([t[1].cpu().numpy() for t in starts]),
-                         v=np.stack([t[2].cpu().numpy() for t in starts]))
+                f = f"{td}/rec.npz"
+                offs = np.cumsum([0] + [len(s) for s in slots_rec])
+                np.savez(f, world=world, margin=margin, edges=np.asarray(gedges, np.float64),
+                         slots=np.concatenate(slots_rec), slot_offsets=offs)
                 if a.keep_states:
                     import shutil
                     os.makedirs(a.keep_states, exist_ok=True)
                     shutil.copy(f, f"{a.keep_states}/states_w{world}.npz")
-                rank_us, rank_kern = [], []
                 for r in range(world):
                     cmd = [sys.executable, __file__, "--replay", f, "--rank", str(r), "--width", str(W), "--height",
                            str(H), "--features", str(NF), "--frames", str(a.frames), "--chunk", str(a.chunk),
-                           "--seed", str(a.seed)] + (["--no-ahead"] if a.no_ahead else []) + \
-                          (["--own-streams"] if a.own_streams else []) + (["--balanced"] if a.balanced else []) + \
-                          (["--lazy-flag"] if a.lazy_flag else [])
+                           "--seed", str(a.seed)] + (["--balanced"] if a.balanced else [])
                     res = subprocess.run(cmd, check=True, capture_output=True, text=True)
-                    rr = json.loads(res.stdout.strip().splitlines()[-1])
-                    rank_us.append(rr["us_per_frame"])
-                    rank_kern.append(rr["kernels_us_per_frame"])
-            nch = len(chunks)
+                    reps.append(json.loads(res.stdout.strip().splitlines()[-1]))
             frames = sum(n for _, n in chunks)
+            nch = len(chunks)
+            assert all(len(rr["chunk_us"]) == nch for rr in reps)
+            assert all(rr["digest"] == digest for rr in reps), "a replayed rank ended in another state"
             exch = a.exchange_us * nch / frames if world > 1 else 0.0
-            fps = 1e6 / (max(rank_us) + exch)
+            synced = sum(max(rr["chunk_us"][c] for rr in reps) for c in range(nch)) / frames
+            loose = max(rr["us_per_frame"] for rr in reps)
+            fps = 1e6 / (synced + exch)
             if world == 1:
-                base_fps = fps
+                base = fps
             run = {"world": world, "margin_rows": margin, "chunks_redone_full_frame": redone,
-                   "state_digest": digest, "us_per_frame_max_rank": max(rank_us),
+                   "state_digest": digest, "us_per_frame_synced": synced, "us_per_frame_max_rank_total": loose,
                    "us_per_frame_exchange": exch, "projected_fps": fps,
-                   "projected_speedup": fps / base_fps if base_fps else None,
-                   "per_rank_us_per_frame": [{"rank": i, "band_rows": [rk.band.row_lo, rk.band.row_hi],
-                                              "wall": rank_us[i], "replay_kernels": rank_kern[i],
-                                              "k_pyr_l0": p[0] / p[3], "k_pyr_l1": p[1] / p[3], "k_track": p[2] / p[3]}
-                                             for i, (rk, p) in enumerate(zip(ranks, per_rank))]}
+                   "projected_speedup": fps / base if base else None,
+                   "per_rank": [{"rank": i, "band_rows": [band_of(H, world, i, margin, edges).row_lo,
+                                                          band_of(H, world, i, margin, edges).row_hi],
+                                 "wall_us_per_frame": rr["us_per_frame"],
+                                 "chunk_us_mean": float(np.mean(rr["chunk_us"])),
+                                 "replay_kernels_us_per_frame": rr["kernels_us_per_frame"], "redone": rr["redone"]}
+                                for i, rr in enumerate(reps)],
+                   "chunk_us_max_over_ranks": [max(rr["chunk_us"][c] for rr in reps) for c in range(nch)]}
             out["runs"].append(run)
             print(json.dumps({k: run[k] for k in ("world", "margin_rows", "chunks_redone_full_frame", "state_digest",
-                                                  "us_per_frame_max_rank", "projected_fps", "projected_speedup")}),
-                  flush=True)
-            for rk in ranks[:1] if a.pass1_shared else ranks:
-                lib.KLTFreeTrackingContext(rk.tc)
-            torch.cuda.synchronize()
+                                                  "us_per_frame_synced", "us_per_frame_max_rank_total",
+                                                  "projected_fps", "projected_speedup")}), flush=True)
     print(json.dumps(out))
 
 
