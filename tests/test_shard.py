@@ -273,6 +273,8 @@ def test_gather_kernels_equal_reference(gpu, world):
     dev = torch.device("cuda", 0)
     tc = gpu.KLTCreateTrackingContext()
     ctx = gpu.klt_amd_device_context(tc)
+    from kltamd.device import use_torch_stream
+    use_torch_stream(gpu, ctx, dev)  # the kernels and torch's allocations and reads on one stream
     state = tuple(torch.from_numpy(a.copy()).to(dev) for a in (x0, y0, v0))
     outs = [tuple(t.to(dev) for t in rr) for rr in res]
     escs = [torch.tensor([r], dtype=torch.int32, device=dev) for r in range(world)]
