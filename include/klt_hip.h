@@ -388,12 +388,18 @@ int klt_hip_select_map(klt_hip_ctx *ctx, int ncols, int nrows, const klt_hip_sel
    one; nothing is unpacked then).  All three queue on the context's stream. */
 #define KLT_HIP_GATHER_MAX_RANKS 64
 #define KLT_HIP_GATHER_SLOT_WORDS(S) (4 + 3 * (long)(S))
-int klt_hip_gather_order(klt_hip_ctx *ctx, const float *y0, const int *v0, int n, const float *edges, int world,
-                         int *work);
+/* gather_order options, each may be NULL: save (device int[3n]) receives a
+   copy of x0 | y0 | v0 bit patterns (the chunk-start state a redo restarts
+   from; needs x0) and *escape (device int) is zeroed, in the same launch;
+   host_counts (pinned host int[world]) and gather_unpack's host_flags (pinned
+   host int[2]) receive the counts / flags from the kernels themselves, to be
+   read once an event recorded after the launch has completed */
+int klt_hip_gather_order(klt_hip_ctx *ctx, const float *x0, const float *y0, const int *v0, int n, const float *edges,
+                         int world, int *work, int *save, int *escape, int *host_counts);
 int klt_hip_gather_pack(klt_hip_ctx *ctx, const float *x, const float *y, const int *val, const int *work, int n,
                         int world, int rank, const int *escape, int nfail, int *slot, int S);
 int klt_hip_gather_unpack(klt_hip_ctx *ctx, const int *slots, int nslots, int first_rank, const int *work, int n,
-                          int S, float *x, float *y, int *val, int *flags);
+                          int S, float *x, float *y, int *val, int *flags, int *host_flags);
 
 /* synthetic frames t0..t0+n-1 (include/klt_synth.h) into device memory */
 int klt_hip_synth_frames(klt_hip_ctx *ctx, unsigned long long seed, int t0, int n, int ncols,

@@ -129,18 +129,31 @@ struct GatherEdges {
   int world;
 };
 
-__global__ __launch_bounds__(kGatherThreads) void k_gather_order(const float *__restrict__ y0,
+// save (optional): x0/y0/v0 also copied to save[0..3n) (the redo's start
+// state) and *escape zeroed -- the chunk-start work of one launch; host_counts
+// (optional, pinned host memory): the counts written there too, so the driver
+// reads them behind an event with no copy-engine hand-off on the stream
+__global__ __launch_bounds__(kGatherThreads) void k_gather_order(const float *__restrict__ x0,
+                                                                 const float *__restrict__ y0,
                                                                  const int *__restrict__ v0, int n, GatherEdges E,
-                                                                 int *__restrict__ code, int *__restrict__ counts) {
+                                                                 int *__restrict__ code, int *__restrict__ counts,
+                                                                 int *__restrict__ save, int *__restrict__ escape,
+                                                                 int *__restrict__ host_counts) {
   constexpr int NW = kGatherThreads / 64;
   __shared__ int wc[NW][KLT_HIP_GATHER_MAX_RANKS];
   __shared__ int base[KLT_HIP_GATHER_MAX_RANKS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid < E.world) base[tid] = 0;
+  if (tid == 0 && escape) *escape = 0;
   __syncthreads();
   for (int r0 = 0; r0 < n; r0 += kGatherThreads) {  // rounds of 1024 features, in index order
     const int i = r0 + tid;
     int q = -1;
+    if (i < n && save) {
+      save[i] = __float_as_int(x0[i]);
+      save[n + i] = __float_as_int(y0[i]);
+      save[2 * n + i] = v0[i];
+    }
     if (i < n && v0[i] >= 0) {
       const float y = y0[i];
       for (int r = 0; r < E.world; ++r)
@@ -171,7 +184,10 @@ __global__ __launch_bounds__(kGatherThreads) void k_gather_order(const float *__
     }
     __syncthreads();
   }
-  if (tid < E.world) counts[tid] = base[tid];
+  if (tid < E.world) {
+    counts[tid] = base[tid];
+    if (host_counts) host_counts[tid] = base[tid];
+  }
 }
 
 __global__ void k_gather_pack(const float *__restrict__ x, const float *__restrict__ y, const int *__restrict__ v,
@@ -202,7 +218,7 @@ __global__ void k_gather_pack(const float *__restrict__ x, const float *__restri
 // short for its count is one); nothing is unpacked when flags[1] != 0.
 __global__ void k_gather_unpack(const int *__restrict__ slots, int nslots, int r0, const int *__restrict__ code,
                                 int n, int S, float *__restrict__ x, float *__restrict__ y, int *__restrict__ v,
-                                int *__restrict__ flags) {
+                                int *__restrict__ flags, int *__restrict__ host_flags) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const long words = kGatherHdr + 3L * S;
   int esc = 0, bad = 0;
@@ -214,6 +230,10 @@ __global__ void k_gather_unpack(const int *__restrict__ slots, int nslots, int r
   if (i == 0) {
     flags[0] = esc;
     flags[1] = bad;
+    if (host_flags) {
+      host_flags[0] = esc;
+      host_flags[1] = bad;
+    }
   }
   if (i >= n || bad) return;
   const int c = code[i];
@@ -257,9 +277,9 @@ int fail_count(const klt_shard *s, int failed) {
 // the ownership of the chunk-start state (d_y0, d_v0) and every rank's count,
 // downloaded behind an event (read after the band call is queued)
 int order_counts(klt_shard *s, hipStream_t st, int n) {
-  if (klt_hip_gather_order(s->ctx, s->d_y0, s->d_v0, n, s->edges.data(), s->world, s->d_work))
+  if (klt_hip_gather_order(s->ctx, nullptr, s->d_y0, s->d_v0, n, s->edges.data(), s->world, s->d_work, nullptr,
+                           nullptr, s->h_flag + 2))
     return sfail(s, "%s", klt_hip_last_error(s->ctx));
-  SHIP(s, hipMemcpyAsync(s->h_flag + 2, s->d_work + n, s->world * sizeof(int), hipMemcpyDeviceToHost, st));
   SHIP(s, hipEventRecord(s->ev_counts, st));
   return 0;
 }
@@ -291,9 +311,8 @@ int exchange(klt_shard *s, hipStream_t st, float *x, float *y, int *v, int n, in
   SNCCL(s, ncclAllGather(s->d_send, s->d_recv, (size_t)words, ncclInt32, s->comm, st));
   int *flags = s->d_esc + 1;
   if (klt_hip_gather_unpack(s->ctx, s->d_recv, s->cranks, s->cranks == 1 ? s->rank : 0, s->d_work, n, S, x, y, v,
-                            flags))
+                            flags, s->h_flag))
     return sfail(s, "%s", klt_hip_last_error(s->ctx));
-  SHIP(s, hipMemcpyAsync(s->h_flag, flags, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
   SHIP(s, hipStreamSynchronize(st));
   return 0;
 }
@@ -312,18 +331,18 @@ int agree(klt_shard *s, hipStream_t st, int failed, int *failed_ranks) {
 
 }  // namespace
 
-KLT_API int klt_hip_gather_order(klt_hip_ctx *ctx, const float *y0, const int *v0, int n, const float *edges,
-                                 int world, int *work) {
+KLT_API int klt_hip_gather_order(klt_hip_ctx *ctx, const float *x0, const float *y0, const int *v0, int n,
+                                 const float *edges, int world, int *work, int *save, int *escape, int *host_counts) {
   if (!ctx || world < 1 || world > KLT_HIP_GATHER_MAX_RANKS || n < 0 || n >= (1 << 24) || !edges || !work ||
-      (n > 0 && (!y0 || !v0)))
+      (n > 0 && (!y0 || !v0)) || (save && n > 0 && !x0))
     return ctx ? kltdev::ctx_fail(ctx, "gather_order: bad argument") : -1;
   DeviceGuard guard;
   if (hipSetDevice(klt_hip_ctx_device(ctx)) != hipSuccess) return kltdev::ctx_fail(ctx, "gather_order: device");
   GatherEdges E{};
   for (int r = 0; r <= world; ++r) E.e[r] = edges[r];
   E.world = world;
-  hipLaunchKernelGGL(k_gather_order, dim3(1), dim3(kGatherThreads), 0, (hipStream_t)klt_hip_get_stream(ctx), y0, v0,
-                     n, E, work, work + n);
+  hipLaunchKernelGGL(k_gather_order, dim3(1), dim3(kGatherThreads), 0, (hipStream_t)klt_hip_get_stream(ctx), x0, y0,
+                     v0, n, E, work, work + n, save, escape, host_counts);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : kltdev::ctx_fail(ctx, "gather_order: %s", hipGetErrorString(e));
 }
@@ -343,7 +362,7 @@ KLT_API int klt_hip_gather_pack(klt_hip_ctx *ctx, const float *x, const float *y
 }
 
 KLT_API int klt_hip_gather_unpack(klt_hip_ctx *ctx, const int *slots, int nslots, int first_rank, const int *work,
-                                  int n, int S, float *x, float *y, int *val, int *flags) {
+                                  int n, int S, float *x, float *y, int *val, int *flags, int *host_flags) {
   if (!ctx || nslots < 1 || first_rank < 0 || n < 0 || S < 0 || !slots || !work || !flags ||
       (n > 0 && (!x || !y || !val)))
     return ctx ? kltdev::ctx_fail(ctx, "gather_unpack: bad argument") : -1;
@@ -351,7 +370,7 @@ KLT_API int klt_hip_gather_unpack(klt_hip_ctx *ctx, const int *slots, int nslots
   if (hipSetDevice(klt_hip_ctx_device(ctx)) != hipSuccess) return kltdev::ctx_fail(ctx, "gather_unpack: device");
   const int nb = n > 0 ? (n + 255) / 256 : 1;
   hipLaunchKernelGGL(k_gather_unpack, dim3(nb), dim3(256), 0, (hipStream_t)klt_hip_get_stream(ctx), slots, nslots,
-                     first_rank, work, n, S, x, y, val, flags);
+                     first_rank, work, n, S, x, y, val, flags, host_flags);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : kltdev::ctx_fail(ctx, "gather_unpack: %s", hipGetErrorString(e));
 }

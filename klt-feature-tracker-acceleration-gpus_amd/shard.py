@@ -197,11 +197,13 @@ def gather_merge_ref(x, y, v, y0, v0, edges, rank: int, all_gather, escape: int 
 
 
 class Exchange:
-    """The device side of the all-gather (klt_hip_gather_*) for one rank: a
-    chunk-start order, this rank's slot, the gathered slots, and pinned
-    host copies of the counts and flags behind one event.  all_gather(out, inp)
-    gathers the ranks' slots into out in rank order
-    (torch.distributed.all_gather_into_tensor in production)."""
+    """The device side of the all-gather (klt_hip_gather_*) for one rank: the
+    chunk-start order (which also saves the start state, alternating between
+    two buffers, and zeroes the escape flag), this rank's slot, the gathered
+    slots, and pinned host words the kernels write the counts and flags into,
+    behind one event -- no copy-engine transfer on the stream between two
+    chunks.  all_gather(out, inp) gathers the ranks' slots into out in rank
+    order (torch.distributed.all_gather_into_tensor in production)."""
 
     def __init__(self, lib, ctx, n: int, edges: list[float], rank: int, all_gather, device):
         self.lib, self.ctx, self.n, self.rank, self.all_gather = lib, ctx, n, rank, all_gather
@@ -211,6 +213,8 @@ class Exchange:
         self.send = torch.empty(slot_words(max(n, 1)), dtype=torch.int32, device=device)
         self.recv = torch.empty(self.world * slot_words(max(n, 1)), dtype=torch.int32, device=device)
         self.flags = torch.zeros(2, dtype=torch.int32, device=device)
+        self.save = torch.empty((2, 3, max(n, 1)), dtype=torch.int32, device=device)
+        self.k = 0  # the save buffer the next order() fills
         self.h_counts = torch.zeros(self.world, dtype=torch.int32, pin_memory=True)
         self.h_flags = torch.zeros(2, dtype=torch.int32, pin_memory=True)
         self.ev = torch.cuda.Event()
@@ -221,39 +225,50 @@ class Exchange:
         from .device import check
         check(self.lib, self.ctx, rc, what)
 
-    def order(self, y, v) -> None:
-        """Ownership of the chunk-start state y/v; counts down behind the event."""
-        self._check(self.lib.klt_hip_gather_order(self.ctx, C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()),
-                                                  self.n, self.edges, self.world, C.c_void_p(self.work.data_ptr())),
-                    "gather_order")
-        self.h_counts.copy_(self.work[self.n:], non_blocking=True)
-        self.h_flags.copy_(self.flags, non_blocking=True)
+    def order(self, x, y, v, escape) -> int:
+        """Ownership of the chunk-start state x/y/v, that state saved, the escape
+        flag zeroed; the counts land in h_counts behind the event.  Returns the
+        save buffer's index."""
+        k = self.k
+        self.k ^= 1
+        self._check(self.lib.klt_hip_gather_order(
+            self.ctx, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()), self.n,
+            self.edges, self.world, C.c_void_p(self.work.data_ptr()), C.c_void_p(self.save[k].data_ptr()),
+            C.c_void_p(escape.data_ptr()), C.c_void_p(self.h_counts.data_ptr())), "gather_order")
         self.ev.record()
+        return k
+
+    def restore(self, k: int, x, y, v) -> None:
+        """The state save buffer k holds, back into x/y/v."""
+        x.view(torch.int32).copy_(self.save[k, 0, :self.n])
+        y.view(torch.int32).copy_(self.save[k, 1, :self.n])
+        v.copy_(self.save[k, 2, :self.n])
 
     def slot_size(self) -> int:
         """The largest count of the last order() (waits for its event)."""
         self.ev.synchronize()
         return max(1, int(self.h_counts.max()))
 
-    def exchange(self, x, y, v, escape, S: int) -> None:
-        """Pack, all-gather, unpack in place; then the next chunk's order()."""
+    def exchange(self, x, y, v, escape, S: int) -> int:
+        """Pack, all-gather, unpack in place; then the next chunk's order()
+        (whose save index is returned)."""
         W = slot_words(S)
         send, recv = self.send[:W], self.recv[:self.world * W]
         self._check(self.lib.klt_hip_gather_pack(
             self.ctx, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()),
-            C.c_void_p(self.work.data_ptr()), self.n, self.world, self.rank,
-            C.c_void_p(escape.data_ptr()) if escape is not None else None, 0, C.c_void_p(send.data_ptr()), S),
-            "gather_pack")
+            C.c_void_p(self.work.data_ptr()), self.n, self.world, self.rank, C.c_void_p(escape.data_ptr()), 0,
+            C.c_void_p(send.data_ptr()), S), "gather_pack")
         self.all_gather(recv, send)
         self._check(self.lib.klt_hip_gather_unpack(
             self.ctx, C.c_void_p(recv.data_ptr()), self.world, 0, C.c_void_p(self.work.data_ptr()), self.n, S,
             C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()),
-            C.c_void_p(self.flags.data_ptr())), "gather_unpack")
-        self.order(y, v)
+            C.c_void_p(self.flags.data_ptr()), C.c_void_p(self.h_flags.data_ptr())), "gather_unpack")
+        k = self.order(x, y, v, escape)
         if self.timing:
             e = torch.cuda.Event(enable_timing=True)
             e.record()
             self.timing_events.append(e)
+        return k
 
     def verdict(self) -> tuple[int, int]:
         """(escape flags summed, failures) of the last exchange (after slot_size or ev.synchronize)."""
@@ -309,19 +324,18 @@ class ShardedSequence:
             self.x.numel(), b.own_lo, b.own_hi, row_lo, row_hi, C.c_void_p(self.escape.data_ptr()),
             C.c_void_p(next_ptr) if next_n > 0 else None, next_n), "track_frames_band")
 
-    def _redo(self, c0: int, n: int, saved) -> None:
-        """Chunk [c0, c0+n) again from whole frames and its start state, exchanged
-        (every rank does it: they all read the same summed escape flag)."""
+    def _redo(self, c0: int, n: int, k: int) -> None:
+        """Chunk [c0, c0+n) again from whole frames and its start state (save
+        buffer k), exchanged (every rank does it: they all read the same summed
+        escape flag)."""
         torch.cuda.current_stream().synchronize()
         self.redone += 1
-        for t, s in zip((self.x, self.y, self.v), saved):
-            t.copy_(s)
-        self.xch.order(self.y, self.v)
+        self.xch.restore(k, self.x, self.y, self.v)
+        self.xch.order(self.x, self.y, self.v, self.escape)
         S = self.xch.slot_size()
         ptr, fb = self.src.full(c0 - 1, n + 1)  # whole frames c0-1 .. c0+n-1
         self._check(self.lib, self.ctx, self.lib.klt_hip_frames_begin(
             self.ctx, C.byref(self.pd), C.c_void_p(ptr), self.W), "frames_begin")
-        self.escape.zero_()
         self._band_call(ptr + fb, fb, n, 0, self.H)
         self.xch.exchange(self.x, self.y, self.v, self.escape, S)
         self.xch.ev.synchronize()
@@ -335,14 +349,12 @@ class ShardedSequence:
         and chunk c+1 runs again."""
         end = t0 + nframes
         chunks = [(c0, min(self.chunk, end - c0)) for c0 in range(t0, end, self.chunk)]
-        self.xch.order(self.y, self.v)  # the first chunk's ownership and counts
-        prev = None  # (c0, n, saved start state) of the chunk whose verdict is still unread
+        k = self.xch.order(self.x, self.y, self.v, self.escape)  # the first chunk's ownership, start state, counts
+        prev = None  # (c0, n, save index) of the chunk whose verdict is still unread
         i = 0
         while i < len(chunks):
             c0, n = chunks[i]
             nn = chunks[i + 1][1] if i + 1 < len(chunks) else 0  # the next chunk, built ahead
-            saved = (self.x.clone(), self.y.clone(), self.v.clone())
-            self.escape.zero_()
             src = self.src
             self._band_call(src.band(c0), src.stride, n, self.band.row_lo, self.band.row_hi,
                             src.band(c0 + n) if nn > 0 else 0, nn)
@@ -352,10 +364,12 @@ class ShardedSequence:
                 assert bad == 0, "exchange failed"
                 if esc:  # the previous chunk escaped: this chunk ran from a wrong state
                     self._redo(*prev)
+                    k = self.xch.k ^ 1  # the redo's exchange ordered (and saved) this chunk's start again
                     prev = None
                     continue
-            self.xch.exchange(self.x, self.y, self.v, self.escape, S)
-            prev = (c0, n, saved)
+            k_next = self.xch.exchange(self.x, self.y, self.v, self.escape, S)
+            prev = (c0, n, k)
+            k = k_next
             i += 1
         self.xch.ev.synchronize()
         if prev is not None and self.xch.verdict()[0]:

@@ -206,8 +206,9 @@ def device_gather_merge(gpu, ctx, state, outs, edges, escapes=None):
     dev = state[0].device
     work = torch.empty(n + world, dtype=torch.int32, device=dev)
     E = (C.c_float * (world + 1))(*edges)
-    check(gpu, ctx, gpu.klt_hip_gather_order(ctx, C.c_void_p(state[1].data_ptr()), C.c_void_p(state[2].data_ptr()),
-                                             n, E, world, C.c_void_p(work.data_ptr())), "order")
+    check(gpu, ctx, gpu.klt_hip_gather_order(ctx, None, C.c_void_p(state[1].data_ptr()),
+                                             C.c_void_p(state[2].data_ptr()), n, E, world,
+                                             C.c_void_p(work.data_ptr()), None, None, None), "order")
     S = max(1, int(work[n:].max().item()))
     W = slot_words(S)
     slots = torch.zeros(world * W, dtype=torch.int32, device=dev)
@@ -222,7 +223,7 @@ def device_gather_merge(gpu, ctx, state, outs, edges, escapes=None):
     check(gpu, ctx, gpu.klt_hip_gather_unpack(ctx, C.c_void_p(slots.data_ptr()), world, 0,
                                               C.c_void_p(work.data_ptr()), n, S, C.c_void_p(x.data_ptr()),
                                               C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()),
-                                              C.c_void_p(flags.data_ptr())), "unpack")
+                                              C.c_void_p(flags.data_ptr()), None), "unpack")
     assert int(flags[1].item()) == 0
     device_gather_merge.flags = flags.cpu().tolist()
     return x, y, v
