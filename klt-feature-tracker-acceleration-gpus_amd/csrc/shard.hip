@@ -132,59 +132,82 @@ struct GatherEdges {
 // save (optional): x0/y0/v0 also copied to save[0..3n) (the redo's start
 // state) and *escape zeroed -- the chunk-start work of one launch; host_counts
 // (optional, pinned host memory): the counts written there too, so the driver
-// reads them behind an event with no copy-engine hand-off on the stream
+// reads them behind an event with no copy-engine hand-off on the stream.
+// One workgroup; features in rounds of 1024 (round k holds [1024k, 1024k+1024)),
+// kGatherBatch rounds at a time: every thread loads its features of the
+// batch's rounds at once, the waves' per-rank counts of every round go to LDS
+// by ballot, and four barriers per batch turn them into places -- this kernel
+// sits between two chunks' trackers, so its latency is the chain's
+constexpr int kGatherBatch = 8;
+
 __global__ __launch_bounds__(kGatherThreads) void k_gather_order(const float *__restrict__ x0,
                                                                  const float *__restrict__ y0,
                                                                  const int *__restrict__ v0, int n, GatherEdges E,
                                                                  int *__restrict__ code, int *__restrict__ counts,
                                                                  int *__restrict__ save, int *__restrict__ escape,
                                                                  int *__restrict__ host_counts) {
-  constexpr int NW = kGatherThreads / 64;
-  __shared__ int wc[NW][KLT_HIP_GATHER_MAX_RANKS];
-  __shared__ int base[KLT_HIP_GATHER_MAX_RANKS];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid < E.world) base[tid] = 0;
+  constexpr int NW = kGatherThreads / 64, B = kGatherBatch, MR = KLT_HIP_GATHER_MAX_RANKS;
+  __shared__ int wc[B][NW][MR];  // wave w's count of rank r in round k of the batch
+  __shared__ int pre[B][MR];     // places before round k's first feature of rank r
+  __shared__ int base[MR];       // places taken by earlier batches
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, world = E.world;
+  if (tid < world) base[tid] = 0;
   if (tid == 0 && escape) *escape = 0;
-  __syncthreads();
-  for (int r0 = 0; r0 < n; r0 += kGatherThreads) {  // rounds of 1024 features, in index order
-    const int i = r0 + tid;
-    int q = -1;
-    if (i < n && save) {
-      save[i] = __float_as_int(x0[i]);
-      save[n + i] = __float_as_int(y0[i]);
-      save[2 * n + i] = v0[i];
-    }
-    if (i < n && v0[i] >= 0) {
-      const float y = y0[i];
-      for (int r = 0; r < E.world; ++r)
-        if (y >= E.e[r] && y < E.e[r + 1]) {
-          q = r;
-          break;
+  for (int b0 = 0; b0 < n; b0 += B * kGatherThreads) {
+    int q[B], mine[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) {  // every load of the batch in flight before any is used
+      const int i = b0 + k * kGatherThreads + tid;
+      q[k] = -1;
+      mine[k] = 0;
+      if (i < n) {
+        const float y = y0[i];
+        const int v = v0[i];
+        if (save) {
+          save[i] = __float_as_int(x0[i]);
+          save[n + i] = __float_as_int(y);
+          save[2 * n + i] = v;
         }
+        if (v >= 0)
+          for (int r = 0; r < world; ++r)
+            if (y >= E.e[r] && y < E.e[r + 1]) {
+              q[k] = r;
+              break;
+            }
+      }
     }
-    int mine = 0;
-    for (int r = 0; r < E.world; ++r) {
-      const unsigned long long b = __ballot(q == r);
-      if (lane == 0) wc[wave][r] = __popcll(b);
-      if (q == r) mine = __popcll(b & ((1ull << lane) - 1ull));
+#pragma unroll
+    for (int k = 0; k < B; ++k)
+      for (int r = 0; r < world; ++r) {
+        const unsigned long long bal = __ballot(q[k] == r);
+        if (lane == 0) wc[k][wave][r] = __popcll(bal);
+        if (q[k] == r) mine[k] = __popcll(bal & ((1ull << lane) - 1ull));
+      }
+    __syncthreads();
+    if (tid < world) {  // rank tid: places before each round of the batch
+      int acc = base[tid];
+      for (int k = 0; k < B; ++k) {
+        pre[k][tid] = acc;
+        for (int w = 0; w < NW; ++w) acc += wc[k][w][tid];
+      }
+      base[tid] = acc;
     }
     __syncthreads();
-    if (q >= 0) {
-      int p = base[q] + mine;
-      for (int w = 0; w < wave; ++w) p += wc[w][q];
-      code[i] = (q << 24) | p;
-    } else if (i < n) {
-      code[i] = -1;
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+      const int i = b0 + k * kGatherThreads + tid;
+      if (i >= n) continue;
+      if (q[k] < 0) {
+        code[i] = -1;
+        continue;
+      }
+      int p = pre[k][q[k]] + mine[k];
+      for (int w = 0; w < wave; ++w) p += wc[k][w][q[k]];
+      code[i] = (q[k] << 24) | p;
     }
-    __syncthreads();
-    if (tid < E.world) {
-      int t = 0;
-      for (int w = 0; w < NW; ++w) t += wc[w][tid];
-      base[tid] += t;
-    }
-    __syncthreads();
+    __syncthreads();  // wc / pre are rewritten by the next batch
   }
-  if (tid < E.world) {
+  if (tid < world) {
     counts[tid] = base[tid];
     if (host_counts) host_counts[tid] = base[tid];
   }
