@@ -50,6 +50,15 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d $OUT/seqprof -o run --output-format csv -- \
         python3 -u tools/seq_variance.py $OUT/seqprof > $OUT/seqprof.log 2>&1 || { tail -20 $OUT/seqprof.log; exit 1; }
       grep -E "fps|seqtrace" $OUT/seqprof.log | cut -c1-220 ;;
+    shardprof)  # one rank of the 8-rank config-4 replay under a kernel trace (tools/rank_timeline.py)
+      timeout -k 10 900 python3 -u tools/shard_sim.py --frames 1001 --chunk 64 --worlds 8 --margins 64 --pass1-shared \
+        --keep-states $OUT/states > $OUT/shardprof_sim.log 2>&1 || { tail -20 $OUT/shardprof_sim.log; exit 1; }
+      timeout -k 10 300 rocprofv3 --kernel-trace -d $OUT/shardprof -o run --output-format csv -- \
+        python3 tools/shard_sim.py --frames 1001 --chunk 64 --replay $OUT/states/states_w8.npz --rank ${SHARD_RANK:-4} \
+        > $OUT/shardprof.log 2>&1 || { tail -20 $OUT/shardprof.log; exit 1; }
+      rm -rf $OUT/states
+      python3 tools/rank_timeline.py $(find $OUT/shardprof -name "*kernel_trace.csv") 3 > $OUT/rank_timeline.txt
+      head -60 $OUT/rank_timeline.txt ;;
     py:*)
       f=${step#py:}; b=$(basename $f .py)
       timeout -k 10 900 python3 -u $f $OUT > $OUT/$b.log 2>&1 || { tail -30 $OUT/$b.log; exit 1; }
