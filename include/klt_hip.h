@@ -376,8 +376,10 @@ int klt_hip_select_map(klt_hip_ctx *ctx, int ncols, int nrows, const klt_hip_sel
    features (val >= 0) whose chunk-start y0 lies in [edges[r], edges[r+1])
    (edges: world+1 floats, edges[0] = -inf, edges[world] = +inf; the band
    test of klt_hip_track_frames_band).  gather_order fills the device int
-   array work[n + world]: per feature its owner and place among the owner's
-   features in index order, then every rank's count (work + n).  gather_pack
+   array work[klt_hip_gather_work_ints(n, world)] (zeroed by the caller once,
+   before its first use): per feature its owner and place among the owner's
+   features in index order, every rank's count (work + n), and the
+   bookkeeping pack and unpack read.  gather_pack
    writes rank `rank`'s owned (x, y, val) bit patterns into its slot of
    KLT_HIP_GATHER_SLOT_WORDS(S) int32 (S >= the largest count) with the escape
    flag (device int, may be NULL) and a failure count; the caller all-gathers
@@ -394,12 +396,13 @@ int klt_hip_select_map(klt_hip_ctx *ctx, int ncols, int nrows, const klt_hip_sel
    host_counts (pinned host int[world]) and gather_unpack's host_flags (pinned
    host int[2]) receive the counts / flags from the kernels themselves, to be
    read once an event recorded after the launch has completed */
+long klt_hip_gather_work_ints(int n, int world);
 int klt_hip_gather_order(klt_hip_ctx *ctx, const float *x0, const float *y0, const int *v0, int n, const float *edges,
                          int world, int *work, int *save, int *escape, int *host_counts);
 int klt_hip_gather_pack(klt_hip_ctx *ctx, const float *x, const float *y, const int *val, const int *work, int n,
                         int world, int rank, const int *escape, int nfail, int *slot, int S);
 int klt_hip_gather_unpack(klt_hip_ctx *ctx, const int *slots, int nslots, int first_rank, const int *work, int n,
-                          int S, float *x, float *y, int *val, int *flags, int *host_flags);
+                          int world, int S, float *x, float *y, int *val, int *flags, int *host_flags);
 
 /* synthetic frames t0..t0+n-1 (include/klt_synth.h) into device memory */
 int klt_hip_synth_frames(klt_hip_ctx *ctx, unsigned long long seed, int t0, int n, int ncols,

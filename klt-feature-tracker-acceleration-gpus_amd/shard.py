@@ -209,7 +209,7 @@ class Exchange:
         self.lib, self.ctx, self.n, self.rank, self.all_gather = lib, ctx, n, rank, all_gather
         self.world = len(edges) - 1
         self.edges = (C.c_float * (self.world + 1))(*edges)
-        self.work = torch.empty(n + self.world, dtype=torch.int32, device=device)
+        self.work = torch.zeros(lib.klt_hip_gather_work_ints(n, self.world), dtype=torch.int32, device=device)
         self.send = torch.empty(slot_words(max(n, 1)), dtype=torch.int32, device=device)
         self.recv = torch.empty(self.world * slot_words(max(n, 1)), dtype=torch.int32, device=device)
         self.flags = torch.zeros(2, dtype=torch.int32, device=device)
@@ -260,7 +260,8 @@ class Exchange:
             C.c_void_p(send.data_ptr()), S), "gather_pack")
         self.all_gather(recv, send)
         self._check(self.lib.klt_hip_gather_unpack(
-            self.ctx, C.c_void_p(recv.data_ptr()), self.world, 0, C.c_void_p(self.work.data_ptr()), self.n, S,
+            self.ctx, C.c_void_p(recv.data_ptr()), self.world, 0, C.c_void_p(self.work.data_ptr()), self.n,
+            self.world, S,
             C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()),
             C.c_void_p(self.flags.data_ptr()), C.c_void_p(self.h_flags.data_ptr())), "gather_unpack")
         k = self.order(x, y, v, escape)

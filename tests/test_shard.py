@@ -204,12 +204,12 @@ def device_gather_merge(gpu, ctx, state, outs, edges, escapes=None):
     world = len(outs)
     n = state[0].numel()
     dev = state[0].device
-    work = torch.empty(n + world, dtype=torch.int32, device=dev)
+    work = torch.zeros(gpu.klt_hip_gather_work_ints(n, world), dtype=torch.int32, device=dev)
     E = (C.c_float * (world + 1))(*edges)
     check(gpu, ctx, gpu.klt_hip_gather_order(ctx, None, C.c_void_p(state[1].data_ptr()),
                                              C.c_void_p(state[2].data_ptr()), n, E, world,
                                              C.c_void_p(work.data_ptr()), None, None, None), "order")
-    S = max(1, int(work[n:].max().item()))
+    S = max(1, int(work[n:n + world].max().item()))
     W = slot_words(S)
     slots = torch.zeros(world * W, dtype=torch.int32, device=dev)
     for r, (xr, yr, vr) in enumerate(outs):
@@ -221,7 +221,7 @@ def device_gather_merge(gpu, ctx, state, outs, edges, escapes=None):
     x, y, v = (t.clone() for t in state)
     flags = torch.zeros(2, dtype=torch.int32, device=dev)
     check(gpu, ctx, gpu.klt_hip_gather_unpack(ctx, C.c_void_p(slots.data_ptr()), world, 0,
-                                              C.c_void_p(work.data_ptr()), n, S, C.c_void_p(x.data_ptr()),
+                                              C.c_void_p(work.data_ptr()), n, world, S, C.c_void_p(x.data_ptr()),
                                               C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()),
                                               C.c_void_p(flags.data_ptr()), None), "unpack")
     assert int(flags[1].item()) == 0
