@@ -318,6 +318,13 @@ int klt_hip_track_frames_host(klt_hip_ctx *ctx, const klt_hip_pyr_desc *pdesc,
    built on the context's pyramid stream while this chunk is tracked and the
    caller exchanges results; the next call with exactly those frames and rows
    uses them.  Needs the default (fused) pyramid parameters. */
+/* band calls of this context: ready != 0 promises that next_frames are ready
+   when each call is made (device-resident, not written by work still queued on
+   the context's stream), so the build-ahead waits only for its bank and starts
+   as soon as the tracker that last read that bank ends, instead of behind
+   everything the caller queued before the call (its exchange).  Default 0;
+   kltamd.shard.ShardedSequence sets it (its frames are loaded up front). */
+int klt_hip_set_ahead_ready(klt_hip_ctx *ctx, int ready);
 int klt_hip_track_frames_band(klt_hip_ctx *ctx, const klt_hip_pyr_desc *pdesc,
                               const klt_hip_track_desc *tdesc, const unsigned char *frames, long pitch,
                               long stride, int nframes, float *x, float *y, int *val, int n, float own_lo,
@@ -403,6 +410,12 @@ int klt_hip_gather_pack(klt_hip_ctx *ctx, const float *x, const float *y, const 
                         int world, int rank, const int *escape, int nfail, int *slot, int S);
 int klt_hip_gather_unpack(klt_hip_ctx *ctx, const int *slots, int nslots, int first_rank, const int *work, int n,
                           int world, int S, float *x, float *y, int *val, int *flags, int *host_flags);
+/* gather_unpack then gather_order of the merged state (the next chunk's
+   ownership, save, escape reset, counts) in one launch -- the step between
+   two chunks' trackers; work is read for the unpack and rewritten */
+int klt_hip_gather_unpack_order(klt_hip_ctx *ctx, const int *slots, int nslots, int first_rank, int *work, int n,
+                                int world, int S, float *x, float *y, int *val, int *flags, int *host_flags,
+                                const float *edges, int *save, int *escape, int *host_counts);
 
 /* synthetic frames t0..t0+n-1 (include/klt_synth.h) into device memory */
 int klt_hip_synth_frames(klt_hip_ctx *ctx, unsigned long long seed, int t0, int n, int ncols,

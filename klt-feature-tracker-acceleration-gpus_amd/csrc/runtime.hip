@@ -219,6 +219,11 @@ struct klt_hip_ctx {
   size_t pl_cap[2][KLT_HIP_MAX_LEVELS] = {};
   int track_impl = 0;    // 0: track7.hip for the default configuration, 1: the generic k_track_frames_g
   const char *track_kernel = nullptr;  // instance name of the last tracker launch (klt_hip_track_kernel)
+  // band calls: 1 = the next chunk's frames are ready when the call is made
+  // (not written by work still queued on the tracking stream), so its
+  // build-ahead waits only for its bank to be free, not for everything queued
+  // before the call (klt_hip_set_ahead_ready)
+  int ahead_ready = 0;
   int serial_frames = 1;  // klt_hip_track_frames: 1 builds and tracks on one stream (default: the
                           // tracker and the pyramid kernels compete for the same CUs; overlap buys ~3 %)
   int *d_perm = nullptr;
@@ -1152,6 +1157,7 @@ KLT_API int klt_hip_ctx_reset(klt_hip_ctx *c) {
   c->track_prio = 1;
   c->track_impl = 0;
   c->serial_frames = 1;
+  c->ahead_ready = 0;
   c->prof = nullptr;
   c->frames_ready = false;
   c->pre.bank = -1;
@@ -1356,6 +1362,12 @@ KLT_API size_t klt_hip_get_bank_budget(klt_hip_ctx *c) { return c ? bank_budget_
 KLT_API int klt_hip_frames_chunk(klt_hip_ctx *c) { return c ? c->chunk_used : -1; }
 
 KLT_API int klt_hip_get_host_threads(klt_hip_ctx *c) { return c ? c->copy_threads : -1; }
+
+KLT_API int klt_hip_set_ahead_ready(klt_hip_ctx *c, int ready) {
+  if (!c) return -1;
+  c->ahead_ready = ready != 0;
+  return 0;
+}
 
 KLT_API int klt_hip_set_frames_overlap(klt_hip_ctx *c, int overlap) {
   if (!c) return fail(c, "set_frames_overlap: null context");
@@ -1950,11 +1962,20 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
   // (~12 us measured between k_pyr_l1's end and k_track7's start).  The next
   // call's pyramid stream still starts behind it (ev_start below).
   const bool serial = band ? false : (c->serial_frames != 0 || nframes <= chunk);
-  // the pyramid stream starts behind everything already queued on the tracking stream
-  if (!serial) {
-    HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
+  // the pyramid stream starts behind everything already queued on the
+  // tracking stream -- except a band call's build-ahead when the caller has
+  // said its frames are ready (klt_hip_set_ahead_ready): that waits only for
+  // its bank, and the build starts as soon as the tracker that last read the
+  // bank ends, not after the caller's exchange between two chunks
+  bool pwait = false;
+  auto pstream_behind = [&]() -> int {
+    if (serial || pwait) return 0;
+    pwait = true;
     HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_start, 0));
-  }
+    return 0;
+  };
+  if (!serial) HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
+  if (!(band && c->ahead_ready) && pstream_behind()) return -1;
   const bool fz = fused_ok(pd) && !c->force_generic;
   if (band && !fz) return fail(c, "track_frames_band: needs the fused (default-parameter) pyramid path");
   // the banks' layout follows their reader: interleaved for k_track7, planes
@@ -1985,6 +2006,7 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
                           c->pre.il == bil;
     if (c->pre.bank == bi) c->pre.bank = -1;  // taken now, or about to be overwritten
     // one stream: stream order is the dependency (an event wait would add a queue barrier)
+    if (!serial && !prebuilt && pstream_behind()) return -1;  // this chunk's own frames: behind the caller's work
     if (!serial && !prebuilt) HIPCHK(c, hipStreamWaitEvent(ps, c->ev_bfree[bi], 0));
     if (prebuilt) {
       // ev_bbuilt[bi] was recorded after that build: the wait below orders it

@@ -149,27 +149,26 @@ __host__ __device__ inline long gather_work_ints(int n, int world) {
   return (long)n + world + 2 * nb * world + 1;
 }
 
-__global__ __launch_bounds__(kOrderBlock) void k_gather_order(const float *__restrict__ x0,
-                                                              const float *__restrict__ y0,
-                                                              const int *__restrict__ v0, int n, GatherEdges E,
-                                                              int *__restrict__ work, int *__restrict__ save,
-                                                              int *__restrict__ escape,
-                                                              int *__restrict__ host_counts) {
-  constexpr int NW = kOrderBlock / 64, MR = KLT_HIP_GATHER_MAX_RANKS;
-  __shared__ int wc[NW][MR];
-  __shared__ int last;
+struct OrderShared {
+  int wc[kOrderBlock / 64][KLT_HIP_GATHER_MAX_RANKS];
+  int last;
+};
+
+// feature i's chunk-start (x, y, v) (valid: i < n) into the order: the save
+// copy, the owner, the place in the block, the block's counts, and -- in the
+// last block to arrive -- every block's starting places and the counts
+__device__ __forceinline__ void order_core(OrderShared &sh, int n, const GatherEdges &E, int *__restrict__ work,
+                                           int i, bool valid, float x, float y, int v, int *__restrict__ save,
+                                           int *__restrict__ host_counts) {
+  constexpr int NW = kOrderBlock / 64;
   const int world = E.world, nb = (n + kOrderBlock - 1) / kOrderBlock;
   int *code = work, *counts = work + n, *pre = counts + world, *blk = pre + (long)nb * world;
   int *done = blk + (long)nb * world;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, b = blockIdx.x;
-  const int i = b * kOrderBlock + tid;
-  if (b == 0 && tid == 0 && escape) *escape = 0;
   int q = -1;
-  if (i < n) {
-    const float y = y0[i];
-    const int v = v0[i];
+  if (valid) {
     if (save) {
-      save[i] = __float_as_int(x0[i]);
+      save[i] = __float_as_int(x);
       save[n + i] = __float_as_int(y);
       save[2 * n + i] = v;
     }
@@ -183,37 +182,111 @@ __global__ __launch_bounds__(kOrderBlock) void k_gather_order(const float *__res
   int mine = 0;
   for (int r = 0; r < world; ++r) {
     const unsigned long long bal = __ballot(q == r);
-    if (lane == 0) wc[wave][r] = __popcll(bal);
+    if (lane == 0) sh.wc[wave][r] = __popcll(bal);
     if (q == r) mine = __popcll(bal & ((1ull << lane) - 1ull));
   }
   __syncthreads();
-  if (i < n) {
+  if (valid) {
     int p = mine;
     if (q >= 0)
-      for (int w = 0; w < wave; ++w) p += wc[w][q];
+      for (int w = 0; w < wave; ++w) p += sh.wc[w][q];
     code[i] = q < 0 ? -1 : ((q << 24) | p);
   }
   if (tid < world) {
     int t = 0;
-    for (int w = 0; w < NW; ++w) t += wc[w][tid];
+    for (int w = 0; w < NW; ++w) t += sh.wc[w][tid];
     blk[(long)b * world + tid] = t;
   }
-  __threadfence();  // this block's counts before its arrival
+  __threadfence();  // this block's counts (and every read of the previous order) before its arrival
   __syncthreads();
-  if (tid == 0) last = atomicAdd(done, 1) == nb - 1;
+  if (tid == 0) sh.last = atomicAdd(done, 1) == nb - 1;
   __syncthreads();
-  if (!last) return;
+  if (!sh.last) return;
   __threadfence();  // every block's counts are visible to the last one
-  if (tid < world) {
+  if (tid < world) {  // rank tid's places: block counts read 16 at a time
     int acc = 0;
-    for (int bb = 0; bb < nb; ++bb) {
-      pre[(long)bb * world + tid] = acc;
-      acc += __atomic_load_n(&blk[(long)bb * world + tid], __ATOMIC_RELAXED);
+    for (int b0 = 0; b0 < nb; b0 += 16) {
+      int t[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) t[k] = b0 + k < nb ? blk[(long)(b0 + k) * world + tid] : 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (b0 + k < nb) {
+          pre[(long)(b0 + k) * world + tid] = acc;
+          acc += t[k];
+        }
     }
     counts[tid] = acc;
     if (host_counts) host_counts[tid] = acc;
   }
   if (tid == 0) *done = 0;  // ready for the next launch
+}
+
+__global__ __launch_bounds__(kOrderBlock) void k_gather_order(const float *__restrict__ x0,
+                                                              const float *__restrict__ y0,
+                                                              const int *__restrict__ v0, int n, GatherEdges E,
+                                                              int *__restrict__ work, int *__restrict__ save,
+                                                              int *__restrict__ escape,
+                                                              int *__restrict__ host_counts) {
+  __shared__ OrderShared sh;
+  const int i = blockIdx.x * kOrderBlock + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && escape) *escape = 0;
+  const bool valid = i < n;
+  const float x = valid && save ? x0[i] : 0.0f, y = valid ? y0[i] : 0.0f;
+  const int v = valid ? v0[i] : -1;
+  order_core(sh, n, E, work, i, valid, x, y, v, save, host_counts);
+}
+
+// gather_unpack and the next chunk's gather_order in one launch: feature i
+// from its owner's slot (the order that packed it: code and places read before
+// this block arrives), then its new ownership (the order the next exchange
+// uses) from the merged state
+__global__ __launch_bounds__(kOrderBlock) void k_gather_unpack_order(
+    const int *__restrict__ slots, int nslots, int r0, int n, int S, float *__restrict__ x, float *__restrict__ y,
+    int *__restrict__ v, int *__restrict__ flags, int *__restrict__ host_flags, GatherEdges E, int *__restrict__ work,
+    int *__restrict__ save, int *__restrict__ escape, int *__restrict__ host_counts) {
+  __shared__ OrderShared sh;
+  const int world = E.world, nb = (n + kOrderBlock - 1) / kOrderBlock;
+  const int *pre = work + n + world;
+  const int i = blockIdx.x * kOrderBlock + threadIdx.x;
+  const long words = kGatherHdr + 3L * S;
+  int esc = 0, bad = 0;
+  for (int k = 0; k < nslots; ++k) {
+    const int *h = slots + k * words;
+    esc += h[0];
+    bad += h[1] + (h[2] > S || h[3] != S ? 1 : 0);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    flags[0] = esc;
+    flags[1] = bad;
+    if (host_flags) {
+      host_flags[0] = esc;
+      host_flags[1] = bad;
+    }
+    if (escape) *escape = 0;
+  }
+  const bool valid = i < n;
+  float xi = 0.0f, yi = 0.0f;
+  int vi = -1;
+  if (valid) {
+    xi = x[i];
+    yi = y[i];
+    vi = v[i];
+    const int c = work[i];
+    const int q = c >> 24, k = q - r0;
+    if (!bad && c >= 0 && k >= 0 && k < nslots) {
+      const int *sl = slots + k * words + kGatherHdr;
+      const int p = pre[(long)blockIdx.x * world + q] + (c & 0xFFFFFF);
+      xi = __int_as_float(sl[p]);
+      yi = __int_as_float(sl[S + p]);
+      vi = sl[2 * S + p];
+      x[i] = xi;
+      y[i] = yi;
+      v[i] = vi;
+    }
+  }
+  (void)nb;
+  order_core(sh, n, E, work, i, valid, xi, yi, vi, save, host_counts);
 }
 
 __global__ void k_gather_pack(const float *__restrict__ x, const float *__restrict__ y, const int *__restrict__ v,
@@ -406,6 +479,26 @@ KLT_API int klt_hip_gather_unpack(klt_hip_ctx *ctx, const int *slots, int nslots
                      first_rank, work, work + n + world, n, world, S, x, y, val, flags, host_flags);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : kltdev::ctx_fail(ctx, "gather_unpack: %s", hipGetErrorString(e));
+}
+
+KLT_API int klt_hip_gather_unpack_order(klt_hip_ctx *ctx, const int *slots, int nslots, int first_rank, int *work,
+                                        int n, int world, int S, float *x, float *y, int *val, int *flags,
+                                        int *host_flags, const float *edges, int *save, int *escape,
+                                        int *host_counts) {
+  if (!ctx || nslots < 1 || first_rank < 0 || first_rank + nslots > world || world > KLT_HIP_GATHER_MAX_RANKS ||
+      n < 0 || n >= (1 << 24) || S < 0 || !slots || !work || !flags || !edges || (n > 0 && (!x || !y || !val)))
+    return ctx ? kltdev::ctx_fail(ctx, "gather_unpack_order: bad argument") : -1;
+  DeviceGuard guard;
+  if (hipSetDevice(klt_hip_ctx_device(ctx)) != hipSuccess) return kltdev::ctx_fail(ctx, "gather_unpack_order: device");
+  GatherEdges E{};
+  for (int r = 0; r <= world; ++r) E.e[r] = edges[r];
+  E.world = world;
+  const int nb = n > 0 ? (n + kOrderBlock - 1) / kOrderBlock : 1;
+  hipLaunchKernelGGL(k_gather_unpack_order, dim3(nb), dim3(kOrderBlock), 0, (hipStream_t)klt_hip_get_stream(ctx),
+                     slots, nslots, first_rank, n, S, x, y, val, flags, host_flags, E, work, save, escape,
+                     host_counts);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : kltdev::ctx_fail(ctx, "gather_unpack_order: %s", hipGetErrorString(e));
 }
 
 KLT_API int klt_shard_unique_id(unsigned char id[KLT_SHARD_ID_BYTES]) {

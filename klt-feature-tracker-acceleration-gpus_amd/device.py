@@ -111,6 +111,9 @@ DEVICE_PROTOS = {
     "klt_hip_gather_pack": (C.c_int, [V, V, V, V, V, C.c_int, C.c_int, C.c_int, V, C.c_int, V, C.c_int]),
     "klt_hip_gather_unpack": (C.c_int, [V, V, C.c_int, C.c_int, V, C.c_int, C.c_int, C.c_int, V, V, V, V, V]),
     "klt_hip_gather_work_ints": (C.c_long, [C.c_int, C.c_int]),
+    "klt_hip_gather_unpack_order": (C.c_int, [V, V, C.c_int, C.c_int, V, C.c_int, C.c_int, C.c_int, V, V, V, V, V,
+                                              FP, V, V, V]),
+    "klt_hip_set_ahead_ready": (C.c_int, [V, C.c_int]),
     "klt_shard_eigen": (C.c_int, [V, C.POINTER(PyrDesc), V, C.c_long, V, V, V]),
     "klt_shard_select": (C.c_int, [V, C.POINTER(PyrDesc), V, C.c_int, C.c_int, V, V, V, V, C.c_int]),
     "klt_shard_replace": (C.c_int, [V, C.POINTER(PyrDesc), V, C.c_long, C.c_int, C.c_int, V, V, V, C.c_int, V, V]),

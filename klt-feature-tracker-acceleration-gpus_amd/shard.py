@@ -259,12 +259,16 @@ class Exchange:
             C.c_void_p(self.work.data_ptr()), self.n, self.world, self.rank, C.c_void_p(escape.data_ptr()), 0,
             C.c_void_p(send.data_ptr()), S), "gather_pack")
         self.all_gather(recv, send)
-        self._check(self.lib.klt_hip_gather_unpack(
+        # unpack and the next chunk's order (ownership, start-state save, escape reset, counts) in one launch
+        k = self.k
+        self.k ^= 1
+        self._check(self.lib.klt_hip_gather_unpack_order(
             self.ctx, C.c_void_p(recv.data_ptr()), self.world, 0, C.c_void_p(self.work.data_ptr()), self.n,
-            self.world, S,
-            C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()),
-            C.c_void_p(self.flags.data_ptr()), C.c_void_p(self.h_flags.data_ptr())), "gather_unpack")
-        k = self.order(x, y, v, escape)
+            self.world, S, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()),
+            C.c_void_p(self.flags.data_ptr()), C.c_void_p(self.h_flags.data_ptr()), self.edges,
+            C.c_void_p(self.save[k].data_ptr()), C.c_void_p(escape.data_ptr()),
+            C.c_void_p(self.h_counts.data_ptr())), "gather_unpack_order")
+        self.ev.record()
         if self.timing:
             e = torch.cuda.Event(enable_timing=True)
             e.record()
@@ -304,6 +308,8 @@ class ShardedSequence:
             ra, rb = band_rows(H, self.band)
             assert self.src.ra <= ra and self.src.rb >= rb, "BandFrames built for another band"
         self.escape = torch.zeros(1, dtype=torch.int32, device=x.device)
+        # the frames are resident before run(): each build-ahead waits only for its bank
+        self._check(lib, ctx, lib.klt_hip_set_ahead_ready(ctx, 1), "set_ahead_ready")
         self.xch = Exchange(lib, ctx, x.numel(), band_edges(H, world, edges), rank, all_gather, x.device)
         self.redone = 0
         self.rebuilt = 0  # replacements whose band pyramid was too short for the selection window

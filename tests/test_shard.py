@@ -283,6 +283,38 @@ def test_gather_kernels_equal_reference(gpu, world):
     for g, w in zip(got, ref):
         assert np.array_equal(g.cpu().numpy().view(np.int32), w.numpy().view(np.int32))
     assert device_gather_merge.flags == [sum(range(world)), 0] == [esc_ref, 0]
+    # the fused step (unpack + the next order, klt_hip_gather_unpack_order) on the same slots: the same
+    # merged state, its start state saved, the escape flag zeroed, and the merged state's counts
+    from kltamd.shard import slot_words
+    E = (C.c_float * (world + 1))(*edges)
+    work = torch.zeros(gpu.klt_hip_gather_work_ints(n, world), dtype=torch.int32, device=dev)
+    assert gpu.klt_hip_gather_order(ctx, None, C.c_void_p(state[1].data_ptr()), C.c_void_p(state[2].data_ptr()), n,
+                                    E, world, C.c_void_p(work.data_ptr()), None, None, None) == 0
+    S = max(1, int(work[n:n + world].max().item()))
+    Wd = slot_words(S)
+    slots = torch.zeros(world * Wd, dtype=torch.int32, device=dev)
+    for r, (xr, yr, vr) in enumerate(outs):
+        assert gpu.klt_hip_gather_pack(ctx, C.c_void_p(xr.data_ptr()), C.c_void_p(yr.data_ptr()),
+                                       C.c_void_p(vr.data_ptr()), C.c_void_p(work.data_ptr()), n, world, r,
+                                       C.c_void_p(escs[r].data_ptr()), 0, C.c_void_p(slots[r * Wd:].data_ptr()),
+                                       S) == 0
+    x, y, v = (t.clone() for t in state)
+    flags = torch.zeros(2, dtype=torch.int32, device=dev)
+    save = torch.zeros(3 * n, dtype=torch.int32, device=dev)
+    esc = torch.ones(1, dtype=torch.int32, device=dev)
+    hc = torch.zeros(world, dtype=torch.int32).pin_memory()
+    assert gpu.klt_hip_gather_unpack_order(ctx, C.c_void_p(slots.data_ptr()), world, 0, C.c_void_p(work.data_ptr()), n,
+                                           world, S, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()),
+                                           C.c_void_p(v.data_ptr()), C.c_void_p(flags.data_ptr()), None, E,
+                                           C.c_void_p(save.data_ptr()), C.c_void_p(esc.data_ptr()),
+                                           C.c_void_p(hc.data_ptr())) == 0
+    torch.cuda.synchronize()
+    for g, w in zip((x, y, v), ref):
+        assert np.array_equal(g.cpu().numpy().view(np.int32), w.numpy().view(np.int32))
+    assert np.array_equal(save.cpu().numpy(), np.concatenate([w.numpy().view(np.int32) for w in ref]))
+    assert int(esc.item()) == 0 and flags.cpu().tolist() == [esc_ref, 0]
+    _, _, counts = gather_order_ref(ref[1], ref[2], edges)
+    assert hc.tolist() == counts == work[n:n + world].cpu().tolist()
     gpu.KLTFreeTrackingContext(tc)
 
 
