@@ -309,7 +309,7 @@ class ShardedSequence:
             assert self.src.ra <= ra and self.src.rb >= rb, "BandFrames built for another band"
         self.escape = torch.zeros(1, dtype=torch.int32, device=x.device)
         # the frames are resident before run(): each build-ahead waits only for its bank
-        self._check(lib, ctx, lib.klt_hip_set_ahead_ready(ctx, 1), "set_ahead_ready")
+        check(lib, ctx, lib.klt_hip_set_ahead_ready(ctx, 1), "set_ahead_ready")
         self.xch = Exchange(lib, ctx, x.numel(), band_edges(H, world, edges), rank, all_gather, x.device)
         self.redone = 0
         self.rebuilt = 0  # replacements whose band pyramid was too short for the selection window
