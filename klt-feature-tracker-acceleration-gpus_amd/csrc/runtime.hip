@@ -298,6 +298,21 @@ namespace {
     if (e_ != hipSuccess) return fail((c), "%s: %s", #expr, hipGetErrorString(e_));    \
   } while (0)
 
+// the pyramid stream: normal priority, or the lowest (KLT_PSTREAM_PRIO=low:
+// the tracking stream's short kernels between two chunks -- the exchange, the
+// processing order -- are then dispatched ahead of queued pyramid workgroups)
+hipError_t make_pstream(klt_hip_ctx *c) {
+  static const bool low = [] {
+    const char *v = getenv("KLT_PSTREAM_PRIO");
+    return v && strcmp(v, "low") == 0;
+  }();
+  if (!low) return hipStreamCreateWithFlags(&c->pstream, hipStreamNonBlocking);
+  int least = 0, greatest = 0;
+  const hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (e != hipSuccess) return e;
+  return hipStreamCreateWithPriority(&c->pstream, hipStreamNonBlocking, least);
+}
+
 bool seq_trace() {
   static const bool t = getenv("KLT_SEQ_TRACE") && atoi(getenv("KLT_SEQ_TRACE")) != 0;
   return t;
@@ -1735,7 +1750,7 @@ KLT_API int klt_hip_track_sequence(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, c
   if (nsteps <= 0) return 0;
   if (use_device(c)) return -1;
   if (!c->pstream) {
-    HIPCHK(c, hipStreamCreateWithFlags(&c->pstream, hipStreamNonBlocking));
+    HIPCHK(c, make_pstream(c));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
     for (int k = 0; k < 3; ++k) {
       HIPCHK(c, hipEventCreateWithFlags(&c->ev_built[k], hipEventDisableTiming));
@@ -1905,7 +1920,7 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
   if (use_device(c)) return -1;
   HMARK("set_device");
   if (!c->pstream) {
-    HIPCHK(c, hipStreamCreateWithFlags(&c->pstream, hipStreamNonBlocking));
+    HIPCHK(c, make_pstream(c));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
     for (int k = 0; k < 3; ++k) {
       HIPCHK(c, hipEventCreateWithFlags(&c->ev_built[k], hipEventDisableTiming));

@@ -228,6 +228,7 @@ __global__ __launch_bounds__(kOrderBlock) void k_gather_order(const float *__res
                                                               int *__restrict__ work, int *__restrict__ save,
                                                               int *__restrict__ escape,
                                                               int *__restrict__ host_counts) {
+  __builtin_amdgcn_s_setprio(3);  // between two trackers: issue ahead of co-resident pyramid waves
   __shared__ OrderShared sh;
   const int i = blockIdx.x * kOrderBlock + threadIdx.x;
   if (blockIdx.x == 0 && threadIdx.x == 0 && escape) *escape = 0;
@@ -245,6 +246,7 @@ __global__ __launch_bounds__(kOrderBlock) void k_gather_unpack_order(
     const int *__restrict__ slots, int nslots, int r0, int n, int S, float *__restrict__ x, float *__restrict__ y,
     int *__restrict__ v, int *__restrict__ flags, int *__restrict__ host_flags, GatherEdges E, int *__restrict__ work,
     int *__restrict__ save, int *__restrict__ escape, int *__restrict__ host_counts) {
+  __builtin_amdgcn_s_setprio(3);  // between two trackers: issue ahead of co-resident pyramid waves
   __shared__ OrderShared sh;
   const int world = E.world, nb = (n + kOrderBlock - 1) / kOrderBlock;
   const int *pre = work + n + world;
@@ -293,6 +295,7 @@ __global__ void k_gather_pack(const float *__restrict__ x, const float *__restri
                               const int *__restrict__ code, const int *__restrict__ counts,
                               const int *__restrict__ pre, int n, int world, int rank,
                               const int *__restrict__ escape, int nfail, int *__restrict__ slot, int S) {
+  __builtin_amdgcn_s_setprio(3);
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
     const int c = code[i];

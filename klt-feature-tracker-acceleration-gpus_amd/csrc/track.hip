@@ -872,6 +872,7 @@ __global__ __launch_bounds__(kSortThreads) void k_band_order(const float *__rest
                                                              const int *__restrict__ fv, int n, int nrows,
                                                              int *__restrict__ perm, float own_lo, float own_hi,
                                                              int *__restrict__ count) {
+  __builtin_amdgcn_s_setprio(3);  // on the chain between two tracker launches
   // count != nullptr: keep only live features with own_lo <= y < own_hi (a
   // rank's band in sharded mode), *count = how many; else every feature
   __shared__ int cnt[kBands + 2];
