@@ -885,17 +885,32 @@ def api_leg(lib, frames, W, H, NF, args):
         lib.KLTFreeTrackingContext(tc)
         return dt, out
 
+    def h2d_gbs():
+        """the bus right now: one 256 MiB pinned -> device copy"""
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        bus_dst.copy_(bus_src, non_blocking=True)
+        torch.cuda.synchronize()
+        return bus_src.numel() / (time.perf_counter() - a) / 1e9
+
     # two calls warm the device context that the timed call's tracking context
     # then takes over (klt_api.c keeps the device contexts of freed tracking
     # contexts: banks, staging, host threads); the table's pages are touched
     dt_cold, _ = sequence()
     sequence()
-    # three timed calls, the median reported: a call now and then runs 2-3x
-    # slower on the pool's boxes, with or without the sort pool's threads
-    # (tools/exp/r04aj.sh), and one sample made the leg swing 10-24k
-    runs = [sequence() for _ in range(3)]
+    # five timed calls, min / median / max reported with the pinned H2D rate
+    # measured right before each: the call moves 2 MB per frame over PCIe
+    # (KLT_SEQ_TRACE: the host-side staging copy and the DMA are its time), so a
+    # slower call goes with a slower bus (tools/seq_variance.py, DESIGN.md 6)
+    bus_src = torch.empty(256 << 20, dtype=torch.uint8).pin_memory()
+    bus_dst = torch.empty(256 << 20, dtype=torch.uint8, device=frames.device)
+    runs, bus = [], []
+    for _ in range(5):
+        bus.append(h2d_gbs())
+        runs.append(sequence())
+    del bus_src, bus_dst
     dts = [r[0] for r in runs]
-    dt, sq = sorted(dts)[1], runs[-1][1]
+    dt, sq = sorted(dts)[len(dts) // 2], runs[-1][1]
     lib.KLTFreeFeatureTable(ft)
     same = all(np.array_equal(np.asarray(p).view(np.int32), np.asarray(q).view(np.int32)) for p, q in zip(pc, sq))
     return {
@@ -906,9 +921,12 @@ def api_leg(lib, frames, W, H, NF, args):
         "sequence": {"value": n / dt, "unit": "frames/s", "frames": n,
                      "region": "one KLTTrackSequence call over host frames 0..n writing every column of a "
                                "KLT_FeatureTable (frame uploads, pyramids of frames 0..n, tracking, table rows "
-                               "down and stored); the median of calls 3-5 in the process on the same table, each "
+                               "down and stored); the median of calls 3-7 in the process on the same table, each "
                                "with a fresh tracking context and selection",
                      "calls_fps": [n / d for d in dts],
+                     "calls_fps_min_median_max": [n / max(dts), n / dt, n / min(dts)],
+                     "h2d_pinned_gbs_before_each_call": bus,
+                     "fraction_of_bus_each_call": [(n / d) * W * H / (b * 1e9) for d, b in zip(dts, bus)],
                      "first_call_value": n / dt_cold,
                      "first_call": "the process's first KLTTrackSequence: device allocations, pinned staging, "
                                    "host threads, the table's first touch"},

@@ -128,129 +128,127 @@ struct GatherEdges {
   int world;
 };
 
-// k_gather_order over blocks of 256 features: each block finds its features'
-// owners and their places within the block (by ballot), writes its per-rank
-// block counts, and the last block to finish (a device-scope counter) turns
-// them into every block's starting place per rank (pre) and the counts.  A
-// feature's place among its owner's features is then pre[block][owner] + its
-// place in the block (code = owner << 24 | place in the block).  One launch,
-// every feature's load in flight at once: this kernel sits between two
-// chunks' trackers, so its latency is the chain's (a one-workgroup version
-// took 65 us for 20 000 features).
-// save (optional): x0/y0/v0 also copied to save[0..3n) (the redo's start
-// state) and *escape zeroed; host_counts (optional, pinned host memory): the
-// counts written there too, read behind an event with no copy-engine
-// hand-off on the stream.
-// work: code[n] | counts[world] | pre[nblocks][world] | blk[nblocks][world] | done
-constexpr int kOrderBlock = 256;
+// k_gather_order: ONE workgroup of 1024 threads (no cross-workgroup
+// handshake: on gfx950 that takes device-scope fences, which write back and
+// invalidate L2 -- tens of us while a pyramid kernel streams beside it).  In
+// passes of 1024 * kOrderM features, thread t takes the contiguous features
+// [t*M, t*M + M) of the pass, loads them all at once and finds their owners;
+// then for each rank r in turn: the thread's count of r, a wave scan, the
+// waves' totals through LDS (one barrier), and every feature of r gets its
+// place -- in index order, since features of lower threads have lower
+// indices.  This kernel sits between two chunks' trackers: its latency is
+// the chain's.  save (optional): x0/y0/v0 also copied to save[0..3n) (the
+// redo's start state) and *escape zeroed; host_counts (optional, pinned host
+// memory): the counts written there too, read behind an event with no
+// copy-engine hand-off on the stream.  work: code[n] | counts[world].
+constexpr int kOrderThreads = 1024, kOrderM = 20;  // 20 480 features a pass (config 4 in one)
 
-__host__ __device__ inline long gather_work_ints(int n, int world) {
-  const long nb = (n + kOrderBlock - 1) / kOrderBlock;
-  return (long)n + world + 2 * nb * world + 1;
-}
+__host__ __device__ inline long gather_work_ints(int n, int world) { return (long)n + world; }
 
 struct OrderShared {
-  int wc[kOrderBlock / 64][KLT_HIP_GATHER_MAX_RANKS];
-  int last;
+  int wtot[KLT_HIP_GATHER_MAX_RANKS][kOrderThreads / 64];
+  int base[KLT_HIP_GATHER_MAX_RANKS];
 };
 
-// feature i's chunk-start (x, y, v) (valid: i < n) into the order: the save
-// copy, the owner, the place in the block, the block's counts, and -- in the
-// last block to arrive -- every block's starting places and the counts
-__device__ __forceinline__ void order_core(OrderShared &sh, int n, const GatherEdges &E, int *__restrict__ work,
-                                           int i, bool valid, float x, float y, int v, int *__restrict__ save,
-                                           int *__restrict__ host_counts) {
-  constexpr int NW = kOrderBlock / 64;
-  const int world = E.world, nb = (n + kOrderBlock - 1) / kOrderBlock;
-  int *code = work, *counts = work + n, *pre = counts + world, *blk = pre + (long)nb * world;
-  int *done = blk + (long)nb * world;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, b = blockIdx.x;
-  int q = -1;
-  if (valid) {
-    if (save) {
-      save[i] = __float_as_int(x);
-      save[n + i] = __float_as_int(y);
-      save[2 * n + i] = v;
-    }
-    if (v >= 0)
-      for (int r = 0; r < world; ++r)
-        if (y >= E.e[r] && y < E.e[r + 1]) {
-          q = r;
-          break;
-        }
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int o = __shfl_up(v, d, 64);
+    if (lane >= d) v += o;
   }
-  int mine = 0;
-  for (int r = 0; r < world; ++r) {
-    const unsigned long long bal = __ballot(q == r);
-    if (lane == 0) sh.wc[wave][r] = __popcll(bal);
-    if (q == r) mine = __popcll(bal & ((1ull << lane) - 1ull));
-  }
+  return v;
+}
+
+// LOAD(i, x, y, v): feature i's chunk-start values (i < n); MERGE: unpack first
+template <class Load>
+__device__ __forceinline__ void order_pass_all(OrderShared &sh, int n, const GatherEdges &E, int *__restrict__ code,
+                                               int *__restrict__ counts, int *__restrict__ save,
+                                               int *__restrict__ host_counts, Load load) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, world = E.world;
+  constexpr int NW = kOrderThreads / 64;
+  if (tid < world) sh.base[tid] = 0;
   __syncthreads();
-  if (valid) {
-    int p = mine;
-    if (q >= 0)
-      for (int w = 0; w < wave; ++w) p += sh.wc[w][q];
-    code[i] = q < 0 ? -1 : ((q << 24) | p);
+  for (int p0 = 0; p0 < n; p0 += kOrderThreads * kOrderM) {
+    const int i0 = p0 + tid * kOrderM;
+    int q[kOrderM];
+    float xs[kOrderM], ys[kOrderM];
+    int vs[kOrderM];
+#pragma unroll
+    for (int k = 0; k < kOrderM; ++k) {  // every load of the pass in flight before any is used
+      vs[k] = -1;
+      xs[k] = ys[k] = 0.0f;
+      if (i0 + k < n) load(i0 + k, xs[k], ys[k], vs[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < kOrderM; ++k) {
+      q[k] = -1;
+      if (i0 + k >= n) continue;
+      if (save) {
+        save[i0 + k] = __float_as_int(xs[k]);
+        save[n + i0 + k] = __float_as_int(ys[k]);
+        save[2 * n + i0 + k] = vs[k];
+      }
+      if (vs[k] >= 0)
+        for (int r = 0; r < world; ++r)
+          if (ys[k] >= E.e[r] && ys[k] < E.e[r + 1]) {
+            q[k] = r;
+            break;
+          }
+      if (q[k] < 0) code[i0 + k] = -1;
+    }
+    for (int r = 0; r < world; ++r) {
+      int c = 0;
+#pragma unroll
+      for (int k = 0; k < kOrderM; ++k) c += q[k] == r;
+      const int incl = wave_incl_scan(c, lane);
+      if (lane == 63) sh.wtot[r][wave] = incl;
+      __syncthreads();
+      int at = sh.base[r] + incl - c;
+      for (int w = 0; w < wave; ++w) at += sh.wtot[r][w];
+#pragma unroll
+      for (int k = 0; k < kOrderM; ++k)
+        if (q[k] == r) code[i0 + k] = (r << 24) | at++;
+    }
+    __syncthreads();
+    if (tid < world) {
+      int t = sh.base[tid];
+      for (int w = 0; w < NW; ++w) t += sh.wtot[tid][w];
+      sh.base[tid] = t;
+    }
+    __syncthreads();
   }
   if (tid < world) {
-    int t = 0;
-    for (int w = 0; w < NW; ++w) t += sh.wc[w][tid];
-    blk[(long)b * world + tid] = t;
+    counts[tid] = sh.base[tid];
+    if (host_counts) host_counts[tid] = sh.base[tid];
   }
-  __threadfence();  // this block's counts (and every read of the previous order) before its arrival
-  __syncthreads();
-  if (tid == 0) sh.last = atomicAdd(done, 1) == nb - 1;
-  __syncthreads();
-  if (!sh.last) return;
-  __threadfence();  // every block's counts are visible to the last one
-  if (tid < world) {  // rank tid's places: block counts read 16 at a time
-    int acc = 0;
-    for (int b0 = 0; b0 < nb; b0 += 16) {
-      int t[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) t[k] = b0 + k < nb ? blk[(long)(b0 + k) * world + tid] : 0;
-#pragma unroll
-      for (int k = 0; k < 16; ++k)
-        if (b0 + k < nb) {
-          pre[(long)(b0 + k) * world + tid] = acc;
-          acc += t[k];
-        }
-    }
-    counts[tid] = acc;
-    if (host_counts) host_counts[tid] = acc;
-  }
-  if (tid == 0) *done = 0;  // ready for the next launch
 }
 
-__global__ __launch_bounds__(kOrderBlock) void k_gather_order(const float *__restrict__ x0,
-                                                              const float *__restrict__ y0,
-                                                              const int *__restrict__ v0, int n, GatherEdges E,
-                                                              int *__restrict__ work, int *__restrict__ save,
-                                                              int *__restrict__ escape,
-                                                              int *__restrict__ host_counts) {
+__global__ __launch_bounds__(kOrderThreads) void k_gather_order(const float *__restrict__ x0,
+                                                                const float *__restrict__ y0,
+                                                                const int *__restrict__ v0, int n, GatherEdges E,
+                                                                int *__restrict__ work, int *__restrict__ save,
+                                                                int *__restrict__ escape,
+                                                                int *__restrict__ host_counts) {
   __builtin_amdgcn_s_setprio(3);  // between two trackers: issue ahead of co-resident pyramid waves
   __shared__ OrderShared sh;
-  const int i = blockIdx.x * kOrderBlock + threadIdx.x;
-  if (blockIdx.x == 0 && threadIdx.x == 0 && escape) *escape = 0;
-  const bool valid = i < n;
-  const float x = valid && save ? x0[i] : 0.0f, y = valid ? y0[i] : 0.0f;
-  const int v = valid ? v0[i] : -1;
-  order_core(sh, n, E, work, i, valid, x, y, v, save, host_counts);
+  if (threadIdx.x == 0 && escape) *escape = 0;
+  order_pass_all(sh, n, E, work, work + n, save, host_counts, [&](int i, float &x, float &y, int &v) {
+    x = save ? x0[i] : 0.0f;
+    y = y0[i];
+    v = v0[i];
+  });
 }
 
-// gather_unpack and the next chunk's gather_order in one launch: feature i
-// from its owner's slot (the order that packed it: code and places read before
-// this block arrives), then its new ownership (the order the next exchange
-// uses) from the merged state
-__global__ __launch_bounds__(kOrderBlock) void k_gather_unpack_order(
+// gather_unpack and the next chunk's gather_order in one launch: each feature
+// from its owner's slot (at the place the previous order gave it), then the
+// ownership of the merged state.  One workgroup reads and rewrites `code`
+// feature by feature, so no place is read after it is rewritten.
+__global__ __launch_bounds__(kOrderThreads) void k_gather_unpack_order(
     const int *__restrict__ slots, int nslots, int r0, int n, int S, float *__restrict__ x, float *__restrict__ y,
     int *__restrict__ v, int *__restrict__ flags, int *__restrict__ host_flags, GatherEdges E, int *__restrict__ work,
     int *__restrict__ save, int *__restrict__ escape, int *__restrict__ host_counts) {
   __builtin_amdgcn_s_setprio(3);  // between two trackers: issue ahead of co-resident pyramid waves
   __shared__ OrderShared sh;
-  const int world = E.world, nb = (n + kOrderBlock - 1) / kOrderBlock;
-  const int *pre = work + n + world;
-  const int i = blockIdx.x * kOrderBlock + threadIdx.x;
   const long words = kGatherHdr + 3L * S;
   int esc = 0, bad = 0;
   for (int k = 0; k < nslots; ++k) {
@@ -258,7 +256,7 @@ __global__ __launch_bounds__(kOrderBlock) void k_gather_unpack_order(
     esc += h[0];
     bad += h[1] + (h[2] > S || h[3] != S ? 1 : 0);
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (threadIdx.x == 0) {
     flags[0] = esc;
     flags[1] = bad;
     if (host_flags) {
@@ -267,40 +265,35 @@ __global__ __launch_bounds__(kOrderBlock) void k_gather_unpack_order(
     }
     if (escape) *escape = 0;
   }
-  const bool valid = i < n;
-  float xi = 0.0f, yi = 0.0f;
-  int vi = -1;
-  if (valid) {
-    xi = x[i];
-    yi = y[i];
-    vi = v[i];
+  order_pass_all(sh, n, E, work, work + n, save, host_counts, [&](int i, float &xi, float &yi, int &vi) {
     const int c = work[i];
     const int q = c >> 24, k = q - r0;
     if (!bad && c >= 0 && k >= 0 && k < nslots) {
       const int *sl = slots + k * words + kGatherHdr;
-      const int p = pre[(long)blockIdx.x * world + q] + (c & 0xFFFFFF);
+      const int p = c & 0xFFFFFF;
       xi = __int_as_float(sl[p]);
       yi = __int_as_float(sl[S + p]);
       vi = sl[2 * S + p];
       x[i] = xi;
       y[i] = yi;
       v[i] = vi;
+    } else {
+      xi = x[i];
+      yi = y[i];
+      vi = v[i];
     }
-  }
-  (void)nb;
-  order_core(sh, n, E, work, i, valid, xi, yi, vi, save, host_counts);
+  });
 }
 
 __global__ void k_gather_pack(const float *__restrict__ x, const float *__restrict__ y, const int *__restrict__ v,
-                              const int *__restrict__ code, const int *__restrict__ counts,
-                              const int *__restrict__ pre, int n, int world, int rank,
+                              const int *__restrict__ code, const int *__restrict__ counts, int n, int world, int rank,
                               const int *__restrict__ escape, int nfail, int *__restrict__ slot, int S) {
   __builtin_amdgcn_s_setprio(3);
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
     const int c = code[i];
     if (c >= 0 && (c >> 24) == rank) {
-      const int p = pre[(long)(i / kOrderBlock) * world + rank] + (c & 0xFFFFFF);
+      const int p = c & 0xFFFFFF;
       if (p < S) {
         slot[kGatherHdr + p] = __float_as_int(x[i]);
         slot[kGatherHdr + S + p] = __float_as_int(y[i]);
@@ -320,7 +313,7 @@ __global__ void k_gather_pack(const float *__restrict__ x, const float *__restri
 // they are.  flags[0]: the escape flags summed, flags[1]: failures (a slot too
 // short for its count is one); nothing is unpacked when flags[1] != 0.
 __global__ void k_gather_unpack(const int *__restrict__ slots, int nslots, int r0, const int *__restrict__ code,
-                                const int *__restrict__ pre, int n, int world, int S, float *__restrict__ x,
+                                int n, int world, int S, float *__restrict__ x,
                                 float *__restrict__ y, int *__restrict__ v, int *__restrict__ flags,
                                 int *__restrict__ host_flags) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -344,7 +337,7 @@ __global__ void k_gather_unpack(const int *__restrict__ slots, int nslots, int r
   if (c < 0) return;
   const int q = c >> 24, k = q - r0;
   if (k < 0 || k >= nslots) return;
-  const int *sl = slots + k * words + kGatherHdr, p = pre[(long)(i / kOrderBlock) * world + q] + (c & 0xFFFFFF);
+  const int *sl = slots + k * words + kGatherHdr, p = c & 0xFFFFFF;
   x[i] = __int_as_float(sl[p]);
   y[i] = __int_as_float(sl[S + p]);
   v[i] = sl[2 * S + p];
@@ -448,8 +441,7 @@ KLT_API int klt_hip_gather_order(klt_hip_ctx *ctx, const float *x0, const float 
   GatherEdges E{};
   for (int r = 0; r <= world; ++r) E.e[r] = edges[r];
   E.world = world;
-  const int nb = n > 0 ? (n + kOrderBlock - 1) / kOrderBlock : 1;
-  hipLaunchKernelGGL(k_gather_order, dim3(nb), dim3(kOrderBlock), 0, (hipStream_t)klt_hip_get_stream(ctx), x0, y0,
+  hipLaunchKernelGGL(k_gather_order, dim3(1), dim3(kOrderThreads), 0, (hipStream_t)klt_hip_get_stream(ctx), x0, y0,
                      v0, n, E, work, save, escape, host_counts);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : kltdev::ctx_fail(ctx, "gather_order: %s", hipGetErrorString(e));
@@ -464,7 +456,7 @@ KLT_API int klt_hip_gather_pack(klt_hip_ctx *ctx, const float *x, const float *y
   if (hipSetDevice(klt_hip_ctx_device(ctx)) != hipSuccess) return kltdev::ctx_fail(ctx, "gather_pack: device");
   const int nb = n > 0 ? (n + 255) / 256 : 1;
   hipLaunchKernelGGL(k_gather_pack, dim3(nb), dim3(256), 0, (hipStream_t)klt_hip_get_stream(ctx), x, y, val, work,
-                     work + n, work + n + world, n, world, rank, escape, nfail, slot, S);
+                     work + n, n, world, rank, escape, nfail, slot, S);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : kltdev::ctx_fail(ctx, "gather_pack: %s", hipGetErrorString(e));
 }
@@ -479,7 +471,7 @@ KLT_API int klt_hip_gather_unpack(klt_hip_ctx *ctx, const int *slots, int nslots
   if (hipSetDevice(klt_hip_ctx_device(ctx)) != hipSuccess) return kltdev::ctx_fail(ctx, "gather_unpack: device");
   const int nb = n > 0 ? (n + 255) / 256 : 1;
   hipLaunchKernelGGL(k_gather_unpack, dim3(nb), dim3(256), 0, (hipStream_t)klt_hip_get_stream(ctx), slots, nslots,
-                     first_rank, work, work + n + world, n, world, S, x, y, val, flags, host_flags);
+                     first_rank, work, n, world, S, x, y, val, flags, host_flags);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : kltdev::ctx_fail(ctx, "gather_unpack: %s", hipGetErrorString(e));
 }
@@ -496,8 +488,7 @@ KLT_API int klt_hip_gather_unpack_order(klt_hip_ctx *ctx, const int *slots, int 
   GatherEdges E{};
   for (int r = 0; r <= world; ++r) E.e[r] = edges[r];
   E.world = world;
-  const int nb = n > 0 ? (n + kOrderBlock - 1) / kOrderBlock : 1;
-  hipLaunchKernelGGL(k_gather_unpack_order, dim3(nb), dim3(kOrderBlock), 0, (hipStream_t)klt_hip_get_stream(ctx),
+  hipLaunchKernelGGL(k_gather_unpack_order, dim3(1), dim3(kOrderThreads), 0, (hipStream_t)klt_hip_get_stream(ctx),
                      slots, nslots, first_rank, n, S, x, y, val, flags, host_flags, E, work, save, escape,
                      host_counts);
   const hipError_t e = hipGetLastError();
