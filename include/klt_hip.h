@@ -320,10 +320,11 @@ int klt_hip_track_frames_host(klt_hip_ctx *ctx, const klt_hip_pyr_desc *pdesc,
    uses them.  Needs the default (fused) pyramid parameters. */
 /* band calls of this context: ready != 0 promises that next_frames are ready
    when each call is made (device-resident, not written by work still queued on
-   the context's stream), so the build-ahead waits only for its bank and starts
-   as soon as the tracker that last read that bank ends, instead of behind
-   everything the caller queued before the call (its exchange).  Default 0;
-   kltamd.shard.ShardedSequence sets it (its frames are loaded up front). */
+   the context's stream), so the build-ahead waits for its bank and starts with
+   this chunk's tracker instead of behind everything the caller queued before
+   the call (its exchange) -- the short kernels between two trackers then run
+   alone.  Default 0; kltamd.shard.ShardedSequence sets it (its frames are
+   loaded up front). */
 int klt_hip_set_ahead_ready(klt_hip_ctx *ctx, int ready);
 int klt_hip_track_frames_band(klt_hip_ctx *ctx, const klt_hip_pyr_desc *pdesc,
                               const klt_hip_track_desc *tdesc, const unsigned char *frames, long pitch,

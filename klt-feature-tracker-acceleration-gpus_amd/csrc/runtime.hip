@@ -221,9 +221,11 @@ struct klt_hip_ctx {
   const char *track_kernel = nullptr;  // instance name of the last tracker launch (klt_hip_track_kernel)
   // band calls: 1 = the next chunk's frames are ready when the call is made
   // (not written by work still queued on the tracking stream), so its
-  // build-ahead waits only for its bank to be free, not for everything queued
-  // before the call (klt_hip_set_ahead_ready)
+  // build-ahead waits for its bank and for this chunk's processing order
+  // (ev_go: the pyramids start with the tracker) -- not for whatever the
+  // caller queues between two chunks (klt_hip_set_ahead_ready)
   int ahead_ready = 0;
+  hipEvent_t ev_go = nullptr;
   int serial_frames = 1;  // klt_hip_track_frames: 1 builds and tracks on one stream (default: the
                           // tracker and the pyramid kernels compete for the same CUs; overlap buys ~3 %)
   int *d_perm = nullptr;
@@ -1100,6 +1102,7 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
   }
   if (c->ev_start) hipEventDestroy(c->ev_start);
   if (c->ev_caller) hipEventDestroy(c->ev_caller);
+  if (c->ev_go) hipEventDestroy(c->ev_go);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
 }
@@ -1979,9 +1982,12 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
   const bool serial = band ? false : (c->serial_frames != 0 || nframes <= chunk);
   // the pyramid stream starts behind everything already queued on the
   // tracking stream -- except a band call's build-ahead when the caller has
-  // said its frames are ready (klt_hip_set_ahead_ready): that waits only for
-  // its bank, and the build starts as soon as the tracker that last read the
-  // bank ends, not after the caller's exchange between two chunks
+  // said its frames are ready (klt_hip_set_ahead_ready): that waits for its
+  // bank and starts with this chunk's tracker (ev_go), so the short kernels
+  // between two trackers (the processing order; the caller's exchange before
+  // the call) run without pyramid waves beside them -- each of them is on the
+  // chain, and measured 3-10x slower with k_pyr_l0 filling the CUs
+  // (profiles/r05_rank_timeline_*.txt)
   bool pwait = false;
   auto pstream_behind = [&]() -> int {
     if (serial || pwait) return 0;
@@ -2055,6 +2061,10 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
       b.tv = tab_val + (long)j0 * tab_stride;
       b.tstride = tab_stride;
     }
+    if (band && c->ahead_ready) {
+      if (!c->ev_go) HIPCHK(c, hipEventCreateWithFlags(&c->ev_go, hipEventDisableTiming));
+      HIPCHK(c, hipEventRecord(c->ev_go, c->stream));
+    }
     if (n > 0 && track_frames_launch(c, c->stream, td, a, b, x, y, val, n, band ? band->own : nullptr, true))
       return -1;
     HMARK("track");
@@ -2067,6 +2077,7 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     const int bj = c->bank_next;
     const int Fn = band->next_n < chunk ? band->next_n : chunk;
     HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_bfree[bj], 0));
+    if (c->ahead_ready && !pwait) HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_go, 0));
     int p0 = 0, p1 = 1 << 30;
     band_planes(*band, p0, p1);
     if (build_fused_bank(c, c->bank[bj], pd, band->next, pitch, stride, Fn, c->pstream, band->row_lo, band->row_hi,
