@@ -396,7 +396,7 @@ int klt_hip_select_map(klt_hip_ctx *ctx, int ncols, int nrows, const klt_hip_sel
    them are left as they are) and writes flags[0] = the escape flags summed,
    flags[1] = the failures summed (a slot shorter than its count counts as
    one; nothing is unpacked then).  All three queue on the context's stream. */
-#define KLT_HIP_GATHER_MAX_RANKS 64
+#define KLT_HIP_GATHER_MAX_RANKS 16
 #define KLT_HIP_GATHER_SLOT_WORDS(S) (4 + 3 * (long)(S))
 /* gather_order options, each may be NULL: save (device int[3n]) receives a
    copy of x0 | y0 | v0 bit patterns (the chunk-start state a redo restarts

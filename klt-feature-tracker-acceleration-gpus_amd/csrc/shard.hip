@@ -130,92 +130,113 @@ struct GatherEdges {
 
 // k_gather_order: ONE workgroup of 1024 threads (no cross-workgroup
 // handshake: on gfx950 that takes device-scope fences, which write back and
-// invalidate L2 -- tens of us while a pyramid kernel streams beside it).  In
-// passes of 1024 * kOrderM features, thread t takes the contiguous features
-// [t*M, t*M + M) of the pass, loads them all at once and finds their owners;
-// then for each rank r in turn: the thread's count of r, a wave scan, the
-// waves' totals through LDS (one barrier), and every feature of r gets its
-// place -- in index order, since features of lower threads have lower
-// indices.  This kernel sits between two chunks' trackers: its latency is
-// the chain's.  save (optional): x0/y0/v0 also copied to save[0..3n) (the
-// redo's start state) and *escape zeroed; host_counts (optional, pinned host
-// memory): the counts written there too, read behind an event with no
-// copy-engine hand-off on the stream.  work: code[n] | counts[world].
-constexpr int kOrderThreads = 1024, kOrderM = 20;  // 20 480 features a pass (config 4 in one)
+// invalidate L2).  Features go in rounds of 1024 (round k: [1024k, 1024k+1024),
+// lane order = index order), kOrderR rounds at a time, every load coalesced
+// and in flight before any is used.  Per round a wave finds, for each lane,
+// the lanes with the same owner from one ballot per owner bit (AND of the
+// bit masks), so its place within the wave is one popcount; lanes 0..world-1
+// count each owner's lanes the same way.  Three barriers per batch turn the
+// waves' counts into places (rounds before, waves before, lanes before): the
+// owner's features in index order.  This kernel sits between two chunks'
+// trackers: its latency is the chain's.  save (optional): x0/y0/v0 also
+// copied to save[0..3n) (the redo's start state) and *escape zeroed;
+// host_counts (optional, pinned host memory): the counts written there too,
+// read behind an event with no copy-engine hand-off on the stream.
+// work: code[n] | counts[world].
+constexpr int kOrderThreads = 1024, kOrderR = 20;  // 20 480 features a batch (config 4 in one)
+constexpr int kOrderWaves = kOrderThreads / 64;
 
 __host__ __device__ inline long gather_work_ints(int n, int world) { return (long)n + world; }
 
 struct OrderShared {
-  int wtot[KLT_HIP_GATHER_MAX_RANKS][kOrderThreads / 64];
-  int base[KLT_HIP_GATHER_MAX_RANKS];
+  int wpre[kOrderR][kOrderWaves][KLT_HIP_GATHER_MAX_RANKS];  // a wave's count, then the waves' before it
+  int pre[kOrderR][KLT_HIP_GATHER_MAX_RANKS];                // the owner's features of earlier rounds
+  int base[KLT_HIP_GATHER_MAX_RANKS];                        // ... and of earlier batches
 };
 
-__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int o = __shfl_up(v, d, 64);
-    if (lane >= d) v += o;
-  }
-  return v;
-}
-
-// LOAD(i, x, y, v): feature i's chunk-start values (i < n); MERGE: unpack first
+// Load(i, x, y, v): feature i's chunk-start values
 template <class Load>
-__device__ __forceinline__ void order_pass_all(OrderShared &sh, int n, const GatherEdges &E, int *__restrict__ code,
-                                               int *__restrict__ counts, int *__restrict__ save,
-                                               int *__restrict__ host_counts, Load load) {
+__device__ __forceinline__ void order_all(OrderShared &sh, int n, const GatherEdges &E, int *__restrict__ code,
+                                          int *__restrict__ counts, int *__restrict__ save,
+                                          int *__restrict__ host_counts, Load load) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, world = E.world;
-  constexpr int NW = kOrderThreads / 64;
+  int nbits = 0;
+  while ((1 << nbits) <= world) ++nbits;  // owner codes 0..world-1, and 2^nbits - 1 = nobody
+  const int nobody = (1 << nbits) - 1;
+  const unsigned long long lt = (1ull << lane) - 1ull;
   if (tid < world) sh.base[tid] = 0;
   __syncthreads();
-  for (int p0 = 0; p0 < n; p0 += kOrderThreads * kOrderM) {
-    const int i0 = p0 + tid * kOrderM;
-    int q[kOrderM];
-    float xs[kOrderM], ys[kOrderM];
-    int vs[kOrderM];
+  for (int p0 = 0; p0 < n; p0 += kOrderThreads * kOrderR) {
+    int q[kOrderR], mine[kOrderR];
+    {
+      float xs[kOrderR], ys[kOrderR];
+      int vs[kOrderR];
 #pragma unroll
-    for (int k = 0; k < kOrderM; ++k) {  // every load of the pass in flight before any is used
-      vs[k] = -1;
-      xs[k] = ys[k] = 0.0f;
-      if (i0 + k < n) load(i0 + k, xs[k], ys[k], vs[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < kOrderM; ++k) {
-      q[k] = -1;
-      if (i0 + k >= n) continue;
-      if (save) {
-        save[i0 + k] = __float_as_int(xs[k]);
-        save[n + i0 + k] = __float_as_int(ys[k]);
-        save[2 * n + i0 + k] = vs[k];
+      for (int k = 0; k < kOrderR; ++k) {  // every load of the batch in flight before any is used
+        const int i = p0 + k * kOrderThreads + tid;
+        vs[k] = -1;
+        xs[k] = ys[k] = 0.0f;
+        if (i < n) load(i, xs[k], ys[k], vs[k]);
       }
-      if (vs[k] >= 0)
-        for (int r = 0; r < world; ++r)
-          if (ys[k] >= E.e[r] && ys[k] < E.e[r + 1]) {
-            q[k] = r;
-            break;
-          }
-      if (q[k] < 0) code[i0 + k] = -1;
+#pragma unroll
+      for (int k = 0; k < kOrderR; ++k) {
+        const int i = p0 + k * kOrderThreads + tid;
+        q[k] = nobody;
+        if (i >= n) continue;
+        if (save) {
+          save[i] = __float_as_int(xs[k]);
+          save[n + i] = __float_as_int(ys[k]);
+          save[2 * n + i] = vs[k];
+        }
+        if (vs[k] >= 0)
+          for (int r = 0; r < world; ++r)
+            if (ys[k] >= E.e[r] && ys[k] < E.e[r + 1]) {
+              q[k] = r;
+              break;
+            }
+      }
     }
-    for (int r = 0; r < world; ++r) {
-      int c = 0;
 #pragma unroll
-      for (int k = 0; k < kOrderM; ++k) c += q[k] == r;
-      const int incl = wave_incl_scan(c, lane);
-      if (lane == 63) sh.wtot[r][wave] = incl;
-      __syncthreads();
-      int at = sh.base[r] + incl - c;
-      for (int w = 0; w < wave; ++w) at += sh.wtot[r][w];
-#pragma unroll
-      for (int k = 0; k < kOrderM; ++k)
-        if (q[k] == r) code[i0 + k] = (r << 24) | at++;
+    for (int k = 0; k < kOrderR; ++k) {
+      unsigned long long same = ~0ull, mr = ~0ull;
+      for (int j = 0; j < nbits; ++j) {
+        const unsigned long long b = __ballot((q[k] >> j) & 1);
+        same &= ((q[k] >> j) & 1) ? b : ~b;
+        mr &= ((lane >> j) & 1) ? b : ~b;  // lane r < world: the lanes owned by rank r
+      }
+      mine[k] = __popcll(same & lt);
+      if (lane < world) sh.wpre[k][wave][lane] = __popcll(mr);
     }
     __syncthreads();
-    if (tid < world) {
-      int t = sh.base[tid];
-      for (int w = 0; w < NW; ++w) t += sh.wtot[tid][w];
-      sh.base[tid] = t;
+    // waves' counts -> counts of the waves before; round totals
+    if (tid < kOrderR * world) {
+      const int k = tid / world, r = tid - k * world;
+      int acc = 0;
+      for (int w = 0; w < kOrderWaves; ++w) {
+        const int c = sh.wpre[k][w][r];
+        sh.wpre[k][w][r] = acc;
+        acc += c;
+      }
+      sh.pre[k][r] = acc;  // this round's total, for now
     }
     __syncthreads();
+    if (tid < world) {  // rounds before, and earlier batches
+      int acc = sh.base[tid];
+      for (int k = 0; k < kOrderR; ++k) {
+        const int t = sh.pre[k][tid];
+        sh.pre[k][tid] = acc;
+        acc += t;
+      }
+      sh.base[tid] = acc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kOrderR; ++k) {
+      const int i = p0 + k * kOrderThreads + tid;
+      if (i >= n) continue;
+      code[i] = q[k] == nobody ? -1 : ((q[k] << 24) | (sh.pre[k][q[k]] + sh.wpre[k][wave][q[k]] + mine[k]));
+    }
+    __syncthreads();  // the next batch rewrites wpre / pre
   }
   if (tid < world) {
     counts[tid] = sh.base[tid];
@@ -232,7 +253,7 @@ __global__ __launch_bounds__(kOrderThreads) void k_gather_order(const float *__r
   __builtin_amdgcn_s_setprio(3);  // between two trackers: issue ahead of co-resident pyramid waves
   __shared__ OrderShared sh;
   if (threadIdx.x == 0 && escape) *escape = 0;
-  order_pass_all(sh, n, E, work, work + n, save, host_counts, [&](int i, float &x, float &y, int &v) {
+  order_all(sh, n, E, work, work + n, save, host_counts, [&](int i, float &x, float &y, int &v) {
     x = save ? x0[i] : 0.0f;
     y = y0[i];
     v = v0[i];
@@ -265,7 +286,7 @@ __global__ __launch_bounds__(kOrderThreads) void k_gather_unpack_order(
     }
     if (escape) *escape = 0;
   }
-  order_pass_all(sh, n, E, work, work + n, save, host_counts, [&](int i, float &xi, float &yi, int &vi) {
+  order_all(sh, n, E, work, work + n, save, host_counts, [&](int i, float &xi, float &yi, int &vi) {
     const int c = work[i];
     const int q = c >> 24, k = q - r0;
     if (!bad && c >= 0 && k >= 0 && k < nslots) {
