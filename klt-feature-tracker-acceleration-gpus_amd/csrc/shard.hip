@@ -143,7 +143,7 @@ struct GatherEdges {
 // host_counts (optional, pinned host memory): the counts written there too,
 // read behind an event with no copy-engine hand-off on the stream.
 // work: code[n] | counts[world].
-constexpr int kOrderThreads = 1024, kOrderR = 20;  // 20 480 features a batch (config 4 in one)
+constexpr int kOrderThreads = 1024, kOrderR = 16;  // 16 384 features a batch
 constexpr int kOrderWaves = kOrderThreads / 64;
 
 __host__ __device__ inline long gather_work_ints(int n, int world) { return (long)n + world; }
@@ -154,11 +154,21 @@ struct OrderShared {
   int base[KLT_HIP_GATHER_MAX_RANKS];                        // ... and of earlier batches
 };
 
-// Load(i, x, y, v): feature i's chunk-start values
-template <class Load>
+// The chunk-start state: (x0, y0, v0) as they are; UNPACK: feature i from its
+// owner's slot first (U.slots ..., at the place code[i] holds), written back
+// to (x0, y0, v0).  Every load of a batch is issued before any is used: first
+// all the codes, then all the slot words (no store in between)
+struct Unpack {
+  const int *slots;
+  int nslots, r0, S, bad;
+  long words;
+};
+
+template <bool UNPACK>
 __device__ __forceinline__ void order_all(OrderShared &sh, int n, const GatherEdges &E, int *__restrict__ code,
-                                          int *__restrict__ counts, int *__restrict__ save,
-                                          int *__restrict__ host_counts, Load load) {
+                                          int *__restrict__ counts, float *__restrict__ x0, float *__restrict__ y0,
+                                          int *__restrict__ v0, int *__restrict__ save, int *__restrict__ host_counts,
+                                          const Unpack U) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, world = E.world;
   int nbits = 0;
   while ((1 << nbits) <= world) ++nbits;  // owner codes 0..world-1, and 2^nbits - 1 = nobody
@@ -171,12 +181,47 @@ __device__ __forceinline__ void order_all(OrderShared &sh, int n, const GatherEd
     {
       float xs[kOrderR], ys[kOrderR];
       int vs[kOrderR];
+      int src[kOrderR];  // UNPACK: the slot word of feature i's x, or -1 (keep its values)
+      if (UNPACK) {
+#pragma unroll
+        for (int k = 0; k < kOrderR; ++k) {
+          const int i = p0 + k * kOrderThreads + tid;
+          src[k] = i < n ? code[i] : -1;
+        }
+#pragma unroll
+        for (int k = 0; k < kOrderR; ++k) {
+          const int c = src[k], kk = (c >> 24) - U.r0;
+          src[k] = (!U.bad && c >= 0 && kk >= 0 && kk < U.nslots) ? (int)(kk * U.words + kGatherHdr + (c & 0xFFFFFF))
+                                                                : -1;
+        }
+      }
 #pragma unroll
       for (int k = 0; k < kOrderR; ++k) {  // every load of the batch in flight before any is used
         const int i = p0 + k * kOrderThreads + tid;
         vs[k] = -1;
         xs[k] = ys[k] = 0.0f;
-        if (i < n) load(i, xs[k], ys[k], vs[k]);
+        if (i >= n) continue;
+        if (UNPACK && src[k] >= 0) {
+          xs[k] = __int_as_float(U.slots[src[k]]);
+          ys[k] = __int_as_float(U.slots[src[k] + U.S]);
+          vs[k] = U.slots[src[k] + 2 * U.S];
+        } else {
+          if (!UNPACK && save) xs[k] = x0[i];
+          if (UNPACK) xs[k] = x0[i];
+          ys[k] = y0[i];
+          vs[k] = v0[i];
+        }
+      }
+      if (UNPACK) {
+#pragma unroll
+        for (int k = 0; k < kOrderR; ++k) {
+          const int i = p0 + k * kOrderThreads + tid;
+          if (i < n && src[k] >= 0) {
+            x0[i] = xs[k];
+            y0[i] = ys[k];
+            v0[i] = vs[k];
+          }
+        }
       }
 #pragma unroll
       for (int k = 0; k < kOrderR; ++k) {
@@ -253,11 +298,8 @@ __global__ __launch_bounds__(kOrderThreads) void k_gather_order(const float *__r
   __builtin_amdgcn_s_setprio(3);  // between two trackers: issue ahead of co-resident pyramid waves
   __shared__ OrderShared sh;
   if (threadIdx.x == 0 && escape) *escape = 0;
-  order_all(sh, n, E, work, work + n, save, host_counts, [&](int i, float &x, float &y, int &v) {
-    x = save ? x0[i] : 0.0f;
-    y = y0[i];
-    v = v0[i];
-  });
+  order_all<false>(sh, n, E, work, work + n, const_cast<float *>(x0), const_cast<float *>(y0),
+                   const_cast<int *>(v0), save, host_counts, Unpack{});
 }
 
 // gather_unpack and the next chunk's gather_order in one launch: each feature
@@ -286,24 +328,7 @@ __global__ __launch_bounds__(kOrderThreads) void k_gather_unpack_order(
     }
     if (escape) *escape = 0;
   }
-  order_all(sh, n, E, work, work + n, save, host_counts, [&](int i, float &xi, float &yi, int &vi) {
-    const int c = work[i];
-    const int q = c >> 24, k = q - r0;
-    if (!bad && c >= 0 && k >= 0 && k < nslots) {
-      const int *sl = slots + k * words + kGatherHdr;
-      const int p = c & 0xFFFFFF;
-      xi = __int_as_float(sl[p]);
-      yi = __int_as_float(sl[S + p]);
-      vi = sl[2 * S + p];
-      x[i] = xi;
-      y[i] = yi;
-      v[i] = vi;
-    } else {
-      xi = x[i];
-      yi = y[i];
-      vi = v[i];
-    }
-  });
+  order_all<true>(sh, n, E, work, work + n, x, y, v, save, host_counts, Unpack{slots, nslots, r0, S, bad, words});
 }
 
 __global__ void k_gather_pack(const float *__restrict__ x, const float *__restrict__ y, const int *__restrict__ v,
