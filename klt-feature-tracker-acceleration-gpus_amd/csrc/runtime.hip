@@ -1988,15 +1988,21 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
   // the call) run without pyramid waves beside them -- each of them is on the
   // chain, and measured 3-10x slower with k_pyr_l0 filling the CUs
   // (profiles/r05_rank_timeline_*.txt)
+  // Every event record and cross-stream wait is a packet the tracking queue
+  // processes between two trackers (several us each), so the ahead-ready
+  // band call records ev_start only when a build needs it, and no ev_bfree
+  // (its build-ahead waits for ev_go, which follows the previous tracker)
+  const bool ahead = band && c->ahead_ready;
   bool pwait = false;
   auto pstream_behind = [&]() -> int {
     if (serial || pwait) return 0;
     pwait = true;
+    if (ahead) HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_start, 0));
     return 0;
   };
-  if (!serial) HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
-  if (!(band && c->ahead_ready) && pstream_behind()) return -1;
+  if (!serial && !ahead) HIPCHK(c, hipEventRecord(c->ev_start, c->stream));
+  if (!ahead && pstream_behind()) return -1;
   const bool fz = fused_ok(pd) && !c->force_generic;
   if (band && !fz) return fail(c, "track_frames_band: needs the fused (default-parameter) pyramid path");
   // the banks' layout follows their reader: interleaved for k_track7, planes
@@ -2028,7 +2034,7 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     if (c->pre.bank == bi) c->pre.bank = -1;  // taken now, or about to be overwritten
     // one stream: stream order is the dependency (an event wait would add a queue barrier)
     if (!serial && !prebuilt && pstream_behind()) return -1;  // this chunk's own frames: behind the caller's work
-    if (!serial && !prebuilt) HIPCHK(c, hipStreamWaitEvent(ps, c->ev_bfree[bi], 0));
+    if (!serial && !prebuilt && !ahead) HIPCHK(c, hipStreamWaitEvent(ps, c->ev_bfree[bi], 0));
     if (prebuilt) {
       // ev_bbuilt[bi] was recorded after that build: the wait below orders it
     } else if (fz) {
@@ -2068,7 +2074,7 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     if (n > 0 && track_frames_launch(c, c->stream, td, a, b, x, y, val, n, band ? band->own : nullptr, true))
       return -1;
     HMARK("track");
-    if (!serial && c->prev.bank >= 0) HIPCHK(c, hipEventRecord(c->ev_bfree[c->prev.bank], c->stream));
+    if (!serial && !ahead && c->prev.bank >= 0) HIPCHK(c, hipEventRecord(c->ev_bfree[c->prev.bank], c->stream));
     c->prev = PrevRef{bi, Fc - 1};
   }
   if (band && band->next && band->next_n > 0 && fz) {
@@ -2076,8 +2082,11 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     // pyramid stream: they depend on frames only, not on this chunk's result
     const int bj = c->bank_next;
     const int Fn = band->next_n < chunk ? band->next_n : chunk;
-    HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_bfree[bj], 0));
-    if (c->ahead_ready && !pwait) HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_go, 0));
+    if (c->ahead_ready) {  // with this chunk's tracker, so after the previous one: bank bj is free
+      if (!pwait) HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_go, 0));
+    } else {
+      HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_bfree[bj], 0));
+    }
     int p0 = 0, p1 = 1 << 30;
     band_planes(*band, p0, p1);
     if (build_fused_bank(c, c->bank[bj], pd, band->next, pitch, stride, Fn, c->pstream, band->row_lo, band->row_hi,
