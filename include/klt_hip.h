@@ -400,7 +400,8 @@ int klt_hip_select_map(klt_hip_ctx *ctx, int ncols, int nrows, const klt_hip_sel
 #define KLT_HIP_GATHER_SLOT_WORDS(S) (4 + 3 * (long)(S))
 /* gather_order options, each may be NULL: save (device int[3n]) receives a
    copy of x0 | y0 | v0 bit patterns (the chunk-start state a redo restarts
-   from; needs x0) and *escape (device int) is zeroed, in the same launch;
+   from; needs x0) and *escape (device int) is zeroed, in the same launches
+   (two: per-block counts, then places; no cross-workgroup handshake);
    host_counts (pinned host int[world]) and gather_unpack's host_flags (pinned
    host int[2]) receive the counts / flags from the kernels themselves, to be
    read once an event recorded after the launch has completed */
@@ -412,7 +413,7 @@ int klt_hip_gather_pack(klt_hip_ctx *ctx, const float *x, const float *y, const 
 int klt_hip_gather_unpack(klt_hip_ctx *ctx, const int *slots, int nslots, int first_rank, const int *work, int n,
                           int world, int S, float *x, float *y, int *val, int *flags, int *host_flags);
 /* gather_unpack then gather_order of the merged state (the next chunk's
-   ownership, save, escape reset, counts) in one launch -- the step between
+   ownership, save, escape reset, counts) in two launches -- the step between
    two chunks' trackers; work is read for the unpack and rewritten */
 int klt_hip_gather_unpack_order(klt_hip_ctx *ctx, const int *slots, int nslots, int first_rank, int *work, int n,
                                 int world, int S, float *x, float *y, int *val, int *flags, int *host_flags,

@@ -114,7 +114,7 @@ __global__ void k_shard_save(const float *__restrict__ x, const float *__restric
 // holds the same chunk-start state and the same band edges, so every rank
 // knows, for every live feature, its owner q (edges[q] <= y0 < edges[q+1],
 // k_band_order's test) and its place p among q's features in index order
-// (k_gather_order: code = q << 24 | p, counts[q]).  Rank q packs its owned
+// (k_gather_count + k_gather_place: code = q << 24 | p, counts[q]).  Rank q packs its owned
 // features' (x, y, val) bit patterns at places 0 .. counts[q]-1 of its slot
 // (k_gather_pack), the slots are all-gathered, and every rank takes each
 // feature from its owner's slot (k_gather_unpack).  Lost features are nobody's
@@ -128,36 +128,34 @@ struct GatherEdges {
   int world;
 };
 
-// k_gather_order: ONE workgroup of 1024 threads (no cross-workgroup
-// handshake: on gfx950 that takes device-scope fences, which write back and
-// invalidate L2).  Features go in rounds of 1024 (round k: [1024k, 1024k+1024),
-// lane order = index order), kOrderR rounds at a time, every load coalesced
-// and in flight before any is used.  Per round a wave finds, for each lane,
-// the lanes with the same owner from one ballot per owner bit (AND of the
-// bit masks), so its place within the wave is one popcount; lanes 0..world-1
-// count each owner's lanes the same way.  Three barriers per batch turn the
-// waves' counts into places (rounds before, waves before, lanes before): the
-// owner's features in index order.  This kernel sits between two chunks'
-// trackers: its latency is the chain's.  save (optional): x0/y0/v0 also
-// copied to save[0..3n) (the redo's start state) and *escape zeroed;
-// host_counts (optional, pinned host memory): the counts written there too,
-// read behind an event with no copy-engine hand-off on the stream.
-// work: code[n] | counts[world].
-constexpr int kOrderThreads = 1024, kOrderR = 16;  // 16 384 features a batch
+// The order in two launches, many workgroups each and no handshake between
+// workgroups (on gfx950 that takes device-scope fences, which write back and
+// invalidate L2 under the pyramid's traffic: the single-workgroup and
+// fence-chained versions cost 50-110 us between two trackers).  Block b owns
+// features [1024b, 1024b + 1024) in 4 rounds of 256 (lane order = index
+// order), every load coalesced and in flight before any is used.
+//  k_gather_count: each feature's owner q; per wave and round, the lanes with
+//    the same owner from one ballot per owner bit (AND of the bit masks), so a
+//    lane's place within the wave is one popcount; the 16 (round, wave) counts
+//    per owner turned into places within the block (index order); code[i] =
+//    q << 24 | that place, bcount[b][q] = the block's count of q.
+//  k_gather_place: the counts of the blocks before b added to every place of
+//    block b; the last block's sums are the totals (counts, host_counts).
+// save (optional): the state (after the unpack) also copied to save[0..3n)
+// (the redo's start state) and *escape zeroed; host_counts (optional, pinned
+// host memory): the counts written there too, read behind an event with no
+// copy-engine hand-off on the stream.  work: code[n] | counts[world] |
+// bcount[blocks][world].
+constexpr int kOrderThreads = 256, kOrderR = 4, kOrderBlock = kOrderThreads * kOrderR;
 constexpr int kOrderWaves = kOrderThreads / 64;
 
-__host__ __device__ inline long gather_work_ints(int n, int world) { return (long)n + world; }
+__host__ __device__ inline int gather_blocks(int n) { return n > 0 ? (n + kOrderBlock - 1) / kOrderBlock : 1; }
+__host__ __device__ inline long gather_work_ints(int n, int world) {
+  return (long)n + world + (long)gather_blocks(n) * world;
+}
 
-struct OrderShared {
-  int wpre[kOrderR][kOrderWaves][KLT_HIP_GATHER_MAX_RANKS];  // a wave's count, then the waves' before it
-  int pre[kOrderR][KLT_HIP_GATHER_MAX_RANKS];                // the owner's features of earlier rounds
-  int base[KLT_HIP_GATHER_MAX_RANKS];                        // ... and of earlier batches
-};
-
-// The chunk-start state: (x0, y0, v0) as they are; UNPACK: feature i from its
-// owner's slot first (U.slots ..., at the place code[i] holds), written back
-// to (x0, y0, v0).  Every load of a batch is issued before any is used: first
-// all the codes, then all the slot words (no store in between)
+// UNPACK: feature i first from its owner's slot (U.slots ..., at the place
+// code[i] holds from the previous order), written back to (x0, y0, v0).
 struct Unpack {
   const int *slots;
   int nslots, r0, S, bad;
@@ -165,153 +163,123 @@ struct Unpack {
 };
 
 template <bool UNPACK>
-__device__ __forceinline__ void order_all(OrderShared &sh, int n, const GatherEdges &E, int *__restrict__ code,
-                                          int *__restrict__ counts, float *__restrict__ x0, float *__restrict__ y0,
-                                          int *__restrict__ v0, int *__restrict__ save, int *__restrict__ host_counts,
-                                          const Unpack U) {
+__device__ __forceinline__ void count_block(int n, const GatherEdges &E, int *__restrict__ code,
+                                            int *__restrict__ bcount, float *__restrict__ x0, float *__restrict__ y0,
+                                            int *__restrict__ v0, int *__restrict__ save, const Unpack U) {
+  __shared__ int wc[kOrderR][kOrderWaves][KLT_HIP_GATHER_MAX_RANKS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, world = E.world;
+  const int p0 = blockIdx.x * kOrderBlock;
   int nbits = 0;
   while ((1 << nbits) <= world) ++nbits;  // owner codes 0..world-1, and 2^nbits - 1 = nobody
   const int nobody = (1 << nbits) - 1;
   const unsigned long long lt = (1ull << lane) - 1ull;
-  if (tid < world) sh.base[tid] = 0;
-  __syncthreads();
-  for (int p0 = 0; p0 < n; p0 += kOrderThreads * kOrderR) {
-    int q[kOrderR], mine[kOrderR];
-    {
-      float xs[kOrderR], ys[kOrderR];
-      int vs[kOrderR];
-      int src[kOrderR];  // UNPACK: the slot word of feature i's x, or -1 (keep its values)
-      if (UNPACK) {
-#pragma unroll
-        for (int k = 0; k < kOrderR; ++k) {
-          const int i = p0 + k * kOrderThreads + tid;
-          src[k] = i < n ? code[i] : -1;
-        }
-#pragma unroll
-        for (int k = 0; k < kOrderR; ++k) {
-          const int c = src[k], kk = (c >> 24) - U.r0;
-          src[k] = (!U.bad && c >= 0 && kk >= 0 && kk < U.nslots) ? (int)(kk * U.words + kGatherHdr + (c & 0xFFFFFF))
-                                                                : -1;
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < kOrderR; ++k) {  // every load of the batch in flight before any is used
-        const int i = p0 + k * kOrderThreads + tid;
-        vs[k] = -1;
-        xs[k] = ys[k] = 0.0f;
-        if (i >= n) continue;
-        if (UNPACK && src[k] >= 0) {
-          xs[k] = __int_as_float(U.slots[src[k]]);
-          ys[k] = __int_as_float(U.slots[src[k] + U.S]);
-          vs[k] = U.slots[src[k] + 2 * U.S];
-        } else {
-          if (!UNPACK && save) xs[k] = x0[i];
-          if (UNPACK) xs[k] = x0[i];
-          ys[k] = y0[i];
-          vs[k] = v0[i];
-        }
-      }
-      if (UNPACK) {
-#pragma unroll
-        for (int k = 0; k < kOrderR; ++k) {
-          const int i = p0 + k * kOrderThreads + tid;
-          if (i < n && src[k] >= 0) {
-            x0[i] = xs[k];
-            y0[i] = ys[k];
-            v0[i] = vs[k];
-          }
-        }
-      }
+  int q[kOrderR], mine[kOrderR];
+  {
+    float xs[kOrderR], ys[kOrderR];
+    int vs[kOrderR], src[kOrderR];  // UNPACK: the slot word of feature i's x, or -1 (keep its values)
+    if (UNPACK) {
 #pragma unroll
       for (int k = 0; k < kOrderR; ++k) {
         const int i = p0 + k * kOrderThreads + tid;
-        q[k] = nobody;
-        if (i >= n) continue;
-        if (save) {
-          save[i] = __float_as_int(xs[k]);
-          save[n + i] = __float_as_int(ys[k]);
-          save[2 * n + i] = vs[k];
-        }
-        if (vs[k] >= 0)
-          for (int r = 0; r < world; ++r)
-            if (ys[k] >= E.e[r] && ys[k] < E.e[r + 1]) {
-              q[k] = r;
-              break;
-            }
+        src[k] = i < n ? code[i] : -1;
+      }
+#pragma unroll
+      for (int k = 0; k < kOrderR; ++k) {
+        const int c = src[k], kk = (c >> 24) - U.r0;
+        src[k] = (!U.bad && c >= 0 && kk >= 0 && kk < U.nslots) ? (int)(kk * U.words + kGatherHdr + (c & 0xFFFFFF))
+                                                              : -1;
       }
     }
 #pragma unroll
-    for (int k = 0; k < kOrderR; ++k) {
-      unsigned long long same = ~0ull, mr = ~0ull;
-      for (int j = 0; j < nbits; ++j) {
-        const unsigned long long b = __ballot((q[k] >> j) & 1);
-        same &= ((q[k] >> j) & 1) ? b : ~b;
-        mr &= ((lane >> j) & 1) ? b : ~b;  // lane r < world: the lanes owned by rank r
+    for (int k = 0; k < kOrderR; ++k) {  // every load in flight before any is used
+      const int i = p0 + k * kOrderThreads + tid;
+      vs[k] = -1;
+      xs[k] = ys[k] = 0.0f;
+      if (i >= n) continue;
+      if (UNPACK && src[k] >= 0) {
+        xs[k] = __int_as_float(U.slots[src[k]]);
+        ys[k] = __int_as_float(U.slots[src[k] + U.S]);
+        vs[k] = U.slots[src[k] + 2 * U.S];
+      } else {
+        if (UNPACK || save) xs[k] = x0[i];
+        ys[k] = y0[i];
+        vs[k] = v0[i];
       }
-      mine[k] = __popcll(same & lt);
-      if (lane < world) sh.wpre[k][wave][lane] = __popcll(mr);
     }
-    __syncthreads();
-    // waves' counts -> counts of the waves before; round totals
-    if (tid < kOrderR * world) {
-      const int k = tid / world, r = tid - k * world;
-      int acc = 0;
-      for (int w = 0; w < kOrderWaves; ++w) {
-        const int c = sh.wpre[k][w][r];
-        sh.wpre[k][w][r] = acc;
-        acc += c;
-      }
-      sh.pre[k][r] = acc;  // this round's total, for now
-    }
-    __syncthreads();
-    if (tid < world) {  // rounds before, and earlier batches
-      int acc = sh.base[tid];
-      for (int k = 0; k < kOrderR; ++k) {
-        const int t = sh.pre[k][tid];
-        sh.pre[k][tid] = acc;
-        acc += t;
-      }
-      sh.base[tid] = acc;
-    }
-    __syncthreads();
 #pragma unroll
     for (int k = 0; k < kOrderR; ++k) {
       const int i = p0 + k * kOrderThreads + tid;
+      q[k] = nobody;
       if (i >= n) continue;
-      code[i] = q[k] == nobody ? -1 : ((q[k] << 24) | (sh.pre[k][q[k]] + sh.wpre[k][wave][q[k]] + mine[k]));
+      if (UNPACK && src[k] >= 0) {
+        x0[i] = xs[k];
+        y0[i] = ys[k];
+        v0[i] = vs[k];
+      }
+      if (save) {
+        save[i] = __float_as_int(xs[k]);
+        save[n + i] = __float_as_int(ys[k]);
+        save[2 * n + i] = vs[k];
+      }
+      if (vs[k] >= 0)
+        for (int r = 0; r < world; ++r)
+          if (ys[k] >= E.e[r] && ys[k] < E.e[r + 1]) {
+            q[k] = r;
+            break;
+          }
     }
-    __syncthreads();  // the next batch rewrites wpre / pre
   }
-  if (tid < world) {
-    counts[tid] = sh.base[tid];
-    if (host_counts) host_counts[tid] = sh.base[tid];
+#pragma unroll
+  for (int k = 0; k < kOrderR; ++k) {
+    unsigned long long same = ~0ull, mr = ~0ull;
+    for (int j = 0; j < nbits; ++j) {
+      const unsigned long long b = __ballot((q[k] >> j) & 1);
+      same &= ((q[k] >> j) & 1) ? b : ~b;
+      mr &= ((lane >> j) & 1) ? b : ~b;  // lane r < world: the lanes owned by rank r
+    }
+    mine[k] = __popcll(same & lt);
+    if (lane < world) wc[k][wave][lane] = __popcll(mr);
+  }
+  __syncthreads();
+  if (tid < world) {  // (round, wave) counts -> the owner's features before them in the block
+    int acc = 0;
+#pragma unroll
+    for (int k = 0; k < kOrderR; ++k)
+#pragma unroll
+      for (int w = 0; w < kOrderWaves; ++w) {
+        const int c = wc[k][w][tid];
+        wc[k][w][tid] = acc;
+        acc += c;
+      }
+    bcount[blockIdx.x * world + tid] = acc;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kOrderR; ++k) {
+    const int i = p0 + k * kOrderThreads + tid;
+    if (i < n) code[i] = q[k] == nobody ? -1 : ((q[k] << 24) | (wc[k][wave][q[k]] + mine[k]));
   }
 }
 
-__global__ __launch_bounds__(kOrderThreads) void k_gather_order(const float *__restrict__ x0,
+__global__ __launch_bounds__(kOrderThreads) void k_gather_count(const float *__restrict__ x0,
                                                                 const float *__restrict__ y0,
                                                                 const int *__restrict__ v0, int n, GatherEdges E,
                                                                 int *__restrict__ work, int *__restrict__ save,
-                                                                int *__restrict__ escape,
-                                                                int *__restrict__ host_counts) {
+                                                                int *__restrict__ escape) {
   __builtin_amdgcn_s_setprio(3);  // between two trackers: issue ahead of co-resident pyramid waves
-  __shared__ OrderShared sh;
-  if (threadIdx.x == 0 && escape) *escape = 0;
-  order_all<false>(sh, n, E, work, work + n, const_cast<float *>(x0), const_cast<float *>(y0),
-                   const_cast<int *>(v0), save, host_counts, Unpack{});
+  if (blockIdx.x == 0 && threadIdx.x == 0 && escape) *escape = 0;
+  count_block<false>(n, E, work, work + n + E.world, const_cast<float *>(x0), const_cast<float *>(y0),
+                     const_cast<int *>(v0), save, Unpack{});
 }
 
-// gather_unpack and the next chunk's gather_order in one launch: each feature
-// from its owner's slot (at the place the previous order gave it), then the
-// ownership of the merged state.  One workgroup reads and rewrites `code`
-// feature by feature, so no place is read after it is rewritten.
-__global__ __launch_bounds__(kOrderThreads) void k_gather_unpack_order(
+// gather_unpack and the next chunk's count in one launch: each feature from
+// its owner's slot (at the place the previous order gave it), then the owner
+// of the merged state.  The thread that reads code[i] rewrites it.
+__global__ __launch_bounds__(kOrderThreads) void k_gather_unpack_count(
     const int *__restrict__ slots, int nslots, int r0, int n, int S, float *__restrict__ x, float *__restrict__ y,
     int *__restrict__ v, int *__restrict__ flags, int *__restrict__ host_flags, GatherEdges E, int *__restrict__ work,
-    int *__restrict__ save, int *__restrict__ escape, int *__restrict__ host_counts) {
-  __builtin_amdgcn_s_setprio(3);  // between two trackers: issue ahead of co-resident pyramid waves
-  __shared__ OrderShared sh;
+    int *__restrict__ save, int *__restrict__ escape) {
+  __builtin_amdgcn_s_setprio(3);
   const long words = kGatherHdr + 3L * S;
   int esc = 0, bad = 0;
   for (int k = 0; k < nslots; ++k) {
@@ -319,7 +287,7 @@ __global__ __launch_bounds__(kOrderThreads) void k_gather_unpack_order(
     esc += h[0];
     bad += h[1] + (h[2] > S || h[3] != S ? 1 : 0);
   }
-  if (threadIdx.x == 0) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     flags[0] = esc;
     flags[1] = bad;
     if (host_flags) {
@@ -328,7 +296,40 @@ __global__ __launch_bounds__(kOrderThreads) void k_gather_unpack_order(
     }
     if (escape) *escape = 0;
   }
-  order_all<true>(sh, n, E, work, work + n, x, y, v, save, host_counts, Unpack{slots, nslots, r0, S, bad, words});
+  count_block<true>(n, E, work, work + n + E.world, x, y, v, save, Unpack{slots, nslots, r0, S, bad, words});
+}
+
+// Block b: its places moved past the owners' features of blocks 0..b-1
+// (b * world counts summed in LDS: a few hundred words at 20k features).
+__global__ __launch_bounds__(kOrderThreads) void k_gather_place(int n, int world, int *__restrict__ work,
+                                                                int *__restrict__ host_counts) {
+  __builtin_amdgcn_s_setprio(3);
+  __shared__ int pre[KLT_HIP_GATHER_MAX_RANKS];
+  const int tid = threadIdx.x, b = blockIdx.x, last = b == (int)gridDim.x - 1;
+  int *code = work, *counts = work + n;
+  const int *bcount = work + n + world;
+  if (tid < world) pre[tid] = 0;
+  __syncthreads();
+  const int ne = (b + last) * world;  // the last block also sums its own: the totals
+  for (int e = tid; e < ne; e += kOrderThreads) atomicAdd(&pre[e % world], bcount[e]);
+  __syncthreads();
+  if (last && tid < world) {
+    counts[tid] = pre[tid];
+    if (host_counts) host_counts[tid] = pre[tid];
+  }
+  if (b == 0) return;
+  const int p0 = b * kOrderBlock;
+  int c[kOrderR];
+#pragma unroll
+  for (int k = 0; k < kOrderR; ++k) {
+    const int i = p0 + k * kOrderThreads + tid;
+    c[k] = i < n ? code[i] : -1;
+  }
+#pragma unroll
+  for (int k = 0; k < kOrderR; ++k) {
+    const int i = p0 + k * kOrderThreads + tid;
+    if (c[k] >= 0) code[i] = c[k] + pre[c[k] >> 24];
+  }
 }
 
 __global__ void k_gather_pack(const float *__restrict__ x, const float *__restrict__ y, const int *__restrict__ v,
@@ -487,8 +488,10 @@ KLT_API int klt_hip_gather_order(klt_hip_ctx *ctx, const float *x0, const float 
   GatherEdges E{};
   for (int r = 0; r <= world; ++r) E.e[r] = edges[r];
   E.world = world;
-  hipLaunchKernelGGL(k_gather_order, dim3(1), dim3(kOrderThreads), 0, (hipStream_t)klt_hip_get_stream(ctx), x0, y0,
-                     v0, n, E, work, save, escape, host_counts);
+  hipStream_t st = (hipStream_t)klt_hip_get_stream(ctx);
+  const int nb = gather_blocks(n);
+  hipLaunchKernelGGL(k_gather_count, dim3(nb), dim3(kOrderThreads), 0, st, x0, y0, v0, n, E, work, save, escape);
+  hipLaunchKernelGGL(k_gather_place, dim3(nb), dim3(kOrderThreads), 0, st, n, world, work, host_counts);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : kltdev::ctx_fail(ctx, "gather_order: %s", hipGetErrorString(e));
 }
@@ -534,9 +537,11 @@ KLT_API int klt_hip_gather_unpack_order(klt_hip_ctx *ctx, const int *slots, int 
   GatherEdges E{};
   for (int r = 0; r <= world; ++r) E.e[r] = edges[r];
   E.world = world;
-  hipLaunchKernelGGL(k_gather_unpack_order, dim3(1), dim3(kOrderThreads), 0, (hipStream_t)klt_hip_get_stream(ctx),
-                     slots, nslots, first_rank, n, S, x, y, val, flags, host_flags, E, work, save, escape,
-                     host_counts);
+  hipStream_t st = (hipStream_t)klt_hip_get_stream(ctx);
+  const int nb = gather_blocks(n);
+  hipLaunchKernelGGL(k_gather_unpack_count, dim3(nb), dim3(kOrderThreads), 0, st, slots, nslots, first_rank, n, S, x,
+                     y, val, flags, host_flags, E, work, save, escape);
+  hipLaunchKernelGGL(k_gather_place, dim3(nb), dim3(kOrderThreads), 0, st, n, world, work, host_counts);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : kltdev::ctx_fail(ctx, "gather_unpack_order: %s", hipGetErrorString(e));
 }
