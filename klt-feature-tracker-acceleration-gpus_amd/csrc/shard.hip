@@ -310,12 +310,12 @@ __global__ __launch_bounds__(kOrderThreads) void k_gather_place(int n, int world
   const int *bcount = work + n + world;
   if (tid < world) pre[tid] = 0;
   __syncthreads();
-  const int ne = (b + last) * world;  // the last block also sums its own: the totals
-  for (int e = tid; e < ne; e += kOrderThreads) atomicAdd(&pre[e % world], bcount[e]);
+  for (int e = tid; e < b * world; e += kOrderThreads) atomicAdd(&pre[e % world], bcount[e]);
   __syncthreads();
-  if (last && tid < world) {
-    counts[tid] = pre[tid];
-    if (host_counts) host_counts[tid] = pre[tid];
+  if (last && tid < world) {  // the totals: the blocks before and this one
+    const int t = pre[tid] + bcount[b * world + tid];
+    counts[tid] = t;
+    if (host_counts) host_counts[tid] = t;
   }
   if (b == 0) return;
   const int p0 = b * kOrderBlock;
