@@ -576,6 +576,15 @@ int launch_l0(klt_hip_ctx *c, hipStream_t st, const uint8_t *src, long pitch, lo
                                                hs, W1, do_hs, fs0, fsh, F, ty0, ty1, py0, py1, il));
 }
 
+// KLT_AHEAD_PIECES: a band call's build-ahead in that many pieces (A/B hook)
+int ahead_pieces(int F) {
+  static const int n = [] {
+    const char *v = getenv("KLT_AHEAD_PIECES");
+    return v && *v ? clampi(atoi(v), 1, 64) : 1;
+  }();
+  return n < F ? n : (F > 0 ? F : 1);
+}
+
 // KLT_L1_THIN=0: a single frame's level 1 in 32-row tiles too (A/B)
 bool l1_thin() {
   static const bool on = [] {
@@ -909,7 +918,7 @@ int ensure_banks(klt_hip_ctx *c, const klt_hip_pyr_desc *d, int frames) {
 // (a band's outer margin feeds only level 1)
 int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
                      long stride, int F, hipStream_t st, int row_lo = 0, int row_hi = 1 << 30, int plane_lo = 0,
-                     int plane_hi = 1 << 30, int il = 1) {
+                     int plane_hi = 1 << 30, int il = 1, int f0 = 0) {
   const int W = d->ncols, H = d->nrows;
   const DefTaps T = default_taps(d);
   const bool two = d->nlevels == 2;
@@ -927,8 +936,11 @@ int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const u
   for (int l = 0; l < d->nlevels; ++l) K.lv[l].il = il;
   {
     TimedScope ts(c, T_L0, st, F);
-    if (launch_l0(c, st, src, pitch, stride, W, H, T, vec_u8, vec_out, K.lv[0].img, K.lv[0].gx, K.lv[0].gy, K.hs,
-                  W1, (two && W1 > 0) ? 1 : 0, np * fs0, fsh, F, r0, r1, &p0, &p1, il))
+    // frames f0 .. f0+F-1 of the bank (a build in pieces)
+    const long o0 = (long)f0 * np * fs0;
+    if (launch_l0(c, st, src, pitch, stride, W, H, T, vec_u8, vec_out, K.lv[0].img + o0, K.lv[0].gx + o0,
+                  K.lv[0].gy + o0, K.hs + (long)f0 * fsh, W1, (two && W1 > 0) ? 1 : 0, np * fs0, fsh, F, r0, r1,
+                  &p0, &p1, il))
       return -1;
   }
   K.vlo[0] = p0;
@@ -950,8 +962,9 @@ int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const u
       HMARK_IN("l0_launched");
       TimedScope ts(c, T_L1, st, F);
       const int vec = (W1 % 4 == 0 && W1 >= 8) ? 1 : 0;
-      if (launched(c, "k_pyr_l1", launch_pyr_l1(st, K.hs, W1, H, H1, T, vec, K.lv[1].img, K.lv[1].gx, K.lv[1].gy,
-                                                fsh, np * fs1, F, t1lo, t1hi, il)))
+      const long o1 = (long)f0 * np * fs1;
+      if (launched(c, "k_pyr_l1", launch_pyr_l1(st, K.hs + (long)f0 * fsh, W1, H, H1, T, vec, K.lv[1].img + o1,
+                                                K.lv[1].gx + o1, K.lv[1].gy + o1, fsh, np * fs1, F, t1lo, t1hi, il)))
         return -1;
       HMARK_IN("l1_launched");
     }
@@ -2087,11 +2100,17 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     } else {
       HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_bfree[bj], 0));
     }
-    int p0 = 0, p1 = 1 << 30;
-    band_planes(*band, p0, p1);
-    if (build_fused_bank(c, c->bank[bj], pd, band->next, pitch, stride, Fn, c->pstream, band->row_lo, band->row_hi,
-                         p0, p1, bil))
-      return -1;
+    // in pieces (KLT_AHEAD_PIECES, default 1): each piece's level 1 right
+    // after its level 0, so the build's tail past the tracker is one piece's
+    for (int q = 0, np = ahead_pieces(Fn); q < np; ++q) {
+      const int fa = (int)((long)Fn * q / np), fb = (int)((long)Fn * (q + 1) / np);
+      if (fb <= fa) continue;
+      int p0 = 0, p1 = 1 << 30;
+      band_planes(*band, p0, p1);
+      if (build_fused_bank(c, c->bank[bj], pd, band->next + (long)fa * stride, pitch, stride, fb - fa, c->pstream,
+                           band->row_lo, band->row_hi, p0, p1, bil, fa))
+        return -1;
+    }
     HIPCHK(c, hipEventRecord(c->ev_bbuilt[bj], c->pstream));
     c->pre.bank = bj;
     c->pre.src = band->next;

@@ -8,6 +8,7 @@
 #   bench      bench.py (default shape); s20: bench.py --steps 20 --warmup 5
 #   shard8     tools/shard_sim.py, 1 and 8 ranks over config 4's 1001 frames
 #   py:<file>  python3 <file> (an experiment script), output in <tag>/
+#   env:N=V    export N=V for the steps after it (A/B hooks)
 set -o pipefail
 TAG=${1:-r05}; shift; OUT=gpurun_out/$TAG; mkdir -p $OUT
 export TMPDIR=/tmp
@@ -36,8 +37,8 @@ for step in "$@"; do
       head -c 400 $OUT/bench_s20.json; echo ;;
     shard8)
       timeout -k 10 1100 python3 -u tools/shard_sim.py --frames 1001 --chunk 64 --worlds 1 8 --margins 64 --pass1-shared \
-        > $OUT/shard8.log 2>&1 || { tail -20 $OUT/shard8.log; exit 1; }
-      head -3 $OUT/shard8.log ;;
+        > $OUT/shard8${LOGSFX}.log 2>&1 || { tail -20 $OUT/shard8${LOGSFX}.log; exit 1; }
+      head -3 $OUT/shard8${LOGSFX}.log ;;
     apitl)  # per-call KLTTrackFeatures timeline, registered buffers (tools/api_timeline.py)
       timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d $OUT/apitl -o run --output-format csv -- \
         python3 tools/api_timeline.py run --register --frames 60 > $OUT/apitl.log 2>&1 || { tail -20 $OUT/apitl.log; exit 1; }
@@ -52,13 +53,15 @@ for step in "$@"; do
       grep -E "fps|seqtrace" $OUT/seqprof.log | cut -c1-220 ;;
     shardprof)  # one rank of the 8-rank config-4 replay under a kernel trace (tools/rank_timeline.py)
       timeout -k 10 900 python3 -u tools/shard_sim.py --frames 1001 --chunk 64 --worlds 8 --margins 64 --pass1-shared \
-        --keep-states $OUT/states > $OUT/shardprof_sim.log 2>&1 || { tail -20 $OUT/shardprof_sim.log; exit 1; }
-      timeout -k 10 300 rocprofv3 --kernel-trace -d $OUT/shardprof -o run --output-format csv -- \
+        --keep-states $OUT/states > $OUT/shardprof_sim${LOGSFX}.log 2>&1 || { tail -20 $OUT/shardprof_sim${LOGSFX}.log; exit 1; }
+      timeout -k 10 300 rocprofv3 --kernel-trace -d $OUT/shardprof${LOGSFX} -o run --output-format csv -- \
         python3 tools/shard_sim.py --frames 1001 --chunk 64 --replay $OUT/states/states_w8.npz --rank ${SHARD_RANK:-4} \
-        > $OUT/shardprof.log 2>&1 || { tail -20 $OUT/shardprof.log; exit 1; }
+        > $OUT/shardprof${LOGSFX}.log 2>&1 || { tail -20 $OUT/shardprof${LOGSFX}.log; exit 1; }
       rm -rf $OUT/states
-      python3 tools/rank_timeline.py $(find $OUT/shardprof -name "*kernel_trace.csv") 3 > $OUT/rank_timeline.txt
-      head -60 $OUT/rank_timeline.txt ;;
+      python3 tools/rank_timeline.py $(find $OUT/shardprof${LOGSFX} -name "*kernel_trace.csv") 3 > $OUT/rank_timeline${LOGSFX}.txt
+      head -60 $OUT/rank_timeline${LOGSFX}.txt ;;
+    env:*)  # export NAME=VALUE for the steps after it
+      export "${step#env:}"; echo "${step#env:}" >> $OUT/commit.txt ;;
     py:*)
       f=${step#py:}; b=$(basename $f .py)
       timeout -k 10 900 python3 -u $f $OUT > $OUT/$b.log 2>&1 || { tail -30 $OUT/$b.log; exit 1; }
