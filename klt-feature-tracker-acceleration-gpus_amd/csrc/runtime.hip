@@ -226,6 +226,11 @@ struct klt_hip_ctx {
   // caller queues between two chunks (klt_hip_set_ahead_ready)
   int ahead_ready = 0;
   hipEvent_t ev_go = nullptr;
+  // KLT_AHEAD_EARLY=1 (A/B): the build-ahead waits instead for ev_after, recorded
+  // after the previous one-chunk band call's tracker (after_ok), so it starts
+  // in the gap between two trackers
+  hipEvent_t ev_after = nullptr;
+  int after_ok = 0;
   int serial_frames = 1;  // klt_hip_track_frames: 1 builds and tracks on one stream (default: the
                           // tracker and the pyramid kernels compete for the same CUs; overlap buys ~3 %)
   int *d_perm = nullptr;
@@ -574,6 +579,14 @@ int launch_l0(klt_hip_ctx *c, hipStream_t st, const uint8_t *src, long pitch, lo
   }
   return launched(c, "k_pyr_l0", launch_pyr_l0(st, src, (int)pitch, stride, W, H, T, vec_u8, vec_out, img, gx, gy,
                                                hs, W1, do_hs, fs0, fsh, F, ty0, ty1, py0, py1, il));
+}
+
+bool ahead_early() {
+  static const bool on = [] {
+    const char *v = getenv("KLT_AHEAD_EARLY");
+    return v && *v && atoi(v) != 0;
+  }();
+  return on;
 }
 
 // KLT_AHEAD_PIECES: a band call's build-ahead in that many pieces (A/B hook)
@@ -1116,6 +1129,7 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
   if (c->ev_start) hipEventDestroy(c->ev_start);
   if (c->ev_caller) hipEventDestroy(c->ev_caller);
   if (c->ev_go) hipEventDestroy(c->ev_go);
+  if (c->ev_after) hipEventDestroy(c->ev_after);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
 }
@@ -1189,6 +1203,7 @@ KLT_API int klt_hip_ctx_reset(klt_hip_ctx *c) {
   c->track_impl = 0;
   c->serial_frames = 1;
   c->ahead_ready = 0;
+  c->after_ok = 0;
   c->prof = nullptr;
   c->frames_ready = false;
   c->pre.bank = -1;
@@ -2095,7 +2110,10 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     // pyramid stream: they depend on frames only, not on this chunk's result
     const int bj = c->bank_next;
     const int Fn = band->next_n < chunk ? band->next_n : chunk;
-    if (c->ahead_ready) {  // with this chunk's tracker, so after the previous one: bank bj is free
+    const bool one = nframes <= F;  // this call took one bank: bj was last read before the previous call's end
+    if (c->ahead_ready && ahead_early() && one && c->after_ok) {
+      HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_after, 0));  // after the previous call's tracker
+    } else if (c->ahead_ready) {  // with this chunk's tracker, so after the previous one: bank bj is free
       if (!pwait) HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_go, 0));
     } else {
       HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_bfree[bj], 0));
@@ -2112,6 +2130,13 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
         return -1;
     }
     HIPCHK(c, hipEventRecord(c->ev_bbuilt[bj], c->pstream));
+    if (c->ahead_ready && ahead_early() && one) {
+      if (!c->ev_after) HIPCHK(c, hipEventCreateWithFlags(&c->ev_after, hipEventDisableTiming));
+      HIPCHK(c, hipEventRecord(c->ev_after, c->stream));
+      c->after_ok = 1;
+    } else {
+      c->after_ok = 0;
+    }
     c->pre.bank = bj;
     c->pre.src = band->next;
     c->pre.F = Fn;
