@@ -581,6 +581,18 @@ int launch_l0(klt_hip_ctx *c, hipStream_t st, const uint8_t *src, long pitch, lo
                                                hs, W1, do_hs, fs0, fsh, F, ty0, ty1, py0, py1, il));
 }
 
+// Flags of the events that only order our two streams on one device (the
+// kernels' own end-of-kernel releases and start-of-kernel acquires make the
+// data visible): KLT_EVENT_NOFENCE=1 drops the record's system-scope fence
+// (an L2 writeback between two trackers) -- A/B hook
+unsigned stream_event_flags() {
+  static const unsigned f = [] {
+    const char *v = getenv("KLT_EVENT_NOFENCE");
+    return (unsigned)hipEventDisableTiming | (v && *v && atoi(v) != 0 ? (unsigned)hipEventDisableSystemFence : 0u);
+  }();
+  return f;
+}
+
 bool ahead_early() {
   static const bool on = [] {
     const char *v = getenv("KLT_AHEAD_EARLY");
@@ -1782,10 +1794,10 @@ KLT_API int klt_hip_track_sequence(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, c
   if (use_device(c)) return -1;
   if (!c->pstream) {
     HIPCHK(c, make_pstream(c));
-    HIPCHK(c, hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_start, stream_event_flags()));
     for (int k = 0; k < 3; ++k) {
-      HIPCHK(c, hipEventCreateWithFlags(&c->ev_built[k], hipEventDisableTiming));
-      HIPCHK(c, hipEventCreateWithFlags(&c->ev_free[k], hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_built[k], stream_event_flags()));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_free[k], stream_event_flags()));
     }
   }
   // the pyramid stream starts behind everything already queued on the tracking stream
@@ -1952,16 +1964,16 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
   HMARK("set_device");
   if (!c->pstream) {
     HIPCHK(c, make_pstream(c));
-    HIPCHK(c, hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_start, stream_event_flags()));
     for (int k = 0; k < 3; ++k) {
-      HIPCHK(c, hipEventCreateWithFlags(&c->ev_built[k], hipEventDisableTiming));
-      HIPCHK(c, hipEventCreateWithFlags(&c->ev_free[k], hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_built[k], stream_event_flags()));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_free[k], stream_event_flags()));
     }
   }
   if (!c->ev_bbuilt[0])
     for (int k = 0; k < 3; ++k) {
-      HIPCHK(c, hipEventCreateWithFlags(&c->ev_bbuilt[k], hipEventDisableTiming));
-      HIPCHK(c, hipEventCreateWithFlags(&c->ev_bfree[k], hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_bbuilt[k], stream_event_flags()));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_bfree[k], stream_event_flags()));
     }
   // the banks' byte budget caps the chunk: a plain call runs shorter launches
   // (results do not depend on the chunk), a band call -- whose chunk is the
@@ -2096,7 +2108,7 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
       b.tstride = tab_stride;
     }
     if (band && c->ahead_ready) {
-      if (!c->ev_go) HIPCHK(c, hipEventCreateWithFlags(&c->ev_go, hipEventDisableTiming));
+      if (!c->ev_go) HIPCHK(c, hipEventCreateWithFlags(&c->ev_go, stream_event_flags()));
       HIPCHK(c, hipEventRecord(c->ev_go, c->stream));
     }
     if (n > 0 && track_frames_launch(c, c->stream, td, a, b, x, y, val, n, band ? band->own : nullptr, true))
@@ -2131,7 +2143,7 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     }
     HIPCHK(c, hipEventRecord(c->ev_bbuilt[bj], c->pstream));
     if (c->ahead_ready && ahead_early() && one) {
-      if (!c->ev_after) HIPCHK(c, hipEventCreateWithFlags(&c->ev_after, hipEventDisableTiming));
+      if (!c->ev_after) HIPCHK(c, hipEventCreateWithFlags(&c->ev_after, stream_event_flags()));
       HIPCHK(c, hipEventRecord(c->ev_after, c->stream));
       c->after_ok = 1;
     } else {
