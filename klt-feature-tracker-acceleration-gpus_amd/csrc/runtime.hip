@@ -226,11 +226,6 @@ struct klt_hip_ctx {
   // caller queues between two chunks (klt_hip_set_ahead_ready)
   int ahead_ready = 0;
   hipEvent_t ev_go = nullptr;
-  // KLT_AHEAD_EARLY=1 (A/B): the build-ahead waits instead for ev_after, recorded
-  // after the previous one-chunk band call's tracker (after_ok), so it starts
-  // in the gap between two trackers
-  hipEvent_t ev_after = nullptr;
-  int after_ok = 0;
   int serial_frames = 1;  // klt_hip_track_frames: 1 builds and tracks on one stream (default: the
                           // tracker and the pyramid kernels compete for the same CUs; overlap buys ~3 %)
   int *d_perm = nullptr;
@@ -581,35 +576,6 @@ int launch_l0(klt_hip_ctx *c, hipStream_t st, const uint8_t *src, long pitch, lo
                                                hs, W1, do_hs, fs0, fsh, F, ty0, ty1, py0, py1, il));
 }
 
-// Flags of the events that only order our two streams on one device (the
-// kernels' own end-of-kernel releases and start-of-kernel acquires make the
-// data visible): KLT_EVENT_NOFENCE=1 drops the record's system-scope fence
-// (an L2 writeback between two trackers) -- A/B hook
-unsigned stream_event_flags() {
-  static const unsigned f = [] {
-    const char *v = getenv("KLT_EVENT_NOFENCE");
-    return (unsigned)hipEventDisableTiming | (v && *v && atoi(v) != 0 ? (unsigned)hipEventDisableSystemFence : 0u);
-  }();
-  return f;
-}
-
-bool ahead_early() {
-  static const bool on = [] {
-    const char *v = getenv("KLT_AHEAD_EARLY");
-    return v && *v && atoi(v) != 0;
-  }();
-  return on;
-}
-
-// KLT_AHEAD_PIECES: a band call's build-ahead in that many pieces (A/B hook)
-int ahead_pieces(int F) {
-  static const int n = [] {
-    const char *v = getenv("KLT_AHEAD_PIECES");
-    return v && *v ? clampi(atoi(v), 1, 64) : 1;
-  }();
-  return n < F ? n : (F > 0 ? F : 1);
-}
-
 // KLT_L1_THIN=0: a single frame's level 1 in 32-row tiles too (A/B)
 bool l1_thin() {
   static const bool on = [] {
@@ -943,7 +909,7 @@ int ensure_banks(klt_hip_ctx *c, const klt_hip_pyr_desc *d, int frames) {
 // (a band's outer margin feeds only level 1)
 int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
                      long stride, int F, hipStream_t st, int row_lo = 0, int row_hi = 1 << 30, int plane_lo = 0,
-                     int plane_hi = 1 << 30, int il = 1, int f0 = 0) {
+                     int plane_hi = 1 << 30, int il = 1) {
   const int W = d->ncols, H = d->nrows;
   const DefTaps T = default_taps(d);
   const bool two = d->nlevels == 2;
@@ -961,11 +927,8 @@ int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const u
   for (int l = 0; l < d->nlevels; ++l) K.lv[l].il = il;
   {
     TimedScope ts(c, T_L0, st, F);
-    // frames f0 .. f0+F-1 of the bank (a build in pieces)
-    const long o0 = (long)f0 * np * fs0;
-    if (launch_l0(c, st, src, pitch, stride, W, H, T, vec_u8, vec_out, K.lv[0].img + o0, K.lv[0].gx + o0,
-                  K.lv[0].gy + o0, K.hs + (long)f0 * fsh, W1, (two && W1 > 0) ? 1 : 0, np * fs0, fsh, F, r0, r1,
-                  &p0, &p1, il))
+    if (launch_l0(c, st, src, pitch, stride, W, H, T, vec_u8, vec_out, K.lv[0].img, K.lv[0].gx, K.lv[0].gy, K.hs,
+                  W1, (two && W1 > 0) ? 1 : 0, np * fs0, fsh, F, r0, r1, &p0, &p1, il))
       return -1;
   }
   K.vlo[0] = p0;
@@ -987,9 +950,8 @@ int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const u
       HMARK_IN("l0_launched");
       TimedScope ts(c, T_L1, st, F);
       const int vec = (W1 % 4 == 0 && W1 >= 8) ? 1 : 0;
-      const long o1 = (long)f0 * np * fs1;
-      if (launched(c, "k_pyr_l1", launch_pyr_l1(st, K.hs + (long)f0 * fsh, W1, H, H1, T, vec, K.lv[1].img + o1,
-                                                K.lv[1].gx + o1, K.lv[1].gy + o1, fsh, np * fs1, F, t1lo, t1hi, il)))
+      if (launched(c, "k_pyr_l1", launch_pyr_l1(st, K.hs, W1, H, H1, T, vec, K.lv[1].img, K.lv[1].gx, K.lv[1].gy,
+                                                fsh, np * fs1, F, t1lo, t1hi, il)))
         return -1;
       HMARK_IN("l1_launched");
     }
@@ -1141,7 +1103,6 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
   if (c->ev_start) hipEventDestroy(c->ev_start);
   if (c->ev_caller) hipEventDestroy(c->ev_caller);
   if (c->ev_go) hipEventDestroy(c->ev_go);
-  if (c->ev_after) hipEventDestroy(c->ev_after);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
 }
@@ -1215,7 +1176,6 @@ KLT_API int klt_hip_ctx_reset(klt_hip_ctx *c) {
   c->track_impl = 0;
   c->serial_frames = 1;
   c->ahead_ready = 0;
-  c->after_ok = 0;
   c->prof = nullptr;
   c->frames_ready = false;
   c->pre.bank = -1;
@@ -1794,10 +1754,10 @@ KLT_API int klt_hip_track_sequence(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, c
   if (use_device(c)) return -1;
   if (!c->pstream) {
     HIPCHK(c, make_pstream(c));
-    HIPCHK(c, hipEventCreateWithFlags(&c->ev_start, stream_event_flags()));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
     for (int k = 0; k < 3; ++k) {
-      HIPCHK(c, hipEventCreateWithFlags(&c->ev_built[k], stream_event_flags()));
-      HIPCHK(c, hipEventCreateWithFlags(&c->ev_free[k], stream_event_flags()));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_built[k], hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_free[k], hipEventDisableTiming));
     }
   }
   // the pyramid stream starts behind everything already queued on the tracking stream
@@ -1964,16 +1924,16 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
   HMARK("set_device");
   if (!c->pstream) {
     HIPCHK(c, make_pstream(c));
-    HIPCHK(c, hipEventCreateWithFlags(&c->ev_start, stream_event_flags()));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming));
     for (int k = 0; k < 3; ++k) {
-      HIPCHK(c, hipEventCreateWithFlags(&c->ev_built[k], stream_event_flags()));
-      HIPCHK(c, hipEventCreateWithFlags(&c->ev_free[k], stream_event_flags()));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_built[k], hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_free[k], hipEventDisableTiming));
     }
   }
   if (!c->ev_bbuilt[0])
     for (int k = 0; k < 3; ++k) {
-      HIPCHK(c, hipEventCreateWithFlags(&c->ev_bbuilt[k], stream_event_flags()));
-      HIPCHK(c, hipEventCreateWithFlags(&c->ev_bfree[k], stream_event_flags()));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_bbuilt[k], hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_bfree[k], hipEventDisableTiming));
     }
   // the banks' byte budget caps the chunk: a plain call runs shorter launches
   // (results do not depend on the chunk), a band call -- whose chunk is the
@@ -2108,7 +2068,7 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
       b.tstride = tab_stride;
     }
     if (band && c->ahead_ready) {
-      if (!c->ev_go) HIPCHK(c, hipEventCreateWithFlags(&c->ev_go, stream_event_flags()));
+      if (!c->ev_go) HIPCHK(c, hipEventCreateWithFlags(&c->ev_go, hipEventDisableTiming));
       HIPCHK(c, hipEventRecord(c->ev_go, c->stream));
     }
     if (n > 0 && track_frames_launch(c, c->stream, td, a, b, x, y, val, n, band ? band->own : nullptr, true))
@@ -2122,33 +2082,17 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     // pyramid stream: they depend on frames only, not on this chunk's result
     const int bj = c->bank_next;
     const int Fn = band->next_n < chunk ? band->next_n : chunk;
-    const bool one = nframes <= F;  // this call took one bank: bj was last read before the previous call's end
-    if (c->ahead_ready && ahead_early() && one && c->after_ok) {
-      HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_after, 0));  // after the previous call's tracker
-    } else if (c->ahead_ready) {  // with this chunk's tracker, so after the previous one: bank bj is free
+    if (c->ahead_ready) {  // with this chunk's tracker, so after the previous one: bank bj is free
       if (!pwait) HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_go, 0));
     } else {
       HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_bfree[bj], 0));
     }
-    // in pieces (KLT_AHEAD_PIECES, default 1): each piece's level 1 right
-    // after its level 0, so the build's tail past the tracker is one piece's
-    for (int q = 0, np = ahead_pieces(Fn); q < np; ++q) {
-      const int fa = (int)((long)Fn * q / np), fb = (int)((long)Fn * (q + 1) / np);
-      if (fb <= fa) continue;
-      int p0 = 0, p1 = 1 << 30;
-      band_planes(*band, p0, p1);
-      if (build_fused_bank(c, c->bank[bj], pd, band->next + (long)fa * stride, pitch, stride, fb - fa, c->pstream,
-                           band->row_lo, band->row_hi, p0, p1, bil, fa))
-        return -1;
-    }
+    int p0 = 0, p1 = 1 << 30;
+    band_planes(*band, p0, p1);
+    if (build_fused_bank(c, c->bank[bj], pd, band->next, pitch, stride, Fn, c->pstream, band->row_lo, band->row_hi,
+                         p0, p1, bil))
+      return -1;
     HIPCHK(c, hipEventRecord(c->ev_bbuilt[bj], c->pstream));
-    if (c->ahead_ready && ahead_early() && one) {
-      if (!c->ev_after) HIPCHK(c, hipEventCreateWithFlags(&c->ev_after, stream_event_flags()));
-      HIPCHK(c, hipEventRecord(c->ev_after, c->stream));
-      c->after_ok = 1;
-    } else {
-      c->after_ok = 0;
-    }
     c->pre.bank = bj;
     c->pre.src = band->next;
     c->pre.F = Fn;
