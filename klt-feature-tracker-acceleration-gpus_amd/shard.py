@@ -77,6 +77,39 @@ def balanced_edges(y: torch.Tensor, v: torch.Tensor, nrows: int, world: int) -> 
     return edges
 
 
+def built_rows(nrows: int, band: Band, tile: int = 32) -> int:
+    """Level-0 rows a rank's band build covers: its rows rounded out to whole tiles."""
+    lo = (band.row_lo // tile) * tile
+    hi = min(nrows, -(-band.row_hi // tile) * tile)
+    return hi - lo
+
+
+def row_edges(nrows: int, world: int, margin: int = DEFAULT_MARGIN, tile: int = 32) -> list[int]:
+    """Row boundaries that give every rank about the same number of level-0
+    rows to build (its band, the margins, whole tiles): the two edge ranks have
+    one margin, so they own about a margin's rows more.  Inner boundaries on
+    tile multiples (no partial tiles on either side); the candidate inner
+    heights around (nrows - 2 margin) / world are scored by their largest
+    build.  Deterministic in its arguments."""
+    if world < 3:
+        return [r * nrows // world for r in range(world + 1)]
+    best = None
+    ideal = (nrows - 2 * margin) / world
+    for k in range(max(1, int(ideal // tile) - 2), int(ideal // tile) + 3):
+        inner = k * tile
+        rest = nrows - (world - 2) * inner
+        if rest < 2 * tile:
+            continue
+        for first in sorted({(rest // 2 // tile) * tile, -(-(rest // 2) // tile) * tile}):
+            edges = [0] + [first + i * inner for i in range(world - 1)] + [nrows]
+            if any(b <= a for a, b in zip(edges, edges[1:])):
+                continue
+            cost = max(built_rows(nrows, band_of(nrows, world, r, margin, edges), tile) for r in range(world))
+            if best is None or cost < best[0]:
+                best = (cost, edges)
+    return best[1] if best else [r * nrows // world for r in range(world + 1)]
+
+
 def band_rows(nrows: int, band: Band, tile: int = 32, halo: int = 8) -> tuple[int, int]:
     """The u8 rows [ra, rb) a rank's band build reads: its level-0 build rows
     rounded out to whole tiles, plus the tiles' halo (k_pyr_l0 reads 5 rows

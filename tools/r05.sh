@@ -36,7 +36,7 @@ for step in "$@"; do
       timeout -k 10 600 python3 bench.py --steps 20 --warmup 5 > $OUT/bench_s20.json 2> $OUT/bench_s20.err || { tail -20 $OUT/bench_s20.err; exit 1; }
       head -c 400 $OUT/bench_s20.json; echo ;;
     shard8)
-      timeout -k 10 1100 python3 -u tools/shard_sim.py --frames 1001 --chunk 64 --worlds 1 8 --margins 64 --pass1-shared \
+      timeout -k 10 1100 python3 -u tools/shard_sim.py --frames 1001 --chunk 64 --worlds 1 8 --margins 64 --pass1-shared $SHARD_ARGS \
         > $OUT/shard8${LOGSFX}.log 2>&1 || { tail -20 $OUT/shard8${LOGSFX}.log; exit 1; }
       head -3 $OUT/shard8${LOGSFX}.log ;;
     apitl)  # per-call KLTTrackFeatures timeline, registered buffers (tools/api_timeline.py)

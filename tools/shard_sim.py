@@ -51,7 +51,9 @@ def main():
     ap.add_argument("--worlds", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--margins", type=int, nargs="+", default=[64])
     ap.add_argument("--seed", type=int, default=2160)
-    ap.add_argument("--balanced", action="store_true", help="bands of equal feature counts (balanced_edges)")
+    ap.add_argument("--bands", choices=["equal", "features", "rows"], default="equal",
+                    help="band edges: equal rows, equal feature counts (balanced_edges), or equal level-0 rows "
+                         "built incl. margins (row_edges)")
     ap.add_argument("--keep-states", default=None, help="save pass 1's record as DIR/states_w<N>.npz")
     ap.add_argument("--pass1-shared", action="store_true",
                     help="pass 1 through one device context for every rank, each chunk started from a "
@@ -65,7 +67,8 @@ def main():
     import torch
     import kltamd
     from kltamd.device import PyrDesc, Timing, TrackDesc, check, use_torch_stream
-    from kltamd.shard import (FullFrames, ShardedSequence, balanced_edges, band_edges, band_of, slot_words)
+    from kltamd.shard import (FullFrames, ShardedSequence, balanced_edges, band_edges, band_of, row_edges,
+                              slot_words)
     from kltabi import fl_to_arrays, u8ptr
 
     lib = kltamd.load()
@@ -100,7 +103,7 @@ def main():
         # its all-gather replaced by pass 1's gathered slots of each chunk
         rec = np.load(a.replay)
         world, margin = int(rec["world"]), int(rec["margin"])
-        edges = [int(e) for e in rec["row_edges"]] if a.balanced else None
+        edges = [int(e) for e in rec["row_edges"]] if len(rec["row_edges"]) else None
         flat = torch.from_numpy(rec["slots"]).to(dev)
         offs = rec["slot_offsets"]
         tc = lib.KLTCreateTrackingContext()
@@ -175,12 +178,14 @@ def main():
                 next_n), "band")
 
     out = {"workload": f"{W}x{H}, {NF} features, {T} tracked frames, {a.chunk}-frame chunks"
-                       + (", bands of equal feature counts" if a.balanced else ""),
+                       + {"equal": "", "features": ", bands of equal feature counts",
+                          "rows": ", bands of equal built rows"}[a.bands],
            "exchange_us_assumed_per_chunk": a.exchange_us, "runs": []}
     base = None
     for margin in a.margins:
         for world in a.worlds:
-            edges = balanced_edges(ys, vs, H, world) if a.balanced else None
+            edges = (balanced_edges(ys, vs, H, world) if a.bands == "features" else
+                     row_edges(H, world, margin) if a.bands == "rows" and world > 1 else None)
             gedges = band_edges(H, world, edges)
             ranks = [Rank(world, r, margin, edges) for r in range(1 if a.pass1_shared else world)]
             if a.pass1_shared:
@@ -257,7 +262,7 @@ def main():
                 for r in range(world):
                     cmd = [sys.executable, __file__, "--replay", f, "--rank", str(r), "--width", str(W), "--height",
                            str(H), "--features", str(NF), "--frames", str(a.frames), "--chunk", str(a.chunk),
-                           "--seed", str(a.seed)] + (["--balanced"] if a.balanced else [])
+                           "--seed", str(a.seed)]
                     res = subprocess.run(cmd, check=True, capture_output=True, text=True)
                     reps.append(json.loads(res.stdout.strip().splitlines()[-1]))
             frames = sum(n for _, n in chunks)
