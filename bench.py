@@ -427,7 +427,7 @@ def run_sharded(args, world, rank, dev) -> None:
 
     import kltamd
     from kltamd.device import EXACT, FAST, PyrDesc, TrackDesc, check, use_torch_stream
-    from kltamd.shard import BandFrames, ShardedSequence, band_of
+    from kltamd.shard import BandFrames, ShardedSequence, band_of, row_edges
 
     lib = kltamd.load()
     lib.KLTSetVerbosity(0)
@@ -442,7 +442,8 @@ def run_sharded(args, world, rank, dev) -> None:
         check(lib, ctx, lib.klt_hip_synth_rows(ctx, args.seed, t0, n, W, row0, nrows, C.c_void_p(dst), W, stride),
               "synth")
 
-    frames = BandFrames(nframes, H, W, band_of(H, world, rank, args.margin), load, dev)
+    edges = row_edges(H, world, args.margin)  # equal level-0 rows built per rank (klt_shard_create's bands)
+    frames = BandFrames(nframes, H, W, band_of(H, world, rank, args.margin, edges), load, dev)
     torch.cuda.synchronize()
     f0 = np.empty((H, W), np.uint8)  # frame 0 whole, for the selection every rank makes
     lib.klt_synth_frame(args.seed, 0, W, H, f0.ctypes.data)
@@ -469,7 +470,7 @@ def run_sharded(args, world, rank, dev) -> None:
             dist.all_gather_into_tensor(out, inp)
 
     seq = ShardedSequence(lib, ctx, pd, td, frames, x, y, v, rank, world, all_gather, chunk=args.chunk,
-                          margin=args.margin)
+                          margin=args.margin, edges=edges)
     seq.begin(0)
     seq.run(1, args.warmup)
     v_warm = v.clone()  # the live count after the warm-up, read after the timed region (as in the default mode)

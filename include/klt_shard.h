@@ -43,6 +43,14 @@ typedef struct klt_shard klt_shard;
    frames (row pitch as in klt_shard_track).  Returns 0, or < 0 to fail. */
 typedef int (*klt_shard_frames_fn)(void *user, const unsigned char **frames, long *stride);
 
+/* the band boundaries klt_shard_create uses (host only, no device work):
+   edges[0..world] = row boundaries giving every rank about the same number of
+   level-0 rows to build (its band, the margins, whole 32-row tiles; the two
+   edge ranks, with one margin, own about a margin's rows more) --
+   kltamd/shard.py row_edges.  Rank r owns live features with edges[r] <= y <
+   edges[r+1] (below edges[1] for rank 0, from edges[world-1] on for the
+   last).  0 on success, -1 for bad arguments (world > 16). */
+int klt_shard_band_edges(int nrows, int world, int margin, int *edges);
 /* a new communicator id (ncclGetUniqueId); 0 on success */
 int klt_shard_unique_id(unsigned char id[KLT_SHARD_ID_BYTES]);
 /* rank `rank` of `world` on the device of `ctx` (ncclCommInitRank; every

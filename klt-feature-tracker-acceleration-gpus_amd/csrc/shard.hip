@@ -557,7 +557,60 @@ KLT_API int klt_shard_unique_id(unsigned char id[KLT_SHARD_ID_BYTES]) {
 
 namespace {
 
-// rank/world's band (kltamd/shard.py band_of and band_rows) and a
+// Level-0 rows rank r builds for bands `e` (its own rows, the margins, whole
+// tiles): kltamd/shard.py built_rows
+int built_rows(const std::vector<int> &e, int r, int nrows, int margin, int TH) {
+  const int world = (int)e.size() - 1;
+  const int lo = e[r] - margin > 0 ? e[r] - margin : 0, hi = e[r + 1] + margin < nrows ? e[r + 1] + margin : nrows;
+  const int tlo = lo / TH * TH, thi = (hi + TH - 1) / TH * TH;
+  (void)world;
+  return (thi < nrows ? thi : nrows) - tlo;
+}
+
+// Bands of equal built rows (kltamd/shard.py row_edges, the same candidates in
+// the same order): the edge ranks have one margin, so they own about a
+// margin's rows more; inner boundaries on tile multiples
+std::vector<int> row_edges(int nrows, int world, int margin, int TH) {
+  std::vector<int> eq(world + 1);
+  for (int r = 0; r <= world; ++r) eq[r] = (int)((long)r * nrows / world);
+  if (world < 3) return eq;
+  // equal bands first: a candidate must build strictly fewer rows to replace them
+  std::vector<int> best = eq;
+  int best_cost = 0;
+  for (int r = 0; r < world; ++r) {
+    const int c = built_rows(eq, r, nrows, margin, TH);
+    best_cost = c > best_cost ? c : best_cost;
+  }
+  const double ideal = (double)(nrows - 2 * margin) / world;
+  const int k0 = (int)floor(ideal / TH);
+  for (int k = (k0 - 2 > 1 ? k0 - 2 : 1); k < k0 + 3; ++k) {
+    const int inner = k * TH, rest = nrows - (world - 2) * inner;
+    if (rest < 2 * TH) continue;
+    const int half = rest / 2, f0 = half / TH * TH, f1 = (half + TH - 1) / TH * TH;
+    for (int first : {f0, f1}) {
+      std::vector<int> e(world + 1);
+      e[0] = 0;
+      for (int i = 0; i < world - 1; ++i) e[i + 1] = first + i * inner;
+      e[world] = nrows;
+      bool ok = true;
+      for (int i = 0; i < world; ++i) ok = ok && e[i + 1] > e[i];
+      if (!ok) continue;
+      int cost = 0;
+      for (int r = 0; r < world; ++r) {
+        const int b = built_rows(e, r, nrows, margin, TH);
+        cost = b > cost ? b : cost;
+      }
+      if (cost < best_cost) {
+        best = e;
+        best_cost = cost;
+      }
+      if (f1 == f0) break;  // one candidate (Python's set)
+    }
+  }
+  return best;
+}
+
+// rank/world's band (kltamd/shard.py band_of over row_edges, band_rows) and a
 // communicator of `cranks` ranks in which this one is `crank`
 klt_shard *make_shard(klt_hip_ctx *ctx, int rank, int world, const unsigned char *id, int cranks, int crank,
                       int nrows, int margin) {
@@ -568,19 +621,20 @@ klt_shard *make_shard(klt_hip_ctx *ctx, int rank, int world, const unsigned char
   s->world = world;
   s->nrows = nrows;
   s->cranks = cranks;
-  const int lo = (int)((long)rank * nrows / world), hi = (int)((long)(rank + 1) * nrows / world);
+  const int TH = kltdev::geom::L0_TH, halo = 8;
+  const std::vector<int> re = row_edges(nrows, world, margin, TH);
+  const int lo = re[rank], hi = re[rank + 1];
   s->own_lo = rank == 0 ? -INFINITY : (float)lo;
   s->own_hi = rank == world - 1 ? INFINITY : (float)hi;
   s->row_lo = lo - margin > 0 ? lo - margin : 0;
   s->row_hi = hi + margin < nrows ? hi + margin : nrows;
-  const int TH = kltdev::geom::L0_TH, halo = 8;
   const int t_lo = (s->row_lo / TH) * TH, t_hi = ((s->row_hi + TH - 1) / TH) * TH;
   s->load_lo = t_lo - halo > 0 ? t_lo - halo : 0;
   s->load_hi = t_hi + halo < nrows ? t_hi + halo : nrows;
   ncclUniqueId u;
   memcpy(&u, id, sizeof u);
   s->edges.resize(world + 1);
-  for (int r = 0; r <= world; ++r) s->edges[r] = (float)((long)r * nrows / world);
+  for (int r = 0; r <= world; ++r) s->edges[r] = (float)re[r];
   s->edges[0] = -INFINITY;
   s->edges[world] = INFINITY;
   if (world > KLT_HIP_GATHER_MAX_RANKS || hipSetDevice(klt_hip_ctx_device(ctx)) != hipSuccess ||
@@ -596,6 +650,13 @@ klt_shard *make_shard(klt_hip_ctx *ctx, int rank, int world, const unsigned char
 }
 
 }  // namespace
+
+KLT_API int klt_shard_band_edges(int nrows, int world, int margin, int *edges) {
+  if (nrows < 1 || world < 1 || world > KLT_HIP_GATHER_MAX_RANKS || margin < 0 || !edges) return -1;
+  const std::vector<int> e = row_edges(nrows, world, margin, kltdev::geom::L0_TH);
+  for (int r = 0; r <= world; ++r) edges[r] = e[r];
+  return 0;
+}
 
 KLT_API klt_shard *klt_shard_create(klt_hip_ctx *ctx, int rank, int world, const unsigned char id[KLT_SHARD_ID_BYTES],
                                     int nrows, int margin) {

@@ -97,6 +97,7 @@ DEVICE_PROTOS = {
                                             C.c_int, V, V, V, C.c_int, C.c_float, C.c_float, C.c_int, C.c_int, V,
                                             V, C.c_int]),
     "klt_shard_unique_id": (C.c_int, [V]),
+    "klt_shard_band_edges": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]),
     "klt_shard_create": (V, [V, C.c_int, C.c_int, V, C.c_int, C.c_int]),
     "klt_shard_create_local": (V, [V, C.c_int, C.c_int, C.c_int, C.c_int]),
     "klt_shard_destroy": (None, [V]),

@@ -90,10 +90,12 @@ def row_edges(nrows: int, world: int, margin: int = DEFAULT_MARGIN, tile: int = 
     one margin, so they own about a margin's rows more.  Inner boundaries on
     tile multiples (no partial tiles on either side); the candidate inner
     heights around (nrows - 2 margin) / world are scored by their largest
-    build.  Deterministic in its arguments."""
+    build against equal bands.  Deterministic in its arguments."""
+    eq = [r * nrows // world for r in range(world + 1)]
     if world < 3:
-        return [r * nrows // world for r in range(world + 1)]
-    best = None
+        return eq
+    # equal bands first: a candidate must build strictly fewer rows to replace them
+    best = (max(built_rows(nrows, band_of(nrows, world, r, margin, eq), tile) for r in range(world)), eq)
     ideal = (nrows - 2 * margin) / world
     for k in range(max(1, int(ideal // tile) - 2), int(ideal // tile) + 3):
         inner = k * tile
@@ -105,9 +107,9 @@ def row_edges(nrows: int, world: int, margin: int = DEFAULT_MARGIN, tile: int = 
             if any(b <= a for a, b in zip(edges, edges[1:])):
                 continue
             cost = max(built_rows(nrows, band_of(nrows, world, r, margin, edges), tile) for r in range(world))
-            if best is None or cost < best[0]:
+            if cost < best[0]:
                 best = (cost, edges)
-    return best[1] if best else [r * nrows // world for r in range(world + 1)]
+    return best[1]
 
 
 def band_rows(nrows: int, band: Band, tile: int = 32, halo: int = 8) -> tuple[int, int]:
@@ -321,7 +323,8 @@ class ShardedSequence:
     them whole) or a BandFrames (the rank's rows only; build it with
     band_of(H, world, rank, margin, edges)); x/y/v: device feature arrays
     (identical on every rank at the start), on the stream the context uses.
-    edges: row boundaries of the bands (balanced_edges), default equal rows.
+    edges: row boundaries of the bands; default row_edges(H, world, margin),
+    the bands klt_shard_create uses (equal level-0 rows built per rank).
     all_gather(out, inp) gathers a device int32 tensor of every rank into out
     in rank order (torch.distributed.all_gather_into_tensor in production).
     """
@@ -335,7 +338,8 @@ class ShardedSequence:
         self.rank, self.world, self.chunk = rank, world, chunk
         H, W = self.src.H, self.src.W
         self.H, self.W = H, W
-        self.edges = edges
+        # default: the C driver's bands (klt_shard_create), equal built rows per rank
+        self.edges = edges = list(edges) if edges is not None else row_edges(H, world, margin)
         self.band = band_of(H, world, rank, margin, edges)
         if isinstance(self.src, BandFrames):
             ra, rb = band_rows(H, self.band)

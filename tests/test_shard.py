@@ -16,13 +16,36 @@ import torch.multiprocessing as mp
 from conftest import synth
 
 import kltamd  # noqa: F401  (package import path)
-from kltamd.shard import Band, band_edges, band_of, gather_merge_ref, gather_order_ref, owned_mask
+from kltamd.shard import Band, band_edges, band_of, gather_merge_ref, gather_order_ref, owned_mask, row_edges
 
 
 def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("H", [7, 100, 251, 480, 1080, 2160, 4320])
+def test_row_edges_c_equals_python(amd, H):
+    """klt_shard_band_edges (the C driver's bands) == kltamd.shard.row_edges
+    for every world size and several margins; the bands partition the rows,
+    and no rank builds more level-0 rows than with equal bands by more than a
+    tile (at 4K / 8 ranks / margin 64: 384 against 448)."""
+    from kltamd.shard import built_rows
+    for world in range(1, 17):
+        for margin in (0, 1, 16, 48, 64, 100):
+            e = (C.c_int * (world + 1))()
+            assert amd.klt_shard_band_edges(H, world, margin, e) == 0
+            py = row_edges(H, world, margin)
+            assert list(e) == py, (H, world, margin, list(e), py)
+            assert py[0] == 0 and py[-1] == H and all(b > a for a, b in zip(py, py[1:])) or H < world
+            eq = [r * H // world for r in range(world + 1)]
+            cost = max(built_rows(H, band_of(H, world, r, margin, py)) for r in range(world))
+            cost_eq = max(built_rows(H, band_of(H, world, r, margin, eq)) for r in range(world))
+            assert cost <= cost_eq + 32, (H, world, margin, cost, cost_eq)
+    assert max(built_rows(2160, band_of(2160, 8, r, 64, row_edges(2160, 8, 64))) for r in range(8)) == 384
+    e = (C.c_int * 20)()
+    assert amd.klt_shard_band_edges(2160, 17, 64, e) == -1 and amd.klt_shard_band_edges(0, 2, 64, e) == -1
 
 
 @pytest.mark.parametrize("H,world", [(480, 2), (2160, 8), (251, 3), (7, 4)])
@@ -139,7 +162,7 @@ def _select(gpu, frame, nfeat):
 
 
 class _Rank:
-    def __init__(self, gpu, dfr, H, W, world, rank, margin):
+    def __init__(self, gpu, dfr, H, W, world, rank, margin, edges=None):
         from kltamd.device import PyrDesc, TrackDesc
         self.gpu, self.dfr, self.H, self.W = gpu, dfr, H, W
         self.tc = gpu.KLTCreateTrackingContext()
@@ -150,7 +173,7 @@ class _Rank:
         self.pd, self.td = PyrDesc(), TrackDesc()
         gpu.klt_amd_pyr_desc(self.tc, W, H, self.tc.contents.nPyramidLevels, 1, C.byref(self.pd))
         gpu.klt_amd_track_desc(self.tc, C.byref(self.td))
-        self.band = band_of(H, world, rank, margin)
+        self.band = band_of(H, world, rank, margin, edges)
         self.rank = rank
         self.src = None
 
@@ -422,8 +445,9 @@ def c_sharded_sequence(gpu, frames, nfeat, world, chunk, margin, band_only=False
     dfr = torch.from_numpy(np.ascontiguousarray(np.stack(frames))).to(dev)
     x, y, v = (torch.from_numpy(a).to(dev) for a in _select(gpu, frames[0], nfeat))
     ranks, shards, keep = [], [], []
+    E = row_edges(H, world, margin)  # klt_shard_create's bands (klt_shard_band_edges)
     for r in range(world):
-        rk = _Rank(gpu, dfr, H, W, world, r, margin)
+        rk = _Rank(gpu, dfr, H, W, world, r, margin, E)
         if real_comm:
             assert world == 1
             uid = (C.c_ubyte * 128)()
@@ -434,7 +458,7 @@ def c_sharded_sequence(gpu, frames, nfeat, world, chunk, margin, band_only=False
         assert s
         lo, hi = C.c_int(), C.c_int()
         assert gpu.klt_shard_rows(s, C.byref(lo), C.byref(hi)) == 0
-        b = band_of(H, world, r, margin)
+        b = band_of(H, world, r, margin, E)
         assert lo.value <= b.row_lo and hi.value >= b.row_hi
         if band_only:  # only rows [lo, hi) of each frame on this rank, addressed as whole frames
             part = dfr[:, lo.value:hi.value].contiguous()
@@ -447,7 +471,7 @@ def c_sharded_sequence(gpu, frames, nfeat, world, chunk, margin, band_only=False
         ranks.append(rk)
         shards.append(s)
     redone, cur, rebuilt = [0], [0], [0]
-    bands = [band_of(H, world, r, margin) for r in range(world)]
+    bands = [band_of(H, world, r, margin, E) for r in range(world)]
 
     def whole(user, frames_out, stride_out):  # whole frames from frame cur[0] on
         frames_out[0] = dfr.data_ptr() + cur[0] * H * W
@@ -555,7 +579,8 @@ def test_eigen_rows_of_band_pyramid(gpu, world, rank, margin):
     H, W = frames[0].shape
     dev = torch.device("cuda", 0)
     dfr = torch.from_numpy(np.ascontiguousarray(np.stack(frames))).to(dev)
-    rk = _Rank(gpu, dfr, H, W, world, rank, margin)
+    E = row_edges(H, world, margin)  # the bands klt_shard_create_local uses below
+    rk = _Rank(gpu, dfr, H, W, world, rank, margin, E)
     tc = rk.tc.contents
     sd = SelectDesc(tc.window_width, tc.window_height, max(tc.borderx, tc.window_width // 2),
                     max(tc.bordery, tc.window_height // 2), tc.nSkippedPixels)
@@ -577,8 +602,8 @@ def test_eigen_rows_of_band_pyramid(gpu, world, rank, margin):
                                          W, H * W, 1, C.c_void_p(e.data_ptr()), C.c_void_p(e.data_ptr()),
                                          C.c_void_p(e.data_ptr()), 0, b.own_lo, b.own_hi, b.row_lo, b.row_hi,
                                          C.c_void_p(esc.data_ptr()), None, 0) == 0
-    lo = 0 if rank == 0 else rank * H // world
-    hi = H if rank == world - 1 else (rank + 1) * H // world
+    lo = 0 if rank == 0 else E[rank]
+    hi = H if rank == world - 1 else E[rank + 1]
     got = torch.full_like(full_map, -7)
     rc = gpu.klt_hip_min_eigen_rows(rk.ctx, C.byref(sd), lo, hi, C.c_void_p(got.data_ptr()), C.byref(nx),
                                     C.byref(ny), C.byref(j0), C.byref(j1))
@@ -812,7 +837,8 @@ def threaded_sequence(gpu, frames, nfeat, world, chunk, margin, replace=False, b
                         check(gpu, ctx, gpu.klt_hip_memcpy(ctx, C.c_void_p(dst + f * stride),
                                                            C.c_void_p(part[f].data_ptr()), nrows * W, D2D), "d2d")
                     gpu.klt_hip_sync(ctx)
-                src = BandFrames(T + 1, H, W, band_of(H, world, rank, margin), load, dev)
+                src = BandFrames(T + 1, H, W, band_of(H, world, rank, margin, row_edges(H, world, margin)), load,
+                                 dev)
             else:
                 src = FullFrames(dfr)
             seq = ShardedSequence(gpu, ctx, pd, td, src, x, y, v, rank, world,

@@ -51,7 +51,7 @@ def main():
     ap.add_argument("--worlds", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--margins", type=int, nargs="+", default=[64])
     ap.add_argument("--seed", type=int, default=2160)
-    ap.add_argument("--bands", choices=["equal", "features", "rows"], default="equal",
+    ap.add_argument("--bands", choices=["equal", "features", "rows"], default="rows",
                     help="band edges: equal rows, equal feature counts (balanced_edges), or equal level-0 rows "
                          "built incl. margins (row_edges)")
     ap.add_argument("--keep-states", default=None, help="save pass 1's record as DIR/states_w<N>.npz")
@@ -185,7 +185,8 @@ def main():
     for margin in a.margins:
         for world in a.worlds:
             edges = (balanced_edges(ys, vs, H, world) if a.bands == "features" else
-                     row_edges(H, world, margin) if a.bands == "rows" and world > 1 else None)
+                     row_edges(H, world, margin) if a.bands == "rows" else
+                     [r * H // world for r in range(world + 1)])
             gedges = band_edges(H, world, edges)
             ranks = [Rank(world, r, margin, edges) for r in range(1 if a.pass1_shared else world)]
             if a.pass1_shared:
