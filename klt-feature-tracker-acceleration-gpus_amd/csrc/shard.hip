@@ -768,10 +768,11 @@ KLT_API int klt_shard_track(klt_shard *s, const klt_hip_pyr_desc *pd, const klt_
 
 namespace {
 
-// rank r's own pixel rows [lo, hi) (rank 0 from row 0, the last to the bottom)
+// rank r's own pixel rows [lo, hi) of the shard's bands (rank 0 from row 0,
+// the last to the bottom)
 void own_rows(const klt_shard *s, int r, int *lo, int *hi) {
-  *lo = r == 0 ? 0 : (int)((long)r * s->nrows / s->world);
-  *hi = r == s->world - 1 ? s->nrows : (int)((long)(r + 1) * s->nrows / s->world);
+  *lo = r == 0 ? 0 : (int)s->edges[r];
+  *hi = r == s->world - 1 ? s->nrows : (int)s->edges[r + 1];
 }
 
 }  // namespace
