@@ -112,6 +112,21 @@ def row_edges(nrows: int, world: int, margin: int = DEFAULT_MARGIN, tile: int = 
     return best[1]
 
 
+def chunk_plan(t0: int, nframes: int, chunk: int, first: int | None = None) -> list[tuple[int, int]]:
+    """(first frame, frames) of each chunk over frames t0 .. t0+nframes-1: a
+    short first chunk (default chunk // 4) and then `chunk` each.  The first
+    chunk's pyramids cannot be built ahead: a short one starts the tracker
+    early, and the next chunk's build-ahead runs beside it (the pipeline
+    fill).  Deterministic, so every rank cuts the same chunks."""
+    first = max(1, chunk // 4) if first is None else max(1, min(first, chunk))
+    out, c0, end = [], t0, t0 + nframes
+    while c0 < end:
+        n = min(first if not out else chunk, end - c0)
+        out.append((c0, n))
+        c0 += n
+    return out
+
+
 def band_rows(nrows: int, band: Band, tile: int = 32, halo: int = 8) -> tuple[int, int]:
     """The u8 rows [ra, rb) a rank's band build reads: its level-0 build rows
     rounded out to whole tiles, plus the tiles' halo (k_pyr_l0 reads 5 rows
@@ -325,17 +340,19 @@ class ShardedSequence:
     (identical on every rank at the start), on the stream the context uses.
     edges: row boundaries of the bands; default row_edges(H, world, margin),
     the bands klt_shard_create uses (equal level-0 rows built per rank).
+    chunk / first_chunk: frames per band call; each run() starts with a
+    shorter chunk (chunk_plan, default chunk // 4) to fill the pipeline.
     all_gather(out, inp) gathers a device int32 tensor of every rank into out
     in rank order (torch.distributed.all_gather_into_tensor in production).
     """
 
     def __init__(self, lib, ctx, pd, td, frames: torch.Tensor, x, y, v, rank: int, world: int, all_gather,
-                 chunk: int = 64, margin: int = DEFAULT_MARGIN, edges=None):
+                 chunk: int = 64, margin: int = DEFAULT_MARGIN, edges=None, first_chunk: int | None = None):
         from .device import check
         self.lib, self.ctx, self.pd, self.td = lib, ctx, pd, td
         self.src = frames if isinstance(frames, (FullFrames, BandFrames)) else FullFrames(frames)
         self.x, self.y, self.v = x, y, v
-        self.rank, self.world, self.chunk = rank, world, chunk
+        self.rank, self.world, self.chunk, self.first_chunk = rank, world, chunk, first_chunk
         H, W = self.src.H, self.src.W
         self.H, self.W = H, W
         # default: the C driver's bands (klt_shard_create), equal built rows per rank
@@ -392,7 +409,7 @@ class ShardedSequence:
         queued before chunk c's verdict is read; an escaped chunk c is redone
         and chunk c+1 runs again."""
         end = t0 + nframes
-        chunks = [(c0, min(self.chunk, end - c0)) for c0 in range(t0, end, self.chunk)]
+        chunks = chunk_plan(t0, nframes, self.chunk, self.first_chunk)
         k = self.xch.order(self.x, self.y, self.v, self.escape)  # the first chunk's ownership, start state, counts
         prev = None  # (c0, n, save index) of the chunk whose verdict is still unread
         i = 0

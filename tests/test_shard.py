@@ -25,6 +25,19 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+def test_chunk_plan():
+    """chunk_plan: a short first chunk (chunk // 4 by default), then whole
+    chunks; contiguous and covering the frames exactly."""
+    from kltamd.shard import chunk_plan
+    assert chunk_plan(1, 1000, 64)[:3] == [(1, 16), (17, 64), (81, 64)]
+    assert chunk_plan(1, 1000, 64, 64)[:2] == [(1, 64), (65, 64)]
+    assert chunk_plan(5, 3, 64) == [(5, 3)] and chunk_plan(5, 0, 64) == [] and chunk_plan(1, 2, 1) == [(1, 1), (2, 1)]
+    for t0, n, c, f in [(1, 1000, 64, None), (3, 129, 32, 5), (0, 7, 4, 100), (2, 65, 64, 1)]:
+        p = chunk_plan(t0, n, c, f)
+        assert p[0][0] == t0 and sum(k for _, k in p) == n and all(k <= c for _, k in p)
+        assert all(a0 + k == b0 for (a0, k), (b0, _) in zip(p, p[1:]))
+
+
 @pytest.mark.parametrize("H", [7, 100, 251, 480, 1080, 2160, 4320])
 def test_row_edges_c_equals_python(amd, H):
     """klt_shard_band_edges (the C driver's bands) == kltamd.shard.row_edges

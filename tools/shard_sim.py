@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--features", type=int, default=20000)
     ap.add_argument("--frames", type=int, default=129, help="frames incl. the selection frame")
     ap.add_argument("--chunk", type=int, default=64)
+    ap.add_argument("--first-chunk", type=int, default=None, help="first chunk's frames (default chunk // 4)")
     ap.add_argument("--worlds", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--margins", type=int, nargs="+", default=[64])
     ap.add_argument("--seed", type=int, default=2160)
@@ -67,8 +68,8 @@ def main():
     import torch
     import kltamd
     from kltamd.device import PyrDesc, Timing, TrackDesc, check, use_torch_stream
-    from kltamd.shard import (FullFrames, ShardedSequence, balanced_edges, band_edges, band_of, row_edges,
-                              slot_words)
+    from kltamd.shard import (FullFrames, ShardedSequence, balanced_edges, band_edges, band_of, chunk_plan,
+                              row_edges, slot_words)
     from kltabi import fl_to_arrays, u8ptr
 
     lib = kltamd.load()
@@ -90,7 +91,7 @@ def main():
     lib.KLTFreeTrackingContext(tc0)
 
     T = a.frames - 1
-    chunks = [(c0, min(a.chunk, 1 + T - c0)) for c0 in range(1, 1 + T, a.chunk)]
+    chunks = chunk_plan(1, T, a.chunk, a.first_chunk)  # the production driver's plan
 
     def descs(tc):
         pd, td = PyrDesc(), TrackDesc()
@@ -126,7 +127,7 @@ def main():
             x, y, v = xs.clone(), ys.clone(), vs.clone()
             k[0] = 0
             seq = ShardedSequence(lib, ctx, pd, td, FullFrames(fr), x, y, v, a.rank, world, replay_gather,
-                                  chunk=a.chunk, margin=margin, edges=edges)
+                                  chunk=a.chunk, margin=margin, edges=edges, first_chunk=a.first_chunk)
             seq.xch.timing = rep == 2
             seq.begin(0)
             lib.klt_hip_set_timing(ctx, 1 if rep == 3 else 0)
@@ -263,7 +264,8 @@ def main():
                 for r in range(world):
                     cmd = [sys.executable, __file__, "--replay", f, "--rank", str(r), "--width", str(W), "--height",
                            str(H), "--features", str(NF), "--frames", str(a.frames), "--chunk", str(a.chunk),
-                           "--seed", str(a.seed)]
+                           "--seed", str(a.seed)] + ([] if a.first_chunk is None else
+                                                     ["--first-chunk", str(a.first_chunk)])
                     res = subprocess.run(cmd, check=True, capture_output=True, text=True)
                     reps.append(json.loads(res.stdout.strip().splitlines()[-1]))
             frames = sum(n for _, n in chunks)
