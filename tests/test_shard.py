@@ -26,11 +26,11 @@ def _free_port() -> int:
 
 
 def test_chunk_plan():
-    """chunk_plan: a short first chunk (chunk // 4 by default), then whole
+    """chunk_plan: the first chunk's length (default: chunk), then whole
     chunks; contiguous and covering the frames exactly."""
     from kltamd.shard import chunk_plan
-    assert chunk_plan(1, 1000, 64)[:3] == [(1, 16), (17, 64), (81, 64)]
-    assert chunk_plan(1, 1000, 64, 64)[:2] == [(1, 64), (65, 64)]
+    assert chunk_plan(1, 1000, 64, 16)[:3] == [(1, 16), (17, 64), (81, 64)]
+    assert chunk_plan(1, 1000, 64)[:2] == [(1, 64), (65, 64)] and chunk_plan(1, 1000, 64)[-1] == (961, 40)
     assert chunk_plan(5, 3, 64) == [(5, 3)] and chunk_plan(5, 0, 64) == [] and chunk_plan(1, 2, 1) == [(1, 1), (2, 1)]
     for t0, n, c, f in [(1, 1000, 64, None), (3, 129, 32, 5), (0, 7, 4, 100), (2, 65, 64, 1)]:
         p = chunk_plan(t0, n, c, f)

@@ -48,7 +48,7 @@ def main():
     ap.add_argument("--features", type=int, default=20000)
     ap.add_argument("--frames", type=int, default=129, help="frames incl. the selection frame")
     ap.add_argument("--chunk", type=int, default=64)
-    ap.add_argument("--first-chunk", type=int, default=None, help="first chunk's frames (default chunk // 4)")
+    ap.add_argument("--first-chunk", type=int, default=None, help="first chunk's frames (default: chunk)")
     ap.add_argument("--worlds", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--margins", type=int, nargs="+", default=[64])
     ap.add_argument("--seed", type=int, default=2160)
