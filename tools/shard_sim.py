@@ -201,7 +201,7 @@ def main():
                 rk.begin(0)
             ctx = ranks[0].ctx
             x, y, v = xs.clone(), ys.clone(), vs.clone()
-            redone, slots_rec = 0, []
+            redone, slots_rec, owned_rec = 0, [], []
             work = torch.zeros(lib.klt_hip_gather_work_ints(NF, world), dtype=torch.int32, device=dev)
             E = (C.c_float * (world + 1))(*gedges)
             flags = torch.zeros(2, dtype=torch.int32, device=dev)
@@ -230,7 +230,8 @@ def main():
                 check(lib, ctx, lib.klt_hip_gather_order(ctx, None, C.c_void_p(state[1].data_ptr()),
                                                          C.c_void_p(state[2].data_ptr()), NF, E, world,
                                                          C.c_void_p(work.data_ptr()), None, None, None), "order")
-                S = max(1, int(work[NF:NF + world].max().item()))
+                owned_rec.append(work[NF:NF + world].cpu().tolist())  # each rank's features at the chunk's start
+                S = max(1, int(max(owned_rec[-1])))
                 Wd = slot_words(S)
                 slots = torch.zeros(world * Wd, dtype=torch.int32, device=dev)
                 for r, ((xr, yr, vr), esc) in enumerate(zip(outs, escs)):
@@ -285,6 +286,7 @@ def main():
                    "per_rank": [{"rank": i, "band_rows": [band_of(H, world, i, margin, edges).row_lo,
                                                           band_of(H, world, i, margin, edges).row_hi],
                                  "wall_us_per_frame": rr["us_per_frame"],
+                                 "owned_features_mean": float(np.mean([c[i] for c in owned_rec])),
                                  "chunk_us_mean": float(np.mean(rr["chunk_us"])),
                                  "replay_kernels_us_per_frame": rr["kernels_us_per_frame"], "redone": rr["redone"]}
                                 for i, rr in enumerate(reps)],
