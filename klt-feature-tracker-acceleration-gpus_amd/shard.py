@@ -128,6 +128,64 @@ def chunk_plan(t0: int, nframes: int, chunk: int, first: int | None = None) -> l
     return out
 
 
+def cost_edges(y: torch.Tensor, v: torch.Tensor, nrows: int, world: int, margin: int = DEFAULT_MARGIN,
+               feat_rows: float = 0.066, tile: int = 32) -> list[int]:
+    """Row boundaries on tile multiples that minimise the largest rank cost
+    built_rows + feat_rows * (live features owned), from the list (y, v) at
+    the start: a rank's level-0 build and its tracker both grow with what it
+    holds.  feat_rows prices one feature in level-0 rows (0.066: one 32-row
+    tile of a 4K band build per ~480 features in tools/shard_sim.py's
+    per-rank times).  Binary search on the cost, each rank taking the
+    longest band that fits.  Deterministic in (y, v): every rank computes
+    the same edges from the same list."""
+    if world < 2:
+        return [0, nrows]
+    ys = torch.sort(y[v >= 0].float().cpu()).values
+    bounds = list(range(0, nrows, tile)) + [nrows]  # candidate edges
+
+    def owned(lo, hi, first, last):
+        a = 0 if first else int(torch.searchsorted(ys, float(lo)).item())
+        b = ys.numel() if last else int(torch.searchsorted(ys, float(hi)).item())
+        return b - a
+
+    def cost(lo, hi, r):
+        e = [0] * (world + 1)
+        e[r], e[r + 1], e[world] = lo, hi, nrows
+        bd = Band(float("-inf") if r == 0 else float(lo), float("inf") if r == world - 1 else float(hi),
+                  max(0, lo - margin), min(nrows, hi + margin))
+        return built_rows(nrows, bd, tile) + feat_rows * owned(lo, hi, r == 0, r == world - 1)
+
+    def fit(T):
+        lo, edges = 0, [0]
+        for r in range(world - 1):
+            best = None
+            for hi in bounds:
+                if hi <= lo or hi > nrows - (world - 1 - r) * tile:  # a tile left for each rank after r
+                    continue
+                if cost(lo, hi, r) <= T:
+                    best = hi
+                else:
+                    break
+            if best is None:
+                return None
+            edges.append(best)
+            lo = best
+        if cost(lo, nrows, world - 1) > T:
+            return None
+        return edges + [nrows]
+
+    lo_t, hi_t = 0.0, float(nrows + feat_rows * ys.numel() + 2 * margin + tile)
+    best = fit(hi_t)
+    for _ in range(40):
+        mid = 0.5 * (lo_t + hi_t)
+        e = fit(mid)
+        if e is not None:
+            best, hi_t = e, mid
+        else:
+            lo_t = mid
+    return best if best is not None else row_edges(nrows, world, margin, tile)
+
+
 def band_rows(nrows: int, band: Band, tile: int = 32, halo: int = 8) -> tuple[int, int]:
     """The u8 rows [ra, rb) a rank's band build reads: its level-0 build rows
     rounded out to whole tiles, plus the tiles' halo (k_pyr_l0 reads 5 rows

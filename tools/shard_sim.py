@@ -52,9 +52,9 @@ def main():
     ap.add_argument("--worlds", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--margins", type=int, nargs="+", default=[64])
     ap.add_argument("--seed", type=int, default=2160)
-    ap.add_argument("--bands", choices=["equal", "features", "rows"], default="rows",
+    ap.add_argument("--bands", choices=["equal", "features", "rows", "cost"], default="rows",
                     help="band edges: equal rows, equal feature counts (balanced_edges), or equal level-0 rows "
-                         "built incl. margins (row_edges)")
+                         "built incl. margins (row_edges), or rows built and features owned together (cost_edges)")
     ap.add_argument("--keep-states", default=None, help="save pass 1's record as DIR/states_w<N>.npz")
     ap.add_argument("--pass1-shared", action="store_true",
                     help="pass 1 through one device context for every rank, each chunk started from a "
@@ -69,7 +69,7 @@ def main():
     import kltamd
     from kltamd.device import PyrDesc, Timing, TrackDesc, check, use_torch_stream
     from kltamd.shard import (FullFrames, ShardedSequence, balanced_edges, band_edges, band_of, chunk_plan,
-                              row_edges, slot_words)
+                              cost_edges, row_edges, slot_words)
     from kltabi import fl_to_arrays, u8ptr
 
     lib = kltamd.load()
@@ -180,13 +180,15 @@ def main():
 
     out = {"workload": f"{W}x{H}, {NF} features, {T} tracked frames, {a.chunk}-frame chunks"
                        + {"equal": "", "features": ", bands of equal feature counts",
-                          "rows": ", bands of equal built rows"}[a.bands],
+                          "rows": ", bands of equal built rows",
+                          "cost": ", bands of equal built rows + features owned"}[a.bands],
            "exchange_us_assumed_per_chunk": a.exchange_us, "runs": []}
     base = None
     for margin in a.margins:
         for world in a.worlds:
             edges = (balanced_edges(ys, vs, H, world) if a.bands == "features" else
                      row_edges(H, world, margin) if a.bands == "rows" else
+                     cost_edges(ys, vs, H, world, margin) if a.bands == "cost" else
                      [r * H // world for r in range(world + 1)])
             gedges = band_edges(H, world, edges)
             ranks = [Rank(world, r, margin, edges) for r in range(1 if a.pass1_shared else world)]
