@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--worlds", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--margins", type=int, nargs="+", default=[64])
     ap.add_argument("--seed", type=int, default=2160)
+    ap.add_argument("--edges", default=None, help="explicit band edges for the largest world, comma-separated "
+                    "(overrides --bands there)")
     ap.add_argument("--bands", choices=["equal", "features", "rows", "cost"], default="rows",
                     help="band edges: equal rows, equal feature counts (balanced_edges), or equal level-0 rows "
                          "built incl. margins (row_edges), or rows built and features owned together (cost_edges)")
@@ -186,7 +188,9 @@ def main():
     base = None
     for margin in a.margins:
         for world in a.worlds:
-            edges = (balanced_edges(ys, vs, H, world) if a.bands == "features" else
+            explicit = [int(e) for e in a.edges.split(",")] if a.edges else None
+            edges = (explicit if explicit and len(explicit) == world + 1 else
+                     balanced_edges(ys, vs, H, world) if a.bands == "features" else
                      row_edges(H, world, margin) if a.bands == "rows" else
                      cost_edges(ys, vs, H, world, margin) if a.bands == "cost" else
                      [r * H // world for r in range(world + 1)])
