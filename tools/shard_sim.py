@@ -219,8 +219,8 @@ def main():
             for ci, (c0, n) in enumerate(chunks):
                 nn = chunks[ci + 1][1] if ci + 1 < len(chunks) else 0
                 state = (x.clone(), y.clone(), v.clone())
-                sched[ci + 2] = (cost_edges(lib, row_hist(state[1], state[2], H).tolist(), H, world, margin, edges)
-                                 if not a.no_rebalance and world > 1 else sched[ci + 1])
+                if not a.no_rebalance and world > 1:
+                    sched[ci + 2] = cost_edges(lib, row_hist(state[1], state[2], H).tolist(), H, world, margin, edges)
                 E = (C.c_float * (world + 1))(*band_edges(H, world, sched[ci]))
                 for r, rk in enumerate(ranks):
                     rk.band = band_of(H, world, r, margin, sched[ci])
