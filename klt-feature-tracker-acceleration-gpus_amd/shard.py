@@ -555,9 +555,9 @@ class ShardedSequence:
             self._band_call(src.band(c0), src.stride, n, self.band.row_lo, self.band.row_hi,
                             src.band(c0 + n) if nn > 0 else 0, nn)
             S = self.xch.slot_size()  # this chunk's counts, with the previous chunk's verdict
-            # chunk i+2's bands from the state at chunk i's start (static: chunk i+1's)
-            sched[i + 2] = (cost_edges(self.lib, self.xch.h_hist.tolist(), H, world, self.margin, self.base_edges)
-                            if self.rebalance else sched[i + 1])
+            if self.rebalance:  # chunk i+2's bands from the state at chunk i's start
+                sched[i + 2] = cost_edges(self.lib, self.xch.h_hist.tolist(), H, world, self.margin,
+                                          self.base_edges)
             if prev is not None:
                 esc, bad = self.xch.verdict()
                 assert bad == 0, "exchange failed"
