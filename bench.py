@@ -427,7 +427,7 @@ def run_sharded(args, world, rank, dev) -> None:
 
     import kltamd
     from kltamd.device import EXACT, FAST, PyrDesc, TrackDesc, check, use_torch_stream
-    from kltamd.shard import MAX_SHIFT, BandFrames, ShardedSequence, band_of, row_edges
+    from kltamd.shard import BandFrames, ShardedSequence, band_of, row_edges
 
     lib = kltamd.load()
     lib.KLTSetVerbosity(0)
@@ -443,8 +443,7 @@ def run_sharded(args, world, rank, dev) -> None:
               "synth")
 
     edges = row_edges(H, world, args.margin)  # equal level-0 rows built per rank (klt_shard_create's bands)
-    # the rows this rank holds: its band moved by up to MAX_SHIFT rows (ShardedSequence rebalances)
-    frames = BandFrames(nframes, H, W, band_of(H, world, rank, args.margin + MAX_SHIFT, edges), load, dev)
+    frames = BandFrames(nframes, H, W, band_of(H, world, rank, args.margin, edges), load, dev)
     torch.cuda.synchronize()
     f0 = np.empty((H, W), np.uint8)  # frame 0 whole, for the selection every rank makes
     lib.klt_synth_frame(args.seed, 0, W, H, f0.ctypes.data)

@@ -326,13 +326,6 @@ int klt_hip_track_frames_host(klt_hip_ctx *ctx, const klt_hip_pyr_desc *pdesc,
    alone.  Default 0; kltamd.shard.ShardedSequence sets it (its frames are
    loaded up front). */
 int klt_hip_set_ahead_ready(klt_hip_ctx *ctx, int ready);
-/* the band (own_lo <= y < own_hi, level-0 rows [row_lo, row_hi)) whose
-   pyramids the next klt_hip_track_frames_band call builds ahead for the chunk
-   after it, instead of that call's own band -- for a driver that moves its
-   bands between chunks (kltamd.shard.ShardedSequence, rebalance); consumed by
-   that call.  The call after uses them when it comes with exactly those
-   frames and rows. */
-int klt_hip_set_next_band(klt_hip_ctx *ctx, float own_lo, float own_hi, int row_lo, int row_hi);
 int klt_hip_track_frames_band(klt_hip_ctx *ctx, const klt_hip_pyr_desc *pdesc,
                               const klt_hip_track_desc *tdesc, const unsigned char *frames, long pitch,
                               long stride, int nframes, float *x, float *y, int *val, int n, float own_lo,
@@ -404,7 +397,6 @@ int klt_hip_select_map(klt_hip_ctx *ctx, int ncols, int nrows, const klt_hip_sel
    flags[1] = the failures summed (a slot shorter than its count counts as
    one; nothing is unpacked then).  All three queue on the context's stream. */
 #define KLT_HIP_GATHER_MAX_RANKS 16
-#define KLT_HIP_GATHER_HIST_BINS 256 /* host_hist bins at most */
 #define KLT_HIP_GATHER_SLOT_WORDS(S) (4 + 3 * (long)(S))
 /* gather_order options, each may be NULL: save (device int[3n]) receives a
    copy of x0 | y0 | v0 bit patterns (the chunk-start state a redo restarts
@@ -412,15 +404,10 @@ int klt_hip_select_map(klt_hip_ctx *ctx, int ncols, int nrows, const klt_hip_sel
    (two: per-block counts, then places; no cross-workgroup handshake);
    host_counts (pinned host int[world]) and gather_unpack's host_flags (pinned
    host int[2]) receive the counts / flags from the kernels themselves, to be
-   read once an event recorded after the launch has completed; host_hist
-   (pinned host int[hist_bins], hist_bins <= KLT_HIP_GATHER_HIST_BINS)
-   receives the live features of the ordered state per hist_rows-row bin of
-   y (bin (int)y / hist_rows clamped to the last; y < 0 and NaN in bin 0), the
-   same way -- what a driver balances its next bands on */
+   read once an event recorded after the launch has completed */
 long klt_hip_gather_work_ints(int n, int world);
 int klt_hip_gather_order(klt_hip_ctx *ctx, const float *x0, const float *y0, const int *v0, int n, const float *edges,
-                         int world, int *work, int *save, int *escape, int *host_counts, int hist_rows,
-                         int hist_bins, int *host_hist);
+                         int world, int *work, int *save, int *escape, int *host_counts);
 int klt_hip_gather_pack(klt_hip_ctx *ctx, const float *x, const float *y, const int *val, const int *work, int n,
                         int world, int rank, const int *escape, int nfail, int *slot, int S);
 int klt_hip_gather_unpack(klt_hip_ctx *ctx, const int *slots, int nslots, int first_rank, const int *work, int n,
@@ -430,8 +417,7 @@ int klt_hip_gather_unpack(klt_hip_ctx *ctx, const int *slots, int nslots, int fi
    two chunks' trackers; work is read for the unpack and rewritten */
 int klt_hip_gather_unpack_order(klt_hip_ctx *ctx, const int *slots, int nslots, int first_rank, int *work, int n,
                                 int world, int S, float *x, float *y, int *val, int *flags, int *host_flags,
-                                const float *edges, int *save, int *escape, int *host_counts, int hist_rows,
-                                int hist_bins, int *host_hist);
+                                const float *edges, int *save, int *escape, int *host_counts);
 
 /* synthetic frames t0..t0+n-1 (include/klt_synth.h) into device memory */
 int klt_hip_synth_frames(klt_hip_ctx *ctx, unsigned long long seed, int t0, int n, int ncols,

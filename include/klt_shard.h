@@ -51,16 +51,6 @@ typedef int (*klt_shard_frames_fn)(void *user, const unsigned char **frames, lon
    edges[r+1] (below edges[1] for rank 0, from edges[world-1] on for the
    last).  0 on success, -1 for bad arguments (world > 16). */
 int klt_shard_band_edges(int nrows, int world, int margin, int *edges);
-/* bands balanced on rows built and features owned (host only): edges[0..world]
-   on multiples of hist_rows within max_shift rows of base[0..world],
-   minimising the largest 1000 * (level-0 rows built) + feat_milli * (live
-   features owned), owned counted from hist[nbins] (live features per
-   hist_rows-row bin of y, as klt_hip_gather_order's host_hist gives it).
-   0 on success, 1 when no edges fit the shift bound (base is returned), -1
-   for bad arguments.  kltamd.shard.ShardedSequence moves its bands with it
-   between chunks (rebalance). */
-int klt_shard_cost_edges(const int *hist, int nbins, int hist_rows, int nrows, int world, int margin,
-                         int feat_milli, const int *base, int max_shift, int *edges);
 /* a new communicator id (ncclGetUniqueId); 0 on success */
 int klt_shard_unique_id(unsigned char id[KLT_SHARD_ID_BYTES]);
 /* rank `rank` of `world` on the device of `ctx` (ncclCommInitRank; every

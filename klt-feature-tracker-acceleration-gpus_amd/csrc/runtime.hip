@@ -226,13 +226,6 @@ struct klt_hip_ctx {
   // caller queues between two chunks (klt_hip_set_ahead_ready)
   int ahead_ready = 0;
   hipEvent_t ev_go = nullptr;
-  // klt_hip_set_next_band: the band the next band call's build-ahead builds
-  // (a driver that moves its bands between chunks); consumed by that call
-  struct {
-    int set = 0;
-    float own[2] = {0.0f, 0.0f};
-    int row_lo = 0, row_hi = 0;
-  } next_band;
   int serial_frames = 1;  // klt_hip_track_frames: 1 builds and tracks on one stream (default: the
                           // tracker and the pyramid kernels compete for the same CUs; overlap buys ~3 %)
   int *d_perm = nullptr;
@@ -1183,7 +1176,6 @@ KLT_API int klt_hip_ctx_reset(klt_hip_ctx *c) {
   c->track_impl = 0;
   c->serial_frames = 1;
   c->ahead_ready = 0;
-  c->next_band.set = 0;
   c->prof = nullptr;
   c->frames_ready = false;
   c->pre.bank = -1;
@@ -2095,26 +2087,18 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     } else {
       HIPCHK(c, hipStreamWaitEvent(c->pstream, c->ev_bfree[bj], 0));
     }
-    // the next chunk's band: this one, or the one klt_hip_set_next_band gave
-    BandSpec nb = *band;
-    if (c->next_band.set) {
-      nb.own[0] = c->next_band.own[0];
-      nb.own[1] = c->next_band.own[1];
-      nb.row_lo = c->next_band.row_lo;
-      nb.row_hi = c->next_band.row_hi;
-    }
     int p0 = 0, p1 = 1 << 30;
-    band_planes(nb, p0, p1);
-    if (build_fused_bank(c, c->bank[bj], pd, band->next, pitch, stride, Fn, c->pstream, nb.row_lo, nb.row_hi, p0,
-                         p1, bil))
+    band_planes(*band, p0, p1);
+    if (build_fused_bank(c, c->bank[bj], pd, band->next, pitch, stride, Fn, c->pstream, band->row_lo, band->row_hi,
+                         p0, p1, bil))
       return -1;
     HIPCHK(c, hipEventRecord(c->ev_bbuilt[bj], c->pstream));
     c->pre.bank = bj;
     c->pre.src = band->next;
     c->pre.F = Fn;
     c->pre.stride = stride;
-    c->pre.row_lo = nb.row_lo;
-    c->pre.row_hi = nb.row_hi;
+    c->pre.row_lo = band->row_lo;
+    c->pre.row_hi = band->row_hi;
     c->pre.il = bil;
   }
   return 0;
@@ -2321,21 +2305,8 @@ KLT_API int klt_hip_track_frames_band(klt_hip_ctx *c, const klt_hip_pyr_desc *pd
                                       int next_nframes) {
   if (!escape) return fail(c, "track_frames_band: null escape flag");
   BandSpec bs{{own_lo, own_hi}, row_lo, row_hi, escape, next_frames, next_nframes};
-  const int rc = track_frames_impl(c, pd, td, frames, pitch, stride, nframes, nframes > 0 ? nframes : 1, x, y, val,
-                                   n, nullptr, nullptr, nullptr, 0, &bs);
-  c->next_band.set = 0;  // for this call only
-  return rc;
-}
-
-KLT_API int klt_hip_set_next_band(klt_hip_ctx *c, float own_lo, float own_hi, int row_lo, int row_hi) {
-  if (!c) return -1;
-  if (row_lo < 0 || row_hi < row_lo) return fail(c, "set_next_band: bad rows [%d, %d)", row_lo, row_hi);
-  c->next_band.set = 1;
-  c->next_band.own[0] = own_lo;
-  c->next_band.own[1] = own_hi;
-  c->next_band.row_lo = row_lo;
-  c->next_band.row_hi = row_hi;
-  return 0;
+  return track_frames_impl(c, pd, td, frames, pitch, stride, nframes, nframes > 0 ? nframes : 1, x, y, val, n,
+                           nullptr, nullptr, nullptr, 0, &bs);
 }
 
 KLT_API int klt_hip_min_eigen(klt_hip_ctx *c, int s, const klt_hip_select_desc *d, int *vals, int *nx,

@@ -144,30 +144,14 @@ struct GatherEdges {
 // save (optional): the state (after the unpack) also copied to save[0..3n)
 // (the redo's start state) and *escape zeroed; host_counts (optional, pinned
 // host memory): the counts written there too, read behind an event with no
-// copy-engine hand-off on the stream.  H.host (optional, pinned host
-// memory): the live features per H.rows-row bin of y (bin (int)y / H.rows,
-// clamped to [0, H.nbins); NaN and y < 0 in bin 0) -- what a driver balances
-// its next bands on (kltamd/shard.py).  work: code[n] | counts[world] |
-// bcount[blocks][world] | bhist[blocks][kHistMax].
+// copy-engine hand-off on the stream.  work: code[n] | counts[world] |
+// bcount[blocks][world].
 constexpr int kOrderThreads = 256, kOrderR = 4, kOrderBlock = kOrderThreads * kOrderR;
 constexpr int kOrderWaves = kOrderThreads / 64;
-constexpr int kHistMax = KLT_HIP_GATHER_HIST_BINS;
 
 __host__ __device__ inline int gather_blocks(int n) { return n > 0 ? (n + kOrderBlock - 1) / kOrderBlock : 1; }
 __host__ __device__ inline long gather_work_ints(int n, int world) {
-  return (long)n + world + (long)gather_blocks(n) * (world + kHistMax);
-}
-
-struct Hist {
-  int rows, nbins;
-  int *host;
-};
-
-__device__ __forceinline__ int hist_bin(float y, const Hist &H) {
-  if (!(y >= 0.0f)) return 0;  // NaN too
-  if (y >= (float)H.rows * (float)H.nbins) return H.nbins - 1;
-  const int b = (int)y / H.rows;
-  return b < H.nbins ? b : H.nbins - 1;
+  return (long)n + world + (long)gather_blocks(n) * world;
 }
 
 // UNPACK: feature i first from its owner's slot (U.slots ..., at the place
@@ -181,18 +165,14 @@ struct Unpack {
 template <bool UNPACK>
 __device__ __forceinline__ void count_block(int n, const GatherEdges &E, int *__restrict__ code,
                                             int *__restrict__ bcount, float *__restrict__ x0, float *__restrict__ y0,
-                                            int *__restrict__ v0, int *__restrict__ save, const Unpack U,
-                                            const Hist H, int *__restrict__ bhist) {
+                                            int *__restrict__ v0, int *__restrict__ save, const Unpack U) {
   __shared__ int wc[kOrderR][kOrderWaves][KLT_HIP_GATHER_MAX_RANKS];
-  __shared__ int hs[kHistMax];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, world = E.world;
   const int p0 = blockIdx.x * kOrderBlock;
   int nbits = 0;
   while ((1 << nbits) <= world) ++nbits;  // owner codes 0..world-1, and 2^nbits - 1 = nobody
   const int nobody = (1 << nbits) - 1;
   const unsigned long long lt = (1ull << lane) - 1ull;
-  if (H.host)
-    for (int k = tid; k < H.nbins; k += kOrderThreads) hs[k] = 0;  // ordered before use by the barrier below
   int q[kOrderR], mine[kOrderR];
   {
     float xs[kOrderR], ys[kOrderR];
@@ -248,12 +228,6 @@ __device__ __forceinline__ void count_block(int n, const GatherEdges &E, int *__
             break;
           }
     }
-    if (H.host) {
-      __syncthreads();  // the bins are zero
-#pragma unroll
-      for (int k = 0; k < kOrderR; ++k)
-        if (p0 + k * kOrderThreads + tid < n && vs[k] >= 0) atomicAdd(&hs[hist_bin(ys[k], H)], 1);
-    }
   }
 #pragma unroll
   for (int k = 0; k < kOrderR; ++k) {
@@ -280,8 +254,6 @@ __device__ __forceinline__ void count_block(int n, const GatherEdges &E, int *__
     bcount[blockIdx.x * world + tid] = acc;
   }
   __syncthreads();
-  if (H.host)
-    for (int k = tid; k < H.nbins; k += kOrderThreads) bhist[blockIdx.x * kHistMax + k] = hs[k];
 #pragma unroll
   for (int k = 0; k < kOrderR; ++k) {
     const int i = p0 + k * kOrderThreads + tid;
@@ -293,12 +265,11 @@ __global__ __launch_bounds__(kOrderThreads) void k_gather_count(const float *__r
                                                                 const float *__restrict__ y0,
                                                                 const int *__restrict__ v0, int n, GatherEdges E,
                                                                 int *__restrict__ work, int *__restrict__ save,
-                                                                int *__restrict__ escape, Hist H) {
+                                                                int *__restrict__ escape) {
   __builtin_amdgcn_s_setprio(3);  // between two trackers: issue ahead of co-resident pyramid waves
   if (blockIdx.x == 0 && threadIdx.x == 0 && escape) *escape = 0;
   count_block<false>(n, E, work, work + n + E.world, const_cast<float *>(x0), const_cast<float *>(y0),
-                     const_cast<int *>(v0), save, Unpack{}, H,
-                     work + n + E.world + (long)gather_blocks(n) * E.world);
+                     const_cast<int *>(v0), save, Unpack{});
 }
 
 // gather_unpack and the next chunk's count in one launch: each feature from
@@ -307,7 +278,7 @@ __global__ __launch_bounds__(kOrderThreads) void k_gather_count(const float *__r
 __global__ __launch_bounds__(kOrderThreads) void k_gather_unpack_count(
     const int *__restrict__ slots, int nslots, int r0, int n, int S, float *__restrict__ x, float *__restrict__ y,
     int *__restrict__ v, int *__restrict__ flags, int *__restrict__ host_flags, GatherEdges E, int *__restrict__ work,
-    int *__restrict__ save, int *__restrict__ escape, Hist H) {
+    int *__restrict__ save, int *__restrict__ escape) {
   __builtin_amdgcn_s_setprio(3);
   const long words = kGatherHdr + 3L * S;
   int esc = 0, bad = 0;
@@ -325,14 +296,13 @@ __global__ __launch_bounds__(kOrderThreads) void k_gather_unpack_count(
     }
     if (escape) *escape = 0;
   }
-  count_block<true>(n, E, work, work + n + E.world, x, y, v, save, Unpack{slots, nslots, r0, S, bad, words}, H,
-                    work + n + E.world + (long)gather_blocks(n) * E.world);
+  count_block<true>(n, E, work, work + n + E.world, x, y, v, save, Unpack{slots, nslots, r0, S, bad, words});
 }
 
 // Block b: its places moved past the owners' features of blocks 0..b-1
 // (b * world counts summed in LDS: a few hundred words at 20k features).
 __global__ __launch_bounds__(kOrderThreads) void k_gather_place(int n, int world, int *__restrict__ work,
-                                                                int *__restrict__ host_counts, Hist H) {
+                                                                int *__restrict__ host_counts) {
   __builtin_amdgcn_s_setprio(3);
   __shared__ int pre[KLT_HIP_GATHER_MAX_RANKS];
   const int tid = threadIdx.x, b = blockIdx.x, last = b == (int)gridDim.x - 1;
@@ -346,14 +316,6 @@ __global__ __launch_bounds__(kOrderThreads) void k_gather_place(int n, int world
     const int t = pre[tid] + bcount[b * world + tid];
     counts[tid] = t;
     if (host_counts) host_counts[tid] = t;
-  }
-  if (last && H.host) {  // the row histogram: every block's bins summed
-    const int *bhist = work + n + world + (long)gridDim.x * world;
-    for (int k = tid; k < H.nbins; k += kOrderThreads) {
-      int t = 0;
-      for (int bb = 0; bb < (int)gridDim.x; ++bb) t += bhist[bb * kHistMax + k];
-      H.host[k] = t;
-    }
   }
   if (b == 0) return;
   const int p0 = b * kOrderBlock;
@@ -461,7 +423,7 @@ int fail_count(const klt_shard *s, int failed) {
 // downloaded behind an event (read after the band call is queued)
 int order_counts(klt_shard *s, hipStream_t st, int n) {
   if (klt_hip_gather_order(s->ctx, nullptr, s->d_y0, s->d_v0, n, s->edges.data(), s->world, s->d_work, nullptr,
-                           nullptr, s->h_flag + 2, 0, 0, nullptr))
+                           nullptr, s->h_flag + 2))
     return sfail(s, "%s", klt_hip_last_error(s->ctx));
   SHIP(s, hipEventRecord(s->ev_counts, st));
   return 0;
@@ -517,11 +479,9 @@ int agree(klt_shard *s, hipStream_t st, int failed, int *failed_ranks) {
 KLT_API long klt_hip_gather_work_ints(int n, int world) { return gather_work_ints(n, world); }
 
 KLT_API int klt_hip_gather_order(klt_hip_ctx *ctx, const float *x0, const float *y0, const int *v0, int n,
-                                 const float *edges, int world, int *work, int *save, int *escape, int *host_counts,
-                                 int hist_rows, int hist_bins, int *host_hist) {
+                                 const float *edges, int world, int *work, int *save, int *escape, int *host_counts) {
   if (!ctx || world < 1 || world > KLT_HIP_GATHER_MAX_RANKS || n < 0 || n >= (1 << 24) || !edges || !work ||
-      (n > 0 && (!y0 || !v0)) || (save && n > 0 && !x0) ||
-      (host_hist && (hist_rows < 1 || hist_bins < 1 || hist_bins > kHistMax)))
+      (n > 0 && (!y0 || !v0)) || (save && n > 0 && !x0))
     return ctx ? kltdev::ctx_fail(ctx, "gather_order: bad argument") : -1;
   DeviceGuard guard;
   if (hipSetDevice(klt_hip_ctx_device(ctx)) != hipSuccess) return kltdev::ctx_fail(ctx, "gather_order: device");
@@ -530,9 +490,8 @@ KLT_API int klt_hip_gather_order(klt_hip_ctx *ctx, const float *x0, const float 
   E.world = world;
   hipStream_t st = (hipStream_t)klt_hip_get_stream(ctx);
   const int nb = gather_blocks(n);
-  const Hist H{hist_rows, hist_bins, host_hist};
-  hipLaunchKernelGGL(k_gather_count, dim3(nb), dim3(kOrderThreads), 0, st, x0, y0, v0, n, E, work, save, escape, H);
-  hipLaunchKernelGGL(k_gather_place, dim3(nb), dim3(kOrderThreads), 0, st, n, world, work, host_counts, H);
+  hipLaunchKernelGGL(k_gather_count, dim3(nb), dim3(kOrderThreads), 0, st, x0, y0, v0, n, E, work, save, escape);
+  hipLaunchKernelGGL(k_gather_place, dim3(nb), dim3(kOrderThreads), 0, st, n, world, work, host_counts);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : kltdev::ctx_fail(ctx, "gather_order: %s", hipGetErrorString(e));
 }
@@ -569,10 +528,9 @@ KLT_API int klt_hip_gather_unpack(klt_hip_ctx *ctx, const int *slots, int nslots
 KLT_API int klt_hip_gather_unpack_order(klt_hip_ctx *ctx, const int *slots, int nslots, int first_rank, int *work,
                                         int n, int world, int S, float *x, float *y, int *val, int *flags,
                                         int *host_flags, const float *edges, int *save, int *escape,
-                                        int *host_counts, int hist_rows, int hist_bins, int *host_hist) {
+                                        int *host_counts) {
   if (!ctx || nslots < 1 || first_rank < 0 || first_rank + nslots > world || world > KLT_HIP_GATHER_MAX_RANKS ||
-      n < 0 || n >= (1 << 24) || S < 0 || !slots || !work || !flags || !edges || (n > 0 && (!x || !y || !val)) ||
-      (host_hist && (hist_rows < 1 || hist_bins < 1 || hist_bins > kHistMax)))
+      n < 0 || n >= (1 << 24) || S < 0 || !slots || !work || !flags || !edges || (n > 0 && (!x || !y || !val)))
     return ctx ? kltdev::ctx_fail(ctx, "gather_unpack_order: bad argument") : -1;
   DeviceGuard guard;
   if (hipSetDevice(klt_hip_ctx_device(ctx)) != hipSuccess) return kltdev::ctx_fail(ctx, "gather_unpack_order: device");
@@ -581,10 +539,9 @@ KLT_API int klt_hip_gather_unpack_order(klt_hip_ctx *ctx, const int *slots, int 
   E.world = world;
   hipStream_t st = (hipStream_t)klt_hip_get_stream(ctx);
   const int nb = gather_blocks(n);
-  const Hist H{hist_rows, hist_bins, host_hist};
   hipLaunchKernelGGL(k_gather_unpack_count, dim3(nb), dim3(kOrderThreads), 0, st, slots, nslots, first_rank, n, S, x,
-                     y, val, flags, host_flags, E, work, save, escape, H);
-  hipLaunchKernelGGL(k_gather_place, dim3(nb), dim3(kOrderThreads), 0, st, n, world, work, host_counts, H);
+                     y, val, flags, host_flags, E, work, save, escape);
+  hipLaunchKernelGGL(k_gather_place, dim3(nb), dim3(kOrderThreads), 0, st, n, world, work, host_counts);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : kltdev::ctx_fail(ctx, "gather_unpack_order: %s", hipGetErrorString(e));
 }
@@ -693,78 +650,6 @@ klt_shard *make_shard(klt_hip_ctx *ctx, int rank, int world, const unsigned char
 }
 
 }  // namespace
-
-// Bands balanced on rows built and features owned (kltamd/shard.py
-// cost_edges, the same search in the same integer arithmetic): edges on
-// multiples of hist_rows within max_shift rows of base, minimising the
-// largest 1000 * built_rows + feat_milli * owned, where owned sums the
-// histogram's bins inside the band (rank 0 from bin 0, the last rank to the
-// last bin).  Binary search on that cost; each rank takes the highest edge
-// whose band fits, leaving a bin for every rank after it.
-namespace {
-long long band_cost(const int *hist, int nbins, int T, int nrows, int world, int margin, int feat_milli, int r,
-                    int lo, int hi) {
-  const int rlo = lo - margin > 0 ? lo - margin : 0, rhi = hi + margin < nrows ? hi + margin : nrows;
-  const int tlo = rlo / T * T, thi = (rhi + T - 1) / T * T;
-  const long long built = (thi < nrows ? thi : nrows) - tlo;
-  const int b0 = r == 0 ? 0 : lo / T, b1 = r == world - 1 ? nbins : (hi / T < nbins ? hi / T : nbins);
-  long long owned = 0;
-  for (int b = b0; b < b1; ++b) owned += hist[b];
-  return 1000 * built + (long long)feat_milli * owned;
-}
-
-bool cost_fit(const int *hist, int nbins, int T, int nrows, int world, int margin, int feat_milli, const int *base,
-              int max_shift, long long limit, int *edges) {
-  int lo = 0;
-  edges[0] = 0;
-  for (int r = 0; r + 1 < world; ++r) {
-    const int cap = nrows - (world - 1 - r) * T;  // a bin left for each rank after r
-    int best = -1;
-    for (int hi = (lo / T + 1) * T; hi <= cap; hi += T) {
-      if (hi < base[r + 1] - max_shift) continue;
-      if (hi > base[r + 1] + max_shift) break;
-      if (band_cost(hist, nbins, T, nrows, world, margin, feat_milli, r, lo, hi) <= limit)
-        best = hi;
-      else
-        break;
-    }
-    if (best < 0) return false;
-    edges[r + 1] = best;
-    lo = best;
-  }
-  edges[world] = nrows;
-  return band_cost(hist, nbins, T, nrows, world, margin, feat_milli, world - 1, lo, nrows) <= limit;
-}
-}  // namespace
-
-KLT_API int klt_shard_cost_edges(const int *hist, int nbins, int hist_rows, int nrows, int world, int margin,
-                                 int feat_milli, const int *base, int max_shift, int *edges) {
-  if (!hist || !base || !edges || nbins < 1 || hist_rows < 1 || nrows < 1 || world < 1 ||
-      world > KLT_HIP_GATHER_MAX_RANKS || margin < 0 || feat_milli < 0 || max_shift < 0)
-    return -1;
-  if (world == 1) {
-    edges[0] = 0;
-    edges[1] = nrows;
-    return 0;
-  }
-  long long lo = 0, hi = 1000LL * 4 * nrows;
-  for (int b = 0; b < nbins; ++b) hi += (long long)feat_milli * hist[b];
-  std::vector<int> e(world + 1);
-  if (!cost_fit(hist, nbins, hist_rows, nrows, world, margin, feat_milli, base, max_shift, hi, e.data())) {
-    for (int r = 0; r <= world; ++r) edges[r] = base[r];  // no band fits the shift bound: keep base
-    return 1;
-  }
-  while (lo < hi) {  // the least limit that fits
-    const long long mid = lo + (hi - lo) / 2;
-    if (cost_fit(hist, nbins, hist_rows, nrows, world, margin, feat_milli, base, max_shift, mid, e.data()))
-      hi = mid;
-    else
-      lo = mid + 1;
-  }
-  cost_fit(hist, nbins, hist_rows, nrows, world, margin, feat_milli, base, max_shift, lo, e.data());
-  for (int r = 0; r <= world; ++r) edges[r] = e[r];
-  return 0;
-}
 
 KLT_API int klt_shard_band_edges(int nrows, int world, int margin, int *edges) {
   if (nrows < 1 || world < 1 || world > KLT_HIP_GATHER_MAX_RANKS || margin < 0 || !edges) return -1;

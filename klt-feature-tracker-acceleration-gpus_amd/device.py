@@ -98,8 +98,6 @@ DEVICE_PROTOS = {
                                             V, C.c_int]),
     "klt_shard_unique_id": (C.c_int, [V]),
     "klt_shard_band_edges": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]),
-    "klt_shard_cost_edges": (C.c_int, [C.POINTER(C.c_int), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
-                                       C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_int)]),
     "klt_shard_create": (V, [V, C.c_int, C.c_int, V, C.c_int, C.c_int]),
     "klt_shard_create_local": (V, [V, C.c_int, C.c_int, C.c_int, C.c_int]),
     "klt_shard_destroy": (None, [V]),
@@ -110,14 +108,13 @@ DEVICE_PROTOS = {
                                   C.c_int, V, V, V, C.c_int, V, V]),
     "klt_hip_select_map": (C.c_int, [V, C.c_int, C.c_int, V, C.c_int, C.c_int, V, V, V, V, C.c_int]),
     "klt_hip_min_eigen_rows": (C.c_int, [V, V, C.c_int, C.c_int, V, IP, IP, IP, IP]),
-    "klt_hip_gather_order": (C.c_int, [V, V, V, V, C.c_int, FP, C.c_int, V, V, V, V, C.c_int, C.c_int, V]),
+    "klt_hip_gather_order": (C.c_int, [V, V, V, V, C.c_int, FP, C.c_int, V, V, V, V]),
     "klt_hip_gather_pack": (C.c_int, [V, V, V, V, V, C.c_int, C.c_int, C.c_int, V, C.c_int, V, C.c_int]),
     "klt_hip_gather_unpack": (C.c_int, [V, V, C.c_int, C.c_int, V, C.c_int, C.c_int, C.c_int, V, V, V, V, V]),
     "klt_hip_gather_work_ints": (C.c_long, [C.c_int, C.c_int]),
     "klt_hip_gather_unpack_order": (C.c_int, [V, V, C.c_int, C.c_int, V, C.c_int, C.c_int, C.c_int, V, V, V, V, V,
-                                              FP, V, V, V, C.c_int, C.c_int, V]),
+                                              FP, V, V, V]),
     "klt_hip_set_ahead_ready": (C.c_int, [V, C.c_int]),
-    "klt_hip_set_next_band": (C.c_int, [V, C.c_float, C.c_float, C.c_int, C.c_int]),
     "klt_shard_eigen": (C.c_int, [V, C.POINTER(PyrDesc), V, C.c_long, V, V, V]),
     "klt_shard_select": (C.c_int, [V, C.POINTER(PyrDesc), V, C.c_int, C.c_int, V, V, V, V, C.c_int]),
     "klt_shard_replace": (C.c_int, [V, C.POINTER(PyrDesc), V, C.c_long, C.c_int, C.c_int, V, V, V, C.c_int, V, V]),

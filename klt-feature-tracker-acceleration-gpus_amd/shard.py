@@ -128,89 +128,62 @@ def chunk_plan(t0: int, nframes: int, chunk: int, first: int | None = None) -> l
     return out
 
 
-HIST_ROWS = 32  # row-histogram bin: one level-0 tile
-FEAT_MILLI = 66  # a live feature priced in thousandths of a level-0 row built (cost_edges)
-MAX_SHIFT = 64  # rows a rebalanced edge may move from its base (BandFrames hold that much more)
-
-
-def row_hist(y: torch.Tensor, v: torch.Tensor, nrows: int, hist_rows: int = HIST_ROWS) -> torch.Tensor:
-    """Live features per hist_rows-row bin of y, as the order kernels count them
-    (klt_hip_gather_order host_hist): bin (int)y // hist_rows clamped to the
-    last, y < 0 and NaN in bin 0."""
-    nb = -(-nrows // hist_rows)
-    yy = y.float().cpu()
-    live = v.cpu() >= 0
-    b = torch.zeros(yy.shape, dtype=torch.int64)
-    ok = yy >= 0  # False for NaN
-    top = yy >= float(hist_rows * nb)
-    mid = ok & ~top
-    b[mid] = torch.clamp(yy[mid].to(torch.int64) // hist_rows, max=nb - 1)
-    b[top] = nb - 1
-    return torch.bincount(b[live], minlength=nb)
-
-
-def cost_edges_ref(hist, hist_rows: int, nrows: int, world: int, margin: int, feat_milli: int, base,
-                   max_shift: int) -> list[int]:
-    """Bands balanced on rows built and features owned: edges on multiples of
-    hist_rows within max_shift of base, minimising the largest
-    1000 * built_rows + feat_milli * owned (owned: the histogram's bins in the
-    band; rank 0 from bin 0, the last rank to the last).  Binary search on
-    that cost, each rank taking the highest edge whose band fits and leaving
-    a bin for every rank after it.  The restatement of klt_shard_cost_edges
-    (the drivers call the library; tests compare the two)."""
-    hist = [int(h) for h in hist]
-    nb, T = len(hist), hist_rows
-    if world == 1:
+def cost_edges(y: torch.Tensor, v: torch.Tensor, nrows: int, world: int, margin: int = DEFAULT_MARGIN,
+               feat_rows: float = 0.066, tile: int = 32) -> list[int]:
+    """Row boundaries on tile multiples that minimise the largest rank cost
+    built_rows + feat_rows * (live features owned), from the list (y, v) at
+    the start: a rank's level-0 build and its tracker both grow with what it
+    holds.  feat_rows prices one feature in level-0 rows (0.066: one 32-row
+    tile of a 4K band build per ~480 features in tools/shard_sim.py's
+    per-rank times).  Binary search on the cost, each rank taking the
+    longest band that fits.  Deterministic in (y, v): every rank computes
+    the same edges from the same list."""
+    if world < 2:
         return [0, nrows]
-    pre = [0]
-    for h in hist:
-        pre.append(pre[-1] + h)
+    ys = torch.sort(y[v >= 0].float().cpu()).values
+    bounds = list(range(0, nrows, tile)) + [nrows]  # candidate edges
 
-    def cost(r, lo, hi):
-        rlo, rhi = max(0, lo - margin), min(nrows, hi + margin)
-        built = min(nrows, -(-rhi // T) * T) - rlo // T * T
-        b0 = 0 if r == 0 else lo // T
-        b1 = nb if r == world - 1 else min(hi // T, nb)
-        return 1000 * built + feat_milli * (pre[max(b1, b0)] - pre[b0])
+    def owned(lo, hi, first, last):
+        a = 0 if first else int(torch.searchsorted(ys, float(lo)).item())
+        b = ys.numel() if last else int(torch.searchsorted(ys, float(hi)).item())
+        return b - a
 
-    def fit(limit):
-        lo, e = 0, [0]
+    def cost(lo, hi, r):
+        e = [0] * (world + 1)
+        e[r], e[r + 1], e[world] = lo, hi, nrows
+        bd = Band(float("-inf") if r == 0 else float(lo), float("inf") if r == world - 1 else float(hi),
+                  max(0, lo - margin), min(nrows, hi + margin))
+        return built_rows(nrows, bd, tile) + feat_rows * owned(lo, hi, r == 0, r == world - 1)
+
+    def fit(T):
+        lo, edges = 0, [0]
         for r in range(world - 1):
-            cap, best, hi = nrows - (world - 1 - r) * T, -1, (lo // T + 1) * T
-            while hi <= cap:
-                if hi >= base[r + 1] - max_shift:
-                    if hi > base[r + 1] + max_shift or cost(r, lo, hi) > limit:
-                        break
+            best = None
+            for hi in bounds:
+                if hi <= lo or hi > nrows - (world - 1 - r) * tile:  # a tile left for each rank after r
+                    continue
+                if cost(lo, hi, r) <= T:
                     best = hi
-                hi += T
-            if best < 0:
+                else:
+                    break
+            if best is None:
                 return None
-            e.append(best)
+            edges.append(best)
             lo = best
-        return e + [nrows] if cost(world - 1, lo, nrows) <= limit else None
+        if cost(lo, nrows, world - 1) > T:
+            return None
+        return edges + [nrows]
 
-    lo, hi = 0, 1000 * 4 * nrows + feat_milli * sum(hist)
-    if fit(hi) is None:
-        return list(base)
-    while lo < hi:
-        mid = lo + (hi - lo) // 2
-        if fit(mid) is not None:
-            hi = mid
+    lo_t, hi_t = 0.0, float(nrows + feat_rows * ys.numel() + 2 * margin + tile)
+    best = fit(hi_t)
+    for _ in range(40):
+        mid = 0.5 * (lo_t + hi_t)
+        e = fit(mid)
+        if e is not None:
+            best, hi_t = e, mid
         else:
-            lo = mid + 1
-    return fit(lo)
-
-
-def cost_edges(lib, hist, nrows: int, world: int, margin: int, base, hist_rows: int = HIST_ROWS,
-               feat_milli: int = FEAT_MILLI, max_shift: int = MAX_SHIFT) -> list[int]:
-    """cost_edges_ref through the library (klt_shard_cost_edges)."""
-    h = (C.c_int * len(hist))(*[int(x) for x in hist])
-    b = (C.c_int * (world + 1))(*[int(x) for x in base])
-    e = (C.c_int * (world + 1))()
-    rc = lib.klt_shard_cost_edges(h, len(hist), hist_rows, nrows, world, margin, feat_milli, b, max_shift, e)
-    if rc < 0:
-        raise ValueError("klt_shard_cost_edges: bad arguments")
-    return list(e)
+            lo_t = mid
+    return best if best is not None else row_edges(nrows, world, margin, tile)
 
 
 def band_rows(nrows: int, band: Band, tile: int = 32, halo: int = 8) -> tuple[int, int]:
@@ -341,14 +314,10 @@ class Exchange:
     chunks.  all_gather(out, inp) gathers the ranks' slots into out in rank
     order (torch.distributed.all_gather_into_tensor in production)."""
 
-    def __init__(self, lib, ctx, n: int, edges: list[float], rank: int, all_gather, device, hist_bins: int = 0):
+    def __init__(self, lib, ctx, n: int, edges: list[float], rank: int, all_gather, device):
         self.lib, self.ctx, self.n, self.rank, self.all_gather = lib, ctx, n, rank, all_gather
         self.world = len(edges) - 1
         self.edges = (C.c_float * (self.world + 1))(*edges)
-        # hist_bins > 0: each order also counts the ordered state's live features per
-        # HIST_ROWS-row bin into h_hist (pinned), read behind the same event
-        self.hist_bins = hist_bins
-        self.h_hist = torch.zeros(max(1, hist_bins), dtype=torch.int32, pin_memory=True)
         self.work = torch.zeros(lib.klt_hip_gather_work_ints(n, self.world), dtype=torch.int32, device=device)
         self.send = torch.empty(slot_words(max(n, 1)), dtype=torch.int32, device=device)
         self.recv = torch.empty(self.world * slot_words(max(n, 1)), dtype=torch.int32, device=device)
@@ -365,16 +334,6 @@ class Exchange:
         from .device import check
         check(self.lib, self.ctx, rc, what)
 
-    def set_edges(self, edges: list[float]) -> None:
-        """The ownership edges (band_edges) the next order uses."""
-        for i, e in enumerate(edges):
-            self.edges[i] = e
-
-    def _hist(self):
-        if self.hist_bins > 0:
-            return HIST_ROWS, self.hist_bins, C.c_void_p(self.h_hist.data_ptr())
-        return 0, 0, None
-
     def order(self, x, y, v, escape) -> int:
         """Ownership of the chunk-start state x/y/v, that state saved, the escape
         flag zeroed; the counts land in h_counts behind the event.  Returns the
@@ -384,7 +343,7 @@ class Exchange:
         self._check(self.lib.klt_hip_gather_order(
             self.ctx, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()), self.n,
             self.edges, self.world, C.c_void_p(self.work.data_ptr()), C.c_void_p(self.save[k].data_ptr()),
-            C.c_void_p(escape.data_ptr()), C.c_void_p(self.h_counts.data_ptr()), *self._hist()), "gather_order")
+            C.c_void_p(escape.data_ptr()), C.c_void_p(self.h_counts.data_ptr())), "gather_order")
         self.ev.record()
         return k
 
@@ -417,7 +376,7 @@ class Exchange:
             self.world, S, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()),
             C.c_void_p(self.flags.data_ptr()), C.c_void_p(self.h_flags.data_ptr()), self.edges,
             C.c_void_p(self.save[k].data_ptr()), C.c_void_p(escape.data_ptr()),
-            C.c_void_p(self.h_counts.data_ptr()), *self._hist()), "gather_unpack_order")
+            C.c_void_p(self.h_counts.data_ptr())), "gather_unpack_order")
         self.ev.record()
         if self.timing:
             e = torch.cuda.Event(enable_timing=True)
@@ -442,21 +401,12 @@ class ShardedSequence:
     the bands klt_shard_create uses (equal level-0 rows built per rank).
     chunk / first_chunk: frames per band call, and of each run()'s first
     call (chunk_plan; default chunk).
-    rebalance: move the bands between chunks (cost_edges: rows built and
-    features owned together, each edge within MAX_SHIFT rows of its base),
-    from the row histogram the order kernels count at each chunk's start.
-    The bands of chunk c+2 come from the state at the start of chunk c, so
-    that every chunk's band is known when the chunk before it builds its
-    pyramids ahead; every rank computes the same edges from the same merged
-    state.  A BandFrames must then hold band_of(..., margin + MAX_SHIFT,
-    edges) rows; one built for the base band only turns rebalancing off.
     all_gather(out, inp) gathers a device int32 tensor of every rank into out
     in rank order (torch.distributed.all_gather_into_tensor in production).
     """
 
     def __init__(self, lib, ctx, pd, td, frames: torch.Tensor, x, y, v, rank: int, world: int, all_gather,
-                 chunk: int = 64, margin: int = DEFAULT_MARGIN, edges=None, first_chunk: int | None = None,
-                 rebalance: bool = True):
+                 chunk: int = 64, margin: int = DEFAULT_MARGIN, edges=None, first_chunk: int | None = None):
         from .device import check
         self.lib, self.ctx, self.pd, self.td = lib, ctx, pd, td
         self.src = frames if isinstance(frames, (FullFrames, BandFrames)) else FullFrames(frames)
@@ -466,22 +416,14 @@ class ShardedSequence:
         self.H, self.W = H, W
         # default: the C driver's bands (klt_shard_create), equal built rows per rank
         self.edges = edges = list(edges) if edges is not None else row_edges(H, world, margin)
-        self.base_edges = list(edges)
-        self.margin = margin
         self.band = band_of(H, world, rank, margin, edges)
-        self.rebalance = rebalance and world > 1
         if isinstance(self.src, BandFrames):
             ra, rb = band_rows(H, self.band)
             assert self.src.ra <= ra and self.src.rb >= rb, "BandFrames built for another band"
-            wa, wb = band_rows(H, band_of(H, world, rank, margin + MAX_SHIFT, edges))
-            if self.src.ra > wa or self.src.rb < wb:
-                self.rebalance = False  # the frames held do not cover a moved band
-        self.next_edges = list(edges)  # the second chunk's bands of the next run()
         self.escape = torch.zeros(1, dtype=torch.int32, device=x.device)
         # the frames are resident before run(): each build-ahead waits only for its bank
         check(lib, ctx, lib.klt_hip_set_ahead_ready(ctx, 1), "set_ahead_ready")
-        self.xch = Exchange(lib, ctx, x.numel(), band_edges(H, world, edges), rank, all_gather, x.device,
-                            hist_bins=-(-H // HIST_ROWS) if self.rebalance else 0)
+        self.xch = Exchange(lib, ctx, x.numel(), band_edges(H, world, edges), rank, all_gather, x.device)
         self.redone = 0
         self.rebuilt = 0  # replacements whose band pyramid was too short for the selection window
         self.t_last = None  # last tracked frame
@@ -502,16 +444,12 @@ class ShardedSequence:
             self.x.numel(), b.own_lo, b.own_hi, row_lo, row_hi, C.c_void_p(self.escape.data_ptr()),
             C.c_void_p(next_ptr) if next_n > 0 else None, next_n), "track_frames_band")
 
-    def _redo(self, c0: int, n: int, k: int, edges=None, next_edges=None) -> None:
+    def _redo(self, c0: int, n: int, k: int) -> None:
         """Chunk [c0, c0+n) again from whole frames and its start state (save
         buffer k), exchanged (every rank does it: they all read the same summed
-        escape flag).  edges: that chunk's bands; next_edges: the next chunk's
-        (its ownership is ordered by the exchange)."""
+        escape flag)."""
         torch.cuda.current_stream().synchronize()
         self.redone += 1
-        if edges is not None:
-            self.band = band_of(self.H, self.world, self.rank, self.margin, edges)
-            self.xch.set_edges(band_edges(self.H, self.world, edges))
         self.xch.restore(k, self.x, self.y, self.v)
         self.xch.order(self.x, self.y, self.v, self.escape)
         S = self.xch.slot_size()
@@ -519,8 +457,6 @@ class ShardedSequence:
         self._check(self.lib, self.ctx, self.lib.klt_hip_frames_begin(
             self.ctx, C.byref(self.pd), C.c_void_p(ptr), self.W), "frames_begin")
         self._band_call(ptr + fb, fb, n, 0, self.H)
-        if next_edges is not None:
-            self.xch.set_edges(band_edges(self.H, self.world, next_edges))
         self.xch.exchange(self.x, self.y, self.v, self.escape, S)
         self.xch.ev.synchronize()
         esc, bad = self.xch.verdict()
@@ -533,54 +469,31 @@ class ShardedSequence:
         and chunk c+1 runs again."""
         end = t0 + nframes
         chunks = chunk_plan(t0, nframes, self.chunk, self.first_chunk)
-        H, world = self.H, self.world
-        sched = {0: list(self.edges), 1: list(self.next_edges)}  # chunk index -> its band edges
-        self.bands_used = {}  # chunk index of this run -> the edges it ran with (tools/shard_sim.py checks them)
-        self.xch.set_edges(band_edges(H, world, sched[0]))
         k = self.xch.order(self.x, self.y, self.v, self.escape)  # the first chunk's ownership, start state, counts
-        prev = None  # (c0, n, save index, chunk index) of the chunk whose verdict is still unread
+        prev = None  # (c0, n, save index) of the chunk whose verdict is still unread
         i = 0
         while i < len(chunks):
             c0, n = chunks[i]
             nn = chunks[i + 1][1] if i + 1 < len(chunks) else 0  # the next chunk, built ahead
             src = self.src
-            self.edges = sched[i]
-            self.band = band_of(H, world, self.rank, self.margin, sched[i])
-            self.bands_used[i] = sched[i]
-            nxt = sched.get(i + 1, sched[i])
-            if nn > 0 and nxt != sched[i]:  # the next chunk's pyramids for its own band
-                nb = band_of(H, world, self.rank, self.margin, nxt)
-                self._check(self.lib, self.ctx, self.lib.klt_hip_set_next_band(
-                    self.ctx, nb.own_lo, nb.own_hi, nb.row_lo, nb.row_hi), "set_next_band")
             self._band_call(src.band(c0), src.stride, n, self.band.row_lo, self.band.row_hi,
                             src.band(c0 + n) if nn > 0 else 0, nn)
             S = self.xch.slot_size()  # this chunk's counts, with the previous chunk's verdict
-            if self.rebalance:  # chunk i+2's bands from the state at chunk i's start
-                sched[i + 2] = cost_edges(self.lib, self.xch.h_hist.tolist(), H, world, self.margin,
-                                          self.base_edges)
             if prev is not None:
                 esc, bad = self.xch.verdict()
                 assert bad == 0, "exchange failed"
                 if esc:  # the previous chunk escaped: this chunk ran from a wrong state
-                    self._redo(*prev[:3], sched[i - 1], sched[i])
+                    self._redo(*prev)
                     k = self.xch.k ^ 1  # the redo's exchange ordered (and saved) this chunk's start again
                     prev = None
                     continue
-            self.xch.set_edges(band_edges(H, world, nxt))  # the next chunk's ownership
             k_next = self.xch.exchange(self.x, self.y, self.v, self.escape, S)
-            prev = (c0, n, k, i)
+            prev = (c0, n, k)
             k = k_next
             i += 1
         self.xch.ev.synchronize()
         if prev is not None and self.xch.verdict()[0]:
-            last = prev[3]
-            self._redo(*prev[:3], sched[last], sched.get(last + 1, sched[last]))
-        # the last chunk's bands (its pyramids are the last built: replace() reads them)
-        last = len(chunks) - 1
-        if last >= 0:
-            self.edges = sched[last]
-            self.band = band_of(H, world, self.rank, self.margin, sched[last])
-            self.next_edges = sched.get(last + 1, sched[last])
+            self._redo(*prev)
         self.t_last = end - 1
 
     # -- KLTReplaceLostFeatures across the ranks (selectGoodFeatures.c:514-541,

@@ -25,34 +25,6 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def test_cost_edges_c_equals_python(amd):
-    """klt_shard_cost_edges (the library's search) == kltamd.shard.cost_edges_ref
-    on random row histograms, heights, world sizes, margins, feature prices
-    and shift bounds; the edges stay within the shift bound of their base, on
-    histogram-bin multiples, and a uniform histogram keeps row_edges."""
-    import random
-    from kltamd.shard import cost_edges, cost_edges_ref, row_hist
-    rnd = random.Random(5)
-    for _ in range(200):
-        H = rnd.choice([251, 480, 1080, 2160, 4320])
-        world = rnd.randint(1, 16)
-        margin = rnd.choice([0, 16, 64])
-        nb = -(-H // 32)
-        hist = [rnd.randint(0, 500) for _ in range(nb)]
-        base = row_edges(H, world, margin)
-        fm, D = rnd.choice([0, 66, 500]), rnd.choice([0, 32, 64, 128])
-        e = cost_edges(amd, hist, H, world, margin, base, 32, fm, D)
-        assert e == cost_edges_ref(hist, 32, H, world, margin, fm, base, D), (H, world, margin, fm, D)
-        assert e[0] == 0 and e[-1] == H and all(b > a for a, b in zip(e, e[1:]))
-        if e != base:
-            assert all(abs(a - b) <= D and a % 32 == 0 for a, b in zip(e[1:-1], base[1:-1]))
-    y = torch.arange(20000, dtype=torch.float32) * (2160 / 20000)
-    hist = row_hist(y, torch.zeros(20000, dtype=torch.int32), 2160).tolist()
-    assert cost_edges(amd, hist, 2160, 8, 64, row_edges(2160, 8, 64)) == row_edges(2160, 8, 64)
-    skew = [h * (3 if i < 12 else 1) for i, h in enumerate(hist)]  # a dense top: rank 0 gives rows away
-    assert cost_edges(amd, skew, 2160, 8, 64, row_edges(2160, 8, 64))[1] < row_edges(2160, 8, 64)[1]
-
-
 def test_chunk_plan():
     """chunk_plan: the first chunk's length (default: chunk), then whole
     chunks; contiguous and covering the frames exactly."""
@@ -272,7 +244,7 @@ def device_gather_merge(gpu, ctx, state, outs, edges, escapes=None):
     E = (C.c_float * (world + 1))(*edges)
     check(gpu, ctx, gpu.klt_hip_gather_order(ctx, None, C.c_void_p(state[1].data_ptr()),
                                              C.c_void_p(state[2].data_ptr()), n, E, world,
-                                             C.c_void_p(work.data_ptr()), None, None, None, 0, 0, None), "order")
+                                             C.c_void_p(work.data_ptr()), None, None, None), "order")
     S = max(1, int(work[n:n + world].max().item()))
     W = slot_words(S)
     slots = torch.zeros(world * W, dtype=torch.int32, device=dev)
@@ -352,15 +324,8 @@ def test_gather_kernels_equal_reference(gpu, world, n):
     from kltamd.shard import slot_words
     E = (C.c_float * (world + 1))(*edges)
     work = torch.zeros(gpu.klt_hip_gather_work_ints(n, world), dtype=torch.int32, device=dev)
-    from kltamd.shard import row_hist
-    nb = -(-H // 32)
-    hh = torch.full((nb,), -1, dtype=torch.int32).pin_memory()
     assert gpu.klt_hip_gather_order(ctx, None, C.c_void_p(state[1].data_ptr()), C.c_void_p(state[2].data_ptr()), n,
-                                    E, world, C.c_void_p(work.data_ptr()), None, None, None, 32, nb,
-                                    C.c_void_p(hh.data_ptr())) == 0
-    torch.cuda.synchronize()
-    # the row histogram the kernels count == kltamd.shard.row_hist (NaN / out-of-frame y in the end bins)
-    assert hh.tolist() == row_hist(torch.from_numpy(y0), torch.from_numpy(v0), H).tolist()
+                                    E, world, C.c_void_p(work.data_ptr()), None, None, None) == 0
     S = max(1, int(work[n:n + world].max().item()))
     Wd = slot_words(S)
     slots = torch.zeros(world * Wd, dtype=torch.int32, device=dev)
@@ -374,12 +339,11 @@ def test_gather_kernels_equal_reference(gpu, world, n):
     save = torch.zeros(3 * n, dtype=torch.int32, device=dev)
     esc = torch.ones(1, dtype=torch.int32, device=dev)
     hc = torch.zeros(world, dtype=torch.int32).pin_memory()
-    hh.fill_(-1)
     assert gpu.klt_hip_gather_unpack_order(ctx, C.c_void_p(slots.data_ptr()), world, 0, C.c_void_p(work.data_ptr()), n,
                                            world, S, C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()),
                                            C.c_void_p(v.data_ptr()), C.c_void_p(flags.data_ptr()), None, E,
                                            C.c_void_p(save.data_ptr()), C.c_void_p(esc.data_ptr()),
-                                           C.c_void_p(hc.data_ptr()), 32, nb, C.c_void_p(hh.data_ptr())) == 0
+                                           C.c_void_p(hc.data_ptr())) == 0
     torch.cuda.synchronize()
     for g, w in zip((x, y, v), ref):
         assert np.array_equal(g.cpu().numpy().view(np.int32), w.numpy().view(np.int32))
@@ -387,7 +351,6 @@ def test_gather_kernels_equal_reference(gpu, world, n):
     assert int(esc.item()) == 0 and flags.cpu().tolist() == [esc_ref, 0]
     _, _, counts = gather_order_ref(ref[1], ref[2], edges)
     assert hc.tolist() == counts == work[n:n + world].cpu().tolist()
-    assert hh.tolist() == row_hist(ref[1], ref[2], H).tolist()
     gpu.KLTFreeTrackingContext(tc)
 
 
@@ -887,9 +850,8 @@ def threaded_sequence(gpu, frames, nfeat, world, chunk, margin, replace=False, b
                         check(gpu, ctx, gpu.klt_hip_memcpy(ctx, C.c_void_p(dst + f * stride),
                                                            C.c_void_p(part[f].data_ptr()), nrows * W, D2D), "d2d")
                     gpu.klt_hip_sync(ctx)
-                from kltamd.shard import MAX_SHIFT  # the rows a rebalanced band may need
-                src = BandFrames(T + 1, H, W, band_of(H, world, rank, margin + MAX_SHIFT, row_edges(H, world, margin)),
-                                 load, dev)
+                src = BandFrames(T + 1, H, W, band_of(H, world, rank, margin, row_edges(H, world, margin)), load,
+                                 dev)
             else:
                 src = FullFrames(dfr)
             seq = ShardedSequence(gpu, ctx, pd, td, src, x, y, v, rank, world,

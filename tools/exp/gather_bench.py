@@ -29,7 +29,6 @@ esc = torch.zeros(1, dtype=torch.int32, device=dev)
 flags = torch.zeros(2, dtype=torch.int32, device=dev)
 hc = torch.zeros(world, dtype=torch.int32).pin_memory()
 hf = torch.zeros(2, dtype=torch.int32).pin_memory()
-hh = torch.zeros(68, dtype=torch.int32).pin_memory()  # the row histogram (32-row bins of 2160 rows)
 P = lambda t: C.c_void_p(t.data_ptr())
 
 
@@ -46,7 +45,7 @@ def timeit(name, fn, reps=200):
 
 
 timeit("gather_order", lambda: check(lib, ctx, lib.klt_hip_gather_order(ctx, P(x), P(y), P(v), n, E, world, P(work),
-                                                                         P(save), P(esc), P(hc), 32, 68, P(hh)), "order"))
+                                                                         P(save), P(esc), P(hc)), "order"))
 S = max(1, int(work[n:n + world].max().item()))
 W = slot_words(S)
 slots = torch.zeros(world * W, dtype=torch.int32, device=dev)
@@ -56,7 +55,6 @@ for r in range(world):
 timeit("gather_pack", lambda: check(lib, ctx, lib.klt_hip_gather_pack(ctx, P(x), P(y), P(v), P(work), n, world, 3,
                                                                        P(esc), 0, P(slots), S), "pack"))
 timeit("gather_unpack_order", lambda: check(lib, ctx, lib.klt_hip_gather_unpack_order(
-    ctx, P(slots), world, 0, P(work), n, world, S, P(x), P(y), P(v), P(flags), P(hf), E, P(save), P(esc), P(hc),
-    32, 68, P(hh)),
+    ctx, P(slots), world, 0, P(work), n, world, S, P(x), P(y), P(v), P(flags), P(hf), E, P(save), P(esc), P(hc)),
     "unpack_order"))
 lib.KLTFreeTrackingContext(tc)

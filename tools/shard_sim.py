@@ -54,11 +54,9 @@ def main():
     ap.add_argument("--seed", type=int, default=2160)
     ap.add_argument("--edges", default=None, help="explicit band edges for the largest world, comma-separated "
                     "(overrides --bands there)")
-    ap.add_argument("--no-rebalance", action="store_true",
-                    help="static bands (ShardedSequence rebalance=False); default: the driver's rebalancing")
-    ap.add_argument("--bands", choices=["equal", "features", "rows"], default="rows",
+    ap.add_argument("--bands", choices=["equal", "features", "rows", "cost"], default="rows",
                     help="band edges: equal rows, equal feature counts (balanced_edges), or equal level-0 rows "
-                         "built incl. margins (row_edges): the base the rebalancing moves from")
+                         "built incl. margins (row_edges), or rows built and features owned together (cost_edges)")
     ap.add_argument("--keep-states", default=None, help="save pass 1's record as DIR/states_w<N>.npz")
     ap.add_argument("--pass1-shared", action="store_true",
                     help="pass 1 through one device context for every rank, each chunk started from a "
@@ -72,8 +70,8 @@ def main():
     import torch
     import kltamd
     from kltamd.device import PyrDesc, Timing, TrackDesc, check, use_torch_stream
-    from kltamd.shard import (MAX_SHIFT, FullFrames, ShardedSequence, balanced_edges, band_edges, band_of,
-                              chunk_plan, cost_edges, row_edges, row_hist, slot_words)
+    from kltamd.shard import (FullFrames, ShardedSequence, balanced_edges, band_edges, band_of, chunk_plan,
+                              cost_edges, row_edges, slot_words)
     from kltabi import fl_to_arrays, u8ptr
 
     lib = kltamd.load()
@@ -131,8 +129,7 @@ def main():
             x, y, v = xs.clone(), ys.clone(), vs.clone()
             k[0] = 0
             seq = ShardedSequence(lib, ctx, pd, td, FullFrames(fr), x, y, v, a.rank, world, replay_gather,
-                                  chunk=a.chunk, margin=margin, edges=edges, first_chunk=a.first_chunk,
-                                  rebalance=not a.no_rebalance)
+                                  chunk=a.chunk, margin=margin, edges=edges, first_chunk=a.first_chunk)
             seq.xch.timing = rep == 2
             seq.begin(0)
             lib.klt_hip_set_timing(ctx, 1 if rep == 3 else 0)
@@ -146,15 +143,13 @@ def main():
                 evs = [ev_start] + seq.xch.timing_events
                 per_chunk = [evs[i].elapsed_time(evs[i + 1]) * 1e3 for i in range(len(evs) - 1)]  # us
                 redone = seq.redone
-                used = [seq.bands_used[c] for c in sorted(seq.bands_used)]
-                sched_equal = used == rec["sched"].tolist()
         tm = Timing()
         check(lib, ctx, lib.klt_hip_get_timing(ctx, C.byref(tm)), "timing")
         # per-kernel event time per frame (build-ahead: contended durations)
         kern = {"k_pyr_l0": 1e3 * tm.ms_pyr_l0 / T, "k_pyr_l1": 1e3 * tm.ms_pyr_l1 / T,
                 "k_track": 1e3 * tm.ms_track / T}
         print(json.dumps({"rank": a.rank, "us_per_frame": 1e6 * wall / T, "chunk_us": per_chunk,
-                          "kernels_us_per_frame": kern, "redone": redone, "bands_equal_pass1": sched_equal,
+                          "kernels_us_per_frame": kern, "redone": redone,
                           "digest": int((x.view(torch.int32).to(torch.int64).sum() * 3 +
                                          y.view(torch.int32).to(torch.int64).sum() * 5 +
                                          v.to(torch.int64).sum() * 7).item())}))
@@ -187,8 +182,8 @@ def main():
 
     out = {"workload": f"{W}x{H}, {NF} features, {T} tracked frames, {a.chunk}-frame chunks"
                        + {"equal": "", "features": ", bands of equal feature counts",
-                          "rows": ", bands of equal built rows"}[a.bands]
-                       + ("" if a.no_rebalance else ", rebalanced between chunks"),
+                          "rows": ", bands of equal built rows",
+                          "cost": ", bands of equal built rows + features owned"}[a.bands],
            "exchange_us_assumed_per_chunk": a.exchange_us, "runs": []}
     base = None
     for margin in a.margins:
@@ -197,6 +192,7 @@ def main():
             edges = (explicit if explicit and len(explicit) == world + 1 else
                      balanced_edges(ys, vs, H, world) if a.bands == "features" else
                      row_edges(H, world, margin) if a.bands == "rows" else
+                     cost_edges(ys, vs, H, world, margin) if a.bands == "cost" else
                      [r * H // world for r in range(world + 1)])
             gedges = band_edges(H, world, edges)
             ranks = [Rank(world, r, margin, edges) for r in range(1 if a.pass1_shared else world)]
@@ -213,17 +209,11 @@ def main():
             x, y, v = xs.clone(), ys.clone(), vs.clone()
             redone, slots_rec, owned_rec = 0, [], []
             work = torch.zeros(lib.klt_hip_gather_work_ints(NF, world), dtype=torch.int32, device=dev)
+            E = (C.c_float * (world + 1))(*gedges)
             flags = torch.zeros(2, dtype=torch.int32, device=dev)
-            # the driver's band schedule (ShardedSequence.run): chunk c+2's bands from the state at chunk c's start
-            sched = {0: list(edges), 1: list(edges)}
             for ci, (c0, n) in enumerate(chunks):
                 nn = chunks[ci + 1][1] if ci + 1 < len(chunks) else 0
                 state = (x.clone(), y.clone(), v.clone())
-                if not a.no_rebalance and world > 1:
-                    sched[ci + 2] = cost_edges(lib, row_hist(state[1], state[2], H).tolist(), H, world, margin, edges)
-                E = (C.c_float * (world + 1))(*band_edges(H, world, sched[ci]))
-                for r, rk in enumerate(ranks):
-                    rk.band = band_of(H, world, r, margin, sched[ci])
                 outs, escs = [], []
                 for rk in ranks:
                     xr, yr, vr = (t.clone() for t in state)
@@ -245,8 +235,7 @@ def main():
                 # the exchange with its own kernels: order, each rank's slot, unpack
                 check(lib, ctx, lib.klt_hip_gather_order(ctx, None, C.c_void_p(state[1].data_ptr()),
                                                          C.c_void_p(state[2].data_ptr()), NF, E, world,
-                                                         C.c_void_p(work.data_ptr()), None, None, None, 0, 0, None),
-                      "order")
+                                                         C.c_void_p(work.data_ptr()), None, None, None), "order")
                 owned_rec.append(work[NF:NF + world].cpu().tolist())  # each rank's features at the chunk's start
                 S = max(1, int(max(owned_rec[-1])))
                 Wd = slot_words(S)
@@ -273,9 +262,7 @@ def main():
             with tempfile.TemporaryDirectory() as td:
                 f = f"{td}/rec.npz"
                 offs = np.cumsum([0] + [len(s) for s in slots_rec])
-                sched_arr = np.asarray([sched[c] for c in range(len(chunks))], np.int64)
                 np.savez(f, world=world, margin=margin, row_edges=np.asarray(edges if edges else [], np.int64),
-                         sched=sched_arr,
                          slots=np.concatenate(slots_rec), slot_offsets=offs)
                 if a.keep_states:
                     import shutil
@@ -285,14 +272,12 @@ def main():
                     cmd = [sys.executable, __file__, "--replay", f, "--rank", str(r), "--width", str(W), "--height",
                            str(H), "--features", str(NF), "--frames", str(a.frames), "--chunk", str(a.chunk),
                            "--seed", str(a.seed)] + ([] if a.first_chunk is None else
-                                                     ["--first-chunk", str(a.first_chunk)]) + (
-                        ["--no-rebalance"] if a.no_rebalance else [])
+                                                     ["--first-chunk", str(a.first_chunk)])
                     res = subprocess.run(cmd, check=True, capture_output=True, text=True)
                     reps.append(json.loads(res.stdout.strip().splitlines()[-1]))
             frames = sum(n for _, n in chunks)
             nch = len(chunks)
             assert all(len(rr["chunk_us"]) == nch for rr in reps)
-            assert all(rr["bands_equal_pass1"] for rr in reps), "a replay's bands differ from pass 1's"
             assert all(rr["digest"] == digest for rr in reps), "a replayed rank ended in another state"
             exch = a.exchange_us * nch / frames if world > 1 else 0.0
             synced = sum(max(rr["chunk_us"][c] for rr in reps) for c in range(nch)) / frames
@@ -302,7 +287,6 @@ def main():
                 base = fps
             run = {"world": world, "margin_rows": margin, "chunks_redone_full_frame": redone,
                    "state_digest": digest, "us_per_frame_synced": synced, "us_per_frame_max_rank_total": loose,
-                   "band_edges_per_chunk": [sched[c] for c in range(nch)],
                    "us_per_frame_exchange": exch, "projected_fps": fps,
                    "projected_speedup": fps / base if base else None,
                    "per_rank": [{"rank": i, "band_rows": [band_of(H, world, i, margin, edges).row_lo,
