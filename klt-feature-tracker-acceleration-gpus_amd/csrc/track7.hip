@@ -38,6 +38,9 @@
 #ifndef KLT_T7_NL2
 #define KLT_T7_NL2 1  // the two-level instances (A/B hook: 0 launches the runtime-depth ones)
 #endif
+#ifndef KLT_T7_REUSE
+#define KLT_T7_REUSE 1  // a pass whose window corners are the previous pass's takes them from registers
+#endif
 #ifndef KLT_T7_BATCH
 #define KLT_T7_BATCH 7  // 16-byte LDS reads in flight per ordered-sum batch (13 per row)
 #endif
@@ -285,6 +288,12 @@ struct LevState {
   float aim, agx, agy;       // this lane's img1 samples at (x1, y1), from the first pass
   int it = 0;                // Newton iterations
   int status = kTracked;
+  // KLT_T7_REUSE: the last pass's image-2 corners (this lane's) and where they
+  // came from; a pass whose corners are the same pixels in every lane takes
+  // these instead of a gather round trip -- the same values, only the weights
+  // (the position's fractions) change
+  unsigned bpx = ~0u;
+  Quad bi, bx, by;
 };
 
 enum { kPassAgain = 0, kPassDone = 1, kPassOOB = 2, kPassLostPrev = 3 };
@@ -324,7 +333,14 @@ __device__ __forceinline__ int pass7(const TrkArgs &a, const Lev &A, const Lev &
   const unsigned rowB = (unsigned)B.w * (AOS ? 12u : 4u);
   const Pix qb = pix_at(B.w, B.h, ls.x2 + fi, ls.y2 + fj);
   Quad bi, bx, by;
-  if constexpr (AOS) {
+  // a later pass whose corners are the last pass's pixels in every lane (the
+  // position moved within its cell): no round trip (wave-uniform test)
+  const bool reuse = !FIRST && KLT_T7_REUSE && __ballot(qb.px != ls.bpx) == 0ull;
+  if (reuse) {
+    bi = ls.bi;
+    bx = ls.bx;
+    by = ls.by;
+  } else if constexpr (AOS) {
     const Tri t = tri(B.img, qb, rowB);
     bi = t.i;
     bx = t.x;
@@ -333,6 +349,12 @@ __device__ __forceinline__ int pass7(const TrkArgs &a, const Lev &A, const Lev &
     bi = quad(B.img, qb, rowB);
     bx = quad(B.gx, qb, rowB);
     by = quad(B.gy, qb, rowB);
+  }
+  if (KLT_T7_REUSE) {
+    ls.bpx = qb.px;
+    ls.bi = bi;
+    ls.bx = bx;
+    ls.by = by;
   }
   Pix qa = qb, qr = qb;
   Quad ai{}, ax{}, ay{}, ri{};
