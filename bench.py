@@ -104,6 +104,10 @@ def parse():
 
 def main() -> None:
     args = parse()
+    # the library's per-call KLTTrackSequence stage line (stderr): the API leg
+    # captures it for each timed call (api.sequence.calls_trace); read once,
+    # at the process's first KLTTrackSequence
+    os.environ.setdefault("KLT_SEQ_TRACE", "1")
     import torch
     import torch.distributed as dist
 
@@ -873,14 +877,37 @@ def api_leg(lib, frames, W, H, NF, args):
     arr = (U8P * (n + 1))(*[u8(a) for a in host])
     ft = lib.KLTCreateFeatureTable(n, NF)
 
-    def sequence():
+    import resource
+    import tempfile
+
+    def sequence(trace=None):
+        """one KLTTrackSequence call; trace (a dict): the library's KLT_SEQ_TRACE line
+        of the call (stderr, captured) and the process's involuntary context switches
+        and page faults over it"""
         tc = lib.KLTCreateTrackingContext()
         tc.contents.sequentialMode = 1
         fl = lib.KLTCreateFeatureList(NF)
         lib.KLTSelectGoodFeatures(tc, u8(host[0]), W, H, fl)
+        if trace is not None:
+            sys.stderr.flush()
+            tmp, saved = tempfile.TemporaryFile(mode="w+"), os.dup(2)
+            os.dup2(tmp.fileno(), 2)
+            r0 = resource.getrusage(resource.RUSAGE_SELF)
         a = time.perf_counter()
         lib.KLTTrackSequence(tc, arr, n + 1, W, H, fl, ft, 0)
         dt = time.perf_counter() - a
+        if trace is not None:
+            r1 = resource.getrusage(resource.RUSAGE_SELF)
+            os.dup2(saved, 2)
+            os.close(saved)
+            tmp.seek(0)
+            line = [t for t in tmp.read().splitlines() if t.startswith("seqtrace")]
+            tmp.close()
+            trace["stages_us"] = {k: float(v) for k, v in (kv.split("=") for kv in line[-1].split()[1:])
+                                  if k.endswith("_us")} if line else None
+            trace["involuntary_context_switches"] = r1.ru_nivcsw - r0.ru_nivcsw
+            trace["minor_page_faults"] = r1.ru_minflt - r0.ru_minflt
+            trace["process_cpu_s"] = (r1.ru_utime + r1.ru_stime) - (r0.ru_utime + r0.ru_stime)
         out = fl_to_arrays(fl)
         lib.KLTFreeFeatureList(fl)
         lib.KLTFreeTrackingContext(tc)
@@ -905,10 +932,11 @@ def api_leg(lib, frames, W, H, NF, args):
     # slower call goes with a slower bus (tools/seq_variance.py)
     bus_src = torch.empty(256 << 20, dtype=torch.uint8).pin_memory()
     bus_dst = torch.empty(256 << 20, dtype=torch.uint8, device=frames.device)
-    runs, bus = [], []
+    runs, bus, traces = [], [], []
     for _ in range(5):
         bus.append(h2d_gbs())
-        runs.append(sequence())
+        traces.append({})
+        runs.append(sequence(traces[-1]))
     del bus_src, bus_dst
     dts = [r[0] for r in runs]
     dt, sq = sorted(dts)[len(dts) // 2], runs[-1][1]
@@ -929,6 +957,7 @@ def api_leg(lib, frames, W, H, NF, args):
                      "h2d_pinned_gbs_before_each_call": bus,
                      "fraction_of_bus_each_call": [(n / d) * W * H / (b * 1e9) for d, b in zip(dts, bus)],
                      "first_call_value": n / dt_cold,
+                     "calls_trace": traces,
                      "first_call": "the process's first KLTTrackSequence: device allocations, pinned staging, "
                                    "host threads, the table's first touch"},
         "per_call_harness": {"value": len(h_times) / sum(h_times), "unit": "frames/s", "calls": len(h_times),
