@@ -150,10 +150,24 @@ __device__ __forceinline__ float interp(const Pix &p, const Quad &q) {
   return p.w0 * q.r0.x + p.w1 * q.r0.y + p.w2 * q.r1.x + p.w3 * q.r1.y;
 }
 
+// The ordered sums hand values between the lanes of one wave through LDS.
+// A wave's LDS operations are performed in order, so a read issued after a
+// write sees it: wavefront-scope fences only keep the compiler from moving
+// the accesses across (no s_waitcnt lgkmcnt(0) between the writes and the
+// reads, as workgroup scope would emit).  KLT_T7_WAVEFENCE=0 restores those.
+#ifndef KLT_T7_WAVEFENCE
+#define KLT_T7_WAVEFENCE 1
+#endif
 __device__ __forceinline__ void wave_lds_sync() {
+#if KLT_T7_WAVEFENCE
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#else
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#endif
 }
 
 typedef float f4 __attribute__((ext_vector_type(4)));
