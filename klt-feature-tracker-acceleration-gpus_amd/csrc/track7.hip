@@ -41,9 +41,6 @@
 #ifndef KLT_T7_REUSE
 #define KLT_T7_REUSE 1  // a pass whose window corners are the previous pass's takes them from registers
 #endif
-#ifndef KLT_T7_AHEAD
-#define KLT_T7_AHEAD 1  // the finest level's first corners fetched with the coarse level's first gathers
-#endif
 #ifndef KLT_T7_BATCH
 #define KLT_T7_BATCH 7  // 16-byte LDS reads in flight per ordered-sum batch (13 per row)
 #endif
@@ -315,40 +312,6 @@ struct LevState {
 
 enum { kPassAgain = 0, kPassDone = 1, kPassOOB = 2, kPassLostPrev = 3 };
 
-// KLT_T7_AHEAD: corners for the finest level's first pass that need no round
-// trip of their own.  Image 1 there is the previous frame's image 2 (the same
-// bank frame) at that frame's final position, so the last corners the
-// previous frame's finest level gathered serve (carried in registers across
-// the frame); image 2's are loaded at the frame's start, in the same round
-// trip as the coarse level's first gathers, at the position the feature's
-// last motion predicts (x1 + the previous frame's displacement).  The first
-// pass takes a set when its pixels are the same in every lane (one ballot),
-// so a good prediction saves that pass's round trip; the values are the same
-// pixels either way.
-struct Corners {
-  bool on = false;
-  unsigned px = ~0u;
-  Quad i, x, y;
-};
-struct Ahead {
-  Corners a, b;  // image 1, image 2
-};
-
-template <bool AOS>
-__device__ __forceinline__ void load3(const Lev &L, const Pix &p, Quad &i, Quad &x, Quad &y) {
-  const unsigned row = (unsigned)L.w * (AOS ? 12u : 4u);
-  if constexpr (AOS) {
-    const Tri t = tri(L.img, p, row);
-    i = t.i;
-    x = t.x;
-    y = t.y;
-  } else {
-    i = quad(L.img, p, row);
-    x = quad(L.gx, p, row);
-    y = quad(L.gy, p, row);
-  }
-}
-
 // One pass of the Newton loop (trackFeatures.c:418-457): the top-of-loop
 // bounds test, one gather round trip (img2's planes at x2; img1's at x1 on the
 // level's FIRST pass; the deferred residue's img2 plane with a JOB), the
@@ -357,7 +320,7 @@ __device__ __forceinline__ void load3(const Lev &L, const Pix &p, Quad &i, Quad 
 template <bool BAND, bool FIRST, bool JOB, bool AOS, bool FAST>
 __device__ __forceinline__ int pass7(const TrkArgs &a, const Lev &A, const Lev &B, float x1, float y1, bool x1_out,
                                      LevState &ls, int lane, float fi, float fj, bool on, float *red, Pending &pd,
-                                     const Lev &R, int &rstat, Counts &cnt, const Ahead &ah) {
+                                     const Lev &R, int &rstat, Counts &cnt) {
   T7_T(t_top);
   bool stop = (FIRST && x1_out) || out7(ls.x2, ls.y2, A.tx, A.ty);
   if (BAND && !stop && (band_bad(B, ls.y2) || (FIRST && band_bad(A, y1)))) {
@@ -387,15 +350,10 @@ __device__ __forceinline__ int pass7(const TrkArgs &a, const Lev &A, const Lev &
   // a later pass whose corners are the last pass's pixels in every lane (the
   // position moved within its cell): no round trip (wave-uniform test)
   const bool reuse = !FIRST && KLT_T7_REUSE && __ballot(qb.px != ls.bpx) == 0ull;
-  const bool ahead_b = FIRST && ah.b.on && __ballot(qb.px != ah.b.px) == 0ull;
   if (reuse) {
     bi = ls.bi;
     bx = ls.bx;
     by = ls.by;
-  } else if (ahead_b) {
-    bi = ah.b.i;
-    bx = ah.b.x;
-    by = ah.b.y;
   } else if constexpr (AOS) {
     const Tri t = tri(B.img, qb, rowB);
     bi = t.i;
@@ -415,13 +373,17 @@ __device__ __forceinline__ int pass7(const TrkArgs &a, const Lev &A, const Lev &
   Pix qa = qb, qr = qb;
   Quad ai{}, ax{}, ay{}, ri{};
   if (FIRST) {
+    const unsigned rowA = (unsigned)A.w * (AOS ? 12u : 4u);
     qa = pix_at(A.w, A.h, x1 + fi, y1 + fj);
-    if (ah.a.on && __ballot(qa.px != ah.a.px) == 0ull) {
-      ai = ah.a.i;
-      ax = ah.a.x;
-      ay = ah.a.y;
+    if constexpr (AOS) {
+      const Tri t = tri(A.img, qa, rowA);
+      ai = t.i;
+      ax = t.x;
+      ay = t.y;
     } else {
-      load3<AOS>(A, qa, ai, ax, ay);
+      ai = quad(A.img, qa, rowA);
+      ax = quad(A.gx, qa, rowA);
+      ay = quad(A.gy, qa, rowA);
     }
   }
   if (JOB) {
@@ -485,28 +447,18 @@ __device__ __forceinline__ int pass7(const TrkArgs &a, const Lev &A, const Lev &
 template <bool BAND, bool AOS, bool FAST>
 __device__ int level7(const TrkArgs &a, const Lev &A, const Lev &B, float x1, float y1, float &x2, float &y2,
                       int lane, float fi, float fj, bool on, float *red, bool residue, bool defer, Pending &pd,
-                      bool job, const Lev &R, int &rstat, bool &lost_prev, Counts &cnt, const Ahead &ah,
-                      Corners &last) {
+                      bool job, const Lev &R, int &rstat, bool &lost_prev, Counts &cnt) {
   const bool x1_out = out7(x1, y1, A.tx, A.ty);
   LevState ls;
   ls.x2 = x2;
   ls.y2 = y2;
-  const Ahead none{};
-  int r = job ? pass7<BAND, true, true, AOS, FAST>(a, A, B, x1, y1, x1_out, ls, lane, fi, fj, on, red, pd, R, rstat, cnt,
-                                                   ah)
+  int r = job ? pass7<BAND, true, true, AOS, FAST>(a, A, B, x1, y1, x1_out, ls, lane, fi, fj, on, red, pd, R, rstat, cnt)
               : pass7<BAND, true, false, AOS, FAST>(a, A, B, x1, y1, x1_out, ls, lane, fi, fj, on, red, pd, R, rstat,
-                                                    cnt, ah);
+                                                    cnt);
   while (r == kPassAgain)
-    r = pass7<BAND, false, false, AOS, FAST>(a, A, B, x1, y1, x1_out, ls, lane, fi, fj, on, red, pd, R, rstat, cnt,
-                                             none);
+    r = pass7<BAND, false, false, AOS, FAST>(a, A, B, x1, y1, x1_out, ls, lane, fi, fj, on, red, pd, R, rstat, cnt);
   x2 = ls.x2;
   y2 = ls.y2;
-  // the last image-2 corners this level gathered (KLT_T7_REUSE keeps them)
-  last.on = KLT_T7_REUSE && ls.bpx != ~0u;
-  last.px = ls.bpx;
-  last.i = ls.bi;
-  last.x = ls.bx;
-  last.y = ls.by;
   if (r == kPassLostPrev) {
     lost_prev = true;
     return kTracked;
@@ -567,8 +519,6 @@ __global__ __launch_bounds__(kBlock) void k_track7(TrkArgs a, TrkFramesArgs b, f
 
   float x = u(fx[f]), y = u(fy[f]);
   int v = u(fv[f]);
-  float vx = 0.0f, vy = 0.0f;  // the last frame's displacement (KLT_T7_AHEAD's prediction)
-  Corners carry;  // the finest level's last image-2 corners of the previous frame (this launch)
   const int nlev = NL > 0 ? NL : a.nlev;
   const bool merge = a.merge_res && nlev >= 2;
   Pending pd;
@@ -593,32 +543,6 @@ __global__ __launch_bounds__(kBlock) void k_track7(TrkArgs a, TrkFramesArgs b, f
       float xo = xl, yo = yl;
       int val = kTracked;
       bool lost_prev = false;
-      Ahead ah;  // the finest level's first corners, in flight with the coarse level's first gathers
-      ah.a = carry;  // image 1 of frame j is image 2 of frame j-1 (the same bank frame); off at j = 0
-      carry.on = false;
-      if (KLT_T7_AHEAD && nlev >= 2 && v >= 0) {
-        float x1f = xl, y1f = yl;  // x1 at the finest level, as the level loop computes it
-#pragma unroll
-        for (int r = nlev - 1; r >= 0; --r) {
-          x1f = u(x1f * a.ss);
-          y1f = u(y1f * a.ss);
-        }
-        const float xq = u(x1f + vx), yq = u(y1f + vy);  // where the finest level's first pass is expected
-        const Lev A0 = lev_prev(a, b, 0, j);
-        const Lev B0 = lev_of(a.B[0], (long)j * b.lfs[0], a.oobx[0], a.ooby[0]);
-        // only a position the passes' own tests would let gather (every corner inside the level)
-        if (!out7(xq, yq, B0.tx, B0.ty) && !(BAND && band_bad(B0, yq))) {
-          const Pix qb = pix_at(B0.w, B0.h, xq + fi, yq + fj);
-          load3<AOS>(B0, qb, ah.b.i, ah.b.x, ah.b.y);
-          ah.b.px = qb.px;
-          ah.b.on = true;
-        }
-        (void)x1f;
-        (void)y1f;
-      } else {
-        ah.a.on = false;
-      }
-      const Ahead none{};
 #pragma unroll
       for (int r = nlev - 1; r >= 0; --r) {
         xl = u(xl * a.ss);
@@ -629,11 +553,8 @@ __global__ __launch_bounds__(kBlock) void k_track7(TrkArgs a, TrkFramesArgs b, f
         const Lev LB = lev_of(a.B[r], (long)j * b.lfs[r], a.oobx[r], a.ooby[r]);
         const bool lj = job && r == nlev - 1;
         T7_T(t_l0);
-        Corners last;
         val = level7<BAND, AOS, FAST>(a, LA, LB, xl, yl, xo, yo, lane, fi, fj, on, red, r == 0,
-                           merge && r == 0 && j + 1 < b.nframes, pd, lj, R, rstat, lost_prev, cnt,
-                           r == 0 ? ah : none, last);
-        if (r == 0) carry = last;
+                           merge && r == 0 && j + 1 < b.nframes, pd, lj, R, rstat, lost_prev, cnt);
         T7_ADD(10, t_l0);
         if (lost_prev) break;
         if (val == kSmallDet || val == kOOB) break;
@@ -651,8 +572,6 @@ __global__ __launch_bounds__(kBlock) void k_track7(TrkArgs a, TrkFramesArgs b, f
           y = -1.0f;
           v = val;
         } else {
-          vx = u(xo - x);  // this frame's displacement: the next frame's prediction
-          vy = u(yo - y);
           x = xo;
           y = yo;
           v = kTracked;
