@@ -49,6 +49,8 @@ def main():
     ap.add_argument("--frames", type=int, default=129, help="frames incl. the selection frame")
     ap.add_argument("--chunk", type=int, default=64)
     ap.add_argument("--first-chunk", type=int, default=None, help="first chunk's frames (default: chunk)")
+    ap.add_argument("--track-prio", type=int, default=None,
+                    help="replays: klt_hip_set_track_prio (default: the library's, raised)")
     ap.add_argument("--worlds", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--margins", type=int, nargs="+", default=[64])
     ap.add_argument("--seed", type=int, default=2160)
@@ -113,6 +115,8 @@ def main():
         tc.contents.sequentialMode = 1
         ctx = lib.klt_amd_device_context(tc)
         use_torch_stream(lib, ctx, dev)
+        if a.track_prio is not None:
+            check(lib, ctx, lib.klt_hip_set_track_prio(ctx, a.track_prio), "track_prio")
         pd, td = descs(tc)
         k = [0]
 
@@ -272,7 +276,8 @@ def main():
                     cmd = [sys.executable, __file__, "--replay", f, "--rank", str(r), "--width", str(W), "--height",
                            str(H), "--features", str(NF), "--frames", str(a.frames), "--chunk", str(a.chunk),
                            "--seed", str(a.seed)] + ([] if a.first_chunk is None else
-                                                     ["--first-chunk", str(a.first_chunk)])
+                                                     ["--first-chunk", str(a.first_chunk)]) + (
+                        [] if a.track_prio is None else ["--track-prio", str(a.track_prio)])
                     res = subprocess.run(cmd, check=True, capture_output=True, text=True)
                     reps.append(json.loads(res.stdout.strip().splitlines()[-1]))
             frames = sum(n for _, n in chunks)
