@@ -91,6 +91,7 @@ def parse():
     p.add_argument("--no-device-warmup", dest="device_warmup", action="store_false",
                    help="skip the untimed, discarded >= 30 ms run of the timed schedule before the W warm-up frames "
                         "(sequences mode; the timed region then starts at the clock left by the host-side selection)")
+    p.add_argument("--keep-order-cache", action="store_true", help=argparse.SUPPRESS)  # A/B hook
     p.add_argument("--event-timing", choices=["timed", "replay"], default="replay",
                    help="record per-kernel HIP events inside the timed region or in a replay")
     a = p.parse_args()
@@ -237,6 +238,12 @@ def main() -> None:
     dev_warm_ms = 1e3 * (time.perf_counter() - d0)
     x.copy_(x0); y.copy_(y0); v.copy_(v0)
     build0(0)
+    # ... and the library's cached processing order (reused by short calls
+    # while it covers <= 32 tracked frames) is dropped, so that the W warm-up
+    # frames and the timed region find the order state they would find with
+    # no device warm-up: the warm-up leaves no state behind but the clock
+    if args.device_warmup and not args.keep_order_cache:
+        check(lib, ctx, lib.klt_hip_set_track_order(ctx, 0), "track order")
     # the W warm-up steps right before the timed K: the harness's own
     # bookkeeping (argument marshalling, the replay's start-state snapshot,
     # the live count) is done around them, not between them and the timed

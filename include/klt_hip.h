@@ -130,7 +130,9 @@ int klt_hip_build_pyramid(klt_hip_ctx *ctx, int slot, const klt_hip_pyr_desc *de
    fused kernels apply (they must agree bit for bit) */
 int klt_hip_set_path(klt_hip_ctx *ctx, int force_generic);
 /* tuning hook: 1 tracks features in input order; 0 (default) in row-band
-   order with each XCD given one band (L2 locality).  Results do not depend on it. */
+   order with each XCD given one band (L2 locality).  Results do not depend on it.
+   Either call also drops the cached band order (reused by short calls while it
+   covers at most 32 tracked frames), so the next call sorts afresh. */
 int klt_hip_set_track_order(klt_hip_ctx *ctx, int input_order);
 /* tracker kernel for the default configuration (7x7 window, exact sums, no
    gain/bias): 0 (default) the latency-lean k_track7 (track7.hip), 1 the

@@ -1453,6 +1453,8 @@ KLT_API int klt_hip_get_track_count(klt_hip_ctx *c, unsigned long long *solves, 
 KLT_API int klt_hip_set_track_order(klt_hip_ctx *c, int input_order) {
   if (!c) return fail(c, "set_track_order: null context");
   c->track_order = input_order ? 1 : 0;
+  c->perm_n = -1;  // the cached processing order is dropped: the next call sorts afresh
+  c->perm_age = 0;
   return 0;
 }
 
