@@ -213,6 +213,10 @@ __device__ __forceinline__ void sums7(float *red, int lane, bool on, const float
 // rotations leave every lane of a 16-lane row its row's sum, then the four
 // row sums are read out and added -- no LDS round trip and no 49-add chain
 constexpr int kQuadXor1 = 0xB1, kQuadXor2 = 0x4E, kRowRor4 = 0x124, kRowRor8 = 0x128;  // DPP controls
+constexpr int kRowBcast15 = 0x142, kRowBcast31 = 0x143;                                // GFX9 DPP broadcasts
+#ifndef KLT_T7_BCAST
+#define KLT_T7_BCAST 1  // the fast sums' row totals combined by DPP broadcasts (A/B hook: 0 reads four lanes)
+#endif
 template <int CTRL>
 __device__ __forceinline__ float dpp_add(float x) {
   return x + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
@@ -231,12 +235,28 @@ __device__ __forceinline__ void tree7(bool on, const float (&v)[NS], float (&out
   for (int s = 0; s < NS; ++s) x[s] = dpp_add<kRowRor4>(x[s]);
 #pragma unroll
   for (int s = 0; s < NS; ++s) x[s] = dpp_add<kRowRor8>(x[s]);
+#if KLT_T7_BCAST
+  // the four row sums r0..r3 combined in the VALU: row_bcast:15 adds row 0's
+  // sum into row 1 and row 2's into row 3, row_bcast:31 then row 1's
+  // (r0 + r1) into row 3, so lane 63 holds (r2 + r3) + (r0 + r1) -- the same
+  // float as (r0 + r1) + (r2 + r3), addition being commutative -- and one
+  // readlane per sum leaves the VALU instead of four
+#pragma unroll
+  for (int s = 0; s < NS; ++s) x[s] = x[s] + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x[s]),
+                                                                                          kRowBcast15, 0xA, 0xF, false));
+#pragma unroll
+  for (int s = 0; s < NS; ++s) x[s] = x[s] + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x[s]),
+                                                                                          kRowBcast31, 0xC, 0xF, false));
+#pragma unroll
+  for (int s = 0; s < NS; ++s) out[s] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x[s]), 63));
+#else
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const int b = __float_as_int(x[s]);
     out[s] = (__int_as_float(__builtin_amdgcn_readlane(b, 0)) + __int_as_float(__builtin_amdgcn_readlane(b, 16))) +
              (__int_as_float(__builtin_amdgcn_readlane(b, 32)) + __int_as_float(__builtin_amdgcn_readlane(b, 48)));
   }
+#endif
 }
 
 template <int NS, bool FAST>
