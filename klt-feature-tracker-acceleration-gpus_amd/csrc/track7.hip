@@ -240,13 +240,15 @@ __device__ __forceinline__ void tree7(bool on, const float (&v)[NS], float (&out
   // sum into row 1 and row 2's into row 3, row_bcast:31 then row 1's
   // (r0 + r1) into row 3, so lane 63 holds (r2 + r3) + (r0 + r1) -- the same
   // float as (r0 + r1) + (r2 + r3), addition being commutative -- and one
-  // readlane per sum leaves the VALU instead of four
+  // readlane per sum leaves the VALU instead of four.  Every row is enabled
+  // (bound_ctrl: a lane without a source adds +0) so that each step is one
+  // v_add_f32_dpp; the other rows' values are not read
 #pragma unroll
   for (int s = 0; s < NS; ++s) x[s] = x[s] + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x[s]),
-                                                                                          kRowBcast15, 0xA, 0xF, false));
+                                                                                          kRowBcast15, 0xF, 0xF, true));
 #pragma unroll
   for (int s = 0; s < NS; ++s) x[s] = x[s] + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x[s]),
-                                                                                          kRowBcast31, 0xC, 0xF, false));
+                                                                                          kRowBcast31, 0xF, 0xF, true));
 #pragma unroll
   for (int s = 0; s < NS; ++s) out[s] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x[s]), 63));
 #else
