@@ -21,7 +21,11 @@ back to back), kernels (avg us per launch), tracker
 (Newton iterations counted on the device in a separate replay,
 feature-iterations/s over the tracker's own event time), cpu_baseline (the reference compiled
 from its own sources, oracle/_ref, timed on this host), parity (GPU vs that
-reference on the CPU sample, cell by cell).
+reference on the CPU sample, cell by cell), sharded_4k (every rank, at every
+N: BASELINE config 4 -- 4K, 20 000 features, 1 000 frames -- with the features
+sharded by row band over the N GPUs and one all-gather per 64-frame chunk;
+strong scaling; the all-gather timed by HIP events in a replay; the list
+checked against the reference's column digests).
 """
 from __future__ import annotations
 
@@ -64,6 +68,9 @@ def parse():
     p.add_argument("--no-4k", action="store_true", help="skip the 4K legs (pass roofline, frames_4k; rank 0, N=1)")
     p.add_argument("--no-frames-4k", action="store_true",
                    help="skip the frames_4k leg (config 4 on one GPU: 1000 4K frames, device and KLTTrackSequence)")
+    p.add_argument("--no-sharded-4k", action="store_true",
+                   help="skip the sharded_4k leg (BASELINE config 4 sharded over the N ranks: 4K, 20 000 features, "
+                        "1 000 frames, one all-gather per chunk; every rank)")
     p.add_argument("--reduction", choices=["exact", "fast"], default="exact")
     p.add_argument("--chunk", type=int, default=None,
                    help="frames per batched pyramid/track launch (klt_hip_track_frames; default 64; sharded: frames "
@@ -448,44 +455,86 @@ def main() -> None:
             if key in result:
                 result[key]["measured_peak"] = dict(mp, frac_vs_copy=result[key]["achieved"] / mp["copy_gbs"],
                                                     frac_vs_fill=result[key]["achieved"] / mp["fill_gbs"])
+    if not args.no_sharded_4k:
+        # every rank: the config-4 strong-scaling leg (4K/20k, row bands, one
+        # all-gather per chunk), so that the driver's --gpus N runs measure it
+        sh = sharded_4k_leg(world, rank, dev, args)
+        if rank == 0:
+            result["sharded_4k"] = sh
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def run_sharded(args, world, rank, dev) -> None:
-    """BASELINE config 4: one sequence (default 4K, 20k features); every rank
-    holds only the rows of each frame its band build reads (its band, margin
-    and tile halo: kltamd.shard.BandFrames, synthesized in place of its
-    ingest), builds pyramids for its row band (+margin) and tracks the features
-    it owns; one all-gather of the owners' (x, y, val) slots per chunk
-    (kltamd.shard)."""
+def gather_floats(vals, world, dev):
+    """Every rank's list of floats (the same length on every rank), in rank order."""
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return [list(vals)]
+    t = torch.tensor(vals, dtype=torch.float64)
+    if dist.get_backend() == "nccl":
+        t = t.to(dev)
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return [p.cpu().tolist() for p in parts]
+
+
+def state_digest(x, y, v) -> str:
+    """The column digest of tests/golden/long_config*.json: sha256(x f32 LE || y f32 LE || val i32 LE)."""
+    import hashlib
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(x.cpu().numpy(), "<f4").tobytes())
+    h.update(np.ascontiguousarray(y.cpu().numpy(), "<f4").tobytes())
+    h.update(np.ascontiguousarray(v.cpu().numpy(), "<i4").tobytes())
+    return h.hexdigest()
+
+
+def sharded_core(world, rank, dev, W, H, NF, seed, warmup, steps, chunk, margin, reduction="exact", replay=True):
+    """BASELINE config 4's sharded loop (trackFeatures.c:1343-1501 inside
+    example3.c:54-76, features sharded over the ranks): every rank holds only
+    the rows of each frame its band build reads (its band, margin and tile
+    halo: kltamd.shard.BandFrames, synthesized in place of its ingest), builds
+    pyramids for its row band (+margin) and tracks the features it owns; one
+    all-gather of the owners' (x, y, val) slots per chunk (kltamd.shard).
+
+    Frames 1 .. warmup are tracked untimed, frames warmup+1 .. warmup+steps
+    are the timed region (barrier + synchronize on both sides, max over
+    ranks).  replay: the timed frames again from the same state with HIP
+    events on the tracking stream around every all-gather (the RCCL
+    collective as the chunk's stream sees it) and after every exchange (chunk
+    times), so the timed region itself carries no timing events.  Parity: the
+    list after the warm-up, after the timed region and after the replay,
+    against the reference's column digests (tests/golden/long_config4.json)
+    when the workload is that sequence."""
     import torch
     import torch.distributed as dist
 
     import kltamd
+    from kltabi import GOLDEN
     from kltamd.device import EXACT, FAST, PyrDesc, TrackDesc, check, use_torch_stream
     from kltamd.shard import BandFrames, ShardedSequence, band_of, row_edges
 
     lib = kltamd.load()
     lib.KLTSetVerbosity(0)
-    W, H, NF = args.width, args.height, args.features
-    nframes = 1 + args.warmup + args.steps
+    nframes = 1 + warmup + steps
     tc = lib.KLTCreateTrackingContext()
     tc.contents.sequentialMode = 1
-    lib.klt_amd_set_reduction(tc, EXACT if args.reduction == "exact" else FAST)
+    lib.klt_amd_set_reduction(tc, EXACT if reduction == "exact" else FAST)
     ctx = lib.klt_amd_device_context(tc)
     use_torch_stream(lib, ctx, dev)  # library kernels and torch ops ordered on one stream
+
     def load(t0, n, row0, nrows, dst, stride):  # this rank's ingest of rows row0 .. row0+nrows-1
-        check(lib, ctx, lib.klt_hip_synth_rows(ctx, args.seed, t0, n, W, row0, nrows, C.c_void_p(dst), W, stride),
+        check(lib, ctx, lib.klt_hip_synth_rows(ctx, seed, t0, n, W, row0, nrows, C.c_void_p(dst), W, stride),
               "synth")
 
-    edges = row_edges(H, world, args.margin)  # equal level-0 rows built per rank (klt_shard_create's bands)
-    frames = BandFrames(nframes, H, W, band_of(H, world, rank, args.margin, edges), load, dev)
+    t_setup = time.perf_counter()
+    edges = row_edges(H, world, margin)  # equal level-0 rows built per rank (klt_shard_create's bands)
+    frames = BandFrames(nframes, H, W, band_of(H, world, rank, margin, edges), load, dev)
     torch.cuda.synchronize()
     f0 = np.empty((H, W), np.uint8)  # frame 0 whole, for the selection every rank makes
-    lib.klt_synth_frame(args.seed, 0, W, H, f0.ctypes.data)
+    lib.klt_synth_frame(seed, 0, W, H, f0.ctypes.data)
     fl = lib.KLTCreateFeatureList(NF)
     lib.KLTSelectGoodFeatures(tc, f0.ctypes.data_as(C.POINTER(C.c_ubyte)), W, H, fl)
     sel = np.array([[fl.contents.feature[k].contents.x, fl.contents.feature[k].contents.y,
@@ -498,7 +547,13 @@ def run_sharded(args, world, rank, dev) -> None:
     lib.klt_amd_pyr_desc(tc, W, H, tc.contents.nPyramidLevels, 1, C.byref(pd))
     lib.klt_amd_track_desc(tc, C.byref(td))
 
+    gather_events = []  # (start, end) HIP event pairs around each all-gather, when timing
+
     def all_gather(out, inp):  # the per-chunk exchange: every rank's slot, in rank order
+        ev = None
+        if timing[0]:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         if world == 1:
             out.copy_(inp)
         elif dist.get_backend() == "gloo":  # the shared-GPU rehearsal (KLT_BENCH_SHARE_GPU=1)
@@ -507,35 +562,145 @@ def run_sharded(args, world, rank, dev) -> None:
             out.copy_(torch.cat(parts))
         else:
             dist.all_gather_into_tensor(out, inp)
+        if ev is not None:
+            ev[1].record()
+            gather_events.append(ev)
 
-    seq = ShardedSequence(lib, ctx, pd, td, frames, x, y, v, rank, world, all_gather, chunk=args.chunk,
-                          margin=args.margin, edges=edges)
+    timing = [False]
+    seq = ShardedSequence(lib, ctx, pd, td, frames, x, y, v, rank, world, all_gather, chunk=chunk,
+                          margin=margin, edges=edges)
     seq.begin(0)
-    seq.run(1, args.warmup)
-    v_warm = v.clone()  # the live count after the warm-up, read after the timed region (as in the default mode)
+    seq.run(1, warmup)
+    torch.cuda.synchronize()
+    d_warm = state_digest(x, y, v)
+    xs, ys, vs = x.clone(), y.clone(), v.clone()
+    live_before = int((vs >= 0).sum().item())
+    setup_s = time.perf_counter() - t_setup
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    seq.run(1 + args.warmup, args.steps)
+    seq.run(1 + warmup, steps)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    live_before = int((v_warm >= 0).sum().item())
     if world > 1:
         dist.barrier()
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    digest = int((x.view(torch.int32).to(torch.int64).sum() * 3 + y.view(torch.int32).to(torch.int64).sum() * 5
-                  + v.to(torch.int64).sum() * 7).item())
+    redone_timed = seq.redone
+    d_end = state_digest(x, y, v)
+    live_end = int((v >= 0).sum().item())
+    per_rank_s = [r[0] for r in gather_floats([dt], world, dev)]
+    dt_max = max(per_rank_s)
+
+    rep = None
+    if replay and steps > 0:
+        # the same frames from the same state, with events: the all-gather's
+        # time per chunk and each chunk's time on this rank
+        x.copy_(xs); y.copy_(ys); v.copy_(vs)
+        seq.begin(warmup)
+        torch.cuda.synchronize()
+        timing[0] = True
+        seq.xch.timing, seq.xch.timing_events = True, []
+        if world > 1:
+            dist.barrier()
+        e_start = torch.cuda.Event(enable_timing=True)
+        e_start.record()
+        seq.run(1 + warmup, steps)
+        torch.cuda.synchronize()
+        timing[0] = False
+        seq.xch.timing = False
+        ag = [a.elapsed_time(b) * 1e3 for a, b in gather_events]
+        ends = [e_start] + seq.xch.timing_events
+        chunk_us = [a.elapsed_time(b) * 1e3 for a, b in zip(ends, ends[1:])]
+        d_rep = state_digest(x, y, v)
+        stats = [float(np.median(ag)) if ag else 0.0, max(ag) if ag else 0.0, float(sum(ag)),
+                 float(np.median(chunk_us)) if chunk_us else 0.0, float(sum(chunk_us))]
+        all_stats = gather_floats(stats, world, dev)
+        rep = {"allgather_us_per_chunk_median": max(s[0] for s in all_stats),
+               "allgather_us_per_chunk_max": max(s[1] for s in all_stats),
+               "allgather_us_per_chunk_median_by_rank": [s[0] for s in all_stats],
+               "allgather_us_per_frame": max(s[2] for s in all_stats) / steps,
+               "allgather_calls_per_rank": len(ag),
+               "chunk_us_median_by_rank": [s[3] for s in all_stats],
+               "replay_us_per_frame_by_rank": [s[4] / steps for s in all_stats],
+               "allgather_op": ("copy (world 1)" if world == 1 else
+                                "torch.distributed.all_gather_into_tensor (" + dist.get_backend() + ")"),
+               "what": "a replay of the timed frames from the same state with HIP events on the tracking stream "
+                       "around each all-gather (the collective as the chunk's stream sees it, wait included) and "
+                       "after each exchange; the timed region carries no events",
+               "state_equals_timed_region": d_rep == d_end}
+    # parity: the reference's column digests of this sequence (column j = the list after frame j+1)
+    fix = GOLDEN / "long_config4.json"
+    parity = None
+    if fix.exists():
+        cfg = json.loads(fix.read_text())
+        if (cfg["w"], cfg["h"], cfg["features"], cfg["seed"]) == (W, H, NF, seed) and nframes <= cfg["frames"]:
+            cols = cfg["columns"]
+            got = [(warmup, d_warm), (warmup + steps, d_end)]
+            if rep is not None:
+                got.append((warmup + steps, d_rep))
+            mism = sum(1 for f, d in got if f >= 1 and d != cols[f - 1])
+            parity = {"against": "tests/golden/long_config4.json (reference src/V3 compiled from its own sources, "
+                                 "oracle/_ref)",
+                      "columns_compared": [f for f, _ in got],
+                      "columns_mismatched": mism,
+                      "digest": "sha256(x f32 LE || y f32 LE || val i32 LE) of the whole list, rank 0"}
+    agree = gather_floats([float(int(d_end[:12], 16))], world, dev)
+    out = {
+        "value": steps / dt_max,
+        "unit": "frames/s",
+        "us_per_frame": 1e6 * dt_max / steps,
+        "n_gpus": world,
+        "scaling": "strong",
+        "frames_timed": steps,
+        "ms": 1e3 * dt_max,
+        "rank_us_per_frame": [1e6 * s / steps for s in per_rank_s],
+        "workload": f"{W}x{H}, {NF} features selected on frame 0, one sequence of {nframes} frames (seed {seed}), "
+                    f"features sharded by row band over {world} GPU(s) (BASELINE config 4); frames 1..{warmup} "
+                    f"untimed, {warmup + 1}..{warmup + steps} timed",
+        "chunk": chunk, "margin_rows": margin, "bands_edges": list(edges),
+        "rank_frame_rows": [frames.ra, frames.rb],
+        "live_features": {"after_warmup": live_before, "at_end": live_end},
+        "chunks_redone_full_frame": redone_timed,
+        "state_digest": d_end,
+        "ranks_agree_on_state": len({a[0] for a in agree}) == 1,
+        "setup_s": setup_s,
+    }
+    if rep is not None:
+        out["exchange"] = rep
+    if parity is not None:
+        out["parity"] = parity
+    lib.KLTFreeTrackingContext(tc)
+    del frames, x, y, v, xs, ys, vs
+    lib.klt_amd_release_cached_devices()
+    torch.cuda.empty_cache()
+    return out
+
+
+def sharded_4k_leg(world, rank, dev, args):
+    """The north-star's strong-scaling workload in every run, at N = 1 and
+    N > 1 (every rank takes part): BASELINE config 4, 3840x2160, 20 000
+    features, the 1 000-frame sequence tests/golden/long_config4.json pins,
+    64-frame chunks, 64-row margins; 64 frames warm up, 935 are timed."""
+    cfg = json.loads((ROOT / "tests" / "golden" / "long_config4.json").read_text())
+    wu = 64
+    return sharded_core(world, rank, dev, cfg["w"], cfg["h"], cfg["features"], cfg["seed"], wu,
+                        cfg["frames"] - 1 - wu, 64, 64)
+
+
+def run_sharded(args, world, rank, dev) -> None:
+    """--mode sharded: config 4 as the whole bench line (sharded_core)."""
+    import torch.distributed as dist
+    r = sharded_core(world, rank, dev, args.width, args.height, args.features, args.seed, args.warmup, args.steps,
+                     args.chunk, args.margin, args.reduction)
+    W, H, NF = args.width, args.height, args.features
     result = {
         "metric": METRIC,
-        "value": args.steps / dt,
+        "value": r["value"],
         "unit": "frames/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": 1000.0 * dt / args.steps,
+        "ms_per_step": r["us_per_frame"] / 1e3,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -543,14 +708,14 @@ def run_sharded(args, world, rank, dev) -> None:
         "data": f"synthetic: include/klt_synth.h value-noise frames, (0.7,0.3) px/frame, seed {args.seed}",
         "config": {"workload": f"{W}x{H}, {NF} features, one sequence, features sharded by row band over "
                                f"{world} GPU(s) (BASELINE config 4)",
-                   "resolution": f"{W}x{H}", "features": NF, "frames": nframes, "chunk": args.chunk,
-                   "margin_rows": args.margin, "parallelism": f"row-band feature sharding x{world}",
-                   "rank_frame_rows": [frames.ra, frames.rb]},
-        "live_features": {"after_warmup": live_before, "at_end": int((v >= 0).sum().item())},
-        "chunks_redone_full_frame": seq.redone,
-        "state_digest": digest,
+                   "resolution": f"{W}x{H}", "features": NF, "frames": 1 + args.warmup + args.steps,
+                   "chunk": args.chunk, "margin_rows": args.margin, "parallelism": f"row-band feature sharding x{world}",
+                   "rank_frame_rows": r["rank_frame_rows"]},
+        "live_features": r["live_features"],
+        "chunks_redone_full_frame": r["chunks_redone_full_frame"],
+        "state_digest": r["state_digest"],
+        "sharded": r,
     }
-    lib.KLTFreeTrackingContext(tc)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

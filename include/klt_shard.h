@@ -55,7 +55,9 @@ int klt_shard_band_edges(int nrows, int world, int margin, int *edges);
 int klt_shard_unique_id(unsigned char id[KLT_SHARD_ID_BYTES]);
 /* rank `rank` of `world` on the device of `ctx` (ncclCommInitRank; every
    rank must call it); nrows: the frame height, margin: level-0 rows built
-   beyond the band (64 suits the synthetic sequences; any value is exact) */
+   beyond the band (64 suits the synthetic sequences; any value is exact).
+   world is at most KLT_HIP_GATHER_MAX_RANKS (16: the exchange kernels keep one
+   slot per rank).  NULL on failure; klt_shard_create_error() then says why. */
 klt_shard *klt_shard_create(klt_hip_ctx *ctx, int rank, int world, const unsigned char id[KLT_SHARD_ID_BYTES],
                             int nrows, int margin);
 /* single-process rehearsal (tests): the band of rank/world, but the exchange
@@ -67,6 +69,9 @@ klt_shard *klt_shard_create_local(klt_hip_ctx *ctx, int rank, int world, int nro
 /* before the tracking context that owns ctx is freed (it synchronizes ctx) */
 void klt_shard_destroy(klt_shard *s);
 const char *klt_shard_last_error(klt_shard *s);
+/* why the calling thread's last klt_shard_create / klt_shard_create_local
+   returned NULL ("" after a success); valid until that thread's next create */
+const char *klt_shard_create_error(void);
 /* Failures and the collectives.  Argument errors (null pointers, a frame
    height that differs from the shard's) return before any collective; a
    caller passes every rank the same geometry, so every rank returns there.

@@ -131,8 +131,8 @@ inline int usable_cpus() {
 // through its OWN queued tasks beside the workers until its count of
 // unfinished tasks is zero, so no wait can deadlock and one caller's sort never
 // runs another's tasks on its thread.  While any sort is in progress an idle
-// worker spins on the queue for up to kSpinUs after its last task instead of
-// sleeping, so a queued half starts within a microsecond or so rather than
+// worker spins on the queue (for up to spin_us() after its last task, by
+// default until the sort ends) instead of sleeping, so a queued half starts within a microsecond or so rather than
 // after a futex wake-up (the wake-ups cost more than the splits they were
 // waking for); past that, and between sorts, it sleeps until a task is
 // queued.  The pool grows to the largest worker count asked for and lives
@@ -148,7 +148,19 @@ struct Pool {
     std::atomic<int> *pending;
   };
 
-  static constexpr double kSpinUs = 50.0;
+  // how long an idle worker spins after its last task while a sort is in
+  // progress: round 4 spun for the whole sort, round 5 bounded it to 50 us and
+  // REPLACE lost 14 % (the host sort 380 -> 493 us: a worker that fell asleep
+  // during the caller's first partition step of a 49k-point segment paid a
+  // futex wake-up for every half); KLT_SORT_SPIN_US (A/B) overrides, < 0 =
+  // the whole sort
+  static double spin_us() {
+    static const double v = [] {
+      const char *e = std::getenv("KLT_SORT_SPIN_US");
+      return e && *e ? std::atof(e) : -1.0;
+    }();
+    return v;
+  }
   static void pause() {
 #if defined(__x86_64__) || defined(__i386__)
     __builtin_ia32_pause();
@@ -173,6 +185,7 @@ struct Pool {
   std::atomic<bool> quit{false};
   std::atomic<unsigned> gen{0};  // sorts started that queue tasks: wakes the sleepers ahead of the first task
   std::vector<std::thread> threads;
+  std::atomic<int> nthreads{0};  // threads.size(), readable without m (sort() on any caller's thread)
 
   // workers: clamped to usable_cpus() - 1 (the caller sorts too)
   static Pool &get(int workers) {
@@ -181,11 +194,15 @@ struct Pool {
     return *p;
   }
   void grow(int workers) {
-    static const int cap = usable_cpus() - 1;
+    static const int cap = [] {  // KLT_SORT_NO_CLAMP=1 (A/B): the round-4 count, unclamped
+      const char *e = std::getenv("KLT_SORT_NO_CLAMP");
+      return e && *e == '1' ? 1 << 20 : usable_cpus() - 1;
+    }();
     if (workers > cap) workers = cap;
     std::lock_guard<std::mutex> lk(m);
     if (quit.load(std::memory_order_relaxed)) return;
     while ((int)threads.size() < workers) threads.emplace_back([this] { work(); });
+    nthreads.store((int)threads.size(), std::memory_order_release);
   }
   // stop and join every worker (no sort may be in progress); later sorts run
   // on their callers' threads alone
@@ -193,11 +210,16 @@ struct Pool {
     {
       std::lock_guard<std::mutex> lk(m);
       quit.store(true, std::memory_order_relaxed);
+      nthreads.store(0, std::memory_order_release);
     }
     cv.notify_all();
-    for (std::thread &t : threads)
+    std::vector<std::thread> ts;
+    {
+      std::lock_guard<std::mutex> lk(m);
+      ts.swap(threads);
+    }
+    for (std::thread &t : ts)
       if (t.joinable()) t.join();
-    threads.clear();
   }
   bool claim() {
     int k = qn.load(std::memory_order_relaxed);
@@ -212,7 +234,7 @@ struct Pool {
     for (;;) {
       if (quit.load(std::memory_order_relaxed)) return;
       if (!claim()) {
-        if (hot.load(std::memory_order_acquire) > 0 && now_us() - last < kSpinUs) {
+        if (hot.load(std::memory_order_acquire) > 0 && (spin_us() < 0 || now_us() - last < spin_us())) {
           for (int k = 0; k < 32; ++k) pause();
         } else {  // no sort in progress, or none of its tasks for a while: sleep until a task comes
           std::unique_lock<std::mutex> lk(m);
@@ -286,7 +308,7 @@ struct Pool {
   // sort a[0..n) with up to 2^par tasks; returns when all of them are done
   void sort(P *a, unsigned n, int par, unsigned par_min) {
     std::atomic<int> pending{1};
-    if (threads.empty()) par = 0;  // no workers (shut down, or one CPU): the sequential recursion
+    if (nthreads.load(std::memory_order_acquire) == 0) par = 0;  // no workers (shut down, one CPU): sequential
     const bool spin = par > 0 && n >= 2 * par_min;  // tasks will be queued: keep the workers awake meanwhile
     if (spin) {
       hot.fetch_add(1, std::memory_order_release);

@@ -206,6 +206,9 @@ hipError_t launch_affine(hipStream_t st, const AffArgs &a);
 
 // runtime.hip: record a failure in the context's error message (klt_hip_last_error); returns -1
 int ctx_fail(klt_hip_ctx *c, const char *fmt, ...);
+// runtime.hip: the exit hook has run (graphs released, sort pool joined): no
+// new selection graphs may be built or launched
+bool lib_exiting();
 
 // select.hip: exact lazy selection (the reference's quicksort order) with the
 // top-level partition steps on the device

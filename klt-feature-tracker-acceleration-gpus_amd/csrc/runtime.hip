@@ -976,7 +976,7 @@ std::set<klt_hip_ctx *> *g_live = new std::set<klt_hip_ctx *>();  // never destr
 std::atomic<bool> g_exiting{false};
 
 void exit_hook() {
-  g_exiting.store(true);
+  g_exiting.store(true, std::memory_order_release);
   std::lock_guard<std::mutex> lk(g_live_m);
   std::set<int> devs;
   for (klt_hip_ctx *c : *g_live) devs.insert(c->device);
@@ -986,6 +986,11 @@ void exit_hook() {
   sel_pool_shutdown();
 }
 
+}  // namespace
+
+bool kltdev::lib_exiting() { return g_exiting.load(std::memory_order_acquire); }
+
+namespace {
 void live_add(klt_hip_ctx *c) {
   static std::once_flag once;
   std::call_once(once, [] { atexit(exit_hook); });
@@ -1003,6 +1008,12 @@ void live_remove(klt_hip_ctx *c) {
 // valid until klt_hip_set_stream(c, NULL), the reset or the destroy)
 int drain_caller(klt_hip_ctx *c) {
   if (c->stream && c->stream != c->own) {
+    // an earlier caller stream's record (A -> own -> B) is waited for before
+    // the event is re-recorded on the current one, which would overwrite it
+    if (c->caller_pending) {
+      HIPCHK(c, hipEventSynchronize(c->ev_caller));
+      c->caller_pending = false;
+    }
     if (!c->ev_caller) HIPCHK(c, hipEventCreateWithFlags(&c->ev_caller, hipEventDisableTiming));
     HIPCHK(c, hipEventRecord(c->ev_caller, c->stream));
     c->caller_pending = true;

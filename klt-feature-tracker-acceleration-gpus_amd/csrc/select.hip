@@ -427,7 +427,7 @@ int refine_launch(SelEngine *e, hipStream_t st, Seg g, std::string *err) {
   int levels = 2;
   for (long l = g.len; l > T; l /= 2) ++levels;
   const int sw = (g.len / 2 + kSelThreads) / kSelThreads;
-  if (sel_graphs()) {
+  if (sel_graphs() && !lib_exiting()) {  // after the exit hook: plain launches, no graph outlives the code object
     // the steps as one graph launch: 5 * levels kernel launches cost more
     // host time than the steps take on the device.  The kernels read the
     // segment from the device state and skip blocks past it, so one graph

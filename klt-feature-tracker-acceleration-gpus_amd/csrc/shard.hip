@@ -610,11 +610,23 @@ std::vector<int> row_edges(int nrows, int world, int margin, int TH) {
   return best;
 }
 
+// why the calling thread's last klt_shard_create* returned NULL (klt_shard_create_error)
+thread_local std::string t_create_err;
+
+klt_shard *create_fail(const char *why) {
+  t_create_err = why;
+  return nullptr;
+}
+
 // rank/world's band (kltamd/shard.py band_of over row_edges, band_rows) and a
 // communicator of `cranks` ranks in which this one is `crank`
 klt_shard *make_shard(klt_hip_ctx *ctx, int rank, int world, const unsigned char *id, int cranks, int crank,
                       int nrows, int margin) {
-  if (!ctx || !id || world < 1 || rank < 0 || rank >= world || nrows < 1 || margin < 0) return nullptr;
+  t_create_err.clear();
+  if (!ctx || !id || world < 1 || rank < 0 || rank >= world || nrows < 1 || margin < 0)
+    return create_fail("bad arguments (null ctx/id, rank outside [0, world), nrows < 1 or margin < 0)");
+  if (world > KLT_HIP_GATHER_MAX_RANKS)
+    return create_fail("world exceeds KLT_HIP_GATHER_MAX_RANKS (16): the exchange kernels hold one slot per rank");
   klt_shard *s = new klt_shard();
   s->ctx = ctx;
   s->rank = rank;
@@ -637,14 +649,20 @@ klt_shard *make_shard(klt_hip_ctx *ctx, int rank, int world, const unsigned char
   for (int r = 0; r <= world; ++r) s->edges[r] = (float)re[r];
   s->edges[0] = -INFINITY;
   s->edges[world] = INFINITY;
-  if (world > KLT_HIP_GATHER_MAX_RANKS || hipSetDevice(klt_hip_ctx_device(ctx)) != hipSuccess ||
-      ncclCommInitRank(&s->comm, cranks, u, crank) != ncclSuccess ||
-      hipHostMalloc((void **)&s->h_flag, (2 + world) * sizeof(int), hipHostMallocDefault) != hipSuccess ||
-      hipEventCreateWithFlags(&s->ev_counts, hipEventDisableTiming) != hipSuccess) {
+  const char *why = nullptr;
+  if (hipSetDevice(klt_hip_ctx_device(ctx)) != hipSuccess)
+    why = "hipSetDevice failed for the context's device";
+  else if (ncclCommInitRank(&s->comm, cranks, u, crank) != ncclSuccess)
+    why = "ncclCommInitRank failed";
+  else if (hipHostMalloc((void **)&s->h_flag, (2 + world) * sizeof(int), hipHostMallocDefault) != hipSuccess)
+    why = "pinned flag words could not be allocated";
+  else if (hipEventCreateWithFlags(&s->ev_counts, hipEventDisableTiming) != hipSuccess)
+    why = "event creation failed";
+  if (why) {
     if (s->comm) ncclCommDestroy(s->comm);
     if (s->h_flag) hipHostFree(s->h_flag);
     delete s;
-    return nullptr;
+    return create_fail(why);
   }
   return s;
 }
@@ -693,6 +711,8 @@ KLT_API int klt_shard_inject_fault(klt_shard *s, int faults) {
 }
 
 KLT_API const char *klt_shard_last_error(klt_shard *s) { return s ? s->err.c_str() : "null shard"; }
+
+KLT_API const char *klt_shard_create_error(void) { return t_create_err.c_str(); }
 
 KLT_API int klt_shard_rows(const klt_shard *s, int *lo, int *hi) {
   if (!s || !lo || !hi) return -1;

@@ -102,6 +102,7 @@ DEVICE_PROTOS = {
     "klt_shard_create_local": (V, [V, C.c_int, C.c_int, C.c_int, C.c_int]),
     "klt_shard_destroy": (None, [V]),
     "klt_shard_last_error": (C.c_char_p, [V]),
+    "klt_shard_create_error": (C.c_char_p, []),
     "klt_shard_inject_fault": (C.c_int, [V, C.c_int]),
     "klt_shard_rows": (C.c_int, [V, IP, IP]),
     "klt_shard_track": (C.c_int, [V, C.POINTER(PyrDesc), C.POINTER(TrackDesc), V, C.c_long, C.c_long, C.c_int, V,

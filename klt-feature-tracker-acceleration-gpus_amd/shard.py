@@ -460,7 +460,8 @@ class ShardedSequence:
         self.xch.exchange(self.x, self.y, self.v, self.escape, S)
         self.xch.ev.synchronize()
         esc, bad = self.xch.verdict()
-        assert esc == 0 and bad == 0, "a chunk redone from whole frames escaped or failed"
+        if esc or bad:
+            raise RuntimeError(f"a chunk redone from whole frames escaped ({esc}) or its exchange failed ({bad})")
 
     def run(self, t0: int, nframes: int) -> None:
         """Track frames t0 .. t0+nframes-1 (the pyramid of t0-1 must be current:
@@ -481,7 +482,8 @@ class ShardedSequence:
             S = self.xch.slot_size()  # this chunk's counts, with the previous chunk's verdict
             if prev is not None:
                 esc, bad = self.xch.verdict()
-                assert bad == 0, "exchange failed"
+                if bad:
+                    raise RuntimeError(f"exchange failed on {bad} rank(s): the merged list would be wrong")
                 if esc:  # the previous chunk escaped: this chunk ran from a wrong state
                     self._redo(*prev)
                     k = self.xch.k ^ 1  # the redo's exchange ordered (and saved) this chunk's start again
@@ -492,8 +494,12 @@ class ShardedSequence:
             k = k_next
             i += 1
         self.xch.ev.synchronize()
-        if prev is not None and self.xch.verdict()[0]:
-            self._redo(*prev)
+        if prev is not None:
+            esc, bad = self.xch.verdict()
+            if bad:  # the unpack skipped a failed exchange: nothing was merged
+                raise RuntimeError(f"exchange failed on {bad} rank(s): the merged list would be wrong")
+            if esc:
+                self._redo(*prev)
         self.t_last = end - 1
 
     # -- KLTReplaceLostFeatures across the ranks (selectGoodFeatures.c:514-541,

@@ -153,13 +153,14 @@ def test_registered_buffers_bit_identical(gpu):
 def test_reset_drains_the_callers_stream(gpu):
     """a context parked (klt_hip_ctx_reset) while the caller's
     stream (klt_hip_set_stream) still runs its work waits for that work before
-    its buffers are freed and the context is handed on -- both for the stream
-    still set and for one the context switched away from."""
+    its buffers are freed and the context is handed on -- for the stream
+    still set, for one the context switched away from, and for
+    stream A after A -> own -> B, where B's record must not replace A's."""
     import torch
     from kltamd.device import check
     W, H, n = 1920, 1080, 96
     dev = torch.device("cuda", 0)
-    for switch_away in (False, True):
+    for mode in ("still_set", "switch_away", "a_own_b"):
         tc = gpu.KLTCreateTrackingContext()
         ctx = gpu.klt_amd_device_context(tc)
         s = torch.cuda.Stream(dev)
@@ -167,9 +168,12 @@ def test_reset_drains_the_callers_stream(gpu):
         fr = torch.empty((n, H, W), dtype=torch.uint8, device=dev)
         torch.cuda.synchronize()
         check(gpu, ctx, gpu.klt_hip_synth_frames(ctx, 9, 0, n, W, H, C.c_void_p(fr.data_ptr()), W, W * H), "synth")
-        if switch_away:
+        if mode != "still_set":
             check(gpu, ctx, gpu.klt_hip_set_stream(ctx, None), "own stream")
+        if mode == "a_own_b":
+            b = torch.cuda.Stream(dev)  # idle: only A holds the context's work
+            check(gpu, ctx, gpu.klt_hip_set_stream(ctx, C.c_void_p(b.cuda_stream)), "set_stream B")
         gpu.KLTFreeTrackingContext(tc)  # parks the device context: klt_hip_ctx_reset
-        assert s.query(), "the reset returned while the caller's stream still ran the context's work"
+        assert s.query(), f"{mode}: the reset returned while the caller's stream still ran the context's work"
         del fr
     assert gpu.klt_amd_release_cached_devices() >= 1

@@ -661,10 +661,13 @@ def test_c_shard_errors(gpu):
     dfr = torch.from_numpy(np.ascontiguousarray(np.stack(frames))).to(dev)
     rk = _Rank(gpu, dfr, H, W, 4, 1, 0)
     assert not gpu.klt_shard_create_local(rk.ctx, 4, 4, H, 0)   # rank out of range
+    assert b"bad arguments" in gpu.klt_shard_create_error()
     assert not gpu.klt_shard_create_local(rk.ctx, 0, 0, H, 0)   # no ranks
     assert not gpu.klt_shard_create_local(rk.ctx, 0, 2, H, -1)  # negative margin
+    assert not gpu.klt_shard_create_local(rk.ctx, 0, 17, H, 0)  # past KLT_HIP_GATHER_MAX_RANKS
+    assert b"KLT_HIP_GATHER_MAX_RANKS" in gpu.klt_shard_create_error()
     s = gpu.klt_shard_create_local(rk.ctx, 1, 4, H, 0)
-    assert s
+    assert s and gpu.klt_shard_create_error() == b""
     x, y, v = (torch.from_numpy(a).to(dev) for a in _select(gpu, frames[0], 800))
     x0, y0, v0 = x.clone(), y.clone(), v.clone()
     ptrs = (C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), C.c_void_p(v.data_ptr()), x.numel())
