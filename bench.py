@@ -1103,8 +1103,10 @@ def api_leg(lib, frames, W, H, NF, args):
             tmp.seek(0)
             line = [t for t in tmp.read().splitlines() if t.startswith("seqtrace")]
             tmp.close()
-            trace["stages_us"] = {k: float(v) for k, v in (kv.split("=") for kv in line[-1].split()[1:])
-                                  if k.endswith("_us")} if line else None
+            kv = dict(t.split("=") for t in line[-1].split()[1:]) if line else {}
+            trace["stages_us"] = {k: float(v) for k, v in kv.items() if k.endswith("_us")} if line else None
+            # minor page faults per stage: the process's (_pf) and the calling thread's (_tf)
+            trace["stage_faults"] = {k: int(v) for k, v in kv.items() if k.endswith(("_pf", "_tf"))} if line else None
             trace["involuntary_context_switches"] = r1.ru_nivcsw - r0.ru_nivcsw
             trace["minor_page_faults"] = r1.ru_minflt - r0.ru_minflt
             trace["process_cpu_s"] = (r1.ru_utime + r1.ru_stime) - (r0.ru_utime + r0.ru_stime)

@@ -2,6 +2,7 @@
 // slots, banks of batched pyramids, feature buffers), the pipelines that drive
 // the kernels of pyramid.hip / track.hip / affine.hip, and the klt_hip_* C ABI
 // declared in include/klt_hip.h.  No kernels here.
+#include <sys/resource.h>
 #include <math.h>
 #include <stdarg.h>
 #include <stdint.h>
@@ -325,6 +326,54 @@ double wall_us() {
   clock_gettime(CLOCK_MONOTONIC, &ts);
   return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
 }
+
+// KLT_SEQ_TRACE's stage clock for klt_hip_track_frames_host: every interval
+// between two marks is charged to the stage named by the later mark, so the
+// stages add up to the whole call; each stage also gets the process's and the
+// calling thread's minor page faults over its intervals (a call
+// with 2 057 faults and 5.5 ms outside the four stages traced then)
+struct SeqStages {
+  enum { PRE, WAIT_DMA, COPY, LAUNCH, WAIT_ROWS, DELIVER, TAIL, N };
+  bool on = false;
+  double t = 0, t0 = 0, us[N] = {};
+  long pf = 0, tf = 0, pfl[N] = {}, tfl[N] = {};
+  static void faults(long &proc, long &thr) {
+    rusage r{};
+    getrusage(RUSAGE_SELF, &r);
+    proc = r.ru_minflt;
+    getrusage(RUSAGE_THREAD, &r);
+    thr = r.ru_minflt;
+  }
+  void start(bool enabled) {
+    on = enabled;
+    if (!on) return;
+    t = t0 = wall_us();
+    faults(pf, tf);
+  }
+  void mark(int stage) {
+    if (!on) return;
+    const double now = wall_us();
+    long p, q;
+    faults(p, q);
+    us[stage] += now - t;
+    pfl[stage] += p - pf;
+    tfl[stage] += q - tf;
+    t = now;
+    pf = p;
+    tf = q;
+  }
+  void print(int nframes, int nchunks, int threads) const {
+    if (!on) return;
+    static const char *name[N] = {"pre", "wait_dma", "stage_copy", "launch", "wait_rows", "deliver", "tail"};
+    char buf[1024];
+    int k = snprintf(buf, sizeof buf, "seqtrace frames=%d chunks=%d threads=%d total_us=%.0f", nframes, nchunks,
+                     threads, t - t0);
+    for (int i = 0; i < N && k < (int)sizeof buf; ++i)
+      k += snprintf(buf + k, sizeof buf - k, " %s_us=%.0f %s_pf=%ld %s_tf=%ld", name[i], us[i], name[i], pfl[i],
+                    name[i], tfl[i]);
+    fprintf(stderr, "%s\n", buf);
+  }
+};
 
 int use_device(klt_hip_ctx *c) {
   HIPCHK(c, hipSetDevice(c->device));
@@ -975,14 +1024,41 @@ std::mutex g_live_m;
 std::set<klt_hip_ctx *> *g_live = new std::set<klt_hip_ctx *>();  // never destroyed: exit_hook reads it
 std::atomic<bool> g_exiting{false};
 
+// a live (or parked) context's host side of the upload pipelines, released
+// at exit after the device is drained: its copy-pool threads (idle between
+// calls, blocked on a condition variable inside this library) are joined, the
+// copy streams destroyed, the caller's page-locked buffers unregistered and
+// the pinned staging freed, so none of it is left to the HIP runtime's own
+// exit-time teardown.  Everything is re-created on demand, should a later
+// exit handler still call in.
+void exit_release_host(klt_hip_ctx *c) {
+  delete c->pool;
+  c->pool = nullptr;
+  for (hipStream_t *st : {&c->cstream, &c->dstream})
+    if (*st) {
+      (void)hipStreamDestroy(*st);
+      *st = nullptr;
+    }
+  for (auto &r : c->registered) (void)hipHostUnregister(const_cast<unsigned char *>(r.first));
+  c->registered.clear();
+  if (c->h_stage) (void)hipHostFree(c->h_stage);
+  if (c->h_rows) (void)hipHostFree(c->h_rows);
+  c->h_stage = nullptr;
+  c->h_rows = nullptr;
+  c->stage_cap = c->hrows_cap = 0;
+}
+
 void exit_hook() {
   g_exiting.store(true, std::memory_order_release);
   std::lock_guard<std::mutex> lk(g_live_m);
   std::set<int> devs;
   for (klt_hip_ctx *c : *g_live) devs.insert(c->device);
-  for (int d : devs)  // a look-ahead refinement's graph may still be in flight
+  for (int d : devs)  // a look-ahead refinement's graph, a copy stream's last DMA may still be in flight
     if (hipSetDevice(d) == hipSuccess) (void)hipDeviceSynchronize();
-  for (klt_hip_ctx *c : *g_live) sel_engine_release_graphs(c->sel);
+  for (klt_hip_ctx *c : *g_live) {
+    sel_engine_release_graphs(c->sel);
+    if (hipSetDevice(c->device) == hipSuccess) exit_release_host(c);
+  }
   sel_pool_shutdown();
 }
 
@@ -2195,6 +2271,12 @@ KLT_API int klt_hip_track_frames_host(klt_hip_ctx *c, const klt_hip_pyr_desc *pd
     if (!frames[f]) return fail(c, "track_frames_host: frame %d is NULL", f);
   if (nframes - (seed_first ? 1 : 0) <= 0) return 0;
   if (use_device(c)) return -1;
+  // KLT_SEQ_TRACE=1: one stderr line per call -- wall time and minor page
+  // faults per stage (SeqStages: host_pipeline_prepare and the feature
+  // staging, waits for a staging slot's previous DMA, copies into staging,
+  // launches, waits for the table rows, handing them out, the final list)
+  SeqStages tr;
+  tr.start(seq_trace());
   const size_t fb = (size_t)pd->ncols * pd->nrows;
   const int F = chunk < nframes ? chunk : nframes;
   const size_t rows_slot = (size_t)3 * F * (n > 0 ? n : 1);  // floats: x | y | val rows of one chunk
@@ -2208,28 +2290,20 @@ KLT_API int klt_hip_track_frames_host(klt_hip_ctx *c, const klt_hip_pyr_desc *pd
     HIPCHK(c, hipEventRecord(c->ev_rows[k], c->stream));
   }
   const int nchunks = (nframes + F - 1) / F;
-  // KLT_SEQ_TRACE=1: one stderr line per call -- host time waiting for the
-  // staging slot's previous DMA, copying frames into staging, waiting for the
-  // table rows and handing them out, and the whole call (tools/seq_variance.py)
-  const bool trace = seq_trace();
-  double tr_dma = 0, tr_copy = 0, tr_rows = 0, tr_deliver = 0;
-  const double tr0 = trace ? wall_us() : 0.0;
+  tr.mark(SeqStages::PRE);
   auto upload = [&](int ci) -> int {
     const int k = ci & 1, f0 = ci * F, nf = F < nframes - f0 ? F : nframes - f0;
     unsigned char *stage = c->h_stage + (size_t)k * F * fb;
-    const double a = trace ? wall_us() : 0.0;
+    tr.mark(SeqStages::LAUNCH);
     HIPCHK(c, hipEventSynchronize(c->ev_dma[k]));  // the slot's previous DMA is done
-    const double b = trace ? wall_us() : 0.0;
+    tr.mark(SeqStages::WAIT_DMA);
     const size_t piece = 512 << 10, per = (fb + piece - 1) / piece;
     if (host_parallel(c, (size_t)nf * per, [&](size_t t) {
           const size_t f = t / per, o = (t - f * per) * piece;
           copy_stream(stage + f * fb + o, frames[f0 + f] + o, fb - o < piece ? fb - o : piece);
         }))
       return -1;
-    if (trace) {
-      tr_dma += b - a;
-      tr_copy += wall_us() - b;
-    }
+    tr.mark(SeqStages::COPY);
     HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_ring_free[k], 0));
     HIPCHK(c, hipMemcpyAsync(c->d_ring + (size_t)k * F * fb, stage, (size_t)nf * fb, hipMemcpyHostToDevice,
                              c->cstream));
@@ -2252,9 +2326,9 @@ KLT_API int klt_hip_track_frames_host(klt_hip_ctx *c, const klt_hip_pyr_desc *pd
     span(ci, t0, nt, skip);
     if (!rows || nt <= 0 || n <= 0) return 0;
     const int k = ci & 1;
-    const double a0 = trace ? wall_us() : 0.0;
+    tr.mark(SeqStages::LAUNCH);
     HIPCHK(c, hipEventSynchronize(c->ev_rows[k]));
-    const double a1 = trace ? wall_us() : 0.0;
+    tr.mark(SeqStages::WAIT_ROWS);
     const float *hx = c->h_rows + k * rows_slot, *hy = hx + (size_t)F * n;
     const int *hv = reinterpret_cast<const int *>(hy + (size_t)F * n);
     const int per = 256;
@@ -2262,10 +2336,7 @@ KLT_API int klt_hip_track_frames_host(klt_hip_ctx *c, const klt_hip_pyr_desc *pd
       const int a = (int)t * per, b = a + per < n ? a + per : n;
       rows(user, t0, nt, a, b, hx, hy, hv, n);
     });
-    if (trace) {
-      tr_rows += a1 - a0;
-      tr_deliver += wall_us() - a1;
-    }
+    tr.mark(SeqStages::DELIVER);
     return rc;
   };
   if (upload(0)) return -1;
@@ -2300,14 +2371,13 @@ KLT_API int klt_hip_track_frames_host(klt_hip_ctx *c, const klt_hip_pyr_desc *pd
     if (ci >= 1 && deliver(ci - 1)) return -1;          // and the rows of chunk ci-1
   }
   if (deliver(nchunks - 1)) return -1;
+  tr.mark(SeqStages::LAUNCH);
   if (n > 0) {
     HIPCHK(c, hipMemcpyAsync(c->h_feat, c->d_feat, 3 * sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
     if (feat_unpack(c, x, y, val, n)) return -1;
   }
-  if (trace)
-    fprintf(stderr, "seqtrace frames=%d chunks=%d total_us=%.0f wait_dma_us=%.0f stage_copy_us=%.0f "
-            "wait_rows_us=%.0f deliver_us=%.0f threads=%d\n", nframes, nchunks, wall_us() - tr0, tr_dma, tr_copy,
-            tr_rows, tr_deliver, c->copy_threads);
+  tr.mark(SeqStages::TAIL);
+  tr.print(nframes, nchunks, c->copy_threads);
   return 0;
 }
 

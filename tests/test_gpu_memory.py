@@ -177,3 +177,55 @@ def test_reset_drains_the_callers_stream(gpu):
         assert s.query(), f"{mode}: the reset returned while the caller's stream still ran the context's work"
         del fr
     assert gpu.klt_amd_release_cached_devices() >= 1
+
+
+SEQ_EXIT_CHILD = r"""
+import ctypes as C, sys, time
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import kltamd
+lib = kltamd.load()
+lib.KLTSetVerbosity(0)
+W, H, NF, n = 1280, 720, 2000, 40
+U8P = C.POINTER(C.c_ubyte)
+fr = []
+for t in range(n):
+    a = np.empty((H, W), np.uint8)
+    lib.klt_synth_frame(720, t, W, H, a.ctypes.data)
+    fr.append(a)
+arr = (U8P * n)(*[a.ctypes.data_as(U8P) for a in fr])
+ft = lib.KLTCreateFeatureTable(n - 1, NF)
+parked = lib.KLTCreateTrackingContext()  # freed below: parked with its copy pool, streams and staging
+tc = lib.KLTCreateTrackingContext()      # never freed: live at exit
+for c in (parked, tc):
+    c.contents.sequentialMode = 1
+    fl = lib.KLTCreateFeatureList(NF)
+    lib.KLTSelectGoodFeatures(c, arr[0], W, H, fl)
+    lib.KLTTrackSequence(c, arr, n, W, H, fl, ft, 0)
+img = np.empty((H, W), np.uint8)  # a registered caller buffer, still registered at exit
+assert lib.klt_amd_register_buffer(tc, img.ctypes.data_as(C.c_void_p), img.nbytes) == 0
+img[:] = fr[-1]
+lib.KLTTrackFeatures(tc, arr[n - 1], img.ctypes.data_as(U8P), W, H, fl)
+lib.KLTFreeTrackingContext(parked)
+print("child done", flush=True)
+"""
+
+
+def test_exit_after_sequence_with_live_context(tmp_path):
+    """a process that ran KLTTrackSequence (copy pool,
+    copy streams, pinned staging) and a registered-buffer KLTTrackFeatures
+    exits with one tracking context live and one parked: rc 0, promptly.  The
+    exit hook (runtime.hip exit_release_host) drains the device and releases
+    the host pipeline of every context before the HIP runtime's teardown."""
+    import subprocess
+    import sys
+    import time
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    script = tmp_path / "seq_exit_child.py"
+    script.write_text(SEQ_EXIT_CHILD)
+    a = time.perf_counter()
+    r = subprocess.run([sys.executable, str(script), str(root)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    assert "child done" in r.stdout
+    assert time.perf_counter() - a < 60

@@ -14,3 +14,4 @@ for round in 1 2 3; do
     tail -1 $OUT/replace_ab.jsonl
   done
 done
+cat /sys/fs/cgroup/cpu.max 2>/dev/null | sed 's/^/cpu.max /'
