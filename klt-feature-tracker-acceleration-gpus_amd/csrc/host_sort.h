@@ -103,6 +103,72 @@ unsigned partition(P *a, unsigned n) {
   return j;
 }
 
+// The reference's recursion on a[0..n) with its own partition step.
+template <class P>
+void sort_hoare(P *a, unsigned n) {
+  while (n > 1) {
+    const unsigned j = partition_hoare(a, n);
+    sort_hoare(a, j);
+    a += j + 1;
+    n -= j + 1;
+  }
+}
+
+// The recursion below 5 elements, by table.  Quicksort only compares keys, so
+// the permutation it applies to n <= 4 elements is a function of the n(n-1)/2
+// pairwise outcomes (<, ==, >) alone.  The tables are built once by running
+// sort_hoare over every key pattern with values below n (every weak order of
+// n elements occurs among them); an n-element subarray then costs its
+// comparisons and one gather instead of up to three branchy partition steps
+// (the recursion's bottom: 2/3 of a map segment's steps are below 16 elements,
+// most of them below 5).  tests/test_host_sort.py checks it exhaustively.
+struct SmallPerm {
+  unsigned char p[5][729][4];  // [n][code][i]: element i of the result is a[p[n][code][i]]
+  static int cmp3(int a, int b) { return (a > b) + (a >= b); }  // 0 <, 1 ==, 2 >
+  template <class K>
+  static int code(const K *k, unsigned n) {
+    int c = 0;
+    for (unsigned i = 0; i < n; ++i)
+      for (unsigned j = i + 1; j < n; ++j) c = 3 * c + cmp3(k[i], k[j]);
+    return c;
+  }
+  SmallPerm() {
+    struct Q {
+      int x, y;
+    };
+    for (unsigned n = 2; n <= 4; ++n) {
+      unsigned total = 1;
+      for (unsigned i = 0; i < n; ++i) total *= n;
+      for (unsigned m = 0; m < total; ++m) {
+        Q q[4];
+        int keys[4];
+        unsigned r = m;
+        for (unsigned i = 0; i < n; ++i, r /= n) {
+          keys[i] = (int)(r % n);
+          q[i] = Q{keys[i], (int)i};
+        }
+        sort_hoare(q, n);
+        const int c = code(keys, n);
+        for (unsigned i = 0; i < n; ++i) p[n][c][i] = (unsigned char)q[i].y;
+      }
+    }
+  }
+  static const SmallPerm &get() {
+    static const SmallPerm t;
+    return t;
+  }
+};
+
+template <class P>
+inline void small_sort(P *a, unsigned n) {  // 2 <= n <= 4: the reference recursion's result
+  int k[4];
+  for (unsigned i = 0; i < n; ++i) k[i] = a[i].x;
+  const unsigned char *perm = SmallPerm::get().p[n][SmallPerm::code(k, n)];
+  P t[4];
+  for (unsigned i = 0; i < n; ++i) t[i] = a[perm[i]];
+  for (unsigned i = 0; i < n; ++i) a[i] = t[i];
+}
+
 // CPUs this process may run on: the affinity mask, capped by a cgroup-v2 CPU
 // quota (cpu.max) when one is set -- std::thread::hardware_concurrency counts
 // every CPU of the machine, which on a shared box is many times its share.
@@ -285,6 +351,10 @@ struct Pool {
   // queues its right part and goes on with the left one.
   void sort_part(Task t) {
     while (t.n > 1) {
+      if (t.n <= 4) {  // the recursion's bottom, by table
+        small_sort(t.a, t.n);
+        return;
+      }
       const unsigned j = partition(t.a, t.n);
       P *lo = t.a, *hi = t.a + j + 1;
       const unsigned nlo = j, nhi = t.n - j - 1;

@@ -956,9 +956,38 @@ int ensure_banks(klt_hip_ctx *c, const klt_hip_pyr_desc *d, int frames) {
 // row_lo/row_hi: the level-0 rows to build (the sigma-3.6 rows pass hs over
 // all of them); plane_lo/plane_hi: the rows whose level-0 planes are stored
 // (a band's outer margin feeds only level 1)
+// KLT_PYR_SUB=S (experiment): build a batch as sub-batches
+// of S frames, each level 0 followed by its level 1, so that level 1 reads the
+// sigma-3.6 row pass (hs) while it may still be in the MALL; 0 = whole batches
+int pyr_sub_batch() {
+  static const int s = [] {
+    const char *e = getenv("KLT_PYR_SUB");
+    return e && *e ? atoi(e) : 0;
+  }();
+  return s;
+}
+
+int build_fused_bank_range(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
+                           long stride, int F, hipStream_t st, int row_lo, int row_hi, int plane_lo, int plane_hi,
+                           int il, int f0);
+
 int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
                      long stride, int F, hipStream_t st, int row_lo = 0, int row_hi = 1 << 30, int plane_lo = 0,
                      int plane_hi = 1 << 30, int il = 1) {
+  const int S = pyr_sub_batch();
+  if (S <= 0 || S >= F)
+    return build_fused_bank_range(c, K, d, src, pitch, stride, F, st, row_lo, row_hi, plane_lo, plane_hi, il, 0);
+  for (int f0 = 0; f0 < F; f0 += S)
+    if (build_fused_bank_range(c, K, d, src + (long)f0 * stride, pitch, stride, F - f0 < S ? F - f0 : S, st, row_lo,
+                               row_hi, plane_lo, plane_hi, il, f0))
+      return -1;
+  return 0;
+}
+
+// frames f0 .. f0+F-1 of bank K (src: frame f0)
+int build_fused_bank_range(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const uint8_t *src, long pitch,
+                           long stride, int F, hipStream_t st, int row_lo, int row_hi, int plane_lo, int plane_hi,
+                           int il, int f0) {
   const int W = d->ncols, H = d->nrows;
   const DefTaps T = default_taps(d);
   const bool two = d->nlevels == 2;
@@ -974,10 +1003,13 @@ int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const u
   // img / gx / gy + f w h), for a batch that a planes-reading tracker takes
   const int np = il ? 3 : 1;
   for (int l = 0; l < d->nlevels; ++l) K.lv[l].il = il;
+  auto at = [](float *p, long off) { return p ? p + off : p; };
+  const long o0 = (long)f0 * np * fs0, oh = (long)f0 * fsh, o1 = (long)f0 * np * fs1;
   {
     TimedScope ts(c, T_L0, st, F);
-    if (launch_l0(c, st, src, pitch, stride, W, H, T, vec_u8, vec_out, K.lv[0].img, K.lv[0].gx, K.lv[0].gy, K.hs,
-                  W1, (two && W1 > 0) ? 1 : 0, np * fs0, fsh, F, r0, r1, &p0, &p1, il))
+    if (launch_l0(c, st, src, pitch, stride, W, H, T, vec_u8, vec_out, at(K.lv[0].img, o0), at(K.lv[0].gx, o0),
+                  at(K.lv[0].gy, o0), at(K.hs, oh), W1, (two && W1 > 0) ? 1 : 0, np * fs0, fsh, F, r0, r1, &p0, &p1,
+                  il))
       return -1;
   }
   K.vlo[0] = p0;
@@ -999,8 +1031,9 @@ int build_fused_bank(klt_hip_ctx *c, Bank &K, const klt_hip_pyr_desc *d, const u
       HMARK_IN("l0_launched");
       TimedScope ts(c, T_L1, st, F);
       const int vec = (W1 % 4 == 0 && W1 >= 8) ? 1 : 0;
-      if (launched(c, "k_pyr_l1", launch_pyr_l1(st, K.hs, W1, H, H1, T, vec, K.lv[1].img, K.lv[1].gx, K.lv[1].gy,
-                                                fsh, np * fs1, F, t1lo, t1hi, il)))
+      if (launched(c, "k_pyr_l1", launch_pyr_l1(st, at(K.hs, oh), W1, H, H1, T, vec, at(K.lv[1].img, o1),
+                                                at(K.lv[1].gx, o1), at(K.lv[1].gy, o1), fsh, np * fs1, F, t1lo, t1hi,
+                                                il)))
         return -1;
       HMARK_IN("l1_launched");
     }
@@ -1055,9 +1088,13 @@ void exit_hook() {
   for (klt_hip_ctx *c : *g_live) devs.insert(c->device);
   for (int d : devs)  // a look-ahead refinement's graph, a copy stream's last DMA may still be in flight
     if (hipSetDevice(d) == hipSuccess) (void)hipDeviceSynchronize();
+  static const bool release_host = [] {  // KLT_EXIT_RELEASE=0 (A/B): the round-5 hook
+    const char *e = getenv("KLT_EXIT_RELEASE");
+    return !(e && *e == '0');
+  }();
   for (klt_hip_ctx *c : *g_live) {
     sel_engine_release_graphs(c->sel);
-    if (hipSetDevice(c->device) == hipSuccess) exit_release_host(c);
+    if (release_host && hipSetDevice(c->device) == hipSuccess) exit_release_host(c);
   }
   sel_pool_shutdown();
 }

@@ -65,6 +65,23 @@ int main() {
         for (unsigned i = 0; same && i < n; ++i) same = a[i].x == b[i].x && a[i].y == b[i].y;
         if (!same) { ++bad; std::printf("partition mismatch kind %d n %u seed %u\n", kind, n, seed); }
       }
+  // the table bottom (small_sort, n <= 4) inside the recursion: every array of
+  // n <= 7 elements with keys below n, sorted whole, equals the reference's
+  for (unsigned n = 1; n <= 7; ++n) {
+    unsigned total = 1;
+    for (unsigned i = 0; i < n; ++i) total *= n;
+    for (unsigned m = 0; m < total; ++m) {
+      std::vector<P> a(n), b;
+      unsigned r = m;
+      for (unsigned i = 0; i < n; ++i, r /= n) a[i] = P{(int)(r % n), (int)i};
+      b = a;
+      pool.sort(a.data(), n, 0, 2);
+      ref_sort(b.data(), n);
+      ++cases;
+      for (unsigned i = 0; i < n; ++i)
+        if (a[i].x != b[i].x || a[i].y != b[i].y) { ++bad; std::printf("small mismatch n %u m %u\n", n, m); break; }
+    }
+  }
   for (int kind = 0; kind < 4; ++kind)
     for (unsigned n : {1000u, 40000u, 100003u}) {
       std::vector<P> a = make(kind, n, n + kind), b = a;
