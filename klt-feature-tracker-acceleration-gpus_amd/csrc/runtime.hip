@@ -263,6 +263,12 @@ struct klt_hip_ctx {
   PrevRef prev;
   bool frames_ready = false;
   hipEvent_t ev_bbuilt[3] = {}, ev_bfree[3] = {};
+  // KLT_WAIT_VALUE=1 (experiment): a built-ahead bank is announced by a
+  // stream write of a sequence number into signal memory on the pyramid
+  // stream, and the tracking stream waits for that value instead of for
+  // ev_bbuilt (hipStreamWaitValue32)
+  unsigned *d_sig = nullptr;
+  unsigned sig_seq[3] = {};
   bool timing = false;
   long frames_timed[T_N] = {};
   std::vector<hipEvent_t> ev_pool;
@@ -959,6 +965,14 @@ int ensure_banks(klt_hip_ctx *c, const klt_hip_pyr_desc *d, int frames) {
 // KLT_PYR_SUB=S (experiment): build a batch as sub-batches
 // of S frames, each level 0 followed by its level 1, so that level 1 reads the
 // sigma-3.6 row pass (hs) while it may still be in the MALL; 0 = whole batches
+bool wait_value_mode() {
+  static const bool on = [] {
+    const char *e = getenv("KLT_WAIT_VALUE");
+    return e && *e == '1';
+  }();
+  return on;
+}
+
 int pyr_sub_batch() {
   static const int s = [] {
     const char *e = getenv("KLT_PYR_SUB");
@@ -1227,6 +1241,7 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
   if (c->ev_start) hipEventDestroy(c->ev_start);
   if (c->ev_caller) hipEventDestroy(c->ev_caller);
   if (c->ev_go) hipEventDestroy(c->ev_go);
+  hipFree(c->d_sig);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
 }
@@ -2178,8 +2193,12 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     }
     HMARK("pyramids");
     if (!serial) {
-      if (!prebuilt) HIPCHK(c, hipEventRecord(c->ev_bbuilt[bi], ps));
-      HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_bbuilt[bi], 0));
+      if (prebuilt && c->d_sig && wait_value_mode()) {
+        HIPCHK(c, hipStreamWaitValue32(c->stream, c->d_sig + bi, c->sig_seq[bi], hipStreamWaitValueGte, 0xFFFFFFFFu));
+      } else {
+        if (!prebuilt) HIPCHK(c, hipEventRecord(c->ev_bbuilt[bi], ps));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_bbuilt[bi], 0));
+      }
     }
     for (int l = 0; l < pd->nlevels; ++l) {
       a.A[l] = prev_level(c, l);
@@ -2218,7 +2237,14 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     if (build_fused_bank(c, c->bank[bj], pd, band->next, pitch, stride, Fn, c->pstream, band->row_lo, band->row_hi,
                          p0, p1, bil))
       return -1;
-    HIPCHK(c, hipEventRecord(c->ev_bbuilt[bj], c->pstream));
+    if (wait_value_mode() && !c->d_sig) {
+      HIPCHK(c, hipExtMallocWithFlags((void **)&c->d_sig, 4 * sizeof(unsigned long long), hipMallocSignalMemory));
+      HIPCHK(c, hipMemsetAsync(c->d_sig, 0, 4 * sizeof(unsigned long long), c->pstream));
+    }
+    if (c->d_sig && wait_value_mode())
+      HIPCHK(c, hipStreamWriteValue32(c->pstream, c->d_sig + bj, ++c->sig_seq[bj], 0));
+    else
+      HIPCHK(c, hipEventRecord(c->ev_bbuilt[bj], c->pstream));
     c->pre.bank = bj;
     c->pre.src = band->next;
     c->pre.F = Fn;
