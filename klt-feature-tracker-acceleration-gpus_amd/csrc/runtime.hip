@@ -267,7 +267,7 @@ struct klt_hip_ctx {
   // stream write of a sequence number into signal memory on the pyramid
   // stream, and the tracking stream waits for that value instead of for
   // ev_bbuilt (hipStreamWaitValue32)
-  unsigned *d_sig = nullptr;
+  unsigned *d_sig[3] = {};  // one 8-byte signal allocation per bank (hipMallocSignalMemory takes 8 bytes)
   unsigned sig_seq[3] = {};
   bool timing = false;
   long frames_timed[T_N] = {};
@@ -1241,7 +1241,7 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
   if (c->ev_start) hipEventDestroy(c->ev_start);
   if (c->ev_caller) hipEventDestroy(c->ev_caller);
   if (c->ev_go) hipEventDestroy(c->ev_go);
-  hipFree(c->d_sig);
+  for (unsigned *p : c->d_sig) hipFree(p);
   if (c->own) hipStreamDestroy(c->own);
   delete c;
 }
@@ -2193,8 +2193,8 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     }
     HMARK("pyramids");
     if (!serial) {
-      if (prebuilt && c->d_sig && wait_value_mode()) {
-        HIPCHK(c, hipStreamWaitValue32(c->stream, c->d_sig + bi, c->sig_seq[bi], hipStreamWaitValueGte, 0xFFFFFFFFu));
+      if (prebuilt && c->d_sig[bi] && wait_value_mode()) {
+        HIPCHK(c, hipStreamWaitValue32(c->stream, c->d_sig[bi], c->sig_seq[bi], hipStreamWaitValueGte, 0xFFFFFFFFu));
       } else {
         if (!prebuilt) HIPCHK(c, hipEventRecord(c->ev_bbuilt[bi], ps));
         HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_bbuilt[bi], 0));
@@ -2237,12 +2237,12 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
     if (build_fused_bank(c, c->bank[bj], pd, band->next, pitch, stride, Fn, c->pstream, band->row_lo, band->row_hi,
                          p0, p1, bil))
       return -1;
-    if (wait_value_mode() && !c->d_sig) {
-      HIPCHK(c, hipExtMallocWithFlags((void **)&c->d_sig, 4 * sizeof(unsigned long long), hipMallocSignalMemory));
-      HIPCHK(c, hipMemsetAsync(c->d_sig, 0, 4 * sizeof(unsigned long long), c->pstream));
+    if (wait_value_mode() && !c->d_sig[bj]) {
+      HIPCHK(c, hipExtMallocWithFlags((void **)&c->d_sig[bj], sizeof(unsigned long long), hipMallocSignalMemory));
+      HIPCHK(c, hipMemsetAsync(c->d_sig[bj], 0, sizeof(unsigned long long), c->pstream));
     }
-    if (c->d_sig && wait_value_mode())
-      HIPCHK(c, hipStreamWriteValue32(c->pstream, c->d_sig + bj, ++c->sig_seq[bj], 0));
+    if (c->d_sig[bj] && wait_value_mode())
+      HIPCHK(c, hipStreamWriteValue32(c->pstream, c->d_sig[bj], ++c->sig_seq[bj], 0));
     else
       HIPCHK(c, hipEventRecord(c->ev_bbuilt[bj], c->pstream));
     c->pre.bank = bj;

@@ -11,6 +11,8 @@ modes:
                klt_hip_* upload path (KLTTrackFeatures per call, registered buffers)
   seq_live     3 KLTTrackSequence calls, exit with the tracking context live
   seq_freed    the same, contexts freed and the parked device contexts released
+  torch_d2h    one pageable device->host copy by torch (tensor.cpu(), 400 MB)
+  torch_d2h_seq  that copy, then seq_live (tools/seq_variance.py's shape)
 usage: python tools/exp/r06_copytrace_probe.py MODE"""
 import ctypes as C
 import sys
@@ -24,7 +26,16 @@ sys.path.insert(0, str(ROOT))
 
 mode = sys.argv[1]
 t0 = time.perf_counter()
-if mode == "torch":
+if mode.startswith("torch_d2h"):
+    import torch
+    fr = torch.zeros((201, 1080, 1920), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    h = fr.cpu().numpy()
+    del fr
+    mode = "seq_live" if mode == "torch_d2h_seq" else "done"
+if mode == "done":
+    pass
+elif mode == "torch":
     import torch
     src = torch.empty(2 << 20, dtype=torch.uint8).pin_memory()
     dst = torch.empty(2 << 20, dtype=torch.uint8, device="cuda")

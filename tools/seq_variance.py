@@ -39,14 +39,13 @@ def main():
     W, H, NF, n = 1920, 1080, 5000, a.frames
     U8P = C.POINTER(C.c_ubyte)
     dev = torch.device("cuda", 0)
-    fr = torch.empty((n, H, W), dtype=torch.uint8, device=dev)
-    tc = lib.KLTCreateTrackingContext()
-    ctx = lib.klt_amd_device_context(tc)
-    lib.klt_hip_synth_frames(ctx, 1080, 0, n, W, H, C.c_void_p(fr.data_ptr()), W, W * H)
-    torch.cuda.synchronize()
-    host = fr.cpu().numpy()
-    lib.KLTFreeTrackingContext(tc)
-    del fr
+    # the frames synthesised on the host (include/klt_synth.h, the same bytes
+    # k_synth writes): no pageable device->host copy by torch, which under
+    # rocprofv3 --memory-copy-trace leaves every later device->host copy's
+    # completion undelivered (tools/exp/r06_copytrace_probe.py)
+    host = np.empty((n, H, W), np.uint8)
+    for t in range(n):
+        lib.klt_synth_frame(1080, t, W, H, host[t].ctypes.data)
     arr = (U8P * n)(*[host[t].ctypes.data_as(U8P) for t in range(n)])
     ft = lib.KLTCreateFeatureTable(n - 1, NF)
     src = np.ones(400 << 20, np.uint8)
