@@ -136,7 +136,10 @@ def main() -> None:
     gpu_index = 0 if share else local
     torch.cuda.set_device(gpu_index)
     dev = torch.device("cuda", gpu_index)
-    if world > 1:
+    # a process group whenever torch.distributed.run launched us (RANK set),
+    # also at N = 1: `torchrun --nproc-per-node 1 bench.py` then runs the
+    # sharded_4k leg's all-gather through RCCL on one GPU
+    if world > 1 or "RANK" in os.environ:
         if share:
             dist.init_process_group("gloo")
         else:
@@ -463,7 +466,7 @@ def main() -> None:
             result["sharded_4k"] = sh
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
@@ -471,7 +474,7 @@ def gather_floats(vals, world, dev):
     """Every rank's list of floats (the same length on every rank), in rank order."""
     import torch
     import torch.distributed as dist
-    if world == 1:
+    if not dist.is_initialized():
         return [list(vals)]
     t = torch.tensor(vals, dtype=torch.float64)
     if dist.get_backend() == "nccl":
@@ -554,7 +557,7 @@ def sharded_core(world, rank, dev, W, H, NF, seed, warmup, steps, chunk, margin,
         if timing[0]:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        if world == 1:
+        if not dist.is_initialized():
             out.copy_(inp)
         elif dist.get_backend() == "gloo":  # the shared-GPU rehearsal (KLT_BENCH_SHARE_GPU=1)
             parts = [torch.empty_like(inp) for _ in range(world)]
@@ -622,7 +625,7 @@ def sharded_core(world, rank, dev, W, H, NF, seed, warmup, steps, chunk, margin,
                "allgather_calls_per_rank": len(ag),
                "chunk_us_median_by_rank": [s[3] for s in all_stats],
                "replay_us_per_frame_by_rank": [s[4] / steps for s in all_stats],
-               "allgather_op": ("copy (world 1)" if world == 1 else
+               "allgather_op": ("copy (world 1, no process group)" if not dist.is_initialized() else
                                 "torch.distributed.all_gather_into_tensor (" + dist.get_backend() + ")"),
                "what": "a replay of the timed frames from the same state with HIP events on the tracking stream "
                        "around each all-gather (the collective as the chunk's stream sees it, wait included) and "
@@ -718,7 +721,7 @@ def run_sharded(args, world, rank, dev) -> None:
     }
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

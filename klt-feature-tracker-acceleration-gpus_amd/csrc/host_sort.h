@@ -380,15 +380,43 @@ struct Pool {
     std::atomic<int> pending{1};
     if (nthreads.load(std::memory_order_acquire) == 0) par = 0;  // no workers (shut down, one CPU): sequential
     const bool spin = par > 0 && n >= 2 * par_min;  // tasks will be queued: keep the workers awake meanwhile
-    if (spin) {
-      hot.fetch_add(1, std::memory_order_release);
-      {
-        std::lock_guard<std::mutex> lk(m);
-        gen.fetch_add(1, std::memory_order_relaxed);
-      }
-      cv.notify_all();
-    }
+    if (spin) wake();
     run(Task{a, n, par, par_min, &pending});
+    wait_for(pending, spin);
+  }
+
+  // Asynchronous sorts (select.hip's lazy walk hands the right part of each
+  // split to the pool and walks the left part meanwhile): start() queues the
+  // whole sort of a[0..n) as one task counted in *pending (0 once every task
+  // of that sort is done; a worker splits it further as sort() would) and
+  // returns whether the workers were woken for it; finish() waits for it,
+  // helping with its queued tasks, and ends the spin start() began.  With no
+  // workers the sort runs inside start().
+  bool start(P *a, unsigned n, int par, unsigned par_min, std::atomic<int> *pending) {
+    pending->store(0, std::memory_order_relaxed);
+    if (nthreads.load(std::memory_order_acquire) == 0) {
+      pending->store(1, std::memory_order_relaxed);
+      run(Task{a, n, 0, par_min, pending});
+      return false;
+    }
+    wake();
+    submit(Task{a, n, par, par_min, pending});
+    return true;
+  }
+  void finish(std::atomic<int> &pending, bool started) { wait_for(pending, started); }
+
+ private:
+  void wake() {  // a sort with queued tasks begins: the workers spin until it ends
+    hot.fetch_add(1, std::memory_order_release);
+    {
+      std::lock_guard<std::mutex> lk(m);
+      gen.fetch_add(1, std::memory_order_relaxed);
+    }
+    cv.notify_all();
+  }
+  // until pending is 0: help with the sort's own queued tasks, else wait for
+  // its last one; spin: the sort woke the workers (wake), end that here
+  void wait_for(std::atomic<int> &pending, bool spin) {
     std::unique_lock<std::mutex> lk(m);
     for (;;) {
       if (pending.load(std::memory_order_acquire) == 0) break;

@@ -41,6 +41,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <deque>
 #include <string>
 #include <thread>
 #include <vector>
@@ -393,7 +394,14 @@ struct Seg {
   int start, len;
   bool host;
   bool sorted = false;  // host segment already in its final order
+  int task = -1;        // host segment being sorted on the pool (LazySort::parts), waited for when reached
 };
+
+// a reached host segment longer than this is not sorted whole before the walk
+// goes on: one exact partition step splits it, its right part is sorted on the
+// pool in the background and the left part is treated the same way, so the
+// walk starts on the leftmost piece while the rest is sorted beside it
+constexpr int kSelSpineMin = 4096;
 
 // levels of two-way task splits in the host sort (2^depth tasks on the pool);
 // KLT_AMD_SORT_DEPTH (0..5) overrides the default for A/B runs, read once
@@ -550,11 +558,20 @@ struct LazySort {
   bool ahead = false;
   int ahead_start = -1;
   double ahead_t0 = 0.0;
+  // background sorts of right parts split off a reached host segment
+  struct Part {
+    std::atomic<int> pending{0};
+    bool started = false, open = false;
+  };
+  std::deque<Part> parts;  // stable addresses: the pool holds &pending
 
   // a walk that stops early may leave a look-ahead refinement in flight: its
-  // state copy into pinned memory must land before the engine is used again
+  // state copy into pinned memory must land before the engine is used again;
+  // and background sorts of segments it never reached still run on h_kv
   ~LazySort() {
     if (ahead) (void)hipEventSynchronize(e->ev_ref);
+    for (Part &pt : parts)
+      if (pt.open) kltsort::Pool<int2>::get(0).finish(pt.pending, pt.started);
   }
 
   long next() {
@@ -616,14 +633,46 @@ struct LazySort {
         g.host = true;
       }
       if (g.len == 1) return g.start;
+      if (g.task >= 0) {  // its background sort began when the segment holding it was split
+        const double t0 = now_us();
+        Part &pt = parts[(size_t)g.task];
+        kltsort::Pool<int2>::get(0).finish(pt.pending, pt.started);
+        pt.open = false;
+        e->us[2] += now_us() - t0;
+        if (sel_trace()) fprintf(stderr, "seltrace wait len=%d us=%.1f\n", g.len, now_us() - t0);
+        g.task = -1;
+        g.sorted = true;
+      }
       if (!g.sorted) {
         // a segment the walk has reached is consumed almost whole: sort it
-        // outright (in parallel) and hand its positions out in order
+        // (in parallel) and hand its positions out in order.  A long one is
+        // split first (kSelSpineMin): the same exact partition step the
+        // recursion takes, the right part's sort queued on the pool, the left
+        // part next -- the parts are disjoint, so the order is the recursion's
         const double t0 = now_us();
         const int depth = sort_depth();
         // 2^depth tasks: up to 2^depth - 1 workers beside the caller (Pool::grow
         // caps them at the process's usable CPUs)
-        kltsort::Pool<int2>::get((1 << depth) - 1).sort(e->h_kv + g.start, (unsigned)g.len, depth, kSelParMin);
+        auto &pool = kltsort::Pool<int2>::get((1 << depth) - 1);
+        if (depth > 0 && g.len > kSelSpineMin) {
+          const int j = (int)kltsort::partition(e->h_kv + g.start, (unsigned)g.len);
+          Seg R{g.start + j + 1, g.len - j - 1, true, true};
+          if (R.len > 1) {
+            parts.emplace_back();
+            Part &pt = parts.back();
+            pt.open = true;
+            pt.started = pool.start(e->h_kv + R.start, (unsigned)R.len, depth, kSelParMin, &pt.pending);
+            R.sorted = false;
+            R.task = (int)parts.size() - 1;
+          }
+          stk.push_back(R);
+          stk.push_back(Seg{g.start + j, 1, true, true});  // the pivot, in its final place
+          stk.push_back(Seg{g.start, j, true, false});     // the left part: reached next
+          e->us[2] += now_us() - t0;
+          if (sel_trace()) fprintf(stderr, "seltrace split len=%d left=%d us=%.1f\n", g.len, j, now_us() - t0);
+          continue;
+        }
+        pool.sort(e->h_kv + g.start, (unsigned)g.len, depth, kSelParMin);
         e->us[2] += now_us() - t0;
         if (sel_trace()) fprintf(stderr, "seltrace sort len=%d us=%.1f\n", g.len, now_us() - t0);
         g.sorted = true;

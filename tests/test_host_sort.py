@@ -25,6 +25,7 @@ CSRC = ROOT / "klt-feature-tracker-acceleration-gpus_amd" / "csrc"
 DRIVER = r"""
 #include <cstdio>
 #include <cstdlib>
+#include <deque>
 #include <random>
 #include <thread>
 #include <vector>
@@ -104,6 +105,32 @@ int main() {
         for (unsigned i = 1; i < n; ++i)
           if (a[i - 1].x < a[i].x) { ++bad; std::printf("unsorted kind %d n %u\n", kind, n); break; }
       }
+  // the selection walk's spine (select.hip LazySort): split, the right part
+  // sorted asynchronously (Pool::start / finish), the left part split again,
+  // parts finished in walk order or never reached (finished at the end)
+  for (int kind = 0; kind < 4; ++kind)
+    for (unsigned n : {5000u, 40000u, 100003u}) {
+      std::vector<P> a = make(kind, n, n * 7 + kind), b = a;
+      ref_sort(b.data(), n);
+      std::deque<std::atomic<int>> pend;
+      std::vector<std::pair<unsigned, unsigned>> spans;  // right parts, in walk order (reversed below)
+      std::vector<bool> started;
+      unsigned lo = 0, len = n;
+      while (len > 3000) {
+        const unsigned j = kltsort::partition(a.data() + lo, len);
+        if (len - j - 1 > 1) {
+          pend.emplace_back();
+          started.push_back(pool.start(a.data() + lo + j + 1, len - j - 1, 3, 256, &pend.back()));
+          spans.push_back({lo + j + 1, len - j - 1});
+        }
+        len = j;
+      }
+      pool.sort(a.data() + lo, len, 2, 256);
+      for (size_t k = pend.size(); k-- > 0;) pool.finish(pend[k], started[k]);  // nearest part first
+      ++cases;
+      for (unsigned i = 0; i < n; ++i)
+        if (a[i].x != b[i].x || a[i].y != b[i].y) { ++bad; std::printf("spine mismatch kind %d n %u at %u\n", kind, n, i); break; }
+    }
   // four callers at once on the shared pool
   std::vector<std::vector<P>> seq(4), par(4);
   for (int c = 0; c < 4; ++c) {

@@ -13,6 +13,7 @@ modes:
   seq_freed    the same, contexts freed and the parked device contexts released
   torch_d2h    one pageable device->host copy by torch (tensor.cpu(), 400 MB)
   torch_d2h_seq  that copy, then seq_live (tools/seq_variance.py's shape)
+  torch_init_seq the device initialised by torch (one tensor, no copy), then seq_live
 usage: python tools/exp/r06_copytrace_probe.py MODE"""
 import ctypes as C
 import sys
@@ -26,6 +27,11 @@ sys.path.insert(0, str(ROOT))
 
 mode = sys.argv[1]
 t0 = time.perf_counter()
+if mode == "torch_init_seq":
+    import torch
+    z = torch.zeros(16, device="cuda")
+    torch.cuda.synchronize()
+    mode = "seq_live"
 if mode.startswith("torch_d2h"):
     import torch
     fr = torch.zeros((201, 1080, 1920), dtype=torch.uint8, device="cuda")

@@ -11,13 +11,18 @@ FAST="--steps 20 --warmup 5 --no-cpu --no-4k --no-fast --api-frames 0 --replace-
 a=$(date +%s)
 timeout -k 10 300 python3 bench.py $FAST > $OUT/n1.json 2> $OUT/n1.err || { tail -20 $OUT/n1.err; exit 1; }
 echo "n1 wall_s=$(( $(date +%s) - a ))"
+# one rank through torch.distributed.run: the sharded_4k all-gather runs through RCCL
+a=$(date +%s)
+timeout -k 10 300 $R --nproc-per-node 1 --master-port 29540 bench.py --gpus 1 $FAST > $OUT/n1rccl.json 2> $OUT/n1rccl.err \
+  || { tail -20 $OUT/n1rccl.err; exit 1; }
+echo "n1rccl wall_s=$(( $(date +%s) - a ))"
 for n in 2 4; do
   a=$(date +%s)
   KLT_BENCH_SHARE_GPU=1 timeout -k 10 600 $R --nproc-per-node $n --master-port 2954$n bench.py --gpus $n $FAST \
     > $OUT/n$n.json 2> $OUT/n$n.err || { tail -20 $OUT/n$n.err; exit 1; }
   echo "n$n wall_s=$(( $(date +%s) - a ))"
 done
-for n in 1 2 4; do
+for n in 1 1rccl 2 4; do
 python3 - $OUT/n$n.json <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])

@@ -32,17 +32,16 @@ def main():
     ap.add_argument("--frames", type=int, default=201)
     a = ap.parse_args()
     os.environ["KLT_SEQ_TRACE"] = "1"
-    import torch
+    # no torch in this process: after a device->host copy in a process whose
+    # device torch initialised, rocprofv3 --memory-copy-trace never receives
+    # another device->host completion (tools/exp/r06_copytrace_probe.py,
+    # DESIGN.md section 5), and this tool is meant to run under that trace
     import kltamd
     lib = kltamd.load()
     lib.KLTSetVerbosity(0)
     W, H, NF, n = 1920, 1080, 5000, a.frames
     U8P = C.POINTER(C.c_ubyte)
-    dev = torch.device("cuda", 0)
-    # the frames synthesised on the host (include/klt_synth.h, the same bytes
-    # k_synth writes): no pageable device->host copy by torch, which under
-    # rocprofv3 --memory-copy-trace leaves every later device->host copy's
-    # completion undelivered (tools/exp/r06_copytrace_probe.py)
+    # the frames synthesised on the host (include/klt_synth.h, the bytes k_synth writes)
     host = np.empty((n, H, W), np.uint8)
     for t in range(n):
         lib.klt_synth_frame(1080, t, W, H, host[t].ctypes.data)
@@ -50,18 +49,21 @@ def main():
     ft = lib.KLTCreateFeatureTable(n - 1, NF)
     src = np.ones(400 << 20, np.uint8)
     dst = np.empty_like(src)
-    pin = torch.empty(256 << 20, dtype=torch.uint8).pin_memory()
-    gdst = torch.empty(256 << 20, dtype=torch.uint8, device=dev)
+    # the bus probe: a 256 MiB page-locked host buffer -> device copy through
+    # the library's own context (klt_hip_register_host + klt_hip_memcpy)
+    ptc = lib.KLTCreateTrackingContext()
+    pctx = lib.klt_amd_device_context(ptc)
+    pin = np.ones(256 << 20, np.uint8)
+    assert lib.klt_hip_register_host(pctx, pin.ctypes.data, pin.nbytes) == 0
+    gdst = lib.klt_hip_malloc(pctx, pin.nbytes)
     rows = []
     for k in range(a.calls):
         t0 = time.perf_counter()
         np.copyto(dst, src)
         memcpy_gbs = src.nbytes / (time.perf_counter() - t0) / 1e9
-        torch.cuda.synchronize()
         t0 = time.perf_counter()
-        gdst.copy_(pin, non_blocking=True)
-        torch.cuda.synchronize()
-        h2d_gbs = pin.numel() / (time.perf_counter() - t0) / 1e9
+        assert lib.klt_hip_memcpy(pctx, gdst, pin.ctypes.data, pin.nbytes, 1) == 0
+        h2d_gbs = pin.nbytes / (time.perf_counter() - t0) / 1e9
         tc = lib.KLTCreateTrackingContext()
         tc.contents.sequentialMode = 1
         fl = lib.KLTCreateFeatureList(NF)
@@ -77,6 +79,8 @@ def main():
         rows.append(row)
         print(json.dumps(row), flush=True)
     lib.KLTFreeFeatureTable(ft)
+    lib.klt_hip_free(pctx, gdst)
+    lib.KLTFreeTrackingContext(ptc)
     Path(a.out, "seq_variance.json").write_text(json.dumps(rows, indent=1) + "\n")
 
 
