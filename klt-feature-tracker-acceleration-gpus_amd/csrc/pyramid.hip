@@ -48,6 +48,18 @@ __device__ __forceinline__ void st4_out(float *p, f4 v) { __builtin_nontemporal_
 __device__ __forceinline__ void st2_out(float *p, f2 v) { __builtin_nontemporal_store(v, reinterpret_cast<f2 *>(p)); }
 typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
 __device__ __forceinline__ void st3_out(float *p, f3u v) { __builtin_nontemporal_store(v, reinterpret_cast<f3u *>(p)); }
+// experiment builds (make variant DEFS=...): the sigma-3.6 row pass (hs) and
+// level 1's interleaved records stored nontemporally as well
+#ifdef KLT_HS_NT
+#define HS_ST4 st4_out
+#else
+#define HS_ST4 st4
+#endif
+#ifdef KLT_L1_NT
+#define L1_ST4 st4_out
+#else
+#define L1_ST4 st4
+#endif
 
 // acc[i] += v[i + off] * k for 4 lanes, as two packed-f32 pairs
 __device__ __forceinline__ void mac4(f4 &acc, const float *v, float k) {
@@ -412,7 +424,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
     const int y = R0 + r;
     const int X = C0 / SS + 4 * q;
     if (INT) {
-      *reinterpret_cast<f4 *>(hs + hs_at32(y, X, H)) = f4{a01.x, a01.y, a23.x, a23.y};
+      HS_ST4(hs + hs_at32(y, X, H), f4{a01.x, a01.y, a23.x, a23.y});
     } else if (y < H) {
       float o[4] = {a01.x, a01.y, a23.x, a23.y};
       if (!cols_in) {
@@ -423,7 +435,7 @@ __device__ __forceinline__ void pyr_l0_tile(float *__restrict__ lds, const uint8
         }
       }
       if (X + 3 < hsW) {  // X % 4 == 0: four columns of one slab
-        *reinterpret_cast<f4 *>(hs + hs_at32(y, X, H)) = f4{o[0], o[1], o[2], o[3]};
+        HS_ST4(hs + hs_at32(y, X, H), f4{o[0], o[1], o[2], o[3]});
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
@@ -762,7 +774,7 @@ __global__ __launch_bounds__(256) void k_pyr_l1(const float *__restrict__ hs, in
     if (vec && nx == TW) {
       for (int i = tid; i < TH * (3 * TW / 4); i += NT) {
         const int r = i / (3 * TW / 4), q = i - r * (3 * TW / 4);
-        if (y0 + r < H1) st4(base + 3u * (unsigned)((y0 + r) * W1) + 4 * q, ld4(stg + r * (3 * TW) + 4 * q));
+        if (y0 + r < H1) L1_ST4(base + 3u * (unsigned)((y0 + r) * W1) + 4 * q, ld4(stg + r * (3 * TW) + 4 * q));
       }
     } else {
       for (int i = tid; i < TH * 3 * TW; i += NT) {
