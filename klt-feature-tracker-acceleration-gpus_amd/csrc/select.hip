@@ -131,35 +131,30 @@ __global__ __launch_bounds__(kSelThreads) void k_sel_paint(const float *__restri
   if (px >= 0 && px < W && py >= 0 && py < H) map[(size_t)py * W + px] = 1;
 }
 
-// step 0: pivot a[n/2] to the front (or stop: the segment is small enough)
-__device__ __forceinline__ void sel_pivot(SelState *s, int2 *kv, int threshold) {
-  if (s->done) return;
-  if (s->len <= threshold) {
-    s->done = 1;
-    return;
-  }
-  const int st = s->start;
-  swap2(kv, st, st + s->len / 2);
-  s->pv = kv[st].x;
-  s->m = 0;
-}
+// A partition step is four launches (count, scan, rank, swap).  The
+// reference's step first swaps a[n/2] to the front (its pivot) and then scans
+// positions 1 .. n-1; round 6 folded that swap, once a one-thread launch of
+// its own, into the next two: the count reads the array as if it were done
+// (position n/2 holds the old a[0]) and the scan, one block between the count
+// and the rank, does it.  The same counts, the same step.
 
-__global__ void k_sel_pivot(SelState *s, int2 *kv, int threshold) { sel_pivot(s, kv, threshold); }
-
-// step 1: left / right stop counts per block (positions 1 .. len-1)
+// step 1: left / right stop counts per block (positions 1 .. len-1, after
+// the pivot swap a[0] <-> a[len/2] that step 2 performs); nothing once the
+// segment is at most `threshold` long (step 2 then marks the state done)
 __device__ __forceinline__ void sel_count(const SelState *s, const int2 *__restrict__ kv, int *__restrict__ cnt,
-                                          int *tmp, int b) {
+                                          int *tmp, int b, int threshold) {
   if (s->done) return;
   const int len = s->len;
-  if (b * kSelBS >= len) return;
+  if (len <= threshold || b * kSelBS >= len) return;
   const int2 *a = kv + s->start;
-  const int pv = s->pv;
+  const int h = len / 2;
+  const int pv = a[h].x, v0 = a[0].x;  // the pivot, and the value the swap moves to position h
   int l = 0, r = 0;
 #pragma unroll
   for (int e = 0; e < kSelPer; ++e) {
     const int p = b * kSelBS + e * kSelThreads + threadIdx.x;
     if (p >= 1 && p < len) {
-      const int v = a[p].x;
+      const int v = p == h ? v0 : a[p].x;
       l += v <= pv;
       r += v >= pv;
     }
@@ -174,17 +169,21 @@ __device__ __forceinline__ void sel_count(const SelState *s, const int2 *__restr
 }
 
 __global__ __launch_bounds__(kSelThreads) void k_sel_count(const SelState *s, const int2 *__restrict__ kv,
-                                                          int *__restrict__ cnt) {
+                                                          int *__restrict__ cnt, int threshold) {
   __shared__ int tmp[kSelThreads / kWave];
-  sel_count(s, kv, cnt, tmp, blockIdx.x);
+  sel_count(s, kv, cnt, tmp, blockIdx.x, threshold);
 }
 
 // step 2 (one block): exclusive prefix of the left counts, exclusive suffix
 // (blocks after b) of the right counts, totals
 template <int NT>
-__device__ __forceinline__ void sel_scan(SelState *s, const int *__restrict__ cnt, int *__restrict__ off, int *sl,
-                                         int *sr) {
+__device__ __forceinline__ void sel_scan(SelState *s, int2 *__restrict__ kv, const int *__restrict__ cnt,
+                                         int *__restrict__ off, int *sl, int *sr, int threshold) {
   if (s->done) return;
+  if (s->len <= threshold) {  // small enough: the host sorts it (no count was made)
+    if (threadIdx.x == 0) s->done = 1;
+    return;
+  }
   const int nb = (s->len + kSelBS - 1) / kSelBS;
   const int per = (nb + NT - 1) / NT;
   const int t = threadIdx.x, b0 = t * per;
@@ -217,13 +216,19 @@ __device__ __forceinline__ void sel_scan(SelState *s, const int *__restrict__ cn
   if (t == 0) {
     s->totL = totL;
     s->totR = totR;
+    // the reference's pivot swap (nothing else touches the array in this launch)
+    const int st = s->start;
+    swap2(kv, st, st + s->len / 2);
+    s->pv = kv[st].x;
+    s->m = 0;
   }
 }
 
-__global__ __launch_bounds__(kSelScanThreads) void k_sel_scan(SelState *s, const int *__restrict__ cnt,
-                                                             int *__restrict__ off) {
+__global__ __launch_bounds__(kSelScanThreads) void k_sel_scan(SelState *s, int2 *__restrict__ kv,
+                                                             const int *__restrict__ cnt, int *__restrict__ off,
+                                                             int threshold) {
   __shared__ int sl[kSelScanThreads], sr[kSelScanThreads];
-  sel_scan<kSelScanThreads>(s, cnt, off, sl, sr);
+  sel_scan<kSelScanThreads>(s, kv, cnt, off, sl, sr, threshold);
 }
 
 // step 3: per position, its rank among the left stops (ascending) and the right
@@ -436,7 +441,7 @@ int refine_launch(SelEngine *e, hipStream_t st, Seg g, std::string *err) {
   for (long l = g.len; l > T; l /= 2) ++levels;
   const int sw = (g.len / 2 + kSelThreads) / kSelThreads;
   if (sel_graphs() && !lib_exiting()) {  // after the exit hook: plain launches, no graph outlives the code object
-    // the steps as one graph launch: 5 * levels kernel launches cost more
+    // the steps as one graph launch: 4 * levels kernel launches cost more
     // host time than the steps take on the device.  The kernels read the
     // segment from the device state and skip blocks past it, so one graph
     // (grids rounded up to a power of two) serves every segment of that size
@@ -472,13 +477,11 @@ int refine_launch(SelEngine *e, hipStream_t st, Seg g, std::string *err) {
       int2 *kv = e->d_kv;
       int *cnt = e->d_cnt, *off = e->d_off, *pl = e->d_posL, *pr = e->d_posR;
       int thr = T;
-      void *a_pivot[] = {&ds, &kv, &thr};
-      void *a_count[] = {&ds, &kv, &cnt};
-      void *a_scan[] = {&ds, &cnt, &off};
+      void *a_count[] = {&ds, &kv, &cnt, &thr};
+      void *a_scan[] = {&ds, &kv, &cnt, &off, &thr};
       void *a_rank[] = {&ds, &kv, &off, &pl, &pr};
       void *a_swap[] = {&ds, &kv, &pl, &pr};
       for (int l = 0; l < levels; ++l) {
-        add(reinterpret_cast<const void *>(k_sel_pivot), 1, 1, a_pivot);
         add(reinterpret_cast<const void *>(k_sel_count), nbp, kSelThreads, a_count);
         add(reinterpret_cast<const void *>(k_sel_scan), 1, kSelScanThreads, a_scan);
         add(reinterpret_cast<const void *>(k_sel_rank), nbp, kSelThreads, a_rank);
@@ -500,9 +503,9 @@ int refine_launch(SelEngine *e, hipStream_t st, Seg g, std::string *err) {
     return 0;
   }
   for (int l = 0; l < levels; ++l) {
-    hipLaunchKernelGGL(k_sel_pivot, dim3(1), dim3(1), 0, st, e->d_state, e->d_kv, T);
-    hipLaunchKernelGGL(k_sel_count, dim3(nb), dim3(kSelThreads), 0, st, e->d_state, e->d_kv, e->d_cnt);
-    hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(kSelScanThreads), 0, st, e->d_state, e->d_cnt, e->d_off);
+    hipLaunchKernelGGL(k_sel_count, dim3(nb), dim3(kSelThreads), 0, st, e->d_state, e->d_kv, e->d_cnt, T);
+    hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(kSelScanThreads), 0, st, e->d_state, e->d_kv, e->d_cnt, e->d_off,
+                       T);
     hipLaunchKernelGGL(k_sel_rank, dim3(nb), dim3(kSelThreads), 0, st, e->d_state, e->d_kv, e->d_off, e->d_posL,
                        e->d_posR);
     hipLaunchKernelGGL(k_sel_swap, dim3(sw), dim3(kSelThreads), 0, st, e->d_state, e->d_kv, e->d_posL, e->d_posR);
