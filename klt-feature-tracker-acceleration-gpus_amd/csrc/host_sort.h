@@ -212,6 +212,7 @@ struct Pool {
     int par;
     unsigned par_min;
     std::atomic<int> *pending;
+    const std::atomic<bool> *stop;  // an asynchronous sort nobody will read any more (nullptr: none)
   };
 
   // how long an idle worker spins after its last task while a sort is in
@@ -351,6 +352,7 @@ struct Pool {
   // queues its right part and goes on with the left one.
   void sort_part(Task t) {
     while (t.n > 1) {
+      if (t.stop && t.stop->load(std::memory_order_relaxed)) return;
       if (t.n <= 4) {  // the recursion's bottom, by table
         small_sort(t.a, t.n);
         return;
@@ -360,16 +362,16 @@ struct Pool {
       const unsigned nlo = j, nhi = t.n - j - 1;
       if (t.par > 0 && nlo >= t.par_min && nhi >= t.par_min) {
         --t.par;
-        submit(Task{hi, nhi, t.par, t.par_min, t.pending});
+        submit(Task{hi, nhi, t.par, t.par_min, t.pending, t.stop});
         t.n = nlo;
         continue;
       }
       if (nlo < nhi) {
-        sort_part(Task{lo, nlo, t.par, t.par_min, t.pending});
+        sort_part(Task{lo, nlo, t.par, t.par_min, t.pending, t.stop});
         t.a = hi;
         t.n = nhi;
       } else {
-        sort_part(Task{hi, nhi, t.par, t.par_min, t.pending});
+        sort_part(Task{hi, nhi, t.par, t.par_min, t.pending, t.stop});
         t.n = nlo;
       }
     }
@@ -381,7 +383,7 @@ struct Pool {
     if (nthreads.load(std::memory_order_acquire) == 0) par = 0;  // no workers (shut down, one CPU): sequential
     const bool spin = par > 0 && n >= 2 * par_min;  // tasks will be queued: keep the workers awake meanwhile
     if (spin) wake();
-    run(Task{a, n, par, par_min, &pending});
+    run(Task{a, n, par, par_min, &pending, nullptr});
     wait_for(pending, spin);
   }
 
@@ -392,15 +394,18 @@ struct Pool {
   // returns whether the workers were woken for it; finish() waits for it,
   // helping with its queued tasks, and ends the spin start() began.  With no
   // workers the sort runs inside start().
-  bool start(P *a, unsigned n, int par, unsigned par_min, std::atomic<int> *pending) {
+  // stop (optional): once set, the sort's tasks end at their next partition
+  // step (the array is then left part-sorted: for a caller that will not read it)
+  bool start(P *a, unsigned n, int par, unsigned par_min, std::atomic<int> *pending,
+             const std::atomic<bool> *stop = nullptr) {
     pending->store(0, std::memory_order_relaxed);
     if (nthreads.load(std::memory_order_acquire) == 0) {
       pending->store(1, std::memory_order_relaxed);
-      run(Task{a, n, 0, par_min, pending});
+      run(Task{a, n, 0, par_min, pending, nullptr});
       return false;
     }
     wake();
-    submit(Task{a, n, par, par_min, pending});
+    submit(Task{a, n, par, par_min, pending, stop});
     return true;
   }
   void finish(std::atomic<int> &pending, bool started) { wait_for(pending, started); }

@@ -564,6 +564,7 @@ struct LazySort {
   // background sorts of right parts split off a reached host segment
   struct Part {
     std::atomic<int> pending{0};
+    std::atomic<bool> stop{false};
     bool started = false, open = false;
   };
   std::deque<Part> parts;  // stable addresses: the pool holds &pending
@@ -571,10 +572,19 @@ struct LazySort {
   // a walk that stops early may leave a look-ahead refinement in flight: its
   // state copy into pinned memory must land before the engine is used again;
   // and background sorts of segments it never reached still run on h_kv
+  // (a walk that ends early never reads them: they are stopped, not finished)
   ~LazySort() {
     if (ahead) (void)hipEventSynchronize(e->ev_ref);
+    const double t0 = now_us();
+    int open = 0;
+    for (Part &pt : parts)
+      if (pt.open) {
+        pt.stop.store(true, std::memory_order_relaxed);
+        ++open;
+      }
     for (Part &pt : parts)
       if (pt.open) kltsort::Pool<int2>::get(0).finish(pt.pending, pt.started);
+    if (open && sel_trace()) fprintf(stderr, "seltrace stop parts=%d us=%.1f\n", open, now_us() - t0);
   }
 
   long next() {
@@ -664,7 +674,7 @@ struct LazySort {
             parts.emplace_back();
             Part &pt = parts.back();
             pt.open = true;
-            pt.started = pool.start(e->h_kv + R.start, (unsigned)R.len, depth, kSelParMin, &pt.pending);
+            pt.started = pool.start(e->h_kv + R.start, (unsigned)R.len, depth, kSelParMin, &pt.pending, &pt.stop);
             R.sorted = false;
             R.task = (int)parts.size() - 1;
           }

@@ -131,6 +131,22 @@ int main() {
       for (unsigned i = 0; i < n; ++i)
         if (a[i].x != b[i].x || a[i].y != b[i].y) { ++bad; std::printf("spine mismatch kind %d n %u at %u\n", kind, n, i); break; }
     }
+  // a background sort stopped before anyone reads it: finish() returns, and
+  // the array still holds the same elements (a permutation, part-sorted)
+  {
+    std::vector<P> a = make(0, 200000, 4242), b = a;
+    std::atomic<int> pend{0};
+    std::atomic<bool> stop{false};
+    const bool st = pool.start(a.data(), 200000, 4, 2048, &pend, &stop);
+    stop.store(true);
+    pool.finish(pend, st);
+    ++cases;
+    auto key = [](const P &p, const P &q) { return p.y < q.y; };
+    std::sort(a.begin(), a.end(), key);
+    std::sort(b.begin(), b.end(), key);
+    for (unsigned i = 0; i < a.size(); ++i)
+      if (a[i].x != b[i].x || a[i].y != b[i].y) { ++bad; std::printf("stopped sort lost elements\n"); break; }
+  }
   // four callers at once on the shared pool
   std::vector<std::vector<P>> seq(4), par(4);
   for (int c = 0; c < 4; ++c) {
