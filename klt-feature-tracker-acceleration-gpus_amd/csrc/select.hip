@@ -407,6 +407,9 @@ struct Seg {
 // pool in the background and the left part is treated the same way, so the
 // walk starts on the leftmost piece while the rest is sorted beside it
 constexpr int kSelSpineMin = 4096;
+#ifndef KLT_SEL_LOPSIDED
+#define KLT_SEL_LOPSIDED 1  // A/B hook (make variant DEFS=-DKLT_SEL_LOPSIDED=0): every right part sorted in the background
+#endif
 
 // levels of two-way task splits in the host sort (2^depth tasks on the pool);
 // KLT_AMD_SORT_DEPTH (0..5) overrides the default for A/B runs, read once
@@ -670,7 +673,13 @@ struct LazySort {
         if (depth > 0 && g.len > kSelSpineMin) {
           const int j = (int)kltsort::partition(e->h_kv + g.start, (unsigned)g.len);
           Seg R{g.start + j + 1, g.len - j - 1, true, true};
-          if (R.len > 1) {
+          // the right part is sorted in the background only when the left
+          // part gives the walk about as much to do first; after a lopsided
+          // split (a small left part) it stays unsorted and is split in turn
+          // when reached, rather than waited for whole
+          if (KLT_SEL_LOPSIDED && R.len > 1 && R.len > 4 * j + kSelSpineMin) {
+            R.sorted = false;
+          } else if (R.len > 1) {
             parts.emplace_back();
             Part &pt = parts.back();
             pt.open = true;
