@@ -42,7 +42,7 @@ int main() {
         }
         std::sort(t.begin(), t.end());
         std::printf("{\"n\": %u, \"depth\": %d, \"workers\": %d, \"us_median\": %.1f, \"us_min\": %.1f}\n", n, depth,
-                    pool.nworkers, t[t.size() / 2], t[0]);
+                    pool.nthreads.load(), t[t.size() / 2], t[0]);
       }
   }
   return 0;
