@@ -56,13 +56,100 @@ unsigned partition_hoare(P *a, unsigned n) {
 // first position whose CURRENT value is >= pv (a[0], the pivot, at worst).
 // Random keys make the reference's branches mispredict about every other
 // element; this runs ~3x faster on them (tools/hostcheck/sortbench.cpp).
+// The stop collection of one 64-position block, eight positions at a time
+// with AVX2 (x86 hosts that have it; the same positions in the same order as
+// the scalar loops): the .x of eight pairs, one compare, a movemask, and the
+// set bits' positions appended through a table.
+#if defined(__x86_64__)
+#include <immintrin.h>
+struct StopLut {
+  alignas(32) unsigned idx[256][8];  // the set bits of a mask, ascending, padded
+  unsigned char rev[256];            // a mask's 8 bits reversed
+  StopLut() {
+    for (unsigned m = 0; m < 256; ++m) {
+      unsigned k = 0, r = 0;
+      for (unsigned b = 0; b < 8; ++b) {
+        if (m >> b & 1) idx[m][k++] = b;
+        r |= (m >> b & 1u) << (7 - b);
+      }
+      for (; k < 8; ++k) idx[m][k] = 0;
+      rev[m] = (unsigned char)r;
+    }
+  }
+  static const StopLut &get() {
+    static const StopLut t;
+    return t;
+  }
+};
+inline bool host_has_avx2() {
+  static const bool v = [] {
+    const char *e = std::getenv("KLT_SORT_SCALAR");  // A/B: the scalar stops
+    return __builtin_cpu_supports("avx2") && !(e && *e && *e != '0');
+  }();
+  return v;
+}
+// x of pairs p .. p+7 (8-byte pairs, x first)
+__attribute__((target("avx2"))) inline __m256i xs8(const int *pairs) {
+  const __m256 lo = _mm256_loadu_ps(reinterpret_cast<const float *>(pairs));
+  const __m256 hi = _mm256_loadu_ps(reinterpret_cast<const float *>(pairs + 8));
+  const __m256 ev = _mm256_shuffle_ps(lo, hi, _MM_SHUFFLE(2, 0, 2, 0));  // x0 x1 x4 x5 | x2 x3 x6 x7
+  return _mm256_castpd_si256(_mm256_permute4x64_pd(_mm256_castps_pd(ev), _MM_SHUFFLE(3, 1, 2, 0)));
+}
+// left stops (x <= pv) among positions lp .. e, ascending, appended to L
+__attribute__((target("avx2"))) inline unsigned stops_left_avx2(const int *pairs, int pv, unsigned lp, unsigned e,
+                                                                unsigned *L) {
+  const StopLut &T = StopLut::get();
+  const __m256i v = _mm256_set1_epi32(pv);
+  unsigned nl = 0, p = lp;
+  for (; p + 7 <= e; p += 8) {
+    const __m256i x = xs8(pairs + 2 * p);
+    const unsigned m = ~(unsigned)_mm256_movemask_ps(_mm256_castsi256_ps(_mm256_cmpgt_epi32(x, v))) & 0xFFu;
+    const __m256i o = _mm256_add_epi32(_mm256_set1_epi32((int)p), _mm256_load_si256(reinterpret_cast<const __m256i *>(T.idx[m])));
+    _mm256_storeu_si256(reinterpret_cast<__m256i *>(L + nl), o);
+    nl += (unsigned)__builtin_popcount(m);
+  }
+  for (; p <= e; ++p) {
+    L[nl] = p;
+    nl += pairs[2 * p] <= pv;
+  }
+  return nl;
+}
+// right stops (x >= pv) among positions rp down to e, descending, appended to R
+__attribute__((target("avx2"))) inline unsigned stops_right_avx2(const int *pairs, int pv, unsigned rp, unsigned e,
+                                                                 unsigned *R) {
+  const StopLut &T = StopLut::get();
+  const __m256i v = _mm256_set1_epi32(pv);
+  unsigned nr = 0, p = rp;  // next position, scanning down
+  for (; p >= e + 7; p -= 8) {
+    const __m256i x = xs8(pairs + 2 * (p - 7));  // positions p-7 .. p
+    const unsigned m = ~(unsigned)_mm256_movemask_ps(_mm256_castsi256_ps(_mm256_cmpgt_epi32(v, x))) & 0xFFu;
+    const unsigned mr = T.rev[m];  // bit k: position p - k
+    const __m256i o = _mm256_sub_epi32(_mm256_set1_epi32((int)p), _mm256_load_si256(reinterpret_cast<const __m256i *>(T.idx[mr])));
+    _mm256_storeu_si256(reinterpret_cast<__m256i *>(R + nr), o);
+    nr += (unsigned)__builtin_popcount(mr);
+  }  // (p >= e + 7 >= 8 in the loop, so p - 8 never wraps)
+  for (; (int)p >= (int)e; --p) {
+    R[nr] = p;
+    nr += pairs[2 * p] >= pv;
+  }
+  return nr;
+}
+#endif
+
 template <class P>
 unsigned partition(P *a, unsigned n) {
   if (n < 16) return partition_hoare(a, n);
   std::swap(a[0], a[n / 2]);
   const auto pv = a[0].x;
   constexpr unsigned B = 64;
-  unsigned L[B], R[B];
+  unsigned L[B + 8], R[B + 8];  // + 8: the vector appends write whole groups
+#if defined(__x86_64__)
+  constexpr bool vec_ok = sizeof(P) == 8 && sizeof(a[0].x) == 4;
+  const bool vec = vec_ok && host_has_avx2();
+#else
+  constexpr bool vec_ok = false;
+  const bool vec = false;
+#endif
   unsigned nl = 0, sl = 0, nr = 0, sr = 0;
   unsigned lp = 1, rp = n - 1;  // next positions to scan: up from lp, down from rp
   unsigned last_r = n;          // the last swapped right stop (n: none)
@@ -71,6 +158,15 @@ unsigned partition(P *a, unsigned n) {
       if (lp > n - 1) break;  // no further left stop: the reference's i runs into j
       nl = sl = 0;
       const unsigned e = lp + B - 1 < n - 1 ? lp + B - 1 : n - 1;
+#if defined(__x86_64__)
+      if constexpr (vec_ok) {
+        if (vec) {
+          nl = stops_left_avx2(reinterpret_cast<const int *>(a), (int)pv, lp, e, L);
+          lp = e + 1;
+          continue;
+        }
+      }
+#endif
       for (unsigned p = lp; p <= e; ++p) {
         L[nl] = p;
         nl += a[p].x <= pv;
@@ -82,6 +178,15 @@ unsigned partition(P *a, unsigned n) {
       if (rp < 1) break;  // no further right stop above the pivot
       nr = sr = 0;
       const unsigned e = rp >= B ? rp - B + 1 : 1;
+#if defined(__x86_64__)
+      if constexpr (vec_ok) {
+        if (vec) {
+          nr = stops_right_avx2(reinterpret_cast<const int *>(a), (int)pv, rp, e, R);
+          rp = e - 1;
+          continue;
+        }
+      }
+#endif
       for (unsigned p = rp + 1; p-- > e;) {
         R[nr] = p;
         nr += a[p].x >= pv;

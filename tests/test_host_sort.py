@@ -9,10 +9,12 @@ small par_min so every size splits) with the one-thread sort, element for
 element, on random, tie-heavy, constant and presorted inputs, including
 several callers sorting at once on the shared pool; and the branch-free
 partition step (host_sort.h partition) with the reference's own
-(partition_hoare), array and pivot slot, on every size up to 139 and more.
+(partition_hoare), array and pivot slot, on every size up to 139 and more --
+with the AVX2 stop collection and with the scalar one.
 """
 from __future__ import annotations
 
+import os
 import shutil
 import subprocess
 from pathlib import Path
@@ -173,6 +175,13 @@ def test_pooled_sort_equals_sequential(tmp_path):
     exe = tmp_path / "drv"
     subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", f"-I{CSRC}", str(src), "-o", str(exe)],
                    check=True, capture_output=True, text=True)
-    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
-    assert out.returncode == 0, out.stdout + out.stderr
-    assert "bad 0" in out.stdout
+    # both stop collections of the block partition: AVX2 (where the host has
+    # it) and the scalar loops (KLT_SORT_SCALAR=1)
+    for scalar in (False, True):
+        env = dict(os.environ)
+        env.pop("KLT_SORT_SCALAR", None)
+        if scalar:
+            env["KLT_SORT_SCALAR"] = "1"
+        out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120, env=env)
+        assert out.returncode == 0, out.stdout + out.stderr
+        assert "bad 0" in out.stdout
