@@ -219,41 +219,60 @@ void sort_hoare(P *a, unsigned n) {
   }
 }
 
-// The recursion below 5 elements, by table.  Quicksort only compares keys, so
-// the permutation it applies to n <= 4 elements is a function of the n(n-1)/2
-// pairwise outcomes (<, ==, >) alone.  The tables are built once by running
-// sort_hoare over every key pattern with values below n (every weak order of
-// n elements occurs among them); an n-element subarray then costs its
-// comparisons and one gather instead of up to three branchy partition steps
-// (the recursion's bottom: 2/3 of a map segment's steps are below 16 elements,
-// most of them below 5).  tests/test_host_sort.py checks it exhaustively.
+// The recursion below 6 elements, by table.  Quicksort only compares keys, so
+// the permutation it applies to n <= 5 elements is a function of their weak
+// order alone, which each element's competition rank (the number of keys
+// strictly below its own) spells out: code = sum_i rank_i * n^i < n^n.  The
+// tables are built once by running sort_hoare over every key pattern with
+// values below n (every weak order of n elements occurs among them); an
+// n-element subarray then costs n(n-1) comparisons and one gather instead of
+// up to four branchy partition steps (the recursion's bottom: 2/3 of a map
+// segment's steps are below 16 elements, most of them below 6).  Ranks instead
+// of round 6's first table (3^(pairs) codes, n <= 4) measured 5 % faster, and
+// n <= 5 another 2-3 % (one-thread sort of 30 000 map-like pairs).
+// tests/test_host_sort.py checks it exhaustively.
+constexpr unsigned kSmallMax = 5;
 struct SmallPerm {
-  unsigned char p[5][729][4];  // [n][code][i]: element i of the result is a[p[n][code][i]]
-  static int cmp3(int a, int b) { return (a > b) + (a >= b); }  // 0 <, 1 ==, 2 >
-  template <class K>
-  static int code(const K *k, unsigned n) {
-    int c = 0;
-    for (unsigned i = 0; i < n; ++i)
-      for (unsigned j = i + 1; j < n; ++j) c = 3 * c + cmp3(k[i], k[j]);
+  static constexpr unsigned kCodes = 3125;  // 5^5
+  unsigned char p[kSmallMax + 1][kCodes][kSmallMax];  // [n][code][i]: element i of the result is a[p[n][code][i]]
+  template <unsigned N, class K>
+  static unsigned code(const K *k) {
+    unsigned c = 0;
+#pragma GCC unroll 8
+    for (int i = (int)N - 1; i >= 0; --i) {
+      unsigned r = 0;
+#pragma GCC unroll 8
+      for (unsigned j = 0; j < N; ++j) r += k[j] < k[i];
+      c = c * N + r;
+    }
     return c;
+  }
+  template <class K>
+  static unsigned code_n(const K *k, unsigned n) {
+    switch (n) {
+      case 2: return code<2>(k);
+      case 3: return code<3>(k);
+      case 4: return code<4>(k);
+      default: return code<5>(k);
+    }
   }
   SmallPerm() {
     struct Q {
       int x, y;
     };
-    for (unsigned n = 2; n <= 4; ++n) {
+    for (unsigned n = 2; n <= kSmallMax; ++n) {
       unsigned total = 1;
       for (unsigned i = 0; i < n; ++i) total *= n;
       for (unsigned m = 0; m < total; ++m) {
-        Q q[4];
-        int keys[4];
+        Q q[kSmallMax];
+        int keys[kSmallMax];
         unsigned r = m;
         for (unsigned i = 0; i < n; ++i, r /= n) {
           keys[i] = (int)(r % n);
           q[i] = Q{keys[i], (int)i};
         }
         sort_hoare(q, n);
-        const int c = code(keys, n);
+        const unsigned c = code_n(keys, n);
         for (unsigned i = 0; i < n; ++i) p[n][c][i] = (unsigned char)q[i].y;
       }
     }
@@ -264,14 +283,24 @@ struct SmallPerm {
   }
 };
 
+template <unsigned N, class P>
+inline void small_sort_n(P *a) {
+  decltype(a[0].x) k[N];
+  for (unsigned i = 0; i < N; ++i) k[i] = a[i].x;
+  const unsigned char *perm = SmallPerm::get().p[N][SmallPerm::code<N>(k)];
+  P t[N];
+  for (unsigned i = 0; i < N; ++i) t[i] = a[perm[i]];
+  for (unsigned i = 0; i < N; ++i) a[i] = t[i];
+}
+
 template <class P>
-inline void small_sort(P *a, unsigned n) {  // 2 <= n <= 4: the reference recursion's result
-  int k[4];
-  for (unsigned i = 0; i < n; ++i) k[i] = a[i].x;
-  const unsigned char *perm = SmallPerm::get().p[n][SmallPerm::code(k, n)];
-  P t[4];
-  for (unsigned i = 0; i < n; ++i) t[i] = a[perm[i]];
-  for (unsigned i = 0; i < n; ++i) a[i] = t[i];
+inline void small_sort(P *a, unsigned n) {  // 2 <= n <= kSmallMax: the reference recursion's result
+  switch (n) {
+    case 2: small_sort_n<2>(a); break;
+    case 3: small_sort_n<3>(a); break;
+    case 4: small_sort_n<4>(a); break;
+    default: small_sort_n<5>(a); break;
+  }
 }
 
 // CPUs this process may run on: the affinity mask, capped by a cgroup-v2 CPU
@@ -458,7 +487,7 @@ struct Pool {
   void sort_part(Task t) {
     while (t.n > 1) {
       if (t.stop && t.stop->load(std::memory_order_relaxed)) return;
-      if (t.n <= 4) {  // the recursion's bottom, by table
+      if (t.n <= kSmallMax) {  // the recursion's bottom, by table
         small_sort(t.a, t.n);
         return;
       }

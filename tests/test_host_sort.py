@@ -68,7 +68,7 @@ int main() {
         for (unsigned i = 0; same && i < n; ++i) same = a[i].x == b[i].x && a[i].y == b[i].y;
         if (!same) { ++bad; std::printf("partition mismatch kind %d n %u seed %u\n", kind, n, seed); }
       }
-  // the table bottom (small_sort, n <= 4) inside the recursion: every array of
+  // the table bottom (small_sort, n <= 5) inside the recursion: every array of
   // n <= 7 elements with keys below n, sorted whole, equals the reference's
   for (unsigned n = 1; n <= 7; ++n) {
     unsigned total = 1;
