@@ -150,6 +150,17 @@ static int default_host_threads() {
   }();
   return n;
 }
+// DMAs a large per-call frame upload is split into (KLT_AMD_UPLOAD_GROUPS, A/B;
+// default 4): the host copies group g+1 into pinned memory while group g's DMA runs
+static size_t upload_groups() {
+  static const size_t g = [] {
+    const char *e = getenv("KLT_AMD_UPLOAD_GROUPS");
+    const long v = e && *e ? atol(e) : 4;
+    return (size_t)(v < 1 ? 1 : v > 64 ? 64 : v);
+  }();
+  return g;
+}
+
 static size_t copy_piece() {
   static const size_t n = [] {
     const char *v = getenv("KLT_AMD_COPY_PIECE");
@@ -1400,7 +1411,8 @@ KLT_API int klt_hip_upload_frame(klt_hip_ctx *c, int buf, const unsigned char *h
   // in groups: the host pool copies group g+1 into pinned memory while group
   // g's DMA runs
   ensure_pool(c);
-  const size_t group = n >= (1u << 20) ? (n + 3) / 4 : n, piece = copy_piece();
+  const size_t G = upload_groups(), piece = copy_piece();
+  const size_t group = n >= (1u << 20) ? (((n + G - 1) / G + 63) & ~(size_t)63) : n;
   for (size_t o = 0; o < n; o += group) {
     const size_t m = n - o < group ? n - o : group;
     unsigned char *dst = c->h_u8[buf] + o;
