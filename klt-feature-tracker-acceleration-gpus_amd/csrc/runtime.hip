@@ -1413,6 +1413,14 @@ KLT_API int klt_hip_upload_frame(klt_hip_ctx *c, int buf, const unsigned char *h
   ensure_pool(c);
   const size_t G = upload_groups(), piece = copy_piece();
   const size_t group = n >= (1u << 20) ? (((n + G - 1) / G + 63) & ~(size_t)63) : n;
+  // KLT_UPLOAD_TRACE=1: per group, the host copy and the DMA's enqueue (us) on stderr
+  static const bool trace = [] {
+    const char *e = getenv("KLT_UPLOAD_TRACE");
+    return e && *e == '1';
+  }();
+  char tl[512];
+  int tn = 0;
+  double t0 = trace ? wall_us() : 0.0;
   for (size_t o = 0; o < n; o += group) {
     const size_t m = n - o < group ? n - o : group;
     unsigned char *dst = c->h_u8[buf] + o;
@@ -1422,8 +1430,15 @@ KLT_API int klt_hip_upload_frame(klt_hip_ctx *c, int buf, const unsigned char *h
           copy_stream(dst + q, src + q, m - q < piece ? m - q : piece);
         }))
       return -1;
+    const double t1 = trace ? wall_us() : 0.0;
     HIPCHK(c, hipMemcpyAsync(c->d_u8[buf] + o, dst, m, hipMemcpyHostToDevice, c->stream));
+    if (trace) {
+      const double t2 = wall_us();
+      if (tn < (int)sizeof tl - 40) tn += snprintf(tl + tn, sizeof tl - tn, " copy=%.1f enq=%.1f", t1 - t0, t2 - t1);
+      t0 = t2;
+    }
   }
+  if (trace) fprintf(stderr, "uptrace groups=%zu%s\n", (n + group - 1) / group, tn ? tl : "");
   HIPCHK(c, hipEventRecord(c->u8_done[buf], c->stream));
   c->u8_w[buf] = ncols;
   c->u8_h[buf] = nrows;
