@@ -121,6 +121,55 @@ struct HostPool {
       finished.fetch_add(1);
     }
   }
+  // fn(0) .. fn(n-1) on the workers in one generation, the tasks taken in
+  // index order and counted per group of `per`; on_group(g) runs on the
+  // calling thread, in group order, as soon as it sees every task of group g
+  // done (one wake-up of the workers per call, not one per group -- a
+  // generation's wake-ups and its wait for the last worker cost ~10 us,
+  // measured per group on the box: tools/exp/r06_upload_ab.sh).  The caller
+  // copies too while the tasks being claimed are its next group's.  Returns
+  // the first non-zero on_group result (the remaining tasks still run).
+  template <class Fn, class OnGroup>
+  int parallel_groups(size_t n, size_t per, const Fn &f, const OnGroup &on_group) {
+    constexpr size_t kMaxGroups = 64;
+    const size_t ng = (n + per - 1) / per;
+    if (ng > kMaxGroups || n == 0) return -1;
+    std::atomic<unsigned> gd[kMaxGroups];
+    for (size_t g = 0; g < ng; ++g) gd[g].store(0, std::memory_order_relaxed);
+    const std::function<void(size_t)> task = [&](size_t i) {
+      f(i);
+      gd[i / per].fetch_add(1, std::memory_order_release);
+    };
+    {
+      std::lock_guard<std::mutex> l(m);
+      fn = &task;
+      ntasks = n;
+      next = 0;
+      finished = 0;
+      ++gen;
+    }
+    cv.notify_all();
+    int rc = 0;
+    for (size_t g = 0; g < ng && rc == 0;) {
+      const unsigned want = (unsigned)(g + 1 < ng ? per : n - g * per);
+      if (gd[g].load(std::memory_order_acquire) == want) {
+        rc = on_group(g);
+        ++g;
+        continue;
+      }
+      if (next.load(std::memory_order_relaxed) / per == g) {
+        const size_t i = next.fetch_add(1);
+        if (i < n) task(i);
+      } else {
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+      }
+    }
+    for (size_t i; (i = next.fetch_add(1)) < n;) task(i);  // an early error: finish the tasks here too
+    while (finished.load() < (int)th.size()) std::this_thread::yield();
+    return rc;
+  }
   // fn(0) .. fn(n-1), on the workers and the calling thread
   void parallel(size_t n, const std::function<void(size_t)> &f) {
     {
@@ -159,6 +208,16 @@ static size_t upload_groups() {
     return (size_t)(v < 1 ? 1 : v > 64 ? 64 : v);
   }();
   return g;
+}
+
+// the per-call upload's groups in one pool generation (round 6; KLT_AMD_UPLOAD_PIPE=0:
+// one generation per group, the round-5 schedule)
+static bool upload_pipelined() {
+  static const bool v = [] {
+    const char *e = getenv("KLT_AMD_UPLOAD_PIPE");
+    return !(e && *e == '0');
+  }();
+  return v;
 }
 
 static size_t copy_piece() {
@@ -1419,26 +1478,53 @@ KLT_API int klt_hip_upload_frame(klt_hip_ctx *c, int buf, const unsigned char *h
     return e && *e == '1';
   }();
   char tl[512];
-  int tn = 0;
+  int tn = 0, nq = 0;
   double t0 = trace ? wall_us() : 0.0;
-  for (size_t o = 0; o < n; o += group) {
-    const size_t m = n - o < group ? n - o : group;
-    unsigned char *dst = c->h_u8[buf] + o;
-    const unsigned char *src = host + o;
-    if (host_parallel(c, (m + piece - 1) / piece, [&](size_t t) {
-          const size_t q = t * piece;
-          copy_stream(dst + q, src + q, m - q < piece ? m - q : piece);
-        }))
-      return -1;
+  const auto enqueue = [&](size_t o, size_t m) -> int {
+    ++nq;
     const double t1 = trace ? wall_us() : 0.0;
-    HIPCHK(c, hipMemcpyAsync(c->d_u8[buf] + o, dst, m, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_u8[buf] + o, c->h_u8[buf] + o, m, hipMemcpyHostToDevice, c->stream));
     if (trace) {
       const double t2 = wall_us();
       if (tn < (int)sizeof tl - 40) tn += snprintf(tl + tn, sizeof tl - tn, " copy=%.1f enq=%.1f", t1 - t0, t2 - t1);
       t0 = t2;
     }
+    return 0;
+  };
+  if (c->pool && upload_pipelined()) {
+    // one generation of the pool over every piece; each group (whole pieces)
+    // is DMAed as soon as its pieces are in pinned memory
+    const size_t np = (n + piece - 1) / piece, per = n >= (1u << 20) ? (np + G - 1) / G : np;
+    const size_t group = per * piece;
+    try {
+      if (c->pool->parallel_groups(
+              np, per,
+              [&](size_t t) {
+                const size_t q = t * piece;
+                copy_stream(c->h_u8[buf] + q, host + q, n - q < piece ? n - q : piece);
+              },
+              [&](size_t g) {
+                const size_t o = g * group;
+                return enqueue(o, n - o < group ? n - o : group);
+              }))
+        return -1;
+    } catch (...) {
+      return fail(c, "upload: host task failed (out of memory?)");
+    }
+  } else {
+    for (size_t o = 0; o < n; o += group) {
+      const size_t m = n - o < group ? n - o : group;
+      unsigned char *dst = c->h_u8[buf] + o;
+      const unsigned char *src = host + o;
+      if (host_parallel(c, (m + piece - 1) / piece, [&](size_t t) {
+            const size_t q = t * piece;
+            copy_stream(dst + q, src + q, m - q < piece ? m - q : piece);
+          }))
+        return -1;
+      if (enqueue(o, m)) return -1;
+    }
   }
-  if (trace) fprintf(stderr, "uptrace groups=%zu%s\n", (n + group - 1) / group, tn ? tl : "");
+  if (trace) fprintf(stderr, "uptrace groups=%d%s\n", nq, tn ? tl : "");
   HIPCHK(c, hipEventRecord(c->u8_done[buf], c->stream));
   c->u8_w[buf] = ncols;
   c->u8_h[buf] = nrows;
