@@ -241,6 +241,7 @@ struct klt_hip_ctx {
   // the context switches away from it, so a reset or destroy can wait for the
   // work queued there even after the caller has destroyed the stream
   hipEvent_t ev_caller = nullptr;
+  hipEvent_t ev_feat = nullptr;  // the per-call feature list's completion (feat_unpack's spin wait)
   bool caller_pending = false;
   Slot slot[KLT_HIP_MAX_SLOTS + 2];  // + the batch seed and scratch slots
   uint8_t *d_u8[2] = {nullptr, nullptr};
@@ -1310,6 +1311,7 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
   }
   if (c->ev_start) hipEventDestroy(c->ev_start);
   if (c->ev_caller) hipEventDestroy(c->ev_caller);
+  if (c->ev_feat) hipEventDestroy(c->ev_feat);
   if (c->ev_go) hipEventDestroy(c->ev_go);
   for (unsigned *p : c->d_sig) hipFree(p);
   if (c->own) hipStreamDestroy(c->own);
@@ -1794,8 +1796,30 @@ int feat_stage_in(klt_hip_ctx *c, const float *x, const float *y, const int *val
 }
 
 // the pinned block back into the host list once the stream is done with it
+// How long a per-call KLTTrackFeatures polls its feature list's completion
+// before it blocks (KLT_AMD_SYNC_SPIN_US, default 2000; 0: block at once).
+// A blocking wait sleeps until the device's completion interrupt, whose
+// wake-up the caller then pays on every call; the call's device work is
+// ~80 us, so polling costs one host thread that long.
+static double sync_spin_us() {
+  static const double v = [] {
+    const char *e = getenv("KLT_AMD_SYNC_SPIN_US");
+    return e && *e ? atof(e) : 2000.0;
+  }();
+  return v;
+}
+
 int feat_unpack(klt_hip_ctx *c, float *x, float *y, int *val, int n) {
   if (n <= 0) return 0;
+  if (sync_spin_us() > 0) {
+    if (!c->ev_feat) HIPCHK(c, hipEventCreateWithFlags(&c->ev_feat, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(c->ev_feat, c->stream));
+    const double t0 = wall_us();
+    hipError_t q;
+    while ((q = hipEventQuery(c->ev_feat)) == hipErrorNotReady && wall_us() - t0 < sync_spin_us())
+      for (int k = 0; k < 16; ++k) __builtin_ia32_pause();
+    if (q != hipSuccess && q != hipErrorNotReady) return fail(c, "feature list: %s", hipGetErrorString(q));
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   memcpy(x, c->h_feat, sizeof(float) * n);
   memcpy(y, c->h_feat + n, sizeof(float) * n);
