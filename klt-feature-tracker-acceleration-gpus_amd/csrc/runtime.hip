@@ -122,23 +122,29 @@ struct HostPool {
     }
   }
   // fn(0) .. fn(n-1) on the workers in one generation, the tasks taken in
-  // index order and counted per group of `per`; on_group(g) runs on the
-  // calling thread, in group order, as soon as it sees every task of group g
-  // done (one wake-up of the workers per call, not one per group -- a
-  // generation's wake-ups and its wait for the last worker cost ~10 us,
-  // measured per group on the box: tools/exp/r06_upload_ab.sh).  The caller
-  // copies too while the tasks being claimed are its next group's.  Returns
-  // the first non-zero on_group result (the remaining tasks still run).
+  // index order; group g is tasks [end[g-1], end[g]) (end[ng-1] == n), and
+  // on_group(g) runs on the calling thread, in group order, as soon as it
+  // sees every task of group g done (one wake-up of the workers per call, not
+  // one per group: a generation's wake-ups and its wait for the last worker
+  // cost ~10 us, measured per group on the box, tools/exp/r06_upload_ab.sh).
+  // The caller copies too while the tasks being claimed are its next
+  // group's.  Returns the first non-zero on_group result (the remaining tasks
+  // still run).
   template <class Fn, class OnGroup>
-  int parallel_groups(size_t n, size_t per, const Fn &f, const OnGroup &on_group) {
+  int parallel_groups(const size_t *end, size_t ng, const Fn &f, const OnGroup &on_group) {
     constexpr size_t kMaxGroups = 64;
-    const size_t ng = (n + per - 1) / per;
-    if (ng > kMaxGroups || n == 0) return -1;
+    if (ng == 0 || ng > kMaxGroups || end[ng - 1] == 0) return -1;
+    const size_t n = end[ng - 1];
     std::atomic<unsigned> gd[kMaxGroups];
     for (size_t g = 0; g < ng; ++g) gd[g].store(0, std::memory_order_relaxed);
+    const auto group_of = [&](size_t i) {
+      size_t g = 0;
+      while (i >= end[g]) ++g;
+      return g;
+    };
     const std::function<void(size_t)> task = [&](size_t i) {
       f(i);
-      gd[i / per].fetch_add(1, std::memory_order_release);
+      gd[group_of(i)].fetch_add(1, std::memory_order_release);
     };
     {
       std::lock_guard<std::mutex> l(m);
@@ -151,13 +157,13 @@ struct HostPool {
     cv.notify_all();
     int rc = 0;
     for (size_t g = 0; g < ng && rc == 0;) {
-      const unsigned want = (unsigned)(g + 1 < ng ? per : n - g * per);
+      const unsigned want = (unsigned)(end[g] - (g ? end[g - 1] : 0));
       if (gd[g].load(std::memory_order_acquire) == want) {
         rc = on_group(g);
         ++g;
         continue;
       }
-      if (next.load(std::memory_order_relaxed) / per == g) {
+      if (next.load(std::memory_order_relaxed) < end[g]) {
         const size_t i = next.fetch_add(1);
         if (i < n) task(i);
       } else {
@@ -220,6 +226,17 @@ static bool upload_pipelined() {
   return v;
 }
 
+// the first DMA group's share of a pipelined per-call upload
+// (KLT_AMD_UPLOAD_FIRST, a fraction; 0 or unset: equal groups)
+static double upload_first() {
+  static const double v = [] {
+    const char *e = getenv("KLT_AMD_UPLOAD_FIRST");
+    const double x = e && *e ? atof(e) : 0.0;
+    return x > 0 && x < 1 ? x : 0.0;
+  }();
+  return v;
+}
+
 static size_t copy_piece() {
   static const size_t n = [] {
     const char *v = getenv("KLT_AMD_COPY_PIECE");
@@ -241,7 +258,10 @@ struct klt_hip_ctx {
   // the context switches away from it, so a reset or destroy can wait for the
   // work queued there even after the caller has destroyed the stream
   hipEvent_t ev_caller = nullptr;
-  hipEvent_t ev_feat = nullptr;  // the per-call feature list's completion (feat_unpack's spin wait)
+  unsigned *h_done = nullptr;  // a pinned word the stream writes after a per-call feature list (feat_unpack's poll)
+  unsigned *d_done = nullptr;  // its device address
+  unsigned done_seq = 0;
+  bool done_broken = false;    // the stream write failed once: block instead
   bool caller_pending = false;
   Slot slot[KLT_HIP_MAX_SLOTS + 2];  // + the batch seed and scratch slots
   uint8_t *d_u8[2] = {nullptr, nullptr};
@@ -1311,7 +1331,7 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
   }
   if (c->ev_start) hipEventDestroy(c->ev_start);
   if (c->ev_caller) hipEventDestroy(c->ev_caller);
-  if (c->ev_feat) hipEventDestroy(c->ev_feat);
+  if (c->h_done) hipHostFree(c->h_done);
   if (c->ev_go) hipEventDestroy(c->ev_go);
   for (unsigned *p : c->d_sig) hipFree(p);
   if (c->own) hipStreamDestroy(c->own);
@@ -1495,19 +1515,32 @@ KLT_API int klt_hip_upload_frame(klt_hip_ctx *c, int buf, const unsigned char *h
   };
   if (c->pool && upload_pipelined()) {
     // one generation of the pool over every piece; each group (whole pieces)
-    // is DMAed as soon as its pieces are in pinned memory
-    const size_t np = (n + piece - 1) / piece, per = n >= (1u << 20) ? (np + G - 1) / G : np;
-    const size_t group = per * piece;
+    // is DMAed as soon as its pieces are in pinned memory.  Each DMA costs
+    // ~10 us besides its bytes (tools/exp/r06_upload_pipe_ab.sh: 16 groups
+    // ~120 us slower than 4), so few groups, the first one short: its DMA
+    // starts early and the rest's copy runs beside it
+    const size_t np = (n + piece - 1) / piece;
+    size_t end[64], ng = 0;
+    if (n < (1u << 20) || G == 1 || np < G) {
+      end[ng++] = np;
+    } else {
+      const double f = upload_first();
+      size_t e0 = f > 0 ? (size_t)(f * (double)np + 0.5) : (np + G - 1) / G;
+      e0 = e0 < 1 ? 1 : e0 > np - (G - 1) ? np - (G - 1) : e0;
+      end[ng++] = e0;
+      for (size_t g = 1; g < G; ++g) end[ng++] = e0 + ((np - e0) * g + (G - 2)) / (G - 1);
+      end[ng - 1] = np;
+    }
     try {
       if (c->pool->parallel_groups(
-              np, per,
+              end, ng,
               [&](size_t t) {
                 const size_t q = t * piece;
                 copy_stream(c->h_u8[buf] + q, host + q, n - q < piece ? n - q : piece);
               },
               [&](size_t g) {
-                const size_t o = g * group;
-                return enqueue(o, n - o < group ? n - o : group);
+                const size_t o = (g ? end[g - 1] : 0) * piece, e = end[g] * piece < n ? end[g] * piece : n;
+                return enqueue(o, e - o);
               }))
         return -1;
     } catch (...) {
@@ -1797,28 +1830,41 @@ int feat_stage_in(klt_hip_ctx *c, const float *x, const float *y, const int *val
 
 // the pinned block back into the host list once the stream is done with it
 // How long a per-call KLTTrackFeatures polls its feature list's completion
-// before it blocks (KLT_AMD_SYNC_SPIN_US, default 2000; 0: block at once).
-// A blocking wait sleeps until the device's completion interrupt, whose
-// wake-up the caller then pays on every call; the call's device work is
-// ~80 us, so polling costs one host thread that long.
+// before it blocks (KLT_AMD_SYNC_SPIN_US; default 0: block at once).  The
+// stream writes a sequence number into a pinned word after the list, and the
+// host reads the word with plain loads -- no runtime call while it polls
+// (polling hipEventQuery instead made the registered call 9-20 us slower).
 static double sync_spin_us() {
   static const double v = [] {
     const char *e = getenv("KLT_AMD_SYNC_SPIN_US");
-    return e && *e ? atof(e) : 2000.0;
+    return e && *e ? atof(e) : 0.0;
   }();
   return v;
 }
 
 int feat_unpack(klt_hip_ctx *c, float *x, float *y, int *val, int n) {
   if (n <= 0) return 0;
-  if (sync_spin_us() > 0) {
-    if (!c->ev_feat) HIPCHK(c, hipEventCreateWithFlags(&c->ev_feat, hipEventDisableTiming));
-    HIPCHK(c, hipEventRecord(c->ev_feat, c->stream));
-    const double t0 = wall_us();
-    hipError_t q;
-    while ((q = hipEventQuery(c->ev_feat)) == hipErrorNotReady && wall_us() - t0 < sync_spin_us())
-      for (int k = 0; k < 16; ++k) __builtin_ia32_pause();
-    if (q != hipSuccess && q != hipErrorNotReady) return fail(c, "feature list: %s", hipGetErrorString(q));
+  if (sync_spin_us() > 0 && !c->done_broken) {
+    if (!c->h_done) {
+      if (hipHostMalloc((void **)&c->h_done, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+          hipHostGetDevicePointer((void **)&c->d_done, c->h_done, 0) != hipSuccess) {
+        if (c->h_done) hipHostFree(c->h_done);
+        c->h_done = nullptr;
+        c->done_broken = true;
+      } else {
+        *reinterpret_cast<volatile unsigned *>(c->h_done) = c->done_seq;
+      }
+    }
+    if (c->h_done) {
+      const unsigned want = ++c->done_seq;
+      if (hipStreamWriteValue32(c->stream, c->d_done, want, 0) != hipSuccess) {
+        c->done_broken = true;
+      } else {
+        const double t0 = wall_us();
+        while (*reinterpret_cast<volatile unsigned *>(c->h_done) != want && wall_us() - t0 < sync_spin_us())
+          for (int k = 0; k < 16; ++k) __builtin_ia32_pause();
+      }
+    }
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   memcpy(x, c->h_feat, sizeof(float) * n);

@@ -91,6 +91,6 @@ rg, d2 = harness(True)
 med = lambda ts: round(1e6 * float(np.median(ts)), 1)  # noqa: E731
 print(json.dumps({"label": label,
                   "env": {k: os.environ.get(k) for k in ("KLT_AMD_UPLOAD_GROUPS", "KLT_AMD_HOST_THREADS",
-                                                         "KLT_AMD_COPY_PIECE", "KLT_AMD_UPLOAD_PIPE", "KLT_AMD_SYNC_SPIN_US")},
+                                                         "KLT_AMD_COPY_PIECE", "KLT_AMD_UPLOAD_PIPE", "KLT_AMD_SYNC_SPIN_US", "KLT_AMD_UPLOAD_FIRST")},
                   "us_per_call_pageable": med(pc), "us_per_call_harness": med(hv), "us_per_call_registered": med(rg),
                   "digest": d0, "lists_equal": d0 == d1 == d2}), flush=True)

@@ -3,25 +3,26 @@
 # (one pool generation per DMA group, KLT_AMD_UPLOAD_PIPE=0, 4 groups) against
 # one generation for the whole frame with each group's DMA queued as soon as
 # its pieces are copied (default), at 4, 8 and 16 groups; and the feature
-# list's completion polled (KLT_AMD_SYNC_SPIN_US, default 2000) against a
-# blocking wait (0).  Configurations PIPE:GROUPS:SPIN; alternating, three
+# list's completion polled (KLT_AMD_SYNC_SPIN_US) against a blocking wait
+# (0), and the first group's share (KLT_AMD_UPLOAD_FIRST, 0: equal groups).
+# Configurations PIPE:GROUPS:FIRST:SPIN; alternating, three
 # rounds, one process per run (tools/exp/r06_upload_ab.py), then one traced
 # run of each.
 set -o pipefail
 OUT=gpurun_out/${1:-r06pipe}; mkdir -p $OUT
 export TMPDIR=/tmp
-CONFS=${CONFS:-"0:4:0 1:4:0 1:4:2000 1:8:2000 1:16:2000"}
+CONFS=${CONFS:-"0:4:0:0 0:2:0:0 1:2:0:0 1:2:0.33:0 1:2:0.25:0 1:3:0.2:0 1:2:0.33:2000"}
 for round in 1 2 3; do
   for cf in $CONFS; do
-    IFS=: read p g sp <<< "$cf"
-    KLT_AMD_SYNC_SPIN_US=$sp KLT_AMD_UPLOAD_PIPE=$p KLT_AMD_UPLOAD_GROUPS=$g timeout -k 10 120 python3 tools/exp/r06_upload_ab.py p${p}g${g}s$sp >> $OUT/pipe_ab.jsonl 2> $OUT/p${p}g${g}s$sp.err || { tail -5 $OUT/p${p}g${g}s$sp.err; exit 1; }
+    IFS=: read p g f sp <<< "$cf"; L=p${p}g${g}f${f}s$sp
+    KLT_AMD_UPLOAD_FIRST=$f KLT_AMD_SYNC_SPIN_US=$sp KLT_AMD_UPLOAD_PIPE=$p KLT_AMD_UPLOAD_GROUPS=$g timeout -k 10 120 python3 tools/exp/r06_upload_ab.py $L >> $OUT/pipe_ab.jsonl 2> $OUT/$L.err || { tail -5 $OUT/$L.err; exit 1; }
     tail -1 $OUT/pipe_ab.jsonl | cut -c1-260
   done
 done
 for cf in $CONFS; do
-  IFS=: read p g sp <<< "$cf"
-  KLT_AMD_SYNC_SPIN_US=$sp KLT_UPLOAD_TRACE=1 KLT_AMD_UPLOAD_PIPE=$p KLT_AMD_UPLOAD_GROUPS=$g timeout -k 10 120 python3 tools/exp/r06_upload_ab.py trace > /dev/null 2> $OUT/trace_p${p}g${g}s$sp.err || { tail -5 $OUT/trace_p${p}g${g}s$sp.err; exit 1; }
-  python3 - $OUT/trace_p${p}g${g}s$sp.err <<'PY'
+  IFS=: read p g f sp <<< "$cf"; L=p${p}g${g}f${f}s$sp
+  KLT_AMD_UPLOAD_FIRST=$f KLT_AMD_SYNC_SPIN_US=$sp KLT_UPLOAD_TRACE=1 KLT_AMD_UPLOAD_PIPE=$p KLT_AMD_UPLOAD_GROUPS=$g timeout -k 10 120 python3 tools/exp/r06_upload_ab.py trace > /dev/null 2> $OUT/trace_$L.err || { tail -5 $OUT/trace_$L.err; exit 1; }
+  python3 - $OUT/trace_$L.err <<'PY'
 import sys
 import numpy as np
 rows = [l.split() for l in open(sys.argv[1]) if l.startswith("uptrace")]
