@@ -206,11 +206,12 @@ static int default_host_threads() {
   return n;
 }
 // DMAs a large per-call frame upload is split into (KLT_AMD_UPLOAD_GROUPS, A/B;
-// default 4): the host copies group g+1 into pinned memory while group g's DMA runs
+// default 2, round 5: 4): the host copies group g+1 into pinned memory while
+// group g's DMA runs
 static size_t upload_groups() {
   static const size_t g = [] {
     const char *e = getenv("KLT_AMD_UPLOAD_GROUPS");
-    const long v = e && *e ? atol(e) : 4;
+    const long v = e && *e ? atol(e) : 2;
     return (size_t)(v < 1 ? 1 : v > 64 ? 64 : v);
   }();
   return g;
@@ -227,11 +228,11 @@ static bool upload_pipelined() {
 }
 
 // the first DMA group's share of a pipelined per-call upload
-// (KLT_AMD_UPLOAD_FIRST, a fraction; 0 or unset: equal groups)
+// (KLT_AMD_UPLOAD_FIRST, a fraction, default 0.25; 0: equal groups)
 static double upload_first() {
   static const double v = [] {
     const char *e = getenv("KLT_AMD_UPLOAD_FIRST");
-    const double x = e && *e ? atof(e) : 0.0;
+    const double x = e && *e ? atof(e) : 0.25;
     return x > 0 && x < 1 ? x : 0.0;
   }();
   return v;
@@ -258,10 +259,6 @@ struct klt_hip_ctx {
   // the context switches away from it, so a reset or destroy can wait for the
   // work queued there even after the caller has destroyed the stream
   hipEvent_t ev_caller = nullptr;
-  unsigned *h_done = nullptr;  // a pinned word the stream writes after a per-call feature list (feat_unpack's poll)
-  unsigned *d_done = nullptr;  // its device address
-  unsigned done_seq = 0;
-  bool done_broken = false;    // the stream write failed once: block instead
   bool caller_pending = false;
   Slot slot[KLT_HIP_MAX_SLOTS + 2];  // + the batch seed and scratch slots
   uint8_t *d_u8[2] = {nullptr, nullptr};
@@ -1331,7 +1328,6 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
   }
   if (c->ev_start) hipEventDestroy(c->ev_start);
   if (c->ev_caller) hipEventDestroy(c->ev_caller);
-  if (c->h_done) hipHostFree(c->h_done);
   if (c->ev_go) hipEventDestroy(c->ev_go);
   for (unsigned *p : c->d_sig) hipFree(p);
   if (c->own) hipStreamDestroy(c->own);
@@ -1829,43 +1825,12 @@ int feat_stage_in(klt_hip_ctx *c, const float *x, const float *y, const int *val
 }
 
 // the pinned block back into the host list once the stream is done with it
-// How long a per-call KLTTrackFeatures polls its feature list's completion
-// before it blocks (KLT_AMD_SYNC_SPIN_US; default 0: block at once).  The
-// stream writes a sequence number into a pinned word after the list, and the
-// host reads the word with plain loads -- no runtime call while it polls
-// (polling hipEventQuery instead made the registered call 9-20 us slower).
-static double sync_spin_us() {
-  static const double v = [] {
-    const char *e = getenv("KLT_AMD_SYNC_SPIN_US");
-    return e && *e ? atof(e) : 0.0;
-  }();
-  return v;
-}
-
+// feat_unpack blocks in hipStreamSynchronize.  Polling instead was measured
+// slower on the registered call (tools/exp/r06_upload_pipe_ab.sh): polling
+// hipEventQuery 112-124 against 103-105 us, polling a pinned word written by
+// hipStreamWriteValue32 109-123 us -- a stream command costs ~10 us here.
 int feat_unpack(klt_hip_ctx *c, float *x, float *y, int *val, int n) {
   if (n <= 0) return 0;
-  if (sync_spin_us() > 0 && !c->done_broken) {
-    if (!c->h_done) {
-      if (hipHostMalloc((void **)&c->h_done, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-          hipHostGetDevicePointer((void **)&c->d_done, c->h_done, 0) != hipSuccess) {
-        if (c->h_done) hipHostFree(c->h_done);
-        c->h_done = nullptr;
-        c->done_broken = true;
-      } else {
-        *reinterpret_cast<volatile unsigned *>(c->h_done) = c->done_seq;
-      }
-    }
-    if (c->h_done) {
-      const unsigned want = ++c->done_seq;
-      if (hipStreamWriteValue32(c->stream, c->d_done, want, 0) != hipSuccess) {
-        c->done_broken = true;
-      } else {
-        const double t0 = wall_us();
-        while (*reinterpret_cast<volatile unsigned *>(c->h_done) != want && wall_us() - t0 < sync_spin_us())
-          for (int k = 0; k < 16; ++k) __builtin_ia32_pause();
-      }
-    }
-  }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   memcpy(x, c->h_feat, sizeof(float) * n);
   memcpy(y, c->h_feat + n, sizeof(float) * n);

@@ -12,7 +12,7 @@ set -o pipefail
 OUT=gpurun_out/${1:-r06pipe}; mkdir -p $OUT
 export TMPDIR=/tmp
 CONFS=${CONFS:-"0:4:0:0 0:2:0:0 1:2:0:0 1:2:0.33:0 1:2:0.25:0 1:3:0.2:0 1:2:0.33:2000"}
-for round in 1 2 3; do
+for round in ${ROUNDS:-1 2 3}; do
   for cf in $CONFS; do
     IFS=: read p g f sp <<< "$cf"; L=p${p}g${g}f${f}s$sp
     KLT_AMD_UPLOAD_FIRST=$f KLT_AMD_SYNC_SPIN_US=$sp KLT_AMD_UPLOAD_PIPE=$p KLT_AMD_UPLOAD_GROUPS=$g timeout -k 10 120 python3 tools/exp/r06_upload_ab.py $L >> $OUT/pipe_ab.jsonl 2> $OUT/$L.err || { tail -5 $OUT/$L.err; exit 1; }
