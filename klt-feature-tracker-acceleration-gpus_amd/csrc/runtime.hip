@@ -1477,11 +1477,13 @@ KLT_API int klt_hip_upload_frame(klt_hip_ctx *c, int buf, const unsigned char *h
     const auto &r = c->registered[i];
     if (host >= r.first && n <= r.second && (size_t)(host - r.first) <= r.second - n) {
       HIPCHK(c, hipMemcpyAsync(c->d_u8[buf], host, n, hipMemcpyHostToDevice, c->stream));
-      // u8_done guards the pinned bounce buffer, which this DMA does not touch;
-      // KLT_AMD_REG_EVENT=0 (A/B) leaves the marker out of the stream
+      // no u8_done record: it guards the pinned bounce buffer, which this DMA
+      // does not touch, and a marker between the DMA and level 0 cost the
+      // call 2 us (100.8 against 102.8 us, tools/exp/r06_regevent_ab.sh);
+      // KLT_AMD_REG_EVENT=1 (A/B) records it
       static const bool rec = [] {
         const char *e = getenv("KLT_AMD_REG_EVENT");
-        return !(e && *e == '0');
+        return e && *e == '1';
       }();
       if (rec) HIPCHK(c, hipEventRecord(c->u8_done[buf], c->stream));
       c->u8_w[buf] = ncols;
