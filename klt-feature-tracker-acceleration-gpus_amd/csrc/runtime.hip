@@ -21,6 +21,8 @@
 #include <thread>
 #include <vector>
 
+#include <hip/hip_ext.h>
+
 #include "klt_dev.h"
 #include "klt_hip.h"
 
@@ -398,11 +400,38 @@ namespace {
 // the pyramid stream: normal priority, or the lowest (KLT_PSTREAM_PRIO=low:
 // the tracking stream's short kernels between two chunks -- the exchange, the
 // processing order -- are then dispatched ahead of queued pyramid workgroups)
+// Experiment (KLT_PYR_CUS / KLT_TRK_CUS = CUs): a stream confined to that
+// many CUs, spread evenly over the XCDs -- the pyramid stream to the first
+// CUs of each XCD, the context's own stream (trackers) to the last.
+// KLT_CU_MAP=div32 if mask bit i is CU i % 32 of XCD i / 32; default mod8
+// (CU i / 8 of XCD i % 8); tools/hipbench/cumask tells which.
+bool cu_masked_stream(hipStream_t *st, const char *env, bool first) {
+  const char *e = getenv(env);
+  const int want = e && *e ? atoi(e) : 0;
+  int dev = 0, ncu = 0;
+  if (want <= 0 || hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu % 8 != 0 ||
+      want >= ncu)
+    return false;
+  const char *mp = getenv("KLT_CU_MAP");
+  const bool div32 = mp && strcmp(mp, "div32") == 0;
+  const int per = ncu / 8, k = (want + 7) / 8;
+  std::vector<unsigned> m((ncu + 31) / 32, 0u);
+  for (int x = 0; x < 8; ++x)
+    for (int j = 0; j < per; ++j) {
+      if (first ? j >= k : j < per - k) continue;
+      const int bit = div32 ? x * per + j : x + 8 * j;
+      m[bit / 32] |= 1u << (bit % 32);
+    }
+  return hipExtStreamCreateWithCUMask(st, (uint32_t)m.size(), m.data()) == hipSuccess;
+}
+
 hipError_t make_pstream(klt_hip_ctx *c) {
   static const bool low = [] {
     const char *v = getenv("KLT_PSTREAM_PRIO");
     return v && strcmp(v, "low") == 0;
   }();
+  if (cu_masked_stream(&c->pstream, "KLT_PYR_CUS", true)) return hipSuccess;
   if (!low) return hipStreamCreateWithFlags(&c->pstream, hipStreamNonBlocking);
   int least = 0, greatest = 0;
   const hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
@@ -1257,7 +1286,8 @@ KLT_API klt_hip_ctx *klt_hip_ctx_create(int device) {
   }
   c->device = device;
   if (hipSetDevice(device) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+      (!cu_masked_stream(&c->own, "KLT_TRK_CUS", false) &&
+       hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess)) {
     delete c;
     return nullptr;
   }
