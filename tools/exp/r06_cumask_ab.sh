@@ -7,8 +7,9 @@ set -o pipefail
 OUT=gpurun_out/${1:-r06cu}; mkdir -p $OUT
 export TMPDIR=/tmp
 B="--no-cpu --no-4k --no-fast --api-frames 0 --replace-frames 0 --no-sharded-4k"
+CONFS=${CONFS:-"0:0 224:0 192:0 0:96 0:64 192:64 160:96"}
 for round in ${ROUNDS:-1 2}; do
-  for cf in ${CONFS:-"0:0 224:0 192:0 0:96 0:64 192:64 160:96"}; do
+  for cf in $CONFS; do
     IFS=: read p t <<< "$cf"
     P=; T=
     [ "$p" != 0 ] && P=$p
