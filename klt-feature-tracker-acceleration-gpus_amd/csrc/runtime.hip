@@ -254,6 +254,8 @@ struct klt_hip_ctx {
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   hipStream_t pstream = nullptr;  // pyramid stream of the pipelined sequence
+  hipStream_t tstream = nullptr;  // experiment: the batched tracker on a CU-confined stream (KLT_TRK_CUS)
+  hipEvent_t ev_tin = nullptr, ev_tout = nullptr;
   hipEvent_t ev_built[KLT_HIP_MAX_SLOTS] = {};
   hipEvent_t ev_free[KLT_HIP_MAX_SLOTS] = {};
   hipEvent_t ev_start = nullptr;
@@ -1286,8 +1288,7 @@ KLT_API klt_hip_ctx *klt_hip_ctx_create(int device) {
   }
   c->device = device;
   if (hipSetDevice(device) != hipSuccess ||
-      (!cu_masked_stream(&c->own, "KLT_TRK_CUS", false) &&
-       hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess)) {
+      hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return nullptr;
   }
@@ -1352,6 +1353,12 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
     hipStreamSynchronize(c->pstream);
     hipStreamDestroy(c->pstream);
   }
+  if (c->tstream) {
+    hipStreamSynchronize(c->tstream);
+    hipStreamDestroy(c->tstream);
+  }
+  for (hipEvent_t e : {c->ev_tin, c->ev_tout})
+    if (e) hipEventDestroy(e);
   for (int k = 0; k < KLT_HIP_MAX_SLOTS; ++k) {
     if (c->ev_built[k]) hipEventDestroy(c->ev_built[k]);
     if (c->ev_free[k]) hipEventDestroy(c->ev_free[k]);
@@ -2402,8 +2409,25 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
       if (!c->ev_go) HIPCHK(c, hipEventCreateWithFlags(&c->ev_go, hipEventDisableTiming));
       HIPCHK(c, hipEventRecord(c->ev_go, c->stream));
     }
-    if (n > 0 && track_frames_launch(c, c->stream, td, a, b, x, y, val, n, band ? band->own : nullptr, true))
+    // experiment (KLT_TRK_CUS): the tracker on a CU-confined stream, joined
+    // to the context's stream by events on both sides
+    static const bool trk_masked = getenv("KLT_TRK_CUS") && atoi(getenv("KLT_TRK_CUS")) > 0;
+    hipStream_t ts = c->stream;
+    if (trk_masked && n > 0) {
+      if (!c->tstream && !cu_masked_stream(&c->tstream, "KLT_TRK_CUS", false))
+        return fail(c, "KLT_TRK_CUS: no CU-masked stream");
+      for (hipEvent_t *e : {&c->ev_tin, &c->ev_tout})
+        if (!*e) HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
+      HIPCHK(c, hipEventRecord(c->ev_tin, c->stream));
+      HIPCHK(c, hipStreamWaitEvent(c->tstream, c->ev_tin, 0));
+      ts = c->tstream;
+    }
+    if (n > 0 && track_frames_launch(c, ts, td, a, b, x, y, val, n, band ? band->own : nullptr, true))
       return -1;
+    if (ts != c->stream) {
+      HIPCHK(c, hipEventRecord(c->ev_tout, ts));
+      HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_tout, 0));
+    }
     HMARK("track");
     if (!serial && !ahead && c->prev.bank >= 0) HIPCHK(c, hipEventRecord(c->ev_bfree[c->prev.bank], c->stream));
     c->prev = PrevRef{bi, Fc - 1};
