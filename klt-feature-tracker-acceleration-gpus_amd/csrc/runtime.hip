@@ -21,8 +21,6 @@
 #include <thread>
 #include <vector>
 
-#include <hip/hip_ext.h>
-
 #include "klt_dev.h"
 #include "klt_hip.h"
 
@@ -254,8 +252,6 @@ struct klt_hip_ctx {
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   hipStream_t pstream = nullptr;  // pyramid stream of the pipelined sequence
-  hipStream_t tstream = nullptr;  // experiment: the batched tracker on a CU-confined stream (KLT_TRK_CUS)
-  hipEvent_t ev_tin = nullptr, ev_tout = nullptr;
   hipEvent_t ev_built[KLT_HIP_MAX_SLOTS] = {};
   hipEvent_t ev_free[KLT_HIP_MAX_SLOTS] = {};
   hipEvent_t ev_start = nullptr;
@@ -402,38 +398,11 @@ namespace {
 // the pyramid stream: normal priority, or the lowest (KLT_PSTREAM_PRIO=low:
 // the tracking stream's short kernels between two chunks -- the exchange, the
 // processing order -- are then dispatched ahead of queued pyramid workgroups)
-// Experiment (KLT_PYR_CUS / KLT_TRK_CUS = CUs): a stream confined to that
-// many CUs, spread evenly over the XCDs -- the pyramid stream to the first
-// CUs of each XCD, the context's own stream (trackers) to the last.
-// KLT_CU_MAP=div32 if mask bit i is CU i % 32 of XCD i / 32; default mod8
-// (CU i / 8 of XCD i % 8); tools/hipbench/cumask tells which.
-bool cu_masked_stream(hipStream_t *st, const char *env, bool first) {
-  const char *e = getenv(env);
-  const int want = e && *e ? atoi(e) : 0;
-  int dev = 0, ncu = 0;
-  if (want <= 0 || hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu % 8 != 0 ||
-      want >= ncu)
-    return false;
-  const char *mp = getenv("KLT_CU_MAP");
-  const bool div32 = mp && strcmp(mp, "div32") == 0;
-  const int per = ncu / 8, k = (want + 7) / 8;
-  std::vector<unsigned> m((ncu + 31) / 32, 0u);
-  for (int x = 0; x < 8; ++x)
-    for (int j = 0; j < per; ++j) {
-      if (first ? j >= k : j < per - k) continue;
-      const int bit = div32 ? x * per + j : x + 8 * j;
-      m[bit / 32] |= 1u << (bit % 32);
-    }
-  return hipExtStreamCreateWithCUMask(st, (uint32_t)m.size(), m.data()) == hipSuccess;
-}
-
 hipError_t make_pstream(klt_hip_ctx *c) {
   static const bool low = [] {
     const char *v = getenv("KLT_PSTREAM_PRIO");
     return v && strcmp(v, "low") == 0;
   }();
-  if (cu_masked_stream(&c->pstream, "KLT_PYR_CUS", true)) return hipSuccess;
   if (!low) return hipStreamCreateWithFlags(&c->pstream, hipStreamNonBlocking);
   int least = 0, greatest = 0;
   const hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
@@ -1353,12 +1322,6 @@ KLT_API void klt_hip_ctx_destroy(klt_hip_ctx *c) {
     hipStreamSynchronize(c->pstream);
     hipStreamDestroy(c->pstream);
   }
-  if (c->tstream) {
-    hipStreamSynchronize(c->tstream);
-    hipStreamDestroy(c->tstream);
-  }
-  for (hipEvent_t e : {c->ev_tin, c->ev_tout})
-    if (e) hipEventDestroy(e);
   for (int k = 0; k < KLT_HIP_MAX_SLOTS; ++k) {
     if (c->ev_built[k]) hipEventDestroy(c->ev_built[k]);
     if (c->ev_free[k]) hipEventDestroy(c->ev_free[k]);
@@ -2409,25 +2372,8 @@ int track_frames_impl(klt_hip_ctx *c, const klt_hip_pyr_desc *pd, const klt_hip_
       if (!c->ev_go) HIPCHK(c, hipEventCreateWithFlags(&c->ev_go, hipEventDisableTiming));
       HIPCHK(c, hipEventRecord(c->ev_go, c->stream));
     }
-    // experiment (KLT_TRK_CUS): the tracker on a CU-confined stream, joined
-    // to the context's stream by events on both sides
-    static const bool trk_masked = getenv("KLT_TRK_CUS") && atoi(getenv("KLT_TRK_CUS")) > 0;
-    hipStream_t ts = c->stream;
-    if (trk_masked && n > 0) {
-      if (!c->tstream && !cu_masked_stream(&c->tstream, "KLT_TRK_CUS", false))
-        return fail(c, "KLT_TRK_CUS: no CU-masked stream");
-      for (hipEvent_t *e : {&c->ev_tin, &c->ev_tout})
-        if (!*e) HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
-      HIPCHK(c, hipEventRecord(c->ev_tin, c->stream));
-      HIPCHK(c, hipStreamWaitEvent(c->tstream, c->ev_tin, 0));
-      ts = c->tstream;
-    }
-    if (n > 0 && track_frames_launch(c, ts, td, a, b, x, y, val, n, band ? band->own : nullptr, true))
+    if (n > 0 && track_frames_launch(c, c->stream, td, a, b, x, y, val, n, band ? band->own : nullptr, true))
       return -1;
-    if (ts != c->stream) {
-      HIPCHK(c, hipEventRecord(c->ev_tout, ts));
-      HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_tout, 0));
-    }
     HMARK("track");
     if (!serial && !ahead && c->prev.bank >= 0) HIPCHK(c, hipEventRecord(c->ev_bfree[c->prev.bank], c->stream));
     c->prev = PrevRef{bi, Fc - 1};
