@@ -872,26 +872,35 @@ __global__ __launch_bounds__(kBlock) void k_min_eigen(const float *__restrict__ 
 }
 
 // The same map for the default 7x7 window, tiled: a workgroup covers 64 x 16
-// grid points (a lane per column, each wave four grid rows), stages the
-// gradients its windows read in LDS once (global reads drop from 49 per
-// point to ~1.4), and sums each window from LDS in the reference's order:
+// grid points (a lane per column, each wave four grid rows), stages its
+// windows' cells in LDS once (global reads drop from 49 per point to ~1.4)
+// as their products {gx*gx, gy*gy, gx*gy} -- each product is the float the
+// reference's loop forms for every window that holds the cell, so it is
+// formed once here -- and sums each window from LDS in the reference's order:
 // rows, then columns, from +0, one rounding per operation (sxx and syy as one
-// packed pair: two independent IEEE sums, the same bits).  step <= kEigMaxStep.
+// packed pair: two independent IEEE sums, the same bits).  A lane walks the
+// window rows of two grid rows at once (rows 0..6 for the first, step..6+step
+// for the second; each sum still in its own row-major order), so a cell read
+// from LDS serves both.  Round 6: 2 VALU and one 16-byte LDS read per term
+// and pair instead of 4 VALU and one 8-byte read per term and point.
+// step <= kEigMaxStep.
 namespace eig {
-constexpr int TX = 64, TY = 16, RPW = TY / 4, HW = 3;
+constexpr int TX = 64, TY = 16, RPW = TY / 4, HW = 3, WIN = 2 * HW + 1;
 constexpr int kMaxStep = 2;
-constexpr int C_MAX = (TX - 1) * kMaxStep + 2 * HW + 1, R_MAX = (TY - 1) * kMaxStep + 2 * HW + 1;
+static_assert(RPW % 2 == 0, "grid rows in pairs");
 }  // namespace eig
 
+// STEP: the grid step (1 or 2), so that the LDS tile is sized for it (24.6 KB
+// at step 1: six workgroups per CU)
+template <int STEP>
 __global__ __launch_bounds__(256) void k_min_eigen7(const float *__restrict__ gx, const float *__restrict__ gy, int W,
-                                                   int ps, int bx, int by, int step, int nx, int ny,
-                                                   int *__restrict__ out) {
+                                                   int ps, int bx, int by, int nx, int ny, int *__restrict__ out) {
   using namespace eig;
-  __shared__ f2 g[R_MAX * C_MAX];
+  constexpr int step = STEP, C = (TX - 1) * STEP + WIN, R = (TY - 1) * STEP + WIN, C_MAX = C;
+  __shared__ f4 g[R * C];  // {gx*gx, gy*gy, gx*gy, unused} per cell
   const int tiles_x = (nx + TX - 1) / TX;
   const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
   const int ix0 = tx * TX, iy0 = ty * TY;
-  const int C = (TX - 1) * step + 2 * HW + 1, R = (TY - 1) * step + 2 * HW + 1;
   // pixel (x0 + c, y0 + r) for LDS cell (r, c); clamped to the last grid
   // point's window (tiles past nx / ny read valid pixels they never use)
   const int x0 = bx + ix0 * step - HW, y0 = by + iy0 * step - HW;
@@ -900,32 +909,49 @@ __global__ __launch_bounds__(256) void k_min_eigen7(const float *__restrict__ gx
     const int r = p / C, c = p - r * C;
     const int yy = min(y0 + r, ymax), xx = min(x0 + c, xmax);
     const long o = ((long)yy * W + xx) * ps;
-    g[r * C_MAX + c] = f2{gx[o], gy[o]};
+    const float a = gx[o], b = gy[o];
+    const f2 ab = {a, b};
+    const f2 sq = ab * ab;
+    g[r * C_MAX + c] = f4{sq.x, sq.y, a * b, 0.0f};
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ix = ix0 + lane;
   if (ix >= nx) return;
-#pragma unroll 1
-  for (int k = 0; k < RPW; ++k) {
-    const int iy = iy0 + w * RPW + k;
-    if (iy >= ny) return;
-    const f2 *base = g + ((w * RPW + k) * step) * C_MAX + lane * step;
-    f2 sq = {0.0f, 0.0f};  // (sxx, syy)
-    float sxy = 0.0f;
-#pragma unroll
-    for (int v = 0; v < 2 * HW + 1; ++v)
-#pragma unroll
-      for (int u = 0; u < 2 * HW + 1; ++u) {
-        const f2 ab = base[v * C_MAX + u];
-        sq += ab * ab;
-        sxy += ab.x * ab.y;
-      }
+  // min eigenvalue of the window sums, :289-292 / :415-420
+  const auto finish = [&](f2 sq, float sxy, int iy) {
     const float sxx = sq.x, syy = sq.y;
     const float disc = (sxx - syy) * (sxx - syy) + 4.0f * sxy * sxy;
     float val = (float)(((double)(sxx + syy) - sqrt((double)disc)) / 2.0);
     if (val > 2147483648.0f) val = 2147483648.0f;
     out[(long)iy * nx + ix] = x86_ftoi(val);
+  };
+#pragma unroll 1
+  for (int k = 0; k < RPW; k += 2) {
+    const int iy = iy0 + w * RPW + k;  // grid rows iy (A) and iy + 1 (B)
+    if (iy >= ny) return;
+    const f4 *base = g + ((w * RPW + k) * step) * C_MAX + lane * step;
+    f2 qa = {0.0f, 0.0f}, qb = {0.0f, 0.0f};  // (sxx, syy)
+    float xa = 0.0f, xb = 0.0f;              // sxy
+    // one window row per iteration (rolled: unrolled, the compiler hoists
+    // every row's loads and the wave needs 190 VGPRs)
+#pragma unroll 1
+    for (int r = 0; r < WIN + step; ++r) {  // step 1: rows 0..7, step 2: rows 0..8
+#pragma unroll
+      for (int u = 0; u < WIN; ++u) {
+        const f4 t = base[r * C_MAX + u];
+        if (r < WIN) {
+          qa += f2{t.x, t.y};
+          xa += t.z;
+        }
+        if (r >= step) {
+          qb += f2{t.x, t.y};
+          xb += t.z;
+        }
+      }
+    }
+    finish(qa, xa, iy);
+    if (iy + 1 < ny) finish(qb, xb, iy + 1);
   }
 }
 
@@ -1082,7 +1108,10 @@ hipError_t launch_min_eigen(hipStream_t st, const float *gx, const float *gy, in
   if (np == 0) return hipSuccess;
   if (hw == eig::HW && hh == eig::HW && step >= 1 && step <= eig::kMaxStep) {
     const long tiles = (long)((nx + eig::TX - 1) / eig::TX) * ((ny + eig::TY - 1) / eig::TY);
-    hipLaunchKernelGGL(k_min_eigen7, dim3((unsigned)tiles), dim3(256), 0, st, gx, gy, W, ps, bx, by, step, nx, ny, out);
+    if (step == 1)
+      hipLaunchKernelGGL(k_min_eigen7<1>, dim3((unsigned)tiles), dim3(256), 0, st, gx, gy, W, ps, bx, by, nx, ny, out);
+    else
+      hipLaunchKernelGGL(k_min_eigen7<2>, dim3((unsigned)tiles), dim3(256), 0, st, gx, gy, W, ps, bx, by, nx, ny, out);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_min_eigen, dim3(blocks_for(np)), dim3(kBlock), 0, st, gx, gy, W, ps, bx, by, step, nx, ny, hw,
