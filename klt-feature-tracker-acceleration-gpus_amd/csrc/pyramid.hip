@@ -881,9 +881,9 @@ __global__ __launch_bounds__(kBlock) void k_min_eigen(const float *__restrict__ 
 // packed pair: two independent IEEE sums, the same bits).  A lane walks the
 // window rows of two grid rows at once (rows 0..6 for the first, step..6+step
 // for the second; each sum still in its own row-major order), so a cell read
-// from LDS serves both.  Round 6: 2 VALU and one 16-byte LDS read per term
+// from LDS serves both.  Round 6: 2 VALU and 12 LDS bytes per term
 // and pair instead of 4 VALU and one 8-byte read per term and point.
-// step <= kEigMaxStep.
+// step <= kMaxStep.
 namespace eig {
 constexpr int TX = 64, TY = 16, RPW = TY / 4, HW = 3, WIN = 2 * HW + 1;
 constexpr int kMaxStep = 2;
@@ -897,7 +897,11 @@ __global__ __launch_bounds__(256) void k_min_eigen7(const float *__restrict__ gx
                                                    int ps, int bx, int by, int nx, int ny, int *__restrict__ out) {
   using namespace eig;
   constexpr int step = STEP, C = (TX - 1) * STEP + WIN, R = (TY - 1) * STEP + WIN, C_MAX = C;
-  __shared__ f4 g[R * C];  // {gx*gx, gy*gy, gx*gy, unused} per cell
+  // per cell {gx*gx, gy*gy} and gx*gy: 12 bytes, 18.5 KB at step 1, so that a
+  // CU holds eight workgroups and a 1080p map's 2 040 tiles run in one round
+  // (16-byte cells: six per CU, and a third of the tiles in a second round)
+  __shared__ f2 gq[R * C];
+  __shared__ float gm[R * C];
   const int tiles_x = (nx + TX - 1) / TX;
   const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
   const int ix0 = tx * TX, iy0 = ty * TY;
@@ -905,14 +909,18 @@ __global__ __launch_bounds__(256) void k_min_eigen7(const float *__restrict__ gx
   // point's window (tiles past nx / ny read valid pixels they never use)
   const int x0 = bx + ix0 * step - HW, y0 = by + iy0 * step - HW;
   const int xmax = bx + (nx - 1) * step + HW, ymax = by + (ny - 1) * step + HW;
-  for (int p = threadIdx.x; p < R * C; p += 256) {
+#pragma unroll
+  for (int p0 = 0; p0 < R * C; p0 += 256) {  // a compile-time trip count: the loads issue together
+    const int p = p0 + (int)threadIdx.x;
+    if (p >= R * C) break;
     const int r = p / C, c = p - r * C;
     const int yy = min(y0 + r, ymax), xx = min(x0 + c, xmax);
     const long o = ((long)yy * W + xx) * ps;
     const float a = gx[o], b = gy[o];
     const f2 ab = {a, b};
     const f2 sq = ab * ab;
-    g[r * C_MAX + c] = f4{sq.x, sq.y, a * b, 0.0f};
+    gq[r * C_MAX + c] = sq;
+    gm[r * C_MAX + c] = a * b;
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -930,7 +938,7 @@ __global__ __launch_bounds__(256) void k_min_eigen7(const float *__restrict__ gx
   for (int k = 0; k < RPW; k += 2) {
     const int iy = iy0 + w * RPW + k;  // grid rows iy (A) and iy + 1 (B)
     if (iy >= ny) return;
-    const f4 *base = g + ((w * RPW + k) * step) * C_MAX + lane * step;
+    const int base = ((w * RPW + k) * step) * C_MAX + lane * step;
     f2 qa = {0.0f, 0.0f}, qb = {0.0f, 0.0f};  // (sxx, syy)
     float xa = 0.0f, xb = 0.0f;              // sxy
     // one window row per iteration (rolled: unrolled, the compiler hoists
@@ -939,14 +947,15 @@ __global__ __launch_bounds__(256) void k_min_eigen7(const float *__restrict__ gx
     for (int r = 0; r < WIN + step; ++r) {  // step 1: rows 0..7, step 2: rows 0..8
 #pragma unroll
       for (int u = 0; u < WIN; ++u) {
-        const f4 t = base[r * C_MAX + u];
+        const f2 q = gq[base + r * C_MAX + u];
+        const float m = gm[base + r * C_MAX + u];
         if (r < WIN) {
-          qa += f2{t.x, t.y};
-          xa += t.z;
+          qa += q;
+          xa += m;
         }
         if (r >= step) {
-          qb += f2{t.x, t.y};
-          xb += t.z;
+          qb += q;
+          xb += m;
         }
       }
     }
