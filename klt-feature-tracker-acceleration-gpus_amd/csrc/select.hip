@@ -68,7 +68,6 @@ struct SelState {
   int m;           // swap pairs of the current step
   int totL, totR;  // left / right stops of the current step
   int nstack;      // segments pushed (start, len), in push order
-  unsigned ticket; // count blocks finished in the current step (k_sel_count_scan; its last block resets it)
   int stack[2 * kSelStack];
   int2 pivot[kSelStack];  // stack entries of length -1 are a split's pivot, this element: no download
 };
@@ -230,32 +229,6 @@ __global__ __launch_bounds__(kSelScanThreads) void k_sel_scan(SelState *s, int2 
                                                              int threshold) {
   __shared__ int sl[kSelScanThreads], sr[kSelScanThreads];
   sel_scan<kSelScanThreads>(s, kv, cnt, off, sl, sr, threshold);
-}
-
-#ifndef KLT_SEL_FUSED
-#define KLT_SEL_FUSED 1  // A/B hook (make variant DEFS=-DKLT_SEL_FUSED=0): count and scan as two launches
-#endif
-
-// steps 1 + 2 in one launch (round 6): every block counts, then takes a
-// ticket; the block that takes the last one runs the scan.  The counts are
-// released by an agent-scope fence before the ticket and acquired by one
-// after it (on gfx950 the XCDs' L2s are not coherent with each other: the
-// fences write back and invalidate them).  One graph node fewer per step.
-__global__ __launch_bounds__(kSelThreads) void k_sel_count_scan(SelState *s, int2 *__restrict__ kv,
-                                                               int *__restrict__ cnt, int *__restrict__ off,
-                                                               int threshold) {
-  __shared__ int tmp[kSelThreads / kWave];
-  __shared__ int sl[kSelThreads], sr[kSelThreads];
-  __shared__ int last;
-  sel_count(s, kv, cnt, tmp, blockIdx.x, threshold);
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(&s->ticket, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  if (threadIdx.x == 0) s->ticket = 0;
-  sel_scan<kSelThreads>(s, kv, cnt, off, sl, sr, threshold);
 }
 
 // step 3: per position, its rank among the left stops (ascending) and the right
@@ -512,12 +485,8 @@ int refine_launch(SelEngine *e, hipStream_t st, Seg g, std::string *err) {
       void *a_rank[] = {&ds, &kv, &off, &pl, &pr};
       void *a_swap[] = {&ds, &kv, &pl, &pr};
       for (int l = 0; l < levels; ++l) {
-        if (KLT_SEL_FUSED) {
-          add(reinterpret_cast<const void *>(k_sel_count_scan), nbp, kSelThreads, a_scan);
-        } else {
-          add(reinterpret_cast<const void *>(k_sel_count), nbp, kSelThreads, a_count);
-          add(reinterpret_cast<const void *>(k_sel_scan), 1, kSelScanThreads, a_scan);
-        }
+        add(reinterpret_cast<const void *>(k_sel_count), nbp, kSelThreads, a_count);
+        add(reinterpret_cast<const void *>(k_sel_scan), 1, kSelScanThreads, a_scan);
         add(reinterpret_cast<const void *>(k_sel_rank), nbp, kSelThreads, a_rank);
         add(reinterpret_cast<const void *>(k_sel_swap), swp, kSelThreads, a_swap);
       }
@@ -537,14 +506,9 @@ int refine_launch(SelEngine *e, hipStream_t st, Seg g, std::string *err) {
     return 0;
   }
   for (int l = 0; l < levels; ++l) {
-    if (KLT_SEL_FUSED) {
-      hipLaunchKernelGGL(k_sel_count_scan, dim3(nb), dim3(kSelThreads), 0, st, e->d_state, e->d_kv, e->d_cnt,
-                         e->d_off, T);
-    } else {
-      hipLaunchKernelGGL(k_sel_count, dim3(nb), dim3(kSelThreads), 0, st, e->d_state, e->d_kv, e->d_cnt, T);
-      hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(kSelScanThreads), 0, st, e->d_state, e->d_kv, e->d_cnt, e->d_off,
-                         T);
-    }
+    hipLaunchKernelGGL(k_sel_count, dim3(nb), dim3(kSelThreads), 0, st, e->d_state, e->d_kv, e->d_cnt, T);
+    hipLaunchKernelGGL(k_sel_scan, dim3(1), dim3(kSelScanThreads), 0, st, e->d_state, e->d_kv, e->d_cnt, e->d_off,
+                       T);
     hipLaunchKernelGGL(k_sel_rank, dim3(nb), dim3(kSelThreads), 0, st, e->d_state, e->d_kv, e->d_off, e->d_posL,
                        e->d_posR);
     hipLaunchKernelGGL(k_sel_swap, dim3(sw), dim3(kSelThreads), 0, st, e->d_state, e->d_kv, e->d_posL, e->d_posR);
