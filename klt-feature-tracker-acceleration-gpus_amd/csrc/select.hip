@@ -439,9 +439,16 @@ int refine_launch(SelEngine *e, hipStream_t st, Seg g, std::string *err) {
   e->h_state->len = g.len;
   SELCHK(hipMemcpyAsync(e->d_state, e->h_state, offsetof(SelState, stack), hipMemcpyHostToDevice, st));
   // splits expected to reach the threshold, plus slack; refine_finish
-  // continues if the pivots were unlucky
-  int levels = 2;
+  // continues if the pivots were unlucky (KLT_SEL_SLACK, default 2: levels
+  // past the threshold cost their four launches as no-ops)
+  static const int slack = [] {
+    const char *v = getenv("KLT_SEL_SLACK");
+    const int x = v && *v ? atoi(v) : 2;
+    return x < -3 ? -3 : x > 4 ? 4 : x;
+  }();
+  int levels = slack;
   for (long l = g.len; l > T; l /= 2) ++levels;
+  if (levels < 1) levels = 1;
   const int sw = (g.len / 2 + kSelThreads) / kSelThreads;
   if (sel_graphs() && !lib_exiting()) {  // after the exit hook: plain launches, no graph outlives the code object
     // the steps as one graph launch: 4 * levels kernel launches cost more
