@@ -145,7 +145,9 @@ unsigned partition(P *a, unsigned n) {
   unsigned L[B + 8], R[B + 8];  // + 8: the vector appends write whole groups
 #if defined(__x86_64__)
   constexpr bool vec_ok = sizeof(P) == 8 && sizeof(a[0].x) == 4;
-  const bool vec = vec_ok && host_has_avx2();
+  // pairs of 4-byte keys, the key first (the vector loads read .x at offset 0)
+  const bool vec = vec_ok && host_has_avx2() &&
+                   reinterpret_cast<const char *>(&a[0].x) == reinterpret_cast<const char *>(&a[0]);
 #else
   constexpr bool vec_ok = false;
   const bool vec = false;
