@@ -6,8 +6,10 @@
   summary: python tools/api_timeline.py summary <dir with *_kernel_trace.csv, *_memory_copy_trace.csv>
 
 The summary splits each steady-state call into device spans: the frame's H2D
-copy, the copy-to-kernel hand-off, k_pyr_l0, k_pyr_l1, the tracker (and the
-band sort when it runs), and the gap from the tracker's end to the next
+copy (first DMA start to last DMA end), the copy-to-kernel hand-off, k_pyr_l0,
+k_pyr_l1, level 1's end to the tracker's start (the feature list's copy kernel
+between them), the tracker, the two copy kernels' own durations, and the gap
+from the tracker's end to the next
 call's copy (host side: synchronize, feature list unpack, the caller's own
 work, the next call's feature pack and frame staging)."""
 from __future__ import annotations
@@ -65,8 +67,8 @@ def summary(a):
     ev = []
     for r in kt:
         name = r["Kernel_Name"]
-        short = next((k for k in ("k_pyr_l0", "k_pyr_l1", "k_track", "k_band_order", "k_min_eigen", "k_sel")
-                      if k in name), "other")
+        short = next((k for k in ("k_pyr_l0", "k_pyr_l1", "k_track", "k_band_order", "k_min_eigen", "k_sel",
+                                  "k_copy_words") if k in name), "other")
         ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short))
     for r in mc:
         if r["Direction"].endswith("HOST_TO_DEVICE"):
@@ -83,8 +85,11 @@ def summary(a):
             else:
                 cur["h2d"][1] = max(cur["h2d"][1], e[1])
         elif cur is not None:
+            if e[2] == "k_copy_words":  # the feature list in (before the tracker) and out (after it)
+                cur.setdefault("copies", []).append(e)
             cur.setdefault(e[2], e)
-    spans = {k: [] for k in ("h2d", "handoff", "k_pyr_l0", "k_pyr_l1", "k_track", "track_end_to_next_h2d", "call")}
+    spans = {k: [] for k in ("h2d", "handoff", "k_pyr_l0", "k_pyr_l1", "l1_to_track", "k_track", "copy_in", "copy_out",
+                             "track_end_to_next_h2d", "call")}
     for i, c in enumerate(calls[2:-1], start=2):
         if not all(k in c for k in ("k_pyr_l0", "k_pyr_l1", "k_track")):
             continue
@@ -93,6 +98,11 @@ def summary(a):
         spans["handoff"].append(c["k_pyr_l0"][0] - c["h2d"][1])
         for k in ("k_pyr_l0", "k_pyr_l1", "k_track"):
             spans[k].append(c[k][1] - c[k][0])
+        spans["l1_to_track"].append(c["k_track"][0] - c["k_pyr_l1"][1])
+        cp = c.get("copies", [])
+        if len(cp) >= 2:
+            spans["copy_in"].append(cp[0][1] - cp[0][0])
+            spans["copy_out"].append(cp[-1][1] - cp[-1][0])
         spans["track_end_to_next_h2d"].append(nxt - c["k_track"][1])
         spans["call"].append(nxt - c["h2d"][0])
     print({k: round(float(np.median(v)) / 1000, 1) for k, v in spans.items() if v}, "us (median),", len(spans["call"]), "calls")
